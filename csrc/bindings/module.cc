@@ -1,0 +1,435 @@
+// pybind11 module `seldon_core_amd._C`: the native engine, front ends, GPU
+// units and raw kernel launchers.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <future>
+
+#include "../core/engine.h"
+#include "../core/json.h"
+#include "../core/message.h"
+#include "../gpu/batcher.h"
+#include "../gpu/models.h"
+#include "../kernels/kernels.h"
+#include "../server/grpc_server.h"
+#include "../server/http_server.h"
+#include "py_unit.h"
+
+namespace py = pybind11;
+using namespace sca;
+
+namespace {
+
+template <class T>
+std::vector<T> to_vec(const py::array_t<T, py::array::c_style | py::array::forcecast>& a) {
+  return std::vector<T>(a.data(), a.data() + a.size());
+}
+
+std::pair<int, std::string> render(const Outcome& o) {
+  if (o.err) return {o.err->http_status, error_to_json(*o.err)};
+  std::string out;
+  if (o.msg) message_to_json(*o.msg, out);
+  else out = "{}";
+  return {200, out};
+}
+
+Outcome wait_outcome(const std::function<void(Done)>& start) {
+  std::promise<Outcome> p;
+  auto f = p.get_future();
+  {
+    py::gil_scoped_release nogil;
+    start([&p](Outcome o) { p.set_value(std::move(o)); });
+    return f.get();
+  }
+}
+
+gpu::BatcherOptions batcher_opts(int device, int max_batch, int max_wait_us, int slots, bool zero_copy,
+                                 size_t zero_copy_max_bytes, bool spin) {
+  gpu::BatcherOptions o;
+  o.device = device;
+  o.max_batch = max_batch;
+  o.max_wait_us = max_wait_us;
+  o.slots = slots;
+  o.zero_copy = zero_copy;
+  o.zero_copy_max_bytes = zero_copy_max_bytes;
+  o.spin_wait = spin;
+  return o;
+}
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+template <class T> T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native Seldon-compatible inference graph engine (native core)";
+  m.def("version", [] { return std::string("0.1.0"); });
+  m.def("gpu_device_count", [] { return gpu::device_count(); });
+
+  // ------------------------------------------------------------- codecs
+  m.def("json_roundtrip", [](const std::string& text) {
+    SeldonMessage msg;
+    message_from_json(parse_json(text), msg);
+    std::string out;
+    message_to_json(msg, out);
+    return out;
+  });
+  m.def("json_to_pb", [](const std::string& text) {
+    SeldonMessage msg;
+    message_from_json(parse_json(text), msg);
+    std::string out;
+    message_to_pb(msg, out);
+    return py::bytes(out);
+  });
+  m.def("pb_to_json", [](const py::bytes& b) {
+    SeldonMessage msg;
+    if (!message_from_pb(std::string(b), msg)) throw std::runtime_error("invalid SeldonMessage protobuf");
+    std::string out;
+    message_to_json(msg, out);
+    return out;
+  });
+  m.def("feedback_json_to_pb", [](const std::string& text) {
+    Feedback f;
+    feedback_from_json(parse_json(text), f);
+    std::string out;
+    feedback_to_pb(f, out);
+    return py::bytes(out);
+  });
+  m.def("feedback_pb_to_json", [](const py::bytes& b) {
+    Feedback f;
+    if (!feedback_from_pb(std::string(b), f)) throw std::runtime_error("invalid Feedback protobuf");
+    std::string out;
+    feedback_to_json(f, out);
+    return out;
+  });
+  m.def("list_json_to_pb", [](const std::string& text) {
+    std::vector<SeldonMessage> v;
+    message_list_from_json(parse_json(text), v);
+    std::vector<const SeldonMessage*> p;
+    for (auto& x : v) p.push_back(&x);
+    std::string out;
+    message_list_to_pb(p, out);
+    return py::bytes(out);
+  });
+  m.def("list_pb_to_json", [](const py::bytes& b) {
+    std::vector<SeldonMessage> v;
+    if (!message_list_from_pb(std::string(b), v)) throw std::runtime_error("invalid SeldonMessageList protobuf");
+    std::vector<const SeldonMessage*> p;
+    for (auto& x : v) p.push_back(&x);
+    std::string out;
+    message_list_to_json(p, out);
+    return out;
+  });
+  m.def("dense_of", [](const std::string& text) {
+    SeldonMessage msg;
+    message_from_json(parse_json(text), msg);
+    std::vector<int64_t> shape;
+    std::vector<double> vals;
+    std::string err;
+    if (!msg.data.dense(shape, vals, &err)) throw std::runtime_error(err);
+    return py::make_tuple(shape, vals);
+  });
+  m.def("new_puid", [] {
+    Engine e(default_predictor_spec(), EngineOptions());
+    return e.new_puid();
+  });
+  m.def("parse_spec", [](const std::string& text, const std::string& predictor) {
+    PredictorSpecC s = parse_predictor_spec(parse_json(text), predictor);
+    py::dict d;
+    d["name"] = s.name;
+    d["graph"] = s.graph.name;
+    d["replicas"] = s.replicas;
+    return d;
+  }, py::arg("text"), py::arg("predictor") = "");
+
+  // ------------------------------------------------------------- models
+  py::class_<gpu::RowModel, std::shared_ptr<gpu::RowModel>>(m, "RowModel")
+      .def_property_readonly("name", &gpu::RowModel::name)
+      .def_property_readonly("in_cols", &gpu::RowModel::in_cols)
+      .def("out_cols", &gpu::RowModel::out_cols)
+      .def("set_class_names", &gpu::RowModel::set_class_names)
+      .def("run_cpu", [](const gpu::RowModel& mdl, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
+        if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
+        const int rows = int(X.shape(0)), cols = int(X.shape(1));
+        const int oc = mdl.out_cols(cols);
+        py::array_t<double> out({rows, oc});
+        mdl.run_cpu(X.data(), rows, cols, out.mutable_data());
+        return out;
+      });
+  m.def("linear_model",
+        [](py::array_t<double, py::array::c_style | py::array::forcecast> W,
+           py::array_t<double, py::array::c_style | py::array::forcecast> b, int act) {
+          if (W.ndim() != 2) throw std::runtime_error("W must be [C, K]");
+          return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::LinearModel>(
+              to_vec(W), to_vec(b), int(W.shape(0)), int(W.shape(1)), act));
+        },
+        py::arg("W"), py::arg("b"), py::arg("act"));
+  m.def("mean_sigmoid_model", [](double thr) {
+    return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MeanSigmoidModel>(thr));
+  });
+  m.def("tree_model",
+        [](py::dict d) {
+          gpu::TreeEnsembleSpec s;
+          s.n_trees = d["n_trees"].cast<int>();
+          s.n_features = d["n_features"].cast<int>();
+          s.groups = d.contains("groups") ? d["groups"].cast<int>() : 1;
+          s.out_cols = d.contains("out_cols") ? d["out_cols"].cast<int>() : s.groups;
+          s.transform = d.contains("transform") ? d["transform"].cast<int>() : 0;
+          s.cmp_le = d.contains("cmp_le") ? d["cmp_le"].cast<int>() : 0;
+          s.scale = d.contains("scale") ? d["scale"].cast<float>() : 1.f;
+          if (d.contains("base_margin")) s.base_margin = d["base_margin"].cast<std::vector<float>>();
+          if (d.contains("tree_group")) s.tree_group = d["tree_group"].cast<std::vector<int>>();
+          s.depth = d.contains("depth") ? d["depth"].cast<int>() : 0;
+          if (s.depth > 0) {
+            s.thr = to_vec(d["thr"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>());
+            s.feat = to_vec(d["feat"].cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>());
+            s.leaves = to_vec(d["leaves"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>());
+          } else {
+            auto thr = to_vec(d["thr"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>());
+            auto feat = to_vec(d["feat"].cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>());
+            auto left = to_vec(d["left"].cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>());
+            auto right = to_vec(d["right"].cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>());
+            if (thr.size() != feat.size() || thr.size() != left.size() || thr.size() != right.size())
+              throw std::runtime_error("sparse tree arrays must have equal length");
+            s.nodes.resize(thr.size());
+            for (size_t i = 0; i < thr.size(); ++i) s.nodes[i] = kern::SparseNode{thr[i], feat[i], left[i], right[i]};
+            s.tree_root = d["tree_root"].cast<std::vector<int>>();
+          }
+          return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::TreeEnsembleModel>(std::move(s)));
+        });
+
+  py::class_<gpu::BatchedUnit, std::shared_ptr<gpu::BatchedUnit>>(m, "BatchedUnit")
+      .def(py::init([](std::shared_ptr<gpu::RowModel> model, int device, int max_batch, int max_wait_us, int slots,
+                       bool zero_copy, size_t zc_bytes, bool spin) {
+             return std::make_shared<gpu::BatchedUnit>(
+                 model, batcher_opts(device, max_batch, max_wait_us, slots, zero_copy, zc_bytes, spin));
+           }),
+           py::arg("model"), py::arg("device") = 0, py::arg("max_batch") = 1024, py::arg("max_wait_us") = 0,
+           py::arg("slots") = 4, py::arg("zero_copy") = true, py::arg("zero_copy_max_bytes") = 256 << 10,
+           py::arg("spin_wait") = true)
+      .def("run", [](gpu::BatchedUnit& u, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
+        if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
+        const int rows = int(X.shape(0)), cols = int(X.shape(1));
+        std::vector<double> x(X.data(), X.data() + X.size());
+        std::vector<double> out;
+        {
+          py::gil_scoped_release nogil;
+          out = u.run_dense(x, rows, cols);
+        }
+        const int oc = int(out.size() / size_t(rows));
+        py::array_t<double> r({rows, oc});
+        std::copy(out.begin(), out.end(), r.mutable_data());
+        return r;
+      })
+      .def("stats", [](const gpu::BatchedUnit& u) {
+        auto s = u.stats();
+        py::dict d;
+        d["batches"] = s.batches;
+        d["rows"] = s.rows;
+        d["requests"] = s.requests;
+        d["max_rows"] = s.max_rows;
+        d["gpu_busy_s"] = s.gpu_busy_s;
+        return d;
+      })
+      .def("reset_stats", &gpu::BatchedUnit::reset_stats)
+      .def("stop", [](gpu::BatchedUnit& u) {
+        py::gil_scoped_release nogil;
+        u.stop();
+      });
+
+  // ------------------------------------------------------------- engine
+  py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
+      .def(py::init([](const std::string& spec_json, const std::string& deployment_name, const std::string& predictor,
+                       bool log_requests, bool log_responses, bool log_feedback) {
+             PredictorSpecC spec = spec_json.empty() ? default_predictor_spec()
+                                                     : parse_predictor_spec(parse_json(spec_json), predictor);
+             EngineOptions o;
+             o.deployment_name = deployment_name;
+             o.log_requests = log_requests;
+             o.log_responses = log_responses;
+             o.log_feedback = log_feedback;
+             return std::make_shared<Engine>(std::move(spec), o);
+           }),
+           py::arg("spec_json") = "", py::arg("deployment_name") = "None", py::arg("predictor") = "",
+           py::arg("log_requests") = false, py::arg("log_responses") = false, py::arg("log_feedback") = false)
+      .def("bind_python",
+           [](Engine& e, const std::string& node, py::object adapter, uint32_t builtin_methods) {
+             e.bind(node, std::make_shared<PyUnit>(std::move(adapter), builtin_methods));
+           },
+           py::arg("node"), py::arg("adapter"), py::arg("builtin_methods") = 0)
+      .def("bind_batched", [](Engine& e, const std::string& node,
+                              std::shared_ptr<gpu::BatchedUnit> u) { e.bind(node, u); })
+      .def("finalize", &Engine::finalize)
+      .def("ready", &Engine::ready)
+      .def("node_names", &Engine::node_names)
+      .def("unit_kind", [](const Engine& e, const std::string& n) {
+        auto u = e.unit_of(n);
+        return u ? u->kind() : std::string();
+      })
+      .def("node_methods", [](const Engine& e, const std::string& n) {
+        const Node* nd = e.node(n);
+        return nd ? nd->methods : 0u;
+      })
+      .def("snapshot", [](const Engine& e, const std::string& n) {
+        auto u = e.unit_of(n);
+        return py::bytes(u ? u->snapshot() : std::string());
+      })
+      .def("restore", [](const Engine& e, const std::string& n, const py::bytes& b) {
+        auto u = e.unit_of(n);
+        if (u) u->restore(std::string(b));
+      })
+      .def("predict_json",
+           [](Engine& e, const std::string& text) {
+             auto msg = std::make_shared<SeldonMessage>();
+             try {
+               message_from_json(parse_json(text), *msg);
+             } catch (const std::exception&) {
+               auto err = make_error(ApiError::INVALID_JSON, text);
+               return std::make_pair(err->http_status, error_to_json(*err));
+             }
+             Outcome o = wait_outcome([&](Done k) { e.predict(msg, std::move(k)); });
+             return render(o);
+           })
+      .def("predict_pb",
+           [](Engine& e, const py::bytes& b) -> py::tuple {
+             auto msg = std::make_shared<SeldonMessage>();
+             if (!message_from_pb(std::string(b), *msg)) {
+               auto err = make_error(ApiError::INVALID_JSON, "invalid protobuf");
+               return py::make_tuple(err->http_status, py::bytes(error_to_json(*err)));
+             }
+             Outcome o = wait_outcome([&](Done k) { e.predict(msg, std::move(k)); });
+             if (o.err) return py::make_tuple(o.err->http_status, py::bytes(error_to_json(*o.err)));
+             std::string out;
+             message_to_pb(*o.msg, out);
+             return py::make_tuple(200, py::bytes(out));
+           })
+      .def("feedback_json",
+           [](Engine& e, const std::string& text) {
+             auto fb = std::make_shared<Feedback>();
+             try {
+               feedback_from_json(parse_json(text), *fb);
+             } catch (const std::exception&) {
+               auto err = make_error(ApiError::INVALID_JSON, text);
+               return std::make_pair(err->http_status, error_to_json(*err));
+             }
+             std::promise<ErrPtr> p;
+             auto f = p.get_future();
+             ErrPtr err;
+             {
+               py::gil_scoped_release nogil;
+               e.send_feedback(fb, [&p](ErrPtr x) { p.set_value(std::move(x)); });
+               err = f.get();
+             }
+             if (err) return std::make_pair(err->http_status, error_to_json(*err));
+             return std::make_pair(200, std::string("{}"));
+           })
+      .def("call_node_json",
+           [](Engine& e, const std::string& node, int method, const std::string& text) {
+             std::vector<MsgPtr> in;
+             Json j = parse_json(text);
+             if (Method(method) == Method::AGGREGATE) {
+               std::vector<SeldonMessage> list;
+               message_list_from_json(j, list);
+               for (auto& x : list) in.push_back(std::make_shared<SeldonMessage>(std::move(x)));
+             } else {
+               auto msg = std::make_shared<SeldonMessage>();
+               message_from_json(j, *msg);
+               in.push_back(msg);
+             }
+             Outcome o = wait_outcome([&](Done k) { e.call_node(node, Method(method), std::move(in), std::move(k)); });
+             return render(o);
+           })
+      .def("metrics_text", [](Engine& e) { return e.metrics().render(); })
+      .def("new_puid", &Engine::new_puid);
+
+  py::class_<HttpServer, std::shared_ptr<HttpServer>>(m, "HttpServer")
+      .def(py::init([](std::shared_ptr<Engine> e, const std::string& host, std::vector<int> ports, int threads,
+                       const std::string& microservice_node, bool internal_api, const std::string& openapi) {
+             HttpOptions o;
+             o.host = host;
+             o.ports = std::move(ports);
+             o.threads = threads;
+             o.microservice_node = microservice_node;
+             o.internal_api = internal_api;
+             o.openapi_json = openapi;
+             return std::make_shared<HttpServer>(std::move(e), o);
+           }),
+           py::arg("engine"), py::arg("host") = "0.0.0.0", py::arg("ports") = std::vector<int>{8000},
+           py::arg("threads") = 4, py::arg("microservice_node") = "", py::arg("internal_api") = true,
+           py::arg("openapi") = "")
+      .def("start", &HttpServer::start)
+      .def("stop", [](HttpServer& s) {
+        py::gil_scoped_release nogil;
+        s.stop();
+      })
+      .def_property_readonly("ports", &HttpServer::bound_ports)
+      .def_property("paused", &HttpServer::paused, &HttpServer::set_paused)
+      .def_property_readonly("requests_served", &HttpServer::requests_served);
+
+  py::class_<GrpcServer, std::shared_ptr<GrpcServer>>(m, "GrpcServer")
+      .def(py::init([](std::shared_ptr<Engine> e, const std::string& host, int port, int threads,
+                       const std::string& microservice_node, size_t max_message) {
+             GrpcOptions o;
+             o.host = host;
+             o.port = port;
+             o.threads = threads;
+             o.microservice_node = microservice_node;
+             o.max_message = max_message;
+             return std::make_shared<GrpcServer>(std::move(e), o);
+           }),
+           py::arg("engine"), py::arg("host") = "0.0.0.0", py::arg("port") = 5001, py::arg("threads") = 4,
+           py::arg("microservice_node") = "", py::arg("max_message") = size_t(64) << 20)
+      .def("start", &GrpcServer::start)
+      .def("stop", [](GrpcServer& s) {
+        py::gil_scoped_release nogil;
+        s.stop();
+      })
+      .def_property_readonly("port", &GrpcServer::bound_port)
+      .def_property_readonly("requests_served", &GrpcServer::requests_served);
+
+  // ------------------------------------------------------------- raw kernels
+  // Pointers are device (or mapped) addresses as Python ints (tensor.data_ptr()),
+  // stream is torch.cuda.current_stream().cuda_stream.
+  py::module_ k = m.def_submodule("kernels", "raw gfx950 kernel launchers");
+  k.def("linear_f64", [](uintptr_t X, int rows, int K, uintptr_t W, uintptr_t b, int C, int act, uintptr_t out,
+                         uintptr_t s) {
+    kern::linear_f64(P<const double>(X), rows, K, P<const double>(W), P<const double>(b), C, act, P<double>(out),
+                     as_stream(s));
+  });
+  k.def("tree_perfect_partial", [](uintptr_t X, int rows, int F, uintptr_t nodes, uintptr_t leaves, int depth,
+                                   int cmp_le, uintptr_t chunk_begin, int n_chunks, int rb, uintptr_t partial,
+                                   uintptr_t s) {
+    kern::tree_perfect_partial(P<const double>(X), rows, F, P<const kern::TreeNode>(nodes), P<const float>(leaves),
+                               depth, cmp_le, P<const int>(chunk_begin), n_chunks, rb, P<float>(partial),
+                               as_stream(s));
+  });
+  k.def("tree_reduce", [](uintptr_t partial, int rows, int n_chunks, uintptr_t chunk_group, int groups,
+                          uintptr_t base, float scale, int transform, uintptr_t out, int out_cols, uintptr_t s) {
+    kern::tree_reduce(P<const float>(partial), rows, n_chunks, P<const int>(chunk_group), groups, P<const float>(base),
+                      scale, transform, P<double>(out), out_cols, as_stream(s));
+  });
+  k.def("combine_mean_f64", [](uintptr_t inputs, int n_in, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::combine_mean_f64(P<const double* const>(inputs), n_in, n, P<double>(out), as_stream(s));
+  });
+  k.def("softmax_rows_f64", [](uintptr_t in, int rows, int C, uintptr_t out, uintptr_t s) {
+    kern::softmax_rows_f64(P<const double>(in), rows, C, P<double>(out), as_stream(s));
+  });
+  k.def("argmax_rows_f64", [](uintptr_t in, int rows, int C, uintptr_t out, uintptr_t s) {
+    kern::argmax_rows_f64(P<const double>(in), rows, C, P<int32_t>(out), as_stream(s));
+  });
+  k.def("minmax_normalize_f64", [](uintptr_t in, int64_t n, uintptr_t out, uintptr_t scratch, uintptr_t s) {
+    kern::minmax_normalize_f64(P<const double>(in), n, P<double>(out), P<double>(scratch), as_stream(s));
+  });
+  k.def("mean_sigmoid_rows_f64", [](uintptr_t in, int rows, int F, double thr, uintptr_t out, uintptr_t s) {
+    kern::mean_sigmoid_rows_f64(P<const double>(in), rows, F, thr, P<double>(out), as_stream(s));
+  });
+  k.def("eg_route", [](uintptr_t values, int nb, float eps, uint64_t seed, uint64_t offset, int n, uintptr_t out,
+                       uintptr_t s) {
+    kern::eg_route(P<const float>(values), nb, eps, seed, offset, n, P<int32_t>(out), as_stream(s));
+  });
+  k.def("ts_route", [](uintptr_t alpha, uintptr_t beta, int nb, uint64_t seed, uint64_t offset, int n, uintptr_t out,
+                       uintptr_t s) {
+    kern::ts_route(P<const float>(alpha), P<const float>(beta), nb, seed, offset, n, P<int32_t>(out), as_stream(s));
+  });
+}

@@ -1,0 +1,517 @@
+#include "engine.h"
+
+#include <chrono>
+#include <cstdio>
+#include <random>
+#include <stdexcept>
+
+namespace sca {
+
+// ------------------------------------------------------------------ errors
+ErrPtr make_error(ApiError kind, std::string info) {
+  auto e = std::make_shared<EngineError>();
+  e->info = std::move(info);
+  e->http_status = 500;
+  switch (kind) {
+    case ApiError::INVALID_JSON: e->code = 201; e->reason = "Invalid JSON"; break;
+    case ApiError::INVALID_ENDPOINT_URL: e->code = 202; e->reason = "Invalid Endpoint URL"; break;
+    case ApiError::MICROSERVICE_ERROR: e->code = 203; e->reason = "Microservice error"; break;
+    case ApiError::INVALID_ABTEST: e->code = 204; e->reason = "Error happened in AB Test Routing"; break;
+    case ApiError::INVALID_COMBINER_RESPONSE: e->code = 204; e->reason = "Invalid number of predictions from combiner"; break;
+    case ApiError::INTERRUPTED: e->code = 205; e->reason = "API call interrupted"; break;
+    case ApiError::EXECUTION_FAILURE: e->code = 206; e->reason = "Execution failure"; break;
+    case ApiError::INVALID_ROUTING: e->code = 207; e->reason = "Invalid Routing"; break;
+    case ApiError::REQUEST_IO_EXCEPTION: e->code = 208; e->reason = "IO Exception"; break;
+    case ApiError::UNAVAILABLE: e->code = 209; e->reason = "Service unavailable"; e->http_status = 503; break;
+    case ApiError::DEADLINE_EXCEEDED: e->code = 210; e->reason = "Deadline exceeded"; e->http_status = 504; break;
+  }
+  return e;
+}
+
+std::string error_to_json(const EngineError& e) {
+  Status s;
+  s.code = e.code;
+  s.info = e.info;
+  s.reason = e.reason;
+  s.status = 1;
+  std::string out;
+  status_to_json(s, out);
+  return out;
+}
+
+bool branch_index(const SeldonMessage& m, int& out) {
+  if (m.payload != Payload::Data) return false;
+  std::vector<int64_t> shape;
+  std::vector<double> vals;
+  if (!m.data.dense(shape, vals, nullptr) || vals.empty()) return false;
+  out = int(vals[0]);
+  return true;
+}
+
+// ------------------------------------------------------------- puid (130b)
+namespace {
+
+struct Xoshiro {
+  uint64_t s[4];
+  Xoshiro() {
+    std::random_device rd;
+    for (auto& x : s) x = (uint64_t(rd()) << 32) ^ rd() ^ 0x9E3779B97F4A7C15ULL;
+  }
+  static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+  uint64_t next() {
+    uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
+    s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3]; s[2] ^= t; s[3] = rotl(s[3], 45);
+    return r;
+  }
+};
+
+const uint32_t kTI = method_bit(Method::TRANSFORM_INPUT), kTO = method_bit(Method::TRANSFORM_OUTPUT),
+               kRO = method_bit(Method::ROUTE), kAG = method_bit(Method::AGGREGATE),
+               kSF = method_bit(Method::SEND_FEEDBACK);
+
+// PredictorConfigBean.java:45-72
+uint32_t type_methods(UnitType t) {
+  switch (t) {
+    case UnitType::MODEL: return kTI | kSF;
+    case UnitType::TRANSFORMER: return kTI;
+    case UnitType::OUTPUT_TRANSFORMER: return kTO;
+    case UnitType::ROUTER: return kRO | kSF;
+    case UnitType::COMBINER: return kAG;
+    default: return 0;
+  }
+}
+
+const char* method_uri(Method m) {
+  switch (m) {
+    case Method::TRANSFORM_INPUT: return "/transform-input";
+    case Method::TRANSFORM_OUTPUT: return "/transform-output";
+    case Method::ROUTE: return "/route";
+    case Method::AGGREGATE: return "/aggregate";
+    case Method::SEND_FEEDBACK: return "/send-feedback";
+  }
+  return "/";
+}
+
+using Clock = std::chrono::steady_clock;
+
+// Wrap a continuation so it fires at most once even if a unit misbehaves,
+// time the call, and turn thrown exceptions into engine errors.
+template <class F>
+void guarded(Series* timer, Done k, F&& body) {
+  struct Once {
+    std::atomic<bool> fired{false};
+    Done k;
+    Series* timer;
+    Clock::time_point t0;
+  };
+  auto st = std::make_shared<Once>();
+  st->k = std::move(k);
+  st->timer = timer;
+  st->t0 = Clock::now();
+  Done kk = [st](Outcome o) {
+    if (st->fired.exchange(true)) return;
+    if (st->timer) st->timer->observe_seconds(std::chrono::duration<double>(Clock::now() - st->t0).count());
+    st->k(std::move(o));
+  };
+  try {
+    body(kk);
+  } catch (const std::exception& e) {
+    kk(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, e.what())));
+  }
+}
+
+MsgPtr merge_meta(MsgPtr latest, const std::vector<const SeldonMessage*>& prev, const std::string& puid) {
+  Json::Object tags;
+  auto put = [&](const Json::Object& src) {
+    for (const auto& kv : src) {
+      bool done = false;
+      for (auto& t : tags)
+        if (t.first == kv.first) { t.second = kv.second; done = true; break; }
+      if (!done) tags.push_back(kv);
+    }
+  };
+  for (const auto* p : prev) put(p->meta.tags);
+  put(latest->meta.tags);
+  MsgPtr out = latest.use_count() == 1 ? std::move(latest) : std::make_shared<SeldonMessage>(*latest);
+  out->has_meta = true;
+  out->meta = Meta();
+  out->meta.puid = puid;
+  out->meta.tags = std::move(tags);
+  return out;
+}
+
+}  // namespace
+
+std::string Engine::new_puid() {
+  thread_local Xoshiro rng;
+  uint64_t hi = rng.next() & 3, mid = rng.next(), lo = rng.next();  // 130 bits
+  static const char* digits = "0123456789abcdefghijklmnopqrstuv";
+  char buf[27];
+  int n = 0;
+  for (int g = 25; g >= 0; --g) {
+    int bit = g * 5;  // 5-bit group starting at bit `bit` of the 130-bit integer
+    uint32_t v = 0;
+    for (int b = 4; b >= 0; --b) {
+      int pos = bit + b;
+      uint64_t w = pos >= 128 ? hi : pos >= 64 ? mid : lo;
+      v = (v << 1) | uint32_t((w >> (pos & 63)) & 1);
+    }
+    if (n == 0 && v == 0) continue;
+    buf[n++] = digits[v];
+  }
+  if (n == 0) buf[n++] = '0';
+  return std::string(buf, size_t(n));
+}
+
+// ------------------------------------------------------------------ engine
+struct Engine::ReqCtx {
+  std::string puid;
+  std::mutex mu;
+  std::vector<std::pair<std::string, int32_t>> routing;
+  StrMap request_path;
+  std::vector<std::pair<std::string, std::vector<Metric>>> metrics;
+};
+
+Engine::Engine(PredictorSpecC spec, EngineOptions opts) : spec_(std::move(spec)), opts_(std::move(opts)) {
+  std::string pname = spec_.name.empty() ? "unknown" : spec_.name;
+  auto it = spec_.labels.find("version");
+  std::string pver = (it == spec_.labels.end() || it->second.empty()) ? "unknown" : it->second;
+  base_labels_ = {{"deployment_name", opts_.deployment_name}, {"predictor_name", pname}, {"predictor_version", pver}};
+}
+
+Engine::~Engine() = default;
+
+void Engine::bind(const std::string& node, UnitPtr unit) {
+  if (root_) throw std::runtime_error("engine already finalized");
+  bound_[node] = std::move(unit);
+}
+
+UnitPtr Engine::unit_of(const std::string& node) const {
+  for (const auto& n : nodes_)
+    if (n->name == node) return n->unit;
+  auto it = bound_.find(node);
+  return it == bound_.end() ? nullptr : it->second;
+}
+
+Node* Engine::compile(const UnitSpec& u) {
+  auto n = std::make_unique<Node>();
+  n->spec = &u;
+  n->name = u.name;
+  n->image = u.image;
+  auto it = bound_.find(u.name);
+  if (it != bound_.end()) {
+    n->unit = it->second;
+  } else {
+    n->unit = make_builtin_unit(u.implementation, u);
+    if (!n->unit)
+      throw std::runtime_error("no implementation bound for graph node '" + u.name + "' (implementation " +
+                               (u.implementation_name.empty() ? "UNKNOWN_IMPLEMENTATION" : u.implementation_name) + ")");
+  }
+  if (uint32_t b = n->unit->builtin_methods()) {
+    n->methods = b;
+    n->builtin = true;
+  } else if (!u.has_type || u.type == UnitType::UNKNOWN_TYPE) {
+    for (Method m : u.methods) n->methods |= method_bit(m);
+  } else {
+    n->methods = type_methods(u.type);
+  }
+  n->model_labels = base_labels_;
+  n->model_labels.push_back({"model_name", u.name.empty() ? "unknown" : u.name});
+  n->model_labels.push_back({"model_image", u.image_name.empty() ? "unknown" : u.image_name});
+  n->model_labels.push_back({"model_version", u.image_version.empty() ? "latest" : u.image_version});
+  for (int m = 0; m < 5; ++m) {
+    if (!(n->methods & (1u << m))) continue;
+    Labels l = n->model_labels;
+    l.push_back({"method", "POST"});
+    l.push_back({"uri", (Method(m) == Method::TRANSFORM_INPUT && (u.type == UnitType::MODEL)) ? "/predict" : method_uri(Method(m))});
+    n->client_timer[m] = metrics_.timer("seldon_api_engine_client_requests", std::move(l), true);
+  }
+  n->fb_reward = metrics_.counter("seldon_api_model_feedback_reward", n->model_labels);
+  n->fb_count = metrics_.counter("seldon_api_model_feedback", n->model_labels);
+  Node* raw = n.get();
+  nodes_.push_back(std::move(n));
+  for (const auto& c : u.children) raw->children.push_back(compile(c));
+  return raw;
+}
+
+void Engine::finalize() {
+  if (root_) return;
+  root_ = compile(spec_.graph);
+}
+
+std::vector<std::string> Engine::node_names() const {
+  std::vector<std::string> v;
+  for (const auto& n : nodes_) v.push_back(n->name);
+  return v;
+}
+
+const Node* Engine::node(const std::string& name) const {
+  for (const auto& n : nodes_)
+    if (n->name == name) return n.get();
+  return nullptr;
+}
+
+bool Engine::ready() const {
+  if (!root_) return false;
+  for (const auto& n : nodes_)
+    if (!n->unit->ready()) return false;
+  return true;
+}
+
+void Engine::add_metrics(Node* n, const SeldonMessage& m, ReqCtx* ctx) {
+  if (!m.has_meta || m.meta.metrics.empty()) return;
+  for (const auto& mt : m.meta.metrics) {
+    Labels l = n->model_labels;
+    for (const auto& t : mt.tags) l.push_back(t);
+    switch (mt.type) {
+      case MetricType::COUNTER: metrics_.counter(mt.key, std::move(l))->inc(mt.value); break;
+      case MetricType::GAUGE: metrics_.gauge(mt.key, std::move(l))->set(mt.value); break;
+      case MetricType::TIMER: metrics_.timer(mt.key, std::move(l))->observe_seconds(double(mt.value) / 1000.0); break;
+    }
+  }
+  if (!ctx) return;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (auto& e : ctx->metrics)
+    if (e.first == n->name) {
+      e.second.insert(e.second.end(), m.meta.metrics.begin(), m.meta.metrics.end());
+      return;
+    }
+  ctx->metrics.emplace_back(n->name, m.meta.metrics);
+}
+
+void Engine::predict(MsgPtr req, Done k) {
+  if (!root_) {
+    k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "graph not finalized")));
+    return;
+  }
+  if (!req->has_meta) {
+    req->has_meta = true;
+    req->meta.puid = new_puid();
+  } else if (req->meta.puid.empty()) {
+    req->meta.puid = new_puid();
+  }
+  auto ctx = std::make_shared<ReqCtx>();
+  ctx->puid = req->meta.puid;
+  MsgPtr request_copy = (pair_hook_ ? req : nullptr);
+  eval(root_, req, ctx, [this, ctx, k = std::move(k), request_copy](Outcome o) {
+    if (o.err) { k(std::move(o)); return; }
+    MsgPtr r = o.msg.use_count() == 1 ? std::move(o.msg) : std::make_shared<SeldonMessage>(*o.msg);
+    {
+      std::lock_guard<std::mutex> g(ctx->mu);
+      r->has_meta = true;
+      for (auto& kv : ctx->routing) r->meta.put_routing(kv.first, kv.second);
+      for (auto& kv : ctx->request_path) r->meta.put_request_path(kv.first, kv.second);
+      for (auto& e : ctx->metrics) r->meta.metrics.insert(r->meta.metrics.end(), e.second.begin(), e.second.end());
+    }
+    r->meta.puid = ctx->puid;
+    if (pair_hook_ && request_copy) pair_hook_(*request_copy, *r);
+    k(Outcome::ok(std::move(r)));
+  });
+}
+
+void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    bool found = false;
+    for (auto& kv : ctx->request_path)
+      if (kv.first == n->name) { kv.second = n->image; found = true; break; }
+    if (!found) ctx->request_path.emplace_back(n->name, n->image);
+  }
+  if (!n->has(Method::TRANSFORM_INPUT)) {
+    after_input(n, input, input, std::move(ctx), std::move(k));
+    return;
+  }
+  CallCtx cc{n, &ctx->puid};
+  guarded(n->client_timer[int(Method::TRANSFORM_INPUT)],
+          [this, n, input, ctx, k](Outcome o) mutable {
+            if (o.err) { k(std::move(o)); return; }
+            if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
+            after_input(n, std::move(input), std::move(o.msg), std::move(ctx), std::move(k));
+          },
+          [&](Done kk) { n->unit->transform_input(cc, input, std::move(kk)); });
+}
+
+void Engine::after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCtx> ctx, Done k) {
+  add_metrics(n, *ti, ctx.get());
+  const SeldonMessage* in_raw = input.get();
+  MsgPtr keep_in = std::move(input);
+  ti = merge_meta(std::move(ti), {in_raw}, ctx->puid);
+  keep_in.reset();
+  if (n->children.empty()) {
+    k(Outcome::ok(std::move(ti)));
+    return;
+  }
+  auto dispatch = [this, n, ctx, k](MsgPtr ti2, int routing) {
+    {
+      std::lock_guard<std::mutex> g(ctx->mu);
+      bool found = false;
+      for (auto& kv : ctx->routing)
+        if (kv.first == n->name) { kv.second = routing; found = true; break; }
+      if (!found) ctx->routing.emplace_back(n->name, routing);
+    }
+    std::vector<Node*> selected;
+    if (routing == -1) selected = n->children;
+    else selected.push_back(n->children[size_t(routing)]);
+    struct Fan {
+      std::vector<MsgPtr> outs;
+      std::atomic<int> remaining;
+      std::atomic<bool> failed{false};
+    };
+    auto fan = std::make_shared<Fan>();
+    fan->outs.resize(selected.size());
+    fan->remaining.store(int(selected.size()));
+    for (size_t i = 0; i < selected.size(); ++i) {
+      eval(selected[i], ti2, ctx, [this, n, ctx, k, fan, i](Outcome o) {
+        if (o.err) {
+          if (!fan->failed.exchange(true)) k(std::move(o));
+          return;
+        }
+        fan->outs[i] = std::move(o.msg);
+        if (fan->remaining.fetch_sub(1, std::memory_order_acq_rel) == 1 && !fan->failed.load())
+          fan_in(n, std::move(fan->outs), ctx, k);
+      });
+    }
+  };
+  if (!n->has(Method::ROUTE)) {
+    dispatch(std::move(ti), -1);
+    return;
+  }
+  CallCtx cc{n, &ctx->puid};
+  MsgPtr ti_keep = ti;
+  guarded(n->client_timer[int(Method::ROUTE)],
+          [this, n, ctx, k, ti_keep, dispatch](Outcome o) {
+            if (o.err) { k(std::move(o)); return; }
+            int routing = -1;
+            if (o.msg) {
+              if (!branch_index(*o.msg, routing)) {
+                k(Outcome::fail(make_error(ApiError::INVALID_ROUTING, "Router that caused the exception: id=" + n->name + " name=" + n->name)));
+                return;
+              }
+              if (routing < -1 || routing >= int(n->children.size())) {
+                k(Outcome::fail(make_error(ApiError::INVALID_ROUTING,
+                                           "Invalid branch index. Router that caused the exception: id=" + n->name + " name=" + n->name)));
+                return;
+              }
+              add_metrics(n, *o.msg, ctx.get());
+            }
+            dispatch(ti_keep, routing);
+          },
+          [&](Done kk) { n->unit->route(cc, ti, std::move(kk)); });
+}
+
+void Engine::fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> ctx, Done k) {
+  auto after_agg = [this, n, ctx, k, outs](Outcome o) {
+    if (o.err) { k(std::move(o)); return; }
+    if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty aggregate from " + n->name))); return; }
+    add_metrics(n, *o.msg, ctx.get());
+    std::vector<const SeldonMessage*> prev;
+    prev.reserve(outs.size());
+    for (const auto& m : outs) prev.push_back(m.get());
+    MsgPtr agg = merge_meta(std::move(o.msg), prev, ctx->puid);
+    if (!n->has(Method::TRANSFORM_OUTPUT)) {  // identity transform: meta already merged
+      k(Outcome::ok(std::move(agg)));
+      return;
+    }
+    CallCtx cc{n, &ctx->puid};
+    guarded(n->client_timer[int(Method::TRANSFORM_OUTPUT)],
+            [this, n, ctx, k, agg](Outcome o2) {
+              if (o2.err) { k(std::move(o2)); return; }
+              if (!o2.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
+              add_metrics(n, *o2.msg, ctx.get());
+              k(Outcome::ok(merge_meta(std::move(o2.msg), {agg.get()}, ctx->puid)));
+            },
+            [&](Done kk) { n->unit->transform_output(cc, agg, std::move(kk)); });
+  };
+  if (!n->has(Method::AGGREGATE)) {
+    after_agg(Outcome::ok(outs[0]));
+    return;
+  }
+  CallCtx cc{n, &ctx->puid};
+  guarded(n->client_timer[int(Method::AGGREGATE)], after_agg,
+          [&](Done kk) { n->unit->aggregate(cc, outs, std::move(kk)); });
+}
+
+// ----------------------------------------------------------------- feedback
+void Engine::send_feedback(std::shared_ptr<Feedback> fb, FbDone k) {
+  if (!root_) {
+    k(make_error(ApiError::UNAVAILABLE, "graph not finalized"));
+    return;
+  }
+  feedback_node(root_, std::move(fb), std::move(k));
+}
+
+void Engine::feedback_node(Node* n, std::shared_ptr<const Feedback> fb, FbDone k) {
+  int32_t routing = -1;
+  fb->response.meta.routing_of(n->name, routing);
+  std::vector<Node*> children;
+  if (routing == -1) children = n->children;
+  else if (routing >= 0) {
+    if (size_t(routing) >= n->children.size()) {
+      k(make_error(ApiError::INVALID_ROUTING, "Invalid feedback routing " + std::to_string(routing) + " for node " + n->name));
+      return;
+    }
+    children.push_back(n->children[size_t(routing)]);
+  }
+  struct Join {
+    std::atomic<int> remaining;
+    std::mutex mu;
+    ErrPtr err;
+  };
+  auto join = std::make_shared<Join>();
+  join->remaining.store(int(children.size()) + 1);
+  auto arrive = [this, n, fb, join, k](ErrPtr e) {
+    if (e) {
+      std::lock_guard<std::mutex> g(join->mu);
+      if (!join->err) join->err = e;
+    }
+    if (join->remaining.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+    if (!join->err) {  // PredictiveUnitBean.java:313-316
+      n->fb_reward->inc(double(fb->reward));
+      n->fb_count->inc(1.0);
+    }
+    k(join->err);
+  };
+  for (Node* c : children) feedback_node(c, fb, arrive);
+  if (!n->has(Method::SEND_FEEDBACK)) {
+    arrive(nullptr);
+    return;
+  }
+  CallCtx cc{n, &fb->response.meta.puid};
+  Series* timer = n->client_timer[int(Method::SEND_FEEDBACK)];
+  auto t0 = Clock::now();
+  auto once = std::make_shared<std::atomic<bool>>(false);
+  FbDone kk = [arrive, once, timer, t0](ErrPtr e) {
+    if (once->exchange(true)) return;
+    if (timer) timer->observe_seconds(std::chrono::duration<double>(Clock::now() - t0).count());
+    arrive(std::move(e));
+  };
+  try {
+    n->unit->send_feedback(cc, fb, kk);
+  } catch (const std::exception& e) {
+    kk(make_error(ApiError::MICROSERVICE_ERROR, e.what()));
+  }
+}
+
+// ---------------------------------------------------------- direct node call
+void Engine::call_node(const std::string& name, Method m, std::vector<MsgPtr> in, Done k) {
+  Node* n = nullptr;
+  for (auto& x : nodes_)
+    if (x->name == name) { n = x.get(); break; }
+  if (!n) {
+    k(Outcome::fail(make_error(ApiError::EXECUTION_FAILURE, "unknown node " + name)));
+    return;
+  }
+  static const std::string empty;
+  CallCtx cc{n, in.empty() ? &empty : &in[0]->meta.puid};
+  guarded(n->client_timer[int(m)], std::move(k), [&](Done kk) {
+    switch (m) {
+      case Method::TRANSFORM_INPUT: n->unit->transform_input(cc, in.at(0), std::move(kk)); break;
+      case Method::TRANSFORM_OUTPUT: n->unit->transform_output(cc, in.at(0), std::move(kk)); break;
+      case Method::ROUTE: n->unit->route(cc, in.at(0), std::move(kk)); break;
+      case Method::AGGREGATE: n->unit->aggregate(cc, std::move(in), std::move(kk)); break;
+      case Method::SEND_FEEDBACK: kk(Outcome::fail(make_error(ApiError::EXECUTION_FAILURE, "use send_feedback"))); break;
+    }
+  });
+}
+
+}  // namespace sca

@@ -1,0 +1,197 @@
+// In-process inference-graph executor.
+//
+// Semantics follow the reference engine's PredictiveUnitBean
+// (engine/src/main/java/io/seldon/engine/predictors/PredictiveUnitBean.java:81-372):
+// transform-input -> merge meta -> (leaf? return) -> route (-1 = all children)
+// -> fan-out -> join -> aggregate -> merge meta -> transform-output -> merge
+// meta, accumulating routing / requestPath / metrics for the final response
+// meta, and feedback traversal along response.meta.routing.
+//
+// Unlike the reference (one HTTP hop + a thread hop per node, graph rebuilt
+// from the spec on every request: PredictionService.java:113) the graph is
+// compiled once and evaluated with continuations: a node bound to a GPU unit
+// enqueues rows into that unit's micro-batcher and the request resumes on the
+// batcher's completion thread, so no thread ever blocks on a device.
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "message.h"
+#include "metrics.h"
+#include "spec.h"
+
+namespace sca {
+
+// ------------------------------------------------------------------ errors
+// engine/src/main/java/io/seldon/engine/exception/APIException.java:28-38
+enum class ApiError : int {
+  INVALID_JSON,
+  INVALID_ENDPOINT_URL,
+  MICROSERVICE_ERROR,
+  INVALID_ABTEST,
+  INVALID_COMBINER_RESPONSE,
+  INTERRUPTED,
+  EXECUTION_FAILURE,
+  INVALID_ROUTING,
+  REQUEST_IO_EXCEPTION,
+  // engine-native additions
+  UNAVAILABLE,
+  DEADLINE_EXCEEDED,
+};
+
+struct EngineError {
+  int code = 206;
+  std::string reason;
+  std::string info;
+  int http_status = 500;
+};
+using ErrPtr = std::shared_ptr<const EngineError>;
+
+ErrPtr make_error(ApiError kind, std::string info);
+std::string error_to_json(const EngineError& e);
+
+struct Outcome {
+  MsgPtr msg;
+  ErrPtr err;
+  static Outcome ok(MsgPtr m) { return Outcome{std::move(m), nullptr}; }
+  static Outcome fail(ErrPtr e) { return Outcome{nullptr, std::move(e)}; }
+};
+using Done = std::function<void(Outcome)>;
+using FbDone = std::function<void(ErrPtr)>;
+
+// --------------------------------------------------------------- node model
+struct Node;
+
+struct CallCtx {
+  const Node* node;
+  const std::string* puid;
+};
+
+// A unit implements a subset of the five predictive-unit methods.  Every
+// method must invoke its continuation exactly once (on any thread).
+class Unit {
+ public:
+  virtual ~Unit() = default;
+  // For built-ins: the methods the implementation overrides (a built-in
+  // implementation short-circuits the type table, PredictorConfigBean.java:84-107).
+  // Return 0 to use the node's type/methods table.
+  virtual uint32_t builtin_methods() const { return 0; }
+  virtual void transform_input(const CallCtx& c, MsgPtr in, Done k) { (void)c; k(Outcome::ok(std::move(in))); }
+  virtual void transform_output(const CallCtx& c, MsgPtr in, Done k) { (void)c; k(Outcome::ok(std::move(in))); }
+  virtual void route(const CallCtx& c, MsgPtr in, Done k) { (void)c; (void)in; k(Outcome::ok(nullptr)); }
+  virtual void aggregate(const CallCtx& c, std::vector<MsgPtr> in, Done k) { (void)c; k(Outcome::ok(in.empty() ? nullptr : in[0])); }
+  virtual void send_feedback(const CallCtx& c, std::shared_ptr<const Feedback> fb, FbDone k) { (void)c; (void)fb; k(nullptr); }
+  virtual bool ready() const { return true; }
+  virtual std::string kind() const { return "unit"; }
+  // Snapshot / restore of online state (routers, detectors); "" = stateless.
+  virtual std::string snapshot() const { return ""; }
+  virtual void restore(const std::string&) {}
+};
+using UnitPtr = std::shared_ptr<Unit>;
+
+struct Node {
+  const UnitSpec* spec = nullptr;
+  std::string name;
+  std::string image;
+  uint32_t methods = 0;  // effective method mask
+  bool builtin = false;
+  std::vector<Node*> children;
+  UnitPtr unit;
+  Labels model_labels;    // deployment/predictor/model tags for metrics
+  Series* client_timer[5] = {};
+  Series* fb_reward = nullptr;
+  Series* fb_count = nullptr;
+  bool has(Method m) const { return methods & method_bit(m); }
+};
+
+struct EngineOptions {
+  std::string deployment_name = "None";
+  bool log_requests = false;
+  bool log_responses = false;
+  bool log_feedback = false;
+  std::string message_logging_service;  // CloudEvents sink (empty = off)
+};
+
+class Engine {
+ public:
+  Engine(PredictorSpecC spec, EngineOptions opts);
+  ~Engine();
+
+  const PredictorSpecC& spec() const { return spec_; }
+  MetricsRegistry& metrics() { return metrics_; }
+  const EngineOptions& options() const { return opts_; }
+
+  // Bind an implementation to a node (before finalize()).
+  void bind(const std::string& node, UnitPtr unit);
+  UnitPtr unit_of(const std::string& node) const;
+  // Compile the graph. Throws std::runtime_error if a node is unbound.
+  void finalize();
+  bool finalized() const { return root_ != nullptr; }
+  std::vector<std::string> node_names() const;
+  const Node* node(const std::string& name) const;
+
+  // Async API (thread-safe).
+  void predict(MsgPtr request, Done k);
+  void send_feedback(std::shared_ptr<Feedback> fb, FbDone k);
+  // Reference "internal API" entry: call one node's method directly
+  // (microservice mode: /predict, /route, ...).  `method` as in Method.
+  void call_node(const std::string& node, Method m, std::vector<MsgPtr> in, Done k);
+
+  bool ready() const;
+  std::string new_puid();
+
+  // Hook invoked after each completed prediction (request, response) — used
+  // by the async request logger.  Called on the completing thread.
+  using PairHook = std::function<void(const SeldonMessage&, const SeldonMessage&)>;
+  void set_pair_hook(PairHook h) { pair_hook_ = std::move(h); }
+
+ private:
+  struct ReqCtx;
+  void eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k);
+  void after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCtx> ctx, Done k);
+  void fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> ctx, Done k);
+  void feedback_node(Node* n, std::shared_ptr<const Feedback> fb, FbDone k);
+  void add_metrics(Node* n, const SeldonMessage& m, ReqCtx* ctx);
+  Node* compile(const UnitSpec& u);
+
+  PredictorSpecC spec_;
+  EngineOptions opts_;
+  MetricsRegistry metrics_;
+  std::unordered_map<std::string, UnitPtr> bound_;
+  std::vector<std::unique_ptr<Node>> nodes_;
+  Node* root_ = nullptr;
+  Labels base_labels_;
+  PairHook pair_hook_;
+};
+
+// Built-in implementations (engine/.../predictors/*Unit.java).
+UnitPtr make_builtin_unit(UnitImpl impl, const UnitSpec& spec);
+
+// Java's java.util.Random (48-bit LCG) so RANDOM_ABTEST reproduces the
+// reference's branch sequence for a given seed (RandomABTestUnit.java:31-59).
+class JavaRandom {
+ public:
+  explicit JavaRandom(int64_t seed) { set_seed(seed); }
+  void set_seed(int64_t seed) { seed_ = (uint64_t(seed) ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); }
+  int32_t next(int bits) {
+    seed_ = (seed_ * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+    return int32_t(int64_t(seed_) >> (48 - bits));
+  }
+  float next_float() { return float(next(24)) / float(1 << 24); }
+  uint64_t state() const { return seed_; }
+  void set_state(uint64_t s) { seed_ = s; }
+
+ private:
+  uint64_t seed_;
+};
+
+// Dense branch index from a router response (PredictiveUnitBean.java:301-311).
+bool branch_index(const SeldonMessage& m, int& out);
+
+}  // namespace sca

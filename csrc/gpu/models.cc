@@ -1,0 +1,234 @@
+#include "models.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace sca::gpu {
+
+// ------------------------------------------------------------------ linear
+LinearModel::LinearModel(std::vector<double> W, std::vector<double> b, int C, int K, int act)
+    : W_(std::move(W)), b_(std::move(b)), C_(C), K_(K), act_(act) {
+  if (int64_t(W_.size()) != int64_t(C) * K) throw std::runtime_error("LinearModel: W size mismatch");
+  if (!b_.empty() && int(b_.size()) != C) throw std::runtime_error("LinearModel: b size mismatch");
+  if (b_.empty()) b_.assign(size_t(C), 0.0);
+  if (act == kern::kActBinaryLogistic && C != 1) throw std::runtime_error("LinearModel: binary logistic needs C == 1");
+}
+
+void LinearModel::to_device(int device) {
+  dW_.alloc(W_.size() * sizeof(double), device);
+  dW_.upload(W_.data(), W_.size() * sizeof(double));
+  db_.alloc(b_.size() * sizeof(double), device);
+  db_.upload(b_.data(), b_.size() * sizeof(double));
+}
+
+void LinearModel::launch(const double* X, int rows, int cols, double* out, void*, hipStream_t s) {
+  (void)cols;
+  kern::linear_f64(X, rows, K_, dW_.as<double>(), db_.as<double>(), C_, act_, out, s);
+}
+
+void LinearModel::run_cpu(const double* X, int rows, int, double* out) const {
+  std::vector<double> z(static_cast<size_t>(C_));
+  const int oc = out_cols(K_);
+  for (int r = 0; r < rows; ++r) {
+    for (int c = 0; c < C_; ++c) {
+      double acc = b_[size_t(c)];
+      for (int k = 0; k < K_; ++k) acc = std::fma(X[size_t(r) * K_ + k], W_[size_t(c) * K_ + k], acc);
+      z[size_t(c)] = acc;
+    }
+    double* o = out + size_t(r) * oc;
+    switch (act_) {
+      case kern::kActIdentity: for (int c = 0; c < C_; ++c) o[c] = z[size_t(c)]; break;
+      case kern::kActSoftmax: {
+        double m = *std::max_element(z.begin(), z.end()), s = 0;
+        for (auto& v : z) { v = std::exp(v - m); s += v; }
+        for (int c = 0; c < C_; ++c) o[c] = z[size_t(c)] / s;
+        break;
+      }
+      case kern::kActBinaryLogistic: {
+        double p = 1.0 / (1.0 + std::exp(-z[0]));
+        o[0] = 1.0 - p;
+        o[1] = p;
+        break;
+      }
+      case kern::kActOvr: {
+        double s = 0;
+        for (auto& v : z) { v = 1.0 / (1.0 + std::exp(-v)); s += v; }
+        for (int c = 0; c < C_; ++c) o[c] = z[size_t(c)] / s;
+        break;
+      }
+      default: for (int c = 0; c < C_; ++c) o[c] = 1.0 / (1.0 + std::exp(-z[size_t(c)]));
+    }
+  }
+}
+
+// ------------------------------------------------------------ tree ensemble
+static const int kPlanSizes[] = {8, 16, 32, 64, 128, 256, 512};
+
+TreeEnsembleModel::TreeEnsembleModel(TreeEnsembleSpec spec) : spec_(std::move(spec)) {
+  const int T = spec_.n_trees;
+  if (T <= 0) throw std::runtime_error("TreeEnsembleModel: no trees");
+  if (int(spec_.tree_group.size()) != T) spec_.tree_group.assign(size_t(T), 0);
+  for (int t = 1; t < T; ++t)
+    if (spec_.tree_group[size_t(t)] < spec_.tree_group[size_t(t - 1)])
+      throw std::runtime_error("TreeEnsembleModel: trees must be sorted by group");
+  if (int(spec_.base_margin.size()) != spec_.groups) spec_.base_margin.resize(size_t(spec_.groups), 0.f);
+  if (spec_.depth > 0) {
+    const size_t ni = (size_t(1) << spec_.depth) - 1;
+    if (spec_.thr.size() != ni * T || spec_.feat.size() != ni * T || spec_.leaves.size() != (ni + 1) * T)
+      throw std::runtime_error("TreeEnsembleModel: perfect-tree arrays have wrong size");
+  } else {
+    if (int(spec_.tree_root.size()) != T) throw std::runtime_error("TreeEnsembleModel: tree_root size mismatch");
+  }
+  for (int f : spec_.feat)
+    if ((f & 0x7fffffff) >= spec_.n_features) throw std::runtime_error("TreeEnsembleModel: feature index out of range");
+  for (const auto& n : spec_.nodes) {
+    if (n.left >= 0 && ((n.feat & 0x7fffffff) >= spec_.n_features || n.left >= int(spec_.nodes.size()) ||
+                        n.right < 0 || n.right >= int(spec_.nodes.size())))
+      throw std::runtime_error("TreeEnsembleModel: bad sparse node");
+  }
+  // Chunk plans: split each group's tree range into chunks of <= S trees.
+  for (int S : kPlanSizes) {
+    auto p = std::make_unique<Plan>();
+    p->chunk_trees = S;
+    int t = 0;
+    while (t < T) {
+      int g = spec_.tree_group[size_t(t)];
+      int e = t;
+      while (e < T && spec_.tree_group[size_t(e)] == g && e - t < S) ++e;
+      p->h_begin.push_back(t);
+      p->h_group.push_back(g);
+      t = e;
+    }
+    p->h_begin.push_back(T);
+    p->n_chunks = int(p->h_group.size());
+    max_chunks_ = std::max(max_chunks_, p->n_chunks);
+    plans_.push_back(std::move(p));
+  }
+}
+
+void TreeEnsembleModel::to_device(int device) {
+  device_ = device;
+  if (spec_.depth > 0) {
+    const size_t n = spec_.thr.size();
+    std::vector<kern::TreeNode> packed(n);
+    for (size_t i = 0; i < n; ++i) packed[i] = kern::TreeNode{spec_.thr[i], spec_.feat[i]};
+    d_nodes_.alloc(n * sizeof(kern::TreeNode), device);
+    d_nodes_.upload(packed.data(), n * sizeof(kern::TreeNode));
+    d_leaves_.alloc(spec_.leaves.size() * sizeof(float), device);
+    d_leaves_.upload(spec_.leaves.data(), spec_.leaves.size() * sizeof(float));
+  } else {
+    d_sparse_.alloc(spec_.nodes.size() * sizeof(kern::SparseNode), device);
+    d_sparse_.upload(spec_.nodes.data(), spec_.nodes.size() * sizeof(kern::SparseNode));
+    d_roots_.alloc(spec_.tree_root.size() * sizeof(int), device);
+    d_roots_.upload(spec_.tree_root.data(), spec_.tree_root.size() * sizeof(int));
+  }
+  d_base_.alloc(spec_.base_margin.size() * sizeof(float), device);
+  d_base_.upload(spec_.base_margin.data(), spec_.base_margin.size() * sizeof(float));
+  for (auto& p : plans_) {
+    p->begin.alloc(p->h_begin.size() * sizeof(int), device);
+    p->begin.upload(p->h_begin.data(), p->h_begin.size() * sizeof(int));
+    p->group.alloc(p->h_group.size() * sizeof(int), device);
+    p->group.upload(p->h_group.data(), p->h_group.size() * sizeof(int));
+  }
+}
+
+size_t TreeEnsembleModel::workspace_bytes(int max_rows, int) const {
+  return size_t(max_chunks_) * size_t(std::max(1, max_rows)) * sizeof(float);
+}
+
+void TreeEnsembleModel::plan_for(int rows, int* rows_per_block, int* plan_index) const {
+  int rb = 1;
+  while (rb < rows && rb < 64) rb <<= 1;
+  const int tpr = 256 / rb;
+  const int row_tiles = (rows + rb - 1) / rb;
+  // Aim for ~4 workgroups per CU (256 CUs) while giving each thread >= 1 tree.
+  const int want_chunks = std::max(1, 1024 / std::max(1, row_tiles));
+  const int chunk = std::max(tpr / 4, (spec_.n_trees + want_chunks - 1) / want_chunks);
+  int idx = int(plans_.size()) - 1;
+  for (int i = 0; i < int(plans_.size()); ++i)
+    if (plans_[size_t(i)]->chunk_trees >= chunk) { idx = i; break; }
+  *rows_per_block = rb;
+  *plan_index = idx;
+}
+
+void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) {
+  (void)cols;
+  int rb, pi;
+  plan_for(rows, &rb, &pi);
+  const Plan& p = *plans_[size_t(pi)];
+  float* partial = static_cast<float*>(ws);
+  if (spec_.depth > 0)
+    kern::tree_perfect_partial(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
+                               spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, s);
+  else
+    kern::tree_sparse_partial(X, rows, spec_.n_features, d_sparse_.as<kern::SparseNode>(), d_roots_.as<int>(),
+                              spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, s);
+  kern::tree_reduce(partial, rows, p.n_chunks, p.group.as<int>(), spec_.groups, d_base_.as<float>(), spec_.scale,
+                    spec_.transform, out, spec_.out_cols, s);
+}
+
+float TreeEnsembleModel::tree_value_cpu(int t, const float* x) const {
+  auto left = [&](float xv, float thr, int32_t f) {
+    if (xv != xv) return f < 0;
+    return spec_.cmp_le ? xv <= thr : xv < thr;
+  };
+  if (spec_.depth > 0) {
+    const int ni = (1 << spec_.depth) - 1;
+    int idx = 0;
+    for (int d = 0; d < spec_.depth; ++d) {
+      const size_t o = size_t(t) * ni + idx;
+      const int32_t f = spec_.feat[o];
+      idx = 2 * idx + (left(x[f & 0x7fffffff], spec_.thr[o], f) ? 1 : 2);
+    }
+    return spec_.leaves[size_t(t) * (ni + 1) + (idx - ni)];
+  }
+  int i = spec_.tree_root[size_t(t)];
+  while (spec_.nodes[size_t(i)].left >= 0) {
+    const auto& n = spec_.nodes[size_t(i)];
+    i = left(x[n.feat & 0x7fffffff], n.thr, n.feat) ? n.left : n.right;
+  }
+  return spec_.nodes[size_t(i)].thr;
+}
+
+void TreeEnsembleModel::run_cpu(const double* X, int rows, int cols, double* out) const {
+  std::vector<float> x(static_cast<size_t>(cols));
+  std::vector<double> m(static_cast<size_t>(spec_.groups));
+  for (int r = 0; r < rows; ++r) {
+    for (int f = 0; f < cols; ++f) x[size_t(f)] = float(X[size_t(r) * cols + f]);
+    std::fill(m.begin(), m.end(), 0.0);
+    for (int t = 0; t < spec_.n_trees; ++t) m[size_t(spec_.tree_group[size_t(t)])] += tree_value_cpu(t, x.data());
+    for (int g = 0; g < spec_.groups; ++g) m[size_t(g)] = m[size_t(g)] * spec_.scale + spec_.base_margin[size_t(g)];
+    double* o = out + size_t(r) * spec_.out_cols;
+    switch (spec_.transform) {
+      case kern::kTreeSigmoid: o[0] = 1.0 / (1.0 + std::exp(-m[0])); break;
+      case kern::kTreeBinaryProba: { double p = 1.0 / (1.0 + std::exp(-m[0])); o[0] = 1 - p; o[1] = p; break; }
+      case kern::kTreeSoftmax: {
+        double mx = *std::max_element(m.begin(), m.end()), s = 0;
+        for (auto& v : m) { v = std::exp(v - mx); s += v; }
+        for (int g = 0; g < spec_.groups; ++g) o[g] = m[size_t(g)] / s;
+        break;
+      }
+      case kern::kTreeIsolation: {
+        double raw = m[0] - spec_.base_margin[0];
+        o[0] = -std::exp2(-raw) - spec_.base_margin[0];
+        break;
+      }
+      default: for (int g = 0; g < spec_.groups; ++g) o[g] = m[size_t(g)];
+    }
+  }
+}
+
+// -------------------------------------------------------------- elementwise
+void MeanSigmoidModel::launch(const double* X, int rows, int cols, double* out, void*, hipStream_t s) {
+  kern::mean_sigmoid_rows_f64(X, rows, cols, thr_, out, s);
+}
+
+void MeanSigmoidModel::run_cpu(const double* X, int rows, int cols, double* out) const {
+  for (int r = 0; r < rows; ++r) {
+    double s = 0;
+    for (int f = 0; f < cols; ++f) s += X[size_t(r) * cols + f];
+    out[r] = 1.0 / (1.0 + std::exp(-(s / cols - thr_)));
+  }
+}
+
+}  // namespace sca::gpu

@@ -1,0 +1,122 @@
+// Row-wise models served by the GPU micro-batcher.
+//
+// Each model owns its parameters in HBM (uploaded once, resident for the
+// life of the deployment) and exposes an async launch over a micro-batch of
+// request rows plus a CPU reference path (used for `device: -1` placement and
+// as the test oracle on machines without a GPU).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../kernels/kernels.h"
+#include "hip_util.h"
+
+namespace sca::gpu {
+
+class RowModel {
+ public:
+  virtual ~RowModel() = default;
+  virtual std::string name() const = 0;
+  virtual int in_cols() const = 0;  // 0 = any width
+  virtual int out_cols(int in_cols) const = 0;
+  virtual std::vector<std::string> class_names() const { return names_; }
+  void set_class_names(std::vector<std::string> n) { names_ = std::move(n); }
+  virtual void to_device(int device) = 0;
+  virtual size_t workspace_bytes(int max_rows, int cols) const { (void)max_rows; (void)cols; return 0; }
+  virtual void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) = 0;
+  virtual void run_cpu(const double* X, int rows, int cols, double* out) const = 0;
+
+ protected:
+  std::vector<std::string> names_;
+};
+using RowModelPtr = std::shared_ptr<RowModel>;
+
+// ---------------------------------------------------------------- linear
+class LinearModel : public RowModel {
+ public:
+  LinearModel(std::vector<double> W, std::vector<double> b, int C, int K, int act);
+  std::string name() const override { return "linear"; }
+  int in_cols() const override { return K_; }
+  int out_cols(int) const override { return act_ == kern::kActBinaryLogistic ? 2 : C_; }
+  void to_device(int device) override;
+  void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  void run_cpu(const double* X, int rows, int cols, double* out) const override;
+
+ private:
+  std::vector<double> W_, b_;
+  int C_, K_, act_;
+  DeviceBuffer dW_, db_;
+};
+
+// ---------------------------------------------------------- tree ensemble
+struct TreeEnsembleSpec {
+  // Common
+  int n_trees = 0;
+  int n_features = 0;
+  int groups = 1;          // output margins (classes for multi:softprob)
+  int out_cols = 1;
+  int transform = 0;       // kern::TreeTransform
+  int cmp_le = 0;          // 1: x <= thr (sklearn), 0: x < thr (xgboost)
+  float scale = 1.f;       // margin multiplier (1/n_trees for averaging)
+  std::vector<float> base_margin;  // [groups]
+  std::vector<int> tree_group;     // [n_trees], must be non-decreasing
+  // Perfect layout (depth > 0)
+  int depth = 0;
+  std::vector<float> thr;          // [n_trees * (2^D - 1)]
+  std::vector<int32_t> feat;       // same, bit31 = default-left
+  std::vector<float> leaves;       // [n_trees * 2^D]
+  // Sparse layout (depth == 0)
+  std::vector<kern::SparseNode> nodes;
+  std::vector<int> tree_root;      // [n_trees]
+};
+
+class TreeEnsembleModel : public RowModel {
+ public:
+  explicit TreeEnsembleModel(TreeEnsembleSpec spec);
+  std::string name() const override { return spec_.depth > 0 ? "tree_perfect" : "tree_sparse"; }
+  int in_cols() const override { return spec_.n_features; }
+  int out_cols(int) const override { return spec_.out_cols; }
+  void to_device(int device) override;
+  size_t workspace_bytes(int max_rows, int cols) const override;
+  void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  void run_cpu(const double* X, int rows, int cols, double* out) const override;
+  const TreeEnsembleSpec& spec() const { return spec_; }
+  // Launch geometry chosen for a batch (exposed for tests/benchmarks).
+  void plan_for(int rows, int* rows_per_block, int* plan_index) const;
+
+ private:
+  struct Plan {
+    int chunk_trees;
+    int n_chunks;
+    DeviceBuffer begin, group;
+    std::vector<int> h_begin, h_group;
+  };
+  float tree_value_cpu(int t, const float* x) const;
+  TreeEnsembleSpec spec_;
+  std::vector<std::unique_ptr<Plan>> plans_;
+  DeviceBuffer d_nodes_, d_leaves_, d_sparse_, d_roots_, d_base_;
+  int max_chunks_ = 1;
+  int device_ = -1;
+};
+
+// ------------------------------------------------------------- elementwise
+// sigmoid(mean(row) - threshold): examples/models/mean_classifier.
+class MeanSigmoidModel : public RowModel {
+ public:
+  explicit MeanSigmoidModel(double threshold) : thr_(threshold) {}
+  std::string name() const override { return "mean_sigmoid"; }
+  int in_cols() const override { return 0; }
+  int out_cols(int) const override { return 1; }
+  void to_device(int) override {}
+  void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  void run_cpu(const double* X, int rows, int cols, double* out) const override;
+
+ private:
+  double thr_;
+};
+
+}  // namespace sca::gpu

@@ -1,0 +1,196 @@
+// Combiner / transformer kernels.
+//
+// Reference CPU code: engine/.../AverageCombinerUnit.java:35-79 (element-wise
+// mean), examples/transformers/mean_transformer/MeanTransformer.py:8-12
+// (global min-max), examples/models/mean_classifier/MeanClassifier.py:19-27
+// (sigmoid(mean(row) - thr)), examples/models/openvino_imagenet_ensemble/
+// .../ImageNetCombiner.py:7-10 (average + argmax).
+//
+// These are HBM-streaming ops: 16-byte (2 x fp64) vector loads per lane,
+// grid-stride, wave-shuffle reductions (64 lanes) before one LDS pass.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "kernels.h"
+
+namespace sca::kern {
+namespace {
+
+constexpr int kBlock = 256;
+
+__global__ __launch_bounds__(kBlock) void mean_kernel(const double* const* __restrict__ inputs, int n_in, int64_t n,
+                                                      double* __restrict__ out) {
+  const double inv = 1.0 / double(n_in);
+  const int64_t n2 = n / 2;
+  for (int64_t i = blockIdx.x * int64_t(kBlock) + threadIdx.x; i < n2; i += int64_t(gridDim.x) * kBlock) {
+    double2 acc = {0.0, 0.0};
+    for (int j = 0; j < n_in; ++j) {
+      const double2 v = reinterpret_cast<const double2*>(inputs[j])[i];
+      acc.x += v.x;
+      acc.y += v.y;
+    }
+    acc.x *= inv;
+    acc.y *= inv;
+    reinterpret_cast<double2*>(out)[i] = acc;
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    double acc = 0.0;
+    for (int j = 0; j < n_in; ++j) acc += inputs[j][n - 1];
+    out[n - 1] = acc * inv;
+  }
+}
+
+__device__ inline double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ inline double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// One wave per row: max, sum(exp) and normalise.
+__global__ __launch_bounds__(kBlock) void softmax_rows(const double* __restrict__ in, int rows, int C,
+                                                       double* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (kBlock / 64) + wave;
+  if (r >= rows) return;
+  const double* x = in + size_t(r) * C;
+  double m = -DBL_MAX;
+  for (int c = lane; c < C; c += 64) m = fmax(m, x[c]);
+  m = wave_max(m);
+  double s = 0.0;
+  for (int c = lane; c < C; c += 64) s += exp(x[c] - m);
+  s = wave_sum(s);
+  const double inv = 1.0 / s;
+  for (int c = lane; c < C; c += 64) out[size_t(r) * C + c] = exp(x[c] - m) * inv;
+}
+
+__global__ __launch_bounds__(kBlock) void argmax_rows(const double* __restrict__ in, int rows, int C,
+                                                      int32_t* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (kBlock / 64) + wave;
+  if (r >= rows) return;
+  const double* x = in + size_t(r) * C;
+  double best = -DBL_MAX;
+  int idx = 0x7fffffff;
+  for (int c = lane; c < C; c += 64)
+    if (x[c] > best) { best = x[c]; idx = c; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(idx, o, 64);
+    if (ob > best || (ob == best && oi < idx)) { best = ob; idx = oi; }
+  }
+  if (lane == 0) out[r] = idx;
+}
+
+// Pass 1: per-block min/max -> atomics on scratch[0..1] (initialised by host
+// launcher via a first tiny kernel). Pass 2: affine rescale.
+__global__ void minmax_init(double* scratch) {
+  scratch[0] = DBL_MAX;
+  scratch[1] = -DBL_MAX;
+}
+
+__device__ inline void atomic_min_f64(double* addr, double v) {
+  unsigned long long* a = reinterpret_cast<unsigned long long*>(addr);
+  unsigned long long old = *a, assumed;
+  do {
+    assumed = old;
+    if (__longlong_as_double(assumed) <= v) return;
+    old = atomicCAS(a, assumed, __double_as_longlong(v));
+  } while (assumed != old);
+}
+__device__ inline void atomic_max_f64(double* addr, double v) {
+  unsigned long long* a = reinterpret_cast<unsigned long long*>(addr);
+  unsigned long long old = *a, assumed;
+  do {
+    assumed = old;
+    if (__longlong_as_double(assumed) >= v) return;
+    old = atomicCAS(a, assumed, __double_as_longlong(v));
+  } while (assumed != old);
+}
+
+__global__ __launch_bounds__(kBlock) void minmax_reduce(const double* __restrict__ in, int64_t n, double* scratch) {
+  __shared__ double smin[kBlock / 64], smax[kBlock / 64];
+  double lo = DBL_MAX, hi = -DBL_MAX;
+  for (int64_t i = blockIdx.x * int64_t(kBlock) + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    const double v = in[i];
+    lo = fmin(lo, v);
+    hi = fmax(hi, v);
+  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { smin[wave] = lo; smax[wave] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) { lo = fmin(lo, smin[w]); hi = fmax(hi, smax[w]); }
+    atomic_min_f64(&scratch[0], lo);
+    atomic_max_f64(&scratch[1], hi);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void minmax_apply(const double* __restrict__ in, int64_t n,
+                                                       const double* __restrict__ scratch, double* __restrict__ out) {
+  const double lo = scratch[0], range = scratch[1] - scratch[0];
+  for (int64_t i = blockIdx.x * int64_t(kBlock) + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+    out[i] = (in[i] - lo) / range;
+}
+
+__global__ __launch_bounds__(kBlock) void mean_sigmoid(const double* __restrict__ in, int rows, int F,
+                                                       double threshold, double* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (kBlock / 64) + wave;
+  if (r >= rows) return;
+  double s = 0.0;
+  for (int f = lane; f < F; f += 64) s += in[size_t(r) * F + f];
+  s = wave_sum(s);
+  if (lane == 0) out[r] = 1.0 / (1.0 + exp(-(s / double(F) - threshold)));
+}
+
+int grid_for(int64_t n) {
+  int64_t g = (n + kBlock - 1) / kBlock;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return int(g);
+}
+
+}  // namespace
+
+void combine_mean_f64(const double* const* inputs, int n_inputs, int64_t n, double* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(mean_kernel, dim3(grid_for(n / 2 + 1)), dim3(kBlock), 0, s, inputs, n_inputs, n, out);
+}
+
+void softmax_rows_f64(const double* in, int rows, int C, double* out, hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(softmax_rows, dim3((rows + 3) / 4), dim3(kBlock), 0, s, in, rows, C, out);
+}
+
+void argmax_rows_f64(const double* in, int rows, int C, int32_t* out, hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(argmax_rows, dim3((rows + 3) / 4), dim3(kBlock), 0, s, in, rows, C, out);
+}
+
+void minmax_normalize_f64(const double* in, int64_t n, double* out, double* scratch2, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(minmax_init, dim3(1), dim3(1), 0, s, scratch2);
+  hipLaunchKernelGGL(minmax_reduce, dim3(grid_for(n)), dim3(kBlock), 0, s, in, n, scratch2);
+  hipLaunchKernelGGL(minmax_apply, dim3(grid_for(n)), dim3(kBlock), 0, s, in, n, scratch2, out);
+}
+
+void mean_sigmoid_rows_f64(const double* in, int rows, int F, double threshold, double* out, hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(mean_sigmoid, dim3((rows + 3) / 4), dim3(kBlock), 0, s, in, rows, F, threshold, out);
+}
+
+}  // namespace sca::kern

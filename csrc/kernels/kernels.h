@@ -1,0 +1,91 @@
+// Host-side launch API for the engine's hand-written CDNA4 (gfx950) kernels.
+//
+// Every launcher is asynchronous on `stream`, allocates nothing, and never
+// synchronises (so a caller may capture it into a hipGraph).  Pointers may be
+// device memory or host memory mapped into the device address space
+// (zero-copy pinned buffers used by the micro-batcher for tiny payloads).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace sca::kern {
+
+// ---------------------------------------------------------------- linear
+// out[r, :] = act(X[r, :] . W^T + b), W is [C, K] row-major.
+// Reference: servers/sklearnserver/.../SKLearnServer.py:32-42 (predict_proba of
+// LogisticRegression / LinearRegression); SURVEY K3.
+enum LinearAct : int {
+  kActIdentity = 0,      // regression: out [R, C]
+  kActSoftmax = 1,       // multinomial logistic regression: out [R, C]
+  kActBinaryLogistic = 2,// binary LR (C == 1): out [R, 2] = [1-p, p]
+  kActOvr = 3,           // one-vs-rest LR: sigmoid per class, row-normalised
+  kActSigmoid = 4,       // independent sigmoid per column
+};
+// fp64 I/O, fp64 accumulate (parity with sklearn to ~1e-15).
+void linear_f64(const double* X, int rows, int K, const double* W, const double* b, int C, int act,
+                double* out, hipStream_t stream);
+
+// ------------------------------------------------------------ tree ensemble
+// Perfect (complete) binary trees of fixed depth D, breadth-first.  Node i of
+// tree t: nodes[t * (2^D - 1) + i] = {threshold, feature | (default_left << 31)}.
+// Decision (XGBoost semantics): go left iff x[f] < thr, NaN -> default dir.
+struct TreeNode {
+  float thr;
+  int32_t feat;  // bit 31: default-left for missing values
+};
+// Partial sums per tree chunk: partial[chunk, r] = sum_{t in chunk} leaf.
+// chunk_begin has n_chunks + 1 entries (tree index ranges).
+// X is the fp64 request matrix [rows, F] (converted to fp32 on load, as
+// XGBoost's DMatrix does).  cmp_le: 1 = sklearn `x <= thr`, 0 = XGBoost `x < thr`.
+// rows_per_block (1..64, power of two) trades row- vs tree-parallelism.
+void tree_perfect_partial(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves,
+                          int depth, int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block,
+                          float* partial, hipStream_t stream);
+// General trees (arbitrary depth): node {thr, feat|flags, left, right}.
+struct SparseNode {
+  float thr;
+  int32_t feat;
+  int32_t left;
+  int32_t right;
+};
+// feat bit 31 = default-left; left < 0 marks a leaf (value in thr).
+void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root,
+                         int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
+                         hipStream_t stream);
+// Reduce chunk partials to per-group margins and apply the objective transform.
+// chunk_group[c] = output column of chunk c; out [rows, out_cols] fp64.
+enum TreeTransform : int {
+  kTreeIdentity = 0,      // reg:squarederror
+  kTreeSigmoid = 1,       // binary:logistic -> [p]
+  kTreeSoftmax = 2,       // multi:softprob
+  kTreeBinaryProba = 3,   // binary:logistic as predict_proba -> [1-p, p]
+  kTreeMean = 4,          // random forest regression average
+  kTreeIsolation = 5,     // isolation forest: 2^(-mean_path / c(n)) score
+};
+void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,
+                 const float* base_margin, float scale, int transform, double* out, int out_cols,
+                 hipStream_t stream);
+
+// ------------------------------------------------------------ combiners
+// out = mean over N inputs (each [n] fp64). inputs: device array of pointers.
+void combine_mean_f64(const double* const* inputs, int n_inputs, int64_t n, double* out, hipStream_t stream);
+// Row softmax / argmax over [rows, C].
+void softmax_rows_f64(const double* in, int rows, int C, double* out, hipStream_t stream);
+void argmax_rows_f64(const double* in, int rows, int C, int32_t* out, hipStream_t stream);
+// Global min-max normalisation (examples/transformers/mean_transformer).
+void minmax_normalize_f64(const double* in, int64_t n, double* out, double* scratch2, hipStream_t stream);
+// sigmoid(mean(row) - threshold)  (examples/models/mean_classifier).
+void mean_sigmoid_rows_f64(const double* in, int rows, int F, double threshold, double* out, hipStream_t stream);
+
+// ------------------------------------------------------------ bandits
+// Epsilon-greedy route for `n` requests given per-branch value estimates.
+// (components/routers/epsilon-greedy/EpsilonGreedy.py:87-106)
+void eg_route(const float* values, int n_branches, float epsilon, uint64_t seed, uint64_t offset, int n,
+              int32_t* branch_out, hipStream_t stream);
+// Thompson sampling: sample Beta(a_i, b_i), argmax (ThompsonSampling.py:78-91).
+void ts_route(const float* alpha, const float* beta, int n_branches, uint64_t seed, uint64_t offset, int n,
+              int32_t* branch_out, hipStream_t stream);
+
+}  // namespace sca::kern

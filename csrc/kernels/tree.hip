@@ -1,0 +1,263 @@
+// Tree-ensemble inference (reference
+// servers/xgboostserver/xgboostserver/XGBoostServer.py:10-26 — xgboost
+// Booster.predict on the CPU — and sklearn IsolationForest / RandomForest).
+//
+// CDNA4 mapping.  A 256-thread workgroup owns a tile of RB request rows and a
+// contiguous chunk of trees (grid = row tiles x tree chunks, so even a batch of
+// one row fills the chip with tree-parallel work):
+//   thread i -> row (i % RB), tree slot (i / RB), stride 256 / RB
+// The RB x F feature tile is staged once in LDS as fp32 (XGBoost's DMatrix
+// precision), so the per-level `x[feature]` gather is an LDS read; node records
+// are 8 bytes ({thr, feat|default_left}) laid out breadth-first per tree so a
+// perfect tree of depth D needs no child pointers (child = 2i + 1 + right) and
+// the whole 1000 x depth-8 model (2 MiB nodes + 1 MiB leaves) stays resident in
+// each XCD's 4 MiB L2 across batches.  Per-row partial sums over the thread's
+// trees are reduced through LDS and written to a [chunk, row] slab that
+// tree_reduce folds (deterministic, no float atomics).
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace sca::kern {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxLdsFloats = 12288;  // 48 KiB feature tile
+
+__device__ __forceinline__ bool go_left(float x, float thr, int32_t feat, int cmp_le) {
+  if (x != x) return feat < 0;  // missing value -> default direction (bit 31)
+  return cmp_le ? (x <= thr) : (x < thr);
+}
+
+template <int D>
+__device__ __forceinline__ int descend_fixed(const TreeNode* __restrict__ tn, const float* __restrict__ xs,
+                                             int cmp_le) {
+  int idx = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const TreeNode nd = tn[idx];
+    const float x = xs[nd.feat & 0x7fffffff];
+    idx = 2 * idx + (go_left(x, nd.thr, nd.feat, cmp_le) ? 1 : 2);
+  }
+  return idx;
+}
+
+__device__ __forceinline__ int descend_any(const TreeNode* __restrict__ tn, const float* __restrict__ xs, int D,
+                                           int cmp_le) {
+  int idx = 0;
+  for (int d = 0; d < D; ++d) {
+    const TreeNode nd = tn[idx];
+    const float x = xs[nd.feat & 0x7fffffff];
+    idx = 2 * idx + (go_left(x, nd.thr, nd.feat, cmp_le) ? 1 : 2);
+  }
+  return idx;
+}
+
+// Stage the RB x F feature tile (fp64 -> fp32) into LDS; rows past `rows`
+// are zero-filled so every thread can traverse unconditionally.
+__device__ __forceinline__ void stage_tile(float* tile, const double* __restrict__ X, int row0, int rows, int RB,
+                                           int F) {
+  const int n = RB * F;
+  for (int i = threadIdx.x; i < n; i += kBlock) {
+    const int r = row0 + i / F;
+    tile[i] = r < rows ? float(X[size_t(row0) * F + i]) : 0.f;
+  }
+}
+
+// Reduce per-thread accumulators of the same row and write the slab row.
+__device__ __forceinline__ void reduce_write(float* red, float acc, int RB, int row0, int rows, int chunk,
+                                             float* __restrict__ partial) {
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  const int tpr = kBlock / RB;
+  if (threadIdx.x < RB) {
+    float s = 0.f;
+    for (int j = 0; j < tpr; ++j) s += red[j * RB + threadIdx.x];
+    const int r = row0 + threadIdx.x;
+    if (r < rows) partial[size_t(chunk) * rows + r] = s;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restrict__ X, int rows, int F,
+                                                          const TreeNode* __restrict__ nodes,
+                                                          const float* __restrict__ leaves, int depth, int cmp_le,
+                                                          const int* __restrict__ chunk_begin, int RB,
+                                                          int stage_lds, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* red = lds;            // [kBlock]
+  float* tile = lds + kBlock;  // [RB * F] when staged
+  const int row0 = blockIdx.x * RB;
+  const int chunk = blockIdx.y;
+  const int r_local = threadIdx.x & (RB - 1);
+  const int slot = threadIdx.x / RB;
+  const int tpr = kBlock / RB;
+  const float* xs;
+  float xreg_dummy = 0.f;
+  (void)xreg_dummy;
+  if (stage_lds) {
+    stage_tile(tile, X, row0, rows, RB, F);
+    __syncthreads();
+    xs = tile + r_local * F;
+  } else {
+    xs = nullptr;
+  }
+  const int n_internal = (1 << depth) - 1;
+  const int t0 = chunk_begin[chunk], t1 = chunk_begin[chunk + 1];
+  float acc = 0.f;
+  const bool row_ok = row0 + r_local < rows;
+  if (stage_lds || row_ok) {
+    for (int t = t0 + slot; t < t1; t += tpr) {
+      const TreeNode* tn = nodes + size_t(t) * n_internal;
+      int idx;
+      if (stage_lds) {
+        idx = D > 0 ? descend_fixed<D>(tn, xs, cmp_le) : descend_any(tn, xs, depth, cmp_le);
+      } else {
+        // Wide feature vectors: read fp64 features straight from global.
+        const double* xg = X + size_t(row0 + r_local) * F;
+        idx = 0;
+        for (int d = 0; d < depth; ++d) {
+          const TreeNode nd = tn[idx];
+          const float x = float(xg[nd.feat & 0x7fffffff]);
+          idx = 2 * idx + (go_left(x, nd.thr, nd.feat, cmp_le) ? 1 : 2);
+        }
+      }
+      acc += leaves[size_t(t) * (n_internal + 1) + (idx - n_internal)];
+    }
+  }
+  if (!row_ok) acc = 0.f;
+  if (stage_lds) __syncthreads();  // tile no longer needed; `red` is disjoint anyway
+  reduce_write(red, acc, RB, row0, rows, chunk, partial);
+}
+
+__global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restrict__ X, int rows, int F,
+                                                         const SparseNode* __restrict__ nodes,
+                                                         const int* __restrict__ tree_root, int cmp_le,
+                                                         const int* __restrict__ chunk_begin, int RB, int stage_lds,
+                                                         float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* red = lds;
+  float* tile = lds + kBlock;
+  const int row0 = blockIdx.x * RB;
+  const int chunk = blockIdx.y;
+  const int r_local = threadIdx.x & (RB - 1);
+  const int slot = threadIdx.x / RB;
+  const int tpr = kBlock / RB;
+  if (stage_lds) {
+    stage_tile(tile, X, row0, rows, RB, F);
+    __syncthreads();
+  }
+  const bool row_ok = row0 + r_local < rows;
+  const int t0 = chunk_begin[chunk], t1 = chunk_begin[chunk + 1];
+  float acc = 0.f;
+  if (row_ok) {
+    const float* xs = tile + r_local * F;
+    const double* xg = X + size_t(row0 + r_local) * F;
+    for (int t = t0 + slot; t < t1; t += tpr) {
+      int i = tree_root[t];
+      SparseNode nd = nodes[i];
+      int guard = 0;
+      while (nd.left >= 0 && guard < 4096) {
+        const int f = nd.feat & 0x7fffffff;
+        const float x = stage_lds ? xs[f] : float(xg[f]);
+        i = go_left(x, nd.thr, nd.feat, cmp_le) ? nd.left : nd.right;
+        nd = nodes[i];
+        ++guard;
+      }
+      acc += nd.thr;
+    }
+  }
+  if (stage_lds) __syncthreads();
+  reduce_write(red, acc, RB, row0, rows, chunk, partial);
+}
+
+constexpr int kMaxGroups = 64;
+
+__global__ __launch_bounds__(kBlock) void reduce_transform(const float* __restrict__ partial, int rows, int n_chunks,
+                                                           const int* __restrict__ chunk_group, int groups,
+                                                           const float* __restrict__ base_margin, float scale,
+                                                           int transform, double* __restrict__ out, int out_cols) {
+  extern __shared__ __attribute__((aligned(16))) double m_lds[];
+  const int r = blockIdx.x * kBlock + threadIdx.x;
+  if (r >= rows) return;
+  double* m = m_lds + size_t(threadIdx.x) * groups;
+  for (int g = 0; g < groups; ++g) m[g] = 0.0;
+  for (int c = 0; c < n_chunks; ++c) m[chunk_group[c]] += double(partial[size_t(c) * rows + r]);
+  for (int g = 0; g < groups; ++g) m[g] = m[g] * double(scale) + (base_margin ? double(base_margin[g]) : 0.0);
+  double* o = out + size_t(r) * out_cols;
+  switch (transform) {
+    case kTreeSigmoid: o[0] = 1.0 / (1.0 + exp(-m[0])); break;
+    case kTreeBinaryProba: {
+      const double p = 1.0 / (1.0 + exp(-m[0]));
+      o[0] = 1.0 - p;
+      o[1] = p;
+      break;
+    }
+    case kTreeSoftmax: {
+      double mx = m[0];
+      for (int g = 1; g < groups; ++g) mx = fmax(mx, m[g]);
+      double s = 0.0;
+      for (int g = 0; g < groups; ++g) { m[g] = exp(m[g] - mx); s += m[g]; }
+      for (int g = 0; g < groups; ++g) o[g] = m[g] / s;
+      break;
+    }
+    case kTreeIsolation: {
+      // m = mean path length / c(max_samples) (scale folds both); base = offset
+      const double raw = m[0] - (base_margin ? double(base_margin[0]) : 0.0);
+      o[0] = -exp2(-raw) - (base_margin ? double(base_margin[0]) : 0.0);
+      break;
+    }
+    default:
+      for (int g = 0; g < groups; ++g) o[g] = m[g];
+  }
+}
+
+int lds_bytes_for(int RB, int F, bool* stage) {
+  *stage = RB * F <= kMaxLdsFloats;
+  return int((kBlock + (*stage ? RB * F : 0)) * sizeof(float));
+}
+
+}  // namespace
+
+void tree_perfect_partial(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                          int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial,
+                          hipStream_t s) {
+  if (rows <= 0 || n_chunks <= 0) return;
+  bool stage;
+  const int lds = lds_bytes_for(RB, F, &stage);
+  dim3 grid((rows + RB - 1) / RB, n_chunks);
+#define SCA_TREE_CASE(DD)                                                                                        \
+  case DD:                                                                                                      \
+    hipLaunchKernelGGL(perfect_partial<DD>, grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, depth, cmp_le, \
+                       chunk_begin, RB, int(stage), partial);                                                   \
+    break;
+  switch (depth) {
+    SCA_TREE_CASE(1) SCA_TREE_CASE(2) SCA_TREE_CASE(3) SCA_TREE_CASE(4) SCA_TREE_CASE(5) SCA_TREE_CASE(6)
+    SCA_TREE_CASE(7) SCA_TREE_CASE(8) SCA_TREE_CASE(9) SCA_TREE_CASE(10) SCA_TREE_CASE(11) SCA_TREE_CASE(12)
+    default:
+      hipLaunchKernelGGL(perfect_partial<0>, grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, depth, cmp_le,
+                         chunk_begin, RB, int(stage), partial);
+  }
+#undef SCA_TREE_CASE
+}
+
+void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
+                         const int* chunk_begin, int n_chunks, int RB, float* partial, hipStream_t s) {
+  if (rows <= 0 || n_chunks <= 0) return;
+  bool stage;
+  const int lds = lds_bytes_for(RB, F, &stage);
+  dim3 grid((rows + RB - 1) / RB, n_chunks);
+  hipLaunchKernelGGL(sparse_partial, grid, dim3(kBlock), lds, s, X, rows, F, nodes, tree_root, cmp_le, chunk_begin,
+                     RB, int(stage), partial);
+}
+
+void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,
+                 const float* base_margin, float scale, int transform, double* out, int out_cols, hipStream_t s) {
+  if (rows <= 0) return;
+  if (groups > kMaxGroups) groups = kMaxGroups;
+  const size_t lds = size_t(kBlock) * groups * sizeof(double);
+  hipLaunchKernelGGL(reduce_transform, dim3((rows + kBlock - 1) / kBlock), dim3(kBlock), lds, s, partial, rows,
+                     n_chunks, chunk_group, groups, base_margin, scale, transform, out, out_cols);
+}
+
+}  // namespace sca::kern
