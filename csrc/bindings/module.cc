@@ -149,6 +149,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("in_cols", &gpu::RowModel::in_cols)
       .def("out_cols", &gpu::RowModel::out_cols)
       .def("set_class_names", &gpu::RowModel::set_class_names)
+      .def("class_names", &gpu::RowModel::class_names)
+      .def_property("flat_output", &gpu::RowModel::flat_output, &gpu::RowModel::set_flat_output)
       .def("run_cpu", [](const gpu::RowModel& mdl, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
         if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
         const int rows = int(X.shape(0)), cols = int(X.shape(1));

@@ -84,13 +84,18 @@ void BatchedUnit::ensure_capacity(Slot& s, int rows, int cols) {
 MsgPtr BatchedUnit::make_response(const Item& it, const double* out, int out_cols) const {
   auto m = std::make_shared<SeldonMessage>();
   m->payload = Payload::Data;
-  std::vector<std::string> names = model_->class_names();
-  if (names.empty())
-    for (int c = 0; c < out_cols; ++c) names.push_back("t:" + std::to_string(c));
+  const bool flat = model_->flat_output() && out_cols == 1;
+  std::vector<std::string> names;
+  if (!flat) {  // client_class_names: explicit names, else t:0..t:C-1
+    names = model_->class_names();
+    if (names.empty())
+      for (int c = 0; c < out_cols; ++c) names.push_back("t:" + std::to_string(c));
+  }
   m->data.names = std::move(names);
   DataKind kind = it.req->payload == Payload::Data ? it.req->data.kind : DataKind::Tensor;
   std::vector<double> vals(out, out + size_t(it.rows) * out_cols);
-  m->data.set_dense(kind, {int64_t(it.rows), int64_t(out_cols)}, std::move(vals));
+  std::vector<int64_t> shape = flat ? std::vector<int64_t>{int64_t(it.rows)} : std::vector<int64_t>{int64_t(it.rows), int64_t(out_cols)};
+  m->data.set_dense(kind, std::move(shape), std::move(vals));
   m->has_meta = true;
   m->meta.puid = it.req->meta.puid;
   return m;

@@ -25,6 +25,10 @@ class RowModel {
   virtual int out_cols(int in_cols) const = 0;
   virtual std::vector<std::string> class_names() const { return names_; }
   void set_class_names(std::vector<std::string> n) { names_ = std::move(n); }
+  // Single-output models whose reference server returns a 1-D array
+  // (e.g. xgboost Booster.predict): response shape [rows], no class names.
+  bool flat_output() const { return flat_; }
+  void set_flat_output(bool f) { flat_ = f; }
   virtual void to_device(int device) = 0;
   virtual size_t workspace_bytes(int max_rows, int cols) const { (void)max_rows; (void)cols; return 0; }
   virtual void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) = 0;
@@ -32,6 +36,7 @@ class RowModel {
 
  protected:
   std::vector<std::string> names_;
+  bool flat_ = false;
 };
 using RowModelPtr = std::shared_ptr<RowModel>;
 

@@ -1,0 +1,19 @@
+"""Engine-native components: routers and outlier detectors.
+
+``NATIVE_IMPLEMENTATIONS`` maps a graph node's ``implementation`` string to a
+component factory (node parameters become constructor kwargs), so specs can
+use them without a container image.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict
+
+NATIVE_IMPLEMENTATIONS: Dict[str, Callable] = {}
+
+
+def register(name: str):
+    def deco(cls):
+        NATIVE_IMPLEMENTATIONS[name] = cls
+        return cls
+
+    return deco

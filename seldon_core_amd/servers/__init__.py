@@ -1,0 +1,172 @@
+"""Prepackaged model servers (reference servers/sklearnserver, servers/
+xgboostserver, servers/mlflowserver, integrations/tfserving; operator wiring
+operator/controllers/seldondeployment_prepackaged_servers.go:30-303).
+
+Each server is a regular component (``predict``) *and* exposes
+``row_model()``: when the model family has a native kernel the deployment binds
+the GPU micro-batched unit instead of calling ``predict`` per request.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import pickle
+from typing import Any, Dict, Optional
+
+import numpy as np
+
+from ..utils.storage import Storage
+
+logger = logging.getLogger(__name__)
+
+JOBLIB_FILE = "model.joblib"
+XGB_JSON_FILES = ("model.json", "model.bst.json")
+
+
+class SKLearnServer:
+    """sklearn estimator from ``<modelUri>/model.joblib``; method predict_proba|predict."""
+
+    def __init__(self, model_uri: str = "", method: str = "predict_proba", model: Any = None):
+        self.model_uri = model_uri
+        self.method = method
+        self._model = model
+        self.ready = model is not None
+
+    def load(self) -> None:
+        if self._model is None:
+            import joblib
+
+            path = os.path.join(Storage.download(self.model_uri), JOBLIB_FILE)
+            self._model = joblib.load(path)
+        self.ready = True
+
+    def predict(self, X, names, meta=None):
+        if not self.ready:
+            self.load()
+        fn = self._model.predict_proba if self.method == "predict_proba" else self._model.predict
+        return fn(X)
+
+    def row_model(self):
+        if not self.ready:
+            self.load()
+        from ..models import to_row_model
+
+        return to_row_model(self._model, self.method)
+
+
+class XGBoostServer:
+    """XGBoost booster from ``<modelUri>/model.json`` (XGBoost JSON schema).
+
+    The binary ``model.bst`` format needs the xgboost library (not available
+    on this platform); save models with ``Booster.save_model('model.json')``.
+    """
+
+    def __init__(self, model_uri: str = "", ensemble=None):
+        self.model_uri = model_uri
+        self._ens = ensemble
+        self.ready = ensemble is not None
+
+    def load(self) -> None:
+        if self._ens is None:
+            from ..models import from_xgboost_json
+
+            root = Storage.download(self.model_uri)
+            path = root
+            if os.path.isdir(root):
+                cands = [os.path.join(root, f) for f in XGB_JSON_FILES if os.path.exists(os.path.join(root, f))]
+                if not cands:
+                    raise FileNotFoundError(f"no XGBoost JSON model ({', '.join(XGB_JSON_FILES)}) in {root}")
+                path = cands[0]
+            self._ens = from_xgboost_json(path)
+        self.ready = True
+
+    def predict(self, X, names, meta=None):
+        if not self.ready:
+            self.load()
+        return self._ens.predict(np.asarray(X, dtype=np.float64))
+
+    def row_model(self):
+        if not self.ready:
+            self.load()
+        from ..models import to_row_model
+
+        return to_row_model(self._ens)
+
+
+class MLFlowServer:
+    """MLflow-style model directory.  Without the mlflow package the supported
+    flavours are TorchScript (``model.pt``, executed on the GPU by PyTorch-ROCm)
+    and scikit-learn (``model.pkl``/``model.joblib``)."""
+
+    def __init__(self, model_uri: str = "", device: Optional[str] = None):
+        self.model_uri = model_uri
+        self.device = device
+        self.ready = False
+        self._fn = None
+
+    def load(self) -> None:
+        root = Storage.download(self.model_uri)
+        pt = os.path.join(root, "model.pt")
+        if os.path.exists(pt):
+            import torch
+
+            dev = self.device or ("cuda" if torch.cuda.is_available() else "cpu")
+            mod = torch.jit.load(pt, map_location=dev).eval()
+
+            def fn(X):
+                with torch.no_grad():
+                    t = torch.as_tensor(np.asarray(X, dtype=np.float32), device=dev)
+                    return mod(t).float().cpu().numpy()
+
+            self._fn = fn
+        else:
+            import joblib
+
+            for f in ("model.joblib", "model.pkl"):
+                p = os.path.join(root, f)
+                if os.path.exists(p):
+                    m = joblib.load(p)
+                    self._fn = getattr(m, "predict")
+                    break
+        if self._fn is None:
+            raise FileNotFoundError(f"no supported model flavour in {root}")
+        self.ready = True
+
+    def predict(self, X, names, meta=None):
+        if not self.ready:
+            self.load()
+        return self._fn(X)
+
+
+class TFServingProxy:
+    """TENSORFLOW_SERVER: the reference proxies to a TF Serving sidecar
+    (integrations/tfserving/TfServingProxy.py).  There is no TF Serving on this
+    platform; SavedModels must be exported to TorchScript and served by
+    MLFlowServer-style loading instead."""
+
+    def __init__(self, model_uri: str = "", **kw):
+        self.model_uri = model_uri
+        self._inner = MLFlowServer(model_uri)
+
+    def load(self) -> None:
+        self._inner.load()
+
+    def predict(self, X, names, meta=None):
+        return self._inner.predict(X, names, meta)
+
+
+def load_prepackaged(impl: str, model_uri: str, params: Dict[str, Any]):
+    p = {k: v for k, v in params.items() if k not in ("model_uri",)}
+    if impl == "SKLEARN_SERVER":
+        s = SKLearnServer(model_uri, method=p.get("method", "predict_proba"))
+    elif impl == "XGBOOST_SERVER":
+        s = XGBoostServer(model_uri)
+    elif impl == "MLFLOW_SERVER":
+        s = MLFlowServer(model_uri)
+    elif impl == "TENSORFLOW_SERVER":
+        s = TFServingProxy(model_uri)
+    else:
+        raise ValueError(f"unknown prepackaged server {impl}")
+    s.load()
+    return s

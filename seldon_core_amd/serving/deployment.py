@@ -1,0 +1,252 @@
+"""In-process deployment of a SeldonDeployment inference graph.
+
+This replaces the reference's control plane + data plane hop chain
+(operator reconcile -> engine pod -> one microservice pod per node)
+with one process: the spec is validated with the operator webhook's rules,
+every graph node is bound to an implementation (built-in, prepackaged server,
+GPU row model behind a micro-batcher, or Python component), the native graph
+is compiled once, and the native REST/gRPC front ends serve it.
+
+Node binding order:
+1. explicit ``components={"node": obj}`` argument (object, class, "module.Class"
+   string, RowModel, model spec),
+2. built-in implementations (SIMPLE_MODEL, SIMPLE_ROUTER, RANDOM_ABTEST,
+   AVERAGE_COMBINER) -- executed natively,
+3. prepackaged servers (SKLEARN_SERVER, XGBOOST_SERVER, MLFLOW_SERVER,
+   TENSORFLOW_SERVER) -- loaded from ``modelUri``,
+4. engine-native component implementations (EPSILON_GREEDY, THOMPSON_SAMPLING,
+   MAHALANOBIS_OD, ISOLATION_FOREST_OD, VAE_OD, SEQ2SEQ_OD, ...),
+5. the node's container: ``MODEL_NAME`` / ``SELDON_PYTHON_CLASS`` env var, or a
+   ``python_class`` parameter, naming a Python component class.
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import logging
+import os
+from typing import Any, Dict, Optional, Union
+
+from .._native import gpu_count, native
+from .adapter import PythonUnit
+from .errors import EngineError
+from .spec import (BUILTIN_IMPLEMENTATIONS, PREPACKAGED_SERVERS, SpecError, container_for, iter_nodes,
+                   load_spec, select_predictor, typed_parameters, validate)
+
+logger = logging.getLogger(__name__)
+
+METHOD_IDS = {"TRANSFORM_INPUT": 0, "TRANSFORM_OUTPUT": 1, "ROUTE": 2, "AGGREGATE": 3, "SEND_FEEDBACK": 4}
+BATCHER_KEYS = ("max_batch", "max_wait_us", "slots", "zero_copy", "zero_copy_max_bytes", "spin_wait")
+
+
+def import_class(path: str):
+    mod, _, cls = path.replace(":", ".").rpartition(".")
+    if not mod:
+        mod, cls = cls, cls  # reference convention: module and class share a name
+    return getattr(importlib.import_module(mod), cls)
+
+
+class Deployment:
+    def __init__(self, spec: Union[str, Dict, None] = None, components: Optional[Dict[str, Any]] = None,
+                 predictor: Optional[str] = None, deployment_name: Optional[str] = None,
+                 device: Optional[int] = None, batcher: Optional[Dict[str, Any]] = None,
+                 log_requests: bool = False, log_responses: bool = False):
+        self.C = native()
+        self.sdep = load_spec(spec)
+        self.predictor = select_predictor(self.sdep, predictor)
+        self.components = dict(components or {})
+        self.deployment_name = deployment_name or os.environ.get("DEPLOYMENT_NAME", "None")
+        if device is None:
+            device = 0 if gpu_count() > 0 else -1
+        self.device = device
+        self.batcher_defaults = dict(max_batch=1024, max_wait_us=0, slots=4, zero_copy=True,
+                                     zero_copy_max_bytes=256 << 10, spin_wait=True)
+        self.batcher_defaults.update(batcher or {})
+        errs = validate({"spec": {"predictors": [self.predictor]}}, bound=set(self.components))
+        errs = [e for e in errs if "Traffic" not in e]
+        if errs:
+            raise SpecError(errs)
+        self.engine = self.C.Engine(json.dumps(self.predictor), self.deployment_name, "", log_requests,
+                                    log_responses, False)
+        self.units: Dict[str, Any] = {}
+        self.batched: Dict[str, Any] = {}
+        for node, _ in iter_nodes(self.predictor["graph"]):
+            self._bind(node)
+        self.engine.finalize()
+        self._servers = []
+
+    # ----------------------------------------------------------- binding
+    def _node_device(self, node: Dict) -> int:
+        d = node.get("device")
+        return self.device if d is None else int(d)
+
+    def _batcher_opts(self, node: Dict) -> Dict[str, Any]:
+        opts = dict(self.batcher_defaults)
+        params = typed_parameters(node)
+        for k in BATCHER_KEYS:
+            if k in params:
+                opts[k] = params[k]
+        return opts
+
+    def bind_row_model(self, node: Dict, row_model) -> None:
+        unit = self.C.BatchedUnit(row_model, self._node_device(node), **self._batcher_opts(node))
+        self.engine.bind_batched(node["name"], unit)
+        self.batched[node["name"]] = unit
+        self.units[node["name"]] = unit
+
+    def bind_python(self, node: Dict, obj: Any) -> None:
+        unit_type = node.get("type", "MODEL")
+        if unit_type in (None, "UNKNOWN_TYPE"):
+            unit_type = "UNKNOWN_TYPE"
+        adapter = PythonUnit(obj, unit_type, node["name"])
+        self.engine.bind_python(node["name"], adapter, 0)
+        self.units[node["name"]] = adapter
+
+    def _bind_object(self, node: Dict, obj: Any) -> None:
+        from ..models import to_row_model
+
+        if isinstance(obj, str):
+            obj = import_class(obj)
+        if isinstance(obj, type):
+            obj = obj(**typed_parameters(node))
+            if hasattr(obj, "load"):
+                obj.load()
+        if isinstance(obj, self.C.RowModel):
+            self.bind_row_model(node, obj)
+            return
+        gpu = getattr(obj, "row_model", None)
+        if callable(gpu):
+            rm = gpu()
+            if rm is not None:
+                self.bind_row_model(node, rm)
+                return
+        rm = to_row_model(obj) if not hasattr(obj, "predict_raw") else None
+        if rm is not None and not any(hasattr(obj, m) for m in ("route", "aggregate", "transform_input")):
+            self.bind_row_model(node, rm)
+            return
+        self.bind_python(node, obj)
+
+    def _bind(self, node: Dict) -> None:
+        name = node["name"]
+        impl = node.get("implementation", "UNKNOWN_IMPLEMENTATION")
+        if name in self.components:
+            self._bind_object(node, self.components[name])
+            return
+        if impl in BUILTIN_IMPLEMENTATIONS:
+            return  # native built-in
+        params = typed_parameters(node)
+        if impl in PREPACKAGED_SERVERS:
+            from ..servers import load_prepackaged
+
+            obj = load_prepackaged(impl, node.get("modelUri", ""), params)
+            self._bind_object(node, obj)
+            return
+        from ..components import NATIVE_IMPLEMENTATIONS
+
+        if impl in NATIVE_IMPLEMENTATIONS:
+            obj = NATIVE_IMPLEMENTATIONS[impl](**params)
+            self._bind_object(node, obj)
+            return
+        cls_path = params.pop("python_class", None)
+        c = container_for(self.predictor, name)
+        if not cls_path and c:
+            for e in c.get("env", []) or []:
+                if e.get("name") in ("MODEL_NAME", "SELDON_PYTHON_CLASS"):
+                    cls_path = e.get("value")
+        if cls_path:
+            obj = import_class(cls_path)(**params)
+            if hasattr(obj, "load"):
+                obj.load()
+            self._bind_object(node, obj)
+            return
+        raise SpecError([f"no implementation for graph node '{name}' ({impl}); pass components={{'{name}': ...}}"])
+
+    # ----------------------------------------------------------- requests
+    def predict(self, payload: Union[Dict, str]) -> Dict:
+        text = payload if isinstance(payload, str) else json.dumps(payload)
+        status, body = self.engine.predict_json(text)
+        out = json.loads(body)
+        if status != 200:
+            raise EngineError(status, out)
+        return out
+
+    def predict_raw(self, payload: Union[Dict, str]):
+        text = payload if isinstance(payload, str) else json.dumps(payload)
+        status, body = self.engine.predict_json(text)
+        return status, json.loads(body)
+
+    def predict_pb(self, data: bytes):
+        return self.engine.predict_pb(data)
+
+    def feedback(self, payload: Union[Dict, str]) -> Dict:
+        text = payload if isinstance(payload, str) else json.dumps(payload)
+        status, body = self.engine.feedback_json(text)
+        out = json.loads(body)
+        if status != 200:
+            raise EngineError(status, out)
+        return out
+
+    def call_node(self, node: str, method: str, payload: Union[Dict, str]):
+        text = payload if isinstance(payload, str) else json.dumps(payload)
+        status, body = self.engine.call_node_json(node, METHOD_IDS[method], text)
+        return status, json.loads(body)
+
+    def metrics(self) -> str:
+        return self.engine.metrics_text()
+
+    def ready(self) -> bool:
+        return bool(self.engine.ready())
+
+    def batcher_stats(self) -> Dict[str, Dict]:
+        return {k: v.stats() for k, v in self.batched.items()}
+
+    # ----------------------------------------------------------- serving
+    def serve(self, http_port: int = 8000, grpc_port: Optional[int] = 5001, admin_port: Optional[int] = None,
+              threads: int = 4, grpc_threads: Optional[int] = None, host: str = "0.0.0.0",
+              microservice_node: str = "") -> "ServerHandle":
+        ports = [http_port] + ([admin_port] if admin_port else [])
+        http = self.C.HttpServer(self.engine, host, ports, threads, microservice_node, True, "")
+        http.start()
+        grpc = None
+        if grpc_port is not None:
+            grpc = self.C.GrpcServer(self.engine, host, grpc_port, grpc_threads or threads, microservice_node)
+            grpc.start()
+        h = ServerHandle(self, http, grpc)
+        self._servers.append(h)
+        return h
+
+    def close(self) -> None:
+        for s in self._servers:
+            s.stop()
+        self._servers = []
+        for u in self.batched.values():
+            u.stop()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class ServerHandle:
+    def __init__(self, dep: Deployment, http, grpc):
+        self.deployment = dep
+        self.http = http
+        self.grpc = grpc
+
+    @property
+    def http_port(self) -> int:
+        return self.http.ports[0]
+
+    @property
+    def grpc_port(self) -> Optional[int]:
+        return self.grpc.port if self.grpc else None
+
+    def stop(self) -> None:
+        if self.http:
+            self.http.stop()
+            self.http = None
+        if self.grpc:
+            self.grpc.stop()
+            self.grpc = None

@@ -1,0 +1,129 @@
+"""End-to-end serving on the GPU: native front ends -> executor -> micro-batcher
+-> HIP kernels, checked against scikit-learn / the CPU reference path."""
+import json
+import threading
+import urllib.request
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _iris_dep(device=0, **batcher):
+    import seldon_core_amd as sca
+    from seldon_core_amd.models import iris_logistic_regression
+    from seldon_core_amd.servers import SKLearnServer
+
+    clf = iris_logistic_regression()
+    spec = {"name": "iris", "graph": {"name": "classifier", "type": "MODEL", "implementation": "SKLEARN_SERVER",
+                                      "modelUri": "memory://iris"}}
+    dep = sca.Deployment(spec, components={"classifier": SKLearnServer(model=clf)}, device=device,
+                         batcher=batcher or None)
+    return dep, clf
+
+
+def test_gpu_unit_is_native():
+    dep, _ = _iris_dep()
+    try:
+        assert dep.engine.unit_kind("classifier") == "gpu:linear"
+    finally:
+        dep.close()
+
+
+@pytest.mark.parametrize("kind", ["ndarray", "tensor"])
+def test_iris_parity(kind):
+    dep, clf = _iris_dep()
+    try:
+        X = np.random.default_rng(0).uniform(0, 8, (33, 4))
+        if kind == "ndarray":
+            payload = {"data": {"ndarray": X.tolist()}}
+        else:
+            payload = {"data": {"tensor": {"shape": [33, 4], "values": X.ravel().tolist()}}}
+        out = dep.predict(payload)
+        if kind == "ndarray":
+            got = np.array(out["data"]["ndarray"])
+        else:
+            got = np.array(out["data"]["tensor"]["values"]).reshape(out["data"]["tensor"]["shape"])
+        np.testing.assert_allclose(got, clf.predict_proba(X), rtol=1e-12, atol=1e-13)
+        assert out["data"]["names"] == ["t:0", "t:1", "t:2"]
+        assert out["meta"]["requestPath"] == {"classifier": ""}
+    finally:
+        dep.close()
+
+
+def test_concurrent_requests_batch_together():
+    dep, clf = _iris_dep(max_batch=512)
+    h = dep.serve(http_port=0, grpc_port=None, threads=4, host="127.0.0.1")
+    errors = []
+    rng = np.random.default_rng(1)
+    rows = rng.uniform(0, 8, (64, 4))
+
+    def worker(i):
+        try:
+            for j in range(20):
+                x = rows[(i + j) % 64]
+                req = urllib.request.Request(f"http://127.0.0.1:{h.http_port}/api/v0.1/predictions",
+                                             data=json.dumps({"data": {"ndarray": [x.tolist()]}}).encode(),
+                                             headers={"Content-Type": "application/json"})
+                out = json.loads(urllib.request.urlopen(req, timeout=30).read())
+                got = np.array(out["data"]["ndarray"])
+                np.testing.assert_allclose(got, clf.predict_proba(x[None, :]), rtol=1e-12, atol=1e-13)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(32)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    h.stop()
+    stats = dep.batcher_stats()["classifier"]
+    dep.close()
+    assert not errors, errors[:3]
+    assert stats["requests"] == 32 * 20
+    assert stats["batches"] <= stats["requests"]
+
+
+def test_xgboost_1000_tree_graph_gpu():
+    import seldon_core_amd as sca
+    from seldon_core_amd.models import synthetic_xgboost
+    from seldon_core_amd.servers import XGBoostServer
+
+    ens = synthetic_xgboost(1000, 8, 32, seed=0)
+    spec = {"name": "xgb", "graph": {"name": "xgb", "type": "MODEL", "implementation": "XGBOOST_SERVER",
+                                     "modelUri": "memory://xgb"}}
+    dep = sca.Deployment(spec, components={"xgb": XGBoostServer(ensemble=ens)}, device=0)
+    try:
+        assert dep.engine.unit_kind("xgb") == "gpu:tree_perfect"
+        X = np.random.default_rng(2).standard_normal((256, 32))
+        out = dep.predict({"data": {"tensor": {"shape": [256, 32], "values": X.ravel().tolist()}}})
+        assert out["data"]["tensor"]["shape"] == [256]
+        got = np.array(out["data"]["tensor"]["values"])
+        np.testing.assert_allclose(got, ens.predict(X), rtol=1e-4, atol=1e-4)
+    finally:
+        dep.close()
+
+
+def test_gpu_abtest_two_devices_or_one():
+    """seldon-abtest graph: RANDOM_ABTEST over two GPU model replicas."""
+    import torch
+
+    import seldon_core_amd as sca
+    from seldon_core_amd.models import iris_logistic_regression
+    from seldon_core_amd.servers import SKLearnServer
+
+    ndev = torch.cuda.device_count()
+    clf = iris_logistic_regression()
+    spec = {"name": "ab", "graph": {"name": "ab", "implementation": "RANDOM_ABTEST",
+                                    "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
+                                    "children": [
+                                        {"name": "a", "type": "MODEL", "device": 0},
+                                        {"name": "b", "type": "MODEL", "device": 1 % ndev}]}}
+    dep = sca.Deployment(spec, components={"a": SKLearnServer(model=clf), "b": SKLearnServer(model=clf)})
+    try:
+        seen = set()
+        for _ in range(40):
+            out = dep.predict({"data": {"ndarray": [[5.0, 3.0, 1.5, 0.3]]}})
+            seen.add(out["meta"]["routing"]["ab"])
+        assert seen == {0, 1}
+    finally:
+        dep.close()

@@ -1,0 +1,164 @@
+"""Numerics of the hand-written gfx950 kernels vs plain PyTorch references.
+
+Each kernel is launched directly (raw device pointers + the current torch
+stream) and compared with an fp32/fp64 PyTorch implementation of the same op.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@pytest.mark.parametrize("rows,K,C,act", [(1, 4, 3, 1), (7, 4, 3, 1), (300, 4, 3, 1), (64, 30, 1, 2),
+                                          (129, 64, 10, 3), (50, 200, 40, 1), (33, 5, 6, 0), (17, 8, 5, 4)])
+def test_linear_f64(C, rows, K, act):
+    g = torch.Generator().manual_seed(rows * 31 + K)
+    X = torch.randn(rows, K, dtype=torch.float64, generator=g).to(dev)
+    W = torch.randn(C, K, dtype=torch.float64, generator=g).to(dev)
+    b = torch.randn(C, dtype=torch.float64, generator=g).to(dev)
+    out_cols = 2 if act == 2 else C
+    out = torch.empty(rows, out_cols, dtype=torch.float64, device=dev)
+    C_.kernels.linear_f64(X.data_ptr(), rows, K, W.data_ptr(), b.data_ptr(), C, act, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    z = X @ W.T + b
+    if act == 0:
+        ref = z
+    elif act == 1:
+        ref = torch.softmax(z, dim=1)
+    elif act == 2:
+        p = torch.sigmoid(z[:, 0])
+        ref = torch.stack([1 - p, p], dim=1)
+    elif act == 3:
+        s = torch.sigmoid(z)
+        ref = s / s.sum(dim=1, keepdim=True)
+    else:
+        ref = torch.sigmoid(z)
+    torch.testing.assert_close(out, ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.fixture(scope="module")
+def C_():
+    from seldon_core_amd import native
+
+    return native()
+
+
+@pytest.mark.parametrize("rows", [1, 3, 64, 1000, 4096])
+def test_tree_perfect_vs_cpu(C_, rows):
+    from seldon_core_amd.models import synthetic_xgboost, to_row_model
+
+    ens = synthetic_xgboost(200, 8, 16, seed=rows)
+    rm = to_row_model(ens)
+    unit = C_.BatchedUnit(rm, 0, max_batch=8192)
+    try:
+        X = np.random.default_rng(rows).standard_normal((rows, 16))
+        X[0, 3] = np.nan  # exercise default direction
+        got = unit.run(X)
+        ref = ens.predict(X)
+        np.testing.assert_allclose(np.asarray(got).reshape(ref.shape), ref, rtol=2e-5, atol=2e-5)
+    finally:
+        unit.stop()
+
+
+def test_tree_softmax_groups(C_):
+    """multi:softprob-style: 3 groups, softmax transform."""
+    from seldon_core_amd.models import to_row_model
+    from seldon_core_amd.models.trees import T_SOFTMAX, TreeEnsemble, synthetic_xgboost
+
+    base = synthetic_xgboost(30, 5, 6, seed=3)
+    for i, t in enumerate(base.trees):
+        t.group = i % 3
+    ens = TreeEnsemble(base.trees, 6, 3, 3, T_SOFTMAX, 0, 1.0, [0.1, 0.2, 0.3])
+    unit = C_.BatchedUnit(to_row_model(ens), 0)
+    try:
+        X = np.random.default_rng(0).standard_normal((40, 6))
+        np.testing.assert_allclose(unit.run(X), ens.predict(X), rtol=2e-5, atol=2e-6)
+    finally:
+        unit.stop()
+
+
+def test_tree_sparse_random_forest(C_):
+    from sklearn.datasets import make_classification
+    from sklearn.ensemble import RandomForestClassifier
+
+    from seldon_core_amd.models import to_row_model
+
+    X, y = make_classification(n_samples=400, n_features=10, n_informative=6, n_classes=3, random_state=0)
+    rf = RandomForestClassifier(n_estimators=20, random_state=0).fit(X, y)  # deep trees -> sparse layout
+    rm = to_row_model(rf)
+    assert rm.name == "tree_sparse"
+    unit = C_.BatchedUnit(rm, 0)
+    try:
+        got = unit.run(X[:100])
+        np.testing.assert_allclose(got, rf.predict_proba(X[:100]), rtol=1e-5, atol=1e-6)
+    finally:
+        unit.stop()
+
+
+def test_combine_mean(C_):
+    n = 1001
+    ins = [torch.randn(n, dtype=torch.float64, device=dev) for _ in range(3)]
+    ptrs = torch.tensor([t.data_ptr() for t in ins], dtype=torch.int64, device=dev)
+    out = torch.empty(n, dtype=torch.float64, device=dev)
+    C_.kernels.combine_mean_f64(ptrs.data_ptr(), 3, n, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, (ins[0] + ins[1] + ins[2]) / 3, rtol=1e-14, atol=1e-14)
+
+
+def test_softmax_argmax_rows(C_):
+    x = torch.randn(37, 1000, dtype=torch.float64, device=dev)
+    out = torch.empty_like(x)
+    idx = torch.empty(37, dtype=torch.int32, device=dev)
+    C_.kernels.softmax_rows_f64(x.data_ptr(), 37, 1000, out.data_ptr(), _stream())
+    C_.kernels.argmax_rows_f64(x.data_ptr(), 37, 1000, idx.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, torch.softmax(x, dim=1), rtol=1e-12, atol=1e-14)
+    assert torch.equal(idx.long(), x.argmax(dim=1))
+
+
+def test_minmax_and_mean_sigmoid(C_):
+    x = torch.randn(5000, dtype=torch.float64, device=dev) * 3 + 1
+    out = torch.empty_like(x)
+    scratch = torch.empty(2, dtype=torch.float64, device=dev)
+    C_.kernels.minmax_normalize_f64(x.data_ptr(), x.numel(), out.data_ptr(), scratch.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, (x - x.min()) / (x.max() - x.min()), rtol=1e-13, atol=1e-13)
+    m = torch.randn(70, 13, dtype=torch.float64, device=dev)
+    o = torch.empty(70, dtype=torch.float64, device=dev)
+    C_.kernels.mean_sigmoid_rows_f64(m.data_ptr(), 70, 13, 0.25, o.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(o, torch.sigmoid(m.mean(dim=1) - 0.25), rtol=1e-13, atol=1e-13)
+
+
+def test_eg_route_statistics(C_):
+    """|p(best) - (1 - eps)| small (components/routers/epsilon-greedy/test_EpsilonGreedy.py:21-25)."""
+    values = torch.tensor([0.1, 0.9, 0.3, 0.2], dtype=torch.float32, device=dev)
+    n = 200000
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    C_.kernels.eg_route(values.data_ptr(), 4, 0.1, 1234, 0, n, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    p_best = (out == 1).float().mean().item()
+    assert abs(p_best - 0.9) < 0.01
+    counts = torch.bincount(out.long(), minlength=4).float() / n
+    for b in (0, 2, 3):
+        assert abs(counts[b].item() - 0.1 / 3) < 0.01
+
+
+def test_ts_route_prefers_better_arm(C_):
+    alpha = torch.tensor([2.0, 50.0, 5.0], dtype=torch.float32, device=dev)
+    beta = torch.tensor([50.0, 2.0, 5.0], dtype=torch.float32, device=dev)
+    n = 50000
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    C_.kernels.ts_route(alpha.data_ptr(), beta.data_ptr(), 3, 99, 0, n, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    frac = torch.bincount(out.long(), minlength=3).float() / n
+    # P(Beta(50,2) > Beta(5,5)) and > Beta(2,50) is ~1
+    assert frac[1].item() > 0.99
+    assert out.min().item() >= 0 and out.max().item() <= 2

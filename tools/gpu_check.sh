@@ -1,0 +1,45 @@
+#!/usr/bin/env bash
+# One-shot GPU validation run (used through gpurun): gpu tests, smoke, benches,
+# rocprofv3 kernel trace.  Each GPU step has its own time limit; test failures
+# (rc 1) do not stop later steps, but a crash / abort / timeout does.
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+STEPS="${STEPS:-tests smoke bench bench_xgb prof}"
+
+run() {  # name timeout cmd...
+  local name=$1 tmo=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/summary.log"
+  timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/summary.log"
+  tail -n 5 "$OUT/$name.log" | tee -a "$OUT/summary.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping after $name (rc=$rc)" | tee -a "$OUT/summary.log"
+    exit $rc
+  fi
+  return 0
+}
+
+rocm-smi --showproductname > "$OUT/rocm_smi.log" 2>&1 || true
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    smoke) run smoke 180 python __graft_entry__.py smoke ;;
+    bench) run bench 400 python bench.py --extra-grpc ;;
+    bench_grpc) run bench_grpc 400 python bench.py --api grpc ;;
+    bench_xgb) run bench_xgb 400 python bench.py --model xgb1000 --step-requests 20000 ;;
+    prof)
+      export TMPDIR=/tmp
+      run prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+        python3 bench.py --steps 3 --warmup 1 --step-requests 20000 ;;
+    prof_xgb)
+      export TMPDIR=/tmp
+      run prof_xgb 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_xgb" -o run --output-format csv -- \
+        python3 bench.py --model xgb1000 --steps 3 --warmup 1 --step-requests 10000 ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "all done" | tee -a "$OUT/summary.log"
