@@ -22,6 +22,12 @@ bool available() { return device_count() > 0; }
 BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::move(model)), opts_(opts) {
   if (opts_.max_batch < 1) opts_.max_batch = 1;
   if (opts_.slots < 1) opts_.slots = 1;
+  {
+    const int oc = model_->out_cols(model_->in_cols() > 0 ? model_->in_cols() : 1);
+    default_names_ = model_->class_names();
+    if (default_names_.empty())
+      for (int c = 0; c < oc; ++c) default_names_.push_back("t:" + std::to_string(c));
+  }
   if (opts_.device < 0) {
     running_.store(true);
     return;
@@ -41,7 +47,12 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
   }
   running_.store(true);
   submit_th_ = std::thread([this] { submit_loop(); });
-  complete_th_ = std::thread([this] { complete_loop(); });
+  // One completion thread per slot: responses of concurrent batches are
+  // scattered (and their graph continuations run) in parallel.
+  for (auto& s : slots_) {
+    Slot* raw = s.get();
+    s->th = std::thread([this, raw] { complete_loop(raw); });
+  }
 }
 
 BatchedUnit::~BatchedUnit() { stop(); }
@@ -52,9 +63,10 @@ void BatchedUnit::stop() {
     std::lock_guard<std::mutex> g(mu_);
   }
   cv_submit_.notify_all();
-  cv_complete_.notify_all();
+  for (auto& s : slots_) s->cv.notify_all();
   if (submit_th_.joinable()) submit_th_.join();
-  if (complete_th_.joinable()) complete_th_.join();
+  for (auto& s : slots_)
+    if (s->th.joinable()) s->th.join();
   // Fail anything still queued.
   std::deque<Item> rest;
   {
@@ -85,13 +97,15 @@ MsgPtr BatchedUnit::make_response(const Item& it, const double* out, int out_col
   auto m = std::make_shared<SeldonMessage>();
   m->payload = Payload::Data;
   const bool flat = model_->flat_output() && out_cols == 1;
-  std::vector<std::string> names;
   if (!flat) {  // client_class_names: explicit names, else t:0..t:C-1
-    names = model_->class_names();
-    if (names.empty())
-      for (int c = 0; c < out_cols; ++c) names.push_back("t:" + std::to_string(c));
+    if (int(default_names_.size()) == out_cols) {
+      m->data.names = default_names_;
+    } else {
+      m->data.names = model_->class_names();
+      if (m->data.names.empty())
+        for (int c = 0; c < out_cols; ++c) m->data.names.push_back("t:" + std::to_string(c));
+    }
   }
-  m->data.names = std::move(names);
   DataKind kind = it.req->payload == Payload::Data ? it.req->data.kind : DataKind::Tensor;
   std::vector<double> vals(out, out + size_t(it.rows) * out_cols);
   std::vector<int64_t> shape = flat ? std::vector<int64_t>{int64_t(it.rows)} : std::vector<int64_t>{int64_t(it.rows), int64_t(out_cols)};
@@ -228,28 +242,27 @@ void BatchedUnit::submit_loop() {
       continue;
     }
     lk.lock();
-    inflight_.push_back(s);
-    cv_complete_.notify_one();
+    s->launched = true;
+    s->cv.notify_one();
   }
 }
 
-void BatchedUnit::complete_loop() {
+void BatchedUnit::complete_loop(Slot* s) {
   (void)hipSetDevice(opts_.device);
   while (true) {
-    Slot* s;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_complete_.wait(lk, [&] { return !inflight_.empty() || !running_.load(); });
-      if (inflight_.empty()) break;
-      s = inflight_.front();
-      inflight_.pop_front();
+      s->cv.wait(lk, [&] { return s->launched || !running_.load(); });
+      if (!s->launched) break;
+      s->launched = false;
     }
     auto t0 = std::chrono::steady_clock::now();
     hipError_t st;
     if (opts_.spin_wait) {
+      // A batch round trip is ~10-30 us: spin briefly, then back off.
       int spins = 0;
       while ((st = hipEventQuery(s->ev.get())) == hipErrorNotReady) {
-        if (++spins < 20000) _mm_pause();
+        if (++spins < 2000) _mm_pause();
         else std::this_thread::yield();
       }
     } else {

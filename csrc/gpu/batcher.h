@@ -86,12 +86,15 @@ class BatchedUnit : public Unit {
     int rows = 0;
     int cols = 0;
     int out_cols = 0;
-    bool busy = false;
+    bool busy = false;      // guarded by BatchedUnit::mu_
+    bool launched = false;  // guarded by BatchedUnit::mu_
+    std::condition_variable cv;
+    std::thread th;         // per-slot completion thread
   };
 
   void ensure_capacity(Slot& s, int rows, int cols);
   void submit_loop();
-  void complete_loop();
+  void complete_loop(Slot* s);
   void finish_items(std::vector<Item>& items, const double* out, int out_cols);
   MsgPtr make_response(const Item& it, const double* out, int out_cols) const;
 
@@ -100,12 +103,11 @@ class BatchedUnit : public Unit {
   std::vector<std::unique_ptr<Slot>> slots_;
   std::mutex mu_;
   std::condition_variable cv_submit_;
-  std::condition_variable cv_complete_;
   std::deque<Item> queue_;
   size_t queued_rows_ = 0;
-  std::deque<Slot*> inflight_;
   std::atomic<bool> running_{false};
-  std::thread submit_th_, complete_th_;
+  std::thread submit_th_;
+  std::vector<std::string> default_names_;
   mutable std::mutex stats_mu_;
   BatcherStats stats_;
 };

@@ -199,13 +199,17 @@ struct GrpcServer::Worker : std::enable_shared_from_this<GrpcServer::Worker> {
       complete(std::move(d), false);
       return;
     }
+    bool was_empty;
     {
       std::lock_guard<std::mutex> g(qmu);
+      was_empty = q.empty();
       q.push_back(std::move(d));
     }
-    uint64_t one = 1;
-    ssize_t w = ::write(evfd, &one, 8);
-    (void)w;
+    if (was_empty) {  // one wakeup per drained batch of completions
+      uint64_t one = 1;
+      ssize_t w = ::write(evfd, &one, 8);
+      (void)w;
+    }
   }
 
   void complete(GCompletion&& d, bool flush_now) {

@@ -495,13 +495,17 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
       if (it != conns.end() && it->second->gen == done.gen && !it->second->dead) finish(it->second.get(), std::move(done), false);
       return;
     }
+    bool was_empty;
     {
       std::lock_guard<std::mutex> g(qmu);
+      was_empty = q.empty();
       q.push_back(std::move(done));
     }
-    uint64_t one = 1;
-    ssize_t w = ::write(evfd, &one, 8);
-    (void)w;
+    if (was_empty) {  // one wakeup per drained batch of completions
+      uint64_t one = 1;
+      ssize_t w = ::write(evfd, &one, 8);
+      (void)w;
+    }
   }
 
   void drain_queue() {

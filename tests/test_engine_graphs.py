@@ -1,0 +1,253 @@
+"""Graph-executor semantics with built-in units and Python components.
+
+Mirrors the reference engine tests (engine/src/test/java/io/seldon/engine/
+predictors/*: AverageCombinerTest, RandomABTestUnitTest, PredictiveUnitBeanTest)
+and the external-graph tests with mocked microservices
+(api/rest/TestRestClientControllerExternalGraphs.java) -- here the
+"microservices" are in-process Python components.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import seldon_core_amd as sca
+from seldon_core_amd.serving.errors import EngineError
+
+REF = "/root/reference/engine/src/test/resources"
+
+
+def dep(graph, components=None, **kw):
+    return sca.Deployment({"name": "p", "graph": graph}, components=components or {}, device=-1, **kw)
+
+
+def test_simple_model_default():
+    d = sca.Deployment(None, device=-1)
+    out = d.predict({"data": {"ndarray": [[1.0, 2.0]]}})
+    assert out["data"]["tensor"] == {"shape": [1, 3], "values": [0.1, 0.9, 0.5]}
+    assert out["data"]["names"] == ["class0", "class1", "class2"]
+    assert out["status"]["status"] == "SUCCESS"
+    assert [m["key"] for m in out["meta"]["metrics"]] == ["mymetric_counter", "mymetric_gauge", "mymetric_timer"]
+    assert out["meta"]["requestPath"] == {"basic-pu": ""}
+    assert len(out["meta"]["puid"]) > 10
+
+
+def test_puid_preserved_and_strdata_echo():
+    d = dep({"name": "m", "type": "MODEL", "implementation": "SIMPLE_MODEL"})
+    out = d.predict({"meta": {"puid": "xyz"}, "strData": "hello"})
+    assert out["meta"]["puid"] == "xyz" and out["strData"] == "hello"
+
+
+def test_abtest_routing_sequence_matches_java_random():
+    """RANDOM_ABTEST uses java.util.Random(1337).nextFloat() <= ratioA."""
+    d = dep({"name": "ab", "implementation": "RANDOM_ABTEST",
+             "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
+             "children": [{"name": "a", "type": "MODEL", "implementation": "SIMPLE_MODEL"},
+                          {"name": "b", "type": "MODEL", "implementation": "SIMPLE_MODEL"}]})
+    # java.util.Random(1337) first nextFloat() values (48-bit LCG)
+    seed = (1337 ^ 0x5DEECE66D) & ((1 << 48) - 1)
+    expect = []
+    for _ in range(20):
+        seed = (seed * 0x5DEECE66D + 0xB) & ((1 << 48) - 1)
+        f = (seed >> 24) / float(1 << 24)
+        expect.append(0 if f <= 0.5 else 1)
+    got = [d.predict({"data": {"ndarray": [[1]]}})["meta"]["routing"]["ab"] for _ in range(20)]
+    assert got == expect
+    out = d.predict({"data": {"ndarray": [[1]]}})
+    assert set(out["meta"]["requestPath"]) == {"ab", "a"} or set(out["meta"]["requestPath"]) == {"ab", "b"}
+
+
+def test_abtest_errors():
+    d = dep({"name": "ab", "implementation": "RANDOM_ABTEST",
+             "children": [{"name": "a", "implementation": "SIMPLE_MODEL"}, {"name": "b", "implementation": "SIMPLE_MODEL"}]})
+    with pytest.raises(EngineError) as e:
+        d.predict({"data": {"ndarray": [[1]]}})
+    assert e.value.body["code"] == 204 and "ratioA" in e.value.body["info"]
+
+
+def test_average_combiner():
+    class M:
+        def __init__(self, v):
+            self.v = v
+
+        def predict(self, X, names):
+            return np.full((X.shape[0], 3), self.v)
+
+    d = dep({"name": "c", "implementation": "AVERAGE_COMBINER",
+             "children": [{"name": "m1", "type": "MODEL"}, {"name": "m2", "type": "MODEL"}, {"name": "m3", "type": "MODEL"}]},
+            {"m1": M(1.0), "m2": M(2.0), "m3": M(6.0)})
+    out = d.predict({"data": {"ndarray": [[1, 2], [3, 4]]}})
+    assert out["data"]["ndarray"] == [[3.0] * 3] * 2
+    assert out["meta"]["routing"] == {"c": -1}
+
+
+def test_average_combiner_shape_mismatch():
+    class M:
+        def __init__(self, n):
+            self.n = n
+
+        def predict(self, X, names):
+            return np.ones((1, self.n))
+
+    d = dep({"name": "c", "implementation": "AVERAGE_COMBINER",
+             "children": [{"name": "m1", "type": "MODEL"}, {"name": "m2", "type": "MODEL"}]}, {"m1": M(2), "m2": M(3)})
+    with pytest.raises(EngineError) as e:
+        d.predict({"data": {"ndarray": [[1]]}})
+    assert e.value.body["code"] == 204
+
+
+def test_transformer_model_output_transformer_chain_and_tags():
+    class T:
+        def transform_input(self, X, names):
+            return X * 2
+
+        def tags(self):
+            return {"t": "in"}
+
+    class M:
+        def predict(self, X, names):
+            return X + 1
+
+        def tags(self):
+            return {"m": 1}
+
+    class O:
+        def transform_output(self, X, names):
+            return X * 10
+
+        def tags(self):
+            return {"t": "out"}
+
+    g = {"name": "t", "type": "TRANSFORMER",
+         "children": [{"name": "o", "type": "OUTPUT_TRANSFORMER", "children": [{"name": "m", "type": "MODEL"}]}]}
+    d = dep(g, {"t": T(), "m": M(), "o": O()})
+    out = d.predict({"data": {"ndarray": [[1.0, 2.0]]}, "meta": {"tags": {"client": "c"}}})
+    assert out["data"]["ndarray"] == [[30.0, 50.0]]
+    # tag merge: union with later nodes overriding (PredictiveUnitBean.mergeMeta)
+    assert out["meta"]["tags"] == {"client": "c", "t": "out", "m": 1.0}
+    assert set(out["meta"]["requestPath"]) == {"t", "o", "m"}
+
+
+def test_python_router_and_feedback():
+    class R:
+        def __init__(self):
+            self.fb = []
+
+        def route(self, X, names):
+            return int(X[0][0]) % 2
+
+        def send_feedback(self, features, feature_names, routing, reward, truth):  # bundled-router order
+            self.fb.append((routing, reward))
+
+    class M:
+        def __init__(self):
+            self.fb = []
+
+        def predict(self, X, names):
+            return X
+
+        def send_feedback(self, X, names, reward, truth, routing=None):
+            self.fb.append(reward)
+
+    r, m0, m1 = R(), M(), M()
+    d = dep({"name": "r", "type": "ROUTER", "children": [{"name": "m0", "type": "MODEL"}, {"name": "m1", "type": "MODEL"}]},
+            {"r": r, "m0": m0, "m1": m1})
+    out = d.predict({"data": {"ndarray": [[3.0]]}})
+    assert out["meta"]["routing"] == {"r": 1}
+    assert set(out["meta"]["requestPath"]) == {"r", "m1"}
+    d.feedback({"request": {"data": {"ndarray": [[3.0]]}}, "response": out, "reward": 0.75})
+    assert r.fb == [(1, 0.75)] and m1.fb == [0.75] and m0.fb == []
+    text = d.metrics()
+    assert "seldon_api_model_feedback_reward_total" in text and "model_name=\"r\"" in text
+
+
+def test_invalid_routing():
+    class R:
+        def route(self, X, names):
+            return 5
+
+    d = dep({"name": "r", "type": "ROUTER", "children": [{"name": "m", "implementation": "SIMPLE_MODEL"}]}, {"r": R()})
+    with pytest.raises(EngineError) as e:
+        d.predict({"data": {"ndarray": [[1.0]]}})
+    assert e.value.body["code"] == 207
+
+
+def test_custom_metrics_to_prometheus():
+    class M:
+        def predict(self, X, names):
+            return X
+
+        def metrics(self):
+            return [{"type": "COUNTER", "key": "mycounter", "value": 1, "tags": {"mytag1": "mytagval1"}},
+                    {"type": "GAUGE", "key": "mygauge", "value": 22},
+                    {"type": "TIMER", "key": "mytimer", "value": 1}]
+
+    pred = {"name": "fx-market-predictor", "componentSpecs": [{"spec": {"containers": [
+        {"name": "mean-classifier", "image": "seldonio/mock_classifier:0.6"}]}}],
+            "graph": {"name": "mean-classifier", "type": "MODEL"}}
+    d = sca.Deployment(pred, components={"mean-classifier": M()}, device=-1)
+    for _ in range(2):
+        out = d.predict({"data": {"ndarray": [[1.0]]}})
+    assert [m["key"] for m in out["meta"]["metrics"]] == ["mycounter", "mygauge", "mytimer"]
+    text = d.metrics()
+    assert ('mycounter_total{deployment_name="None",model_image="seldonio/mock_classifier",model_name="mean-classifier",'
+            'model_version="0.6",mytag1="mytagval1",predictor_name="fx-market-predictor",predictor_version="unknown",} 2.0') in text
+    assert ('mygauge{deployment_name="None",model_image="seldonio/mock_classifier",model_name="mean-classifier",'
+            'model_version="0.6",predictor_name="fx-market-predictor",predictor_version="unknown",} 22.0') in text
+    assert ('mytimer_seconds_count{deployment_name="None",model_image="seldonio/mock_classifier",model_name="mean-classifier",'
+            'model_version="0.6",predictor_name="fx-market-predictor",predictor_version="unknown",} 2.0') in text
+
+
+def test_bad_metric_is_microservice_error():
+    class M:
+        def predict(self, X, names):
+            return X
+
+        def metrics(self):
+            return [{"type": "BAD", "key": "k", "value": 1}]
+
+    d = dep({"name": "m", "type": "MODEL"}, {"m": M()})
+    with pytest.raises(EngineError) as e:
+        d.predict({"data": {"ndarray": [[1.0]]}})
+    assert e.value.body["code"] == 203
+
+
+def test_unknown_type_needs_methods():
+    from seldon_core_amd.serving.spec import SpecError
+
+    with pytest.raises(SpecError):
+        sca.Deployment({"name": "p", "graph": {"name": "x"}}, device=-1)
+
+
+@pytest.mark.skipif(not os.path.exists(REF), reason="reference fixtures not mounted")
+@pytest.mark.parametrize("fixture", ["abtest.json", "model_simple.json", "router_simple.json", "combiner_simple.json",
+                                     "transformer_simple.json", "transform_output_simple.json"])
+def test_reference_spec_fixtures_parse(fixture, C):
+    """The reference's graph fixtures load and compile (with in-process stand-ins)."""
+    from seldon_core_amd.serving.spec import iter_nodes
+
+    spec = json.load(open(os.path.join(REF, fixture)))
+
+    class Echo:
+        def predict(self, X, names):
+            return X
+
+        def route(self, X, names):
+            return 0
+
+        def aggregate(self, Xs, names):
+            return Xs[0]
+
+        def transform_input(self, X, names):
+            return X
+
+        def transform_output(self, X, names):
+            return X
+
+    comps = {n["name"]: Echo() for n, _ in iter_nodes(spec["graph"])
+             if n.get("implementation", "UNKNOWN_IMPLEMENTATION") == "UNKNOWN_IMPLEMENTATION"}
+    d = sca.Deployment(spec, components=comps, device=-1)
+    params = {p["name"] for n, _ in iter_nodes(spec["graph"]) for p in n.get("parameters", [])}
+    out = d.predict({"data": {"ndarray": [[1.0]]}}) if "ratioA" in params or fixture != "abtest.json" else None
+    assert out is None or "data" in out

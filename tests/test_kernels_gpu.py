@@ -18,7 +18,7 @@ def _stream():
 
 @pytest.mark.parametrize("rows,K,C,act", [(1, 4, 3, 1), (7, 4, 3, 1), (300, 4, 3, 1), (64, 30, 1, 2),
                                           (129, 64, 10, 3), (50, 200, 40, 1), (33, 5, 6, 0), (17, 8, 5, 4)])
-def test_linear_f64(C, rows, K, act):
+def test_linear_f64(C_, rows, K, C, act):
     g = torch.Generator().manual_seed(rows * 31 + K)
     X = torch.randn(rows, K, dtype=torch.float64, generator=g).to(dev)
     W = torch.randn(C, K, dtype=torch.float64, generator=g).to(dev)
