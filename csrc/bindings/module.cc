@@ -11,6 +11,7 @@
 #include "../core/message.h"
 #include "../gpu/batcher.h"
 #include "../gpu/models.h"
+#include "../gpu/router.h"
 #include "../kernels/kernels.h"
 #include "../server/grpc_server.h"
 #include "../server/http_server.h"
@@ -201,7 +202,12 @@ PYBIND11_MODULE(_C, m) {
           return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::TreeEnsembleModel>(std::move(s)));
         });
 
-  py::class_<gpu::BatchedUnit, std::shared_ptr<gpu::BatchedUnit>>(m, "BatchedUnit")
+  py::class_<Unit, std::shared_ptr<Unit>>(m, "Unit")
+      .def_property_readonly("kind", &Unit::kind)
+      .def("snapshot", [](const Unit& u) { return py::bytes(u.snapshot()); })
+      .def("restore", [](Unit& u, const py::bytes& b) { u.restore(std::string(b)); });
+
+  py::class_<gpu::BatchedUnit, Unit, std::shared_ptr<gpu::BatchedUnit>>(m, "BatchedUnit")
       .def(py::init([](std::shared_ptr<gpu::RowModel> model, int device, int max_batch, int max_wait_us, int slots,
                        bool zero_copy, size_t zc_bytes, bool spin) {
              return std::make_shared<gpu::BatchedUnit>(
@@ -262,6 +268,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("node"), py::arg("adapter"), py::arg("builtin_methods") = 0)
       .def("bind_batched", [](Engine& e, const std::string& node,
                               std::shared_ptr<gpu::BatchedUnit> u) { e.bind(node, u); })
+      .def("bind_unit", [](Engine& e, const std::string& node, std::shared_ptr<Unit> u) { e.bind(node, u); })
       .def("finalize", &Engine::finalize)
       .def("ready", &Engine::ready)
       .def("node_names", &Engine::node_names)
@@ -426,12 +433,49 @@ PYBIND11_MODULE(_C, m) {
   k.def("mean_sigmoid_rows_f64", [](uintptr_t in, int rows, int F, double thr, uintptr_t out, uintptr_t s) {
     kern::mean_sigmoid_rows_f64(P<const double>(in), rows, F, thr, P<double>(out), as_stream(s));
   });
-  k.def("eg_route", [](uintptr_t values, int nb, float eps, uint64_t seed, uint64_t offset, int n, uintptr_t out,
+  k.def("eg_route", [](uintptr_t best, int nb, float eps, uint64_t seed, uint64_t offset, int n, uintptr_t out,
                        uintptr_t s) {
-    kern::eg_route(P<const float>(values), nb, eps, seed, offset, n, P<int32_t>(out), as_stream(s));
+    kern::eg_route(P<const int32_t>(best), nb, eps, seed, offset, n, P<double>(out), as_stream(s));
   });
   k.def("ts_route", [](uintptr_t alpha, uintptr_t beta, int nb, uint64_t seed, uint64_t offset, int n, uintptr_t out,
                        uintptr_t s) {
-    kern::ts_route(P<const float>(alpha), P<const float>(beta), nb, seed, offset, n, P<int32_t>(out), as_stream(s));
+    kern::ts_route(P<const float>(alpha), P<const float>(beta), nb, seed, offset, n, P<double>(out), as_stream(s));
   });
+
+  // ------------------------------------------------------------- routers
+  py::class_<gpu::BanditModel, gpu::RowModel, std::shared_ptr<gpu::BanditModel>>(m, "BanditModel")
+      .def(py::init([](int kind, int n_branches, float epsilon, int64_t seed, int best_branch) {
+             return std::make_shared<gpu::BanditModel>(gpu::BanditModel::Kind(kind), n_branches, epsilon, seed,
+                                                       best_branch);
+           }),
+           py::arg("kind"), py::arg("n_branches"), py::arg("epsilon") = 0.1f, py::arg("seed") = -1,
+           py::arg("best_branch") = -1)
+      .def("feedback", &gpu::BanditModel::feedback)
+      .def("values", &gpu::BanditModel::values)
+      .def_property_readonly("best_branch", &gpu::BanditModel::best_branch)
+      .def_property_readonly("n_branches", &gpu::BanditModel::n_branches)
+      .def("snapshot", &gpu::BanditModel::snapshot)
+      .def("restore", &gpu::BanditModel::restore);
+  py::class_<gpu::BanditRouterUnit, Unit, std::shared_ptr<gpu::BanditRouterUnit>>(m, "BanditRouterUnit")
+      .def(py::init([](std::shared_ptr<gpu::BanditModel> model, int device, int max_batch, int slots) {
+             gpu::BatcherOptions o;
+             o.device = device;
+             o.max_batch = max_batch;
+             o.slots = slots;
+             return std::make_shared<gpu::BanditRouterUnit>(model, o);
+           }),
+           py::arg("model"), py::arg("device") = 0, py::arg("max_batch") = 4096, py::arg("slots") = 2)
+      .def_property_readonly("model", &gpu::BanditRouterUnit::model)
+      .def("stats", [](const gpu::BanditRouterUnit& u) {
+        auto s = u.batcher()->stats();
+        py::dict d;
+        d["batches"] = s.batches;
+        d["rows"] = s.rows;
+        d["requests"] = s.requests;
+        return d;
+      })
+      .def("stop", [](gpu::BanditRouterUnit& u) {
+        py::gil_scoped_release nogil;
+        u.batcher()->stop();
+      });
 }

@@ -1,0 +1,186 @@
+#include "router.h"
+
+#include <sstream>
+
+namespace sca::gpu {
+
+BanditModel::BanditModel(Kind kind, int n_branches, float epsilon, int64_t seed, int best_branch)
+    : kind_(kind), nb_(n_branches), eps_(epsilon) {
+  if (n_branches < 1 || n_branches > kMaxBranches)
+    throw std::runtime_error("bandit router: n_branches must be in [1, " + std::to_string(kMaxBranches) + "]");
+  seed_ = seed >= 0 ? uint64_t(seed) : std::random_device()() ^ (uint64_t(std::random_device()()) << 32);
+  rng_.seed(seed_);
+  success_.assign(size_t(nb_), 0);
+  tries_.assign(size_t(nb_), 0);
+  values_.assign(size_t(nb_), 0.0);
+  a_.assign(size_t(nb_), 1.0);
+  b_.assign(size_t(nb_), 1.0);
+  if (best_branch >= 0 && best_branch < nb_) best_ = best_branch;
+  else best_ = int(rng_() % uint64_t(nb_));  // EpsilonGreedy: random starting branch
+  std::lock_guard<std::mutex> g(mu_);
+  publish();
+}
+
+void BanditModel::publish() {
+  host_state_.best = best_;
+  for (int i = 0; i < nb_; ++i) {
+    host_state_.alpha[i] = float(a_[size_t(i)]);
+    host_state_.beta[i] = float(b_[size_t(i)]);
+  }
+  if (state_.bytes()) memcpy(state_.host<State>(), &host_state_, sizeof(State));
+}
+
+void BanditModel::to_device(int) {
+  std::lock_guard<std::mutex> g(mu_);
+  state_.alloc(sizeof(State));
+  publish();
+}
+
+void BanditModel::launch(const double*, int rows, int, double* out, void*, hipStream_t s) {
+  const uint64_t off = offset_.fetch_add(uint64_t(rows));
+  State* st = state_.dev<State>();
+  if (kind_ == kEpsilonGreedy)
+    kern::eg_route(&st->best, nb_, eps_, seed_, off, rows, out, s);
+  else
+    kern::ts_route(st->alpha, st->beta, nb_, seed_, off, rows, out, s);
+}
+
+void BanditModel::run_cpu(const double*, int rows, int, double* out) const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  for (int r = 0; r < rows; ++r) {
+    if (kind_ == kEpsilonGreedy) {
+      int pick = best_;
+      if (nb_ > 1 && !(U(rng_) > eps_)) {
+        int other = int(rng_() % uint64_t(nb_ - 1));
+        if (other >= best_) ++other;
+        pick = other;
+      }
+      out[r] = pick;
+    } else {
+      double best = -1;
+      int pick = 0;
+      for (int i = 0; i < nb_; ++i) {
+        std::gamma_distribution<double> ga(a_[size_t(i)], 1.0), gb(b_[size_t(i)], 1.0);
+        const double x = ga(rng_), y = gb(rng_);
+        const double v = x / (x + y);
+        if (v > best) { best = v; pick = i; }
+      }
+      out[r] = pick;
+    }
+  }
+}
+
+void BanditModel::feedback(int routing, int n_success, int n_failures) {
+  if (routing < 0 || routing >= nb_) throw std::runtime_error("bandit feedback: invalid routing " + std::to_string(routing));
+  std::lock_guard<std::mutex> g(mu_);
+  success_[size_t(routing)] += n_success;
+  tries_[size_t(routing)] += n_success + n_failures;
+  if (kind_ == kEpsilonGreedy) {
+    if (tries_[size_t(routing)] > 0)
+      values_[size_t(routing)] = double(success_[size_t(routing)]) / double(tries_[size_t(routing)]);
+    double mx = values_[0];
+    for (double v : values_) mx = std::max(mx, v);
+    std::vector<int> ties;
+    for (int i = 0; i < nb_; ++i)
+      if (values_[size_t(i)] == mx) ties.push_back(i);
+    best_ = ties[size_t(rng_() % ties.size())];  // break ties randomly
+  } else {
+    a_[size_t(routing)] += n_success;
+    b_[size_t(routing)] += n_failures;
+  }
+  publish();
+}
+
+std::vector<double> BanditModel::values() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return values_;
+}
+
+int BanditModel::best_branch() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return best_;
+}
+
+std::string BanditModel::snapshot() const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::ostringstream o;
+  o.precision(17);
+  o << "{\"kind\":" << int(kind_) << ",\"best\":" << best_ << ",\"offset\":" << offset_.load() << ",\"success\":[";
+  for (int i = 0; i < nb_; ++i) o << (i ? "," : "") << success_[size_t(i)];
+  o << "],\"tries\":[";
+  for (int i = 0; i < nb_; ++i) o << (i ? "," : "") << tries_[size_t(i)];
+  o << "],\"values\":[";
+  for (int i = 0; i < nb_; ++i) o << (i ? "," : "") << values_[size_t(i)];
+  o << "],\"alpha\":[";
+  for (int i = 0; i < nb_; ++i) o << (i ? "," : "") << a_[size_t(i)];
+  o << "],\"beta\":[";
+  for (int i = 0; i < nb_; ++i) o << (i ? "," : "") << b_[size_t(i)];
+  o << "]}";
+  return o.str();
+}
+
+void BanditModel::restore(const std::string& s) {
+  Json j = parse_json(s);
+  auto arr = [&](const char* k, auto& dst) {
+    const Json* a = j.find(k);
+    if (!a || !a->is_array() || int(a->items().size()) != nb_) throw std::runtime_error(std::string("bad router snapshot field ") + k);
+    using T = std::remove_reference_t<decltype(dst[0])>;
+    for (int i = 0; i < nb_; ++i) dst[size_t(i)] = T(a->items()[size_t(i)].as_number());
+  };
+  std::lock_guard<std::mutex> g(mu_);
+  arr("success", success_);
+  arr("tries", tries_);
+  arr("values", values_);
+  arr("alpha", a_);
+  arr("beta", b_);
+  if (const Json* b = j.find("best")) best_ = int(b->as_number());
+  if (const Json* o = j.find("offset")) offset_.store(uint64_t(o->as_number()));
+  publish();
+}
+
+// ------------------------------------------------------------------ unit
+BanditRouterUnit::BanditRouterUnit(std::shared_ptr<BanditModel> model, BatcherOptions opts)
+    : model_(std::move(model)), opts_(opts) {
+  batched_ = std::make_shared<BatchedUnit>(model_, opts_);
+}
+
+void BanditRouterUnit::route(const CallCtx& c, MsgPtr, Done k) {
+  static thread_local MsgPtr probe = [] {
+    auto m = std::make_shared<SeldonMessage>();
+    m->payload = Payload::Data;
+    m->data.kind = DataKind::Tensor;
+    m->data.shape = {1, 1};
+    m->data.values = {0.0};
+    return m;
+  }();
+  batched_->transform_input(c, probe, [k](Outcome o) {
+    if (o.err) { k(std::move(o)); return; }
+    auto m = std::make_shared<SeldonMessage>();
+    m->payload = Payload::Data;
+    m->data.kind = DataKind::Tensor;
+    m->data.shape = {1, 1};
+    m->data.values = {o.msg->data.values.empty() ? 0.0 : o.msg->data.values[0]};
+    k(Outcome::ok(std::move(m)));
+  });
+}
+
+void BanditRouterUnit::send_feedback(const CallCtx& c, std::shared_ptr<const Feedback> fb, FbDone k) {
+  int32_t routing = -1;
+  if (!c.node || !fb->response.meta.routing_of(c.node->name, routing) || routing < 0) {
+    k(nullptr);  // not routed through this router (or routing unknown): nothing to learn
+    return;
+  }
+  int64_t n = 0;
+  if (fb->request.payload == Payload::Data) n = fb->request.data.rows();
+  const int n_success = int(double(fb->reward) * double(n));
+  try {
+    model_->feedback(routing, n_success, int(n) - n_success);
+  } catch (const std::exception& e) {
+    k(make_error(ApiError::INVALID_ROUTING, e.what()));
+    return;
+  }
+  k(nullptr);
+}
+
+}  // namespace sca::gpu

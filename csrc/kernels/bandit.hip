@@ -1,14 +1,15 @@
 // Device-side multi-armed-bandit routers (reference
 // components/routers/epsilon-greedy/EpsilonGreedy.py:87-106 and
 // components/routers/thompson-sampling/ThompsonSampling.py:78-91, which draw
-// one numpy random number per request on the CPU).
+// numpy random numbers on the CPU for every request).
 //
 // A micro-batch of n routing decisions is one launch: thread i owns request i
 // and a counter-based Philox4x32-10 stream (seed, offset + i), so decisions are
-// reproducible and independent of how requests were batched.
+// reproducible and independent of how requests were grouped into batches.
+// Router state (best branch / Beta parameters) is read straight from
+// fine-grained pinned host memory that feedback updates, so no copy precedes
+// a launch.  Decisions are written as fp64 (the batcher's output format).
 #include <hip/hip_runtime.h>
-
-#include <cfloat>
 
 #include "kernels.h"
 
@@ -58,7 +59,7 @@ struct Philox {
     const float u1 = uniform(), u2 = uniform();
     return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
   }
-  // Marsaglia-Tsang gamma(alpha, 1); alpha < 1 boosted.
+  // Marsaglia-Tsang gamma(alpha, 1); alpha < 1 boosted by U^(1/alpha).
   __device__ float gamma(float alpha) {
     float boost = 1.0f;
     if (alpha < 1.0f) {
@@ -66,12 +67,13 @@ struct Philox {
       alpha += 1.0f;
     }
     const float d = alpha - 1.0f / 3.0f, c = rsqrtf(9.0f * d);
-    for (int it = 0; it < 64; ++it) {
+    for (int it = 0; it < 64; ++it) {  // bounded: acceptance rate > 95%
       float x, v;
+      int tries = 0;
       do {
         x = normal();
         v = 1.0f + c * x;
-      } while (v <= 0.0f);
+      } while (v <= 0.0f && ++tries < 64);
       v = v * v * v;
       const float u = uniform();
       if (u < 1.0f - 0.0331f * x * x * x * x) return d * v * boost;
@@ -81,33 +83,25 @@ struct Philox {
   }
 };
 
-__global__ void eg_route_kernel(const float* __restrict__ values, int nb, float eps, uint64_t seed, uint64_t offset,
-                                int n, int32_t* __restrict__ out) {
+// EpsilonGreedy.route: x > eps -> best branch, else uniform over the others.
+__global__ void eg_route_kernel(const int32_t* __restrict__ best, int nb, float eps, uint64_t seed, uint64_t offset,
+                                int n, double* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Philox rng(seed, offset + uint64_t(i));
-  // argmax with uniform random tie-breaking (EpsilonGreedy.py:132-136)
-  float best = -FLT_MAX;
-  int nbest = 0, pick = 0;
-  for (int b = 0; b < nb; ++b) {
-    const float v = values[b];
-    if (v > best) { best = v; nbest = 1; pick = b; }
-    else if (v == best) {
-      ++nbest;
-      if (rng.next() % uint32_t(nbest) == 0) pick = b;  // reservoir sample among ties
-    }
-  }
+  const int b = best[0];
+  int pick = b;
   if (nb > 1 && rng.uniform() <= eps) {
-    // random branch other than the best one
     int other = int(rng.next() % uint32_t(nb - 1));
-    if (other >= pick) ++other;
+    if (other >= b) ++other;
     pick = other;
   }
-  out[i] = pick;
+  out[i] = double(pick);
 }
 
+// ThompsonSampling.route: sample Beta(a_i, b_i) per branch, argmax.
 __global__ void ts_route_kernel(const float* __restrict__ alpha, const float* __restrict__ beta, int nb, uint64_t seed,
-                                uint64_t offset, int n, int32_t* __restrict__ out) {
+                                uint64_t offset, int n, double* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Philox rng(seed, offset + uint64_t(i));
@@ -119,20 +113,20 @@ __global__ void ts_route_kernel(const float* __restrict__ alpha, const float* __
     const float s = x / (x + y);
     if (s > best) { best = s; pick = b; }
   }
-  out[i] = pick;
+  out[i] = double(pick);
 }
 
 }  // namespace
 
-void eg_route(const float* values, int n_branches, float epsilon, uint64_t seed, uint64_t offset, int n,
-              int32_t* branch_out, hipStream_t s) {
+void eg_route(const int32_t* best_branch, int n_branches, float epsilon, uint64_t seed, uint64_t offset, int n,
+              double* branch_out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(eg_route_kernel, dim3((n + 255) / 256), dim3(256), 0, s, values, n_branches, epsilon, seed,
+  hipLaunchKernelGGL(eg_route_kernel, dim3((n + 255) / 256), dim3(256), 0, s, best_branch, n_branches, epsilon, seed,
                      offset, n, branch_out);
 }
 
 void ts_route(const float* alpha, const float* beta, int n_branches, uint64_t seed, uint64_t offset, int n,
-              int32_t* branch_out, hipStream_t s) {
+              double* branch_out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(ts_route_kernel, dim3((n + 255) / 256), dim3(256), 0, s, alpha, beta, n_branches, seed, offset,
                      n, branch_out);

@@ -80,12 +80,12 @@ void minmax_normalize_f64(const double* in, int64_t n, double* out, double* scra
 void mean_sigmoid_rows_f64(const double* in, int rows, int F, double threshold, double* out, hipStream_t stream);
 
 // ------------------------------------------------------------ bandits
-// Epsilon-greedy route for `n` requests given per-branch value estimates.
-// (components/routers/epsilon-greedy/EpsilonGreedy.py:87-106)
-void eg_route(const float* values, int n_branches, float epsilon, uint64_t seed, uint64_t offset, int n,
-              int32_t* branch_out, hipStream_t stream);
+// Epsilon-greedy route for `n` requests given the current best branch
+// (components/routers/epsilon-greedy/EpsilonGreedy.py:87-106).
+void eg_route(const int32_t* best_branch, int n_branches, float epsilon, uint64_t seed, uint64_t offset, int n,
+              double* branch_out, hipStream_t stream);
 // Thompson sampling: sample Beta(a_i, b_i), argmax (ThompsonSampling.py:78-91).
 void ts_route(const float* alpha, const float* beta, int n_branches, uint64_t seed, uint64_t offset, int n,
-              int32_t* branch_out, hipStream_t stream);
+              double* branch_out, hipStream_t stream);
 
 }  // namespace sca::kern

@@ -17,3 +17,6 @@ def register(name: str):
         return cls
 
     return deco
+
+
+from . import routers  # noqa: E402,F401  (registers EPSILON_GREEDY / THOMPSON_SAMPLING)

@@ -70,6 +70,7 @@ class Deployment:
                                     log_responses, False)
         self.units: Dict[str, Any] = {}
         self.batched: Dict[str, Any] = {}
+        self.native_units: Dict[str, Any] = {}
         for node, _ in iter_nodes(self.predictor["graph"]):
             self._bind(node)
         self.engine.finalize()
@@ -113,6 +114,17 @@ class Deployment:
                 obj.load()
         if isinstance(obj, self.C.RowModel):
             self.bind_row_model(node, obj)
+            return
+        if isinstance(obj, self.C.Unit):
+            self.engine.bind_unit(node["name"], obj)
+            self.units[node["name"]] = obj
+            return
+        native_unit = getattr(obj, "native_unit", None)
+        if callable(native_unit):
+            unit = native_unit(self._node_device(node))
+            self.engine.bind_unit(node["name"], unit)
+            self.units[node["name"]] = unit
+            self.native_units[node["name"]] = unit
             return
         gpu = getattr(obj, "row_model", None)
         if callable(gpu):
@@ -219,7 +231,7 @@ class Deployment:
         for s in self._servers:
             s.stop()
         self._servers = []
-        for u in self.batched.values():
+        for u in list(self.batched.values()) + list(self.native_units.values()):
             u.stop()
 
     def __enter__(self):

@@ -139,11 +139,12 @@ def test_minmax_and_mean_sigmoid(C_):
 
 def test_eg_route_statistics(C_):
     """|p(best) - (1 - eps)| small (components/routers/epsilon-greedy/test_EpsilonGreedy.py:21-25)."""
-    values = torch.tensor([0.1, 0.9, 0.3, 0.2], dtype=torch.float32, device=dev)
+    best = torch.tensor([1], dtype=torch.int32, device=dev)
     n = 200000
-    out = torch.empty(n, dtype=torch.int32, device=dev)
-    C_.kernels.eg_route(values.data_ptr(), 4, 0.1, 1234, 0, n, out.data_ptr(), _stream())
+    out = torch.empty(n, dtype=torch.float64, device=dev)
+    C_.kernels.eg_route(best.data_ptr(), 4, 0.1, 1234, 0, n, out.data_ptr(), _stream())
     torch.cuda.synchronize()
+    out = out.long()
     p_best = (out == 1).float().mean().item()
     assert abs(p_best - 0.9) < 0.01
     counts = torch.bincount(out.long(), minlength=4).float() / n
@@ -155,9 +156,10 @@ def test_ts_route_prefers_better_arm(C_):
     alpha = torch.tensor([2.0, 50.0, 5.0], dtype=torch.float32, device=dev)
     beta = torch.tensor([50.0, 2.0, 5.0], dtype=torch.float32, device=dev)
     n = 50000
-    out = torch.empty(n, dtype=torch.int32, device=dev)
+    out = torch.empty(n, dtype=torch.float64, device=dev)
     C_.kernels.ts_route(alpha.data_ptr(), beta.data_ptr(), 3, 99, 0, n, out.data_ptr(), _stream())
     torch.cuda.synchronize()
+    out = out.long()
     frac = torch.bincount(out.long(), minlength=3).float() / n
     # P(Beta(50,2) > Beta(5,5)) and > Beta(2,50) is ~1
     assert frac[1].item() > 0.99
