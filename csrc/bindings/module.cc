@@ -346,7 +346,7 @@ PYBIND11_MODULE(_C, m) {
                message_from_json(j, *msg);
                in.push_back(msg);
              }
-             Outcome o = wait_outcome([&](Done k) { e.call_node(node, Method(method), std::move(in), std::move(k)); });
+             Outcome o = wait_outcome([&](Done k) { e.call_node(node, method, std::move(in), std::move(k)); });
              return render(o);
            })
       .def("metrics_text", [](Engine& e) { return e.metrics().render(); })

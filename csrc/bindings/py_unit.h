@@ -27,6 +27,7 @@ class PyUnit : public Unit {
   std::string kind() const override { return "python"; }
 
   void transform_input(const CallCtx& c, MsgPtr in, Done k) override { call1("transform_input", c, in, std::move(k)); }
+  void predict(const CallCtx& c, MsgPtr in, Done k) override { call1("predict", c, in, std::move(k)); }
   void transform_output(const CallCtx& c, MsgPtr in, Done k) override { call1("transform_output", c, in, std::move(k)); }
   void route(const CallCtx& c, MsgPtr in, Done k) override { call1("route", c, in, std::move(k)); }
   void aggregate(const CallCtx& c, std::vector<MsgPtr> in, Done k) override {

@@ -215,6 +215,7 @@ Node* Engine::compile(const UnitSpec& u) {
   } else {
     n->methods = type_methods(u.type);
   }
+  n->is_model = u.has_type && u.type == UnitType::MODEL;
   n->model_labels = base_labels_;
   n->model_labels.push_back({"model_name", u.name.empty() ? "unknown" : u.name});
   n->model_labels.push_back({"model_image", u.image_name.empty() ? "unknown" : u.image_name});
@@ -328,7 +329,10 @@ void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
             if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
             after_input(n, std::move(input), std::move(o.msg), std::move(ctx), std::move(k));
           },
-          [&](Done kk) { n->unit->transform_input(cc, input, std::move(kk)); });
+          [&](Done kk) {
+            if (n->is_model) n->unit->predict(cc, input, std::move(kk));
+            else n->unit->transform_input(cc, input, std::move(kk));
+          });
 }
 
 void Engine::after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCtx> ctx, Done k) {
@@ -493,7 +497,7 @@ void Engine::feedback_node(Node* n, std::shared_ptr<const Feedback> fb, FbDone k
 }
 
 // ---------------------------------------------------------- direct node call
-void Engine::call_node(const std::string& name, Method m, std::vector<MsgPtr> in, Done k) {
+void Engine::call_node(const std::string& name, int method, std::vector<MsgPtr> in, Done k) {
   Node* n = nullptr;
   for (auto& x : nodes_)
     if (x->name == name) { n = x.get(); break; }
@@ -501,9 +505,19 @@ void Engine::call_node(const std::string& name, Method m, std::vector<MsgPtr> in
     k(Outcome::fail(make_error(ApiError::EXECUTION_FAILURE, "unknown node " + name)));
     return;
   }
+  if ((method != kPredictMethod && method != int(Method::SEND_FEEDBACK) && in.empty()) ||
+      (method == kPredictMethod && in.empty())) {
+    k(Outcome::fail(make_error(ApiError::INVALID_JSON, "missing request")));
+    return;
+  }
   static const std::string empty;
   CallCtx cc{n, in.empty() ? &empty : &in[0]->meta.puid};
+  const Method m = method == kPredictMethod ? Method::TRANSFORM_INPUT : Method(method);
   guarded(n->client_timer[int(m)], std::move(k), [&](Done kk) {
+    if (method == kPredictMethod) {
+      n->unit->predict(cc, in.at(0), std::move(kk));
+      return;
+    }
     switch (m) {
       case Method::TRANSFORM_INPUT: n->unit->transform_input(cc, in.at(0), std::move(kk)); break;
       case Method::TRANSFORM_OUTPUT: n->unit->transform_output(cc, in.at(0), std::move(kk)); break;

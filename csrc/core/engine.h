@@ -83,6 +83,9 @@ class Unit {
   // Return 0 to use the node's type/methods table.
   virtual uint32_t builtin_methods() const { return 0; }
   virtual void transform_input(const CallCtx& c, MsgPtr in, Done k) { (void)c; k(Outcome::ok(std::move(in))); }
+  // MODEL nodes: the reference calls the component's /predict for a MODEL's
+  // transform-input (InternalPredictionService.java:255-256).
+  virtual void predict(const CallCtx& c, MsgPtr in, Done k) { transform_input(c, std::move(in), std::move(k)); }
   virtual void transform_output(const CallCtx& c, MsgPtr in, Done k) { (void)c; k(Outcome::ok(std::move(in))); }
   virtual void route(const CallCtx& c, MsgPtr in, Done k) { (void)c; (void)in; k(Outcome::ok(nullptr)); }
   virtual void aggregate(const CallCtx& c, std::vector<MsgPtr> in, Done k) { (void)c; k(Outcome::ok(in.empty() ? nullptr : in[0])); }
@@ -101,6 +104,7 @@ struct Node {
   std::string image;
   uint32_t methods = 0;  // effective method mask
   bool builtin = false;
+  bool is_model = false;  // MODEL type: transform-input is the component's predict
   std::vector<Node*> children;
   UnitPtr unit;
   Labels model_labels;    // deployment/predictor/model tags for metrics
@@ -140,8 +144,10 @@ class Engine {
   void predict(MsgPtr request, Done k);
   void send_feedback(std::shared_ptr<Feedback> fb, FbDone k);
   // Reference "internal API" entry: call one node's method directly
-  // (microservice mode: /predict, /route, ...).  `method` as in Method.
-  void call_node(const std::string& node, Method m, std::vector<MsgPtr> in, Done k);
+  // (microservice mode: /predict, /route, ...).  `method` as in Method, or
+  // kPredictMethod for /predict.
+  static constexpr int kPredictMethod = 5;
+  void call_node(const std::string& node, int method, std::vector<MsgPtr> in, Done k);
 
   bool ready() const;
   std::string new_puid();

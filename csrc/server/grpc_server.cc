@@ -307,15 +307,16 @@ struct GrpcServer::Worker : std::enable_shared_from_this<GrpcServer::Worker> {
       eng.predict(msg, on_msg);
       return;
     }
-    Method m;
-    if (method == "Predict" || method == "TransformInput") m = Method::TRANSFORM_INPUT;
-    else if (method == "TransformOutput") m = Method::TRANSFORM_OUTPUT;
-    else if (method == "Route") m = Method::ROUTE;
-    else if (method == "Aggregate") m = Method::AGGREGATE;
+    int m;
+    if (method == "Predict") m = Engine::kPredictMethod;
+    else if (method == "TransformInput") m = int(Method::TRANSFORM_INPUT);
+    else if (method == "TransformOutput") m = int(Method::TRANSFORM_OUTPUT);
+    else if (method == "Route") m = int(Method::ROUTE);
+    else if (method == "Aggregate") m = int(Method::AGGREGATE);
     else { send_error(c, sid, kUnimplemented, "unknown method " + path); return; }
     if (service.rfind("/seldon.protos.", 0) != 0) { send_error(c, sid, kUnimplemented, "unknown service " + path); return; }
     std::vector<MsgPtr> in;
-    if (m == Method::AGGREGATE) {
+    if (m == int(Method::AGGREGATE)) {
       std::vector<SeldonMessage> list;
       if (!message_list_from_pb(pb, list)) { send_error(c, sid, kInvalidArgument, "invalid SeldonMessageList"); return; }
       for (auto& x : list) in.push_back(std::make_shared<SeldonMessage>(std::move(x)));

@@ -475,13 +475,14 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
         respond_now(c, 200, "application/json", srv->opts_.openapi_json.empty() ? "{}" : srv->opts_.openapi_json, rq.keep_alive);
         return;
       }
-      Method m;
+      int m = 0;
       bool internal = true;
-      if (p == "/predict" || p == "/transform-input") m = Method::TRANSFORM_INPUT;
-      else if (p == "/transform-output") m = Method::TRANSFORM_OUTPUT;
-      else if (p == "/route") m = Method::ROUTE;
-      else if (p == "/aggregate") m = Method::AGGREGATE;
-      else if (p == "/send-feedback") m = Method::SEND_FEEDBACK;
+      if (p == "/predict") m = Engine::kPredictMethod;
+      else if (p == "/transform-input") m = int(Method::TRANSFORM_INPUT);
+      else if (p == "/transform-output") m = int(Method::TRANSFORM_OUTPUT);
+      else if (p == "/route") m = int(Method::ROUTE);
+      else if (p == "/aggregate") m = int(Method::AGGREGATE);
+      else if (p == "/send-feedback") m = int(Method::SEND_FEEDBACK);
       else internal = false;
       if (internal) { internal_call(c, rq, m); return; }
     }
@@ -649,7 +650,7 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
     });
   }
 
-  void internal_call(Conn* c, const Request& rq, Method m) {
+  void internal_call(Conn* c, const Request& rq, int m) {
     std::string text, err;
     auto bad = [&](const std::string& info) {
       std::string body = "{\"status\":{\"status\":1,\"info\":";
@@ -671,7 +672,7 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
     };
     try {
       Json j = parse_json(text);
-      if (m == Method::SEND_FEEDBACK) {
+      if (m == int(Method::SEND_FEEDBACK)) {
         auto fb = std::make_shared<Feedback>();
         feedback_from_json(j, *fb);
         c->busy = true;
@@ -685,7 +686,7 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
         return;
       }
       std::vector<MsgPtr> in;
-      if (m == Method::AGGREGATE) {
+      if (m == int(Method::AGGREGATE)) {
         std::vector<SeldonMessage> list;
         message_list_from_json(j, list);
         for (auto& x : list) in.push_back(std::make_shared<SeldonMessage>(std::move(x)));

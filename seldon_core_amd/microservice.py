@@ -1,0 +1,180 @@
+"""``seldon-core-microservice``-compatible launcher (reference
+python/seldon_core/microservice.py:177-322).
+
+    python -m seldon_core_amd.microservice <Interface> REST|GRPC \
+        [--service-type MODEL|ROUTER|TRANSFORMER|COMBINER|OUTLIER_DETECTOR] \
+        [--persistence] [--parameters '<json list>'] [--log-level INFO] \
+        [--tracing] [--workers N]
+
+The user class is imported exactly as the reference does (``Module`` ->
+``Module.Module``, ``pkg.mod.Class`` -> ``pkg.mod.Class``), built from the
+typed ``PREDICTIVE_UNIT_PARAMETERS`` and served by the native HTTP/1.1 server
+(internal API: /predict /transform-input /transform-output /route /aggregate
+/send-feedback /seldon.json, plus /ping /ready /live /prometheus) or the native
+gRPC server (Generic / Model / Router / Transformer / OutputTransformer /
+Combiner services) on ``PREDICTIVE_UNIT_SERVICE_PORT`` (default 5000).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import logging
+import os
+import signal
+import sys
+import threading
+import time
+from typing import Any, Dict, List
+
+logger = logging.getLogger(__name__)
+
+PARAMETERS_ENV_NAME = "PREDICTIVE_UNIT_PARAMETERS"
+SERVICE_PORT_ENV_NAME = "PREDICTIVE_UNIT_SERVICE_PORT"
+LOG_LEVEL_ENV = "SELDON_LOG_LEVEL"
+DEFAULT_PORT = 5000
+ANNOTATIONS_FILE = "/etc/podinfo/annotations"
+
+SERVICE_TO_NODE_TYPE = {"MODEL": "MODEL", "ROUTER": "ROUTER", "TRANSFORMER": "TRANSFORMER",
+                        "COMBINER": "COMBINER", "OUTLIER_DETECTOR": "TRANSFORMER"}
+
+
+def parse_parameters(parameters: List[Dict]) -> Dict[str, Any]:
+    casts = {"INT": int, "FLOAT": float, "DOUBLE": float, "STRING": str,
+             "BOOL": lambda v: str(v).lower() in ("1", "true")}
+    out = {}
+    for p in parameters:
+        t = p.get("type", "STRING")
+        if t not in casts:
+            raise ValueError(f"Bad parameter type {t} for {p.get('name')}")
+        try:
+            out[p["name"]] = casts[t](p["value"])
+        except ValueError as e:
+            raise ValueError(f"Bad value {p['value']!r} for {t} parameter {p['name']}") from e
+    return out
+
+
+def load_annotations(path: str = ANNOTATIONS_FILE) -> Dict[str, str]:
+    """Downward-API annotations file: ``key="value"`` per line."""
+    out: Dict[str, str] = {}
+    try:
+        with open(path) as f:
+            for line in f:
+                line = line.strip()
+                if "=" not in line:
+                    continue
+                k, v = line.split("=", 1)
+                out[k] = v.strip().strip('"')
+    except OSError:
+        pass
+    return out
+
+
+def import_user_class(interface_name: str):
+    parts = interface_name.rsplit(".", 1)
+    if len(parts) == 1:
+        mod = importlib.import_module(interface_name)
+        return getattr(mod, interface_name)
+    mod = importlib.import_module(parts[0])
+    return getattr(mod, parts[1])
+
+
+def build_microservice(user_object: Any, service_type: str = "MODEL", name: str = None, device: int = None):
+    """A one-node deployment wrapping the component (graph-equivalent)."""
+    from .serving.deployment import Deployment
+
+    name = name or os.environ.get("PREDICTIVE_UNIT_ID", "model")
+    node_type = SERVICE_TO_NODE_TYPE.get(service_type, "MODEL")
+    spec = {"name": os.environ.get("PREDICTOR_ID", "microservice"),
+            "graph": {"name": name, "type": node_type, "children": []}}
+    if node_type == "ROUTER":  # a router needs children to be a valid graph node type; keep methods explicit
+        spec["graph"] = {"name": name, "type": "UNKNOWN_TYPE", "methods": ["ROUTE", "SEND_FEEDBACK"]}
+    elif node_type == "COMBINER":
+        spec["graph"] = {"name": name, "type": "UNKNOWN_TYPE", "methods": ["AGGREGATE"]}
+    return Deployment(spec, components={name: user_object}, device=device)
+
+
+def main(argv=None) -> None:
+    logging.basicConfig(level=logging.INFO,
+                        format="%(asctime)s - %(name)s:%(funcName)s:%(lineno)s - %(levelname)s:  %(message)s")
+    sys.path.append(os.getcwd())
+    ap = argparse.ArgumentParser(prog="seldon-core-microservice")
+    ap.add_argument("interface_name", type=str)
+    ap.add_argument("api_type", type=str, choices=["REST", "GRPC", "FBS"])
+    ap.add_argument("--service-type", type=str, default="MODEL",
+                    choices=["MODEL", "ROUTER", "TRANSFORMER", "COMBINER", "OUTLIER_DETECTOR"])
+    ap.add_argument("--persistence", nargs="?", default=0, const=1, type=int)
+    ap.add_argument("--parameters", type=str, default=os.environ.get(PARAMETERS_ENV_NAME, "[]"))
+    ap.add_argument("--log-level", type=str, default="INFO")
+    ap.add_argument("--tracing", nargs="?", default=int(os.environ.get("TRACING", "0")), const=1, type=int)
+    ap.add_argument("--workers", type=int, default=int(os.environ.get("GUNICORN_WORKERS", "4")),
+                    help="native front-end I/O threads")
+    ap.add_argument("--port", type=int, default=int(os.environ.get(SERVICE_PORT_ENV_NAME, DEFAULT_PORT)))
+    ap.add_argument("--device", type=int, default=None, help="GPU for native units (-1 = CPU)")
+    args = ap.parse_args(argv)
+
+    level = getattr(logging, os.environ.get(LOG_LEVEL_ENV, args.log_level.upper()), None)
+    if not isinstance(level, int):
+        raise ValueError(f"Invalid log level: {args.log_level}")
+    logging.getLogger().setLevel(level)
+    if args.api_type == "FBS":
+        raise SystemExit("FBS (FlatBuffers) API is not supported (vestigial in the reference too)")
+
+    parameters = parse_parameters(json.loads(args.parameters))
+    annotations = load_annotations()
+    logger.info("Annotations: %s", annotations)
+    user_class = import_user_class(args.interface_name)
+    persister = None
+    if args.persistence:
+        from .utils import persistence
+
+        user_object = persistence.restore(user_class, parameters)
+        persister = persistence.persist(user_object, parameters.get("push_frequency"))
+    else:
+        user_object = user_class(**parameters)
+    try:
+        user_object.load()
+    except (NotImplementedError, AttributeError):
+        pass
+    if args.tracing:
+        from .utils.tracing import configure_tracing
+
+        configure_tracing(args.interface_name)
+
+    dep = build_microservice(user_object, args.service_type, device=args.device)
+    node = dep.predictor["graph"]["name"]
+    from .serving.openapi import wrapper_spec_json
+
+    if args.api_type == "REST":
+        http = dep.C.HttpServer(dep.engine, "0.0.0.0", [args.port], args.workers, node, True, wrapper_spec_json())
+        http.start()
+        servers = [http]
+        logger.info("REST microservice running on port %i", http.ports[0])
+    else:
+        max_msg = int(annotations.get("seldon.io/grpc-max-message-size", 64 << 20))
+        grpc = dep.C.GrpcServer(dep.engine, "0.0.0.0", args.port, args.workers, node, max_msg)
+        grpc.start()
+        servers = [grpc]
+        logger.info("GRPC microservice running on port %i", grpc.port)
+    if callable(getattr(user_object, "custom_service", None)):
+        threading.Thread(target=user_object.custom_service, daemon=True).start()
+
+    stop = threading.Event()
+
+    def _term(*_):
+        stop.set()
+
+    signal.signal(signal.SIGTERM, _term)
+    signal.signal(signal.SIGINT, _term)
+    while not stop.is_set():
+        time.sleep(0.5)
+    for s in servers:
+        s.stop()
+    if persister is not None:
+        persister.push()
+        persister.stop()
+    dep.close()
+
+
+if __name__ == "__main__":
+    main()

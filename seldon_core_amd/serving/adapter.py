@@ -33,13 +33,11 @@ class PythonUnit:
         with self._lock:
             return fn(*args)
 
+    def predict(self, text: str, node: str) -> str:
+        return dumps(self._run(dispatch.predict, self.user_model, json.loads(text)))
+
     def transform_input(self, text: str, node: str) -> str:
-        req = json.loads(text)
-        if self.unit_type == "MODEL":
-            out = self._run(dispatch.predict, self.user_model, req)
-        else:
-            out = self._run(dispatch.transform_input, self.user_model, req)
-        return dumps(out)
+        return dumps(self._run(dispatch.transform_input, self.user_model, json.loads(text)))
 
     def transform_output(self, text: str, node: str) -> str:
         return dumps(self._run(dispatch.transform_output, self.user_model, json.loads(text)))
