@@ -15,6 +15,7 @@
 #include "../kernels/kernels.h"
 #include "../server/grpc_server.h"
 #include "../server/http_server.h"
+#include "../server/remote_unit.h"
 #include "py_unit.h"
 
 namespace py = pybind11;
@@ -441,6 +442,36 @@ PYBIND11_MODULE(_C, m) {
                        uintptr_t s) {
     kern::ts_route(P<const float>(alpha), P<const float>(beta), nb, seed, offset, n, P<double>(out), as_stream(s));
   });
+
+  // ------------------------------------------------------------- remote nodes
+  py::class_<RemoteUnit, Unit, std::shared_ptr<RemoteUnit>>(m, "RemoteUnit")
+      .def(py::init([](const std::string& host, int port, bool grpc, const std::string& node_type,
+                       const std::string& model_name, const std::string& model_image, const std::string& model_version,
+                       int connect_timeout_ms, int read_timeout_ms, int retries, int threads) {
+             RemoteOptions o;
+             o.host = host;
+             o.port = port;
+             o.grpc = grpc;
+             o.node_type = node_type;
+             o.model_name = model_name;
+             o.model_image = model_image;
+             o.model_version = model_version;
+             o.connect_timeout_ms = connect_timeout_ms;
+             o.read_timeout_ms = read_timeout_ms;
+             o.retries = retries;
+             o.threads = threads;
+             return std::make_shared<RemoteUnit>(o);
+           }),
+           py::arg("host"), py::arg("port"), py::arg("grpc") = false, py::arg("node_type") = "MODEL",
+           py::arg("model_name") = "", py::arg("model_image") = "", py::arg("model_version") = "",
+           py::arg("connect_timeout_ms") = 200, py::arg("read_timeout_ms") = 5000, py::arg("retries") = 3,
+           py::arg("threads") = 8)
+      .def("ready", &RemoteUnit::ready)
+      .def("call_rest", [](RemoteUnit& u, const std::string& path, const std::string& body) {
+        py::gil_scoped_release nogil;
+        return u.call_rest(path, body);
+      })
+      .def("stop", [](RemoteUnit&) {});
 
   // ------------------------------------------------------------- routers
   py::class_<gpu::BanditModel, gpu::RowModel, std::shared_ptr<gpu::BanditModel>>(m, "BanditModel")

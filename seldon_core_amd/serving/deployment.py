@@ -172,7 +172,31 @@ class Deployment:
                 obj.load()
             self._bind_object(node, obj)
             return
+        ep = node.get("endpoint") or {}
+        host = ep.get("service_host") or ep.get("serviceHost")
+        port = ep.get("service_port") or ep.get("servicePort")
+        if host and port:
+            self.bind_remote(node, host, int(port), ep.get("type", "REST") == "GRPC", c)
+            return
         raise SpecError([f"no implementation for graph node '{name}' ({impl}); pass components={{'{name}': ...}}"])
+
+    def annotations(self) -> Dict[str, str]:
+        ann = dict((self.sdep.get("spec") or {}).get("annotations") or {})
+        ann.update(self.predictor.get("annotations") or {})
+        return ann
+
+    def bind_remote(self, node: Dict, host: str, port: int, grpc: bool, container: Optional[Dict] = None) -> None:
+        """Out-of-process microservice node (reference InternalPredictionService)."""
+        ann = self.annotations()
+        image = (container or {}).get("image", "")
+        img_name, _, img_ver = image.rpartition(":") if ":" in image else (image, "", "")
+        unit = self.C.RemoteUnit(
+            host, port, grpc, node.get("type", "MODEL"), node["name"], img_name, img_ver,
+            int(ann.get("seldon.io/rest-connection-timeout", 200)),
+            int(ann.get("seldon.io/grpc-read-timeout" if grpc else "seldon.io/rest-read-timeout", 5000)),
+            int(ann.get("seldon.io/rest-connect-retries", 3)))
+        self.engine.bind_unit(node["name"], unit)
+        self.units[node["name"]] = unit
 
     # ----------------------------------------------------------- requests
     def predict(self, payload: Union[Dict, str]) -> Dict:

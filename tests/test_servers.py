@@ -271,3 +271,43 @@ def test_microservice_cli_subprocess(tmp_path):
     finally:
         p.terminate()
         p.wait(timeout=20)
+
+
+@pytest.mark.parametrize("proto", ["REST", "GRPC"])
+def test_remote_microservice_node(proto):
+    """A graph node served by an out-of-process microservice (REST or gRPC)."""
+    from seldon_core_amd.microservice import build_microservice
+
+    class Doubler:
+        def predict(self, X, names):
+            return X * 2
+
+    md = build_microservice(Doubler(), "MODEL", name="remote", device=-1)
+    if proto == "REST":
+        srv = md.C.HttpServer(md.engine, "127.0.0.1", [0], 2, "remote", True, "")
+        srv.start()
+        port = srv.ports[0]
+    else:
+        srv = md.C.GrpcServer(md.engine, "127.0.0.1", 0, 2, "remote")
+        srv.start()
+        port = srv.port
+    try:
+        spec = {"name": "p", "componentSpecs": [{"spec": {"containers": [{"name": "remote", "image": "me/doubler:1.2"}]}}],
+                "graph": {"name": "t", "implementation": "SIMPLE_ROUTER", "children": [
+                    {"name": "remote", "type": "MODEL",
+                     "endpoint": {"type": proto, "service_host": "127.0.0.1", "service_port": port}}]}}
+        d = sca.Deployment(spec, device=-1)
+        out = d.predict({"data": {"ndarray": [[1.5, 2.0]]}})
+        assert out["data"]["ndarray"] == [[3.0, 4.0]]
+        assert out["meta"]["requestPath"] == {"t": "", "remote": "me/doubler:1.2"}
+        assert d.engine.unit_kind("remote").startswith(proto.lower())
+        import time
+        for _ in range(100):
+            if d.ready():
+                break
+            time.sleep(0.05)
+        assert d.ready()
+        d.close()
+    finally:
+        srv.stop()
+        md.close()
