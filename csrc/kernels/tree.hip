@@ -173,16 +173,29 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
 
 constexpr int kMaxGroups = 64;
 
+// Block = RB rows x (blockDim / RB) chunk-lanes: the lanes of a row sum a
+// strided subset of the tree chunks (independent, coalesced slab loads), fold
+// through LDS, and lane 0 applies the objective transform.
 __global__ __launch_bounds__(kBlock) void reduce_transform(const float* __restrict__ partial, int rows, int n_chunks,
                                                            const int* __restrict__ chunk_group, int groups,
                                                            const float* __restrict__ base_margin, float scale,
-                                                           int transform, double* __restrict__ out, int out_cols) {
-  extern __shared__ __attribute__((aligned(16))) double m_lds[];
-  const int r = blockIdx.x * kBlock + threadIdx.x;
-  if (r >= rows) return;
-  double* m = m_lds + size_t(threadIdx.x) * groups;
-  for (int g = 0; g < groups; ++g) m[g] = 0.0;
-  for (int c = 0; c < n_chunks; ++c) m[chunk_group[c]] += double(partial[size_t(c) * rows + r]);
+                                                           int transform, double* __restrict__ out, int out_cols,
+                                                           int RB) {
+  extern __shared__ __attribute__((aligned(16))) double m_lds[];  // [blockDim][groups]
+  const int nthr = int(blockDim.x);
+  const int r_local = int(threadIdx.x) % RB, slot = int(threadIdx.x) / RB, tpr = nthr / RB;
+  const int r = int(blockIdx.x) * RB + r_local;
+  double* acc = m_lds + size_t(threadIdx.x) * groups;
+  for (int g = 0; g < groups; ++g) acc[g] = 0.0;
+  if (r < rows)
+    for (int c = slot; c < n_chunks; c += tpr) acc[chunk_group[c]] += double(partial[size_t(c) * rows + r]);
+  __syncthreads();
+  if (slot != 0 || r >= rows) return;
+  double* m = acc;
+  for (int s = 1; s < tpr; ++s) {
+    const double* o2 = m_lds + size_t(s * RB + r_local) * groups;
+    for (int g = 0; g < groups; ++g) m[g] += o2[g];
+  }
   for (int g = 0; g < groups; ++g) m[g] = m[g] * double(scale) + (base_margin ? double(base_margin[g]) : 0.0);
   double* o = out + size_t(r) * out_cols;
   switch (transform) {
@@ -255,9 +268,14 @@ void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_
                  const float* base_margin, float scale, int transform, double* out, int out_cols, hipStream_t s) {
   if (rows <= 0) return;
   if (groups > kMaxGroups) groups = kMaxGroups;
-  const size_t lds = size_t(kBlock) * groups * sizeof(double);
-  hipLaunchKernelGGL(reduce_transform, dim3((rows + kBlock - 1) / kBlock), dim3(kBlock), lds, s, partial, rows,
-                     n_chunks, chunk_group, groups, base_margin, scale, transform, out, out_cols);
+  // Keep LDS <= 64 KB per block: 256 threads up to 32 groups, 64 beyond.
+  const int nthr = groups > 32 ? 64 : kBlock;
+  int RB = 1;
+  while (RB < rows && RB < 64) RB <<= 1;
+  if (n_chunks <= 1) RB = nthr;  // nothing to split: one row per thread
+  const size_t lds = size_t(nthr) * groups * sizeof(double);
+  hipLaunchKernelGGL(reduce_transform, dim3((rows + RB - 1) / RB), dim3(nthr), lds, s, partial, rows, n_chunks,
+                     chunk_group, groups, base_margin, scale, transform, out, out_cols, RB);
 }
 
 }  // namespace sca::kern

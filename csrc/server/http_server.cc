@@ -451,7 +451,13 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
   }
 
   void handle(Conn* c, const Request& rq) {
-    const std::string_view p = rq.path;
+    std::string_view p = rq.path;
+    // Gateway-style paths (Ambassador/Istio prefix routing, reference
+    // operator/controllers/ambassador.go:81): /seldon/[<ns>/]<sdep>/api/...
+    if (p.rfind("/seldon/", 0) == 0) {
+      const size_t api = p.find("/api/");
+      if (api != std::string_view::npos) p = p.substr(api);
+    }
     Engine& eng = *srv->engine_;
     if (p == "/api/v0.1/predictions" || p == "/api/v1.0/predictions") { predict_external(c, rq); return; }
     if (p == "/api/v0.1/feedback" || p == "/api/v1.0/feedback") { feedback_external(c, rq); return; }
