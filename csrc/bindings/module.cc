@@ -10,6 +10,7 @@
 #include "../core/json.h"
 #include "../core/message.h"
 #include "../gpu/batcher.h"
+#include "../gpu/graph.h"
 #include "../gpu/models.h"
 #include "../gpu/router.h"
 #include "../kernels/kernels.h"
@@ -169,6 +170,27 @@ PYBIND11_MODULE(_C, m) {
               to_vec(W), to_vec(b), int(W.shape(0)), int(W.shape(1)), act));
         },
         py::arg("W"), py::arg("b"), py::arg("act"));
+  // stages: list of dicts {kind: "model"|"mean", model?, device, inputs: [int], node}
+  m.def("graph_model", [](py::list stages, int in_cols) {
+    std::vector<gpu::GraphStage> st;
+    for (auto h : stages) {
+      py::dict d = h.cast<py::dict>();
+      gpu::GraphStage s;
+      const std::string kind = d["kind"].cast<std::string>();
+      s.kind = kind == "mean" ? gpu::GraphStage::kMean : gpu::GraphStage::kModel;
+      if (s.kind == gpu::GraphStage::kModel) s.model = d["model"].cast<std::shared_ptr<gpu::RowModel>>();
+      s.device = d.contains("device") ? d["device"].cast<int>() : 0;
+      s.inputs = d["inputs"].cast<std::vector<int>>();
+      s.node = d.contains("node") ? d["node"].cast<std::string>() : std::string();
+      st.push_back(std::move(s));
+    }
+    return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::GraphModel>(std::move(st), in_cols));
+  }, py::arg("stages"), py::arg("in_cols") = 0);
+  m.def("graph_devices", [](std::shared_ptr<gpu::RowModel> m) {
+    auto g = std::dynamic_pointer_cast<gpu::GraphModel>(m);
+    if (!g) throw std::runtime_error("not a graph model");
+    return g->devices();
+  });
   m.def("mean_sigmoid_model", [](double thr) {
     return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MeanSigmoidModel>(thr));
   });
@@ -270,6 +292,14 @@ PYBIND11_MODULE(_C, m) {
       .def("bind_batched", [](Engine& e, const std::string& node,
                               std::shared_ptr<gpu::BatchedUnit> u) { e.bind(node, u); })
       .def("bind_unit", [](Engine& e, const std::string& node, std::shared_ptr<Unit> u) { e.bind(node, u); })
+      .def("bind_fused", [](Engine& e, const std::string& root, std::shared_ptr<Unit> u,
+                            const std::vector<std::string>& absorbed) { e.bind_fused(root, u, absorbed); })
+      .def("fused_nodes", [](const Engine& e, const std::string& n) {
+        std::vector<std::string> v;
+        if (const Node* nd = e.node(n))
+          for (const Node* f : nd->fused) v.push_back(f->name);
+        return v;
+      })
       .def("finalize", &Engine::finalize)
       .def("ready", &Engine::ready)
       .def("node_names", &Engine::node_names)

@@ -203,6 +203,7 @@ Node* Engine::compile(const UnitSpec& u) {
     n->unit = it->second;
   } else {
     n->unit = make_builtin_unit(u.implementation, u);
+    if (!n->unit && absorbed_.count(u.name)) n->unit = std::make_shared<Unit>();  // computed by a fused ancestor
     if (!n->unit)
       throw std::runtime_error("no implementation bound for graph node '" + u.name + "' (implementation " +
                                (u.implementation_name.empty() ? "UNKNOWN_IMPLEMENTATION" : u.implementation_name) + ")");
@@ -238,6 +239,30 @@ Node* Engine::compile(const UnitSpec& u) {
 void Engine::finalize() {
   if (root_) return;
   root_ = compile(spec_.graph);
+  for (const auto& f : fused_) {
+    Node* r = nullptr;
+    for (const auto& n : nodes_)
+      if (n->name == f.first) r = n.get();
+    if (!r) throw std::runtime_error("fused root '" + f.first + "' is not a graph node");
+    // Pre-order walk of the subtree; every absorbed node must be inside it.
+    std::vector<Node*> stack{r};
+    std::set<std::string> want(f.second.begin(), f.second.end());
+    while (!stack.empty()) {
+      Node* v = stack.back();
+      stack.pop_back();
+      r->fused.push_back(v);
+      want.erase(v->name);
+      for (auto it = v->children.rbegin(); it != v->children.rend(); ++it) stack.push_back(*it);
+    }
+    if (!want.empty()) throw std::runtime_error("fused node '" + *want.begin() + "' is not below '" + f.first + "'");
+  }
+}
+
+void Engine::bind_fused(const std::string& root, UnitPtr unit, const std::vector<std::string>& absorbed) {
+  if (root_) throw std::runtime_error("engine already finalized");
+  bound_[root] = std::move(unit);
+  fused_[root] = absorbed;
+  for (const auto& a : absorbed) absorbed_.insert(a);
 }
 
 std::vector<std::string> Engine::node_names() const {
@@ -311,12 +336,33 @@ void Engine::predict(MsgPtr req, Done k) {
 }
 
 void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
-  {
-    std::lock_guard<std::mutex> g(ctx->mu);
+  auto visit = [&ctx](const Node* v) {
     bool found = false;
     for (auto& kv : ctx->request_path)
-      if (kv.first == n->name) { kv.second = n->image; found = true; break; }
-    if (!found) ctx->request_path.emplace_back(n->name, n->image);
+      if (kv.first == v->name) { kv.second = v->image; found = true; break; }
+    if (!found) ctx->request_path.emplace_back(v->name, v->image);
+  };
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    visit(n);
+    // A fused device graph evaluates its whole subtree in one unit call; record
+    // the per-node meta the unfused walk would have produced.
+    for (const Node* f : n->fused) {
+      if (f != n) visit(f);
+      if (!f->children.empty()) ctx->routing.emplace_back(f->name, -1);
+    }
+  }
+  if (!n->fused.empty()) {
+    CallCtx cc{n, &ctx->puid};
+    guarded(n->client_timer[int(Method::TRANSFORM_INPUT)],
+            [this, n, input, ctx, k](Outcome o) mutable {
+              if (o.err) { k(std::move(o)); return; }
+              if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
+              add_metrics(n, *o.msg, ctx.get());
+              k(Outcome::ok(merge_meta(std::move(o.msg), {input.get()}, ctx->puid)));
+            },
+            [&](Done kk) { n->unit->transform_input(cc, input, std::move(kk)); });
+    return;
   }
   if (!n->has(Method::TRANSFORM_INPUT)) {
     after_input(n, input, input, std::move(ctx), std::move(k));

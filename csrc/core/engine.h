@@ -16,7 +16,9 @@
 
 #include <atomic>
 #include <functional>
+#include <map>
 #include <memory>
+#include <set>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -111,6 +113,7 @@ struct Node {
   Series* client_timer[5] = {};
   Series* fb_reward = nullptr;
   Series* fb_count = nullptr;
+  std::vector<Node*> fused;  // non-empty: this node evaluates the listed subtree (itself first)
   bool has(Method m) const { return methods & method_bit(m); }
 };
 
@@ -133,6 +136,10 @@ class Engine {
 
   // Bind an implementation to a node (before finalize()).
   void bind(const std::string& node, UnitPtr unit);
+  // Bind `unit` to evaluate the whole subtree rooted at `root` in one call
+  // (a device graph); `absorbed` are the subtree nodes it computes.  They keep
+  // their place in the graph for meta (requestPath/routing) and feedback.
+  void bind_fused(const std::string& root, UnitPtr unit, const std::vector<std::string>& absorbed);
   UnitPtr unit_of(const std::string& node) const;
   // Compile the graph. Throws std::runtime_error if a node is unbound.
   void finalize();
@@ -170,6 +177,8 @@ class Engine {
   EngineOptions opts_;
   MetricsRegistry metrics_;
   std::unordered_map<std::string, UnitPtr> bound_;
+  std::map<std::string, std::vector<std::string>> fused_;
+  std::set<std::string> absorbed_;
   std::vector<std::unique_ptr<Node>> nodes_;
   Node* root_ = nullptr;
   Labels base_labels_;

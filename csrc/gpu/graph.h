@@ -1,0 +1,73 @@
+// Device graph: a fused, device-resident sub-graph of row models.
+//
+// The reference evaluates every node of an inference graph as a separate
+// microservice hop (PredictiveUnitBean.java:112-197 -> InternalPredictionService
+// HTTP/gRPC call per node), serialising the SeldonMessage to JSON at every edge.
+// On MI355X a chain (TRANSFORMER -> MODEL -> OUTPUT_TRANSFORMER) or an ensemble
+// (COMBINER over N MODELs, possibly placed on different GPUs) whose nodes are all
+// row models runs as ONE micro-batched unit:
+//
+//   request rows -> [pinned host] -> stage 0 on GPU a -> stage 1 on GPU b ... ->
+//   mean-combine on GPU c -> [pinned host] -> responses
+//
+// Activations never leave HBM between stages.  Cross-GPU edges are direct xGMI
+// peer accesses (the consumer kernel reads the producer's HBM; peer access is
+// enabled between every pair of participating GPUs at to_device()), ordered by
+// cross-device events on per-slot streams, so a fan-out to K GPUs is K
+// concurrent kernels and a fan-in is one combine kernel gathering over xGMI.
+// Stages that do not feed the graph output (non-first children of a MODEL,
+// whose outputs the default aggregate discards) are pruned at build time.
+#pragma once
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "models.h"
+
+namespace sca::gpu {
+
+struct GraphStage {
+  enum Kind { kModel = 0, kMean = 1 };
+  int kind = kModel;
+  RowModelPtr model;        // kModel
+  int device = 0;           // GPU the stage runs on
+  std::vector<int> inputs;  // producer stage indices; -1 = graph input
+  std::string node;         // graph node name (diagnostics)
+};
+
+class GraphModel : public RowModel {
+ public:
+  // `stages` in topological order; the last stage is the graph output.
+  GraphModel(std::vector<GraphStage> stages, int in_cols);
+  ~GraphModel() override;
+  std::string name() const override { return "graph" + std::to_string(st_.size()); }
+  int in_cols() const override { return in_cols_; }
+  int out_cols(int in_cols) const override;
+  std::vector<std::string> class_names() const override;
+  void to_device(int device) override;
+  void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  void run_cpu(const double* X, int rows, int cols, double* out) const override;
+
+  const std::vector<GraphStage>& stages() const { return st_; }
+  std::vector<int> devices() const;
+  bool peer_direct() const { return peer_direct_; }
+
+ private:
+  struct Aux;  // per-caller-stream resources (one per batcher slot)
+  void stage_cols(int in_cols, std::vector<int>& cols) const;
+  std::vector<std::string> names_of(int stage) const;
+  Aux& aux_for(hipStream_t s, int rows, int cols);
+
+  std::vector<GraphStage> st_;
+  int in_cols_ = 0;
+  int root_device_ = -1;
+  bool peer_direct_ = true;
+  std::mutex mu_;
+  std::unordered_map<hipStream_t, std::unique_ptr<Aux>> aux_;
+};
+
+}  // namespace sca::gpu

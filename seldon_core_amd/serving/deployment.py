@@ -30,6 +30,7 @@ from typing import Any, Dict, Optional, Union
 from .._native import gpu_count, native
 from .adapter import PythonUnit
 from .errors import EngineError
+from ..parallel.device_graph import fusion_enabled
 from .spec import (BUILTIN_IMPLEMENTATIONS, PREPACKAGED_SERVERS, SpecError, container_for, iter_nodes,
                    load_spec, select_predictor, typed_parameters, validate)
 
@@ -51,7 +52,7 @@ class Deployment:
     def __init__(self, spec: Union[str, Dict, None] = None, components: Optional[Dict[str, Any]] = None,
                  predictor: Optional[str] = None, deployment_name: Optional[str] = None,
                  device: Optional[int] = None, batcher: Optional[Dict[str, Any]] = None,
-                 log_requests: bool = False, log_responses: bool = False):
+                 log_requests: bool = False, log_responses: bool = False, fuse: Optional[bool] = None):
         self.C = native()
         self.sdep = load_spec(spec)
         self.predictor = select_predictor(self.sdep, predictor)
@@ -72,8 +73,13 @@ class Deployment:
         self.units: Dict[str, Any] = {}
         self.batched: Dict[str, Any] = {}
         self.native_units: Dict[str, Any] = {}
+        self.fused: Dict[str, Any] = {}
+        self._row_models: Dict[str, Any] = {}
+        self._row_nodes: Dict[str, Dict] = {}
+        self.fuse = fuse if fuse is not None else fusion_enabled(self.annotations())
         for node, _ in iter_nodes(self.predictor["graph"]):
             self._bind(node)
+        self._bind_row_models()
         self.engine.finalize()
         self._servers = []
 
@@ -91,10 +97,38 @@ class Deployment:
         return opts
 
     def bind_row_model(self, node: Dict, row_model) -> None:
+        # Deferred: row models may fuse into a device graph (_bind_row_models).
+        self._row_models[node["name"]] = row_model
+        self._row_nodes[node["name"]] = node
+
+    def _bind_batched(self, node: Dict, row_model) -> None:
         unit = self.C.BatchedUnit(row_model, self._node_device(node), **self._batcher_opts(node))
         self.engine.bind_batched(node["name"], unit)
         self.batched[node["name"]] = unit
         self.units[node["name"]] = unit
+
+    def _bind_row_models(self) -> None:
+        from ..parallel import device_graph
+
+        done = set()
+        if self.fuse and self._row_models:
+            for fg in device_graph.plan(self.predictor["graph"], self._row_models, self.units, self._node_device):
+                try:
+                    gm = device_graph.build(self.C, fg)
+                except Exception as e:  # stage widths disagree: the engine reports it per request
+                    logger.info("device graph at %s not fused: %s", fg.root, e)
+                    continue
+                root = next(n for n, _ in iter_nodes(self.predictor["graph"]) if n["name"] == fg.root)
+                unit = self.C.BatchedUnit(gm, self._node_device(root), **self._batcher_opts(root))
+                self.engine.bind_fused(fg.root, unit, fg.absorbed)
+                self.batched[fg.root] = unit
+                self.units[fg.root] = unit
+                self.fused[fg.root] = fg
+                logger.info("device graph %s: %s", fg.root, device_graph.describe(fg))
+                done.update(fg.absorbed)
+        for name, rm in self._row_models.items():
+            if name not in done:
+                self._bind_batched(self._row_nodes[name], rm)
 
     def bind_python(self, node: Dict, obj: Any) -> None:
         unit_type = node.get("type", "MODEL")
