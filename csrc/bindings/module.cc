@@ -272,7 +272,8 @@ PYBIND11_MODULE(_C, m) {
   // ------------------------------------------------------------- engine
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
       .def(py::init([](const std::string& spec_json, const std::string& deployment_name, const std::string& predictor,
-                       bool log_requests, bool log_responses, bool log_feedback) {
+                       bool log_requests, bool log_responses, bool log_feedback,
+                       std::shared_ptr<Engine> share_metrics_with) {
              PredictorSpecC spec = spec_json.empty() ? default_predictor_spec()
                                                      : parse_predictor_spec(parse_json(spec_json), predictor);
              EngineOptions o;
@@ -280,10 +281,13 @@ PYBIND11_MODULE(_C, m) {
              o.log_requests = log_requests;
              o.log_responses = log_responses;
              o.log_feedback = log_feedback;
-             return std::make_shared<Engine>(std::move(spec), o);
+             return std::make_shared<Engine>(std::move(spec), o,
+                                             share_metrics_with ? share_metrics_with->metrics_ptr() : nullptr);
            }),
            py::arg("spec_json") = "", py::arg("deployment_name") = "None", py::arg("predictor") = "",
-           py::arg("log_requests") = false, py::arg("log_responses") = false, py::arg("log_feedback") = false)
+           py::arg("log_requests") = false, py::arg("log_responses") = false, py::arg("log_feedback") = false,
+           py::arg("share_metrics_with") = nullptr)
+      .def("set_traffic", &Engine::set_traffic, py::arg("self_weight"), py::arg("peers"), py::arg("shadows"))
       .def("bind_python",
            [](Engine& e, const std::string& node, py::object adapter, uint32_t builtin_methods) {
              e.bind(node, std::make_shared<PyUnit>(std::move(adapter), builtin_methods));

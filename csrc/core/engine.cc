@@ -172,7 +172,11 @@ struct Engine::ReqCtx {
   std::vector<std::pair<std::string, std::vector<Metric>>> metrics;
 };
 
-Engine::Engine(PredictorSpecC spec, EngineOptions opts) : spec_(std::move(spec)), opts_(std::move(opts)) {
+Engine::Engine(PredictorSpecC spec, EngineOptions opts, std::shared_ptr<MetricsRegistry> shared_metrics)
+    : spec_(std::move(spec)),
+      opts_(std::move(opts)),
+      metrics_owner_(shared_metrics ? std::move(shared_metrics) : std::make_shared<MetricsRegistry>()),
+      metrics_(*metrics_owner_) {
   std::string pname = spec_.name.empty() ? "unknown" : spec_.name;
   auto it = spec_.labels.find("version");
   std::string pver = (it == spec_.labels.end() || it->second.empty()) ? "unknown" : it->second;
@@ -279,6 +283,8 @@ const Node* Engine::node(const std::string& name) const {
 
 bool Engine::ready() const {
   if (!root_) return false;
+  for (const auto& p : peers_)
+    if (!p->ready()) return false;
   for (const auto& n : nodes_)
     if (!n->unit->ready()) return false;
   return true;
@@ -305,7 +311,55 @@ void Engine::add_metrics(Node* n, const SeldonMessage& m, ReqCtx* ctx) {
   ctx->metrics.emplace_back(n->name, m.meta.metrics);
 }
 
+// ------------------------------------------------------------ traffic split
+void Engine::set_traffic(int self_weight, std::vector<std::pair<std::shared_ptr<Engine>, int>> peers,
+                         std::vector<std::shared_ptr<Engine>> shadows) {
+  routes_.clear();
+  shadows_.clear();
+  peers_.clear();
+  route_total_ = 0;
+  if (self_weight > 0) { routes_.emplace_back(this, self_weight); route_total_ += self_weight; }
+  for (auto& p : peers) {
+    if (p.second > 0) { routes_.emplace_back(p.first.get(), p.second); route_total_ += p.second; }
+    peers_.push_back(std::move(p.first));
+  }
+  for (auto& s : shadows) {
+    shadows_.push_back(s.get());
+    peers_.push_back(std::move(s));
+  }
+  if (route_total_ <= 0) throw std::runtime_error("traffic weights must sum to a positive value");
+}
+
+namespace {
+uint32_t traffic_draw(int total) {
+  thread_local uint64_t x = 0x9E3779B97F4A7C15ULL ^ uint64_t(reinterpret_cast<uintptr_t>(&x));
+  x ^= x << 13;
+  x ^= x >> 7;
+  x ^= x << 17;
+  return uint32_t((x >> 11) % uint64_t(total));
+}
+}  // namespace
+
 void Engine::predict(MsgPtr req, Done k) {
+  if (routes_.empty() && shadows_.empty()) {
+    predict_local(std::move(req), std::move(k));
+    return;
+  }
+  for (Engine* s : shadows_) s->predict_local(std::make_shared<SeldonMessage>(*req), [](Outcome) {});
+  Engine* target = this;
+  if (routes_.size() > 1) {
+    int r = int(traffic_draw(route_total_));
+    for (const auto& rt : routes_) {
+      if (r < rt.second) { target = rt.first; break; }
+      r -= rt.second;
+    }
+  } else if (!routes_.empty()) {
+    target = routes_[0].first;
+  }
+  target->predict_local(std::move(req), std::move(k));
+}
+
+void Engine::predict_local(MsgPtr req, Done k) {
   if (!root_) {
     k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "graph not finalized")));
     return;
@@ -483,6 +537,36 @@ void Engine::fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> c
 
 // ----------------------------------------------------------------- feedback
 void Engine::send_feedback(std::shared_ptr<Feedback> fb, FbDone k) {
+  // The reference routes /feedback through the same weighted ingress mapping.
+  if (routes_.size() > 1) {
+    // Sticky when the response identifies its predictor: a node (name and
+    // image) in meta.requestPath that only one predictor has.
+    Engine* owner = nullptr;
+    for (const auto& kv : fb->response.meta.request_path) {
+      Engine* only = nullptr;
+      int hits = 0;
+      for (const auto& rt : routes_) {
+        const Node* nd = rt.first->node(kv.first);
+        if (nd && nd->image == kv.second) { only = rt.first; ++hits; }
+      }
+      if (hits == 1) { owner = only; break; }
+    }
+    if (!owner) {
+      int r = int(traffic_draw(route_total_));
+      for (const auto& rt : routes_) {
+        if (r < rt.second) { owner = rt.first; break; }
+        r -= rt.second;
+      }
+    }
+    if (owner) {
+      owner->send_feedback_local(std::move(fb), std::move(k));
+      return;
+    }
+  }
+  send_feedback_local(std::move(fb), std::move(k));
+}
+
+void Engine::send_feedback_local(std::shared_ptr<Feedback> fb, FbDone k) {
   if (!root_) {
     k(make_error(ApiError::UNAVAILABLE, "graph not finalized"));
     return;

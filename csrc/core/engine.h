@@ -127,11 +127,24 @@ struct EngineOptions {
 
 class Engine {
  public:
-  Engine(PredictorSpecC spec, EngineOptions opts);
+  // `shared_metrics`: registry shared with sibling predictors (one /prometheus).
+  Engine(PredictorSpecC spec, EngineOptions opts, std::shared_ptr<MetricsRegistry> shared_metrics = nullptr);
   ~Engine();
 
   const PredictorSpecC& spec() const { return spec_; }
   MetricsRegistry& metrics() { return metrics_; }
+  std::shared_ptr<MetricsRegistry> metrics_ptr() const { return metrics_owner_; }
+
+  // Split traffic between this predictor and sibling predictors by integer
+  // weight (PredictorSpec.traffic; reference: Istio/Ambassador route weights,
+  // seldondeployment_controller.go:180-215, ambassador.go:88) and mirror every
+  // request to `shadows` (ambassador.go:119-122), discarding their responses.
+  // `self_weight` is this predictor's own share.
+  void set_traffic(int self_weight, std::vector<std::pair<std::shared_ptr<Engine>, int>> peers,
+                   std::vector<std::shared_ptr<Engine>> shadows);
+  // Graph evaluation on THIS predictor (no traffic split).
+  void predict_local(MsgPtr request, Done k);
+  void send_feedback_local(std::shared_ptr<Feedback> fb, FbDone k);
   const EngineOptions& options() const { return opts_; }
 
   // Bind an implementation to a node (before finalize()).
@@ -175,7 +188,13 @@ class Engine {
 
   PredictorSpecC spec_;
   EngineOptions opts_;
-  MetricsRegistry metrics_;
+  std::shared_ptr<MetricsRegistry> metrics_owner_;
+  MetricsRegistry& metrics_;
+  // Traffic split across predictors (ingress weights / shadow).
+  std::vector<std::pair<Engine*, int>> routes_;
+  int route_total_ = 0;
+  std::vector<Engine*> shadows_;
+  std::vector<std::shared_ptr<Engine>> peers_;
   std::unordered_map<std::string, UnitPtr> bound_;
   std::map<std::string, std::vector<std::string>> fused_;
   std::set<std::string> absorbed_;

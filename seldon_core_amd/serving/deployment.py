@@ -31,8 +31,8 @@ from .._native import gpu_count, native
 from .adapter import PythonUnit
 from .errors import EngineError
 from ..parallel.device_graph import fusion_enabled
-from .spec import (BUILTIN_IMPLEMENTATIONS, PREPACKAGED_SERVERS, SpecError, container_for, iter_nodes,
-                   load_spec, select_predictor, typed_parameters, validate)
+from .spec import (BUILTIN_IMPLEMENTATIONS, PREPACKAGED_SERVERS, SpecError, container_for, is_shadow, iter_nodes,
+                   load_spec, predictors, select_predictor, typed_parameters, validate)
 
 logger = logging.getLogger(__name__)
 
@@ -52,11 +52,31 @@ class Deployment:
     def __init__(self, spec: Union[str, Dict, None] = None, components: Optional[Dict[str, Any]] = None,
                  predictor: Optional[str] = None, deployment_name: Optional[str] = None,
                  device: Optional[int] = None, batcher: Optional[Dict[str, Any]] = None,
-                 log_requests: bool = False, log_responses: bool = False, fuse: Optional[bool] = None):
+                 log_requests: bool = False, log_responses: bool = False, fuse: Optional[bool] = None,
+                 _metrics_from=None):
         self.C = native()
         self.sdep = load_spec(spec)
+        all_preds = predictors(self.sdep)
+        split = predictor is None and len(all_preds) > 1
+        if split:
+            # Traffic split across predictors: the first live predictor hosts the
+            # front end; the others are sibling engines sharing its metrics.
+            errs = [e for e in validate(self.sdep, bound=set(components or {})) if "Traffic" in e]
+            if errs:
+                raise SpecError(errs)
+            live = [p for p in all_preds if not is_shadow(p)]
+            if not live:
+                raise SpecError(["SeldonDeployment has only shadow predictors"])
+            predictor = live[0]["name"]
         self.predictor = select_predictor(self.sdep, predictor)
         self.components = dict(components or {})
+        pname = self.predictor.get("name", "")
+        for k in list(self.components):  # "predictor/node" keys target one predictor
+            if "/" in k:
+                p, _, n = k.partition("/")
+                obj = self.components.pop(k)
+                if p == pname:
+                    self.components[n] = obj
         self.deployment_name = deployment_name or os.environ.get("DEPLOYMENT_NAME", "None")
         if device is None:
             device = 0 if gpu_count() > 0 else -1
@@ -69,7 +89,7 @@ class Deployment:
         if errs:
             raise SpecError(errs)
         self.engine = self.C.Engine(json.dumps(self.predictor), self.deployment_name, "", log_requests,
-                                    log_responses, False)
+                                    log_responses, False, _metrics_from)
         self.units: Dict[str, Any] = {}
         self.batched: Dict[str, Any] = {}
         self.native_units: Dict[str, Any] = {}
@@ -82,6 +102,21 @@ class Deployment:
         self._bind_row_models()
         self.engine.finalize()
         self._servers = []
+        self.peers: Dict[str, "Deployment"] = {}
+        if split:
+            kw = dict(components=components, deployment_name=self.deployment_name, device=device, batcher=batcher,
+                      log_requests=log_requests, log_responses=log_responses, fuse=fuse, _metrics_from=self.engine)
+            routes, shadows = [], []
+            for p in all_preds:
+                if p["name"] == pname:
+                    continue
+                peer = Deployment(self.sdep, predictor=p["name"], **kw)
+                self.peers[p["name"]] = peer
+                if is_shadow(p):
+                    shadows.append(peer.engine)
+                else:
+                    routes.append((peer.engine, int(p.get("traffic", 0) or 0)))
+            self.engine.set_traffic(int(self.predictor.get("traffic", 0) or 0), routes, shadows)
 
     # ----------------------------------------------------------- binding
     def _node_device(self, node: Dict) -> int:
@@ -269,7 +304,10 @@ class Deployment:
         return bool(self.engine.ready())
 
     def batcher_stats(self) -> Dict[str, Dict]:
-        return {k: v.stats() for k, v in self.batched.items()}
+        out = {k: v.stats() for k, v in self.batched.items()}
+        for pn, p in getattr(self, "peers", {}).items():
+            out.update({f"{pn}/{k}": v for k, v in p.batcher_stats().items()})
+        return out
 
     # ----------------------------------------------------------- serving
     def serve(self, http_port: int = 8000, grpc_port: Optional[int] = 5001, admin_port: Optional[int] = None,
@@ -292,6 +330,8 @@ class Deployment:
         self._servers = []
         for u in list(self.batched.values()) + list(self.native_units.values()):
             u.stop()
+        for p in getattr(self, "peers", {}).values():
+            p.close()
 
     def __enter__(self):
         return self

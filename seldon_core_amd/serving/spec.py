@@ -81,6 +81,16 @@ def select_predictor(spec: Dict, name: Optional[str] = None) -> Dict:
     return preds[0]
 
 
+def is_shadow(predictor: Dict) -> bool:
+    """Shadow predictor: receives a mirrored copy of every request, its response
+    is discarded (reference ``seldon.io/ambassador-shadow``, ambassador.go:119-122;
+    here per predictor via ``shadow: true`` or that annotation)."""
+    if predictor.get("shadow") in (True, "true", "True"):
+        return True
+    ann = predictor.get("annotations") or {}
+    return str(ann.get("seldon.io/shadow", ann.get("seldon.io/ambassador-shadow", ""))).lower() in ("1", "true")
+
+
 def iter_nodes(graph: Dict, parent: Optional[Dict] = None) -> Iterator[Tuple[Dict, Optional[Dict]]]:
     yield graph, parent
     for c in graph.get("children", []) or []:
@@ -183,11 +193,12 @@ def validate(sdep: Dict, bound: Optional[set] = None) -> List[str]:
                     errors.append(f"spec.predictors[{i}].graph: Invalid value: \"{name}\": Predictive Unit has no implementation methods defined. Change to a know type or add what methods it defines")
             elif impl in PREPACKAGED_SERVERS and not node.get("modelUri"):
                 errors.append(f"spec.predictors[{i}].graph: Invalid value: \"{name}\": Predictive unit modelUri required when using standalone servers")
-    traffic = sum(int(p.get("traffic", 0) or 0) for p in preds)
+    live = [p for p in preds if not is_shadow(p)]
+    traffic = sum(int(p.get("traffic", 0) or 0) for p in live)
     name = sdep.get("metadata", {}).get("name", "")
-    if traffic != 100 and len(preds) > 1:
+    if traffic != 100 and len(live) > 1:
         errors.append(f"spec: Invalid value: \"{name}\": Traffic must sum to 100 for multiple predictors")
-    if 0 < traffic < 100 and len(preds) == 1:
+    if 0 < traffic < 100 and len(live) == 1:
         errors.append(f"spec: Invalid value: \"{name}\": Traffic must sum be 100 for a single predictor when set")
     return errors
 
