@@ -9,8 +9,10 @@
 #include "../core/engine.h"
 #include "../core/json.h"
 #include "../core/message.h"
+#include "../core/msglog.h"
 #include "../gpu/batcher.h"
 #include "../gpu/graph.h"
+#include "../gpu/replica.h"
 #include "../gpu/models.h"
 #include "../gpu/router.h"
 #include "../kernels/kernels.h"
@@ -154,6 +156,11 @@ PYBIND11_MODULE(_C, m) {
       .def("set_class_names", &gpu::RowModel::set_class_names)
       .def("class_names", &gpu::RowModel::class_names)
       .def_property("flat_output", &gpu::RowModel::flat_output, &gpu::RowModel::set_flat_output)
+      .def("clone", &gpu::RowModel::clone)
+      .def("clone_on", [](const gpu::RowModel& mdl, int device) {
+        auto* g = dynamic_cast<const gpu::GraphModel*>(&mdl);
+        return g ? g->clone_on(device) : mdl.clone();
+      })
       .def("run_cpu", [](const gpu::RowModel& mdl, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
         if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
         const int rows = int(X.shape(0)), cols = int(X.shape(1));
@@ -269,11 +276,44 @@ PYBIND11_MODULE(_C, m) {
         u.stop();
       });
 
+  py::class_<gpu::ReplicaUnit, Unit, std::shared_ptr<gpu::ReplicaUnit>>(m, "ReplicaUnit")
+      .def(py::init([](std::vector<std::shared_ptr<gpu::BatchedUnit>> reps) {
+        return std::make_shared<gpu::ReplicaUnit>(std::move(reps));
+      }))
+      .def_property_readonly("replicas", &gpu::ReplicaUnit::replicas)
+      .def("requests_per_replica", &gpu::ReplicaUnit::requests_per_replica)
+      .def("stats", [](const gpu::ReplicaUnit& u) {
+        py::dict d;
+        uint64_t b = 0, r = 0, q = 0, mx = 0;
+        double busy = 0;
+        for (const auto& rep : u.replicas()) {
+          auto s = rep->stats();
+          b += s.batches; r += s.rows; q += s.requests; busy += s.gpu_busy_s;
+          mx = std::max<uint64_t>(mx, s.max_rows);
+        }
+        d["batches"] = b;
+        d["rows"] = r;
+        d["requests"] = q;
+        d["max_rows"] = mx;
+        d["gpu_busy_s"] = busy;
+        d["per_replica"] = u.requests_per_replica();
+        return d;
+      })
+      .def("reset_stats", [](gpu::ReplicaUnit& u) {
+        for (auto& rep : u.replicas()) rep->reset_stats();
+      })
+      .def("stop", [](gpu::ReplicaUnit& u) {
+        py::gil_scoped_release nogil;
+        u.stop();
+      });
+
   // ------------------------------------------------------------- engine
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
       .def(py::init([](const std::string& spec_json, const std::string& deployment_name, const std::string& predictor,
                        bool log_requests, bool log_responses, bool log_feedback,
-                       std::shared_ptr<Engine> share_metrics_with) {
+                       std::shared_ptr<Engine> share_metrics_with, const std::string& logging_service,
+                       bool log_externally, const std::string& message_type, const std::string& dep_name_env,
+                       const std::string& dep_namespace) {
              PredictorSpecC spec = spec_json.empty() ? default_predictor_spec()
                                                      : parse_predictor_spec(parse_json(spec_json), predictor);
              EngineOptions o;
@@ -281,12 +321,31 @@ PYBIND11_MODULE(_C, m) {
              o.log_requests = log_requests;
              o.log_responses = log_responses;
              o.log_feedback = log_feedback;
+             o.message_logging_service = logging_service;
+             o.log_messages_externally = log_externally;
+             o.message_type = message_type;
+             o.deployment_name_env = dep_name_env;
+             o.deployment_namespace = dep_namespace;
              return std::make_shared<Engine>(std::move(spec), o,
                                              share_metrics_with ? share_metrics_with->metrics_ptr() : nullptr);
            }),
            py::arg("spec_json") = "", py::arg("deployment_name") = "None", py::arg("predictor") = "",
            py::arg("log_requests") = false, py::arg("log_responses") = false, py::arg("log_feedback") = false,
-           py::arg("share_metrics_with") = nullptr)
+           py::arg("share_metrics_with") = nullptr, py::arg("message_logging_service") = "",
+           py::arg("log_messages_externally") = false, py::arg("message_type") = "seldon.message.pair",
+           py::arg("deployment_name_env") = "", py::arg("deployment_namespace") = "")
+      .def("flush_message_log", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        if (auto* l = e.message_logger()) l->flush();
+      })
+      .def("message_log_stats", [](Engine& e) {
+        py::dict d;
+        auto* l = e.message_logger();
+        d["sent"] = l ? l->sent() : 0;
+        d["failed"] = l ? l->failed() : 0;
+        d["dropped"] = l ? l->dropped() : 0;
+        return d;
+      })
       .def("set_traffic", &Engine::set_traffic, py::arg("self_weight"), py::arg("peers"), py::arg("shadows"))
       .def("bind_python",
            [](Engine& e, const std::string& node, py::object adapter, uint32_t builtin_methods) {
@@ -305,6 +364,7 @@ PYBIND11_MODULE(_C, m) {
         return v;
       })
       .def("finalize", &Engine::finalize)
+      .def("inflight", &Engine::inflight)
       .def("ready", &Engine::ready)
       .def("node_names", &Engine::node_names)
       .def("unit_kind", [](const Engine& e, const std::string& n) {

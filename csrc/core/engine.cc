@@ -1,5 +1,7 @@
 #include "engine.h"
 
+#include "msglog.h"
+
 #include <chrono>
 #include <cstdio>
 #include <random>
@@ -181,6 +183,16 @@ Engine::Engine(PredictorSpecC spec, EngineOptions opts, std::shared_ptr<MetricsR
   auto it = spec_.labels.find("version");
   std::string pver = (it == spec_.labels.end() || it->second.empty()) ? "unknown" : it->second;
   base_labels_ = {{"deployment_name", opts_.deployment_name}, {"predictor_name", pname}, {"predictor_version", pver}};
+  MessageLogOptions lo;
+  lo.log_requests = opts_.log_requests;
+  lo.log_responses = opts_.log_responses;
+  lo.log_feedback = opts_.log_feedback;
+  lo.external = opts_.log_messages_externally && !opts_.message_logging_service.empty();
+  lo.url = opts_.message_logging_service;
+  lo.message_type = opts_.message_type;
+  lo.deployment_name = opts_.deployment_name_env;
+  lo.deployment_namespace = opts_.deployment_namespace;
+  if (lo.log_requests || lo.log_responses || lo.log_feedback || lo.external) msglog_ = std::make_shared<MessageLogger>(lo);
 }
 
 Engine::~Engine() = default;
@@ -341,6 +353,11 @@ uint32_t traffic_draw(int total) {
 }  // namespace
 
 void Engine::predict(MsgPtr req, Done k) {
+  inflight_.fetch_add(1, std::memory_order_relaxed);
+  k = [this, k = std::move(k)](Outcome o) {
+    k(std::move(o));
+    inflight_.fetch_sub(1, std::memory_order_release);
+  };
   if (routes_.empty() && shadows_.empty()) {
     predict_local(std::move(req), std::move(k));
     return;
@@ -372,8 +389,10 @@ void Engine::predict_local(MsgPtr req, Done k) {
   }
   auto ctx = std::make_shared<ReqCtx>();
   ctx->puid = req->meta.puid;
-  MsgPtr request_copy = (pair_hook_ ? req : nullptr);
-  eval(root_, req, ctx, [this, ctx, k = std::move(k), request_copy](Outcome o) {
+  const bool log_pair = msglog_ && msglog_->wants_pairs();
+  MsgPtr request_copy = (pair_hook_ || log_pair ? req : nullptr);
+  const auto t_req = log_pair ? std::chrono::system_clock::now() : std::chrono::system_clock::time_point();
+  eval(root_, req, ctx, [this, ctx, k = std::move(k), request_copy, t_req, log_pair](Outcome o) {
     if (o.err) { k(std::move(o)); return; }
     MsgPtr r = o.msg.use_count() == 1 ? std::move(o.msg) : std::make_shared<SeldonMessage>(*o.msg);
     {
@@ -385,6 +404,7 @@ void Engine::predict_local(MsgPtr req, Done k) {
     }
     r->meta.puid = ctx->puid;
     if (pair_hook_ && request_copy) pair_hook_(*request_copy, *r);
+    if (log_pair) msglog_->pair(request_copy, r, t_req);
     k(Outcome::ok(std::move(r)));
   });
 }
@@ -571,6 +591,7 @@ void Engine::send_feedback_local(std::shared_ptr<Feedback> fb, FbDone k) {
     k(make_error(ApiError::UNAVAILABLE, "graph not finalized"));
     return;
   }
+  if (msglog_ && msglog_->wants_feedback()) msglog_->feedback(fb);
   feedback_node(root_, std::move(fb), std::move(k));
 }
 

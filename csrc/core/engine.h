@@ -122,8 +122,14 @@ struct EngineOptions {
   bool log_requests = false;
   bool log_responses = false;
   bool log_feedback = false;
-  std::string message_logging_service;  // CloudEvents sink (empty = off)
+  std::string message_logging_service;  // CloudEvents sink (SELDON_MESSAGE_LOGGING_SERVICE)
+  bool log_messages_externally = false;  // SELDON_LOG_MESSAGES_EXTERNALLY
+  std::string message_type = "seldon.message.pair";
+  std::string deployment_name_env;       // DEPLOYMENT_NAME as set in the environment ("" = unset)
+  std::string deployment_namespace;      // DEPLOYMENT_NAMESPACE
 };
+
+class MessageLogger;
 
 class Engine {
  public:
@@ -171,6 +177,9 @@ class Engine {
 
   bool ready() const;
   std::string new_puid();
+  // Requests accepted by predict() and not yet answered (graceful drain).
+  int64_t inflight() const { return inflight_.load(std::memory_order_acquire); }
+  MessageLogger* message_logger() const { return msglog_.get(); }
 
   // Hook invoked after each completed prediction (request, response) — used
   // by the async request logger.  Called on the completing thread.
@@ -195,6 +204,8 @@ class Engine {
   int route_total_ = 0;
   std::vector<Engine*> shadows_;
   std::vector<std::shared_ptr<Engine>> peers_;
+  std::atomic<int64_t> inflight_{0};
+  std::shared_ptr<MessageLogger> msglog_;
   std::unordered_map<std::string, UnitPtr> bound_;
   std::map<std::string, std::vector<std::string>> fused_;
   std::set<std::string> absorbed_;

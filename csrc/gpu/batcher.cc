@@ -166,6 +166,7 @@ void BatchedUnit::transform_input(const CallCtx&, MsgPtr in, Done k) {
     it.k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "GPU unit stopped")));
     return;
   }
+  inflight_rows_.fetch_add(it.rows, std::memory_order_relaxed);
   {
     std::lock_guard<std::mutex> g(mu_);
     queued_rows_ += size_t(it.rows);
@@ -209,6 +210,7 @@ void BatchedUnit::submit_loop() {
     s->cols = cols;
     s->out_cols = model_->out_cols(cols);
     hipError_t err = hipSuccess;
+    std::string launch_error;
     try {
       ensure_capacity(*s, rows, cols);
       double* hin = s->h_in.host<double>();
@@ -230,11 +232,14 @@ void BatchedUnit::submit_loop() {
       }
       if (err == hipSuccess) err = hipGetLastError();
       if (err == hipSuccess) err = hipEventRecord(s->ev.get(), st);
-    } catch (const std::exception&) {
-      err = hipErrorOutOfMemory;
+    } catch (const std::exception& ex) {
+      err = hipErrorUnknown;
+      launch_error = ex.what();
     }
     if (err != hipSuccess) {
-      auto e = make_error(ApiError::EXECUTION_FAILURE, std::string("GPU launch failed: ") + hipGetErrorString(err));
+      auto e = make_error(ApiError::EXECUTION_FAILURE,
+                          "GPU launch failed: " + (launch_error.empty() ? std::string(hipGetErrorString(err)) : launch_error));
+      inflight_rows_.fetch_sub(rows, std::memory_order_relaxed);
       for (auto& it : s->items) it.k(Outcome::fail(e));
       s->items.clear();
       lk.lock();
@@ -269,6 +274,7 @@ void BatchedUnit::complete_loop(Slot* s) {
       st = hipEventSynchronize(s->ev.get());
     }
     const double busy = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    inflight_rows_.fetch_sub(s->rows, std::memory_order_relaxed);
     if (st != hipSuccess) {
       auto e = make_error(ApiError::EXECUTION_FAILURE, std::string("GPU execution failed: ") + hipGetErrorString(st));
       for (auto& it : s->items) it.k(Outcome::fail(e));

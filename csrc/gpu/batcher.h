@@ -61,6 +61,8 @@ class BatchedUnit : public Unit {
   BatcherStats stats() const;
   void reset_stats();
   const BatcherOptions& options() const { return opts_; }
+  // Rows queued or on the device (replica load balancing).
+  int64_t inflight_rows() const { return inflight_rows_.load(std::memory_order_relaxed); }
   RowModelPtr model() const { return model_; }
 
   // Synchronous dense call (tests / python ops): X [rows, cols] -> out.
@@ -106,6 +108,7 @@ class BatchedUnit : public Unit {
   std::deque<Item> queue_;
   size_t queued_rows_ = 0;
   std::atomic<bool> running_{false};
+  std::atomic<int64_t> inflight_rows_{0};
   std::thread submit_th_;
   std::vector<std::string> default_names_;
   mutable std::mutex stats_mu_;

@@ -70,6 +70,20 @@ void GraphModel::stage_cols(int in_cols, std::vector<int>& cols) const {
   }
 }
 
+std::shared_ptr<RowModel> GraphModel::clone_on(int device) const {
+  std::vector<GraphStage> st = st_;
+  std::map<const RowModel*, std::shared_ptr<RowModel>> copies;  // keep shared models shared
+  for (auto& s : st) {
+    if (device != -2) s.device = device;
+    if (s.kind != GraphStage::kModel) continue;
+    auto& c = copies[s.model.get()];
+    if (!c) c = s.model->clone();
+    s.model = c;
+  }
+  auto g = std::make_shared<GraphModel>(std::move(st), in_cols_);
+  return with_meta(g);
+}
+
 int GraphModel::out_cols(int in_cols) const {
   std::vector<int> cols;
   stage_cols(in_cols, cols);

@@ -52,6 +52,10 @@ class GraphModel : public RowModel {
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
 
+  std::shared_ptr<RowModel> clone() const override { return clone_on(-2); }
+  // Copy with every stage placed on `device` (-2: keep stage placement): one
+  // whole-graph replica per GPU for data-parallel serving.
+  std::shared_ptr<RowModel> clone_on(int device) const;
   const std::vector<GraphStage>& stages() const { return st_; }
   std::vector<int> devices() const;
   bool peer_direct() const { return peer_direct_; }

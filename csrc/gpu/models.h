@@ -9,6 +9,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -33,8 +34,16 @@ class RowModel {
   virtual size_t workspace_bytes(int max_rows, int cols) const { (void)max_rows; (void)cols; return 0; }
   virtual void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) = 0;
   virtual void run_cpu(const double* X, int rows, int cols, double* out) const = 0;
+  // Independent copy (host parameters only; call to_device on it) -- one per
+  // GPU replica.
+  virtual std::shared_ptr<RowModel> clone() const { throw std::runtime_error(name() + " cannot be replicated"); }
 
  protected:
+  template <class T> std::shared_ptr<RowModel> with_meta(std::shared_ptr<T> m) const {
+    m->names_ = names_;
+    m->flat_ = flat_;
+    return m;
+  }
   std::vector<std::string> names_;
   bool flat_ = false;
 };
@@ -50,6 +59,9 @@ class LinearModel : public RowModel {
   void to_device(int device) override;
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
+  std::shared_ptr<RowModel> clone() const override {
+    return with_meta(std::make_shared<LinearModel>(W_, b_, C_, K_, act_));
+  }
 
  private:
   std::vector<double> W_, b_;
@@ -90,6 +102,7 @@ class TreeEnsembleModel : public RowModel {
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
   const TreeEnsembleSpec& spec() const { return spec_; }
+  std::shared_ptr<RowModel> clone() const override { return with_meta(std::make_shared<TreeEnsembleModel>(spec_)); }
   // Launch geometry chosen for a batch (exposed for tests/benchmarks).
   void plan_for(int rows, int* rows_per_block, int* plan_index) const;
 
@@ -119,6 +132,7 @@ class MeanSigmoidModel : public RowModel {
   void to_device(int) override {}
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
+  std::shared_ptr<RowModel> clone() const override { return with_meta(std::make_shared<MeanSigmoidModel>(thr_)); }
 
  private:
   double thr_;

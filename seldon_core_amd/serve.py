@@ -1,0 +1,202 @@
+"""Engine entry point and one-process-per-GPU replica supervisor.
+
+    python -m seldon_core_amd.serve --spec sdep.json [--predictor NAME] \
+        [--http-port 8000] [--grpc-port 5001] [--admin-port 8082] [--threads 4] \
+        [--gpus 1|N|all] [--component node=module.Class ...] [--no-fuse]
+
+Replaces the reference's engine container (``engine/.../App.java``: boot, serve
+REST + gRPC, drain on shutdown) and the slice of the operator that keeps
+``replicas`` copies of it running (``operator/controllers/
+seldondeployment_controller.go:296-302,548-636``: Deployment replicas, rolling
+restarts, ``terminationGracePeriodSeconds`` 20, preStop ``/pause``).
+
+``--gpus N`` (N > 1) starts N worker processes, one per MI355X, each seeing
+only its own GPU (``HIP_VISIBLE_DEVICES``).  All workers bind the same REST and
+gRPC ports with ``SO_REUSEPORT``, so the kernel spreads connections across
+them -- the in-host equivalent of a Service over N pods, with no proxy hop.
+The supervisor never touches a GPU itself; it restarts a worker that dies
+(bounded restart rate) and, on SIGTERM/SIGINT, forwards SIGTERM so every
+worker drains: readiness off, wait for in-flight requests, stop.
+
+Configuration precedence: defaults < ``/etc/podinfo/annotations`` < spec
+annotations < environment (``ENGINE_SERVER_PORT``, ``SELDON_LOG_*``, ...) < flags.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import signal
+import subprocess
+import sys
+import threading
+import time
+from typing import Dict, List, Optional
+
+logger = logging.getLogger("seldon_core_amd.serve")
+
+
+def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
+    ap = argparse.ArgumentParser(prog="seldon-amd-engine")
+    ap.add_argument("--spec", default=None, help="SeldonDeployment / PredictorSpec JSON or YAML (default: "
+                                                  "ENGINE_PREDICTOR env, ./deploymentdef.json, SIMPLE_MODEL graph)")
+    ap.add_argument("--predictor", default=None)
+    ap.add_argument("--http-port", type=int, default=None)
+    ap.add_argument("--grpc-port", type=int, default=None)
+    ap.add_argument("--admin-port", type=int, default=None)
+    ap.add_argument("--host", default=None)
+    ap.add_argument("--threads", type=int, default=None)
+    ap.add_argument("--gpus", default="1", help="worker processes, one per GPU: N or 'all'")
+    ap.add_argument("--device", type=int, default=None, help="GPU for a single worker (-1 = CPU)")
+    ap.add_argument("--component", action="append", default=[], help="node=module.Class binding")
+    ap.add_argument("--no-fuse", action="store_true", help="disable device-graph fusion")
+    ap.add_argument("--max-restarts", type=int, default=5, help="per worker per minute")
+    ap.add_argument("--log-level", default=os.environ.get("SELDON_LOG_LEVEL", "INFO"))
+    ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+def _gpu_total() -> int:
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())  # does not initialise the GPU on this stack
+    except Exception:
+        return 0
+
+
+def _n_workers(arg: str) -> int:
+    if str(arg).lower() == "all":
+        return max(1, _gpu_total())
+    return max(1, int(arg))
+
+
+# ------------------------------------------------------------------ worker
+def run_worker(args: argparse.Namespace) -> int:
+    from .serving.config import EngineConfig
+    from .serving.deployment import Deployment
+    from .serving.spec import load_spec, predictors
+
+    sdep = load_spec(args.spec)
+    spec_ann: Dict[str, str] = dict(((sdep.get("spec") or {}).get("annotations") or {}))
+    for p in predictors(sdep):
+        spec_ann.update(p.get("annotations") or {})
+    cfg = EngineConfig.resolve(spec_annotations=spec_ann, http_port=args.http_port, grpc_port=args.grpc_port,
+                               admin_port=args.admin_port, host=args.host, threads=args.threads)
+    comps = {}
+    for c in args.component:
+        node, _, cls = c.partition("=")
+        comps[node] = cls
+    dep = Deployment(sdep, components=comps, predictor=args.predictor, deployment_name=cfg.deployment_name,
+                     device=args.device, fuse=False if args.no_fuse else None, config=cfg)
+    h = dep.serve(http_port=cfg.http_port, grpc_port=cfg.grpc_port, admin_port=cfg.admin_port,
+                  threads=cfg.threads, grpc_threads=cfg.grpc_threads, host=cfg.host)
+    rank = os.environ.get("SCA_WORKER_RANK", "0")
+    logger.info("worker %s serving %s: REST :%s gRPC :%s admin :%s (device %s, units %s)", rank,
+                dep.predictor.get("name"), h.http_port, h.grpc_port, cfg.admin_port, dep.device,
+                {n: dep.engine.unit_kind(n) for n in dep.engine.node_names()})
+    stop = threading.Event()
+
+    def on_signal(signum, frame):  # noqa: ARG001
+        stop.set()
+
+    signal.signal(signal.SIGTERM, on_signal)
+    signal.signal(signal.SIGINT, on_signal)
+    stop.wait()
+    clean = h.drain(cfg.drain_seconds)
+    dep.engine.flush_message_log()
+    dep.close()
+    logger.info("worker %s drained (%s)", rank, "clean" if clean else "timeout")
+    return 0
+
+
+# -------------------------------------------------------------- supervisor
+class Supervisor:
+    """Keeps one worker process per GPU alive."""
+
+    def __init__(self, n: int, worker_argv: List[str], max_restarts: int = 5):
+        self.n = n
+        self.argv = worker_argv
+        self.max_restarts = max_restarts
+        self.procs: Dict[int, subprocess.Popen] = {}
+        self.restarts: Dict[int, List[float]] = {i: [] for i in range(n)}
+        self.stopping = False
+
+    def spawn(self, rank: int) -> None:
+        env = dict(os.environ)
+        env["HIP_VISIBLE_DEVICES"] = str(rank)
+        env["SCA_WORKER_RANK"] = str(rank)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        self.procs[rank] = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--worker", *self.argv],
+                                            env=env)
+        logger.info("started worker %d (pid %d) on GPU %d", rank, self.procs[rank].pid, rank)
+
+    def status(self) -> Dict:
+        return {"workers": {r: {"pid": p.pid, "alive": p.poll() is None, "restarts": len(self.restarts[r])}
+                            for r, p in self.procs.items()}}
+
+    def terminate(self) -> None:
+        self.stopping = True
+        for p in self.procs.values():
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+
+    def run(self) -> int:
+        for r in range(self.n):
+            self.spawn(r)
+        signal.signal(signal.SIGTERM, lambda *_: self.terminate())
+        signal.signal(signal.SIGINT, lambda *_: self.terminate())
+        rc = 0
+        while True:
+            time.sleep(0.2)
+            alive = 0
+            for r, p in list(self.procs.items()):
+                code = p.poll()
+                if code is None:
+                    alive += 1
+                    continue
+                if self.stopping:
+                    continue
+                now = time.monotonic()
+                self.restarts[r] = [t for t in self.restarts[r] if now - t < 60.0]
+                if len(self.restarts[r]) >= self.max_restarts:
+                    logger.error("worker %d exited with %s and hit the restart limit; shutting down", r, code)
+                    rc = code or 1
+                    self.terminate()
+                    continue
+                self.restarts[r].append(now)
+                logger.warning("worker %d exited with %s; restarting", r, code)
+                self.spawn(r)
+                alive += 1
+            if self.stopping and alive == 0:
+                return rc
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    args = parse_args(argv)
+    logging.basicConfig(level=getattr(logging, str(args.log_level).upper(), logging.INFO),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    if args.worker:
+        return run_worker(args)
+    n = _n_workers(args.gpus)
+    if n == 1:
+        return run_worker(args)
+    raw = list(sys.argv[1:] if argv is None else argv)
+    worker_argv: List[str] = []
+    skip = False
+    for i, a in enumerate(raw):  # drop --gpus from the workers' command line
+        if skip:
+            skip = False
+            continue
+        if a == "--gpus":
+            skip = True
+            continue
+        if a.startswith("--gpus="):
+            continue
+        worker_argv.append(a)
+    return Supervisor(n, worker_argv, args.max_restarts).run()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

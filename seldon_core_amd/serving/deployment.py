@@ -53,7 +53,7 @@ class Deployment:
                  predictor: Optional[str] = None, deployment_name: Optional[str] = None,
                  device: Optional[int] = None, batcher: Optional[Dict[str, Any]] = None,
                  log_requests: bool = False, log_responses: bool = False, fuse: Optional[bool] = None,
-                 _metrics_from=None):
+                 config=None, _metrics_from=None):
         self.C = native()
         self.sdep = load_spec(spec)
         all_preds = predictors(self.sdep)
@@ -88,8 +88,11 @@ class Deployment:
         errs = [e for e in errs if "Traffic" not in e]
         if errs:
             raise SpecError(errs)
-        self.engine = self.C.Engine(json.dumps(self.predictor), self.deployment_name, "", log_requests,
-                                    log_responses, False, _metrics_from)
+        self.config = config
+        ekw = config.engine_kwargs() if config is not None else dict(log_requests=log_requests,
+                                                                     log_responses=log_responses)
+        self.engine = self.C.Engine(json.dumps(self.predictor), self.deployment_name, "",
+                                    share_metrics_with=_metrics_from, **ekw)
         self.units: Dict[str, Any] = {}
         self.batched: Dict[str, Any] = {}
         self.native_units: Dict[str, Any] = {}
@@ -105,7 +108,8 @@ class Deployment:
         self.peers: Dict[str, "Deployment"] = {}
         if split:
             kw = dict(components=components, deployment_name=self.deployment_name, device=device, batcher=batcher,
-                      log_requests=log_requests, log_responses=log_responses, fuse=fuse, _metrics_from=self.engine)
+                      log_requests=log_requests, log_responses=log_responses, fuse=fuse, config=config,
+                      _metrics_from=self.engine)
             routes, shadows = [], []
             for p in all_preds:
                 if p["name"] == pname:
@@ -136,9 +140,35 @@ class Deployment:
         self._row_models[node["name"]] = row_model
         self._row_nodes[node["name"]] = node
 
+    def replica_devices(self, node: Dict):
+        """GPUs serving a node: ``devices: [..]`` or ``replicas: N`` (extension
+        fields; N consecutive GPUs from the node's device), or every GPU with the
+        ``seldon.io/gpu-replicas: all`` annotation."""
+        if node.get("devices"):
+            return [int(d) for d in node["devices"]]
+        base = self._node_device(node)
+        n = int(node.get("replicas", 1) or 1)
+        if str(self.annotations().get("seldon.io/gpu-replicas", "")).lower() == "all" and base >= 0:
+            n = max(n, gpu_count())
+        if n <= 1 or base < 0:
+            return [base]
+        ngpu = max(1, gpu_count())
+        return [(base + i) % ngpu for i in range(n)]
+
+    def _make_unit(self, node: Dict, row_model, whole_graph: bool = False):
+        devs = self.replica_devices(node)
+        opts = self._batcher_opts(node)
+        if len(devs) == 1:
+            return self.C.BatchedUnit(row_model, devs[0], **opts)
+        reps = []
+        for i, d in enumerate(devs):
+            rm = row_model.clone_on(d) if whole_graph else (row_model if i == 0 else row_model.clone())
+            reps.append(self.C.BatchedUnit(rm, d, **opts))
+        return self.C.ReplicaUnit(reps)
+
     def _bind_batched(self, node: Dict, row_model) -> None:
-        unit = self.C.BatchedUnit(row_model, self._node_device(node), **self._batcher_opts(node))
-        self.engine.bind_batched(node["name"], unit)
+        unit = self._make_unit(node, row_model)
+        self.engine.bind_unit(node["name"], unit)
         self.batched[node["name"]] = unit
         self.units[node["name"]] = unit
 
@@ -154,7 +184,7 @@ class Deployment:
                     logger.info("device graph at %s not fused: %s", fg.root, e)
                     continue
                 root = next(n for n, _ in iter_nodes(self.predictor["graph"]) if n["name"] == fg.root)
-                unit = self.C.BatchedUnit(gm, self._node_device(root), **self._batcher_opts(root))
+                unit = self._make_unit(root, gm, whole_graph=True)
                 self.engine.bind_fused(fg.root, unit, fg.absorbed)
                 self.batched[fg.root] = unit
                 self.units[fg.root] = unit
@@ -353,6 +383,23 @@ class ServerHandle:
     @property
     def grpc_port(self) -> Optional[int]:
         return self.grpc.port if self.grpc else None
+
+    def drain(self, timeout_s: float = 20.0, poll_s: float = 0.01) -> bool:
+        """Graceful shutdown (reference App.java:39-107 + preStop ``/pause``):
+        flip readiness off so load balancers stop sending, wait up to
+        ``timeout_s`` for in-flight requests to finish, then stop the servers.
+        Returns True if everything in flight completed."""
+        import time
+
+        if self.http:
+            self.http.paused = True
+        eng = self.deployment.engine
+        deadline = time.monotonic() + timeout_s
+        while eng.inflight() > 0 and time.monotonic() < deadline:
+            time.sleep(poll_s)
+        clean = eng.inflight() == 0
+        self.stop()
+        return clean
 
     def stop(self) -> None:
         if self.http:

@@ -1,0 +1,167 @@
+"""Engine process lifecycle and ops features: config precedence, CloudEvents
+request logging, graceful drain, multi-process replica supervisor.
+
+Reference: engine/.../service/PredictionService.java:98-191 (logging),
+App.java:39-107 (drain), config/AnnotationsConfig.java:26-79 (annotations file),
+application.properties (env switches)."""
+import http.server
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+import urllib.request
+
+import pytest
+
+import seldon_core_amd as sca
+from seldon_core_amd.serving.config import EngineConfig, read_annotations
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_config_precedence(tmp_path):
+    ann = tmp_path / "annotations"
+    ann.write_text('seldon.io/grpc-max-message-size="1000"\nseldon.io/engine-drain-seconds="3"\nother="x"\n')
+    assert read_annotations(str(ann))["other"] == "x"
+    env = {"ENGINE_SERVER_PORT": "9100", "SELDON_LOG_REQUESTS": "true", "DEPLOYMENT_NAME": "dep",
+           "DEPLOYMENT_NAMESPACE": "ns"}
+    c = EngineConfig.resolve(env=env, spec_annotations={"seldon.io/engine-drain-seconds": "5"},
+                             annotations_file=str(ann), grpc_port=7000)
+    assert c.http_port == 9100 and c.grpc_port == 7000
+    assert c.grpc_max_message_size == 1000
+    assert c.drain_seconds == 5.0  # spec annotation beats the file
+    assert c.log_requests and not c.log_responses
+    assert c.message_logging_service == "http://default-broker.ns.svc.cluster.local"
+    assert c.deployment_name == "dep" and c.deployment_namespace == "ns"
+
+
+class _Sink(http.server.BaseHTTPRequestHandler):
+    got = []
+
+    def do_POST(self):
+        n = int(self.headers["Content-Length"])
+        _Sink.got.append((dict(self.headers), json.loads(self.rfile.read(n))))
+        self.send_response(200)
+        self.send_header("Content-Length", "0")
+        self.end_headers()
+
+    def log_message(self, *a):
+        pass
+
+
+def test_cloudevents_pair_logging():
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _Sink)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    _Sink.got.clear()
+    try:
+        cfg = EngineConfig.resolve(env={"SELDON_LOG_MESSAGES_EXTERNALLY": "true", "DEPLOYMENT_NAME": "mydep",
+                                        "DEPLOYMENT_NAMESPACE": "prod",
+                                        "SELDON_MESSAGE_LOGGING_SERVICE": f"http://127.0.0.1:{srv.server_port}/"},
+                                   annotations_file="/nonexistent")
+        dep = sca.Deployment(None, device=-1, config=cfg)
+        try:
+            out = dep.predict({"meta": {"puid": "p123"}, "data": {"ndarray": [[1.0, 2.0]]}})
+            assert out["meta"]["puid"] == "p123"
+            dep.engine.flush_message_log()
+            assert dep.engine.message_log_stats()["sent"] == 1
+        finally:
+            dep.close()
+        headers, body = _Sink.got[0]
+        h = {k.lower(): v for k, v in headers.items()}
+        assert h["ce-specversion"] == "0.2" and h["ce-type"] == "seldon.message.pair"
+        assert h["ce-eventid"] == "p123" and h["ce-source"] == "application/json"
+        assert body["sdepName"] == "mydep" and body["namespace"] == "prod"
+        assert body["request"]["data"]["ndarray"] == [[1.0, 2.0]] and "date" in body["request"]
+        assert body["response"]["data"]["tensor"]["values"] == [0.1, 0.9, 0.5] and "date" in body["response"]
+    finally:
+        srv.shutdown()
+
+
+def test_stdout_request_logging(capfd):
+    cfg = EngineConfig.resolve(env={"SELDON_LOG_REQUESTS": "1", "SELDON_LOG_RESPONSES": "1",
+                                    "SELDON_LOG_FEEDBACK_REQUESTS": "1"}, annotations_file="/nonexistent")
+    dep = sca.Deployment(None, device=-1, config=cfg)
+    try:
+        req = {"meta": {"puid": "zz"}, "data": {"ndarray": [[1.0]]}}
+        out = dep.predict(req)
+        dep.feedback({"request": req, "response": out, "reward": 1.0})
+        dep.engine.flush_message_log()
+    finally:
+        dep.close()
+    lines = [json.loads(l) for l in capfd.readouterr().out.splitlines() if l.startswith("{")]
+    assert lines[0]["meta"]["puid"] == "zz" and "ndarray" in lines[0]["data"]
+    assert "tensor" in lines[1]["data"]
+    assert lines[2]["reward"] == 1.0
+
+
+def test_drain_waits_for_inflight():
+    class Slow:
+        def predict(self, X, names):
+            time.sleep(0.3)
+            return X
+
+    spec = {"name": "p", "graph": {"name": "m", "type": "MODEL"}, "componentSpecs": [{"spec": {"containers": []}}]}
+    dep = sca.Deployment(spec, components={"m": Slow()}, device=-1)
+    h = dep.serve(http_port=0, grpc_port=None, threads=2, host="127.0.0.1")
+    port = h.http_port
+    result = {}
+
+    def call():
+        req = urllib.request.Request(f"http://127.0.0.1:{port}/api/v0.1/predictions",
+                                     data=json.dumps({"data": {"ndarray": [[1.0]]}}).encode(),
+                                     headers={"Content-Type": "application/json"})
+        result["body"] = json.loads(urllib.request.urlopen(req, timeout=10).read())
+
+    t = threading.Thread(target=call)
+    t.start()
+    time.sleep(0.1)
+    assert dep.engine.inflight() == 1
+    assert h.drain(5.0) is True
+    t.join()
+    assert result["body"]["data"]["ndarray"] == [[1.0]]
+    dep.close()
+
+
+def _wait_ready(port, timeout=90):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        try:
+            if urllib.request.urlopen(f"http://127.0.0.1:{port}/ready", timeout=1).status == 200:
+                return True
+        except Exception:
+            time.sleep(0.2)
+    return False
+
+
+def test_supervisor_two_workers_share_port():
+    hp, gp = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    p = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--gpus", "2", "--device", "-1",
+                          "--http-port", str(hp), "--grpc-port", str(gp), "--admin-port", "0", "--threads", "1",
+                          "--log-level", "WARNING"], env=env, cwd=ROOT, start_new_session=True)
+    try:
+        assert _wait_ready(hp), "engine did not become ready"
+        for _ in range(20):
+            req = urllib.request.Request(f"http://127.0.0.1:{hp}/api/v0.1/predictions",
+                                         data=b'{"data":{"ndarray":[[1.0]]}}',
+                                         headers={"Content-Type": "application/json", "Connection": "close"})
+            out = json.loads(urllib.request.urlopen(req, timeout=5).read())
+            assert out["data"]["tensor"]["values"] == [0.1, 0.9, 0.5]
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 0
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()

@@ -32,9 +32,9 @@ NGHTTP2_LIB = Path("/opt/conda/lib/libnghttp2.so.14")
 
 LIB_SOURCES = [
     "core/json.cc", "core/message.cc", "core/pbwire.cc", "core/spec.cc", "core/metrics.cc",
-    "core/engine.cc", "core/units.cc",
+    "core/engine.cc", "core/units.cc", "core/msglog.cc",
     "server/http_server.cc", "server/grpc_server.cc", "server/remote_unit.cc",
-    "gpu/models.cc", "gpu/batcher.cc", "gpu/router.cc", "gpu/graph.cc",
+    "gpu/models.cc", "gpu/batcher.cc", "gpu/router.cc", "gpu/graph.cc", "gpu/replica.cc",
     "kernels/linear.hip", "kernels/tree.hip", "kernels/combine.hip", "kernels/bandit.hip",
     "bindings/module.cc",
 ]
