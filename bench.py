@@ -47,11 +47,13 @@ def parse_args():
     ap.add_argument("--step-requests", type=int, default=40000, help="predictions per step per GPU")
     ap.add_argument("--server-threads", type=int, default=6)
     ap.add_argument("--client-threads", type=int, default=6)
+    ap.add_argument("--graph", choices=["single", "abtest", "pipeline", "mab"], default="single",
+                    help="graph shape (single = the headline single-model graph)")
     ap.add_argument("--extra-grpc", action="store_true", help="also report the gRPC API (untimed extra)")
     return ap.parse_args()
 
 
-def build_deployment(model: str, device: int):
+def build_deployment(model: str, device: int, graph_kind: str = "single"):
     import numpy as np  # noqa: F401
 
     import seldon_core_amd as sca
@@ -73,15 +75,59 @@ def build_deployment(model: str, device: int):
         row = [0.1 * ((i * 7) % 13 - 6) for i in range(32)]
         label = "xgboost-1000trees-depth8 regressor (tree_perfect HIP kernel, random-init)"
     impl = "SKLEARN_SERVER" if model == "iris" else "XGBOOST_SERVER"
+    graph = {"name": "classifier", "type": "MODEL", "implementation": impl,
+             "modelUri": "memory://bench", "children": [], "device": device}
+    comps = {"classifier": comp}
+    if graph_kind != "single":
+        graph, comps, glabel = _graph_variant(graph_kind, comp, model, device, len(row))
+        label = f"{glabel} [{label}]"
     spec = {"apiVersion": "machinelearning.seldon.io/v1alpha2", "kind": "SeldonDeployment",
             "metadata": {"name": "bench"},
             "spec": {"name": "bench", "predictors": [{
                 "name": "default", "replicas": 1, "componentSpecs": [{"spec": {"containers": []}}],
-                "graph": {"name": "classifier", "type": "MODEL", "implementation": impl,
-                          "modelUri": "memory://bench", "children": [], "device": device}}]}}
-    dep = sca.Deployment(spec, components={"classifier": comp}, device=device,
-                         batcher={"max_batch": 4096, "slots": 4})
+                "graph": graph}]}}
+    dep = sca.Deployment(spec, components=comps, device=device, batcher={"max_batch": 4096, "slots": 4})
     return dep, names, row, label
+
+
+def _graph_variant(kind: str, comp, model: str, device: int, n_features: int):
+    """Multi-node graphs of BASELINE.json's other configs (extra measurements,
+    not the headline): GPU placement spreads nodes over the visible GPUs."""
+    import numpy as np
+
+    import seldon_core_amd as sca
+    from seldon_core_amd.models import to_row_model
+
+    C = sca.native()
+    ngpu = max(1, sca.gpu_count()) if device >= 0 else 1
+    dev = (lambda i: (device + i) % ngpu) if device >= 0 else (lambda i: -1)
+    rm_a = comp.row_model() if hasattr(comp, "row_model") else to_row_model(comp)
+    rm_b = rm_a.clone()
+    if kind == "abtest":  # seldon-abtest: RANDOM_ABTEST router over 2 model replicas on 2 GPUs
+        g = {"name": "ab", "type": "ROUTER", "implementation": "RANDOM_ABTEST", "device": dev(0),
+             "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
+             "children": [{"name": "a", "type": "MODEL", "device": dev(0)},
+                          {"name": "b", "type": "MODEL", "device": dev(1)}]}
+        return g, {"a": rm_a, "b": rm_b}, "RANDOM_ABTEST(2 replicas)"
+    if kind == "pipeline":  # transformer -> combiner over 2 models, one stage per GPU (device graph)
+        rng = np.random.default_rng(0)
+        scale = np.diag(1.0 + 0.01 * rng.random(n_features))
+        tr = C.linear_model(scale, np.zeros(n_features), 0)  # standard-scaler-style affine transform
+        g = {"name": "scaler", "type": "TRANSFORMER", "device": dev(0), "children": [
+            {"name": "combiner", "type": "COMBINER", "implementation": "AVERAGE_COMBINER", "device": dev(3),
+             "children": [{"name": "a", "type": "MODEL", "device": dev(1)},
+                          {"name": "b", "type": "MODEL", "device": dev(2)}]}]}
+        return g, {"scaler": tr, "a": rm_a, "b": rm_b}, "TRANSFORMER->COMBINER(2 models) device graph"
+    if kind == "mab":  # epsilon-greedy router over one model replica per GPU
+        from seldon_core_amd.components.routers import EpsilonGreedy
+
+        n = max(2, ngpu)
+        kids = [{"name": f"m{i}", "type": "MODEL", "device": dev(i)} for i in range(n)]
+        comps = {f"m{i}": (rm_a if i == 0 else rm_a.clone()) for i in range(n)}
+        comps["mab"] = EpsilonGreedy(n_branches=n, epsilon=0.1, seed=1)
+        g = {"name": "mab", "type": "ROUTER", "device": dev(0), "children": kids}
+        return g, comps, f"EPSILON_GREEDY router over {n} replicas"
+    raise ValueError(kind)
 
 
 def run_loadgen(args, port: int, steps: int, warmup: int, api: str, body: bytes | str) -> dict:
@@ -134,7 +180,7 @@ def main() -> None:
         if has_gpu:
             torch.cuda.synchronize()
 
-    dep, names, row, label = build_deployment(args.model, device)
+    dep, names, row, label = build_deployment(args.model, device, args.graph)
     handle = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
     payload = json.dumps({"data": {"names": names, "ndarray": [row]}})
     C = dep.C
@@ -177,10 +223,11 @@ def main() -> None:
         value = sum(r["rps"] for r in results)
         ms_per_step = max(r["wall"] for r in results) / args.steps * 1000.0
         base = REST_BASELINE if args.api == "rest" else GRPC_BASELINE
-        batch = results[0]["batch"].get("classifier", {})
+        batch = next(iter(results[0]["batch"].values()), {}) if results[0]["batch"] else {}
         mean_rows = batch.get("rows", 0) / max(1, batch.get("batches", 1))
         line = {
-            "metric": "predictions/sec (single-model graph, %s)" % args.api.upper(),
+            "metric": "predictions/sec (%s graph, %s)" % ("single-model" if args.graph == "single" else args.graph,
+                                                          args.api.upper()),
             "value": round(value, 2), "unit": "predictions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / base, 3), "dtype": "fp64",
@@ -189,7 +236,7 @@ def main() -> None:
             "baseline": {"rest_rps": REST_BASELINE, "rest_p50_ms": 4, "rest_p99_ms": 69, "grpc_rps": GRPC_BASELINE,
                          "grpc_p50_ms": 1, "grpc_p99_ms": 6},
             "config": {"model": label, "global_batch": args.users * world, "seq_len": len(row),
-                       "parallelism": f"dp{world}", "graph": "single MODEL node", "api": args.api,
+                       "parallelism": f"dp{world}", "graph": args.graph, "api": args.api,
                        "users_per_gpu": args.users, "requests_per_step_per_gpu": args.step_requests,
                        "device": "gpu" if has_gpu else "cpu", "gpu_batches": batch.get("batches", 0),
                        "mean_rows_per_gpu_batch": round(mean_rows, 2)},

@@ -31,6 +31,9 @@ for s in $STEPS; do
     bench) run bench 400 python bench.py --extra-grpc ;;
     bench_grpc) run bench_grpc 400 python bench.py --api grpc ;;
     bench_xgb) run bench_xgb 400 python bench.py --model xgb1000 --step-requests 20000 ;;
+    bench_abtest) run bench_abtest 300 python bench.py --graph abtest --steps 5 ;;
+    bench_pipeline) run bench_pipeline 300 python bench.py --graph pipeline --steps 5 ;;
+    bench_mab) run bench_mab 300 python bench.py --graph mab --steps 5 ;;
     prof)
       export TMPDIR=/tmp
       run prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
