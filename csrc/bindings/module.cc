@@ -16,6 +16,7 @@
 #include "../gpu/models.h"
 #include "../gpu/router.h"
 #include "../kernels/kernels.h"
+#include "../parallel/fabric.h"
 #include "../server/grpc_server.h"
 #include "../server/http_server.h"
 #include "../server/remote_unit.h"
@@ -306,6 +307,48 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         u.stop();
       });
+
+  // ------------------------------------------------------- RCCL fabric
+  m.def("rccl_unique_id", [] { return py::bytes(par::rccl_unique_id()); });
+  py::class_<par::Fabric, std::shared_ptr<par::Fabric>>(m, "Fabric")
+      .def(py::init([](int rank, int world, const py::bytes& uid, int device) {
+             std::string id(uid);
+             py::gil_scoped_release nogil;  // collective: blocks until every rank joins
+             return std::make_shared<par::Fabric>(rank, world, id, device);
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"))
+      .def_property_readonly("rank", &par::Fabric::rank)
+      .def_property_readonly("world", &par::Fabric::world)
+      .def_property_readonly("device", &par::Fabric::device)
+      .def("stop_peers", [](par::Fabric& f) {
+        py::gil_scoped_release nogil;
+        par::stop_peers(f);
+      })
+      .def("close", [](par::Fabric& f) {
+        py::gil_scoped_release nogil;
+        f.close();
+      });
+  m.def("peer_row_model",
+        [](std::shared_ptr<par::Fabric> f, std::vector<int> peers, int model_id, int in_cols, int out_cols,
+           std::vector<std::string> names, bool flat) {
+          auto mdl = std::make_shared<par::PeerRowModel>(std::move(f), std::move(peers), model_id, in_cols, out_cols);
+          mdl->set_class_names(std::move(names));
+          mdl->set_flat_output(flat);
+          return std::static_pointer_cast<gpu::RowModel>(mdl);
+        },
+        py::arg("fabric"), py::arg("peers"), py::arg("model_id"), py::arg("in_cols"), py::arg("out_cols"),
+        py::arg("class_names") = std::vector<std::string>(), py::arg("flat_output") = false);
+  py::class_<par::PeerServer, std::shared_ptr<par::PeerServer>>(m, "PeerServer")
+      .def(py::init<std::shared_ptr<par::Fabric>>())
+      .def("add_model", &par::PeerServer::add_model)
+      .def("start", &par::PeerServer::start)
+      .def("join", [](par::PeerServer& s) {
+        py::gil_scoped_release nogil;
+        s.join();
+      })
+      .def_property_readonly("batches", &par::PeerServer::batches)
+      .def_property_readonly("rows", &par::PeerServer::rows)
+      .def("error", &par::PeerServer::error);
 
   // ------------------------------------------------------------- engine
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")

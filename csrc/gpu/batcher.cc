@@ -22,6 +22,8 @@ bool available() { return device_count() > 0; }
 BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::move(model)), opts_(opts) {
   if (opts_.max_batch < 1) opts_.max_batch = 1;
   if (opts_.slots < 1) opts_.slots = 1;
+  device_io_ = model_->device_io_only();
+  zc_input_ = model_->zero_copy_input();
   {
     const int oc = model_->out_cols(model_->in_cols() > 0 ? model_->in_cols() : 1);
     default_names_ = model_->class_names();
@@ -80,16 +82,20 @@ void BatchedUnit::ensure_capacity(Slot& s, int rows, int cols) {
   const int oc = model_->out_cols(cols);
   const size_t need_in = size_t(rows) * cols * sizeof(double);
   const size_t need_out = size_t(rows) * oc * sizeof(double);
+  // Geometric growth: pinned/device allocations are slow, batches vary.
+  auto grow = [](size_t have, size_t need) { return std::max(need, 2 * have); };
   if (s.h_in.bytes() < need_in) {
-    s.h_in.alloc(need_in);
-    s.d_in.alloc(need_in, opts_.device);
+    const size_t b = grow(s.h_in.bytes(), need_in);
+    s.h_in.alloc(b);
+    s.d_in.alloc(b, opts_.device);
   }
   if (s.h_out.bytes() < need_out) {
-    s.h_out.alloc(need_out);
-    s.d_out.alloc(need_out, opts_.device);
+    const size_t b = grow(s.h_out.bytes(), need_out);
+    s.h_out.alloc(b);
+    s.d_out.alloc(b, opts_.device);
   }
   const size_t ws = model_->workspace_bytes(rows, cols);
-  if (s.ws.bytes() < ws) s.ws.alloc(ws, opts_.device);
+  if (s.ws.bytes() < ws) s.ws.alloc(grow(s.ws.bytes(), ws), opts_.device);
   s.cap_rows = std::max(s.cap_rows, size_t(rows));
 }
 
@@ -221,8 +227,16 @@ void BatchedUnit::submit_loop() {
       }
       const size_t bin = size_t(rows) * cols * sizeof(double), bout = size_t(rows) * s->out_cols * sizeof(double);
       hipStream_t st = s->stream.get();
-      if (opts_.zero_copy && bin + bout <= opts_.zero_copy_max_bytes) {
-        model_->launch(s->h_in.dev<double>(), rows, cols, s->h_out.dev<double>(), s->ws.get(), st);
+      if (opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes) {
+        // Output always zero-copy (written once); input zero-copy only if the
+        // kernel reads each element once -- models that re-read X from many
+        // workgroups (tree chunks) get one DMA into HBM first.
+        const double* xin = s->h_in.dev<double>();
+        if (!zc_input_) {
+          err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
+          xin = s->d_in.as<double>();
+        }
+        if (err == hipSuccess) model_->launch(xin, rows, cols, s->h_out.dev<double>(), s->ws.get(), st);
       } else {
         err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
         if (err == hipSuccess) {

@@ -109,6 +109,8 @@ class BatchedUnit : public Unit {
   size_t queued_rows_ = 0;
   std::atomic<bool> running_{false};
   std::atomic<int64_t> inflight_rows_{0};
+  bool device_io_ = false;  // model needs device-memory I/O (no zero-copy)
+  bool zc_input_ = true;    // model reads X once per element (zero-copy input is cheaper than a DMA)
   std::thread submit_th_;
   std::vector<std::string> default_names_;
   mutable std::mutex stats_mu_;

@@ -49,6 +49,17 @@ class GraphModel : public RowModel {
   int out_cols(int in_cols) const override;
   std::vector<std::string> class_names() const override;
   void to_device(int device) override;
+  bool zero_copy_input() const override {
+    for (const auto& s : st_)
+      for (int j : s.inputs)
+        if (j < 0 && s.model && !s.model->zero_copy_input()) return false;
+    return true;
+  }
+  bool device_io_only() const override {
+    for (const auto& s : st_)
+      if (s.model && s.model->device_io_only()) return true;
+    return false;
+  }
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
 

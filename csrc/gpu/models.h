@@ -31,6 +31,11 @@ class RowModel {
   bool flat_output() const { return flat_; }
   void set_flat_output(bool f) { flat_ = f; }
   virtual void to_device(int device) = 0;
+  // True if launch() needs X/out in device memory (no zero-copy host I/O).
+  virtual bool device_io_only() const { return false; }
+  // False if many workgroups re-read X (stage it in HBM instead of reading
+  // pinned host memory over PCIe from every workgroup).
+  virtual bool zero_copy_input() const { return true; }
   virtual size_t workspace_bytes(int max_rows, int cols) const { (void)max_rows; (void)cols; return 0; }
   virtual void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) = 0;
   virtual void run_cpu(const double* X, int rows, int cols, double* out) const = 0;
@@ -102,6 +107,7 @@ class TreeEnsembleModel : public RowModel {
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
   const TreeEnsembleSpec& spec() const { return spec_; }
+  bool zero_copy_input() const override { return false; }  // every tree-chunk block stages the X tile
   std::shared_ptr<RowModel> clone() const override { return with_meta(std::make_shared<TreeEnsembleModel>(spec_)); }
   // Launch geometry chosen for a batch (exposed for tests/benchmarks).
   void plan_for(int rows, int* rows_per_block, int* plan_index) const;

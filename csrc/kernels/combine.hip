@@ -41,6 +41,24 @@ __global__ __launch_bounds__(kBlock) void mean_kernel(const double* const* __res
   }
 }
 
+// Mean over K slabs of one contiguous buffer (gathered replica outputs).
+__global__ __launch_bounds__(kBlock) void mean_strided_kernel(const double* __restrict__ base, int k, int64_t n,
+                                                              double* __restrict__ out) {
+  const double inv = 1.0 / double(k);
+  for (int64_t i = blockIdx.x * int64_t(kBlock) + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    double acc = 0.0;
+    for (int j = 0; j < k; ++j) acc += base[size_t(j) * n + i];
+    out[i] = acc * inv;
+  }
+}
+
+__global__ void fill4_kernel(int32_t* dst, int a, int b, int c, int d) {
+  dst[0] = a;
+  dst[1] = b;
+  dst[2] = c;
+  dst[3] = d;
+}
+
 __device__ inline double wave_max(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
@@ -169,6 +187,15 @@ int grid_for(int64_t n) {
 void combine_mean_f64(const double* const* inputs, int n_inputs, int64_t n, double* out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(mean_kernel, dim3(grid_for(n / 2 + 1)), dim3(kBlock), 0, s, inputs, n_inputs, n, out);
+}
+
+void combine_mean_strided_f64(const double* base, int k, int64_t n, double* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(mean_strided_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, base, k, n, out);
+}
+
+void fill_i32x4(int32_t* dst, int a, int b, int c, int d, hipStream_t s) {
+  hipLaunchKernelGGL(fill4_kernel, dim3(1), dim3(1), 0, s, dst, a, b, c, d);
 }
 
 void softmax_rows_f64(const double* in, int rows, int C, double* out, hipStream_t s) {

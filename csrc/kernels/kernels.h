@@ -71,6 +71,10 @@ void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_
 // ------------------------------------------------------------ combiners
 // out = mean over N inputs (each [n] fp64). inputs: device array of pointers.
 void combine_mean_f64(const double* const* inputs, int n_inputs, int64_t n, double* out, hipStream_t stream);
+// out = mean over k slabs base[j*n : (j+1)*n] (gathered replica outputs).
+void combine_mean_strided_f64(const double* base, int k, int64_t n, double* out, hipStream_t stream);
+// dst[0..3] = {a, b, c, d} (device-side header for fabric transfers).
+void fill_i32x4(int32_t* dst, int a, int b, int c, int d, hipStream_t stream);
 // Row softmax / argmax over [rows, C].
 void softmax_rows_f64(const double* in, int rows, int C, double* out, hipStream_t stream);
 void argmax_rows_f64(const double* in, int rows, int C, int32_t* out, hipStream_t stream);

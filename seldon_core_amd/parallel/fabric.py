@@ -1,0 +1,89 @@
+"""Cross-process graph placement over RCCL (one engine process per MI355X).
+
+Spec extension: a graph node may carry ``rank: r`` -- the torch.distributed
+rank (= GPU) whose process hosts that node's row model.  Rank 0 runs the front
+end (REST/gRPC), the graph executor, routers and the micro-batchers; every
+batch bound for a node on rank r is shipped GPU-to-GPU with RCCL point-to-point
+transfers over xGMI (csrc/parallel/fabric.h) and answered the same way.  Worker
+ranks run only a native ``PeerServer`` loop.
+
+Typical launch (one process per GPU)::
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 my_server.py
+
+    fabric = init_fabric()                      # RCCL communicator over all ranks
+    if fabric.rank == 0:
+        dep = Deployment(spec, fabric=fabric)   # nodes with rank != 0 become PeerRowModels
+        dep.serve(...)
+    else:
+        serve_peer(spec, fabric).join()         # until rank 0 calls dep.close()
+
+Reference behaviour replaced: each graph hop is an HTTP/gRPC call to another
+pod (InternalPredictionService.java:186-453) carrying JSON.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, List, Optional
+
+from .._native import native
+from ..serving.spec import SpecError, iter_nodes, load_spec, select_predictor
+
+
+def init_fabric(device: Optional[int] = None):
+    """Create the RCCL communicator for the current torch.distributed job
+    (the unique id is broadcast over the default process group)."""
+    import torch.distributed as dist
+
+    C = native()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    box = [C.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", rank))
+    return C.Fabric(rank, world, box[0], device)
+
+
+def node_rank(node: Dict) -> Optional[int]:
+    r = node.get("rank")
+    return None if r is None else int(r)
+
+
+def rank_assignments(graph: Dict) -> Dict[int, List[str]]:
+    """rank -> node names hosted there, in graph order (= PeerServer model ids)."""
+    out: Dict[int, List[str]] = {}
+    for n, _ in iter_nodes(graph):
+        r = node_rank(n)
+        if r is not None:
+            out.setdefault(r, []).append(n["name"])
+    return out
+
+
+def peer_model_for(C, fabric, node: Dict, local_rm, model_id: int):
+    """Front-end stand-in for a node hosted on another rank."""
+    in_cols = int(local_rm.in_cols)
+    if in_cols <= 0:
+        raise SpecError([f"node '{node['name']}' on rank {node_rank(node)} needs a model with a fixed input width"])
+    return C.peer_row_model(fabric, [node_rank(node)], model_id, in_cols, int(local_rm.out_cols(in_cols)),
+                            list(local_rm.class_names()), bool(local_rm.flat_output))
+
+
+def serve_peer(spec: Any, fabric, components: Optional[Dict[str, Any]] = None, predictor: Optional[str] = None):
+    """Worker rank: build the row models of the nodes placed on this rank and
+    serve them until rank 0 stops the fabric.  Returns the started PeerServer."""
+    from ..serving.deployment import Deployment
+
+    sdep = load_spec(spec)
+    pred = select_predictor(sdep, predictor)
+    res = Deployment.resolver(sdep, components, pred)
+    C = native()
+    server = C.PeerServer(fabric)
+    for name in rank_assignments(pred["graph"]).get(fabric.rank, []):
+        node = next(n for n, _ in iter_nodes(pred["graph"]) if n["name"] == name)
+        kind, obj = res._resolve(node)
+        rm = res._row_model_of(res._instantiate(node, obj)) if kind == "object" else None
+        if rm is None:
+            raise SpecError([f"node '{name}' placed on rank {fabric.rank} is not a GPU row model"])
+        server.add_model(rm)
+    server.start()
+    return server

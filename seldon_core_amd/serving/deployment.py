@@ -53,8 +53,9 @@ class Deployment:
                  predictor: Optional[str] = None, deployment_name: Optional[str] = None,
                  device: Optional[int] = None, batcher: Optional[Dict[str, Any]] = None,
                  log_requests: bool = False, log_responses: bool = False, fuse: Optional[bool] = None,
-                 config=None, _metrics_from=None):
+                 config=None, fabric=None, _metrics_from=None):
         self.C = native()
+        self.fabric = fabric
         self.sdep = load_spec(spec)
         all_preds = predictors(self.sdep)
         split = predictor is None and len(all_preds) > 1
@@ -122,8 +123,21 @@ class Deployment:
                     routes.append((peer.engine, int(p.get("traffic", 0) or 0)))
             self.engine.set_traffic(int(self.predictor.get("traffic", 0) or 0), routes, shadows)
 
+    @classmethod
+    def resolver(cls, sdep: Dict, components: Optional[Dict[str, Any]], predictor: Dict) -> "Deployment":
+        """A binding-only view (no engine): resolves nodes to component objects
+        / row models the same way a Deployment does (used by worker ranks)."""
+        self = cls.__new__(cls)
+        self.C = native()
+        self.sdep = sdep
+        self.predictor = predictor
+        self.components = dict(components or {})
+        return self
+
     # ----------------------------------------------------------- binding
     def _node_device(self, node: Dict) -> int:
+        if self.fabric is not None and node.get("rank") is not None:
+            return int(self.fabric.device)  # rank-placed: the front end's side lives on its own GPU
         d = node.get("device")
         return self.device if d is None else int(d)
 
@@ -174,7 +188,23 @@ class Deployment:
 
     def _bind_row_models(self) -> None:
         from ..parallel import device_graph
+        from ..parallel.fabric import peer_model_for, rank_assignments
 
+        # Nodes placed on other ranks (``rank: r``) are served there; here they
+        # become RCCL peer models on this rank's GPU.
+        placed = rank_assignments(self.predictor["graph"])
+        for r, names in placed.items():
+            if self.fabric is None:
+                if r != 0:
+                    raise SpecError([f"graph places nodes on rank {r}; pass fabric=init_fabric()"])
+                continue
+            if r == self.fabric.rank:
+                continue
+            for mid, name in enumerate(names):
+                if name not in self._row_models:
+                    raise SpecError([f"node '{name}' placed on rank {r} is not a GPU row model"])
+                node = self._row_nodes[name]
+                self._row_models[name] = peer_model_for(self.C, self.fabric, node, self._row_models[name], mid)
         done = set()
         if self.fuse and self._row_models:
             for fg in device_graph.plan(self.predictor["graph"], self._row_models, self.units, self._node_device):
@@ -203,17 +233,38 @@ class Deployment:
         self.engine.bind_python(node["name"], adapter, 0)
         self.units[node["name"]] = adapter
 
-    def _bind_object(self, node: Dict, obj: Any) -> None:
-        from ..models import to_row_model
-
+    def _instantiate(self, node: Dict, obj: Any) -> Any:
         if isinstance(obj, str):
             obj = import_class(obj)
         if isinstance(obj, type):
             obj = obj(**typed_parameters(node))
             if hasattr(obj, "load"):
                 obj.load()
+        return obj
+
+    def _row_model_of(self, obj: Any):
+        """The native RowModel behind a component object, or None."""
+        from ..models import to_row_model
+
         if isinstance(obj, self.C.RowModel):
-            self.bind_row_model(node, obj)
+            return obj
+        if isinstance(obj, self.C.Unit) or callable(getattr(obj, "native_unit", None)):
+            return None
+        gpu = getattr(obj, "row_model", None)
+        if callable(gpu):
+            rm = gpu()
+            if rm is not None:
+                return rm
+        rm = to_row_model(obj) if not hasattr(obj, "predict_raw") else None
+        if rm is not None and not any(hasattr(obj, m) for m in ("route", "aggregate", "transform_input")):
+            return rm
+        return None
+
+    def _bind_object(self, node: Dict, obj: Any) -> None:
+        obj = self._instantiate(node, obj)
+        rm = self._row_model_of(obj)
+        if rm is not None:
+            self.bind_row_model(node, rm)
             return
         if isinstance(obj, self.C.Unit):
             self.engine.bind_unit(node["name"], obj)
@@ -226,39 +277,26 @@ class Deployment:
             self.units[node["name"]] = unit
             self.native_units[node["name"]] = unit
             return
-        gpu = getattr(obj, "row_model", None)
-        if callable(gpu):
-            rm = gpu()
-            if rm is not None:
-                self.bind_row_model(node, rm)
-                return
-        rm = to_row_model(obj) if not hasattr(obj, "predict_raw") else None
-        if rm is not None and not any(hasattr(obj, m) for m in ("route", "aggregate", "transform_input")):
-            self.bind_row_model(node, rm)
-            return
         self.bind_python(node, obj)
 
-    def _bind(self, node: Dict) -> None:
+    def _resolve(self, node: Dict):
+        """What implements a node: ("builtin", None), ("object", obj) or
+        ("remote", (host, port, grpc, container))."""
         name = node["name"]
         impl = node.get("implementation", "UNKNOWN_IMPLEMENTATION")
         if name in self.components:
-            self._bind_object(node, self.components[name])
-            return
+            return "object", self.components[name]
         if impl in BUILTIN_IMPLEMENTATIONS:
-            return  # native built-in
+            return "builtin", None
         params = typed_parameters(node)
         if impl in PREPACKAGED_SERVERS:
             from ..servers import load_prepackaged
 
-            obj = load_prepackaged(impl, node.get("modelUri", ""), params)
-            self._bind_object(node, obj)
-            return
+            return "object", load_prepackaged(impl, node.get("modelUri", ""), params)
         from ..components import NATIVE_IMPLEMENTATIONS
 
         if impl in NATIVE_IMPLEMENTATIONS:
-            obj = NATIVE_IMPLEMENTATIONS[impl](**params)
-            self._bind_object(node, obj)
-            return
+            return "object", NATIVE_IMPLEMENTATIONS[impl](**params)
         cls_path = params.pop("python_class", None)
         c = container_for(self.predictor, name)
         if not cls_path and c:
@@ -269,15 +307,20 @@ class Deployment:
             obj = import_class(cls_path)(**params)
             if hasattr(obj, "load"):
                 obj.load()
-            self._bind_object(node, obj)
-            return
+            return "object", obj
         ep = node.get("endpoint") or {}
         host = ep.get("service_host") or ep.get("serviceHost")
         port = ep.get("service_port") or ep.get("servicePort")
         if host and port:
-            self.bind_remote(node, host, int(port), ep.get("type", "REST") == "GRPC", c)
-            return
+            return "remote", (host, int(port), ep.get("type", "REST") == "GRPC", c)
         raise SpecError([f"no implementation for graph node '{name}' ({impl}); pass components={{'{name}': ...}}"])
+
+    def _bind(self, node: Dict) -> None:
+        kind, what = self._resolve(node)
+        if kind == "object":
+            self._bind_object(node, what)
+        elif kind == "remote":
+            self.bind_remote(node, *what)
 
     def annotations(self) -> Dict[str, str]:
         ann = dict((self.sdep.get("spec") or {}).get("annotations") or {})
@@ -362,6 +405,9 @@ class Deployment:
             u.stop()
         for p in getattr(self, "peers", {}).values():
             p.close()
+        if getattr(self, "fabric", None) is not None and self.fabric.rank == 0:
+            self.fabric.stop_peers()  # worker ranks leave their PeerServer loops
+            self.fabric = None
 
     def __enter__(self):
         return self

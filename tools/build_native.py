@@ -34,7 +34,7 @@ LIB_SOURCES = [
     "core/json.cc", "core/message.cc", "core/pbwire.cc", "core/spec.cc", "core/metrics.cc",
     "core/engine.cc", "core/units.cc", "core/msglog.cc",
     "server/http_server.cc", "server/grpc_server.cc", "server/remote_unit.cc",
-    "gpu/models.cc", "gpu/batcher.cc", "gpu/router.cc", "gpu/graph.cc", "gpu/replica.cc",
+    "gpu/models.cc", "gpu/batcher.cc", "gpu/router.cc", "gpu/graph.cc", "gpu/replica.cc", "parallel/fabric.cc",
     "kernels/linear.hip", "kernels/tree.hip", "kernels/combine.hip", "kernels/bandit.hip",
     "bindings/module.cc",
 ]
@@ -130,7 +130,7 @@ def build(jobs: int = 8, verbose: bool = False) -> Path:
     newest = max(o.stat().st_mtime for o in objs)
     if not out.exists() or out.stat().st_mtime < newest:
         cmd = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
-               "-o", str(out), f"-L{ROCM / 'lib'}", "-lamdhip64", str(ng),
+               "-o", str(out), f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", str(ng),
                "-Wl,-rpath,$ORIGIN/lib", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
         if verbose:
             print(" ".join(cmd), flush=True)
