@@ -199,6 +199,7 @@ PYBIND11_MODULE(_C, m) {
     if (!g) throw std::runtime_error("not a graph model");
     return g->devices();
   });
+  m.def("minmax_model", [] { return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MinMaxModel>()); });
   m.def("mean_sigmoid_model", [](double thr) {
     return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MeanSigmoidModel>(thr));
   });
@@ -567,6 +568,15 @@ PYBIND11_MODULE(_C, m) {
   });
   k.def("minmax_normalize_f64", [](uintptr_t in, int64_t n, uintptr_t out, uintptr_t scratch, uintptr_t s) {
     kern::minmax_normalize_f64(P<const double>(in), n, P<double>(out), P<double>(scratch), as_stream(s));
+  });
+  k.def("segment_minmax_f64", [](uintptr_t in, uintptr_t seg, int nseg, int cols, uintptr_t out, uintptr_t s) {
+    kern::segment_minmax_f64(P<const double>(in), P<const int32_t>(seg), nseg, cols, P<double>(out), as_stream(s));
+  });
+  k.def("crop_resize_chw_u8", [](uintptr_t img, int H, int W, int C, int crop, uintptr_t out, uintptr_t s) {
+    kern::crop_resize_chw_u8(P<const uint8_t>(img), H, W, C, crop, P<float>(out), as_stream(s));
+  });
+  k.def("combine_mean_strided_f64", [](uintptr_t base, int k_, int64_t n, uintptr_t out, uintptr_t s) {
+    kern::combine_mean_strided_f64(P<const double>(base), k_, n, P<double>(out), as_stream(s));
   });
   k.def("mean_sigmoid_rows_f64", [](uintptr_t in, int rows, int F, double thr, uintptr_t out, uintptr_t s) {
     kern::mean_sigmoid_rows_f64(P<const double>(in), rows, F, thr, P<double>(out), as_stream(s));

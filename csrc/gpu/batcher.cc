@@ -24,6 +24,7 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
   if (opts_.slots < 1) opts_.slots = 1;
   device_io_ = model_->device_io_only();
   zc_input_ = model_->zero_copy_input();
+  segmented_ = model_->segmented();
   {
     const int oc = model_->out_cols(model_->in_cols() > 0 ? model_->in_cols() : 1);
     default_names_ = model_->class_names();
@@ -227,6 +228,20 @@ void BatchedUnit::submit_loop() {
       }
       const size_t bin = size_t(rows) * cols * sizeof(double), bout = size_t(rows) * s->out_cols * sizeof(double);
       hipStream_t st = s->stream.get();
+      const int32_t* seg = nullptr;
+      const int nseg = int(s->items.size());
+      if (segmented_) {  // request boundaries for per-request models
+        if (s->h_seg.bytes() < (s->items.size() + 1) * sizeof(int32_t))
+          s->h_seg.alloc(std::max<size_t>(1024, 2 * (s->items.size() + 1)) * sizeof(int32_t));
+        int32_t* o = s->h_seg.host<int32_t>();
+        o[0] = 0;
+        for (size_t i = 0; i < s->items.size(); ++i) o[i + 1] = o[i] + s->items[i].rows;
+        seg = s->h_seg.dev<int32_t>();
+      }
+      auto run = [&](const double* x, double* y) {
+        if (seg) model_->launch_segments(x, rows, cols, y, s->ws.get(), seg, nseg, st);
+        else model_->launch(x, rows, cols, y, s->ws.get(), st);
+      };
       if (opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes) {
         // Output always zero-copy (written once); input zero-copy only if the
         // kernel reads each element once -- models that re-read X from many
@@ -236,11 +251,11 @@ void BatchedUnit::submit_loop() {
           err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
           xin = s->d_in.as<double>();
         }
-        if (err == hipSuccess) model_->launch(xin, rows, cols, s->h_out.dev<double>(), s->ws.get(), st);
+        if (err == hipSuccess) run(xin, s->h_out.dev<double>());
       } else {
         err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
         if (err == hipSuccess) {
-          model_->launch(s->d_in.as<double>(), rows, cols, s->d_out.as<double>(), s->ws.get(), st);
+          run(s->d_in.as<double>(), s->d_out.as<double>());
           err = hipMemcpyAsync(s->h_out.host<double>(), s->d_out.get(), bout, hipMemcpyDeviceToHost, st);
         }
       }

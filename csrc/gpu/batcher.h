@@ -81,6 +81,7 @@ class BatchedUnit : public Unit {
   struct Slot {
     PinnedBuffer h_in, h_out;
     DeviceBuffer d_in, d_out, ws;
+    PinnedBuffer h_seg;  // request row offsets (segmented models)
     Stream stream;
     Event ev;
     size_t cap_rows = 0;
@@ -110,7 +111,8 @@ class BatchedUnit : public Unit {
   std::atomic<bool> running_{false};
   std::atomic<int64_t> inflight_rows_{0};
   bool device_io_ = false;  // model needs device-memory I/O (no zero-copy)
-  bool zc_input_ = true;    // model reads X once per element (zero-copy input is cheaper than a DMA)
+  bool zc_input_ = true;
+  bool segmented_ = false;    // model reads X once per element (zero-copy input is cheaper than a DMA)
   std::thread submit_th_;
   std::vector<std::string> default_names_;
   mutable std::mutex stats_mu_;

@@ -182,7 +182,8 @@ GraphModel::Aux& GraphModel::aux_for(hipStream_t s, int rows, int cols) {
   return a;
 }
 
-void GraphModel::launch(const double* X, int rows, int cols, double* out, void*, hipStream_t s) {
+void GraphModel::launch_segments(const double* X, int rows, int cols, double* out, void*, const int32_t* seg,
+                                 int nseg, hipStream_t s) {
   if (root_device_ < 0) throw std::runtime_error("GraphModel: to_device() not called");
   Aux& a = aux_for(s, rows, cols);
   const bool multi = a.ev_start.get() != nullptr;
@@ -215,7 +216,8 @@ void GraphModel::launch(const double* X, int rows, int cols, double* out, void*,
     double* o = direct_out ? out : a.out[i].as<double>();
     if (st.kind == GraphStage::kModel) {
       const int ic = st.inputs[0] < 0 ? cols : a.cols[size_t(st.inputs[0])];
-      st.model->launch(in_ptr[0], rows, ic, o, a.ws[i].get(), ss);
+      if (seg && st.model->segmented()) st.model->launch_segments(in_ptr[0], rows, ic, o, a.ws[i].get(), seg, nseg, ss);
+      else st.model->launch(in_ptr[0], rows, ic, o, a.ws[i].get(), ss);
     } else {
       const double** arr = a.ptrs[i].host<const double*>();
       for (size_t k = 0; k < n_in; ++k) arr[k] = in_ptr[k];

@@ -60,7 +60,16 @@ class GraphModel : public RowModel {
       if (s.model && s.model->device_io_only()) return true;
     return false;
   }
-  void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override {
+    launch_segments(X, rows, cols, out, ws, nullptr, 0, s);
+  }
+  bool segmented() const override {
+    for (const auto& s : st_)
+      if (s.model && s.model->segmented()) return true;
+    return false;
+  }
+  void launch_segments(const double* X, int rows, int cols, double* out, void* ws, const int32_t* seg, int nseg,
+                       hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
 
   std::shared_ptr<RowModel> clone() const override { return clone_on(-2); }

@@ -231,4 +231,22 @@ void MeanSigmoidModel::run_cpu(const double* X, int rows, int cols, double* out)
   }
 }
 
+// ------------------------------------------------------------------ minmax
+void MinMaxModel::launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) {
+  kern::minmax_normalize_f64(X, int64_t(rows) * cols, out, static_cast<double*>(ws), s);
+}
+
+void MinMaxModel::launch_segments(const double* X, int, int cols, double* out, void*, const int32_t* seg, int nseg,
+                                  hipStream_t s) {
+  kern::segment_minmax_f64(X, seg, nseg, cols, out, s);
+}
+
+void MinMaxModel::run_cpu(const double* X, int rows, int cols, double* out) const {
+  const size_t n = size_t(rows) * cols;
+  if (!n) return;
+  const auto mm = std::minmax_element(X, X + n);
+  const double lo = *mm.first, range = *mm.second - *mm.first;
+  for (size_t i = 0; i < n; ++i) out[i] = range == 0.0 ? 0.0 : (X[i] - lo) / range;
+}
+
 }  // namespace sca::gpu

@@ -36,6 +36,15 @@ class RowModel {
   // False if many workgroups re-read X (stage it in HBM instead of reading
   // pinned host memory over PCIe from every workgroup).
   virtual bool zero_copy_input() const { return true; }
+  // Segment-aware models compute per request (not per row): the batcher passes
+  // the request boundaries (nseg + 1 row offsets, device-visible).
+  virtual bool segmented() const { return false; }
+  virtual void launch_segments(const double* X, int rows, int cols, double* out, void* ws, const int32_t* seg, int nseg,
+                               hipStream_t s) {
+    (void)seg;
+    (void)nseg;
+    launch(X, rows, cols, out, ws, s);
+  }
   virtual size_t workspace_bytes(int max_rows, int cols) const { (void)max_rows; (void)cols; return 0; }
   virtual void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) = 0;
   virtual void run_cpu(const double* X, int rows, int cols, double* out) const = 0;
@@ -142,6 +151,24 @@ class MeanSigmoidModel : public RowModel {
 
  private:
   double thr_;
+};
+
+// ------------------------------------------------------- min-max transform
+// (X - min) / (max - min) over each request's whole X (0 if constant):
+// examples/transformers/mean_transformer/MeanTransformer.py:8-12.
+class MinMaxModel : public RowModel {
+ public:
+  std::string name() const override { return "minmax"; }
+  int in_cols() const override { return 0; }
+  int out_cols(int c) const override { return c; }
+  void to_device(int) override {}
+  bool segmented() const override { return true; }
+  size_t workspace_bytes(int, int) const override { return 2 * sizeof(double); }
+  void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  void launch_segments(const double* X, int rows, int cols, double* out, void* ws, const int32_t* seg, int nseg,
+                       hipStream_t s) override;
+  void run_cpu(const double* X, int rows, int cols, double* out) const override;
+  std::shared_ptr<RowModel> clone() const override { return with_meta(std::make_shared<MinMaxModel>()); }
 };
 
 }  // namespace sca::gpu

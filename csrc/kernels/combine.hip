@@ -175,6 +175,31 @@ __global__ __launch_bounds__(kBlock) void mean_sigmoid(const double* __restrict_
   if (lane == 0) out[r] = 1.0 / (1.0 + exp(-(s / double(F) - threshold)));
 }
 
+// Per-request min-max normalisation over a micro-batch: block b owns the rows
+// [seg[b], seg[b+1]) of one request (MeanTransformer normalises each request's
+// X by that request's own global min / max).
+__global__ __launch_bounds__(kBlock) void segment_minmax(const double* __restrict__ in, const int32_t* __restrict__ seg,
+                                                         int cols, double* __restrict__ out) {
+  __shared__ double smin[kBlock / 64], smax[kBlock / 64];
+  const int64_t b0 = int64_t(seg[blockIdx.x]) * cols, b1 = int64_t(seg[blockIdx.x + 1]) * cols;
+  double lo = DBL_MAX, hi = -DBL_MAX;
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += kBlock) {
+    const double v = in[i];
+    lo = fmin(lo, v);
+    hi = fmax(hi, v);
+  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) { smin[w] = lo; smax[w] = hi; }
+  __syncthreads();
+  lo = smin[0];
+  hi = smax[0];
+  for (int j = 1; j < kBlock / 64; ++j) { lo = fmin(lo, smin[j]); hi = fmax(hi, smax[j]); }
+  const double range = hi - lo;
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += kBlock) out[i] = range == 0.0 ? 0.0 : (in[i] - lo) / range;
+}
+
 int grid_for(int64_t n) {
   int64_t g = (n + kBlock - 1) / kBlock;
   if (g > 2048) g = 2048;
@@ -192,6 +217,11 @@ void combine_mean_f64(const double* const* inputs, int n_inputs, int64_t n, doub
 void combine_mean_strided_f64(const double* base, int k, int64_t n, double* out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(mean_strided_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, base, k, n, out);
+}
+
+void segment_minmax_f64(const double* in, const int32_t* seg, int nseg, int cols, double* out, hipStream_t s) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(segment_minmax, dim3(nseg), dim3(kBlock), 0, s, in, seg, cols, out);
 }
 
 void fill_i32x4(int32_t* dst, int a, int b, int c, int d, hipStream_t s) {

@@ -1,0 +1,64 @@
+// Image pre-processing for the ImageNet ensemble example (SURVEY K14;
+// reference examples/models/openvino_imagenet_ensemble/resources/transformer/
+// ImageNetTransformer.py:20-63: cv2 decode -> centre crop (bilinear up-size of
+// an axis shorter than the crop, cv2.INTER_LINEAR) -> HWC uint8 to CHW float).
+//
+// One fused pass: every output element (c, y, x) computes its source
+// coordinate in the decoded HWC image (resize + crop folded into one affine
+// map), samples bilinearly in uint8 and writes fp32 CHW -- the intermediate
+// resized image never exists.  Threads are laid out along x so the fp32
+// stores are coalesced; the uint8 HWC gathers hit L2 (a 224x224 crop of a
+// multi-megapixel image is < 1 MiB).
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace sca::kern {
+namespace {
+
+// cv2 INTER_LINEAR source coordinate for destination index d along an axis
+// resized from n_src to n_dst (pixel-centre aligned, clamped).
+__device__ __forceinline__ void lin_src(int d, int n_src, int n_dst, int& i0, int& i1, float& w) {
+  if (n_src == n_dst) {
+    i0 = i1 = d;
+    w = 0.f;
+    return;
+  }
+  const float scale = float(n_src) / float(n_dst);
+  float s = (float(d) + 0.5f) * scale - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = int(s);
+  if (i0 > n_src - 1) i0 = n_src - 1;
+  i1 = i0 + 1 < n_src ? i0 + 1 : n_src - 1;
+  w = s - float(i0);
+}
+
+__global__ __launch_bounds__(256) void crop_resize_chw(const uint8_t* __restrict__ img, int H, int W, int C,
+                                                       int rh, int rw, int crop, float* __restrict__ out) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  const int y = blockIdx.y;
+  if (x >= crop) return;
+  // Resized image is rh x rw; crop window starts at its centre.
+  const int sx = rw / 2 - crop / 2 + x, sy = rh / 2 - crop / 2 + y;
+  int x0, x1, y0, y1;
+  float wx, wy;
+  lin_src(sx, W, rw, x0, x1, wx);
+  lin_src(sy, H, rh, y0, y1, wy);
+  for (int c = 0; c < C; ++c) {
+    const float p00 = img[(size_t(y0) * W + x0) * C + c], p01 = img[(size_t(y0) * W + x1) * C + c];
+    const float p10 = img[(size_t(y1) * W + x0) * C + c], p11 = img[(size_t(y1) * W + x1) * C + c];
+    float v = (p00 * (1.f - wx) + p01 * wx) * (1.f - wy) + (p10 * (1.f - wx) + p11 * wx) * wy;
+    if (rw != W || rh != H) v = rintf(v);  // cv2 resizes uint8 -> uint8 (rounded) before the float cast
+    out[(size_t(c) * crop + y) * crop + x] = v;
+  }
+}
+
+}  // namespace
+
+void crop_resize_chw_u8(const uint8_t* img, int H, int W, int C, int crop, float* out, hipStream_t s) {
+  const int rh = H < crop ? crop : H, rw = W < crop ? crop : W;
+  hipLaunchKernelGGL(crop_resize_chw, dim3((crop + 255) / 256, crop), dim3(256), 0, s, img, H, W, C, rh, rw, crop,
+                     out);
+}
+
+}  // namespace sca::kern

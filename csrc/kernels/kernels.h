@@ -73,6 +73,10 @@ void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_
 void combine_mean_f64(const double* const* inputs, int n_inputs, int64_t n, double* out, hipStream_t stream);
 // out = mean over k slabs base[j*n : (j+1)*n] (gathered replica outputs).
 void combine_mean_strided_f64(const double* base, int k, int64_t n, double* out, hipStream_t stream);
+// Per-segment (request) global min-max normalisation; seg = nseg+1 row offsets.
+void segment_minmax_f64(const double* in, const int32_t* seg, int nseg, int cols, double* out, hipStream_t stream);
+// Decoded HWC uint8 image -> centre crop (bilinear up-size of short axes) -> CHW fp32.
+void crop_resize_chw_u8(const uint8_t* img, int H, int W, int C, int crop, float* out, hipStream_t stream);
 // dst[0..3] = {a, b, c, d} (device-side header for fabric transfers).
 void fill_i32x4(int32_t* dst, int a, int b, int c, int d, hipStream_t stream);
 // Row softmax / argmax over [rows, C].

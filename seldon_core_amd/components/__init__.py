@@ -20,3 +20,4 @@ def register(name: str):
 
 
 from . import routers  # noqa: E402,F401  (registers EPSILON_GREEDY / THOMPSON_SAMPLING)
+from . import examples  # noqa: E402,F401  (MEAN_TRANSFORMER, MEAN_CLASSIFIER, IMAGENET_*, ...)

@@ -1,0 +1,171 @@
+"""The reference's example transformers / models / combiners,
+with the same class names, constructor parameters and method signatures, but
+backed by the engine's GPU kernels when they sit in a graph:
+
+* ``MeanTransformer`` -- examples/transformers/mean_transformer/MeanTransformer.py:8-12:
+  per-request global min-max normalisation -> native ``minmax`` row model
+  (``segment_minmax`` kernel: one workgroup per request of a micro-batch).
+* ``MeanClassifier`` -- examples/models/mean_classifier/MeanClassifier.py:19-27:
+  ``sigmoid(mean(row) - threshold)`` -> native ``mean_sigmoid`` row model.
+* ``MnistCombiner`` -- examples/combiners/mnist_combiner/MnistCombiner.py:8-11.
+* ``OutputTransformer`` -- examples/output_transformers/OutputTransformer.py:9-11.
+* ``ImageNetTransformer`` / ``ImageNetCombiner`` / ``ImageNetOutputTransformer``
+  -- examples/models/openvino_imagenet_ensemble/resources/{transformer,combiner}:
+  JPEG decode on the host, centre crop / resize / HWC->CHW on the GPU
+  (``crop_resize_chw`` kernel), average of two model outputs, argmax -> class name.
+"""
+from __future__ import annotations
+
+import base64
+import io
+import json
+import logging
+import os
+from typing import List, Optional
+
+import numpy as np
+
+from . import register
+
+logger = logging.getLogger(__name__)
+
+
+def _native():
+    from .._native import native
+
+    return native()
+
+
+@register("MEAN_TRANSFORMER")
+class MeanTransformer:
+    def transform_input(self, X, feature_names):
+        X = np.asarray(X, dtype=float)
+        if X.max() == X.min():
+            return np.zeros_like(X)
+        return (X - X.min()) / (X.max() - X.min())
+
+    def row_model(self):
+        return _native().minmax_model()
+
+
+@register("MEAN_CLASSIFIER")
+class MeanClassifier:
+    def __init__(self, intValue: int = 0, model_path: str = "model.npy", threshold: Optional[float] = None):
+        if not isinstance(intValue, int):
+            raise TypeError("intValue parameters must be an integer")
+        self.class_names = ["proba"]
+        self.int_value = intValue
+        if threshold is None:
+            base = 0.0
+            if os.path.exists(model_path):
+                base = float(np.load(model_path, allow_pickle=False).mean())
+            threshold = base + intValue
+        self.threshold_ = float(threshold)
+
+    def predict(self, X, feature_names):
+        X = np.asarray(X, dtype=float)
+        if X.ndim != 2:
+            raise ValueError("Incorrect shape")
+        return 1.0 / (1.0 + np.exp(-(X.mean(axis=1, keepdims=True) - self.threshold_)))
+
+    def row_model(self):
+        m = _native().mean_sigmoid_model(self.threshold_)
+        m.set_class_names(self.class_names)
+        return m
+
+
+@register("MNIST_COMBINER")
+class MnistCombiner:
+    def __init__(self, metrics_ok: bool = True):
+        pass
+
+    def aggregate(self, Xs, features_names):
+        return (np.asarray(Xs[0]) + np.asarray(Xs[1])) / 2.0
+
+
+@register("APPEND_ONE_OUTPUT_TRANSFORMER")
+class OutputTransformer:
+    def transform_output(self, X, names):
+        return np.vstack((X, np.array([1])))
+
+
+def _tftensor_json(arr: np.ndarray) -> dict:
+    return {"dtype": "DT_FLOAT", "tensorShape": {"dim": [{"size": str(int(d))} for d in arr.shape]},
+            "tensorContent": base64.b64encode(np.ascontiguousarray(arr, dtype="<f4").tobytes()).decode()}
+
+
+def _tftensor_array(t: dict) -> np.ndarray:
+    shape = [int(d.get("size", 0)) for d in (t.get("tensorShape") or {}).get("dim", [])]
+    if t.get("tensorContent"):
+        dt = {"DT_FLOAT": "<f4", "DT_DOUBLE": "<f8"}.get(t.get("dtype", "DT_FLOAT"), "<f4")
+        a = np.frombuffer(base64.b64decode(t["tensorContent"]), dtype=dt)
+    else:
+        a = np.asarray(t.get("floatVal") or t.get("doubleVal") or [], dtype=np.float64)
+    return a.reshape(shape) if shape else a
+
+
+@register("IMAGENET_TRANSFORMER")
+class ImageNetTransformer:
+    def __init__(self, metrics_ok: bool = True, size: int = 224, classes: int = 1000, device: Optional[int] = None):
+        self.size = int(os.environ.get("SIZE", size))
+        self.classes = int(os.environ.get("CLASSES", classes))
+        self.device = device
+
+    def _use_gpu(self) -> bool:
+        try:
+            import torch
+
+            return torch.cuda.is_available() and self.device != -1
+        except Exception:
+            return False
+
+    def preprocess(self, jpeg: bytes) -> np.ndarray:
+        from PIL import Image
+
+        img = np.asarray(Image.open(io.BytesIO(jpeg)).convert("RGB"))[:, :, ::-1]  # BGR, as cv2.imdecode
+        img = np.ascontiguousarray(img)
+        if self._use_gpu():
+            import torch
+
+            from .. import ops
+
+            t = torch.from_numpy(img).cuda(self.device or 0)
+            out = ops.crop_resize_chw(t, self.size).cpu().numpy()
+        else:
+            from ..ops import crop_resize_chw_ref
+
+            out = crop_resize_chw_ref(img, self.size)
+        return out.reshape(1, 3, self.size, self.size)
+
+    def transform_input_raw(self, request: dict) -> dict:
+        jpeg = base64.b64decode(request["binData"]) if isinstance(request.get("binData"), str) else request["binData"]
+        X = self.preprocess(jpeg)
+        return {"data": {"names": ["x"], "tftensor": _tftensor_json(X)}}
+
+
+@register("IMAGENET_COMBINER")
+class ImageNetCombiner:
+    def aggregate(self, Xs, features_names):
+        return (np.reshape(Xs[0], (1, -1)) + np.reshape(Xs[1], (1, -1))) / 2.0
+
+
+@register("IMAGENET_OUTPUT_TRANSFORMER")
+class ImageNetOutputTransformer:
+    def __init__(self, classes: int = 1000, class_names_path: str = ""):
+        self.classes = int(os.environ.get("CLASSES", classes))
+        self.cnames: List[str] = [str(i) for i in range(self.classes)]
+        if class_names_path and os.path.exists(class_names_path):
+            with open(class_names_path) as f:
+                names = json.load(f)  # JSON list or {index: name}
+            self.cnames = [names[str(i)] if isinstance(names, dict) else names[i] for i in range(self.classes)]
+
+    def transform_output_raw(self, request: dict) -> dict:
+        data = request.get("data") or {}
+        if "tftensor" in data:
+            result = _tftensor_array(data["tftensor"])
+        elif "tensor" in data:
+            result = np.asarray(data["tensor"]["values"], dtype=float)
+        else:
+            result = np.asarray(data.get("ndarray"), dtype=float)
+        result = np.reshape(result, (1, self.classes))
+        return {"strData": self.cnames[int(np.argmax(result[0]))]}

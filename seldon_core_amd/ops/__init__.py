@@ -1,1 +1,157 @@
-"""ops"""
+"""Torch-facing wrappers over the engine's hand-written gfx950 kernels.
+
+Each op takes/returns ``torch`` tensors resident on an MI355X and launches the
+HIP kernel from ``seldon_core_amd._C.kernels`` on the current HIP stream (so it
+orders with surrounding torch work and can be captured in a hipGraph).  There
+is no silent fallback: calling an op on CPU tensors or without the native
+extension raises.  CPU references for the tests live next to each op.
+
+Kernel sources: csrc/kernels/{linear,combine,image,tree,bandit}.hip.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+from .._native import native
+
+
+def _k():
+    return native().kernels
+
+
+def _check(t, dtype=None, name="tensor"):
+    import torch
+
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+def _stream(t) -> int:
+    import torch
+
+    return int(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+ACT = {"identity": 0, "softmax": 1, "binary_logistic": 2, "ovr": 3, "sigmoid": 4}
+
+
+def linear(X, W, b, act: str = "softmax"):
+    """act(X @ W.T + b), fp64 (sklearn linear models' predict_proba)."""
+    import torch
+
+    X = _check(X, torch.float64, "X")
+    W = _check(W, torch.float64, "W")
+    b = _check(b, torch.float64, "b")
+    C, K = W.shape
+    oc = 2 if act == "binary_logistic" else C
+    out = torch.empty((X.shape[0], oc), dtype=torch.float64, device=X.device)
+    _k().linear_f64(X.data_ptr(), X.shape[0], K, W.data_ptr(), b.data_ptr(), C, ACT[act], out.data_ptr(), _stream(X))
+    return out
+
+
+def softmax_rows(x):
+    import torch
+
+    x = _check(x, torch.float64, "x")
+    out = torch.empty_like(x)
+    _k().softmax_rows_f64(x.data_ptr(), x.shape[0], x.shape[1], out.data_ptr(), _stream(x))
+    return out
+
+
+def argmax_rows(x):
+    import torch
+
+    x = _check(x, torch.float64, "x")
+    out = torch.empty((x.shape[0],), dtype=torch.int32, device=x.device)
+    _k().argmax_rows_f64(x.data_ptr(), x.shape[0], x.shape[1], out.data_ptr(), _stream(x))
+    return out
+
+
+def combine_mean(xs: Sequence):
+    """Element-wise mean of same-shaped fp64 tensors (AVERAGE_COMBINER)."""
+    import torch
+
+    xs = [_check(x, torch.float64, "input") for x in xs]
+    shape = xs[0].shape
+    if any(x.shape != shape for x in xs):
+        raise ValueError("combine_mean inputs must share a shape")
+    ptrs = torch.tensor([x.data_ptr() for x in xs], dtype=torch.int64, device=xs[0].device)
+    out = torch.empty_like(xs[0])
+    _k().combine_mean_f64(ptrs.data_ptr(), len(xs), out.numel(), out.data_ptr(), _stream(out))
+    return out
+
+
+def minmax_normalize(x):
+    import torch
+
+    x = _check(x, torch.float64, "x")
+    out = torch.empty_like(x)
+    scratch = torch.empty(2, dtype=torch.float64, device=x.device)
+    _k().minmax_normalize_f64(x.data_ptr(), x.numel(), out.data_ptr(), scratch.data_ptr(), _stream(x))
+    return out
+
+
+def segment_minmax(x, row_offsets: List[int]):
+    """Per-segment min-max normalisation of the rows of a 2-D tensor."""
+    import torch
+
+    x = _check(x, torch.float64, "x")
+    seg = torch.tensor(list(row_offsets), dtype=torch.int32, device=x.device)
+    out = torch.empty_like(x)
+    _k().segment_minmax_f64(x.data_ptr(), seg.data_ptr(), len(row_offsets) - 1, x.shape[1], out.data_ptr(),
+                            _stream(x))
+    return out
+
+
+def mean_sigmoid(x, threshold: float):
+    import torch
+
+    x = _check(x, torch.float64, "x")
+    out = torch.empty((x.shape[0], 1), dtype=torch.float64, device=x.device)
+    _k().mean_sigmoid_rows_f64(x.data_ptr(), x.shape[0], x.shape[1], float(threshold), out.data_ptr(), _stream(x))
+    return out
+
+
+def crop_resize_chw(img, crop: int = 224):
+    """Decoded HWC uint8 image -> [C, crop, crop] fp32 (centre crop; axes
+    shorter than ``crop`` are bilinearly up-sized first, as cv2 does)."""
+    import torch
+
+    img = _check(img, torch.uint8, "img")
+    H, W, C = img.shape
+    out = torch.empty((C, crop, crop), dtype=torch.float32, device=img.device)
+    _k().crop_resize_chw_u8(img.data_ptr(), H, W, C, crop, out.data_ptr(), _stream(img))
+    return out
+
+
+# ------------------------------------------------------------ CPU references
+def crop_resize_chw_ref(img, crop: int = 224):
+    """numpy reference of :func:`crop_resize_chw` (same fused bilinear map)."""
+    import numpy as np
+
+    H, W, C = img.shape
+    rh, rw = max(H, crop), max(W, crop)
+
+    def axis(n_src, n_dst, idx):
+        if n_src == n_dst:
+            return idx, idx, np.zeros(len(idx), np.float32)
+        s = (idx.astype(np.float32) + 0.5) * np.float32(n_src / n_dst) - 0.5
+        s = np.maximum(s, 0)
+        i0 = np.minimum(s.astype(np.int64), n_src - 1)
+        i1 = np.minimum(i0 + 1, n_src - 1)
+        return i0, i1, (s - i0).astype(np.float32)
+
+    xs = rw // 2 - crop // 2 + np.arange(crop)
+    ys = rh // 2 - crop // 2 + np.arange(crop)
+    x0, x1, wx = axis(W, rw, xs)
+    y0, y1, wy = axis(H, rh, ys)
+    f = img.astype(np.float32)
+    top = f[y0][:, x0] * (1 - wx)[None, :, None] + f[y0][:, x1] * wx[None, :, None]
+    bot = f[y1][:, x0] * (1 - wx)[None, :, None] + f[y1][:, x1] * wx[None, :, None]
+    v = top * (1 - wy)[:, None, None] + bot * wy[:, None, None]
+    if rw != W or rh != H:
+        v = np.rint(v)
+    return v.transpose(2, 0, 1).astype(np.float32)
