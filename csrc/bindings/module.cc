@@ -12,6 +12,7 @@
 #include "../core/msglog.h"
 #include "../gpu/batcher.h"
 #include "../gpu/graph.h"
+#include "../gpu/mlp_model.h"
 #include "../gpu/replica.h"
 #include "../gpu/models.h"
 #include "../gpu/router.h"
@@ -199,6 +200,30 @@ PYBIND11_MODULE(_C, m) {
     if (!g) throw std::runtime_error("not a graph model");
     return g->devices();
   });
+  auto to_layers = [](py::list ls) {
+    std::vector<gpu::DenseLayer> out;
+    for (auto h : ls) {
+      py::dict d = h.cast<py::dict>();
+      auto W = d["W"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+      auto b = d["b"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+      if (W.ndim() != 2) throw std::runtime_error("layer W must be [out, in]");
+      gpu::DenseLayer L;
+      L.N = int(W.shape(0));
+      L.K = int(W.shape(1));
+      L.W = to_vec(W);
+      L.b = to_vec(b);
+      L.act = d.contains("act") ? d["act"].cast<int>() : 0;
+      out.push_back(std::move(L));
+    }
+    return out;
+  };
+  m.def("mlp_model", [to_layers](py::list layers, int out_mode) {
+    return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MlpModel>(to_layers(layers), out_mode));
+  }, py::arg("layers"), py::arg("out_mode") = 0);
+  m.def("vae_model", [to_layers](py::list encoder, int latent, py::list decoder, int samples, uint64_t seed) {
+    return std::static_pointer_cast<gpu::RowModel>(
+        gpu::MlpModel::vae(to_layers(encoder), latent, to_layers(decoder), samples, seed));
+  }, py::arg("encoder"), py::arg("latent"), py::arg("decoder"), py::arg("samples") = 10, py::arg("seed") = 0);
   m.def("minmax_model", [] { return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MinMaxModel>()); });
   m.def("mean_sigmoid_model", [](double thr) {
     return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MeanSigmoidModel>(thr));
@@ -577,6 +602,11 @@ PYBIND11_MODULE(_C, m) {
   });
   k.def("combine_mean_strided_f64", [](uintptr_t base, int k_, int64_t n, uintptr_t out, uintptr_t s) {
     kern::combine_mean_strided_f64(P<const double>(base), k_, n, P<double>(out), as_stream(s));
+  });
+  k.def("mahalanobis_sm_scores", [](uintptr_t B, uintptr_t cov0, uintptr_t xd, int nb, int k_, double n, uintptr_t out,
+                                     uintptr_t s) {
+    return kern::mahalanobis_sm_scores(P<const double>(B), P<const double>(cov0), P<const double>(xd), nb, k_, n,
+                                       P<double>(out), as_stream(s));
   });
   k.def("mean_sigmoid_rows_f64", [](uintptr_t in, int rows, int F, double thr, uintptr_t out, uintptr_t s) {
     kern::mean_sigmoid_rows_f64(P<const double>(in), rows, F, thr, P<double>(out), as_stream(s));

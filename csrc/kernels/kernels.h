@@ -77,6 +77,43 @@ void combine_mean_strided_f64(const double* base, int k, int64_t n, double* out,
 void segment_minmax_f64(const double* in, const int32_t* seg, int nseg, int cols, double* out, hipStream_t stream);
 // Decoded HWC uint8 image -> centre crop (bilinear up-size of short axes) -> CHW fp32.
 void crop_resize_chw_u8(const uint8_t* img, int H, int W, int C, int crop, float* out, hipStream_t stream);
+// ------------------------------------------------------------ fused MLP
+// A whole dense network (and the VAE outlier detector's encoder -> MC
+// reparameterised decoder -> reconstruction-MSE loop) in one launch: a
+// 256-thread workgroup owns a 16-row tile, keeps every activation in LDS and
+// runs each Dense layer on f32-input MFMA (v_mfma_f32_16x16x4_f32: exact fp32
+// products, i.e. Keras/torch float32 numerics) with bias + activation fused
+// into the epilogue.  Weights are stored transposed and zero-padded
+// (Wt [Kp][Np], Kp % 4 == 0, Np % 16 == 0) so B-fragment loads are coalesced
+// and the K loop has no bounds checks.
+enum MlpOpType : int { kMlpDense = 0, kMlpDenseMse = 1, kMlpReparam = 2 };
+enum MlpAct : int { kMlpIdentity = 0, kMlpRelu = 1, kMlpSigmoid = 2, kMlpTanh = 3 };
+struct MlpOp {
+  int type, act;
+  int in_buf, out_buf;
+  int K, Kp, N, Np;        // Reparam: N = latent dim (input holds [mean | log_var])
+  long long w_off, b_off;  // float offsets into the parameter blob
+};
+constexpr int kMlpMaxOps = 24;
+constexpr int kMlpMaxBufs = 6;
+constexpr int kMlpRows = 16;  // rows per workgroup (one MFMA tile)
+struct MlpProgram {
+  int n_pre = 0, n_loop = 0, loops = 0;  // ops[0, n_pre) once; ops[n_pre, n_pre + n_loop) `loops` times
+  int F = 0, Fp = 0;                     // input width (buffer 0 keeps the input tile)
+  int buf_off[kMlpMaxBufs] = {}, buf_ld[kMlpMaxBufs] = {};
+  int out_buf = 0, out_dim = 0, out_softmax = 0;
+  int mse_mode = 0, mse_dim = 0;         // 1: out[r] = mean over loops of mean_c (recon - x)^2
+  int lds_floats = 0;
+  MlpOp ops[kMlpMaxOps];
+};
+void mlp_forward(const double* X, int rows, const MlpProgram& prog, const float* params, uint64_t seed,
+                 uint64_t offset, double* out, hipStream_t stream);
+
+// Mahalanobis detector: Sherman-Morrison recurrence + scores over a batch
+// (B [nb][k][k], cov0 [k][k], xd [nb][k]); false if k > 16.
+bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd, int nb, int k, double n, double* out,
+                           hipStream_t stream);
+
 // dst[0..3] = {a, b, c, d} (device-side header for fabric transfers).
 void fill_i32x4(int32_t* dst, int a, int b, int c, int d, hipStream_t stream);
 // Row softmax / argmax over [rows, C].

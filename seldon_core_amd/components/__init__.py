@@ -21,3 +21,4 @@ def register(name: str):
 
 from . import routers  # noqa: E402,F401  (registers EPSILON_GREEDY / THOMPSON_SAMPLING)
 from . import examples  # noqa: E402,F401  (MEAN_TRANSFORMER, MEAN_CLASSIFIER, IMAGENET_*, ...)
+from . import outlier  # noqa: E402,F401  (MAHALANOBIS_OD, ISOLATION_FOREST_OD, VAE_OD, SEQ2SEQ_OD)

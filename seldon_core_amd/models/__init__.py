@@ -24,6 +24,15 @@ def to_row_model(obj: Any, method: str = "predict_proba"):
 
     C = native()
     spec: Any = obj
+    from .mlp import from_sklearn_mlp, from_torch
+
+    for conv in (from_sklearn_mlp, lambda o, m: from_torch(o) if _is_torch_module(o) else None):
+        try:
+            rm = conv(obj, method)
+        except Exception:
+            rm = None
+        if rm is not None:
+            return rm
     if not isinstance(obj, (LinearSpec, TreeEnsemble)):
         try:
             spec = from_sklearn_linear(obj, method)
@@ -45,6 +54,15 @@ def to_row_model(obj: Any, method: str = "predict_proba"):
         m.set_class_names(list(spec.class_names))
     m.flat_output = bool(spec.flat_output)
     return m
+
+
+def _is_torch_module(obj: Any) -> bool:
+    try:
+        import torch.nn as nn
+
+        return isinstance(obj, nn.Module)
+    except Exception:
+        return False
 
 
 def _is_classifier(obj: Any) -> bool:

@@ -127,6 +127,25 @@ def crop_resize_chw(img, crop: int = 224):
     return out
 
 
+def mahalanobis_sm_scores(B, proj_cov, x_diff, n: float, device: int = 0):
+    """Sherman-Morrison inverse recurrence + Mahalanobis scores for one batch
+    (numpy in/out; None if k > 16 -- caller falls back to numpy)."""
+    import numpy as np
+    import torch
+
+    nb, k = x_diff.shape
+    if k > 16:
+        return None
+    dev = torch.device(f"cuda:{device}")
+    tB = torch.as_tensor(np.ascontiguousarray(B, dtype=np.float64), device=dev)
+    tC = torch.as_tensor(np.ascontiguousarray(proj_cov, dtype=np.float64), device=dev)
+    tX = torch.as_tensor(np.ascontiguousarray(x_diff, dtype=np.float64), device=dev)
+    out = torch.empty(nb, dtype=torch.float64, device=dev)
+    ok = _k().mahalanobis_sm_scores(tB.data_ptr(), tC.data_ptr(), tX.data_ptr(), nb, k, float(n), out.data_ptr(),
+                                    _stream(out))
+    return out.cpu().numpy() if ok else None
+
+
 # ------------------------------------------------------------ CPU references
 def crop_resize_chw_ref(img, crop: int = 224):
     """numpy reference of :func:`crop_resize_chw` (same fused bilinear map)."""

@@ -1,0 +1,140 @@
+"""Fused MLP / VAE row models: CPU reference path vs sklearn / torch / numpy,
+and (GPU) the MFMA kernel vs the same references."""
+import numpy as np
+import pytest
+
+import seldon_core_amd as sca
+from seldon_core_amd.models import to_row_model
+from seldon_core_amd.models.mlp import OUT_SOFTMAX, layer, mlp_row_model, random_dense_stack
+
+
+def _sk_mlp(kind="clf", n_classes=3, hidden=(37, 19), activation="relu", seed=0):
+    from sklearn.neural_network import MLPClassifier, MLPRegressor
+
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(200, 13))
+    if kind == "clf":
+        y = rng.integers(0, n_classes, size=200)
+        est = MLPClassifier(hidden_layer_sizes=hidden, activation=activation, max_iter=50, random_state=seed)
+    else:
+        y = X[:, 0] * 2 + X[:, 1]
+        est = MLPRegressor(hidden_layer_sizes=hidden, activation=activation, max_iter=50, random_state=seed)
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        est.fit(X, y)
+    return est, X
+
+
+@pytest.mark.parametrize("activation", ["relu", "tanh", "logistic"])
+@pytest.mark.parametrize("n_classes", [2, 4])
+def test_sklearn_mlp_classifier_cpu(activation, n_classes):
+    est, X = _sk_mlp("clf", n_classes, activation=activation)
+    rm = to_row_model(est)
+    assert rm is not None and rm.name == "mlp"
+    np.testing.assert_allclose(rm.run_cpu(X), est.predict_proba(X), rtol=2e-5, atol=2e-6)
+    assert rm.class_names() == [str(c) for c in est.classes_]
+
+
+def test_sklearn_mlp_regressor_cpu():
+    est, X = _sk_mlp("reg")
+    rm = to_row_model(est, "predict")
+    assert rm.flat_output
+    np.testing.assert_allclose(rm.run_cpu(X)[:, 0], est.predict(X), rtol=1e-4, atol=1e-5)
+
+
+def test_torch_sequential_cpu():
+    import torch
+
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(9, 33), torch.nn.ReLU(), torch.nn.Linear(33, 5), torch.nn.Tanh(),
+                              torch.nn.Linear(5, 7), torch.nn.Softmax(dim=1))
+    rm = to_row_model(net)
+    X = np.random.default_rng(0).normal(size=(21, 9))
+    with torch.no_grad():
+        ref = net(torch.tensor(X, dtype=torch.float32)).double().numpy()
+    np.testing.assert_allclose(rm.run_cpu(X), ref, rtol=1e-5, atol=1e-6)
+
+
+def _vae_layers(F=12, hidden=(8, 6), latent=2, seed=0, logvar_bias=0.0):
+    enc = random_dense_stack([F, *hidden], ["relu"] * len(hidden), seed)
+    rng = np.random.default_rng(seed + 1)
+    head_W = rng.normal(scale=0.3, size=(2 * latent, hidden[-1]))
+    head_b = np.concatenate([np.zeros(latent), np.full(latent, logvar_bias)])
+    enc.append(layer(head_W, head_b, "identity"))
+    dec = random_dense_stack([latent, *hidden[::-1], F], ["relu"] * len(hidden) + ["sigmoid"], seed + 2)
+    return enc, dec
+
+
+def _np_dense(x, layers):
+    for L in layers:
+        z = x @ L["W"].T.astype(np.float64) + L["b"]
+        x = {0: z, 1: np.maximum(z, 0), 2: 1 / (1 + np.exp(-z)), 3: np.tanh(z)}[L["act"]]
+    return x
+
+
+def test_vae_cpu_deterministic_limit():
+    """With log_var -> -inf the sample is z_mean: score == MSE of the mean decode."""
+    C = sca.native()
+    enc, dec = _vae_layers(logvar_bias=-80.0)
+    rm = C.vae_model(enc, 2, dec, 10, 7)
+    X = np.random.default_rng(3).random(size=(9, 12))
+    h = _np_dense(X, enc)
+    recon = _np_dense(h[:, :2], dec)
+    want = ((recon - X) ** 2).mean(axis=1)
+    np.testing.assert_allclose(rm.run_cpu(X)[:, 0], want, rtol=1e-4)
+
+
+def test_vae_cpu_is_stochastic_and_positive():
+    C = sca.native()
+    enc, dec = _vae_layers(logvar_bias=0.0)
+    rm = C.vae_model(enc, 2, dec, 10, 7)
+    X = np.random.default_rng(3).random(size=(5, 12))
+    a, b = rm.run_cpu(X), rm.run_cpu(X)
+    assert (a > 0).all() and not np.array_equal(a, b)  # fresh MC draws per call
+
+
+def test_lds_budget_error():
+    C = sca.native()
+    with pytest.raises(Exception, match="LDS"):
+        C.mlp_model(random_dense_stack([2048, 2048, 10], ["relu", "identity"]), 0)
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", [(13, 37, 19, 3), (784, 256, 64, 10), (5, 1, 2), (64, 128, 128, 64, 33)])
+@pytest.mark.parametrize("rows", [1, 16, 37, 300])
+def test_mlp_gpu_matches_torch_fp32(dims, rows):
+    import torch
+
+    layers = random_dense_stack(list(dims), ["relu"] * (len(dims) - 2) + ["identity"], seed=len(dims))
+    rm = mlp_row_model(layers, OUT_SOFTMAX)
+    X = np.random.default_rng(rows).normal(size=(rows, dims[0]))
+    unit = sca.native().BatchedUnit(rm, 0)
+    try:
+        got = unit.run(X)
+    finally:
+        unit.stop()
+    x = torch.tensor(X, dtype=torch.float32)
+    for L in layers:
+        x = x @ torch.tensor(L["W"]).T + torch.tensor(L["b"])
+        if L["act"] == 1:
+            x = torch.relu(x)
+    ref = torch.softmax(x, 1).double().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_vae_gpu_matches_cpu_reference():
+    C = sca.native()
+    enc, dec = _vae_layers(F=30, hidden=(20, 10), latent=3)
+    gpu_m = C.vae_model(enc, 3, dec, 10, 11)
+    cpu_m = C.vae_model(enc, 3, dec, 10, 11)
+    X = np.random.default_rng(5).random(size=(40, 30))
+    unit = C.BatchedUnit(gpu_m, 0)
+    try:
+        got = unit.run(X)  # one launch = offset 0, same Philox streams as the CPU twin
+    finally:
+        unit.stop()
+    np.testing.assert_allclose(got[:, 0], cpu_m.run_cpu(X)[:, 0], rtol=2e-4)

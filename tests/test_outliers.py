@@ -1,0 +1,204 @@
+"""Outlier detectors against independent numpy statements of
+the reference algorithms (components/outlier-detection/*)."""
+import os
+
+import numpy as np
+import pytest
+
+import seldon_core_amd as sca
+from seldon_core_amd.components.outlier import (OutlierIsolationForest, OutlierMahalanobis, OutlierSeq2SeqLSTM,
+                                                 OutlierVAE, performance)
+
+
+def test_mahalanobis_online_mean_and_covariance_recursion():
+    """One row per request (CoreMahalanobis.py:89-101 with nb = 1): the mean is
+    the running sample mean and C_{n+1} = (n-1)/(n+1) C_n + n/(n+1)^2 d d^T,
+    d = x - mean_n (the reference's normalisation, not Welford's)."""
+    det = OutlierMahalanobis(n_components=3, start_clip=10 ** 9, device=-1)
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(60, 5)) * np.array([1, 2, 3, 0.5, 4])
+    mean, C = np.zeros(5), np.zeros((5, 5))
+    for i in range(len(X)):
+        det.predict(X[i:i + 1], [])
+        n = i
+        d = X[i] - mean
+        C = (n - 1.0) / (n + 1.0) * C + n / (n + 1.0) ** 2 * np.outer(d, d)
+        mean = mean + d / (n + 1.0)
+    np.testing.assert_allclose(det.mean, X.mean(axis=0), rtol=1e-12)
+    np.testing.assert_allclose(det.mean, mean, rtol=1e-12)
+    np.testing.assert_allclose(det.C, C, rtol=1e-10)
+
+
+def _oracle_scores(det_before, X):
+    """Scores of one batch by explicit inverses: C_i = inv(M_i),
+    M_0 = V^T C V, M_i = (n+i-2)/(n+i-1) M_{i-1} + B_{i-1}."""
+    from scipy.linalg import eigh
+
+    n = det_before["n"]
+    mean, C = det_before["mean"], det_before["C"]
+    nb, p = X.shape
+    k = det_before["k"]
+    steps = np.arange(nb)
+    roll = X.cumsum(axis=0) / (steps + 1)[:, None]
+    new_means = mean + ((steps + 1.0) / (steps + n + 1.0))[:, None] * (roll - mean)
+    means_off = np.vstack([mean[None, :], new_means[:-1]])
+    d = X - means_off
+    Bfull = ((n + steps) / (n + steps + 1.0))[:, None, None] * (d[:, :, None] * d[:, None, :])
+    cov = (n - 1.0) / (n + max(1, nb - 1.0)) * C + Bfull.sum(axis=0) / (n + max(1, nb - 1.0))
+    _, V = eigh(cov, subset_by_index=[p - k, p - 1])
+    dp = X @ V - means_off @ V
+    Bp = (1.0 / (n + steps + 1.0))[:, None, None] * (dp[:, :, None] * dp[:, None, :])
+    M = V.T @ C @ V
+    out = []
+    for i in range(nb):
+        if i > 0:
+            M = (n + i - 2.0) / (n + i - 1.0) * M + Bp[i - 1]
+        out.append(dp[i] @ np.linalg.inv(M) @ dp[i])
+    return np.array(out)
+
+
+def test_mahalanobis_batch_scores_match_explicit_inverse():
+    det = OutlierMahalanobis(threshold=10, n_components=3, start_clip=10 ** 9, device=-1)
+    rng = np.random.default_rng(1)
+    for _ in range(30):
+        det.predict(rng.normal(size=(2, 6)), [])
+    for nb in [1, 5, 17]:
+        X = rng.normal(size=(nb, 6))
+        before = {"n": det.n, "mean": np.array(det.mean), "C": np.array(det.C), "k": 3}
+        det.predict(X.copy(), [])
+        np.testing.assert_allclose(det.score, _oracle_scores(before, X), rtol=1e-8)
+
+
+def test_mahalanobis_flags_far_points_and_metrics():
+    det = OutlierMahalanobis(threshold=15, n_components=2, device=-1)
+    rng = np.random.default_rng(1)
+    for _ in range(10):
+        det.predict(rng.normal(size=(20, 4)), [])
+    p = det.predict(np.vstack([rng.normal(size=(5, 4)), np.full((1, 4), 12.0)]), [])
+    assert p[-1] == 1 and p[:5].sum() <= 1
+    m = {x["key"] for x in det.metrics()}
+    assert {"is_outlier", "outlier_score", "observation", "threshold"} <= m
+
+
+def test_isolation_forest_detector_matches_sklearn():
+    from sklearn.ensemble import IsolationForest
+
+    rng = np.random.default_rng(2)
+    clf = IsolationForest(n_estimators=50, random_state=0).fit(rng.normal(size=(500, 5)))
+    det = OutlierIsolationForest(threshold=0.0, model=clf, device=-1)
+    X = np.vstack([rng.normal(size=(30, 5)), rng.normal(size=(3, 5)) * 8])
+    pred = det.predict(X, [])
+    np.testing.assert_allclose(det.decision_val, clf.decision_function(X), rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(pred, (clf.decision_function(X) < 0).astype(int))
+
+
+def test_isolation_forest_from_npz(tmp_path):
+    rng = np.random.default_rng(3)
+    np.savez(tmp_path / "if.npz", X=rng.normal(size=(200, 4)))
+    det = OutlierIsolationForest(load_path=str(tmp_path) + "/", device=-1)
+    assert det.predict(rng.normal(size=(4, 4)), []).shape == (4,)
+
+
+def test_vae_detector_random_and_feedback_metrics():
+    det = OutlierVAE.random(n_features=10, hidden_layers=2, latent_dim=2, threshold=0.5, reservoir_size=50,
+                            device=-1)
+    rng = np.random.default_rng(4)
+    X = rng.random(size=(1, 10))
+    det.transform_input(X, [])
+    assert det.tags()["outlier-predictions"] in ([0], [1])
+    det.send_feedback(X, [], 0.0, np.array([1]))
+    det.predict(rng.random(size=(1, 10)), [])
+    keys = [m["key"] for m in det.metrics()]
+    assert keys[:5] == ["is_outlier", "mse", "observation", "threshold", "label"]
+    assert len(keys) == 23
+    for _ in range(60):  # the reservoir starts refreshing the scaling stats once full
+        det.predict(rng.random(size=(1, 10)), [])
+    assert det.N == 62 and len(det.batch) == 50
+
+
+def test_vae_weights_roundtrip(tmp_path):
+    from seldon_core_amd.components.outlier import load_vae_weights, random_vae_weights, save_vae_weights
+
+    w = random_vae_weights(8, hidden_layers=1, latent_dim=2)
+    save_vae_weights(str(tmp_path / "vae.npz"), w)
+    det = OutlierVAE(load_path=str(tmp_path) + "/", device=-1)
+    w2 = load_vae_weights(str(tmp_path / "vae.npz"))
+    assert w2["latent"] == 2 and len(w2["encoder"]) == len(w["encoder"])
+    assert det.predict(np.random.default_rng(0).random(size=(3, 8)), []).shape == (3,)
+
+
+def test_vae_in_graph_as_input_transformer():
+    det = OutlierVAE.random(n_features=4, threshold=0.1, device=-1)
+    from seldon_core_amd.models import iris_logistic_regression
+
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+            "graph": {"name": "od", "type": "TRANSFORMER", "children": [{"name": "clf", "type": "MODEL"}]}}
+    dep = sca.Deployment(spec, components={"od": det, "clf": iris_logistic_regression()}, device=-1)
+    try:
+        out = dep.predict({"data": {"ndarray": [[5.1, 3.5, 1.4, 0.2]]}})
+        assert "outlier-predictions" in out["meta"]["tags"]
+        assert len(out["data"]["ndarray"][0]) == 3
+        assert "mse" in {m["key"] for m in out["meta"]["metrics"]}
+    finally:
+        dep.close()
+
+
+def test_performance_helper():
+    scores = performance([0, 1, 1, 0], [0, 1, 0, 0])
+    assert scores[:4] == [2, 0, 1, 1] and scores[4] == 0.75
+
+
+def test_seq2seq_cpu_shapes_and_threshold():
+    det = OutlierSeq2SeqLSTM(threshold=0.5, timesteps=6, n_features=3, encoder_dim=(4,), decoder_dim=(8,),
+                             device=-1)
+    X = np.random.default_rng(5).random(size=(4, 6 * 3))
+    p = det.predict(X, [])
+    assert p.shape == (4,) and det.mse.shape == (4,) and (det.mse > 0).all()
+
+
+def test_registered_native_implementations():
+    from seldon_core_amd.components import NATIVE_IMPLEMENTATIONS
+
+    for k in ("MAHALANOBIS_OD", "ISOLATION_FOREST_OD", "VAE_OD", "SEQ2SEQ_OD", "EPSILON_GREEDY",
+              "THOMPSON_SAMPLING", "MEAN_TRANSFORMER"):
+        assert k in NATIVE_IMPLEMENTATIONS
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_mahalanobis_gpu_recurrence_matches_numpy():
+    rng = np.random.default_rng(6)
+    cpu = OutlierMahalanobis(threshold=10, n_components=4, device=-1)
+    gpu = OutlierMahalanobis(threshold=10, n_components=4, device=0, gpu_min_rows=1)
+    for nb in [1, 3, 300, 64, 1000]:
+        X = rng.normal(size=(nb, 9))
+        cpu.predict(X.copy(), [])
+        gpu.predict(X.copy(), [])
+        np.testing.assert_allclose(gpu.score, cpu.score, rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.gpu
+def test_vae_and_isolation_forest_on_gpu():
+    from sklearn.ensemble import IsolationForest
+
+    rng = np.random.default_rng(7)
+    clf = IsolationForest(n_estimators=100, random_state=0).fit(rng.normal(size=(400, 6)))
+    det = OutlierIsolationForest(model=clf, device=0)
+    X = rng.normal(size=(50, 6))
+    det.predict(X, [])
+    np.testing.assert_allclose(det.decision_val, clf.decision_function(X), rtol=1e-5, atol=1e-6)
+    vae = OutlierVAE.random(n_features=30, hidden_layers=2, latent_dim=3, device=0)
+    p = vae.predict(rng.random(size=(40, 30)), [])
+    assert p.shape == (40,) and np.isfinite(vae.mse).all()
+
+
+@pytest.mark.gpu
+def test_seq2seq_gpu_graph_matches_cpu():
+    cpu = OutlierSeq2SeqLSTM(timesteps=8, n_features=3, encoder_dim=(5,), decoder_dim=(10,), device=-1, seed=3)
+    gpu = OutlierSeq2SeqLSTM(timesteps=8, n_features=3, encoder_dim=(5,), decoder_dim=(10,), device=0, seed=3)
+    X = np.random.default_rng(8).random(size=(6, 8, 3))
+    a = cpu.net.reconstruct(X)
+    b = gpu.net.reconstruct(X)  # captured HIP graph
+    c = gpu.net.reconstruct(X)  # replay
+    np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-5)
+    np.testing.assert_array_equal(b, c)
