@@ -104,6 +104,7 @@ class MLFlowServer:
         self.device = device
         self.ready = False
         self._fn = None
+        self._model = None
 
     def load(self) -> None:
         root = Storage.download(self.model_uri)
@@ -127,6 +128,7 @@ class MLFlowServer:
                 p = os.path.join(root, f)
                 if os.path.exists(p):
                     m = joblib.load(p)
+                    self._model = m
                     self._fn = getattr(m, "predict")
                     break
         if self._fn is None:
@@ -138,22 +140,43 @@ class MLFlowServer:
             self.load()
         return self._fn(X)
 
+    def row_model(self):
+        """scikit-learn flavour with a native kernel (linear, trees, MLP): the
+        pyfunc ``predict`` is served by the GPU micro-batcher."""
+        m = getattr(self, "_model", None)
+        if m is None:
+            return None
+        from ..models import to_row_model
+
+        return to_row_model(m, "predict")
+
 
 class TFServingProxy:
     """TENSORFLOW_SERVER: the reference proxies to a TF Serving sidecar
-    (integrations/tfserving/TfServingProxy.py).  There is no TF Serving on this
-    platform; SavedModels must be exported to TorchScript and served by
-    MLFlowServer-style loading instead."""
+    (integrations/tfserving/TfServingProxy.py).  With ``rest_endpoint`` (and
+    ``model_name``) requests are forwarded to a TF Serving REST server; without
+    one the model directory is served in-process (TorchScript export on the GPU
+    via PyTorch-ROCm, or a scikit-learn flavour on the native kernels)."""
 
-    def __init__(self, model_uri: str = "", **kw):
+    def __init__(self, model_uri: str = "", rest_endpoint: str = "", model_name: str = "", **kw):
         self.model_uri = model_uri
-        self._inner = MLFlowServer(model_uri)
+        if rest_endpoint:
+            from .proxies import TfServingRestProxy
+
+            self._inner = TfServingRestProxy(rest_endpoint, model_name or "model", **kw)
+        else:
+            self._inner = MLFlowServer(model_uri)
 
     def load(self) -> None:
-        self._inner.load()
+        if hasattr(self._inner, "load"):
+            self._inner.load()
 
     def predict(self, X, names, meta=None):
         return self._inner.predict(X, names, meta)
+
+    def row_model(self):
+        rm = getattr(self._inner, "row_model", None)
+        return rm() if callable(rm) else None
 
 
 def load_prepackaged(impl: str, model_uri: str, params: Dict[str, Any]):
@@ -165,7 +188,7 @@ def load_prepackaged(impl: str, model_uri: str, params: Dict[str, Any]):
     elif impl == "MLFLOW_SERVER":
         s = MLFlowServer(model_uri)
     elif impl == "TENSORFLOW_SERVER":
-        s = TFServingProxy(model_uri)
+        s = TFServingProxy(model_uri, rest_endpoint=p.get("rest_endpoint", ""), model_name=p.get("model_name", ""))
     else:
         raise ValueError(f"unknown prepackaged server {impl}")
     s.load()

@@ -83,3 +83,17 @@ def test_microservice_tester(tmp_path):
     finally:
         h.stop()
         d.close()
+
+
+def test_loadtester_predict_and_feedback(server):
+    from seldon_core_amd import loadtester
+
+    out = loadtester.run_predict_load("127.0.0.1", server.http_port, "rest", users=8, threads=1, steps=1, warmup=0,
+                                      step_requests=200)
+    assert out["errors"] == 0 and out["ok"] >= 200
+    g = loadtester.run_predict_load("127.0.0.1", server.grpc_port, "grpc", users=8, threads=1, steps=1, warmup=0,
+                                    step_requests=200, data_size=6)
+    assert g["errors"] == 0
+    fb = loadtester.run_feedback_load("127.0.0.1", server.http_port, "none", [1.0], requests=20, workers=4,
+                                      namespace="seldon")
+    assert fb["requests"] == 20
