@@ -434,6 +434,25 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("finalize", &Engine::finalize)
       .def("inflight", &Engine::inflight)
+      .def("enable_tracing", &Engine::enable_tracing, py::arg("rate") = 1.0)
+      .def("drain_spans", [](Engine& e) {
+        py::list out;
+        for (auto& s : e.drain_spans()) {
+          py::dict d;
+          d["traceId"] = s.trace_id;
+          d["id"] = s.span_id;
+          if (!s.parent_id.empty()) d["parentId"] = s.parent_id;
+          d["name"] = s.name;
+          d["timestamp"] = s.start_us;
+          d["duration"] = std::max<int64_t>(1, s.dur_us);
+          py::dict tags;
+          tags["seldon.puid"] = s.puid;
+          if (s.error) tags["error"] = "true";
+          d["tags"] = tags;
+          out.append(d);
+        }
+        return out;
+      })
       .def("ready", &Engine::ready)
       .def("node_names", &Engine::node_names)
       .def("unit_kind", [](const Engine& e, const std::string& n) {

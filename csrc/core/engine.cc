@@ -168,6 +168,9 @@ std::string Engine::new_puid() {
 // ------------------------------------------------------------------ engine
 struct Engine::ReqCtx {
   std::string puid;
+  bool traced = false;
+  std::string trace_id, root_span;
+  int64_t t0_us = 0;
   std::mutex mu;
   std::vector<std::pair<std::string, int32_t>> routing;
   StrMap request_path;
@@ -323,6 +326,59 @@ void Engine::add_metrics(Node* n, const SeldonMessage& m, ReqCtx* ctx) {
   ctx->metrics.emplace_back(n->name, m.meta.metrics);
 }
 
+// ------------------------------------------------------------------ tracing
+namespace {
+int64_t wall_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+std::string rand_hex(int bytes) {
+  thread_local Xoshiro rng;
+  static const char* hx = "0123456789abcdef";
+  std::string s;
+  s.reserve(size_t(bytes) * 2);
+  uint64_t v = 0;
+  for (int i = 0; i < bytes * 2; ++i) {
+    if (i % 16 == 0) v = rng.next();
+    s.push_back(hx[v & 15]);
+    v >>= 4;
+  }
+  return s;
+}
+}  // namespace
+
+void Engine::push_span(TraceSpan s) {
+  std::lock_guard<std::mutex> g(span_mu_);
+  if (spans_.size() >= 200000) spans_.erase(spans_.begin(), spans_.begin() + 100000);  // exporter stalled: keep recent
+  spans_.push_back(std::move(s));
+}
+
+std::vector<TraceSpan> Engine::drain_spans() {
+  std::vector<TraceSpan> out;
+  std::lock_guard<std::mutex> g(span_mu_);
+  out.swap(spans_);
+  return out;
+}
+
+Done Engine::traced(const std::shared_ptr<ReqCtx>& ctx, const Node* n, const char* what, Done k) {
+  if (!ctx->traced) return k;
+  const int64_t t0 = wall_us();
+  std::string name = n->name + ":" + what;
+  return [this, ctx, t0, name = std::move(name), k = std::move(k)](Outcome o) {
+    TraceSpan s;
+    s.trace_id = ctx->trace_id;
+    s.span_id = rand_hex(8);
+    s.parent_id = ctx->root_span;
+    s.name = name;
+    s.puid = ctx->puid;
+    s.start_us = t0;
+    s.dur_us = wall_us() - t0;
+    s.error = bool(o.err);
+    push_span(std::move(s));
+    k(std::move(o));
+  };
+}
+
 // ------------------------------------------------------------ traffic split
 void Engine::set_traffic(int self_weight, std::vector<std::pair<std::shared_ptr<Engine>, int>> peers,
                          std::vector<std::shared_ptr<Engine>> shadows) {
@@ -389,10 +445,30 @@ void Engine::predict_local(MsgPtr req, Done k) {
   }
   auto ctx = std::make_shared<ReqCtx>();
   ctx->puid = req->meta.puid;
+  if (trace_rate_ > 0.0) {
+    thread_local Xoshiro rng;
+    if (trace_rate_ >= 1.0 || double(rng.next() >> 11) * (1.0 / 9007199254740992.0) < trace_rate_) {
+      ctx->traced = true;
+      ctx->trace_id = rand_hex(16);
+      ctx->root_span = rand_hex(8);
+      ctx->t0_us = wall_us();
+    }
+  }
   const bool log_pair = msglog_ && msglog_->wants_pairs();
   MsgPtr request_copy = (pair_hook_ || log_pair ? req : nullptr);
   const auto t_req = log_pair ? std::chrono::system_clock::now() : std::chrono::system_clock::time_point();
   eval(root_, req, ctx, [this, ctx, k = std::move(k), request_copy, t_req, log_pair](Outcome o) {
+    if (ctx->traced) {
+      TraceSpan s;
+      s.trace_id = ctx->trace_id;
+      s.span_id = ctx->root_span;
+      s.name = "predictions";
+      s.puid = ctx->puid;
+      s.start_us = ctx->t0_us;
+      s.dur_us = wall_us() - ctx->t0_us;
+      s.error = bool(o.err);
+      push_span(std::move(s));
+    }
     if (o.err) { k(std::move(o)); return; }
     MsgPtr r = o.msg.use_count() == 1 ? std::move(o.msg) : std::make_shared<SeldonMessage>(*o.msg);
     {
@@ -429,12 +505,12 @@ void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
   if (!n->fused.empty()) {
     CallCtx cc{n, &ctx->puid};
     guarded(n->client_timer[int(Method::TRANSFORM_INPUT)],
-            [this, n, input, ctx, k](Outcome o) mutable {
+            traced(ctx, n, "device-graph", [this, n, input, ctx, k](Outcome o) mutable {
               if (o.err) { k(std::move(o)); return; }
               if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
               add_metrics(n, *o.msg, ctx.get());
               k(Outcome::ok(merge_meta(std::move(o.msg), {input.get()}, ctx->puid)));
-            },
+            }),
             [&](Done kk) { n->unit->transform_input(cc, input, std::move(kk)); });
     return;
   }
@@ -444,11 +520,11 @@ void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
   }
   CallCtx cc{n, &ctx->puid};
   guarded(n->client_timer[int(Method::TRANSFORM_INPUT)],
-          [this, n, input, ctx, k](Outcome o) mutable {
+          traced(ctx, n, n->is_model ? "predict" : "transform-input", [this, n, input, ctx, k](Outcome o) mutable {
             if (o.err) { k(std::move(o)); return; }
             if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
             after_input(n, std::move(input), std::move(o.msg), std::move(ctx), std::move(k));
-          },
+          }),
           [&](Done kk) {
             if (n->is_model) n->unit->predict(cc, input, std::move(kk));
             else n->unit->transform_input(cc, input, std::move(kk));
@@ -503,7 +579,7 @@ void Engine::after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCt
   CallCtx cc{n, &ctx->puid};
   MsgPtr ti_keep = ti;
   guarded(n->client_timer[int(Method::ROUTE)],
-          [this, n, ctx, k, ti_keep, dispatch](Outcome o) {
+          traced(ctx, n, "route", [this, n, ctx, k, ti_keep, dispatch](Outcome o) {
             if (o.err) { k(std::move(o)); return; }
             int routing = -1;
             if (o.msg) {
@@ -519,7 +595,7 @@ void Engine::after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCt
               add_metrics(n, *o.msg, ctx.get());
             }
             dispatch(ti_keep, routing);
-          },
+          }),
           [&](Done kk) { n->unit->route(cc, ti, std::move(kk)); });
 }
 
@@ -538,12 +614,12 @@ void Engine::fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> c
     }
     CallCtx cc{n, &ctx->puid};
     guarded(n->client_timer[int(Method::TRANSFORM_OUTPUT)],
-            [this, n, ctx, k, agg](Outcome o2) {
+            traced(ctx, n, "transform-output", [this, n, ctx, k, agg](Outcome o2) {
               if (o2.err) { k(std::move(o2)); return; }
               if (!o2.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
               add_metrics(n, *o2.msg, ctx.get());
               k(Outcome::ok(merge_meta(std::move(o2.msg), {agg.get()}, ctx->puid)));
-            },
+            }),
             [&](Done kk) { n->unit->transform_output(cc, agg, std::move(kk)); });
   };
   if (!n->has(Method::AGGREGATE)) {
@@ -551,7 +627,7 @@ void Engine::fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> c
     return;
   }
   CallCtx cc{n, &ctx->puid};
-  guarded(n->client_timer[int(Method::AGGREGATE)], after_agg,
+  guarded(n->client_timer[int(Method::AGGREGATE)], traced(ctx, n, "aggregate", after_agg),
           [&](Done kk) { n->unit->aggregate(cc, outs, std::move(kk)); });
 }
 

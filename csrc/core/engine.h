@@ -131,6 +131,19 @@ struct EngineOptions {
 
 class MessageLogger;
 
+// One finished span of the native tracer (E14; reference
+// engine/.../tracing/TracingProvider.java:25-40 opens a Jaeger span per request
+// and per microservice call).  Exported by the Python side as Zipkin v2 JSON.
+struct TraceSpan {
+  std::string trace_id;   // 32 hex
+  std::string span_id;    // 16 hex
+  std::string parent_id;  // "" for the request's root span
+  std::string name;       // "predictions" or "<node>:<method>"
+  std::string puid;
+  int64_t start_us = 0, dur_us = 0;
+  bool error = false;
+};
+
 class Engine {
  public:
   // `shared_metrics`: registry shared with sibling predictors (one /prometheus).
@@ -180,6 +193,10 @@ class Engine {
   // Requests accepted by predict() and not yet answered (graceful drain).
   int64_t inflight() const { return inflight_.load(std::memory_order_acquire); }
   MessageLogger* message_logger() const { return msglog_.get(); }
+  // Native tracing: sample `rate` of requests; spans are buffered (bounded)
+  // until drain_spans().
+  void enable_tracing(double rate) { trace_rate_ = rate; }
+  std::vector<TraceSpan> drain_spans();
 
   // Hook invoked after each completed prediction (request, response) — used
   // by the async request logger.  Called on the completing thread.
@@ -206,6 +223,11 @@ class Engine {
   std::vector<std::shared_ptr<Engine>> peers_;
   std::atomic<int64_t> inflight_{0};
   std::shared_ptr<MessageLogger> msglog_;
+  double trace_rate_ = 0.0;
+  std::mutex span_mu_;
+  std::vector<TraceSpan> spans_;
+  void push_span(TraceSpan s);
+  Done traced(const std::shared_ptr<ReqCtx>& ctx, const Node* n, const char* what, Done k);
   std::unordered_map<std::string, UnitPtr> bound_;
   std::map<std::string, std::vector<std::string>> fused_;
   std::set<std::string> absorbed_;

@@ -106,6 +106,11 @@ class Deployment:
         self._bind_row_models()
         self.engine.finalize()
         self._servers = []
+        self._span_exporter = None
+        if config is not None and config.tracing:
+            from ..utils.tracing import NativeSpanExporter, configure_tracing
+
+            self._span_exporter = NativeSpanExporter(self.engine, configure_tracing("seldon-svc-orch"))
         self.peers: Dict[str, "Deployment"] = {}
         if split:
             kw = dict(components=components, deployment_name=self.deployment_name, device=device, batcher=batcher,
@@ -405,6 +410,9 @@ class Deployment:
             u.stop()
         for p in getattr(self, "peers", {}).values():
             p.close()
+        if getattr(self, "_span_exporter", None) is not None:
+            self._span_exporter.close()
+            self._span_exporter = None
         if getattr(self, "fabric", None) is not None and self.fabric.rank == 0:
             self.fabric.stop_peers()  # worker ranks leave their PeerServer loops
             self.fabric = None

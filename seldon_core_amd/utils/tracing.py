@@ -165,3 +165,47 @@ def configure_tracing(service: str) -> Tracer:
 
 def get_tracer() -> Optional[Tracer]:
     return _tracer
+
+
+class NativeSpanExporter:
+    """Drains the native engine's span buffer (per-request root span +
+    one span per node method call, csrc/core/engine.cc) and exports it through
+    a :class:`Tracer` (Zipkin v2 JSON to the collector / trace file)."""
+
+    def __init__(self, engine, tracer: Tracer, interval_s: float = 0.2):
+        self.engine = engine
+        self.tracer = tracer
+        self.interval_s = interval_s
+        self._stop = threading.Event()
+        engine.enable_tracing(tracer.sample_rate)
+        self._th = threading.Thread(target=self._run, name="span-exporter", daemon=True)
+        self._th.start()
+
+    def export_once(self) -> int:
+        spans = self.engine.drain_spans()
+        if not spans:
+            return 0
+        for s in spans:
+            s["localEndpoint"] = {"serviceName": self.tracer.service}
+            s["tags"].update(self.tracer.extra_tags)
+        if self.tracer.trace_file:
+            with open(self.tracer.trace_file, "a") as f:
+                for s in spans:
+                    f.write(json.dumps(s) + "\n")
+        if self.tracer.collector:
+            try:
+                req = urllib.request.Request(self.tracer.collector, data=json.dumps(spans).encode(),
+                                             headers={"Content-Type": "application/json"})
+                urllib.request.urlopen(req, timeout=2).read()
+            except Exception as e:
+                logger.debug("trace export failed: %s", e)
+        return len(spans)
+
+    def _run(self):
+        while not self._stop.wait(self.interval_s):
+            self.export_once()
+
+    def close(self):
+        self._stop.set()
+        self._th.join(timeout=5)
+        self.export_once()

@@ -165,3 +165,29 @@ def test_supervisor_two_workers_share_port():
         if p.poll() is None:
             os.killpg(p.pid, signal.SIGKILL)
             p.wait()
+
+
+def test_native_tracing_spans(tmp_path):
+    trace_file = tmp_path / "spans.jsonl"
+    os.environ["SELDON_TRACE_FILE"] = str(trace_file)
+    try:
+        cfg = EngineConfig.resolve(env={"TRACING": "1"}, annotations_file="/nonexistent")
+        spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+                "graph": {"name": "ab", "type": "ROUTER", "implementation": "RANDOM_ABTEST",
+                          "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
+                          "children": [{"name": "a", "type": "MODEL", "implementation": "SIMPLE_MODEL"},
+                                       {"name": "b", "type": "MODEL", "implementation": "SIMPLE_MODEL"}]}}
+        dep = sca.Deployment(spec, device=-1, config=cfg)
+        out = dep.predict({"meta": {"puid": "tr1"}, "data": {"ndarray": [[1.0]]}})
+        dep.close()  # flushes the exporter
+    finally:
+        del os.environ["SELDON_TRACE_FILE"]
+    spans = [json.loads(l) for l in trace_file.read_text().splitlines()]
+    root = [s for s in spans if s["name"] == "predictions"]
+    assert len(root) == 1 and root[0]["tags"]["seldon.puid"] == "tr1"
+    kids = [s for s in spans if s.get("parentId") == root[0]["id"]]
+    names = {s["name"] for s in kids}
+    branch = "a" if out["meta"]["routing"]["ab"] == 0 else "b"
+    assert names == {"ab:route", f"{branch}:predict"}
+    assert all(s["traceId"] == root[0]["traceId"] for s in kids)
+    assert all(s["localEndpoint"]["serviceName"] == "seldon-svc-orch" for s in spans)
