@@ -396,7 +396,9 @@ class Deployment:
         http.start()
         grpc = None
         if grpc_port is not None:
-            grpc = self.C.GrpcServer(self.engine, host, grpc_port, grpc_threads or threads, microservice_node)
+            max_msg = (self.config.grpc_max_message_size if self.config is not None else None) or (64 << 20)
+            grpc = self.C.GrpcServer(self.engine, host, grpc_port, grpc_threads or threads, microservice_node,
+                                     int(max_msg))
             grpc.start()
         h = ServerHandle(self, http, grpc)
         self._servers.append(h)
