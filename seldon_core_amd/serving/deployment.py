@@ -144,7 +144,15 @@ class Deployment:
         if self.fabric is not None and node.get("rank") is not None:
             return int(self.fabric.device)  # rank-placed: the front end's side lives on its own GPU
         d = node.get("device")
-        return self.device if d is None else int(d)
+        if d is None:
+            return self.device
+        d = int(d)
+        # Placement is a hint: a CPU deployment (device -1) runs everything on
+        # the host, and GPU ordinals wrap onto the GPUs that are present.
+        if self.device < 0 or d < 0:
+            return -1
+        n = gpu_count()
+        return d % n if n > 0 else -1
 
     def _batcher_opts(self, node: Dict) -> Dict[str, Any]:
         opts = dict(self.batcher_defaults)
@@ -164,7 +172,7 @@ class Deployment:
         fields; N consecutive GPUs from the node's device), or every GPU with the
         ``seldon.io/gpu-replicas: all`` annotation."""
         if node.get("devices"):
-            return [int(d) for d in node["devices"]]
+            return [self._node_device({"device": int(d)}) for d in node["devices"]]
         base = self._node_device(node)
         n = int(node.get("replicas", 1) or 1)
         if str(self.annotations().get("seldon.io/gpu-replicas", "")).lower() == "all" and base >= 0:
