@@ -47,13 +47,15 @@ def parse_args():
     ap.add_argument("--step-requests", type=int, default=40000, help="predictions per step per GPU")
     ap.add_argument("--server-threads", type=int, default=6)
     ap.add_argument("--client-threads", type=int, default=6)
+    ap.add_argument("--slots", type=int, default=4, help="GPU batches in flight per unit")
+    ap.add_argument("--no-spin", action="store_true", help="block on events instead of spinning")
     ap.add_argument("--graph", choices=["single", "abtest", "pipeline", "mab"], default="single",
                     help="graph shape (single = the headline single-model graph)")
     ap.add_argument("--extra-grpc", action="store_true", help="also report the gRPC API (untimed extra)")
     return ap.parse_args()
 
 
-def build_deployment(model: str, device: int, graph_kind: str = "single"):
+def build_deployment(model: str, device: int, graph_kind: str = "single", slots: int = 4, spin: bool = True):
     import numpy as np  # noqa: F401
 
     import seldon_core_amd as sca
@@ -86,7 +88,8 @@ def build_deployment(model: str, device: int, graph_kind: str = "single"):
             "spec": {"name": "bench", "predictors": [{
                 "name": "default", "replicas": 1, "componentSpecs": [{"spec": {"containers": []}}],
                 "graph": graph}]}}
-    dep = sca.Deployment(spec, components=comps, device=device, batcher={"max_batch": 4096, "slots": 4})
+    dep = sca.Deployment(spec, components=comps, device=device,
+                         batcher={"max_batch": 4096, "slots": slots, "spin_wait": spin})
     return dep, names, row, label
 
 
@@ -180,7 +183,7 @@ def main() -> None:
         if has_gpu:
             torch.cuda.synchronize()
 
-    dep, names, row, label = build_deployment(args.model, device, args.graph)
+    dep, names, row, label = build_deployment(args.model, device, args.graph, args.slots, not args.no_spin)
     handle = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
     payload = json.dumps({"data": {"names": names, "ndarray": [row]}})
     C = dep.C
@@ -239,7 +242,11 @@ def main() -> None:
                        "parallelism": f"dp{world}", "graph": args.graph, "api": args.api,
                        "users_per_gpu": args.users, "requests_per_step_per_gpu": args.step_requests,
                        "device": "gpu" if has_gpu else "cpu", "gpu_batches": batch.get("batches", 0),
-                       "mean_rows_per_gpu_batch": round(mean_rows, 2)},
+                       "mean_rows_per_gpu_batch": round(mean_rows, 2),
+                       "gpu_busy_frac_per_slot": round(batch.get("gpu_busy_s", 0.0) /
+                                                       max(1e-9, results[0]["wall"] * args.slots), 3),
+                       "slots": args.slots, "server_threads": args.server_threads,
+                       "client_threads": args.client_threads, "host_cpus": os.cpu_count()},
         }
         if extras[0] is not None:
             g_rps = sum(e["rps"] for e in extras if e)

@@ -1,0 +1,31 @@
+#!/usr/bin/env bash
+# Front-end / batcher parameter sweep for the headline REST bench (1 GPU).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+mkdir -p gpurun_out/sweep
+OUT=gpurun_out/sweep/results.jsonl
+: > "$OUT"
+{ nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -c processor /proc/cpuinfo; } > gpurun_out/sweep/cpu.txt 2>&1
+run() {  # tag args...
+  local tag=$1; shift
+  timeout -k 10 240 python bench.py --steps 6 --warmup 1 "$@" > gpurun_out/sweep/$tag.log 2>&1
+  local rc=$?
+  echo "$tag rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 gpurun_out/sweep/$tag.log; [ $rc -ge 124 ] && exit $rc; return; fi
+  python - "$tag" >> "$OUT" <<PY
+import json,sys
+d=json.loads(open("gpurun_out/sweep/$tag.log").read().strip().splitlines()[-1])
+c=d["config"]
+print(json.dumps({"tag":sys.argv[1],"rps":d["value"],"p50":d["p50_ms"],"p99":d["p99_ms"],"rows":c["mean_rows_per_gpu_batch"],"busy":c["gpu_busy_frac_per_slot"],"cpus":c["host_cpus"]}))
+PY
+  tail -1 "$OUT"
+}
+for spec in "${SWEEP[@]:-}"; do :; done
+run base
+run slots2 --slots 2
+run slots8 --slots 8
+run nospin --no-spin
+run srv8 --server-threads 8
+run srv12 --server-threads 12 --client-threads 8
+run srv4cl4 --server-threads 4 --client-threads 4
+echo done
