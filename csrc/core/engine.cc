@@ -168,6 +168,7 @@ std::string Engine::new_puid() {
 // ------------------------------------------------------------------ engine
 struct Engine::ReqCtx {
   std::string puid;
+  ExecPtr exec;
   bool traced = false;
   std::string trace_id, root_span;
   int64_t t0_us = 0;
@@ -408,14 +409,14 @@ uint32_t traffic_draw(int total) {
 }
 }  // namespace
 
-void Engine::predict(MsgPtr req, Done k) {
+void Engine::predict(MsgPtr req, Done k, ExecPtr exec) {
   inflight_.fetch_add(1, std::memory_order_relaxed);
   k = [this, k = std::move(k)](Outcome o) {
     k(std::move(o));
     inflight_.fetch_sub(1, std::memory_order_release);
   };
   if (routes_.empty() && shadows_.empty()) {
-    predict_local(std::move(req), std::move(k));
+    predict_local(std::move(req), std::move(k), std::move(exec));
     return;
   }
   for (Engine* s : shadows_) s->predict_local(std::make_shared<SeldonMessage>(*req), [](Outcome) {});
@@ -429,10 +430,10 @@ void Engine::predict(MsgPtr req, Done k) {
   } else if (!routes_.empty()) {
     target = routes_[0].first;
   }
-  target->predict_local(std::move(req), std::move(k));
+  target->predict_local(std::move(req), std::move(k), std::move(exec));
 }
 
-void Engine::predict_local(MsgPtr req, Done k) {
+void Engine::predict_local(MsgPtr req, Done k, ExecPtr exec) {
   if (!root_) {
     k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "graph not finalized")));
     return;
@@ -445,6 +446,7 @@ void Engine::predict_local(MsgPtr req, Done k) {
   }
   auto ctx = std::make_shared<ReqCtx>();
   ctx->puid = req->meta.puid;
+  ctx->exec = std::move(exec);
   if (trace_rate_ > 0.0) {
     thread_local Xoshiro rng;
     if (trace_rate_ >= 1.0 || double(rng.next() >> 11) * (1.0 / 9007199254740992.0) < trace_rate_) {
@@ -503,7 +505,7 @@ void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
     }
   }
   if (!n->fused.empty()) {
-    CallCtx cc{n, &ctx->puid};
+    CallCtx cc{n, &ctx->puid, &ctx->exec};
     guarded(n->client_timer[int(Method::TRANSFORM_INPUT)],
             traced(ctx, n, "device-graph", [this, n, input, ctx, k](Outcome o) mutable {
               if (o.err) { k(std::move(o)); return; }
@@ -518,7 +520,7 @@ void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
     after_input(n, input, input, std::move(ctx), std::move(k));
     return;
   }
-  CallCtx cc{n, &ctx->puid};
+  CallCtx cc{n, &ctx->puid, &ctx->exec};
   guarded(n->client_timer[int(Method::TRANSFORM_INPUT)],
           traced(ctx, n, n->is_model ? "predict" : "transform-input", [this, n, input, ctx, k](Outcome o) mutable {
             if (o.err) { k(std::move(o)); return; }
@@ -576,7 +578,7 @@ void Engine::after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCt
     dispatch(std::move(ti), -1);
     return;
   }
-  CallCtx cc{n, &ctx->puid};
+  CallCtx cc{n, &ctx->puid, &ctx->exec};
   MsgPtr ti_keep = ti;
   guarded(n->client_timer[int(Method::ROUTE)],
           traced(ctx, n, "route", [this, n, ctx, k, ti_keep, dispatch](Outcome o) {
@@ -612,7 +614,7 @@ void Engine::fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> c
       k(Outcome::ok(std::move(agg)));
       return;
     }
-    CallCtx cc{n, &ctx->puid};
+    CallCtx cc{n, &ctx->puid, &ctx->exec};
     guarded(n->client_timer[int(Method::TRANSFORM_OUTPUT)],
             traced(ctx, n, "transform-output", [this, n, ctx, k, agg](Outcome o2) {
               if (o2.err) { k(std::move(o2)); return; }
@@ -626,7 +628,7 @@ void Engine::fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> c
     after_agg(Outcome::ok(outs[0]));
     return;
   }
-  CallCtx cc{n, &ctx->puid};
+  CallCtx cc{n, &ctx->puid, &ctx->exec};
   guarded(n->client_timer[int(Method::AGGREGATE)], traced(ctx, n, "aggregate", after_agg),
           [&](Done kk) { n->unit->aggregate(cc, outs, std::move(kk)); });
 }

@@ -70,9 +70,22 @@ using FbDone = std::function<void(ErrPtr)>;
 // --------------------------------------------------------------- node model
 struct Node;
 
+// Where a request's continuations should run: the front-end thread that
+// owns its connection.  A unit that completes on a thread of its own (a GPU
+// batcher's device thread) posts the rest of the request there, so graph
+// walking, meta merging and serialisation spread over the front-end threads
+// instead of piling onto the device thread.
+class Executor {
+ public:
+  virtual ~Executor() = default;
+  virtual void post(std::function<void()> fn) = 0;
+};
+using ExecPtr = std::shared_ptr<Executor>;
+
 struct CallCtx {
   const Node* node;
   const std::string* puid;
+  const ExecPtr* exec = nullptr;  // may be null: continue on the completing thread
 };
 
 // A unit implements a subset of the five predictive-unit methods.  Every
@@ -162,7 +175,7 @@ class Engine {
   void set_traffic(int self_weight, std::vector<std::pair<std::shared_ptr<Engine>, int>> peers,
                    std::vector<std::shared_ptr<Engine>> shadows);
   // Graph evaluation on THIS predictor (no traffic split).
-  void predict_local(MsgPtr request, Done k);
+  void predict_local(MsgPtr request, Done k, ExecPtr exec = nullptr);
   void send_feedback_local(std::shared_ptr<Feedback> fb, FbDone k);
   const EngineOptions& options() const { return opts_; }
 
@@ -179,8 +192,8 @@ class Engine {
   std::vector<std::string> node_names() const;
   const Node* node(const std::string& name) const;
 
-  // Async API (thread-safe).
-  void predict(MsgPtr request, Done k);
+  // Async API (thread-safe).  `exec`: the caller's executor (see Executor).
+  void predict(MsgPtr request, Done k, ExecPtr exec = nullptr);
   void send_feedback(std::shared_ptr<Feedback> fb, FbDone k);
   // Reference "internal API" entry: call one node's method directly
   // (microservice mode: /predict, /route, ...).  `method` as in Method, or

@@ -2,6 +2,7 @@
 
 #include <immintrin.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <future>
@@ -26,10 +27,13 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
   zc_input_ = model_->zero_copy_input();
   segmented_ = model_->segmented();
   {
+    auto info = std::make_shared<RespInfo>();
+    info->model = model_;
     const int oc = model_->out_cols(model_->in_cols() > 0 ? model_->in_cols() : 1);
-    default_names_ = model_->class_names();
-    if (default_names_.empty())
-      for (int c = 0; c < oc; ++c) default_names_.push_back("t:" + std::to_string(c));
+    info->names = model_->class_names();
+    if (info->names.empty())
+      for (int c = 0; c < oc; ++c) info->names.push_back("t:" + std::to_string(c));
+    resp_ = std::move(info);
   }
   if (opts_.device < 0) {
     running_.store(true);
@@ -49,13 +53,7 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
     slots_.push_back(std::move(s));
   }
   running_.store(true);
-  submit_th_ = std::thread([this] { submit_loop(); });
-  // One completion thread per slot: responses of concurrent batches are
-  // scattered (and their graph continuations run) in parallel.
-  for (auto& s : slots_) {
-    Slot* raw = s.get();
-    s->th = std::thread([this, raw] { complete_loop(raw); });
-  }
+  device_th_ = std::thread([this] { device_loop(); });
 }
 
 BatchedUnit::~BatchedUnit() { stop(); }
@@ -66,15 +64,13 @@ void BatchedUnit::stop() {
     std::lock_guard<std::mutex> g(mu_);
   }
   cv_submit_.notify_all();
-  for (auto& s : slots_) s->cv.notify_all();
-  if (submit_th_.joinable()) submit_th_.join();
-  for (auto& s : slots_)
-    if (s->th.joinable()) s->th.join();
-  // Fail anything still queued.
+  if (device_th_.joinable()) device_th_.join();  // completes everything in flight
   std::deque<Item> rest;
   {
     std::lock_guard<std::mutex> g(mu_);
     rest.swap(queue_);
+    queued_rows_ = 0;
+    queued_n_.store(0);
   }
   for (auto& it : rest) it.k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "GPU unit stopped")));
 }
@@ -100,15 +96,15 @@ void BatchedUnit::ensure_capacity(Slot& s, int rows, int cols) {
   s.cap_rows = std::max(s.cap_rows, size_t(rows));
 }
 
-MsgPtr BatchedUnit::make_response(const Item& it, const double* out, int out_cols) const {
+MsgPtr BatchedUnit::make_response(const RespInfo& info, const Item& it, const double* out, int out_cols) {
   auto m = std::make_shared<SeldonMessage>();
   m->payload = Payload::Data;
-  const bool flat = model_->flat_output() && out_cols == 1;
-  if (!flat) {  // client_class_names: explicit names, else t:0..t:C-1
-    if (int(default_names_.size()) == out_cols) {
-      m->data.names = default_names_;
+  const bool flat = info.model->flat_output() && out_cols == 1;
+  if (!flat) {
+    if (int(info.names.size()) == out_cols) {
+      m->data.names = info.names;
     } else {
-      m->data.names = model_->class_names();
+      m->data.names = info.model->class_names();
       if (m->data.names.empty())
         for (int c = 0; c < out_cols; ++c) m->data.names.push_back("t:" + std::to_string(c));
     }
@@ -122,7 +118,7 @@ MsgPtr BatchedUnit::make_response(const Item& it, const double* out, int out_col
   return m;
 }
 
-void BatchedUnit::transform_input(const CallCtx&, MsgPtr in, Done k) {
+void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
   if (in->payload != Payload::Data) {
     k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, model_->name() + " expects numeric 'data' payload")));
     return;
@@ -142,9 +138,9 @@ void BatchedUnit::transform_input(const CallCtx&, MsgPtr in, Done k) {
     it.cols = int(shape[0]);
   } else {
     it.rows = int(shape[0]);
-    int64_t c = 1;
-    for (size_t i = 1; i < shape.size(); ++i) c *= shape[i];
-    it.cols = int(c);
+    int64_t cc = 1;
+    for (size_t i = 1; i < shape.size(); ++i) cc *= shape[i];
+    it.cols = int(cc);
   }
   const int want = model_->in_cols();
   if (it.rows == 0 || (want > 0 && it.cols != want)) {
@@ -155,11 +151,12 @@ void BatchedUnit::transform_input(const CallCtx&, MsgPtr in, Done k) {
   }
   it.req = std::move(in);
   it.k = std::move(k);
+  if (c.exec) it.exec = *c.exec;
   if (opts_.device < 0) {
     const int oc = model_->out_cols(it.cols);
     std::vector<double> out(size_t(it.rows) * oc);
     model_->run_cpu(it.x.data(), it.rows, it.cols, out.data());
-    MsgPtr r = make_response(it, out.data(), oc);
+    MsgPtr r = make_response(*resp_, it, out.data(), oc);
     {
       std::lock_guard<std::mutex> g(stats_mu_);
       stats_.batches++;
@@ -174,166 +171,208 @@ void BatchedUnit::transform_input(const CallCtx&, MsgPtr in, Done k) {
     return;
   }
   inflight_rows_.fetch_add(it.rows, std::memory_order_relaxed);
+  bool wake;
   {
     std::lock_guard<std::mutex> g(mu_);
     queued_rows_ += size_t(it.rows);
+    wake = queue_.empty();
     queue_.push_back(std::move(it));
   }
-  cv_submit_.notify_one();
+  queued_n_.fetch_add(1, std::memory_order_release);
+  if (wake) cv_submit_.notify_one();  // the device thread sleeps only with an empty queue
 }
 
-void BatchedUnit::submit_loop() {
-  (void)hipSetDevice(opts_.device);
-  std::unique_lock<std::mutex> lk(mu_);
-  auto free_slot = [&]() -> Slot* {
-    for (auto& s : slots_)
-      if (!s->busy) return s.get();
-    return nullptr;
-  };
-  while (true) {
-    cv_submit_.wait(lk, [&] { return !running_.load() || (!queue_.empty() && free_slot()); });
-    if (!running_.load()) break;
-    if (opts_.max_wait_us > 0 && queued_rows_ < size_t(opts_.max_batch)) {
-      auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(opts_.max_wait_us);
-      cv_submit_.wait_until(lk, deadline, [&] { return !running_.load() || queued_rows_ >= size_t(opts_.max_batch); });
-      if (!running_.load()) break;
+bool BatchedUnit::launch(Slot* s) {
+  const int rows = s->rows, cols = s->cols;
+  s->out_cols = model_->out_cols(cols);
+  hipError_t err = hipSuccess;
+  std::string launch_error;
+  try {
+    ensure_capacity(*s, rows, cols);
+    double* hin = s->h_in.host<double>();
+    size_t off = 0;
+    for (const auto& it : s->items) {
+      memcpy(hin + off, it.x.data(), it.x.size() * sizeof(double));
+      off += it.x.size();
     }
-    Slot* s = free_slot();
-    s->busy = true;
-    s->items.clear();
-    int rows = 0;
-    const int cols = queue_.front().cols;
-    while (!queue_.empty()) {
-      Item& it = queue_.front();
-      if (!s->items.empty() && (it.cols != cols || rows + it.rows > opts_.max_batch)) break;
-      rows += it.rows;
-      queued_rows_ -= size_t(it.rows);
-      s->items.push_back(std::move(it));
-      queue_.pop_front();
+    const size_t bin = size_t(rows) * cols * sizeof(double), bout = size_t(rows) * s->out_cols * sizeof(double);
+    hipStream_t st = s->stream.get();
+    const int32_t* seg = nullptr;
+    const int nseg = int(s->items.size());
+    if (segmented_) {  // request boundaries for per-request models
+      if (s->h_seg.bytes() < (s->items.size() + 1) * sizeof(int32_t))
+        s->h_seg.alloc(std::max<size_t>(1024, 2 * (s->items.size() + 1)) * sizeof(int32_t));
+      int32_t* o = s->h_seg.host<int32_t>();
+      o[0] = 0;
+      for (size_t i = 0; i < s->items.size(); ++i) o[i + 1] = o[i] + s->items[i].rows;
+      seg = s->h_seg.dev<int32_t>();
     }
-    lk.unlock();
-
-    s->rows = rows;
-    s->cols = cols;
-    s->out_cols = model_->out_cols(cols);
-    hipError_t err = hipSuccess;
-    std::string launch_error;
-    try {
-      ensure_capacity(*s, rows, cols);
-      double* hin = s->h_in.host<double>();
-      size_t off = 0;
-      for (const auto& it : s->items) {
-        memcpy(hin + off, it.x.data(), it.x.size() * sizeof(double));
-        off += it.x.size();
-      }
-      const size_t bin = size_t(rows) * cols * sizeof(double), bout = size_t(rows) * s->out_cols * sizeof(double);
-      hipStream_t st = s->stream.get();
-      const int32_t* seg = nullptr;
-      const int nseg = int(s->items.size());
-      if (segmented_) {  // request boundaries for per-request models
-        if (s->h_seg.bytes() < (s->items.size() + 1) * sizeof(int32_t))
-          s->h_seg.alloc(std::max<size_t>(1024, 2 * (s->items.size() + 1)) * sizeof(int32_t));
-        int32_t* o = s->h_seg.host<int32_t>();
-        o[0] = 0;
-        for (size_t i = 0; i < s->items.size(); ++i) o[i + 1] = o[i] + s->items[i].rows;
-        seg = s->h_seg.dev<int32_t>();
-      }
-      auto run = [&](const double* x, double* y) {
-        if (seg) model_->launch_segments(x, rows, cols, y, s->ws.get(), seg, nseg, st);
-        else model_->launch(x, rows, cols, y, s->ws.get(), st);
-      };
-      if (opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes) {
-        // Output always zero-copy (written once); input zero-copy only if the
-        // kernel reads each element once -- models that re-read X from many
-        // workgroups (tree chunks) get one DMA into HBM first.
-        const double* xin = s->h_in.dev<double>();
-        if (!zc_input_) {
-          err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
-          xin = s->d_in.as<double>();
-        }
-        if (err == hipSuccess) run(xin, s->h_out.dev<double>());
-      } else {
+    auto run = [&](const double* x, double* y) {
+      if (seg) model_->launch_segments(x, rows, cols, y, s->ws.get(), seg, nseg, st);
+      else model_->launch(x, rows, cols, y, s->ws.get(), st);
+    };
+    if (opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes) {
+      // Output always zero-copy (written once); input zero-copy only if the
+      // kernel reads each element once -- models that re-read X from many
+      // workgroups (tree chunks) get one DMA into HBM first.
+      const double* xin = s->h_in.dev<double>();
+      if (!zc_input_) {
         err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
-        if (err == hipSuccess) {
-          run(s->d_in.as<double>(), s->d_out.as<double>());
-          err = hipMemcpyAsync(s->h_out.host<double>(), s->d_out.get(), bout, hipMemcpyDeviceToHost, st);
-        }
+        xin = s->d_in.as<double>();
       }
-      if (err == hipSuccess) err = hipGetLastError();
-      if (err == hipSuccess) err = hipEventRecord(s->ev.get(), st);
-    } catch (const std::exception& ex) {
-      err = hipErrorUnknown;
-      launch_error = ex.what();
+      if (err == hipSuccess) run(xin, s->h_out.dev<double>());
+    } else {
+      err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
+      if (err == hipSuccess) {
+        run(s->d_in.as<double>(), s->d_out.as<double>());
+        err = hipMemcpyAsync(s->h_out.host<double>(), s->d_out.get(), bout, hipMemcpyDeviceToHost, st);
+      }
     }
-    if (err != hipSuccess) {
-      auto e = make_error(ApiError::EXECUTION_FAILURE,
-                          "GPU launch failed: " + (launch_error.empty() ? std::string(hipGetErrorString(err)) : launch_error));
-      inflight_rows_.fetch_sub(rows, std::memory_order_relaxed);
-      for (auto& it : s->items) it.k(Outcome::fail(e));
-      s->items.clear();
-      lk.lock();
-      s->busy = false;
-      continue;
-    }
-    lk.lock();
-    s->launched = true;
-    s->cv.notify_one();
+    if (err == hipSuccess) err = hipGetLastError();
+    if (err == hipSuccess) err = hipEventRecord(s->ev.get(), st);
+  } catch (const std::exception& ex) {
+    err = hipErrorUnknown;
+    launch_error = ex.what();
   }
+  s->t_launch = std::chrono::steady_clock::now();
+  if (err == hipSuccess) return true;
+  auto e = make_error(ApiError::EXECUTION_FAILURE,
+                      "GPU launch failed: " + (launch_error.empty() ? std::string(hipGetErrorString(err)) : launch_error));
+  inflight_rows_.fetch_sub(rows, std::memory_order_relaxed);
+  for (auto& it : s->items) it.k(Outcome::fail(e));
+  s->items.clear();
+  return false;
 }
 
-void BatchedUnit::complete_loop(Slot* s) {
+void BatchedUnit::complete(Slot* s, hipError_t st) {
+  const double busy = std::chrono::duration<double>(std::chrono::steady_clock::now() - s->t_launch).count();
+  inflight_rows_.fetch_sub(s->rows, std::memory_order_relaxed);
+  std::vector<Item> items;
+  items.swap(s->items);
+  const size_t n_items = items.size();
+  if (st != hipSuccess) {
+    auto e = make_error(ApiError::EXECUTION_FAILURE, std::string("GPU execution failed: ") + hipGetErrorString(st));
+    for (auto& it : items) it.k(Outcome::fail(e));
+  } else {
+    // Copy each request's rows out of the slot (it is reused at once), then
+    // hand the requests to their front-end threads, one task per thread.
+    const int oc = s->out_cols;
+    const double* out = s->h_out.host<double>();
+    using Req = std::pair<Item, std::vector<double>>;
+    struct Group {
+      ExecPtr ex;
+      std::shared_ptr<std::vector<Req>> reqs;
+    };
+    std::vector<Group> groups;
+    size_t row = 0;
+    for (auto& it : items) {
+      std::vector<double> y(out + row * oc, out + (row + size_t(it.rows)) * oc);
+      row += size_t(it.rows);
+      if (!it.exec) {
+        Done k = std::move(it.k);
+        k(Outcome::ok(make_response(*resp_, it, y.data(), oc)));
+        continue;
+      }
+      Group* g = nullptr;
+      for (auto& gg : groups)
+        if (gg.ex.get() == it.exec.get()) { g = &gg; break; }
+      if (!g) {
+        groups.push_back(Group{it.exec, std::make_shared<std::vector<Req>>()});
+        g = &groups.back();
+      }
+      g->reqs->emplace_back(std::move(it), std::move(y));
+    }
+    for (auto& g : groups) {
+      g.ex->post([info = resp_, reqs = g.reqs, oc]() {
+        for (auto& r : *reqs) {
+          Done k = std::move(r.first.k);
+          k(Outcome::ok(make_response(*info, r.first, r.second.data(), oc)));
+        }
+      });
+    }
+  }
+  std::lock_guard<std::mutex> g(stats_mu_);
+  stats_.batches++;
+  stats_.rows += uint64_t(s->rows);
+  stats_.requests += n_items;
+  stats_.max_rows = std::max<uint64_t>(stats_.max_rows, uint64_t(s->rows));
+  stats_.gpu_busy_s += busy;
+}
+
+void BatchedUnit::device_loop() {
   (void)hipSetDevice(opts_.device);
+  std::vector<Slot*> free_list, inflight;
+  for (auto& s : slots_) free_list.push_back(s.get());
+  using clk = std::chrono::steady_clock;
+  clk::time_point wait_start{};
+  int spins = 0;
   while (true) {
+    // ---- launch everything that fits into the free slots
     {
       std::unique_lock<std::mutex> lk(mu_);
-      s->cv.wait(lk, [&] { return s->launched || !running_.load(); });
-      if (!s->launched) break;
-      s->launched = false;
-    }
-    auto t0 = std::chrono::steady_clock::now();
-    hipError_t st;
-    if (opts_.spin_wait) {
-      // A batch round trip is ~10-30 us: spin briefly, then back off.
-      int spins = 0;
-      while ((st = hipEventQuery(s->ev.get())) == hipErrorNotReady) {
-        if (++spins < 2000) _mm_pause();
-        else std::this_thread::yield();
+      if (inflight.empty()) {
+        cv_submit_.wait(lk, [&] { return !running_.load() || !queue_.empty(); });
+        if (!running_.load()) break;
+        if (opts_.max_wait_us > 0 && queued_rows_ < size_t(opts_.max_batch)) {
+          const auto deadline = clk::now() + std::chrono::microseconds(opts_.max_wait_us);
+          cv_submit_.wait_until(lk, deadline, [&] { return !running_.load() || queued_rows_ >= size_t(opts_.max_batch); });
+          if (!running_.load()) break;
+        }
       }
+      while (!queue_.empty() && !free_list.empty()) {
+        Slot* s = free_list.back();
+        free_list.pop_back();
+        int rows = 0, n = 0;
+        const int cols = queue_.front().cols;
+        while (!queue_.empty()) {
+          Item& it = queue_.front();
+          if (!s->items.empty() && (it.cols != cols || rows + it.rows > opts_.max_batch)) break;
+          rows += it.rows;
+          queued_rows_ -= size_t(it.rows);
+          s->items.push_back(std::move(it));
+          queue_.pop_front();
+          ++n;
+        }
+        queued_n_.fetch_sub(n, std::memory_order_relaxed);
+        s->rows = rows;
+        s->cols = cols;
+        lk.unlock();
+        const bool ok = launch(s);
+        lk.lock();
+        (ok ? inflight : free_list).push_back(s);
+      }
+    }
+    if (inflight.empty()) continue;
+    // ---- reap finished batches
+    bool progress = false;
+    for (size_t i = 0; i < inflight.size();) {
+      Slot* s = inflight[i];
+      const hipError_t st = hipEventQuery(s->ev.get());
+      if (st == hipErrorNotReady) { ++i; continue; }
+      complete(s, st);
+      inflight.erase(inflight.begin() + long(i));
+      free_list.push_back(s);
+      progress = true;
+    }
+    if (progress) { spins = 0; continue; }
+    if (!opts_.spin_wait) {  // low-CPU mode: block on the oldest batch
+      (void)hipEventSynchronize(inflight.front()->ev.get());
+      continue;
+    }
+    if (!free_list.empty() && queued_n_.load(std::memory_order_acquire) > 0) continue;  // new work: launch it
+    // Spin through the usual 10-50 us round trip; back off if the GPU is slow
+    // so a long kernel does not burn a core (and CPU quota) for nothing.
+    if (spins++ == 0) wait_start = clk::now();
+    if (spins < 512) {
+      _mm_pause();
+    } else if (clk::now() - wait_start < std::chrono::microseconds(200)) {
+      std::this_thread::yield();
     } else {
-      st = hipEventSynchronize(s->ev.get());
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
-    const double busy = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    inflight_rows_.fetch_sub(s->rows, std::memory_order_relaxed);
-    if (st != hipSuccess) {
-      auto e = make_error(ApiError::EXECUTION_FAILURE, std::string("GPU execution failed: ") + hipGetErrorString(st));
-      for (auto& it : s->items) it.k(Outcome::fail(e));
-    } else {
-      finish_items(s->items, s->h_out.host<double>(), s->out_cols);
-    }
-    {
-      std::lock_guard<std::mutex> g(stats_mu_);
-      stats_.batches++;
-      stats_.rows += uint64_t(s->rows);
-      stats_.requests += s->items.size();
-      stats_.max_rows = std::max<uint64_t>(stats_.max_rows, uint64_t(s->rows));
-      stats_.gpu_busy_s += busy;
-    }
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      s->items.clear();
-      s->busy = false;
-    }
-    cv_submit_.notify_one();
   }
-}
-
-void BatchedUnit::finish_items(std::vector<Item>& items, const double* out, int out_cols) {
-  size_t row = 0;
-  for (auto& it : items) {
-    MsgPtr r = make_response(it, out + row * out_cols, out_cols);
-    row += size_t(it.rows);
-    it.k(Outcome::ok(std::move(r)));
-  }
+  // Shutdown: finish (and answer) everything already launched.
+  for (Slot* s : inflight) complete(s, hipEventSynchronize(s->ev.get()));
 }
 
 BatcherStats BatchedUnit::stats() const {

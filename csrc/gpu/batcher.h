@@ -4,17 +4,22 @@
 // (engine/.../InternalPredictionService.java:248-296 -> python wrapper ->
 // sklearn/xgboost on the CPU) with an in-process queue feeding a GPU.
 //
-//   request threads --(rows)--> queue --submit thread--> slot k: pack rows into
-//   pinned memory, launch kernel(s) on slot stream, record event
-//   --completion thread--> wait event, scatter rows back into responses, resume
-//   each request's graph continuation.
+//   front-end threads --(rows)--> queue --> device thread: pack rows into a
+//   slot's pinned buffer, launch on the slot's stream, record its event ...
+//   poll the in-flight events; a finished batch is split per request and each
+//   request's continuation is posted back to the front-end thread that owns
+//   it (Executor), which builds the response and walks on through the graph.
 //
-// Batching is "greedy continuous": when the device is idle a lone request is
-// launched immediately (latency = one launch); while `slots` batches are in
-// flight new requests accumulate and the next batch takes all of them (up to
-// max_batch rows), so throughput scales with load without a fixed timeout.
-// Small batches run zero-copy (the kernel reads/writes fine-grained pinned host
-// memory over PCIe: one launch, no DMA); large ones use async H2D/D2H copies.
+// One device thread per unit does all launching and completion polling, so
+// the unit costs one core while busy and none while idle; the per-request
+// work (response construction, meta merge, serialisation) runs on the
+// front-end threads.  Batching is "greedy continuous": when the device is
+// idle a lone request is launched immediately (latency = one launch); while
+// `slots` batches are in flight new requests accumulate and the next batch
+// takes all of them (up to max_batch rows), so batch size tracks load without
+// a fixed timeout.  Small batches run zero-copy (kernels read/write
+// fine-grained pinned host memory: one launch, no DMA); large ones, or models
+// that re-read their input from many workgroups, go through HBM.
 #pragma once
 
 #include <atomic>
@@ -33,11 +38,11 @@ namespace sca::gpu {
 struct BatcherOptions {
   int device = 0;            // -1 = run on the CPU (reference path)
   int max_batch = 1024;      // rows per launch
-  int max_wait_us = 0;       // extra wait for a fuller batch (0 = greedy)
+  int max_wait_us = 0;       // extra wait for a fuller batch when the device is idle (0 = greedy)
   int slots = 4;             // batches in flight
   bool zero_copy = true;
   size_t zero_copy_max_bytes = 256 << 10;
-  bool spin_wait = true;     // completion thread spins on the event (lowest latency)
+  bool spin_wait = true;     // poll events (lowest latency); false = block on the oldest batch
 };
 
 struct BatcherStats {
@@ -45,7 +50,7 @@ struct BatcherStats {
   uint64_t rows = 0;
   uint64_t requests = 0;
   uint64_t max_rows = 0;
-  double gpu_busy_s = 0;
+  double gpu_busy_s = 0;     // sum over batches of launch -> completion observed
 };
 
 class BatchedUnit : public Unit {
@@ -61,14 +66,21 @@ class BatchedUnit : public Unit {
   BatcherStats stats() const;
   void reset_stats();
   const BatcherOptions& options() const { return opts_; }
+  RowModelPtr model() const { return model_; }
   // Rows queued or on the device (replica load balancing).
   int64_t inflight_rows() const { return inflight_rows_.load(std::memory_order_relaxed); }
-  RowModelPtr model() const { return model_; }
 
   // Synchronous dense call (tests / python ops): X [rows, cols] -> out.
   std::vector<double> run_dense(const std::vector<double>& X, int rows, int cols);
 
   void stop();
+
+  // Response construction shared with posted continuations (outlives no unit
+  // state it does not own).
+  struct RespInfo {
+    RowModelPtr model;
+    std::vector<std::string> names;  // client_class_names: explicit, else t:0..t:C-1
+  };
 
  private:
   struct Item {
@@ -77,11 +89,11 @@ class BatchedUnit : public Unit {
     int rows = 0;
     int cols = 0;
     Done k;
+    ExecPtr exec;
   };
   struct Slot {
-    PinnedBuffer h_in, h_out;
+    PinnedBuffer h_in, h_out, h_seg;
     DeviceBuffer d_in, d_out, ws;
-    PinnedBuffer h_seg;  // request row offsets (segmented models)
     Stream stream;
     Event ev;
     size_t cap_rows = 0;
@@ -89,32 +101,30 @@ class BatchedUnit : public Unit {
     int rows = 0;
     int cols = 0;
     int out_cols = 0;
-    bool busy = false;      // guarded by BatchedUnit::mu_
-    bool launched = false;  // guarded by BatchedUnit::mu_
-    std::condition_variable cv;
-    std::thread th;         // per-slot completion thread
+    std::chrono::steady_clock::time_point t_launch;
   };
 
   void ensure_capacity(Slot& s, int rows, int cols);
-  void submit_loop();
-  void complete_loop(Slot* s);
-  void finish_items(std::vector<Item>& items, const double* out, int out_cols);
-  MsgPtr make_response(const Item& it, const double* out, int out_cols) const;
+  void device_loop();
+  bool launch(Slot* s);
+  void complete(Slot* s, hipError_t st);
+  static MsgPtr make_response(const RespInfo& info, const Item& it, const double* out, int out_cols);
 
   RowModelPtr model_;
   BatcherOptions opts_;
+  std::shared_ptr<const RespInfo> resp_;
   std::vector<std::unique_ptr<Slot>> slots_;
   std::mutex mu_;
   std::condition_variable cv_submit_;
   std::deque<Item> queue_;
-  size_t queued_rows_ = 0;
+  size_t queued_rows_ = 0;              // guarded by mu_
+  std::atomic<int> queued_n_{0};        // lock-free "work waiting" hint for the device thread
   std::atomic<bool> running_{false};
   std::atomic<int64_t> inflight_rows_{0};
   bool device_io_ = false;  // model needs device-memory I/O (no zero-copy)
-  bool zc_input_ = true;
-  bool segmented_ = false;    // model reads X once per element (zero-copy input is cheaper than a DMA)
-  std::thread submit_th_;
-  std::vector<std::string> default_names_;
+  bool zc_input_ = true;    // model reads X once per element (zero-copy input is cheaper than a DMA)
+  bool segmented_ = false;
+  std::thread device_th_;
   mutable std::mutex stats_mu_;
   BatcherStats stats_;
 };

@@ -87,7 +87,7 @@ int grpc_status_of(const EngineError& e) {
 
 }  // namespace
 
-struct GrpcServer::Worker : std::enable_shared_from_this<GrpcServer::Worker> {
+struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::Worker> {
   GrpcServer* srv = nullptr;
   int epfd = -1, evfd = -1, lfd = -1;
   std::thread th;
@@ -97,7 +97,28 @@ struct GrpcServer::Worker : std::enable_shared_from_this<GrpcServer::Worker> {
   uint64_t next_gen = 1;
   std::mutex qmu;
   std::vector<GCompletion> q;
+  std::vector<std::function<void()>> tasks;  // continuations posted by GPU units
+  bool running_tasks = false;                // worker thread only
   nghttp2_session_callbacks* cbs = nullptr;
+
+  // Executor: run a request's continuation on this I/O thread.
+  void post(std::function<void()> fn) override {
+    if (std::this_thread::get_id() == tid || stop.load(std::memory_order_relaxed)) {
+      fn();
+      return;
+    }
+    bool was_empty;
+    {
+      std::lock_guard<std::mutex> g(qmu);
+      was_empty = q.empty() && tasks.empty();
+      tasks.push_back(std::move(fn));
+    }
+    if (was_empty) {
+      uint64_t one = 1;
+      ssize_t w = ::write(evfd, &one, 8);
+      (void)w;
+    }
+  }
 
   ~Worker() {
     for (auto& kv : conns)
@@ -195,6 +216,11 @@ struct GrpcServer::Worker : std::enable_shared_from_this<GrpcServer::Worker> {
   }
 
   void deliver(GCompletion&& d) {
+    if (std::this_thread::get_id() == tid && running_tasks) {  // flushed after the task batch
+      std::lock_guard<std::mutex> g(qmu);
+      q.push_back(std::move(d));
+      return;
+    }
     if (std::this_thread::get_id() == tid) {
       complete(std::move(d), false);
       return;
@@ -202,7 +228,7 @@ struct GrpcServer::Worker : std::enable_shared_from_this<GrpcServer::Worker> {
     bool was_empty;
     {
       std::lock_guard<std::mutex> g(qmu);
-      was_empty = q.empty();
+      was_empty = q.empty() && tasks.empty();
       q.push_back(std::move(d));
     }
     if (was_empty) {  // one wakeup per drained batch of completions
@@ -227,6 +253,14 @@ struct GrpcServer::Worker : std::enable_shared_from_this<GrpcServer::Worker> {
     ssize_t r = ::read(evfd, &v, 8);
     (void)r;
     std::vector<GCompletion> items;
+    std::vector<std::function<void()>> run;
+    {
+      std::lock_guard<std::mutex> g(qmu);
+      run.swap(tasks);
+    }
+    running_tasks = true;
+    for (auto& fn : run) fn();
+    running_tasks = false;
     {
       std::lock_guard<std::mutex> g(qmu);
       items.swap(q);
@@ -304,7 +338,7 @@ struct GrpcServer::Worker : std::enable_shared_from_this<GrpcServer::Worker> {
     if (service == "/seldon.protos.Seldon" && method == "Predict") {
       auto msg = std::make_shared<SeldonMessage>();
       if (!message_from_pb(pb, *msg)) { send_error(c, sid, kInvalidArgument, "invalid SeldonMessage"); return; }
-      eng.predict(msg, on_msg);
+      eng.predict(msg, on_msg, self);
       return;
     }
     int m;

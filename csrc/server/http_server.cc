@@ -192,7 +192,7 @@ enum class Route { Predict, Feedback, Internal, Other };
 
 }  // namespace
 
-struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
+struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::Worker> {
   HttpServer* srv;
   int epfd = -1;
   int evfd = -1;
@@ -203,6 +203,8 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
   uint64_t next_gen = 1;
   std::mutex qmu;
   std::vector<Completion> q;
+  std::vector<std::function<void()>> tasks;  // continuations posted by GPU units
+  bool running_tasks = false;               // worker thread only
   std::atomic<bool> stop{false};
   std::unordered_map<std::string, Series*> timers;
 
@@ -497,6 +499,11 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
 
   // Engine continuation -> this worker (inline when already on it).
   void deliver(Completion&& done) {
+    if (std::this_thread::get_id() == tid && running_tasks) {  // finish after the task batch (may resume the conn)
+      std::lock_guard<std::mutex> g(qmu);
+      q.push_back(std::move(done));
+      return;
+    }
     if (std::this_thread::get_id() == tid) {
       auto it = conns.find(done.fd);
       if (it != conns.end() && it->second->gen == done.gen && !it->second->dead) finish(it->second.get(), std::move(done), false);
@@ -505,10 +512,29 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
     bool was_empty;
     {
       std::lock_guard<std::mutex> g(qmu);
-      was_empty = q.empty();
+      was_empty = q.empty() && tasks.empty();
       q.push_back(std::move(done));
     }
     if (was_empty) {  // one wakeup per drained batch of completions
+      uint64_t one = 1;
+      ssize_t w = ::write(evfd, &one, 8);
+      (void)w;
+    }
+  }
+
+  // Executor: run a request's continuation on this I/O thread.
+  void post(std::function<void()> fn) override {
+    if (std::this_thread::get_id() == tid || stop.load(std::memory_order_relaxed)) {
+      fn();
+      return;
+    }
+    bool was_empty;
+    {
+      std::lock_guard<std::mutex> g(qmu);
+      was_empty = q.empty() && tasks.empty();
+      tasks.push_back(std::move(fn));
+    }
+    if (was_empty) {
       uint64_t one = 1;
       ssize_t w = ::write(evfd, &one, 8);
       (void)w;
@@ -520,9 +546,19 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
     ssize_t r = ::read(evfd, &v, 8);
     (void)r;
     std::vector<Completion> items;
+    std::vector<std::function<void()>> run;
     {
       std::lock_guard<std::mutex> g(qmu);
       items.swap(q);
+      run.swap(tasks);
+    }
+    running_tasks = true;
+    for (auto& fn : run) fn();  // completions they produce are queued in q
+    running_tasks = false;
+    {
+      std::lock_guard<std::mutex> g(qmu);  // completions queued by other threads meanwhile
+      for (auto& d : q) items.push_back(std::move(d));
+      q.clear();
     }
     for (auto& d : items) {
       auto it = conns.find(d.fd);
@@ -617,7 +653,8 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
     int fd = c->fd;
     uint64_t gen = c->gen;
     bool ka = rq.keep_alive;
-    srv->engine_->predict(msg, [self = shared_from_this(), fd, gen, ka, uri, t0](Outcome o) {
+    auto self = shared_from_this();
+    srv->engine_->predict(msg, [self, fd, gen, ka, uri, t0](Outcome o) {
       Completion d{fd, gen, 200, "", "", ka};
       d.has_outcome = true;
       d.outcome = std::move(o);
@@ -625,7 +662,7 @@ struct HttpServer::Worker : std::enable_shared_from_this<HttpServer::Worker> {
       d.uri = uri;
       d.t0 = t0;
       self->deliver(std::move(d));
-    });
+    }, self);
   }
 
   void feedback_external(Conn* c, const Request& rq) {

@@ -20,12 +20,13 @@ print(json.dumps({"tag":sys.argv[1],"rps":d["value"],"p50":d["p50_ms"],"p99":d["
 PY
   tail -1 "$OUT"
 }
-for spec in "${SWEEP[@]:-}"; do :; done
-run base
-run slots2 --slots 2
-run slots8 --slots 8
-run nospin --no-spin
-run srv8 --server-threads 8
-run srv12 --server-threads 12 --client-threads 8
-run srv4cl4 --server-threads 4 --client-threads 4
+if [ "${TESTS:-1}" = "1" ]; then
+  timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/sweep/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/sweep/pytest_gpu.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+for cfg in ${CONFIGS:-"base::" "base2::" "srv8::--server-threads 8" "srv10::--server-threads 10 --client-threads 5" "slots2::--slots 2" "slots8::--slots 8" "grpc::--api grpc"}; do
+  tag=${cfg%%::*}; args=${cfg#*::}
+  run "$tag" $args
+done
 echo done
