@@ -416,6 +416,8 @@ PYBIND11_MODULE(_C, m) {
         return d;
       })
       .def("set_traffic", &Engine::set_traffic, py::arg("self_weight"), py::arg("peers"), py::arg("shadows"))
+      .def("add_header_route", &Engine::add_header_route, py::arg("name"), py::arg("value"), py::arg("regex"),
+           py::arg("target"))
       .def("bind_python",
            [](Engine& e, const std::string& node, py::object adapter, uint32_t builtin_methods) {
              e.bind(node, std::make_shared<PyUnit>(std::move(adapter), builtin_methods));
@@ -472,7 +474,7 @@ PYBIND11_MODULE(_C, m) {
         if (u) u->restore(std::string(b));
       })
       .def("predict_json",
-           [](Engine& e, const std::string& text) {
+           [](Engine& e, const std::string& text, const std::map<std::string, std::string>& headers) {
              auto msg = std::make_shared<SeldonMessage>();
              try {
                message_from_json(parse_json(text), *msg);
@@ -480,9 +482,16 @@ PYBIND11_MODULE(_C, m) {
                auto err = make_error(ApiError::INVALID_JSON, text);
                return std::make_pair(err->http_status, error_to_json(*err));
              }
-             Outcome o = wait_outcome([&](Done k) { e.predict(msg, std::move(k)); });
+             std::vector<std::pair<std::string, std::string>> hv;
+             for (const auto& kv : headers)
+               if (e.is_route_header(kv.first)) hv.emplace_back(kv.first, kv.second);
+             Outcome o = wait_outcome([&](Done k) {
+               if (hv.empty()) e.predict(msg, std::move(k));
+               else e.predict_with_headers(msg, std::move(k), nullptr, hv);
+             });
              return render(o);
-           })
+           },
+           py::arg("text"), py::arg("headers") = std::map<std::string, std::string>())
       .def("predict_pb",
            [](Engine& e, const py::bytes& b) -> py::tuple {
              auto msg = std::make_shared<SeldonMessage>();

@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstdio>
 #include <random>
+#include <regex>
 #include <stdexcept>
 
 namespace sca {
@@ -397,6 +398,50 @@ void Engine::set_traffic(int self_weight, std::vector<std::pair<std::shared_ptr<
     peers_.push_back(std::move(s));
   }
   if (route_total_ <= 0) throw std::runtime_error("traffic weights must sum to a positive value");
+}
+
+void Engine::add_header_route(const std::string& name, const std::string& value, bool regex,
+                              std::shared_ptr<Engine> target) {
+  HeaderRoute r;
+  r.name_lc = name;
+  for (auto& ch : r.name_lc) ch = char(std::tolower(static_cast<unsigned char>(ch)));
+  r.value = value;
+  r.regex = regex;
+  if (regex) r.re = std::make_shared<std::regex>(value);
+  r.target = target.get();
+  peers_.push_back(std::move(target));
+  header_routes_.push_back(std::move(r));
+}
+
+bool Engine::is_route_header(std::string_view name) const {
+  for (const auto& r : header_routes_) {
+    if (r.name_lc.size() != name.size()) continue;
+    bool eq = true;
+    for (size_t i = 0; i < name.size() && eq; ++i)
+      eq = r.name_lc[i] == char(std::tolower(static_cast<unsigned char>(name[i])));
+    if (eq) return true;
+  }
+  return false;
+}
+
+void Engine::predict_with_headers(MsgPtr req, Done k, ExecPtr exec,
+                                  const std::vector<std::pair<std::string, std::string>>& headers) {
+  for (const auto& r : header_routes_)
+    for (const auto& h : headers) {
+      std::string n = h.first;
+      for (auto& ch : n) ch = char(std::tolower(static_cast<unsigned char>(ch)));
+      if (n != r.name_lc) continue;
+      const bool hit = r.regex ? std::regex_match(h.second, *std::static_pointer_cast<std::regex>(r.re))
+                               : h.second == r.value;
+      if (!hit) continue;
+      inflight_.fetch_add(1, std::memory_order_relaxed);
+      r.target->predict_local(std::move(req), [this, k = std::move(k)](Outcome o) {
+        k(std::move(o));
+        inflight_.fetch_sub(1, std::memory_order_release);
+      }, std::move(exec));
+      return;
+    }
+  predict(std::move(req), std::move(k), std::move(exec));
 }
 
 namespace {

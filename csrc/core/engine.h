@@ -174,6 +174,17 @@ class Engine {
   // `self_weight` is this predictor's own share.
   void set_traffic(int self_weight, std::vector<std::pair<std::shared_ptr<Engine>, int>> peers,
                    std::vector<std::shared_ptr<Engine>> shadows);
+  // Header-match routing (reference ambassador `seldon.io/ambassador-header` /
+  // `-regex-header`, operator/controllers/ambassador.go:99-118): a request
+  // carrying header `name` whose value equals (or, regex, matches) `value` is
+  // served by `target` regardless of the traffic weights.
+  void add_header_route(const std::string& name, const std::string& value, bool regex, std::shared_ptr<Engine> target);
+  bool has_header_routes() const { return !header_routes_.empty(); }
+  bool is_route_header(std::string_view name) const;
+  // predict() after header matching; `headers` = (name, value) pairs the front
+  // end kept because is_route_header() was true for them.
+  void predict_with_headers(MsgPtr request, Done k, ExecPtr exec,
+                            const std::vector<std::pair<std::string, std::string>>& headers);
   // Graph evaluation on THIS predictor (no traffic split).
   void predict_local(MsgPtr request, Done k, ExecPtr exec = nullptr);
   void send_feedback_local(std::shared_ptr<Feedback> fb, FbDone k);
@@ -234,6 +245,13 @@ class Engine {
   int route_total_ = 0;
   std::vector<Engine*> shadows_;
   std::vector<std::shared_ptr<Engine>> peers_;
+  struct HeaderRoute {
+    std::string name_lc, value;
+    bool regex = false;
+    std::shared_ptr<void> re;  // std::regex, type-erased to keep <regex> out of the header
+    Engine* target = nullptr;
+  };
+  std::vector<HeaderRoute> header_routes_;
   std::atomic<int64_t> inflight_{0};
   std::shared_ptr<MessageLogger> msglog_;
   double trace_rate_ = 0.0;

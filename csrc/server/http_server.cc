@@ -158,6 +158,7 @@ namespace {
 struct Request {
   std::string_view method, target, path, query, content_type, body;
   bool keep_alive = true;
+  std::vector<std::pair<std::string, std::string>> route_headers;  // only when the engine routes on headers
 };
 
 struct Conn {
@@ -381,6 +382,8 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
             else if (iequals(val, "keep-alive")) rq.keep_alive = true;
           } else if (iequals(name, "content-type")) rq.content_type = val;
           else if (iequals(name, "expect")) expect_continue = iequals(val, "100-continue");
+          else if (srv->engine_->has_header_routes() && srv->engine_->is_route_header(name))
+            rq.route_headers.emplace_back(std::string(name), std::string(val));
         }
         hp = e + 2;
       }
@@ -654,7 +657,7 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
     uint64_t gen = c->gen;
     bool ka = rq.keep_alive;
     auto self = shared_from_this();
-    srv->engine_->predict(msg, [self, fd, gen, ka, uri, t0](Outcome o) {
+    Done done = [self, fd, gen, ka, uri, t0](Outcome o) {
       Completion d{fd, gen, 200, "", "", ka};
       d.has_outcome = true;
       d.outcome = std::move(o);
@@ -662,7 +665,9 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
       d.uri = uri;
       d.t0 = t0;
       self->deliver(std::move(d));
-    }, self);
+    };
+    if (!rq.route_headers.empty()) srv->engine_->predict_with_headers(msg, std::move(done), self, rq.route_headers);
+    else srv->engine_->predict(msg, std::move(done), self);
   }
 
   void feedback_external(Conn* c, const Request& rq) {

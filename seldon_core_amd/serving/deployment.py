@@ -31,8 +31,8 @@ from .._native import gpu_count, native
 from .adapter import PythonUnit
 from .errors import EngineError
 from ..parallel.device_graph import fusion_enabled
-from .spec import (BUILTIN_IMPLEMENTATIONS, PREPACKAGED_SERVERS, SpecError, container_for, is_shadow, iter_nodes,
-                   load_spec, predictors, select_predictor, typed_parameters, validate)
+from .spec import (BUILTIN_IMPLEMENTATIONS, PREPACKAGED_SERVERS, SpecError, container_for, header_route, is_shadow,
+                   iter_nodes, load_spec, predictors, select_predictor, typed_parameters, validate)
 
 logger = logging.getLogger(__name__)
 
@@ -122,9 +122,12 @@ class Deployment:
                     continue
                 peer = Deployment(self.sdep, predictor=p["name"], **kw)
                 self.peers[p["name"]] = peer
+                hdr = header_route(p, self.sdep)
+                if hdr is not None:
+                    self.engine.add_header_route(hdr[0], hdr[1], hdr[2], peer.engine)
                 if is_shadow(p):
                     shadows.append(peer.engine)
-                else:
+                elif int(p.get("traffic", 0) or 0) > 0 or hdr is None:
                     routes.append((peer.engine, int(p.get("traffic", 0) or 0)))
             self.engine.set_traffic(int(self.predictor.get("traffic", 0) or 0), routes, shadows)
 
@@ -354,9 +357,9 @@ class Deployment:
         self.units[node["name"]] = unit
 
     # ----------------------------------------------------------- requests
-    def predict(self, payload: Union[Dict, str]) -> Dict:
+    def predict(self, payload: Union[Dict, str], headers: Optional[Dict[str, str]] = None) -> Dict:
         text = payload if isinstance(payload, str) else json.dumps(payload)
-        status, body = self.engine.predict_json(text)
+        status, body = self.engine.predict_json(text, dict(headers or {}))
         out = json.loads(body)
         if status != 200:
             raise EngineError(status, out)

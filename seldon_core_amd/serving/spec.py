@@ -91,6 +91,21 @@ def is_shadow(predictor: Dict) -> bool:
     return str(ann.get("seldon.io/shadow", ann.get("seldon.io/ambassador-shadow", ""))).lower() in ("1", "true")
 
 
+def header_route(predictor: Dict, sdep: Optional[Dict] = None) -> Optional[Tuple[str, str, bool]]:
+    """(header, value, is_regex) routing a request to this predictor: predictor
+    annotations ``seldon.io/header`` / ``seldon.io/regex-header`` (or the
+    reference's ``seldon.io/ambassador-header`` / ``-regex-header`` spelling),
+    value "name:value" (ambassador.go:99-118)."""
+    ann = predictor.get("annotations") or {}  # per predictor: a deployment-wide header would match them all
+    for key, regex in (("seldon.io/header", False), ("seldon.io/regex-header", True),
+                       ("seldon.io/ambassador-header", False), ("seldon.io/ambassador-regex-header", True)):
+        v = ann.get(key)
+        if v and ":" in v:
+            name, _, value = v.partition(":")
+            return name.strip(), value.strip(), regex
+    return None
+
+
 def iter_nodes(graph: Dict, parent: Optional[Dict] = None) -> Iterator[Tuple[Dict, Optional[Dict]]]:
     yield graph, parent
     for c in graph.get("children", []) or []:

@@ -96,6 +96,32 @@ def test_predictor_scoped_components():
         dep.close()
 
 
+def test_header_routing_python_and_http():
+    import urllib.request
+
+    a, b, c = Const(1.0), Const(2.0), Const(3.0)
+    spec = _sdep([_pred("main", 100, "ma"),
+                  _pred("london", 0, "mb", annotations={"seldon.io/header": "location:london"}),
+                  _pred("beta", 0, "mc", annotations={"seldon.io/regex-header": "x-user:beta-.*"})])
+    dep = sca.Deployment(spec, components={"ma": a, "mb": b, "mc": c}, device=-1)
+    try:
+        v = lambda out: out["data"]["ndarray"][0][0]  # noqa: E731
+        req = {"data": {"ndarray": [[0.0]]}}
+        assert {v(dep.predict(req)) for _ in range(50)} == {1.0}  # weights: main only
+        assert v(dep.predict(req, headers={"Location": "london"})) == 2.0
+        assert v(dep.predict(req, headers={"location": "paris"})) == 1.0
+        assert v(dep.predict(req, headers={"X-User": "beta-42"})) == 3.0
+        h = dep.serve(http_port=0, grpc_port=None, threads=1, host="127.0.0.1")
+        r = urllib.request.Request(f"http://127.0.0.1:{h.http_port}/api/v0.1/predictions",
+                                   data=b'{"data":{"ndarray":[[0.0]]}}',
+                                   headers={"Content-Type": "application/json", "location": "london"})
+        import json as _json
+
+        assert _json.loads(urllib.request.urlopen(r, timeout=5).read())["data"]["ndarray"][0][0] == 2.0
+    finally:
+        dep.close()
+
+
 def test_traffic_must_sum_to_100():
     spec = _sdep([_pred("main", 60, "ma"), _pred("canary", 30, "mb")])
     with pytest.raises(SpecError, match="Traffic must sum to 100"):
