@@ -52,7 +52,7 @@ Outcome wait_outcome(const std::function<void(Done)>& start) {
 }
 
 gpu::BatcherOptions batcher_opts(int device, int max_batch, int max_wait_us, int slots, bool zero_copy,
-                                 size_t zero_copy_max_bytes, bool spin) {
+                                 size_t zero_copy_max_bytes, bool spin, bool cpu_batching = false) {
   gpu::BatcherOptions o;
   o.device = device;
   o.max_batch = max_batch;
@@ -61,6 +61,7 @@ gpu::BatcherOptions batcher_opts(int device, int max_batch, int max_wait_us, int
   o.zero_copy = zero_copy;
   o.zero_copy_max_bytes = zero_copy_max_bytes;
   o.spin_wait = spin;
+  o.cpu_batching = cpu_batching;
   return o;
 }
 
@@ -266,13 +267,13 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<gpu::BatchedUnit, Unit, std::shared_ptr<gpu::BatchedUnit>>(m, "BatchedUnit")
       .def(py::init([](std::shared_ptr<gpu::RowModel> model, int device, int max_batch, int max_wait_us, int slots,
-                       bool zero_copy, size_t zc_bytes, bool spin) {
+                       bool zero_copy, size_t zc_bytes, bool spin, bool cpu_batching) {
              return std::make_shared<gpu::BatchedUnit>(
-                 model, batcher_opts(device, max_batch, max_wait_us, slots, zero_copy, zc_bytes, spin));
+                 model, batcher_opts(device, max_batch, max_wait_us, slots, zero_copy, zc_bytes, spin, cpu_batching));
            }),
            py::arg("model"), py::arg("device") = 0, py::arg("max_batch") = 1024, py::arg("max_wait_us") = 0,
            py::arg("slots") = 4, py::arg("zero_copy") = true, py::arg("zero_copy_max_bytes") = 256 << 10,
-           py::arg("spin_wait") = true)
+           py::arg("spin_wait") = true, py::arg("cpu_batching") = false)
       .def("run", [](gpu::BatchedUnit& u, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
         if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
         const int rows = int(X.shape(0)), cols = int(X.shape(1));

@@ -37,6 +37,11 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
   }
   if (opts_.device < 0) {
     running_.store(true);
+    if (opts_.cpu_batching) {
+      cpu_ = true;
+      for (int i = 0; i < opts_.slots; ++i) slots_.push_back(std::make_unique<Slot>());
+      device_th_ = std::thread([this] { device_loop(); });
+    }
     return;
   }
   if (opts_.device >= device_count())
@@ -152,7 +157,7 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
   it.req = std::move(in);
   it.k = std::move(k);
   if (c.exec) it.exec = *c.exec;
-  if (opts_.device < 0) {
+  if (opts_.device < 0 && !cpu_) {
     const int oc = model_->out_cols(it.cols);
     std::vector<double> out(size_t(it.rows) * oc);
     model_->run_cpu(it.x.data(), it.rows, it.cols, out.data());
@@ -185,6 +190,24 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
 bool BatchedUnit::launch(Slot* s) {
   const int rows = s->rows, cols = s->cols;
   s->out_cols = model_->out_cols(cols);
+  if (cpu_) {  // reference path, one call per request (segment semantics for per-request models)
+    s->t_launch = std::chrono::steady_clock::now();
+    try {
+      s->cpu_out.assign(size_t(rows) * s->out_cols, 0.0);
+      size_t row = 0;
+      for (const auto& it : s->items) {
+        model_->run_cpu(it.x.data(), it.rows, cols, s->cpu_out.data() + row * s->out_cols);
+        row += size_t(it.rows);
+      }
+      return true;
+    } catch (const std::exception& ex) {
+      auto e = make_error(ApiError::EXECUTION_FAILURE, std::string("CPU model failed: ") + ex.what());
+      inflight_rows_.fetch_sub(rows, std::memory_order_relaxed);
+      for (auto& it : s->items) it.k(Outcome::fail(e));
+      s->items.clear();
+      return false;
+    }
+  }
   hipError_t err = hipSuccess;
   std::string launch_error;
   try {
@@ -257,7 +280,7 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     // Copy each request's rows out of the slot (it is reused at once), then
     // hand the requests to their front-end threads, one task per thread.
     const int oc = s->out_cols;
-    const double* out = s->h_out.host<double>();
+    const double* out = cpu_ ? s->cpu_out.data() : s->h_out.host<double>();
     using Req = std::pair<Item, std::vector<double>>;
     struct Group {
       ExecPtr ex;
@@ -300,7 +323,7 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
 }
 
 void BatchedUnit::device_loop() {
-  (void)hipSetDevice(opts_.device);
+  if (!cpu_) (void)hipSetDevice(opts_.device);
   std::vector<Slot*> free_list, inflight;
   for (auto& s : slots_) free_list.push_back(s.get());
   using clk = std::chrono::steady_clock;
@@ -347,7 +370,7 @@ void BatchedUnit::device_loop() {
     bool progress = false;
     for (size_t i = 0; i < inflight.size();) {
       Slot* s = inflight[i];
-      const hipError_t st = hipEventQuery(s->ev.get());
+      const hipError_t st = cpu_ ? hipSuccess : hipEventQuery(s->ev.get());
       if (st == hipErrorNotReady) { ++i; continue; }
       complete(s, st);
       inflight.erase(inflight.begin() + long(i));
@@ -355,7 +378,7 @@ void BatchedUnit::device_loop() {
       progress = true;
     }
     if (progress) { spins = 0; continue; }
-    if (!opts_.spin_wait) {  // low-CPU mode: block on the oldest batch
+    if (!opts_.spin_wait && !cpu_) {  // low-CPU mode: block on the oldest batch
       (void)hipEventSynchronize(inflight.front()->ev.get());
       continue;
     }
@@ -372,7 +395,7 @@ void BatchedUnit::device_loop() {
     }
   }
   // Shutdown: finish (and answer) everything already launched.
-  for (Slot* s : inflight) complete(s, hipEventSynchronize(s->ev.get()));
+  for (Slot* s : inflight) complete(s, cpu_ ? hipSuccess : hipEventSynchronize(s->ev.get()));
 }
 
 BatcherStats BatchedUnit::stats() const {

@@ -43,6 +43,10 @@ struct BatcherOptions {
   bool zero_copy = true;
   size_t zero_copy_max_bytes = 256 << 10;
   bool spin_wait = true;     // poll events (lowest latency); false = block on the oldest batch
+  // device -1 only: run the CPU reference path through the same queue /
+  // device-thread / executor machinery instead of inline (tests, CPU serving
+  // of heavier models).
+  bool cpu_batching = false;
 };
 
 struct BatcherStats {
@@ -93,6 +97,7 @@ class BatchedUnit : public Unit {
   };
   struct Slot {
     PinnedBuffer h_in, h_out, h_seg;
+    std::vector<double> cpu_out;  // device -1 (cpu_batching)
     DeviceBuffer d_in, d_out, ws;
     Stream stream;
     Event ev;
@@ -124,6 +129,7 @@ class BatchedUnit : public Unit {
   bool device_io_ = false;  // model needs device-memory I/O (no zero-copy)
   bool zc_input_ = true;    // model reads X once per element (zero-copy input is cheaper than a DMA)
   bool segmented_ = false;
+  bool cpu_ = false;        // device -1 with cpu_batching
   std::thread device_th_;
   mutable std::mutex stats_mu_;
   BatcherStats stats_;

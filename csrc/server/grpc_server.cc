@@ -99,6 +99,7 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
   std::vector<GCompletion> q;
   std::vector<std::function<void()>> tasks;  // continuations posted by GPU units
   bool running_tasks = false;                // worker thread only
+  bool wake_pending = false;                 // eventfd written and not yet drained (guarded by qmu)
   nghttp2_session_callbacks* cbs = nullptr;
 
   // Executor: run a request's continuation on this I/O thread.
@@ -110,7 +111,8 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
     bool was_empty;
     {
       std::lock_guard<std::mutex> g(qmu);
-      was_empty = q.empty() && tasks.empty();
+      was_empty = !wake_pending;
+      wake_pending = true;
       tasks.push_back(std::move(fn));
     }
     if (was_empty) {
@@ -228,7 +230,8 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
     bool was_empty;
     {
       std::lock_guard<std::mutex> g(qmu);
-      was_empty = q.empty() && tasks.empty();
+      was_empty = !wake_pending;
+      wake_pending = true;
       q.push_back(std::move(d));
     }
     if (was_empty) {  // one wakeup per drained batch of completions
@@ -256,6 +259,7 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
     std::vector<std::function<void()>> run;
     {
       std::lock_guard<std::mutex> g(qmu);
+      wake_pending = false;  // anything queued from now on signals again
       run.swap(tasks);
     }
     running_tasks = true;

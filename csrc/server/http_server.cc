@@ -206,6 +206,7 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
   std::vector<Completion> q;
   std::vector<std::function<void()>> tasks;  // continuations posted by GPU units
   bool running_tasks = false;               // worker thread only
+  bool wake_pending = false;                // eventfd written and not yet drained (guarded by qmu)
   std::atomic<bool> stop{false};
   std::unordered_map<std::string, Series*> timers;
 
@@ -515,7 +516,8 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
     bool was_empty;
     {
       std::lock_guard<std::mutex> g(qmu);
-      was_empty = q.empty() && tasks.empty();
+      was_empty = !wake_pending;
+      wake_pending = true;
       q.push_back(std::move(done));
     }
     if (was_empty) {  // one wakeup per drained batch of completions
@@ -534,7 +536,8 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
     bool was_empty;
     {
       std::lock_guard<std::mutex> g(qmu);
-      was_empty = q.empty() && tasks.empty();
+      was_empty = !wake_pending;
+      wake_pending = true;
       tasks.push_back(std::move(fn));
     }
     if (was_empty) {
@@ -552,6 +555,7 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
     std::vector<std::function<void()>> run;
     {
       std::lock_guard<std::mutex> g(qmu);
+      wake_pending = false;  // anything queued from now on signals again
       items.swap(q);
       run.swap(tasks);
     }

@@ -38,7 +38,7 @@ logger = logging.getLogger(__name__)
 
 METHOD_IDS = {"TRANSFORM_INPUT": 0, "TRANSFORM_OUTPUT": 1, "ROUTE": 2, "AGGREGATE": 3, "SEND_FEEDBACK": 4,
               "PREDICT": 5}
-BATCHER_KEYS = ("max_batch", "max_wait_us", "slots", "zero_copy", "zero_copy_max_bytes", "spin_wait")
+BATCHER_KEYS = ("max_batch", "max_wait_us", "slots", "zero_copy", "zero_copy_max_bytes", "spin_wait", "cpu_batching")
 
 
 def import_class(path: str):

@@ -1,0 +1,98 @@
+"""The micro-batcher's device thread + executor hand-off, exercised on the CPU
+(``cpu_batching``: same queue / device-thread / continuation-posting path as
+a GPU unit, with the reference CPU kernels).  Concurrent REST and gRPC
+clients must all get their own answers, and requests must share batches."""
+import concurrent.futures as cf
+import json
+import urllib.request
+
+import numpy as np
+import pytest
+
+import seldon_core_amd as sca
+from seldon_core_amd.client import SeldonClient
+from seldon_core_amd.models import iris_logistic_regression
+
+
+def _spec(graph):
+    return {"name": "p", "graph": graph, "componentSpecs": [{"spec": {"containers": []}}]}
+
+
+@pytest.fixture(scope="module")
+def served():
+    clf = iris_logistic_regression()
+    dep = sca.Deployment(_spec({"name": "clf", "type": "MODEL"}), components={"clf": clf}, device=-1,
+                         batcher={"cpu_batching": True, "slots": 2, "max_wait_us": 100})
+    h = dep.serve(http_port=0, grpc_port=0, threads=3, host="127.0.0.1")
+    yield dep, h, clf
+    dep.close()
+
+
+def test_concurrent_rest_requests_share_batches(served):
+    dep, h, clf = served
+    rng = np.random.default_rng(0)
+    rows = rng.uniform(0, 8, (64, 4))
+    dep.batched["clf"].reset_stats()
+
+    def call(i):
+        x = rows[i % 64]
+        req = urllib.request.Request(f"http://127.0.0.1:{h.http_port}/api/v0.1/predictions",
+                                     data=json.dumps({"data": {"ndarray": [x.tolist()]}}).encode(),
+                                     headers={"Content-Type": "application/json"})
+        out = json.loads(urllib.request.urlopen(req, timeout=30).read())
+        np.testing.assert_allclose(out["data"]["ndarray"], clf.predict_proba(x[None, :]), rtol=1e-12)
+        return True
+
+    with cf.ThreadPoolExecutor(32) as ex:
+        assert all(ex.map(call, range(640)))
+    st = dep.batched["clf"].stats()
+    assert st["requests"] == 640 and st["batches"] < 640
+
+
+def test_concurrent_grpc_requests(served):
+    dep, h, clf = served
+    sc = SeldonClient(gateway="ambassador", transport="grpc", gateway_endpoint=f"127.0.0.1:{h.grpc_port}",
+                      deployment_name="d", namespace="n")
+    rng = np.random.default_rng(1)
+
+    def call(i):
+        x = rng.uniform(0, 8, (1 + i % 3, 4))
+        r = sc.predict(data=x)
+        assert r.success, r.msg
+        got = np.array(r.response.data.tensor.values).reshape(x.shape[0], 3)
+        np.testing.assert_allclose(got, clf.predict_proba(x), rtol=1e-12)
+        return True
+
+    with cf.ThreadPoolExecutor(16) as ex:
+        assert all(ex.map(call, range(200)))
+
+
+def test_device_graph_through_batched_cpu_path():
+    C = sca.native()
+    rng = np.random.default_rng(2)
+    comps = {"t": C.linear_model(rng.normal(size=(4, 4)), rng.normal(size=4), 0),
+             "a": C.linear_model(rng.normal(size=(3, 4)), rng.normal(size=3), 1),
+             "b": C.linear_model(rng.normal(size=(3, 4)), rng.normal(size=3), 1)}
+    graph = {"name": "t", "type": "TRANSFORMER", "children": [
+        {"name": "c", "type": "COMBINER", "implementation": "AVERAGE_COMBINER",
+         "children": [{"name": "a", "type": "MODEL"}, {"name": "b", "type": "MODEL"}]}]}
+    fused = sca.Deployment(_spec(graph), components=comps, device=-1, batcher={"cpu_batching": True})
+    plain = sca.Deployment(_spec(graph), components=comps, device=-1, fuse=False)
+    h = fused.serve(http_port=0, grpc_port=None, threads=2, host="127.0.0.1")
+    try:
+        X = rng.normal(size=(3, 4))
+
+        def call(_):
+            req = urllib.request.Request(f"http://127.0.0.1:{h.http_port}/api/v0.1/predictions",
+                                         data=json.dumps({"data": {"ndarray": X.tolist()}}).encode(),
+                                         headers={"Content-Type": "application/json"})
+            return json.loads(urllib.request.urlopen(req, timeout=30).read())
+
+        want = plain.predict({"data": {"ndarray": X.tolist()}})
+        with cf.ThreadPoolExecutor(8) as ex:
+            for out in ex.map(call, range(40)):
+                np.testing.assert_allclose(out["data"]["ndarray"], want["data"]["ndarray"], rtol=1e-12)
+                assert out["meta"]["requestPath"] == want["meta"]["requestPath"]
+    finally:
+        fused.close()
+        plain.close()
