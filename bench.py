@@ -45,14 +45,40 @@ def parse_args():
     ap.add_argument("--model", choices=["iris", "xgb1000"], default="iris")
     ap.add_argument("--users", type=int, default=256, help="concurrent clients per GPU")
     ap.add_argument("--step-requests", type=int, default=40000, help="predictions per step per GPU")
-    ap.add_argument("--server-threads", type=int, default=6)
-    ap.add_argument("--client-threads", type=int, default=6)
+    ap.add_argument("--server-threads", type=int, default=None, help="default: sized from the CPU quota per rank")
+    ap.add_argument("--client-threads", type=int, default=None, help="default: sized from the CPU quota per rank")
     ap.add_argument("--slots", type=int, default=4, help="GPU batches in flight per unit")
     ap.add_argument("--no-spin", action="store_true", help="block on events instead of spinning")
     ap.add_argument("--graph", choices=["single", "abtest", "pipeline", "mab"], default="single",
                     help="graph shape (single = the headline single-model graph)")
     ap.add_argument("--extra-grpc", action="store_true", help="also report the gRPC API (untimed extra)")
     return ap.parse_args()
+
+
+def cpu_budget() -> float:
+    """CPUs this process may use: cgroup v2 quota (cpu.max) or affinity."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            return float(quota) / float(period)
+    except (OSError, ValueError):
+        pass
+    try:
+        return float(len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return float(os.cpu_count() or 8)
+
+
+def size_threads(args, local_world: int) -> None:
+    """Split the CPU share of one rank between the front end (~60%), the
+    closed-loop load generator (~32%) and the GPU device thread (measured on
+    a 16-CPU MI355X share: 10 front-end / 5 generator threads was the best
+    split, profiles/r01f_sweep_executor)."""
+    per_rank = max(2.0, cpu_budget() / max(1, local_world))
+    if args.server_threads is None:
+        args.server_threads = max(1, min(16, int(round(per_rank * 0.6))))
+    if args.client_threads is None:
+        args.client_threads = max(1, min(10, int(round(per_rank * 0.32))))
 
 
 def build_deployment(model: str, device: int, graph_kind: str = "single", slots: int = 4, spin: bool = True):
@@ -183,6 +209,7 @@ def main() -> None:
         if has_gpu:
             torch.cuda.synchronize()
 
+    size_threads(args, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     dep, names, row, label = build_deployment(args.model, device, args.graph, args.slots, not args.no_spin)
     handle = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
     payload = json.dumps({"data": {"names": names, "ndarray": [row]}})
@@ -246,7 +273,8 @@ def main() -> None:
                        "gpu_busy_frac_per_slot": round(batch.get("gpu_busy_s", 0.0) /
                                                        max(1e-9, results[0]["wall"] * args.slots), 3),
                        "slots": args.slots, "server_threads": args.server_threads,
-                       "client_threads": args.client_threads, "host_cpus": os.cpu_count()},
+                       "client_threads": args.client_threads, "host_cpus": os.cpu_count(),
+                       "cpu_budget": round(cpu_budget(), 2)},
         }
         if extras[0] is not None:
             g_rps = sum(e["rps"] for e in extras if e)
