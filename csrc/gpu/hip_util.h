@@ -52,6 +52,7 @@ class DeviceBuffer {
     if (!bytes) return;
     DeviceGuard g(device);
     SCA_HIP_CHECK(hipMalloc(&ptr_, bytes));
+    SCA_HIP_CHECK(hipMemset(ptr_, 0, bytes));  // workspaces may hold counters that must start at 0
   }
   void reset() {
     if (ptr_) {

@@ -132,8 +132,11 @@ void TreeEnsembleModel::to_device(int device) {
   }
 }
 
+// Workspace: [fused-reduce counter, padded to 256 B][chunk partial slab].
+static constexpr size_t kTreeWsHeader = 256;
+
 size_t TreeEnsembleModel::workspace_bytes(int max_rows, int) const {
-  return size_t(max_chunks_) * size_t(std::max(1, max_rows)) * sizeof(float);
+  return kTreeWsHeader + size_t(max_chunks_) * size_t(std::max(1, max_rows)) * sizeof(float);
 }
 
 void TreeEnsembleModel::plan_for(int rows, int* rows_per_block, int* plan_index) const {
@@ -141,9 +144,11 @@ void TreeEnsembleModel::plan_for(int rows, int* rows_per_block, int* plan_index)
   while (rb < rows && rb < 64) rb <<= 1;
   const int tpr = 256 / rb;
   const int row_tiles = (rows + rb - 1) / rb;
-  // Aim for ~4 workgroups per CU (256 CUs) while giving each thread >= 1 tree.
+  // Aim for ~4 workgroups per CU (256 CUs) while giving every thread of a
+  // workgroup >= 1 tree (chunk >= trees-per-row lanes): a tree traversal is a
+  // chain of dependent loads, so idle lanes buy no latency, only more slab.
   const int want_chunks = std::max(1, 1024 / std::max(1, row_tiles));
-  const int chunk = std::max(tpr / 4, (spec_.n_trees + want_chunks - 1) / want_chunks);
+  const int chunk = std::max(tpr, (spec_.n_trees + want_chunks - 1) / want_chunks);
   int idx = int(plans_.size()) - 1;
   for (int i = 0; i < int(plans_.size()); ++i)
     if (plans_[size_t(i)]->chunk_trees >= chunk) { idx = i; break; }
@@ -156,7 +161,22 @@ void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out,
   int rb, pi;
   plan_for(rows, &rb, &pi);
   const Plan& p = *plans_[size_t(pi)];
-  float* partial = static_cast<float*>(ws);
+  int* counter = static_cast<int*>(ws);
+  float* partial = reinterpret_cast<float*>(static_cast<char*>(ws) + kTreeWsHeader);
+  // Small slabs: the partial kernel's last workgroup folds + transforms (one
+  // launch per batch); the tail does <= 16 slab loads per thread.
+  const bool fused = spec_.groups <= kern::kTreeFusedMaxGroups && size_t(rows) * p.n_chunks <= 4096;
+  if (fused) {
+    const kern::TreeReduceArgs red{counter, p.group.as<int>(), spec_.groups, d_base_.as<float>(), spec_.scale,
+                                   spec_.transform, out, spec_.out_cols};
+    if (spec_.depth > 0)
+      kern::tree_perfect_fused(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
+                               spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s);
+    else
+      kern::tree_sparse_fused(X, rows, spec_.n_features, d_sparse_.as<kern::SparseNode>(), d_roots_.as<int>(),
+                              spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s);
+    return;
+  }
   if (spec_.depth > 0)
     kern::tree_perfect_partial(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
                                spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, s);

@@ -67,6 +67,28 @@ enum TreeTransform : int {
 void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,
                  const float* base_margin, float scale, int transform, double* out, int out_cols,
                  hipStream_t stream);
+// Fused variant: the partial kernel's last workgroup to finish (device-scope
+// counter, reset by that workgroup) folds the slab and writes `out` -- one
+// launch per batch instead of two.  Used for small slabs (rows x chunks) and
+// <= kTreeFusedMaxGroups output groups.  `counter` must start at 0 (it is
+// returned to 0 by every launch).
+constexpr int kTreeFusedMaxGroups = 16;
+struct TreeReduceArgs {
+  int* counter;
+  const int* chunk_group;
+  int groups;
+  const float* base_margin;
+  float scale;
+  int transform;
+  double* out;
+  int out_cols;
+};
+void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                        int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
+                        const TreeReduceArgs& red, hipStream_t stream);
+void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
+                       const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
+                       const TreeReduceArgs& red, hipStream_t stream);
 
 // ------------------------------------------------------------ combiners
 // out = mean over N inputs (each [n] fp64). inputs: device array of pointers.

@@ -78,14 +78,101 @@ __device__ __forceinline__ void reduce_write(float* red, float acc, int RB, int 
   }
 }
 
-template <int D>
+// Objective transform of one row's margins m[0..groups) (scale and base
+// margin applied here) -> o.  G > 0: loops are unrolled to G with a guard so
+// a caller's register array m[G] stays in VGPRs (no scratch); G == 0: generic.
+#define SCA_FOR_G(g) _Pragma("unroll") for (int g = 0; g < (G ? G : groups); ++g) if (G == 0 || g < groups)
+template <int G>
+__device__ __forceinline__ void apply_transform(double* m, int groups, int transform, float scale,
+                                                const float* base_margin, double* o) {
+  SCA_FOR_G(g) m[g] = m[g] * double(scale) + (base_margin ? double(base_margin[g]) : 0.0);
+  switch (transform) {
+    case kTreeSigmoid: o[0] = 1.0 / (1.0 + exp(-m[0])); break;
+    case kTreeBinaryProba: {
+      const double p = 1.0 / (1.0 + exp(-m[0]));
+      o[0] = 1.0 - p;
+      o[1] = p;
+      break;
+    }
+    case kTreeSoftmax: {
+      double mx = m[0];
+      SCA_FOR_G(g) mx = fmax(mx, m[g]);
+      double s = 0.0;
+      SCA_FOR_G(g) { m[g] = exp(m[g] - mx); s += m[g]; }
+      SCA_FOR_G(g) o[g] = m[g] / s;
+      break;
+    }
+    case kTreeIsolation: {
+      // m = mean path length / c(max_samples) (scale folds both); base = offset
+      const double raw = m[0] - (base_margin ? double(base_margin[0]) : 0.0);
+      o[0] = -exp2(-raw) - (base_margin ? double(base_margin[0]) : 0.0);
+      break;
+    }
+    default:
+      SCA_FOR_G(g) o[g] = m[g];
+  }
+}
+#undef SCA_FOR_G
+
+// Last-workgroup-reduces tail of the fused kernels.  Every workgroup has
+// written its slab rows; the one whose increment brings the device-scope
+// counter to the grid size (release fence before / acquire fence after the
+// RMW, so the other XCDs' slab writes are visible past their L2s) folds the
+// slab in fixed chunk order -- deterministic, no float atomics -- and rearms
+// the counter for the next launch.  The fold uses the whole workgroup:
+// RB rows x (256 / RB) chunk lanes, lanes combined through LDS per group.
+__device__ void fused_tail(const float* partial, int rows, int n_chunks, const TreeReduceArgs& red) {
+  __shared__ int s_last;
+  __shared__ double s_fold[kBlock];
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(red.counter, 1) == int(gridDim.x * gridDim.y) - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  int RB = 1;
+  while (RB < rows && RB < kBlock) RB <<= 1;
+  const int r_local = int(threadIdx.x) & (RB - 1), slot = int(threadIdx.x) / RB, tpr = kBlock / RB;
+  // Per-group margins are folded into the output row itself (out_cols >=
+  // groups for every objective) and transformed in place, so the tail adds no
+  // register pressure to the traversal part of the kernel.
+  for (int row0 = 0; row0 < rows; row0 += RB) {
+    const int r = row0 + r_local;
+    double* o = red.out + size_t(r) * red.out_cols;
+    for (int g = 0; g < red.groups; ++g) {
+      double acc = 0.0;
+      if (r < rows) {
+        if (red.groups == 1) {  // common case: unconditional, unrolled loads (ILP across the slab)
+#pragma unroll 4
+          for (int c = slot; c < n_chunks; c += tpr) acc += double(partial[size_t(c) * rows + r]);
+        } else {
+          for (int c = slot; c < n_chunks; c += tpr)
+            if (red.chunk_group[c] == g) acc += double(partial[size_t(c) * rows + r]);
+        }
+      }
+      if (tpr > 1) {
+        s_fold[threadIdx.x] = acc;
+        __syncthreads();
+        if (slot == 0)
+          for (int j = 1; j < tpr; ++j) acc += s_fold[j * RB + r_local];
+        __syncthreads();
+      }
+      if (slot == 0 && r < rows) o[g] = acc;
+    }
+    if (slot == 0 && r < rows) apply_transform<0>(o, red.groups, red.transform, red.scale, red.base_margin, o);
+  }
+  if (threadIdx.x == 0) *red.counter = 0;
+}
+
+template <int D, bool FUSED>
 __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restrict__ X, int rows, int F,
                                                           const TreeNode* __restrict__ nodes,
                                                           const float* __restrict__ leaves, int depth, int cmp_le,
                                                           const int* __restrict__ chunk_begin, int RB,
-                                                          int stage_lds, float* __restrict__ partial) {
+                                                          int stage_lds, float* __restrict__ partial, int n_chunks,
+                                                          TreeReduceArgs red) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* red = lds;            // [kBlock]
+  float* red_lds = lds;        // [kBlock]
   float* tile = lds + kBlock;  // [RB * F] when staged
   const int row0 = blockIdx.x * RB;
   const int chunk = blockIdx.y;
@@ -127,16 +214,19 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
   }
   if (!row_ok) acc = 0.f;
   if (stage_lds) __syncthreads();  // tile no longer needed; `red` is disjoint anyway
-  reduce_write(red, acc, RB, row0, rows, chunk, partial);
+  reduce_write(red_lds, acc, RB, row0, rows, chunk, partial);
+  if constexpr (FUSED) fused_tail(partial, rows, n_chunks, red);
 }
 
+template <bool FUSED>
 __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restrict__ X, int rows, int F,
                                                          const SparseNode* __restrict__ nodes,
                                                          const int* __restrict__ tree_root, int cmp_le,
                                                          const int* __restrict__ chunk_begin, int RB, int stage_lds,
-                                                         float* __restrict__ partial) {
+                                                         float* __restrict__ partial, int n_chunks,
+                                                         TreeReduceArgs red) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* red = lds;
+  float* red_lds = lds;
   float* tile = lds + kBlock;
   const int row0 = blockIdx.x * RB;
   const int chunk = blockIdx.y;
@@ -168,7 +258,8 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
     }
   }
   if (stage_lds) __syncthreads();
-  reduce_write(red, acc, RB, row0, rows, chunk, partial);
+  reduce_write(red_lds, acc, RB, row0, rows, chunk, partial);
+  if constexpr (FUSED) fused_tail(partial, rows, n_chunks, red);
 }
 
 constexpr int kMaxGroups = 64;
@@ -196,38 +287,45 @@ __global__ __launch_bounds__(kBlock) void reduce_transform(const float* __restri
     const double* o2 = m_lds + size_t(s * RB + r_local) * groups;
     for (int g = 0; g < groups; ++g) m[g] += o2[g];
   }
-  for (int g = 0; g < groups; ++g) m[g] = m[g] * double(scale) + (base_margin ? double(base_margin[g]) : 0.0);
-  double* o = out + size_t(r) * out_cols;
-  switch (transform) {
-    case kTreeSigmoid: o[0] = 1.0 / (1.0 + exp(-m[0])); break;
-    case kTreeBinaryProba: {
-      const double p = 1.0 / (1.0 + exp(-m[0]));
-      o[0] = 1.0 - p;
-      o[1] = p;
-      break;
-    }
-    case kTreeSoftmax: {
-      double mx = m[0];
-      for (int g = 1; g < groups; ++g) mx = fmax(mx, m[g]);
-      double s = 0.0;
-      for (int g = 0; g < groups; ++g) { m[g] = exp(m[g] - mx); s += m[g]; }
-      for (int g = 0; g < groups; ++g) o[g] = m[g] / s;
-      break;
-    }
-    case kTreeIsolation: {
-      // m = mean path length / c(max_samples) (scale folds both); base = offset
-      const double raw = m[0] - (base_margin ? double(base_margin[0]) : 0.0);
-      o[0] = -exp2(-raw) - (base_margin ? double(base_margin[0]) : 0.0);
-      break;
-    }
-    default:
-      for (int g = 0; g < groups; ++g) o[g] = m[g];
-  }
+  apply_transform<0>(m, groups, transform, scale, base_margin, out + size_t(r) * out_cols);
 }
 
 int lds_bytes_for(int RB, int F, bool* stage) {
   *stage = RB * F <= kMaxLdsFloats;
   return int((kBlock + (*stage ? RB * F : 0)) * sizeof(float));
+}
+
+template <bool FUSED>
+void launch_perfect(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                    int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
+                    hipStream_t s) {
+  bool stage;
+  const int lds = lds_bytes_for(RB, F, &stage);
+  dim3 grid((rows + RB - 1) / RB, n_chunks);
+#define SCA_TREE_CASE(DD)                                                                                        \
+  case DD:                                                                                                      \
+    hipLaunchKernelGGL((perfect_partial<DD, FUSED>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, depth, \
+                       cmp_le, chunk_begin, RB, int(stage), partial, n_chunks, red);                           \
+    break;
+  switch (depth) {
+    SCA_TREE_CASE(1) SCA_TREE_CASE(2) SCA_TREE_CASE(3) SCA_TREE_CASE(4) SCA_TREE_CASE(5) SCA_TREE_CASE(6)
+    SCA_TREE_CASE(7) SCA_TREE_CASE(8) SCA_TREE_CASE(9) SCA_TREE_CASE(10) SCA_TREE_CASE(11) SCA_TREE_CASE(12)
+    default:
+      hipLaunchKernelGGL((perfect_partial<0, FUSED>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, depth,
+                         cmp_le, chunk_begin, RB, int(stage), partial, n_chunks, red);
+  }
+#undef SCA_TREE_CASE
+}
+
+template <bool FUSED>
+void launch_sparse(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
+                   const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
+                   hipStream_t s) {
+  bool stage;
+  const int lds = lds_bytes_for(RB, F, &stage);
+  dim3 grid((rows + RB - 1) / RB, n_chunks);
+  hipLaunchKernelGGL((sparse_partial<FUSED>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, tree_root, cmp_le,
+                     chunk_begin, RB, int(stage), partial, n_chunks, red);
 }
 
 }  // namespace
@@ -236,32 +334,28 @@ void tree_perfect_partial(const double* X, int rows, int F, const TreeNode* node
                           int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial,
                           hipStream_t s) {
   if (rows <= 0 || n_chunks <= 0) return;
-  bool stage;
-  const int lds = lds_bytes_for(RB, F, &stage);
-  dim3 grid((rows + RB - 1) / RB, n_chunks);
-#define SCA_TREE_CASE(DD)                                                                                        \
-  case DD:                                                                                                      \
-    hipLaunchKernelGGL(perfect_partial<DD>, grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, depth, cmp_le, \
-                       chunk_begin, RB, int(stage), partial);                                                   \
-    break;
-  switch (depth) {
-    SCA_TREE_CASE(1) SCA_TREE_CASE(2) SCA_TREE_CASE(3) SCA_TREE_CASE(4) SCA_TREE_CASE(5) SCA_TREE_CASE(6)
-    SCA_TREE_CASE(7) SCA_TREE_CASE(8) SCA_TREE_CASE(9) SCA_TREE_CASE(10) SCA_TREE_CASE(11) SCA_TREE_CASE(12)
-    default:
-      hipLaunchKernelGGL(perfect_partial<0>, grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, depth, cmp_le,
-                         chunk_begin, RB, int(stage), partial);
-  }
-#undef SCA_TREE_CASE
+  launch_perfect<false>(X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, n_chunks, RB, partial,
+                        TreeReduceArgs{}, s);
 }
 
 void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
                          const int* chunk_begin, int n_chunks, int RB, float* partial, hipStream_t s) {
   if (rows <= 0 || n_chunks <= 0) return;
-  bool stage;
-  const int lds = lds_bytes_for(RB, F, &stage);
-  dim3 grid((rows + RB - 1) / RB, n_chunks);
-  hipLaunchKernelGGL(sparse_partial, grid, dim3(kBlock), lds, s, X, rows, F, nodes, tree_root, cmp_le, chunk_begin,
-                     RB, int(stage), partial);
+  launch_sparse<false>(X, rows, F, nodes, tree_root, cmp_le, chunk_begin, n_chunks, RB, partial, TreeReduceArgs{}, s);
+}
+
+void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                        int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial,
+                        const TreeReduceArgs& red, hipStream_t s) {
+  if (rows <= 0 || n_chunks <= 0) return;
+  launch_perfect<true>(X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, n_chunks, RB, partial, red, s);
+}
+
+void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
+                       const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
+                       hipStream_t s) {
+  if (rows <= 0 || n_chunks <= 0) return;
+  launch_sparse<true>(X, rows, F, nodes, tree_root, cmp_le, chunk_begin, n_chunks, RB, partial, red, s);
 }
 
 void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,

@@ -26,7 +26,13 @@ if [ "${TESTS:-1}" = "1" ]; then
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
 for cfg in ${CONFIGS:-"base::" "base2::" "srv8::--server-threads 8" "srv10::--server-threads 10 --client-threads 5" "slots2::--slots 2" "slots8::--slots 8" "grpc::--api grpc"}; do
-  tag=${cfg%%::*}; args=${cfg#*::}
+  tag=${cfg%%::*}; args=${cfg#*::}; args=${args//_/ }  # "_" separates arguments inside one config word
   run "$tag" $args
 done
+if [ "${PROF:-0}" = "1" ]; then
+  export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/sweep/prof -o run --output-format csv -- \
+    python3 bench.py --steps 3 --warmup 1 --step-requests 20000 > gpurun_out/sweep/prof.log 2>&1
+  echo "prof rc=$?"
+fi
 echo done
