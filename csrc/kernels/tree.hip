@@ -65,6 +65,10 @@ __device__ __forceinline__ void stage_tile(float* tile, const double* __restrict
 }
 
 // Reduce per-thread accumulators of the same row and write the slab row.
+// COHERENT: the slab is read back inside the same launch by the fused tail on
+// another XCD, so rows are written with agent-scope (sc1, write-through past
+// this XCD's L2) stores -- no whole-L2 writeback/invalidate fences needed.
+template <bool COHERENT>
 __device__ __forceinline__ void reduce_write(float* red, float acc, int RB, int row0, int rows, int chunk,
                                              float* __restrict__ partial) {
   red[threadIdx.x] = acc;
@@ -74,7 +78,12 @@ __device__ __forceinline__ void reduce_write(float* red, float acc, int RB, int 
     float s = 0.f;
     for (int j = 0; j < tpr; ++j) s += red[j * RB + threadIdx.x];
     const int r = row0 + threadIdx.x;
-    if (r < rows) partial[size_t(chunk) * rows + r] = s;
+    if (r < rows) {
+      if constexpr (COHERENT)
+        __hip_atomic_store(partial + size_t(chunk) * rows + r, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        partial[size_t(chunk) * rows + r] = s;
+    }
   }
 }
 
@@ -115,21 +124,29 @@ __device__ __forceinline__ void apply_transform(double* m, int groups, int trans
 #undef SCA_FOR_G
 
 // Last-workgroup-reduces tail of the fused kernels.  Every workgroup has
-// written its slab rows; the one whose increment brings the device-scope
-// counter to the grid size (release fence before / acquire fence after the
-// RMW, so the other XCDs' slab writes are visible past their L2s) folds the
-// slab in fixed chunk order -- deterministic, no float atomics -- and rearms
-// the counter for the next launch.  The fold uses the whole workgroup:
-// RB rows x (256 / RB) chunk lanes, lanes combined through LDS per group.
+// written its slab rows with write-through agent-scope stores; it waits for
+// them to complete (s_waitcnt), then one lane bumps the device-scope counter.
+// The workgroup that brings it to the grid size folds the slab -- read with
+// agent-scope loads that bypass stale L2 lines -- in fixed chunk order
+// (deterministic, no float atomics) and rearms the counter.  A __threadfence()
+// here would instead emit buffer_wbl2 + buffer_inv on every workgroup, which
+// flushes each XCD's L2 and evicts the resident tree model (measured 15 us vs
+// ~6 us per launch).  The fold uses the whole workgroup: RB rows x (256 / RB)
+// chunk lanes, lanes combined through LDS per group.
+__device__ __forceinline__ float coherent_load(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ void fused_tail(const float* partial, int rows, int n_chunks, const TreeReduceArgs& red) {
   __shared__ int s_last;
   __shared__ double s_fold[kBlock];
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slab stores acknowledged at the coherence point
   __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(red.counter, 1) == int(gridDim.x * gridDim.y) - 1;
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(red.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             int(gridDim.x * gridDim.y) - 1;
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
   int RB = 1;
   while (RB < rows && RB < kBlock) RB <<= 1;
   const int r_local = int(threadIdx.x) & (RB - 1), slot = int(threadIdx.x) / RB, tpr = kBlock / RB;
@@ -144,10 +161,10 @@ __device__ void fused_tail(const float* partial, int rows, int n_chunks, const T
       if (r < rows) {
         if (red.groups == 1) {  // common case: unconditional, unrolled loads (ILP across the slab)
 #pragma unroll 4
-          for (int c = slot; c < n_chunks; c += tpr) acc += double(partial[size_t(c) * rows + r]);
+          for (int c = slot; c < n_chunks; c += tpr) acc += double(coherent_load(partial + size_t(c) * rows + r));
         } else {
           for (int c = slot; c < n_chunks; c += tpr)
-            if (red.chunk_group[c] == g) acc += double(partial[size_t(c) * rows + r]);
+            if (red.chunk_group[c] == g) acc += double(coherent_load(partial + size_t(c) * rows + r));
         }
       }
       if (tpr > 1) {
@@ -161,7 +178,7 @@ __device__ void fused_tail(const float* partial, int rows, int n_chunks, const T
     }
     if (slot == 0 && r < rows) apply_transform<0>(o, red.groups, red.transform, red.scale, red.base_margin, o);
   }
-  if (threadIdx.x == 0) *red.counter = 0;
+  if (threadIdx.x == 0) __hip_atomic_store(red.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int D, bool FUSED>
@@ -214,7 +231,7 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
   }
   if (!row_ok) acc = 0.f;
   if (stage_lds) __syncthreads();  // tile no longer needed; `red` is disjoint anyway
-  reduce_write(red_lds, acc, RB, row0, rows, chunk, partial);
+  reduce_write<FUSED>(red_lds, acc, RB, row0, rows, chunk, partial);
   if constexpr (FUSED) fused_tail(partial, rows, n_chunks, red);
 }
 
@@ -258,7 +275,7 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
     }
   }
   if (stage_lds) __syncthreads();
-  reduce_write(red_lds, acc, RB, row0, rows, chunk, partial);
+  reduce_write<FUSED>(red_lds, acc, RB, row0, rows, chunk, partial);
   if constexpr (FUSED) fused_tail(partial, rows, n_chunks, red);
 }
 

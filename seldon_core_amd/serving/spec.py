@@ -182,11 +182,19 @@ def apply_defaults(sdep: Dict, first_port: Optional[int] = None) -> Dict:
     return sdep
 
 
-def validate(sdep: Dict, bound: Optional[set] = None) -> List[str]:
-    """Validating-webhook rules.  ``bound``: node names with an in-process
+def validate(sdep: Dict, bound: Optional[set] = None, schema: bool = True) -> List[str]:
+    """Structural checks against ``schema/seldondeployment.schema.json`` (what
+    the API server enforces from the CRD's openAPIV3Schema) followed by the
+    validating-webhook rules.  ``bound``: node names with an in-process
     implementation (count as having a container)."""
     bound = bound or set()
     errors: List[str] = []
+    if schema:
+        from .jsonschema import validate_schema
+
+        errors = validate_schema(sdep if "spec" in sdep else {"spec": sdep})
+        if errors:
+            return errors
     preds = predictors(sdep)
     seen = set()
     for i, p in enumerate(preds):

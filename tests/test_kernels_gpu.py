@@ -67,6 +67,27 @@ def test_tree_perfect_vs_cpu(C_, rows):
         unit.stop()
 
 
+def test_tree_fused_reduce_many_batches(C_):
+    """Fused last-workgroup reduce: many back-to-back launches of varying
+    size from concurrent callers (several slots, one counter each) must all
+    match, i.e. the counter is rearmed and no slab value is read stale."""
+    import concurrent.futures as cf
+
+    from seldon_core_amd.models import synthetic_xgboost, to_row_model
+
+    ens = synthetic_xgboost(1000, 8, 32, seed=11)
+    unit = C_.BatchedUnit(to_row_model(ens), 0, max_batch=1024, slots=4)
+    rng = np.random.default_rng(5)
+    Xs = [rng.standard_normal((n, 32)) for n in list(range(1, 41)) * 3 + [64, 128, 300]]
+    try:
+        with cf.ThreadPoolExecutor(8) as ex:
+            outs = list(ex.map(unit.run, Xs))
+        for X, got in zip(Xs, outs):
+            np.testing.assert_allclose(np.asarray(got).reshape(-1), ens.predict(X).reshape(-1), rtol=2e-5, atol=2e-5)
+    finally:
+        unit.stop()
+
+
 def test_tree_softmax_groups(C_):
     """multi:softprob-style: 3 groups, softmax transform."""
     from seldon_core_amd.models import to_row_model
