@@ -62,7 +62,7 @@ void LinearModel::run_cpu(const double* X, int rows, int, double* out) const {
 }
 
 // ------------------------------------------------------------ tree ensemble
-static const int kPlanSizes[] = {8, 16, 32, 64, 128, 256, 512};
+static const int kPlanSizes[] = {1, 2, 4, 8, 16, 32, 64, 128, 256, 512};
 
 TreeEnsembleModel::TreeEnsembleModel(TreeEnsembleSpec spec) : spec_(std::move(spec)) {
   const int T = spec_.n_trees;
@@ -139,27 +139,40 @@ size_t TreeEnsembleModel::workspace_bytes(int max_rows, int) const {
   return kTreeWsHeader + size_t(max_chunks_) * size_t(std::max(1, max_rows)) * sizeof(float);
 }
 
-void TreeEnsembleModel::plan_for(int rows, int* rows_per_block, int* plan_index) const {
+void TreeEnsembleModel::plan_for(int rows, int* rows_per_block, int* plan_index, int* lds_trees) const {
   int rb = 1;
   while (rb < rows && rb < 64) rb <<= 1;
   const int tpr = 256 / rb;
   const int row_tiles = (rows + rb - 1) / rb;
-  // Aim for ~4 workgroups per CU (256 CUs) while giving every thread of a
-  // workgroup >= 1 tree (chunk >= trees-per-row lanes): a tree traversal is a
-  // chain of dependent loads, so idle lanes buy no latency, only more slab.
+  *rows_per_block = rb;
+  if (lds_trees) *lds_trees = 0;
+  // Perfect trees that fit: chunks as large as LDS allows (one staging round
+  // trip per workgroup amortised over every tree and row it holds).
+  const int cap = spec_.depth > 0 ? kern::tree_lds_max_trees(spec_.depth, rb, spec_.n_features) : 0;
+  if (cap >= 1) {
+    int idx = 0;
+    for (int i = 0; i < int(plans_.size()); ++i)
+      if (plans_[size_t(i)]->chunk_trees <= cap) idx = i;
+    *plan_index = idx;
+    if (lds_trees) *lds_trees = plans_[size_t(idx)]->chunk_trees;
+    return;
+  }
+  // Otherwise aim for ~4 workgroups per CU (256 CUs) while giving every
+  // thread of a workgroup >= 1 tree (chunk >= trees-per-row lanes): a tree
+  // traversal from L2 is a chain of dependent loads, so idle lanes buy no
+  // latency, only more slab.
   const int want_chunks = std::max(1, 1024 / std::max(1, row_tiles));
   const int chunk = std::max(tpr, (spec_.n_trees + want_chunks - 1) / want_chunks);
   int idx = int(plans_.size()) - 1;
   for (int i = 0; i < int(plans_.size()); ++i)
     if (plans_[size_t(i)]->chunk_trees >= chunk) { idx = i; break; }
-  *rows_per_block = rb;
   *plan_index = idx;
 }
 
 void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) {
   (void)cols;
-  int rb, pi;
-  plan_for(rows, &rb, &pi);
+  int rb, pi, lt;
+  plan_for(rows, &rb, &pi, &lt);
   const Plan& p = *plans_[size_t(pi)];
   int* counter = static_cast<int*>(ws);
   float* partial = reinterpret_cast<float*>(static_cast<char*>(ws) + kTreeWsHeader);
@@ -171,7 +184,7 @@ void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out,
                                    spec_.transform, out, spec_.out_cols};
     if (spec_.depth > 0)
       kern::tree_perfect_fused(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
-                               spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s);
+                               spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s, lt);
     else
       kern::tree_sparse_fused(X, rows, spec_.n_features, d_sparse_.as<kern::SparseNode>(), d_roots_.as<int>(),
                               spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s);
@@ -179,7 +192,7 @@ void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out,
   }
   if (spec_.depth > 0)
     kern::tree_perfect_partial(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
-                               spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, s);
+                               spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, s, lt);
   else
     kern::tree_sparse_partial(X, rows, spec_.n_features, d_sparse_.as<kern::SparseNode>(), d_roots_.as<int>(),
                               spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, s);

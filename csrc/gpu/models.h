@@ -119,7 +119,7 @@ class TreeEnsembleModel : public RowModel {
   bool zero_copy_input() const override { return false; }  // every tree-chunk block stages the X tile
   std::shared_ptr<RowModel> clone() const override { return with_meta(std::make_shared<TreeEnsembleModel>(spec_)); }
   // Launch geometry chosen for a batch (exposed for tests/benchmarks).
-  void plan_for(int rows, int* rows_per_block, int* plan_index) const;
+  void plan_for(int rows, int* rows_per_block, int* plan_index, int* lds_trees = nullptr) const;
 
  private:
   struct Plan {

@@ -40,9 +40,14 @@ struct TreeNode {
 // X is the fp64 request matrix [rows, F] (converted to fp32 on load, as
 // XGBoost's DMatrix does).  cmp_le: 1 = sklearn `x <= thr`, 0 = XGBoost `x < thr`.
 // rows_per_block (1..64, power of two) trades row- vs tree-parallelism.
+// lds_trees > 0: chunks hold at most that many trees and are staged in LDS
+// (perfect trees of depth <= 10; see tree_lds_max_trees).
 void tree_perfect_partial(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves,
                           int depth, int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block,
-                          float* partial, hipStream_t stream);
+                          float* partial, hipStream_t stream, int lds_trees = 0);
+// Largest chunk (in trees) whose nodes + leaves fit in LDS next to the
+// feature tile for this geometry (0: depth too large for LDS staging).
+int tree_lds_max_trees(int depth, int rows_per_block, int F);
 // General trees (arbitrary depth): node {thr, feat|flags, left, right}.
 struct SparseNode {
   float thr;
@@ -85,7 +90,7 @@ struct TreeReduceArgs {
 };
 void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
-                        const TreeReduceArgs& red, hipStream_t stream);
+                        const TreeReduceArgs& red, hipStream_t stream, int lds_trees = 0);
 void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
                        const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
                        const TreeReduceArgs& red, hipStream_t stream);

@@ -16,6 +16,8 @@
 // tree_reduce folds (deterministic, no float atomics).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace sca::kern {
@@ -181,38 +183,52 @@ __device__ void fused_tail(const float* partial, int rows, int n_chunks, const T
   if (threadIdx.x == 0) __hip_atomic_store(red.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int D, bool FUSED>
+// TREES_LDS: the chunk's trees (nodes + leaves, contiguous in HBM) are copied
+// into LDS with wide coalesced loads before traversal, so each of the D + 1
+// dependent loads of a descent is a ds_read (~100 cycles) instead of an L2/MALL
+// round trip (~1 us): one memory round trip per workgroup instead of D + 1 per
+// tree.  The host caps the chunk at what fits (lds_trees trees).
+template <int D, bool FUSED, bool TREES_LDS>
 __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restrict__ X, int rows, int F,
                                                           const TreeNode* __restrict__ nodes,
                                                           const float* __restrict__ leaves, int depth, int cmp_le,
                                                           const int* __restrict__ chunk_begin, int RB,
                                                           int stage_lds, float* __restrict__ partial, int n_chunks,
-                                                          TreeReduceArgs red) {
+                                                          int lds_trees, TreeReduceArgs red) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* red_lds = lds;        // [kBlock]
   float* tile = lds + kBlock;  // [RB * F] when staged
+  const int tile_floats = stage_lds ? ((RB * F + 3) & ~3) : 0;
+  const int n_internal = (1 << depth) - 1;
+  TreeNode* s_nodes = reinterpret_cast<TreeNode*>(lds + kBlock + tile_floats);  // [lds_trees][n_internal]
+  float* s_leaves = reinterpret_cast<float*>(s_nodes + size_t(lds_trees) * n_internal);
   const int row0 = blockIdx.x * RB;
   const int chunk = blockIdx.y;
   const int r_local = threadIdx.x & (RB - 1);
   const int slot = threadIdx.x / RB;
   const int tpr = kBlock / RB;
-  const float* xs;
-  float xreg_dummy = 0.f;
-  (void)xreg_dummy;
-  if (stage_lds) {
-    stage_tile(tile, X, row0, rows, RB, F);
-    __syncthreads();
-    xs = tile + r_local * F;
-  } else {
-    xs = nullptr;
-  }
-  const int n_internal = (1 << depth) - 1;
   const int t0 = chunk_begin[chunk], t1 = chunk_begin[chunk + 1];
+  if (stage_lds) stage_tile(tile, X, row0, rows, RB, F);
+  if constexpr (TREES_LDS) {
+    const int nn = (t1 - t0) * n_internal, nl = (t1 - t0) * (n_internal + 1);
+    const uint2* gn = reinterpret_cast<const uint2*>(nodes + size_t(t0) * n_internal);
+    uint2* sn = reinterpret_cast<uint2*>(s_nodes);
+    for (int i = threadIdx.x; i < nn; i += kBlock) sn[i] = gn[i];
+    const float4* gl = reinterpret_cast<const float4*>(leaves + size_t(t0) * (n_internal + 1));  // 2^D floats/tree
+    float4* sl = reinterpret_cast<float4*>(s_leaves);
+    if ((nl & 3) == 0 && (n_internal + 1) % 4 == 0) {
+      for (int i = threadIdx.x; i < nl / 4; i += kBlock) sl[i] = gl[i];
+    } else {
+      for (int i = threadIdx.x; i < nl; i += kBlock) s_leaves[i] = leaves[size_t(t0) * (n_internal + 1) + i];
+    }
+  }
+  if (stage_lds || TREES_LDS) __syncthreads();
+  const float* xs = stage_lds ? tile + r_local * F : nullptr;
   float acc = 0.f;
   const bool row_ok = row0 + r_local < rows;
   if (stage_lds || row_ok) {
     for (int t = t0 + slot; t < t1; t += tpr) {
-      const TreeNode* tn = nodes + size_t(t) * n_internal;
+      const TreeNode* tn = TREES_LDS ? s_nodes + size_t(t - t0) * n_internal : nodes + size_t(t) * n_internal;
       int idx;
       if (stage_lds) {
         idx = D > 0 ? descend_fixed<D>(tn, xs, cmp_le) : descend_any(tn, xs, depth, cmp_le);
@@ -226,7 +242,9 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
           idx = 2 * idx + (go_left(x, nd.thr, nd.feat, cmp_le) ? 1 : 2);
         }
       }
-      acc += leaves[size_t(t) * (n_internal + 1) + (idx - n_internal)];
+      const float* lf = TREES_LDS ? s_leaves + size_t(t - t0) * (n_internal + 1)
+                                  : leaves + size_t(t) * (n_internal + 1);
+      acc += lf[idx - n_internal];
     }
   }
   if (!row_ok) acc = 0.f;
@@ -312,26 +330,38 @@ int lds_bytes_for(int RB, int F, bool* stage) {
   return int((kBlock + (*stage ? RB * F : 0)) * sizeof(float));
 }
 
+constexpr int kMaxTreeLdsDepth = 10;
+constexpr int kMaxLdsBytes = 64 * 1024;
+
+int tree_bytes(int depth) { return ((1 << depth) - 1) * int(sizeof(TreeNode)) + (1 << depth) * int(sizeof(float)); }
+
 template <bool FUSED>
 void launch_perfect(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                     int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
-                    hipStream_t s) {
+                    int lds_trees, hipStream_t s) {
   bool stage;
-  const int lds = lds_bytes_for(RB, F, &stage);
+  int lds = lds_bytes_for(RB, F, &stage);
+  if (stage) lds = int((kBlock + ((RB * F + 3) & ~3)) * sizeof(float));
+  if (depth > kMaxTreeLdsDepth || lds + lds_trees * tree_bytes(depth) > kMaxLdsBytes) lds_trees = 0;
+  lds += lds_trees * tree_bytes(depth);
   dim3 grid((rows + RB - 1) / RB, n_chunks);
-#define SCA_TREE_CASE(DD)                                                                                        \
-  case DD:                                                                                                      \
-    hipLaunchKernelGGL((perfect_partial<DD, FUSED>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, depth, \
-                       cmp_le, chunk_begin, RB, int(stage), partial, n_chunks, red);                           \
+#define SCA_TREE_LAUNCH(DD, TL)                                                                                  \
+  hipLaunchKernelGGL((perfect_partial<DD, FUSED, TL>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves,   \
+                     depth, cmp_le, chunk_begin, RB, int(stage), partial, n_chunks, lds_trees, red)
+#define SCA_TREE_CASE(DD)                                  \
+  case DD:                                                 \
+    if (lds_trees) SCA_TREE_LAUNCH(DD, true);              \
+    else SCA_TREE_LAUNCH(DD, false);                       \
     break;
   switch (depth) {
     SCA_TREE_CASE(1) SCA_TREE_CASE(2) SCA_TREE_CASE(3) SCA_TREE_CASE(4) SCA_TREE_CASE(5) SCA_TREE_CASE(6)
-    SCA_TREE_CASE(7) SCA_TREE_CASE(8) SCA_TREE_CASE(9) SCA_TREE_CASE(10) SCA_TREE_CASE(11) SCA_TREE_CASE(12)
-    default:
-      hipLaunchKernelGGL((perfect_partial<0, FUSED>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, depth,
-                         cmp_le, chunk_begin, RB, int(stage), partial, n_chunks, red);
+    SCA_TREE_CASE(7) SCA_TREE_CASE(8) SCA_TREE_CASE(9) SCA_TREE_CASE(10)
+    case 11: SCA_TREE_LAUNCH(11, false); break;
+    case 12: SCA_TREE_LAUNCH(12, false); break;
+    default: SCA_TREE_LAUNCH(0, false);
   }
 #undef SCA_TREE_CASE
+#undef SCA_TREE_LAUNCH
 }
 
 template <bool FUSED>
@@ -349,10 +379,18 @@ void launch_sparse(const double* X, int rows, int F, const SparseNode* nodes, co
 
 void tree_perfect_partial(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                           int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial,
-                          hipStream_t s) {
+                          hipStream_t s, int lds_trees) {
   if (rows <= 0 || n_chunks <= 0) return;
   launch_perfect<false>(X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, n_chunks, RB, partial,
-                        TreeReduceArgs{}, s);
+                        TreeReduceArgs{}, lds_trees, s);
+}
+
+int tree_lds_max_trees(int depth, int rows_per_block, int F) {
+  if (depth <= 0 || depth > kMaxTreeLdsDepth) return 0;
+  bool stage;
+  int lds = lds_bytes_for(rows_per_block, F, &stage);
+  if (stage) lds = int((kBlock + ((rows_per_block * F + 3) & ~3)) * sizeof(float));
+  return std::max(0, (kMaxLdsBytes - lds) / tree_bytes(depth));
 }
 
 void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
@@ -363,9 +401,10 @@ void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nod
 
 void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial,
-                        const TreeReduceArgs& red, hipStream_t s) {
+                        const TreeReduceArgs& red, hipStream_t s, int lds_trees) {
   if (rows <= 0 || n_chunks <= 0) return;
-  launch_perfect<true>(X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, n_chunks, RB, partial, red, s);
+  launch_perfect<true>(X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, n_chunks, RB, partial, red, lds_trees,
+                       s);
 }
 
 void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
@@ -381,9 +420,12 @@ void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_
   if (groups > kMaxGroups) groups = kMaxGroups;
   // Keep LDS <= 64 KB per block: 256 threads up to 32 groups, 64 beyond.
   const int nthr = groups > 32 ? 64 : kBlock;
-  int RB = 1;
-  while (RB < rows && RB < 64) RB <<= 1;
-  if (n_chunks <= 1) RB = nthr;  // nothing to split: one row per thread
+  // Lanes per row: enough that each sums <= 4 slab entries (independent loads
+  // in flight), the rest of the block takes more rows -> many small blocks
+  // instead of a few long serial ones.
+  int L = 1;
+  while (L < nthr && L * 4 < n_chunks) L <<= 1;
+  const int RB = nthr / L;
   const size_t lds = size_t(nthr) * groups * sizeof(double);
   hipLaunchKernelGGL(reduce_transform, dim3((rows + RB - 1) / RB), dim3(nthr), lds, s, partial, rows, n_chunks,
                      chunk_group, groups, base_margin, scale, transform, out, out_cols, RB);

@@ -187,16 +187,30 @@ class SeldonClient:
         except SeldonClientException as e:
             return SeldonClientFeedback(self._ret(c, fb, prediction_pb2.Feedback), None, False, e.message)
 
-    def explain(self, data=None, shape=(1, 1), names=None, **kw) -> SeldonClientPrediction:
+    def explain(self, data=None, shape=(1, 1), names=None, bin_data=None, str_data=None, headers=None,
+                http_path=None, gateway_prefix=None, **kw) -> Dict:
+        """REST explain call through the gateway to ``<dep>-explainer``
+        (reference seldon_client.py:353-425, 1223-1321): returns the
+        explanation JSON, or ``{"success": False, "response_code": code}``."""
         c = self._cfg(kw)
-        req = _payload(data, None, None, None, names, c["payload_type"], shape, None)
+        if c["transport"] == "grpc":
+            raise SeldonClientException("gRPC not supported for explain")
+        req = _payload(data, bin_data, str_data, None, names, c["payload_type"], shape, None)
         dep, ns = c.get("deployment_name"), c.get("namespace")
-        url = "http://" + c["gateway_endpoint"] + "/seldon/" + (ns + "/" if ns else "") + f"{dep}-explainer/models/{dep}:explain"
+        base = "http://" + c["gateway_endpoint"]
+        if http_path is not None:
+            url = f"{base}/seldon/{ns}/{dep}{http_path}"
+        elif gateway_prefix is not None:
+            url = f"{base}{gateway_prefix}/models/{dep}:explain"
+        else:
+            url = base + "/seldon/" + (ns + "/" if ns else "") + f"{dep}-explainer/models/{dep}:explain"
+        body = json.dumps(req).encode()
+        r = urllib.request.Request(url, data=body, headers={"Content-Type": "application/json", **(headers or {})})
         try:
-            resp = self._rest(url, req, timeout=c["timeout"])
-            return SeldonClientPrediction(req, resp, True, "")
-        except (SeldonClientException, urllib.error.URLError) as e:
-            return SeldonClientPrediction(req, None, False, str(e))
+            with urllib.request.urlopen(r, timeout=c["timeout"]) as resp:
+                return json.loads(resp.read())
+        except urllib.error.HTTPError as e:
+            return {"success": False, "response_code": e.code}
 
     def microservice(self, method: str = "predict", data=None, shape=(1, 1), names=None, datas: Optional[List] = None,
                      ndatas: Optional[int] = None, bin_data=None, str_data=None, json_data=None, meta=None,

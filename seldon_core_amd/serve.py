@@ -53,6 +53,8 @@ def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
     ap.add_argument("--no-fuse", action="store_true", help="disable device-graph fusion")
     ap.add_argument("--max-restarts", type=int, default=5, help="per worker per minute")
     ap.add_argument("--log-level", default=os.environ.get("SELDON_LOG_LEVEL", "INFO"))
+    ap.add_argument("--explainer-port", type=int, default=None,
+                    help="port of the predictor's explainer (default: explainer.endpoint.service_port or 9000)")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -96,6 +98,17 @@ def run_worker(args: argparse.Namespace) -> int:
     logger.info("worker %s serving %s: REST :%s gRPC :%s admin :%s (device %s, units %s)", rank,
                 dep.predictor.get("name"), h.http_port, h.grpc_port, cfg.admin_port, dep.device,
                 {n: dep.engine.unit_kind(n) for n in dep.engine.node_names()})
+    explainer = None
+    if rank == "0" and (dep.predictor.get("explainer") or {}).get("type"):
+        # The reference runs the explainer as its own Deployment pointed at the
+        # predictor (seldondeployment_explainers.go:32-184); here it shares the
+        # worker process and labels perturbation batches through the engine.
+        from .explainers.server import deployment_predictor, from_spec
+
+        model_name = (sdep.get("metadata") or {}).get("name") or cfg.deployment_name
+        explainer = from_spec(dep.predictor, deployment_predictor(dep), model_name, cfg.host, args.explainer_port)
+        explainer.start()
+        logger.info("explainer %s on :%d", dep.predictor["explainer"]["type"], explainer.port)
     stop = threading.Event()
 
     def on_signal(signum, frame):  # noqa: ARG001
@@ -104,6 +117,8 @@ def run_worker(args: argparse.Namespace) -> int:
     signal.signal(signal.SIGTERM, on_signal)
     signal.signal(signal.SIGINT, on_signal)
     stop.wait()
+    if explainer is not None:
+        explainer.stop()
     clean = h.drain(cfg.drain_seconds)
     dep.engine.flush_message_log()
     dep.close()

@@ -1,0 +1,185 @@
+"""Anchor explainers and the explainer server (reference
+operator/controllers/seldondeployment_explainers.go:32-184, the alibi
+explainer image it deploys, and python/seldon_core/seldon_client.py:1223-1321).
+
+Oracles are models with a known decision rule: the anchor must consist of
+exactly the predicates that pin the rule, with precision >= the threshold."""
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.request
+
+import numpy as np
+import pytest
+
+import seldon_core_amd as sca
+from seldon_core_amd.client import SeldonClient
+from seldon_core_amd.explainers import AnchorImage, AnchorTabular, AnchorText
+from seldon_core_amd.explainers.anchor import kl_bernoulli, kl_lower, kl_upper
+from seldon_core_amd.explainers.server import Explainer, ExplainerServer, deployment_predictor, rest_predictor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_kl_bounds():
+    for p in (0.0, 0.3, 0.9, 1.0):
+        for level in (0.01, 0.1, 1.0):
+            lo, hi = kl_lower(p, level), kl_upper(p, level)
+            assert 0.0 <= lo <= p + 1e-12 and p - 1e-12 <= hi <= 1.0
+            if 0 < p < 1:
+                # the bound sits where KL(p||q) reaches the level (bisection tolerance)
+                assert kl_bernoulli(p, hi) == pytest.approx(level, rel=0.05) or hi == 1.0
+                assert kl_bernoulli(p, lo) == pytest.approx(level, rel=0.05) or lo == 0.0
+    assert kl_upper(0.5, 0.01) < kl_upper(0.5, 0.1)
+
+
+def _rule(A):
+    A = np.atleast_2d(A)
+    return ((A[:, 0] > 5) & (A[:, 2] < 3)).astype(int)
+
+
+def test_anchor_tabular_recovers_rule():
+    rng = np.random.default_rng(0)
+    X = rng.uniform(0, 10, (3000, 5))
+    ex = AnchorTabular(_rule, ["a", "b", "c", "d", "e"]).fit(X)
+    e = ex.explain(np.array([8.0, 1.0, 1.0, 4.0, 4.0]))
+    assert sorted(n.split()[0] if not n[0].isdigit() else n.split()[2] for n in e["names"]) == ["a", "c"]
+    assert e["precision"] >= 0.95 and 0 < e["coverage"] < 0.2
+    assert e["raw"]["prediction"] == 1 and len(e["raw"]["precision"]) == 2
+    assert set(e["raw"]["examples"][0]) == {"covered", "covered_true", "covered_false"}
+    # negative instance: a <= 5 alone pins class 0
+    e0 = ex.explain(np.array([1.0, 1.0, 1.0, 4.0, 4.0]))
+    assert len(e0["names"]) == 1 and e0["names"][0].startswith("a <=")
+
+
+def test_anchor_tabular_categorical_names():
+    rng = np.random.default_rng(1)
+    X = np.column_stack([rng.integers(0, 3, 2000), rng.uniform(0, 1, 2000)]).astype(float)
+    f = lambda A: (np.atleast_2d(A)[:, 0] == 2).astype(int)  # noqa: E731
+    ex = AnchorTabular(f, ["Marital Status", "x"], {0: ["Married", "Separated", "Never-Married"]}).fit(X)
+    e = ex.explain(np.array([2.0, 0.4]))
+    assert e["names"] == ["Marital Status = Never-Married"] and e["precision"] == 1.0
+
+
+def test_anchor_text_trigger_word():
+    f = lambda texts: np.array([int("great" in t.split()) for t in texts])  # noqa: E731
+    e = AnchorText(f).explain("this film has great actors")
+    assert e["names"] == ["great"] and e["precision"] == 1.0
+    assert 0.3 < e["coverage"] < 0.7  # P(word kept) = 1 - sample_proba
+
+
+def test_anchor_image_segments():
+    rng = np.random.default_rng(0)
+    img = rng.uniform(0, 1, (16, 16, 3))
+    img[:8, :8] = (np.indices((8, 8)).sum(0) % 2 * 10)[:, :, None]  # textured top-left quadrant
+    f = lambda B: (B.reshape(len(B), 16, 16, 3)[:, :8, :8].std(axis=(1, 2, 3)) > 4.5).astype(int)  # noqa: E731
+    e = AnchorImage(f, (16, 16, 3), segmentation_kwargs={"n_segments": 16, "compactness": 200}).explain(img)
+    seg = np.array(e["segments"])
+    assert e["precision"] >= 0.95 and len(e["names"]) >= 1
+    for s in e["names"]:  # every anchored superpixel overlaps the textured quadrant
+        assert (seg[:8, :8] == s).any()
+    anchor = np.array(e["anchor"])
+    assert anchor.shape == img.shape and np.all(anchor[seg != e["names"][0]][..., 0] >= 0)
+
+
+def _mean_spec(explainer=None):
+    pred = {"name": "p", "graph": {"name": "clf", "type": "MODEL", "implementation": "MEAN_CLASSIFIER",
+                                   "parameters": [{"name": "threshold", "value": "6", "type": "FLOAT"}],
+                                   "children": []},
+            "componentSpecs": [{"spec": {"containers": []}}]}
+    if explainer:
+        pred["explainer"] = explainer
+    return {"apiVersion": "machinelearning.seldon.io/v1alpha2", "kind": "SeldonDeployment",
+            "metadata": {"name": "meanc"}, "spec": {"name": "meanc", "predictors": [pred]}}
+
+
+def test_explainer_server_over_engine(tmp_path):
+    rng = np.random.default_rng(2)
+    train = rng.uniform(0, 10, (2000, 3))
+    np.save(tmp_path / "train.npy", train)
+    dep = sca.Deployment(_mean_spec(), device=-1)
+    h = dep.serve(http_port=0, grpc_port=None, threads=2, host="127.0.0.1")
+    srv = None
+    try:
+        # labels through the REST front end (seldon.http protocol)
+        ex = Explainer("anchor_tabular", rest_predictor(f"127.0.0.1:{h.http_port}"),
+                       {"feature_names": "x0,x1,x2", "threshold": "0.95"}, storage_uri=str(tmp_path))
+        srv = ExplainerServer(ex, "meanc", "127.0.0.1", 0).start()
+        sc = SeldonClient(gateway="ambassador", transport="rest", gateway_endpoint=f"127.0.0.1:{srv.port}",
+                          deployment_name="meanc", namespace="seldon", payload_type="ndarray")
+        x = np.array([[9.5, 9.0, 9.2]])
+        out = sc.explain(data=x)
+        assert out["precision"] >= 0.9 and out["names"] and out["meta"]["name"] == "AnchorTabular"
+        # every predicate bounds a feature from below near the top of its range
+        assert all(">" in n for n in out["names"])
+        # in-process predictor + the kfserving-style path
+        ex2 = Explainer("anchor_tabular", deployment_predictor(dep), {"training_data": str(tmp_path / "train.npy")})
+        srv2 = ExplainerServer(ex2, "meanc", "127.0.0.1", 0).start()
+        try:
+            req = urllib.request.Request(f"http://127.0.0.1:{srv2.port}/v1/models/meanc:explain",
+                                         data=json.dumps({"instances": [[0.5, 0.2, 0.1]]}).encode(),
+                                         headers={"Content-Type": "application/json"})
+            out2 = json.loads(urllib.request.urlopen(req, timeout=60).read())
+            assert out2["raw"]["prediction"] == 0 and out2["precision"] >= 0.9
+        finally:
+            srv2.stop()
+        bad = SeldonClient(gateway="ambassador", transport="rest", gateway_endpoint=f"127.0.0.1:{srv.port}",
+                           deployment_name="other", namespace=None).explain(data=x)
+        assert bad == {"success": False, "response_code": 404}
+    finally:
+        if srv:
+            srv.stop()
+        dep.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_serve_starts_explainer_from_spec(tmp_path):
+    rng = np.random.default_rng(3)
+    np.save(tmp_path / "train.npy", rng.uniform(0, 10, (1000, 3)))
+    spec = _mean_spec({"type": "anchor_tabular", "modelUri": f"file://{tmp_path}",
+                       "config": {"feature_names": "a,b,c", "batch_size": "200"}})
+    (tmp_path / "sdep.json").write_text(json.dumps(spec))
+    hp, gp, ep = _free_port(), _free_port(), _free_port()
+    p = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--spec", str(tmp_path / "sdep.json"),
+                          "--device", "-1", "--http-port", str(hp), "--grpc-port", str(gp), "--admin-port", "0",
+                          "--explainer-port", str(ep), "--threads", "1", "--log-level", "WARNING"],
+                         env=dict(os.environ, PYTHONPATH=ROOT), cwd=ROOT, start_new_session=True)
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            try:
+                if urllib.request.urlopen(f"http://127.0.0.1:{ep}/health", timeout=1).status == 200:
+                    break
+            except Exception:
+                time.sleep(0.2)
+        sc = SeldonClient(gateway="ambassador", transport="rest", gateway_endpoint=f"127.0.0.1:{ep}",
+                          deployment_name="meanc", payload_type="ndarray")
+        out = sc.explain(data=np.array([[9.0, 9.5, 9.9]]))
+        assert out["names"] and out["precision"] >= 0.9
+        assert all(n[0] in "abc" or n.split()[2] in "abc" for n in out["names"])
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 0
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+
+
+def test_explainer_cli_rejects_bad_config():
+    from seldon_core_amd.explainers.server import main
+
+    with pytest.raises(SystemExit):
+        main(["--model_name", "m", "--predictor_host", "h:1", "anchor_tabular", "notakey"])
+    with pytest.raises(ValueError, match="training_data"):
+        main(["--model_name", "m", "--predictor_host", "h:1", "anchor_tabular", "--feature_names=a"])

@@ -67,6 +67,24 @@ def test_tree_perfect_vs_cpu(C_, rows):
         unit.stop()
 
 
+@pytest.mark.parametrize("trees,depth,F,rows", [(50, 11, 10, 37), (100, 6, 300, 70), (64, 10, 20, 5),
+                                               (64, 10, 20, 900), (300, 3, 8, 2000)])
+def test_tree_geometries(C_, trees, depth, F, rows):
+    """LDS-staged trees (depth <= 10), global-memory trees (depth 11), wide
+    features without an LDS tile, fused and two-pass reduces."""
+    from seldon_core_amd.models import synthetic_xgboost, to_row_model
+
+    ens = synthetic_xgboost(trees, depth, F, seed=depth * 7 + F)
+    unit = C_.BatchedUnit(to_row_model(ens), 0, max_batch=4096)
+    try:
+        X = np.random.default_rng(rows).standard_normal((rows, F))
+        X[::7, 1] = np.nan
+        np.testing.assert_allclose(np.asarray(unit.run(X)).reshape(-1), ens.predict(X).reshape(-1),
+                                   rtol=2e-5, atol=2e-5)
+    finally:
+        unit.stop()
+
+
 def test_tree_fused_reduce_many_batches(C_):
     """Fused last-workgroup reduce: many back-to-back launches of varying
     size from concurrent callers (several slots, one counter each) must all
