@@ -542,7 +542,7 @@ PYBIND11_MODULE(_C, m) {
              Outcome o = wait_outcome([&](Done k) { e.call_node(node, method, std::move(in), std::move(k)); });
              return render(o);
            })
-      .def("metrics_text", [](Engine& e) { return e.metrics().render(); })
+      .def("metrics_text", [](Engine& e) { py::gil_scoped_release r; return e.render_metrics(); })
       .def("new_puid", &Engine::new_puid);
 
   py::class_<HttpServer, std::shared_ptr<HttpServer>>(m, "HttpServer")

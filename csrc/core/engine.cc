@@ -2,6 +2,7 @@
 
 #include "msglog.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <random>
@@ -800,6 +801,25 @@ void Engine::call_node(const std::string& name, int method, std::vector<MsgPtr> 
       case Method::SEND_FEEDBACK: kk(Outcome::fail(make_error(ApiError::EXECUTION_FAILURE, "use send_feedback"))); break;
     }
   });
+}
+
+std::string Engine::render_metrics() {
+  std::vector<const Engine*> engines{this};
+  for (auto& [e, w] : routes_) {
+    (void)w;
+    if (e != this) engines.push_back(e);
+  }
+  for (Engine* e : shadows_) engines.push_back(e);
+  std::vector<const Unit*> seen;
+  for (const Engine* e : engines) {
+    for (const auto& n : e->nodes_) {
+      const Unit* u = n->unit.get();
+      if (!u || std::find(seen.begin(), seen.end(), u) != seen.end()) continue;
+      seen.push_back(u);
+      u->collect_metrics(metrics_, n->model_labels);
+    }
+  }
+  return metrics_.render();
 }
 
 }  // namespace sca

@@ -110,6 +110,9 @@ class Unit {
   // Snapshot / restore of online state (routers, detectors); "" = stateless.
   virtual std::string snapshot() const { return ""; }
   virtual void restore(const std::string&) {}
+  // Scrape-time export of unit-internal statistics (GPU batchers) into the
+  // registry, labelled with the owning node's model labels.
+  virtual void collect_metrics(MetricsRegistry& m, const Labels& labels) const { (void)m; (void)labels; }
 };
 using UnitPtr = std::shared_ptr<Unit>;
 
@@ -165,6 +168,9 @@ class Engine {
 
   const PredictorSpecC& spec() const { return spec_; }
   MetricsRegistry& metrics() { return metrics_; }
+  // Prometheus text: unit collectors of this engine and its traffic peers /
+  // shadows run first, then the (shared) registry renders.
+  std::string render_metrics();
   std::shared_ptr<MetricsRegistry> metrics_ptr() const { return metrics_owner_; }
 
   // Split traffic between this predictor and sibling predictors by integer

@@ -403,6 +403,19 @@ BatcherStats BatchedUnit::stats() const {
   return stats_;
 }
 
+void BatchedUnit::collect_metrics(MetricsRegistry& m, const Labels& labels) const {
+  const BatcherStats st = stats();
+  Labels l = labels;
+  l.emplace_back("device", std::to_string(opts_.device));
+  m.counter("seldon_gpu_batches", l)->set(double(st.batches));
+  m.counter("seldon_gpu_rows", l)->set(double(st.rows));
+  m.counter("seldon_gpu_requests", l)->set(double(st.requests));
+  m.counter("seldon_gpu_busy_seconds", l)->set(st.gpu_busy_s);
+  m.gauge("seldon_gpu_max_batch_rows", l)->set(double(st.max_rows));
+  m.gauge("seldon_gpu_inflight_rows", l)->set(double(inflight_rows()));
+  m.gauge("seldon_gpu_slots", l)->set(double(opts_.slots));
+}
+
 void BatchedUnit::reset_stats() {
   std::lock_guard<std::mutex> g(stats_mu_);
   stats_ = BatcherStats();

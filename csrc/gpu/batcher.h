@@ -69,6 +69,7 @@ class BatchedUnit : public Unit {
 
   BatcherStats stats() const;
   void reset_stats();
+  void collect_metrics(MetricsRegistry& m, const Labels& labels) const override;
   const BatcherOptions& options() const { return opts_; }
   RowModelPtr model() const { return model_; }
   // Rows queued or on the device (replica load balancing).

@@ -29,6 +29,13 @@ class ReplicaUnit : public Unit {
   const std::vector<std::shared_ptr<BatchedUnit>>& replicas() const { return reps_; }
   std::vector<uint64_t> requests_per_replica() const;
   void stop();
+  void collect_metrics(MetricsRegistry& m, const Labels& labels) const override {
+    for (size_t i = 0; i < reps_.size(); ++i) {
+      Labels l = labels;
+      l.emplace_back("replica", std::to_string(i));
+      reps_[i]->collect_metrics(m, l);
+    }
+  }
 
  private:
   BatchedUnit* pick();

@@ -477,7 +477,7 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
     if (p == "/pause") { srv->paused_.store(true); respond_now(c, 200, "text/plain", "paused", rq.keep_alive); return; }
     if (p == "/unpause") { srv->paused_.store(false); respond_now(c, 200, "text/plain", "unpaused", rq.keep_alive); return; }
     if (p == "/prometheus" || p == "/metrics") {
-      std::string body = eng.metrics().render();
+      std::string body = eng.render_metrics();
       respond_now(c, 200, "text/plain; version=0.0.4", body, rq.keep_alive);
       return;
     }
