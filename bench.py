@@ -261,7 +261,9 @@ def main() -> None:
             "value": round(value, 2), "unit": "predictions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / base, 3), "dtype": "fp64",
-            "data": "synthetic (locust-shaped JSON payload, iris feature row); model fit on sklearn's bundled iris",
+            "data": ("synthetic (locust-shaped JSON payload, iris feature row); model fit on sklearn's bundled iris"
+                     if args.model == "iris" else
+                     f"synthetic (locust-shaped JSON payload, {len(row)}-feature random row); random-init model"),
             "p50_ms": round(max(r["p50"] for r in results), 4), "p99_ms": round(max(r["p99"] for r in results), 4),
             "baseline": {"rest_rps": REST_BASELINE, "rest_p50_ms": 4, "rest_p99_ms": 69, "grpc_rps": GRPC_BASELINE,
                          "grpc_p50_ms": 1, "grpc_p99_ms": 6},

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 
 #include "kernels.h"
 
@@ -56,13 +57,51 @@ __device__ __forceinline__ int descend_any(const TreeNode* __restrict__ tn, cons
 }
 
 // Stage the RB x F feature tile (fp64 -> fp32) into LDS; rows past `rows`
-// are zero-filled so every thread can traverse unconditionally.
+// are zero-filled so every thread can traverse unconditionally.  Loads are
+// issued kU at a time into registers before any LDS write, so the tile costs
+// one memory round trip, not one per loop trip.
 __device__ __forceinline__ void stage_tile(float* tile, const double* __restrict__ X, int row0, int rows, int RB,
                                            int F) {
-  const int n = RB * F;
-  for (int i = threadIdx.x; i < n; i += kBlock) {
-    const int r = row0 + i / F;
-    tile[i] = r < rows ? float(X[size_t(row0) * F + i]) : 0.f;
+  constexpr int kU = 8;
+  const int n = RB * F, valid = (rows - row0) * F;  // elements of real rows
+  for (int i0 = threadIdx.x; i0 < n; i0 += kBlock * kU) {
+    double v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {  // branch-free: clamped address, select after the load
+      const int i = i0 + u * kBlock;
+      const double x = X[size_t(row0) * F + min(i, valid - 1)];
+      v[u] = i < valid ? x : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * kBlock;
+      if (i < n) tile[i] = float(v[u]);
+    }
+  }
+}
+
+// Contiguous global -> LDS copy with gfx950 direct-to-LDS loads
+// (global_load_lds_dwordx4: each lane's 16 B land at M0 + lane * 16, no VGPR
+// round trip, all loads in flight at once).  Falls back to dword granules when
+// the source or size is not 16 B aligned.  Caller waits (vmcnt) + barriers.
+__device__ __forceinline__ void copy_to_lds(void* lds_dst, const void* gsrc, int bytes) {
+  typedef __attribute__((address_space(1))) const void* gptr;
+  typedef __attribute__((address_space(3))) void* lptr;
+  const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63, stride = kBlock;
+  char* dst = static_cast<char*>(lds_dst);
+  const char* src = static_cast<const char*>(gsrc);
+  if (((reinterpret_cast<uintptr_t>(gsrc) | uintptr_t(bytes)) & 15) == 0) {
+    const int n = bytes >> 4;
+    for (int base = wave * 64; base < n; base += stride)
+      if (base + lane < n)
+        __builtin_amdgcn_global_load_lds((gptr)(src + size_t(base + lane) * 16), (lptr)(dst + size_t(base) * 16), 16,
+                                         0, 0);
+  } else {
+    const int n = bytes >> 2;
+    for (int base = wave * 64; base < n; base += stride)
+      if (base + lane < n)
+        __builtin_amdgcn_global_load_lds((gptr)(src + size_t(base + lane) * 4), (lptr)(dst + size_t(base) * 4), 4, 0,
+                                         0);
   }
 }
 
@@ -201,27 +240,20 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
   const int tile_floats = stage_lds ? ((RB * F + 3) & ~3) : 0;
   const int n_internal = (1 << depth) - 1;
   TreeNode* s_nodes = reinterpret_cast<TreeNode*>(lds + kBlock + tile_floats);  // [lds_trees][n_internal]
-  float* s_leaves = reinterpret_cast<float*>(s_nodes + size_t(lds_trees) * n_internal);
+  float* s_leaves = reinterpret_cast<float*>(reinterpret_cast<char*>(s_nodes) +
+                                            ((size_t(lds_trees) * n_internal * sizeof(TreeNode) + 15) & ~size_t(15)));
   const int row0 = blockIdx.x * RB;
   const int chunk = blockIdx.y;
   const int r_local = threadIdx.x & (RB - 1);
   const int slot = threadIdx.x / RB;
   const int tpr = kBlock / RB;
   const int t0 = chunk_begin[chunk], t1 = chunk_begin[chunk + 1];
-  if (stage_lds) stage_tile(tile, X, row0, rows, RB, F);
-  if constexpr (TREES_LDS) {
-    const int nn = (t1 - t0) * n_internal, nl = (t1 - t0) * (n_internal + 1);
-    const uint2* gn = reinterpret_cast<const uint2*>(nodes + size_t(t0) * n_internal);
-    uint2* sn = reinterpret_cast<uint2*>(s_nodes);
-    for (int i = threadIdx.x; i < nn; i += kBlock) sn[i] = gn[i];
-    const float4* gl = reinterpret_cast<const float4*>(leaves + size_t(t0) * (n_internal + 1));  // 2^D floats/tree
-    float4* sl = reinterpret_cast<float4*>(s_leaves);
-    if ((nl & 3) == 0 && (n_internal + 1) % 4 == 0) {
-      for (int i = threadIdx.x; i < nl / 4; i += kBlock) sl[i] = gl[i];
-    } else {
-      for (int i = threadIdx.x; i < nl; i += kBlock) s_leaves[i] = leaves[size_t(t0) * (n_internal + 1) + i];
-    }
+  if constexpr (TREES_LDS) {  // issued first: in flight while the feature tile loads
+    copy_to_lds(s_nodes, nodes + size_t(t0) * n_internal, (t1 - t0) * n_internal * int(sizeof(TreeNode)));
+    copy_to_lds(s_leaves, leaves + size_t(t0) * (n_internal + 1), (t1 - t0) * (n_internal + 1) * int(sizeof(float)));
   }
+  if (stage_lds) stage_tile(tile, X, row0, rows, RB, F);
+  if constexpr (TREES_LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (stage_lds || TREES_LDS) __syncthreads();
   const float* xs = stage_lds ? tile + r_local * F : nullptr;
   float acc = 0.f;
@@ -334,6 +366,7 @@ constexpr int kMaxTreeLdsDepth = 10;
 constexpr int kMaxLdsBytes = 64 * 1024;
 
 int tree_bytes(int depth) { return ((1 << depth) - 1) * int(sizeof(TreeNode)) + (1 << depth) * int(sizeof(float)); }
+constexpr int kTreeLdsPad = 16;  // leaves slab rounded up to 16 B
 
 template <bool FUSED>
 void launch_perfect(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
@@ -342,8 +375,8 @@ void launch_perfect(const double* X, int rows, int F, const TreeNode* nodes, con
   bool stage;
   int lds = lds_bytes_for(RB, F, &stage);
   if (stage) lds = int((kBlock + ((RB * F + 3) & ~3)) * sizeof(float));
-  if (depth > kMaxTreeLdsDepth || lds + lds_trees * tree_bytes(depth) > kMaxLdsBytes) lds_trees = 0;
-  lds += lds_trees * tree_bytes(depth);
+  if (depth > kMaxTreeLdsDepth || lds + lds_trees * tree_bytes(depth) + kTreeLdsPad > kMaxLdsBytes) lds_trees = 0;
+  if (lds_trees) lds += lds_trees * tree_bytes(depth) + kTreeLdsPad;
   dim3 grid((rows + RB - 1) / RB, n_chunks);
 #define SCA_TREE_LAUNCH(DD, TL)                                                                                  \
   hipLaunchKernelGGL((perfect_partial<DD, FUSED, TL>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves,   \
@@ -390,7 +423,7 @@ int tree_lds_max_trees(int depth, int rows_per_block, int F) {
   bool stage;
   int lds = lds_bytes_for(rows_per_block, F, &stage);
   if (stage) lds = int((kBlock + ((rows_per_block * F + 3) & ~3)) * sizeof(float));
-  return std::max(0, (kMaxLdsBytes - lds) / tree_bytes(depth));
+  return std::max(0, (kMaxLdsBytes - lds - kTreeLdsPad) / tree_bytes(depth));
 }
 
 void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
