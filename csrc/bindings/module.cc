@@ -257,7 +257,9 @@ PYBIND11_MODULE(_C, m) {
             for (size_t i = 0; i < thr.size(); ++i) s.nodes[i] = kern::SparseNode{thr[i], feat[i], left[i], right[i]};
             s.tree_root = d["tree_root"].cast<std::vector<int>>();
           }
-          return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::TreeEnsembleModel>(std::move(s)));
+          auto tm = std::make_shared<gpu::TreeEnsembleModel>(std::move(s));
+          if (d.contains("fused_reduce")) tm->set_fused_reduce(d["fused_reduce"].cast<bool>());
+          return std::static_pointer_cast<gpu::RowModel>(tm);
         });
 
   py::class_<Unit, std::shared_ptr<Unit>>(m, "Unit")
@@ -601,11 +603,24 @@ PYBIND11_MODULE(_C, m) {
   });
   k.def("tree_perfect_partial", [](uintptr_t X, int rows, int F, uintptr_t nodes, uintptr_t leaves, int depth,
                                    int cmp_le, uintptr_t chunk_begin, int n_chunks, int rb, uintptr_t partial,
-                                   uintptr_t s) {
+                                   uintptr_t s, int lds_trees) {
     kern::tree_perfect_partial(P<const double>(X), rows, F, P<const kern::TreeNode>(nodes), P<const float>(leaves),
                                depth, cmp_le, P<const int>(chunk_begin), n_chunks, rb, P<float>(partial),
-                               as_stream(s));
+                               as_stream(s), lds_trees);
+  }, py::arg("X"), py::arg("rows"), py::arg("F"), py::arg("nodes"), py::arg("leaves"), py::arg("depth"),
+     py::arg("cmp_le"), py::arg("chunk_begin"), py::arg("n_chunks"), py::arg("rb"), py::arg("partial"), py::arg("s"),
+     py::arg("lds_trees") = 0);
+  k.def("tree_perfect_fused", [](uintptr_t X, int rows, int F, uintptr_t nodes, uintptr_t leaves, int depth,
+                                 int cmp_le, uintptr_t chunk_begin, int n_chunks, int rb, uintptr_t partial,
+                                 uintptr_t counter, uintptr_t chunk_group, int groups, uintptr_t base, float scale,
+                                 int transform, uintptr_t out, int out_cols, uintptr_t s, int lds_trees) {
+    const kern::TreeReduceArgs red{P<int>(counter), P<const int>(chunk_group), groups, P<const float>(base), scale,
+                                   transform, P<double>(out), out_cols};
+    kern::tree_perfect_fused(P<const double>(X), rows, F, P<const kern::TreeNode>(nodes), P<const float>(leaves),
+                             depth, cmp_le, P<const int>(chunk_begin), n_chunks, rb, P<float>(partial), red,
+                             as_stream(s), lds_trees);
   });
+  k.def("tree_lds_max_trees", &kern::tree_lds_max_trees);
   k.def("tree_reduce", [](uintptr_t partial, int rows, int n_chunks, uintptr_t chunk_group, int groups,
                           uintptr_t base, float scale, int transform, uintptr_t out, int out_cols, uintptr_t s) {
     kern::tree_reduce(P<const float>(partial), rows, n_chunks, P<const int>(chunk_group), groups, P<const float>(base),

@@ -239,7 +239,7 @@ bool BatchedUnit::launch(Slot* s) {
       // kernel reads each element once -- models that re-read X from many
       // workgroups (tree chunks) get one DMA into HBM first.
       const double* xin = s->h_in.dev<double>();
-      if (!zc_input_) {
+      if (!zc_input_ && !model_->zero_copy_input_for(rows, cols)) {
         err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
         xin = s->d_in.as<double>();
       }

@@ -62,7 +62,7 @@ void LinearModel::run_cpu(const double* X, int rows, int, double* out) const {
 }
 
 // ------------------------------------------------------------ tree ensemble
-static const int kPlanSizes[] = {1, 2, 4, 8, 16, 32, 64, 128, 256, 512};
+static const int kPlanSizes[] = {4, 8, 16, 32, 64, 128, 256, 512};
 
 TreeEnsembleModel::TreeEnsembleModel(TreeEnsembleSpec spec) : spec_(std::move(spec)) {
   const int T = spec_.n_trees;
@@ -136,37 +136,54 @@ void TreeEnsembleModel::to_device(int device) {
 static constexpr size_t kTreeWsHeader = 256;
 
 size_t TreeEnsembleModel::workspace_bytes(int max_rows, int) const {
-  return kTreeWsHeader + size_t(max_chunks_) * size_t(std::max(1, max_rows)) * sizeof(float);
+  // Largest slab any batch size up to max_rows plans for (chunks shrink as
+  // batches grow, so this is far below max_chunks x max_rows).
+  size_t slab = 0;
+  for (int r = 1; r <= std::max(1, max_rows); ++r) {
+    int rb, pi;
+    plan_for(r, &rb, &pi);
+    slab = std::max(slab, size_t(plans_[size_t(pi)]->n_chunks) * size_t(r));
+  }
+  return kTreeWsHeader + slab * sizeof(float);
 }
 
 void TreeEnsembleModel::plan_for(int rows, int* rows_per_block, int* plan_index, int* lds_trees) const {
+  // Measured on MI355X (profiles/r01g_tree_variants): a descent costs ~2 us of
+  // dependent L2 loads per tree a lane walks, and every extra tree chunk adds
+  // slab to fold.  So: few rows per block (more lanes per row = one tree per
+  // lane with few chunks), growing with the batch (rows / 16, 2..64), and
+  // trees per lane raised only once the grid passes ~2048 workgroups.
   int rb = 1;
-  while (rb < rows && rb < 64) rb <<= 1;
+  if (rows > 1) {
+    rb = 2;
+    while (rb * 2 <= rows / 16 && rb < 64) rb <<= 1;
+  }
   const int tpr = 256 / rb;
   const int row_tiles = (rows + rb - 1) / rb;
   *rows_per_block = rb;
+  // Trees are traversed from global memory (L2-resident across batches).
+  // Staging a chunk's trees in LDS (lds_trees) and folding the slab in the
+  // partial kernel's last workgroup (fused reduce) are kept as options but
+  // measured slower: per-batch time is dominated by per-kernel dispatch +
+  // completion and the descent chain, not by where the nodes are read from,
+  // and the in-kernel fold's cross-XCD write-through / atomic / reload chain
+  // costs more than a second launch.
   if (lds_trees) *lds_trees = 0;
-  // Perfect trees that fit: chunks as large as LDS allows (one staging round
-  // trip per workgroup amortised over every tree and row it holds).
-  const int cap = spec_.depth > 0 ? kern::tree_lds_max_trees(spec_.depth, rb, spec_.n_features) : 0;
-  if (cap >= 1) {
-    int idx = 0;
-    for (int i = 0; i < int(plans_.size()); ++i)
-      if (plans_[size_t(i)]->chunk_trees <= cap) idx = i;
-    *plan_index = idx;
-    if (lds_trees) *lds_trees = plans_[size_t(idx)]->chunk_trees;
-    return;
-  }
-  // Otherwise aim for ~4 workgroups per CU (256 CUs) while giving every
-  // thread of a workgroup >= 1 tree (chunk >= trees-per-row lanes): a tree
-  // traversal from L2 is a chain of dependent loads, so idle lanes buy no
-  // latency, only more slab.
-  const int want_chunks = std::max(1, 1024 / std::max(1, row_tiles));
-  const int chunk = std::max(tpr, (spec_.n_trees + want_chunks - 1) / want_chunks);
+  const long long want = (static_cast<long long>(spec_.n_trees) * row_tiles + 2047) / 2048;
+  const int chunk = static_cast<int>(std::max<long long>(tpr, want));
   int idx = int(plans_.size()) - 1;
   for (int i = 0; i < int(plans_.size()); ++i)
     if (plans_[size_t(i)]->chunk_trees >= chunk) { idx = i; break; }
   *plan_index = idx;
+}
+
+bool TreeEnsembleModel::zero_copy_input_for(int rows, int cols) const {
+  int rb, pi;
+  plan_for(rows, &rb, &pi);
+  // Every chunk's workgroups re-read their rows' tile: keep the host traffic of
+  // one batch within ~64 KB (one PCIe/IF round trip per workgroup is cheaper
+  // than a separate H2D blit launch below that).
+  return size_t(rows) * size_t(cols) * sizeof(double) * size_t(plans_[size_t(pi)]->n_chunks) <= (64u << 10);
 }
 
 void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) {
@@ -176,9 +193,10 @@ void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out,
   const Plan& p = *plans_[size_t(pi)];
   int* counter = static_cast<int*>(ws);
   float* partial = reinterpret_cast<float*>(static_cast<char*>(ws) + kTreeWsHeader);
-  // Small slabs: the partial kernel's last workgroup folds + transforms (one
-  // launch per batch); the tail does <= 16 slab loads per thread.
-  const bool fused = spec_.groups <= kern::kTreeFusedMaxGroups && size_t(rows) * p.n_chunks <= 4096;
+  // Small slabs may fold in the partial kernel's last workgroup (one launch
+  // per batch; the tail does <= 16 slab loads per thread) -- off by default,
+  // see plan_for.
+  const bool fused = fused_reduce_ && spec_.groups <= kern::kTreeFusedMaxGroups && size_t(rows) * p.n_chunks <= 4096;
   if (fused) {
     const kern::TreeReduceArgs red{counter, p.group.as<int>(), spec_.groups, d_base_.as<float>(), spec_.scale,
                                    spec_.transform, out, spec_.out_cols};

@@ -36,6 +36,10 @@ class RowModel {
   // False if many workgroups re-read X (stage it in HBM instead of reading
   // pinned host memory over PCIe from every workgroup).
   virtual bool zero_copy_input() const { return true; }
+  // Per-batch refinement: a model whose re-read factor depends on the batch
+  // geometry may still read small batches straight from pinned host memory
+  // (saves the H2D blit launch).
+  virtual bool zero_copy_input_for(int rows, int cols) const { (void)rows; (void)cols; return zero_copy_input(); }
   // Segment-aware models compute per request (not per row): the batcher passes
   // the request boundaries (nseg + 1 row offsets, device-visible).
   virtual bool segmented() const { return false; }
@@ -117,9 +121,14 @@ class TreeEnsembleModel : public RowModel {
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
   const TreeEnsembleSpec& spec() const { return spec_; }
   bool zero_copy_input() const override { return false; }  // every tree-chunk block stages the X tile
+  // Host reads = rows x cols x 8 B x chunks: zero-copy while that stays small.
+  bool zero_copy_input_for(int rows, int cols) const override;
   std::shared_ptr<RowModel> clone() const override { return with_meta(std::make_shared<TreeEnsembleModel>(spec_)); }
   // Launch geometry chosen for a batch (exposed for tests/benchmarks).
   void plan_for(int rows, int* rows_per_block, int* plan_index, int* lds_trees = nullptr) const;
+  // In-kernel last-workgroup slab fold for small batches (default off: slower
+  // than the two-pass reduce on MI355X, see plan_for).
+  void set_fused_reduce(bool on) { fused_reduce_ = on; }
 
  private:
   struct Plan {
@@ -134,6 +143,7 @@ class TreeEnsembleModel : public RowModel {
   DeviceBuffer d_nodes_, d_leaves_, d_sparse_, d_roots_, d_base_;
   int max_chunks_ = 1;
   int device_ = -1;
+  bool fused_reduce_ = false;
 };
 
 // ------------------------------------------------------------- elementwise

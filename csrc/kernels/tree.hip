@@ -106,18 +106,24 @@ __device__ __forceinline__ void copy_to_lds(void* lds_dst, const void* gsrc, int
 }
 
 // Reduce per-thread accumulators of the same row and write the slab row.
+// Lanes of one row sit RB apart inside a wave: a butterfly (shfl_xor over
+// offsets 32..RB) leaves each wave's per-row sums in lanes 0..RB-1, and the
+// four waves' sums are added from LDS -- O(log) steps instead of a serial
+// 256 / RB-long LDS walk by one lane (6 us at RB = 1).
 // COHERENT: the slab is read back inside the same launch by the fused tail on
 // another XCD, so rows are written with agent-scope (sc1, write-through past
 // this XCD's L2) stores -- no whole-L2 writeback/invalidate fences needed.
 template <bool COHERENT>
 __device__ __forceinline__ void reduce_write(float* red, float acc, int RB, int row0, int rows, int chunk,
                                              float* __restrict__ partial) {
-  red[threadIdx.x] = acc;
+  for (int off = 32; off >= RB; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  const int lane = int(threadIdx.x) & 63, wave = int(threadIdx.x) >> 6;
+  if (lane < RB) red[wave * RB + lane] = acc;
   __syncthreads();
-  const int tpr = kBlock / RB;
-  if (threadIdx.x < RB) {
+  if (int(threadIdx.x) < RB) {
     float s = 0.f;
-    for (int j = 0; j < tpr; ++j) s += red[j * RB + threadIdx.x];
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) s += red[w * RB + threadIdx.x];
     const int r = row0 + threadIdx.x;
     if (r < rows) {
       if constexpr (COHERENT)

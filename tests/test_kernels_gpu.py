@@ -94,7 +94,9 @@ def test_tree_fused_reduce_many_batches(C_):
     from seldon_core_amd.models import synthetic_xgboost, to_row_model
 
     ens = synthetic_xgboost(1000, 8, 32, seed=11)
-    unit = C_.BatchedUnit(to_row_model(ens), 0, max_batch=1024, slots=4)
+    d = ens.device_spec()
+    d["fused_reduce"] = True
+    unit = C_.BatchedUnit(C_.tree_model(d), 0, max_batch=1024, slots=4)
     rng = np.random.default_rng(5)
     Xs = [rng.standard_normal((n, 32)) for n in list(range(1, 41)) * 3 + [64, 128, 300]]
     try:
@@ -104,6 +106,32 @@ def test_tree_fused_reduce_many_batches(C_):
             np.testing.assert_allclose(np.asarray(got).reshape(-1), ens.predict(X).reshape(-1), rtol=2e-5, atol=2e-5)
     finally:
         unit.stop()
+
+
+def test_tree_lds_staging_matches_global(C_):
+    """Trees staged in LDS by global_load_lds (kernel option) == traversal from
+    global memory, for odd chunk starts (dword copy path) and 16-B aligned."""
+    D, F, T = 6, 12, 90
+    ni = (1 << D) - 1
+    g = torch.Generator().manual_seed(3)
+    nodes = torch.stack([torch.randn(T * ni, generator=g).view(torch.int32),
+                         torch.randint(0, F, (T * ni,), generator=g, dtype=torch.int32)], 1).contiguous().to(dev)
+    leaves = torch.randn(T * (ni + 1), generator=g).to(dev)
+    for rows in (1, 9, 100):
+        X = torch.randn(rows, F, dtype=torch.float64, generator=g).to(dev)
+        rb = min(64, 1 << (rows - 1).bit_length())
+        outs = []
+        for begin, lds in (([0, 7, 23, 40, 41, 64, 90], 32), ([0, 16, 32, 48, 64, 80, 90], 16),
+                           ([0, 7, 23, 40, 41, 64, 90], 0)):
+            b = torch.tensor(begin, dtype=torch.int32, device=dev)
+            nc = len(begin) - 1
+            part = torch.empty(nc * rows, dtype=torch.float32, device=dev)
+            C_.kernels.tree_perfect_partial(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0,
+                                            b.data_ptr(), nc, rb, part.data_ptr(), _stream(), lds)
+            torch.cuda.synchronize()
+            outs.append(part.view(nc, rows).double().sum(0))
+        torch.testing.assert_close(outs[0], outs[2], rtol=0, atol=0)
+        torch.testing.assert_close(outs[1], outs[2], rtol=1e-6, atol=1e-5)
 
 
 def test_tree_softmax_groups(C_):
