@@ -250,8 +250,11 @@ def main() -> None:
     handle.stop()
     dep.close()
     if rank == 0:
-        value = sum(r["rps"] for r in results)
-        ms_per_step = max(r["wall"] for r in results) / args.steps * 1000.0
+        # whole-job throughput: every rank's completed predictions over the
+        # slowest rank's timed window
+        wall_max = max(r["wall"] for r in results)
+        value = sum(r["ok"] for r in results) / wall_max
+        ms_per_step = wall_max / args.steps * 1000.0
         base = REST_BASELINE if args.api == "rest" else GRPC_BASELINE
         batch = next(iter(results[0]["batch"].values()), {}) if results[0]["batch"] else {}
         mean_rows = batch.get("rows", 0) / max(1, batch.get("batches", 1))

@@ -52,8 +52,12 @@ Outcome wait_outcome(const std::function<void(Done)>& start) {
 }
 
 gpu::BatcherOptions batcher_opts(int device, int max_batch, int max_wait_us, int slots, bool zero_copy,
-                                 size_t zero_copy_max_bytes, bool spin, bool cpu_batching = false) {
+                                 size_t zero_copy_max_bytes, bool spin, bool cpu_batching = false,
+                                 int fail_threshold = 3, int cooldown_ms = 2000, int hang_timeout_ms = 10000) {
   gpu::BatcherOptions o;
+  o.fail_threshold = fail_threshold;
+  o.cooldown_ms = cooldown_ms;
+  o.hang_timeout_ms = hang_timeout_ms;
   o.device = device;
   o.max_batch = max_batch;
   o.max_wait_us = max_wait_us;
@@ -269,13 +273,36 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<gpu::BatchedUnit, Unit, std::shared_ptr<gpu::BatchedUnit>>(m, "BatchedUnit")
       .def(py::init([](std::shared_ptr<gpu::RowModel> model, int device, int max_batch, int max_wait_us, int slots,
-                       bool zero_copy, size_t zc_bytes, bool spin, bool cpu_batching) {
+                       bool zero_copy, size_t zc_bytes, bool spin, bool cpu_batching, int fail_threshold,
+                       int cooldown_ms, int hang_timeout_ms) {
              return std::make_shared<gpu::BatchedUnit>(
-                 model, batcher_opts(device, max_batch, max_wait_us, slots, zero_copy, zc_bytes, spin, cpu_batching));
+                 model, batcher_opts(device, max_batch, max_wait_us, slots, zero_copy, zc_bytes, spin, cpu_batching,
+                                     fail_threshold, cooldown_ms, hang_timeout_ms));
            }),
            py::arg("model"), py::arg("device") = 0, py::arg("max_batch") = 1024, py::arg("max_wait_us") = 0,
            py::arg("slots") = 4, py::arg("zero_copy") = true, py::arg("zero_copy_max_bytes") = 256 << 10,
-           py::arg("spin_wait") = true, py::arg("cpu_batching") = false)
+           py::arg("spin_wait") = true, py::arg("cpu_batching") = false, py::arg("fail_threshold") = 3,
+           py::arg("cooldown_ms") = 2000, py::arg("hang_timeout_ms") = 10000)
+      .def("health", [](const gpu::BatchedUnit& u) {
+        const auto h = u.health();
+        py::dict d;
+        d["healthy"] = h.healthy;
+        d["consecutive_failures"] = h.consecutive_failures;
+        d["failed_batches"] = h.failed_batches;
+        d["hangs"] = h.hangs;
+        d["trips"] = h.trips;
+        d["injected"] = h.injected;
+        return d;
+      })
+      .def("inject_fault", [](gpu::BatchedUnit& u, int64_t fail_after, int64_t fail_count, int hang_ms) {
+             gpu::FaultSpec f;
+             f.fail_after = fail_after;
+             f.fail_count = fail_count;
+             f.hang_ms = hang_ms;
+             u.inject_fault(f);
+           },
+           py::arg("fail_after") = -1, py::arg("fail_count") = -1, py::arg("hang_ms") = 0)
+      .def_property_readonly("ready", &gpu::BatchedUnit::ready)
       .def("run", [](gpu::BatchedUnit& u, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
         if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
         const int rows = int(X.shape(0)), cols = int(X.shape(1));
@@ -307,10 +334,13 @@ PYBIND11_MODULE(_C, m) {
       });
 
   py::class_<gpu::ReplicaUnit, Unit, std::shared_ptr<gpu::ReplicaUnit>>(m, "ReplicaUnit")
-      .def(py::init([](std::vector<std::shared_ptr<gpu::BatchedUnit>> reps) {
-        return std::make_shared<gpu::ReplicaUnit>(std::move(reps));
-      }))
+      .def(py::init([](std::vector<std::shared_ptr<gpu::BatchedUnit>> reps, int max_retries) {
+             return std::make_shared<gpu::ReplicaUnit>(std::move(reps), max_retries);
+           }),
+           py::arg("replicas"), py::arg("max_retries") = 1)
       .def_property_readonly("replicas", &gpu::ReplicaUnit::replicas)
+      .def_property_readonly("ready", &gpu::ReplicaUnit::ready)
+      .def_property_readonly("retries", &gpu::ReplicaUnit::retries)
       .def("requests_per_replica", &gpu::ReplicaUnit::requests_per_replica)
       .def("stats", [](const gpu::ReplicaUnit& u) {
         py::dict d;

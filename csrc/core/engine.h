@@ -52,6 +52,10 @@ struct EngineError {
   std::string reason;
   std::string info;
   int http_status = 500;
+  // Set by device units for failures of the device itself (launch / execution
+  // error, hang, unhealthy replica), not of the request: a replica set may
+  // re-run the request on another GPU.
+  bool device_fault = false;
 };
 using ErrPtr = std::shared_ptr<const EngineError>;
 

@@ -165,7 +165,7 @@ bool TfTensor::to_dense(std::vector<int64_t>& shape, std::vector<double>& v, std
     v.resize(size_t(n));
     switch (dtype) {
       case DT_FLOAT: { if (!need(4)) return false; for (int64_t i = 0; i < n; ++i) { float f; memcpy(&f, p + 4 * i, 4); v[i] = f; } return true; }
-      case DT_DOUBLE: { if (!need(8)) return false; memcpy(v.data(), p, 8 * n); return true; }
+      case DT_DOUBLE: { if (!need(8)) return false; if (n > 0) memcpy(v.data(), p, 8 * n); return true; }
       case DT_INT32: { if (!need(4)) return false; for (int64_t i = 0; i < n; ++i) { int32_t x; memcpy(&x, p + 4 * i, 4); v[i] = x; } return true; }
       case DT_INT64: { if (!need(8)) return false; for (int64_t i = 0; i < n; ++i) { int64_t x; memcpy(&x, p + 8 * i, 8); v[i] = double(x); } return true; }
       case DT_INT16: { if (!need(2)) return false; for (int64_t i = 0; i < n; ++i) { int16_t x; memcpy(&x, p + 2 * i, 2); v[i] = x; } return true; }

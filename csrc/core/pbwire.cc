@@ -414,6 +414,7 @@ void read_packed_fixed(Reader& r, uint32_t wt, std::vector<T>& out) {
   if (wt == 2) {
     std::string_view b = r.bytes();
     size_t n = b.size() / sizeof(T);
+    if (n == 0) return;  // empty packed field (b.data() may be null)
     size_t old = out.size();
     out.resize(old + n);
     memcpy(out.data() + old, b.data(), n * sizeof(T));

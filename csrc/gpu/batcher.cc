@@ -20,9 +20,55 @@ int device_count() {
 
 bool available() { return device_count() > 0; }
 
+namespace {
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+std::vector<std::string> split(const std::string& s, char sep) {
+  std::vector<std::string> out;
+  size_t pos = 0;
+  while (true) {
+    const size_t end = s.find(sep, pos);
+    out.push_back(s.substr(pos, end == std::string::npos ? std::string::npos : end - pos));
+    if (end == std::string::npos) return out;
+    pos = end + 1;
+  }
+}
+
+}  // namespace
+
+FaultSpec fault_from_env(int device) {
+  FaultSpec f;
+  const char* env = std::getenv("SCA_FAULT");
+  if (!env || !*env) return f;
+  for (const auto& entry : split(env, ';')) {
+    const size_t c1 = entry.find(':');
+    const size_t c2 = c1 == std::string::npos ? c1 : entry.find(':', c1 + 1);
+    if (c2 == std::string::npos) continue;
+    const std::string kind = entry.substr(0, c1), dev = entry.substr(c1 + 1, c2 - c1 - 1);
+    if ((kind == "gpu") != (device >= 0) || (kind != "gpu" && kind != "cpu")) continue;
+    if (dev != "*" && (kind == "cpu" || std::atoi(dev.c_str()) != device)) continue;
+    for (const auto& kv : split(entry.substr(c2 + 1), ',')) {
+      const size_t eq = kv.find('=');
+      if (eq == std::string::npos) continue;
+      const std::string k = kv.substr(0, eq);
+      const long long v = std::atoll(kv.c_str() + eq + 1);
+      if (k == "fail_after") f.fail_after = v;
+      else if (k == "fail_count") f.fail_count = v;
+      else if (k == "hang_ms") f.hang_ms = int(v);
+    }
+  }
+  return f;
+}
+
 BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::move(model)), opts_(opts) {
   if (opts_.max_batch < 1) opts_.max_batch = 1;
   if (opts_.slots < 1) opts_.slots = 1;
+  if (opts_.fail_threshold < 1) opts_.fail_threshold = 1;
+  inject_fault(fault_from_env(opts_.device));
   device_io_ = model_->device_io_only();
   zc_input_ = model_->zero_copy_input();
   segmented_ = model_->segmented();
@@ -158,6 +204,12 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
   it.k = std::move(k);
   if (c.exec) it.exec = *c.exec;
   if (opts_.device < 0 && !cpu_) {
+    if (fault_armed_.load(std::memory_order_relaxed) && take_injected_failure()) {
+      note_failure();
+      it.k(Outcome::fail(device_error(ApiError::EXECUTION_FAILURE, "injected device fault (SCA_FAULT)")));
+      return;
+    }
+    note_success();
     const int oc = model_->out_cols(it.cols);
     std::vector<double> out(size_t(it.rows) * oc);
     model_->run_cpu(it.x.data(), it.rows, it.cols, out.data());
@@ -175,6 +227,10 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
     it.k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "GPU unit stopped")));
     return;
   }
+  if (abandoned_slots_.load(std::memory_order_relaxed) >= int(slots_.size())) {
+    it.k(Outcome::fail(device_error(ApiError::UNAVAILABLE, "every batch slot of this GPU is wedged")));
+    return;
+  }
   inflight_rows_.fetch_add(it.rows, std::memory_order_relaxed);
   bool wake;
   {
@@ -190,6 +246,14 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
 bool BatchedUnit::launch(Slot* s) {
   const int rows = s->rows, cols = s->cols;
   s->out_cols = model_->out_cols(cols);
+  if (fault_armed_.load(std::memory_order_relaxed) && take_injected_failure()) {
+    auto e = device_error(ApiError::EXECUTION_FAILURE, "injected device fault (SCA_FAULT)");
+    note_failure();
+    inflight_rows_.fetch_sub(rows, std::memory_order_relaxed);
+    for (auto& it : s->items) it.k(Outcome::fail(e));
+    s->items.clear();
+    return false;
+  }
   if (cpu_) {  // reference path, one call per request (segment semantics for per-request models)
     s->t_launch = std::chrono::steady_clock::now();
     try {
@@ -259,8 +323,9 @@ bool BatchedUnit::launch(Slot* s) {
   }
   s->t_launch = std::chrono::steady_clock::now();
   if (err == hipSuccess) return true;
-  auto e = make_error(ApiError::EXECUTION_FAILURE,
-                      "GPU launch failed: " + (launch_error.empty() ? std::string(hipGetErrorString(err)) : launch_error));
+  auto e = device_error(ApiError::EXECUTION_FAILURE,
+                        "GPU launch failed: " + (launch_error.empty() ? std::string(hipGetErrorString(err)) : launch_error));
+  note_failure();
   inflight_rows_.fetch_sub(rows, std::memory_order_relaxed);
   for (auto& it : s->items) it.k(Outcome::fail(e));
   s->items.clear();
@@ -269,14 +334,22 @@ bool BatchedUnit::launch(Slot* s) {
 
 void BatchedUnit::complete(Slot* s, hipError_t st) {
   const double busy = std::chrono::duration<double>(std::chrono::steady_clock::now() - s->t_launch).count();
+  if (s->abandoned) {  // the watchdog already answered these requests
+    s->abandoned = false;
+    abandoned_slots_.fetch_sub(1, std::memory_order_relaxed);
+    if (st != hipSuccess) note_failure();
+    return;
+  }
   inflight_rows_.fetch_sub(s->rows, std::memory_order_relaxed);
   std::vector<Item> items;
   items.swap(s->items);
   const size_t n_items = items.size();
   if (st != hipSuccess) {
-    auto e = make_error(ApiError::EXECUTION_FAILURE, std::string("GPU execution failed: ") + hipGetErrorString(st));
+    auto e = device_error(ApiError::EXECUTION_FAILURE, std::string("GPU execution failed: ") + hipGetErrorString(st));
+    note_failure();
     for (auto& it : items) it.k(Outcome::fail(e));
   } else {
+    note_success();
     // Copy each request's rows out of the slot (it is reused at once), then
     // hand the requests to their front-end threads, one task per thread.
     const int oc = s->out_cols;
@@ -368,18 +441,48 @@ void BatchedUnit::device_loop() {
     if (inflight.empty()) continue;
     // ---- reap finished batches
     bool progress = false;
+    const auto now = clk::now();
+    const int hang_ms = hang_ms_.load(std::memory_order_relaxed);
     for (size_t i = 0; i < inflight.size();) {
       Slot* s = inflight[i];
-      const hipError_t st = cpu_ ? hipSuccess : hipEventQuery(s->ev.get());
-      if (st == hipErrorNotReady) { ++i; continue; }
+      hipError_t st = cpu_ ? hipSuccess : hipEventQuery(s->ev.get());
+      if (st == hipSuccess && hang_ms > 0 && now - s->t_launch < std::chrono::milliseconds(hang_ms))
+        st = hipErrorNotReady;  // injected slow / hung device
+      if (st == hipErrorNotReady) {
+        if (opts_.hang_timeout_ms > 0 && !s->abandoned &&
+            now - s->t_launch > std::chrono::milliseconds(opts_.hang_timeout_ms))
+          abandon(s);
+        ++i;
+        continue;
+      }
       complete(s, st);
       inflight.erase(inflight.begin() + long(i));
       free_list.push_back(s);
       progress = true;
     }
     if (progress) { spins = 0; continue; }
+    if (abandoned_slots_.load(std::memory_order_relaxed) >= int(slots_.size())) {
+      // Wedged device: answer what is still queued instead of letting it wait.
+      std::deque<Item> rest;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        rest.swap(queue_);
+        queued_rows_ = 0;
+        queued_n_.store(0);
+      }
+      if (!rest.empty()) {
+        auto e = device_error(ApiError::UNAVAILABLE, "every batch slot of this GPU is wedged");
+        for (auto& it : rest) {
+          inflight_rows_.fetch_sub(it.rows, std::memory_order_relaxed);
+          it.k(Outcome::fail(e));
+        }
+      }
+    }
     if (!opts_.spin_wait && !cpu_) {  // low-CPU mode: block on the oldest batch
-      (void)hipEventSynchronize(inflight.front()->ev.get());
+      if (opts_.hang_timeout_ms > 0 || hang_ms > 0)
+        std::this_thread::sleep_for(std::chrono::microseconds(20));  // stay able to run the watchdog
+      else
+        (void)hipEventSynchronize(inflight.front()->ev.get());
       continue;
     }
     if (!free_list.empty() && queued_n_.load(std::memory_order_acquire) > 0) continue;  // new work: launch it
@@ -398,6 +501,76 @@ void BatchedUnit::device_loop() {
   for (Slot* s : inflight) complete(s, cpu_ ? hipSuccess : hipEventSynchronize(s->ev.get()));
 }
 
+ErrPtr BatchedUnit::device_error(ApiError kind, std::string info) {
+  auto e = std::make_shared<EngineError>(*make_error(kind, std::move(info)));
+  e->device_fault = true;
+  return e;
+}
+
+void BatchedUnit::note_failure() {
+  failed_batches_.fetch_add(1, std::memory_order_relaxed);
+  if (consec_fail_.fetch_add(1, std::memory_order_relaxed) + 1 >= opts_.fail_threshold) {
+    open_until_ns_.store(now_ns() + int64_t(opts_.cooldown_ms) * 1000000, std::memory_order_release);
+    trips_.fetch_add(1, std::memory_order_relaxed);
+  }
+}
+
+void BatchedUnit::note_success() {
+  if (consec_fail_.load(std::memory_order_relaxed) != 0) consec_fail_.store(0, std::memory_order_relaxed);
+}
+
+bool BatchedUnit::healthy() const {
+  const int64_t until = open_until_ns_.load(std::memory_order_acquire);
+  return until == 0 || now_ns() >= until;
+}
+
+void BatchedUnit::abandon(Slot* s) {
+  std::vector<Item> items;
+  items.swap(s->items);
+  inflight_rows_.fetch_sub(s->rows, std::memory_order_relaxed);
+  s->rows = 0;
+  s->abandoned = true;
+  abandoned_slots_.fetch_add(1, std::memory_order_relaxed);
+  hangs_.fetch_add(1, std::memory_order_relaxed);
+  // A hang trips the unit at once; the next failure after the cooldown re-trips it.
+  consec_fail_.store(std::max(consec_fail_.load(), opts_.fail_threshold - 1));
+  note_failure();
+  auto e = device_error(ApiError::DEADLINE_EXCEEDED, "GPU batch exceeded the hang watchdog (" +
+                                                         std::to_string(opts_.hang_timeout_ms) + " ms)");
+  for (auto& it : items) it.k(Outcome::fail(e));
+}
+
+bool BatchedUnit::take_injected_failure() {
+  std::lock_guard<std::mutex> g(fault_mu_);
+  if (fault_.fail_after < 0) return false;
+  ++fault_launches_;
+  if (fault_launches_ <= fault_.fail_after) return false;
+  if (fault_.fail_count >= 0 && fault_injected_ >= fault_.fail_count) return false;
+  ++fault_injected_;
+  return true;
+}
+
+void BatchedUnit::inject_fault(const FaultSpec& f) {
+  std::lock_guard<std::mutex> g(fault_mu_);
+  fault_ = f;
+  fault_launches_ = 0;
+  fault_injected_ = 0;
+  fault_armed_.store(f.fail_after >= 0, std::memory_order_relaxed);
+  hang_ms_.store(std::max(0, f.hang_ms), std::memory_order_relaxed);
+}
+
+UnitHealth BatchedUnit::health() const {
+  UnitHealth h;
+  h.healthy = healthy();
+  h.consecutive_failures = consec_fail_.load();
+  h.failed_batches = failed_batches_.load();
+  h.hangs = hangs_.load();
+  h.trips = trips_.load();
+  std::lock_guard<std::mutex> g(fault_mu_);
+  h.injected = uint64_t(fault_injected_);
+  return h;
+}
+
 BatcherStats BatchedUnit::stats() const {
   std::lock_guard<std::mutex> g(stats_mu_);
   return stats_;
@@ -414,6 +587,11 @@ void BatchedUnit::collect_metrics(MetricsRegistry& m, const Labels& labels) cons
   m.gauge("seldon_gpu_max_batch_rows", l)->set(double(st.max_rows));
   m.gauge("seldon_gpu_inflight_rows", l)->set(double(inflight_rows()));
   m.gauge("seldon_gpu_slots", l)->set(double(opts_.slots));
+  const UnitHealth h = health();
+  m.gauge("seldon_gpu_healthy", l)->set(h.healthy ? 1.0 : 0.0);
+  m.counter("seldon_gpu_failed_batches", l)->set(double(h.failed_batches));
+  m.counter("seldon_gpu_hangs", l)->set(double(h.hangs));
+  m.counter("seldon_gpu_unhealthy_trips", l)->set(double(h.trips));
 }
 
 void BatchedUnit::reset_stats() {

@@ -47,6 +47,39 @@ struct BatcherOptions {
   // device-thread / executor machinery instead of inline (tests, CPU serving
   // of heavier models).
   bool cpu_batching = false;
+  // Failure detection (the reference relies on k8s probes,
+  // seldondeployment_controller.go:518,521, and the engine's TCP readiness
+  // checker, SeldonGraphReadyChecker.java:45-118).  A unit whose batches fail
+  // `fail_threshold` times in a row, or whose oldest in-flight batch is older
+  // than `hang_timeout_ms` (the watchdog: its requests are answered with 210
+  // at once, the slot is parked until the device lets it go), is unhealthy for
+  // `cooldown_ms`: ready() is false and replica sets route around it.  After
+  // the cooldown it takes traffic again (half-open); one more failure re-trips.
+  int fail_threshold = 3;
+  int cooldown_ms = 2000;
+  int hang_timeout_ms = 10000;  // 0 = no watchdog
+};
+
+// Fault injection for tests and drills (SURVEY §5.3 "fault-injection hook").
+// Set per unit (inject_fault) or from the environment at construction:
+//   SCA_FAULT="gpu:1:fail_after=100,fail_count=5;cpu:*:hang_ms=50"
+// entries `<gpu|cpu>:<device|*>:key=value,...`.  Injected failures never
+// touch the device: the batch is failed before launch (fail_*), or its
+// completion is held on the host (hang_ms), so a drill cannot wedge a GPU.
+struct FaultSpec {
+  int64_t fail_after = -1;  // batches that run normally before injected failures begin (-1 = off)
+  int64_t fail_count = -1;  // injected failures before the unit recovers (-1 = forever)
+  int hang_ms = 0;          // hold each batch's completion this long (slow / hung device)
+};
+FaultSpec fault_from_env(int device);
+
+struct UnitHealth {
+  bool healthy = true;
+  int consecutive_failures = 0;
+  uint64_t failed_batches = 0;
+  uint64_t hangs = 0;
+  uint64_t trips = 0;
+  uint64_t injected = 0;
 };
 
 struct BatcherStats {
@@ -65,7 +98,11 @@ class BatchedUnit : public Unit {
   void transform_input(const CallCtx& c, MsgPtr in, Done k) override;
   void transform_output(const CallCtx& c, MsgPtr in, Done k) override { transform_input(c, std::move(in), std::move(k)); }
   std::string kind() const override { return "gpu:" + model_->name(); }
-  bool ready() const override { return running_.load(); }
+  bool ready() const override { return running_.load() && healthy(); }
+  // Circuit state (see BatcherOptions): false while a trip's cooldown runs.
+  bool healthy() const;
+  UnitHealth health() const;
+  void inject_fault(const FaultSpec& f);
 
   BatcherStats stats() const;
   void reset_stats();
@@ -107,6 +144,7 @@ class BatchedUnit : public Unit {
     int rows = 0;
     int cols = 0;
     int out_cols = 0;
+    bool abandoned = false;  // watchdog answered its requests; waiting for the device to finish
     std::chrono::steady_clock::time_point t_launch;
   };
 
@@ -114,6 +152,11 @@ class BatchedUnit : public Unit {
   void device_loop();
   bool launch(Slot* s);
   void complete(Slot* s, hipError_t st);
+  void abandon(Slot* s);
+  bool take_injected_failure();
+  void note_failure();
+  void note_success();
+  static ErrPtr device_error(ApiError kind, std::string info);
   static MsgPtr make_response(const RespInfo& info, const Item& it, const double* out, int out_cols);
 
   RowModelPtr model_;
@@ -134,6 +177,16 @@ class BatchedUnit : public Unit {
   std::thread device_th_;
   mutable std::mutex stats_mu_;
   BatcherStats stats_;
+  // health / fault injection
+  std::atomic<int> consec_fail_{0};
+  std::atomic<int64_t> open_until_ns_{0};  // steady_clock ns; unhealthy before this
+  std::atomic<uint64_t> failed_batches_{0}, hangs_{0}, trips_{0};
+  std::atomic<int> hang_ms_{0};             // injected completion delay (read by the device thread)
+  std::atomic<bool> fault_armed_{false};
+  std::atomic<int> abandoned_slots_{0};    // all of them = device wedged: fail fast
+  mutable std::mutex fault_mu_;
+  FaultSpec fault_;
+  int64_t fault_launches_ = 0, fault_injected_ = 0;
 };
 
 }  // namespace sca::gpu

@@ -7,6 +7,14 @@
 // the parameters in that GPU's HBM) and sends every request to the replica
 // with the fewest rows in flight -- join-shortest-queue, which keeps every
 // GPU's batches similarly sized instead of hashing connections.
+//
+// Failure handling ("drop a failed replica from the scheduler and
+// re-route"): replicas whose circuit is open (BatchedUnit::healthy) get no new
+// requests while a healthy one exists, and a request that fails with a device
+// fault (launch/execution error, hang watchdog) is re-run on another healthy
+// replica, up to `max_retries` times -- the in-process counterpart of the
+// engine's REST retries (InternalPredictionService.java:388-452) and
+// Ambassador's connect-failure retry (ambassador.go:84-87).
 #pragma once
 
 #include <atomic>
@@ -19,15 +27,17 @@ namespace sca::gpu {
 
 class ReplicaUnit : public Unit {
  public:
-  explicit ReplicaUnit(std::vector<std::shared_ptr<BatchedUnit>> replicas);
+  explicit ReplicaUnit(std::vector<std::shared_ptr<BatchedUnit>> replicas, int max_retries = 1);
 
-  void transform_input(const CallCtx& c, MsgPtr in, Done k) override { pick()->transform_input(c, std::move(in), std::move(k)); }
-  void transform_output(const CallCtx& c, MsgPtr in, Done k) override { pick()->transform_output(c, std::move(in), std::move(k)); }
+  void transform_input(const CallCtx& c, MsgPtr in, Done k) override { submit(c, std::move(in), std::move(k), 0, -1); }
+  void transform_output(const CallCtx& c, MsgPtr in, Done k) override { submit(c, std::move(in), std::move(k), 0, -1); }
   std::string kind() const override;
+  // Degraded but serving while any replica is healthy.
   bool ready() const override;
 
   const std::vector<std::shared_ptr<BatchedUnit>>& replicas() const { return reps_; }
   std::vector<uint64_t> requests_per_replica() const;
+  uint64_t retries() const { return retries_.load(); }
   void stop();
   void collect_metrics(MetricsRegistry& m, const Labels& labels) const override {
     for (size_t i = 0; i < reps_.size(); ++i) {
@@ -35,12 +45,16 @@ class ReplicaUnit : public Unit {
       l.emplace_back("replica", std::to_string(i));
       reps_[i]->collect_metrics(m, l);
     }
+    m.counter("seldon_replica_retries", labels)->set(double(retries()));
   }
 
  private:
-  BatchedUnit* pick();
+  int pick(int exclude);
+  void submit(const CallCtx& c, MsgPtr in, Done k, int attempt, int exclude);
   std::vector<std::shared_ptr<BatchedUnit>> reps_;
+  int max_retries_;
   std::atomic<uint32_t> rr_{0};
+  std::atomic<uint64_t> retries_{0};
   std::unique_ptr<std::atomic<uint64_t>[]> picked_;
 };
 

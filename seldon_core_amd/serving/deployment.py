@@ -38,7 +38,8 @@ logger = logging.getLogger(__name__)
 
 METHOD_IDS = {"TRANSFORM_INPUT": 0, "TRANSFORM_OUTPUT": 1, "ROUTE": 2, "AGGREGATE": 3, "SEND_FEEDBACK": 4,
               "PREDICT": 5}
-BATCHER_KEYS = ("max_batch", "max_wait_us", "slots", "zero_copy", "zero_copy_max_bytes", "spin_wait", "cpu_batching")
+BATCHER_KEYS = ("max_batch", "max_wait_us", "slots", "zero_copy", "zero_copy_max_bytes", "spin_wait", "cpu_batching",
+                "fail_threshold", "cooldown_ms", "hang_timeout_ms")
 
 
 def import_class(path: str):
@@ -160,7 +161,7 @@ class Deployment:
     def _batcher_opts(self, node: Dict) -> Dict[str, Any]:
         opts = dict(self.batcher_defaults)
         params = typed_parameters(node)
-        for k in BATCHER_KEYS:
+        for k in BATCHER_KEYS + ("max_retries",):
             if k in params:
                 opts[k] = params[k]
         return opts
@@ -188,13 +189,14 @@ class Deployment:
     def _make_unit(self, node: Dict, row_model, whole_graph: bool = False):
         devs = self.replica_devices(node)
         opts = self._batcher_opts(node)
+        retries = int(opts.pop("max_retries", 1))
         if len(devs) == 1:
             return self.C.BatchedUnit(row_model, devs[0], **opts)
         reps = []
         for i, d in enumerate(devs):
             rm = row_model.clone_on(d) if whole_graph else (row_model if i == 0 else row_model.clone())
             reps.append(self.C.BatchedUnit(rm, d, **opts))
-        return self.C.ReplicaUnit(reps)
+        return self.C.ReplicaUnit(reps, max_retries=retries)
 
     def _bind_batched(self, node: Dict, row_model) -> None:
         unit = self._make_unit(node, row_model)

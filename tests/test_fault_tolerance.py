@@ -1,0 +1,158 @@
+"""Failure detection, re-routing and fault injection.
+
+The reference leans on Kubernetes for this: TCP/HTTP probes
+(seldondeployment_controller.go:518,521; seldondeployment_engine.go:161-172),
+the engine's 5 s graph readiness checker (SeldonGraphReadyChecker.java:45-118)
+and REST retries on connect failures (InternalPredictionService.java:388-452).
+In-process, each GPU unit is a circuit breaker (consecutive failures or the
+hang watchdog trip it), replica sets route around tripped GPUs and re-run
+device-faulted requests elsewhere, and SCA_FAULT / inject_fault drive it all
+without touching a device.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import seldon_core_amd as sca
+from seldon_core_amd.models import iris_logistic_regression, to_row_model
+from seldon_core_amd.serving.errors import EngineError
+
+
+def _spec(node_extra):
+    g = {"name": "clf", "type": "MODEL", "children": []}
+    g.update(node_extra)
+    return {"name": "p", "graph": g, "componentSpecs": [{"spec": {"containers": []}}]}
+
+
+def _payload(X):
+    return {"data": {"ndarray": np.asarray(X).tolist()}}
+
+
+@pytest.mark.parametrize("cpu_batching", [False, True])
+def test_failed_replica_is_routed_around(cpu_batching):
+    lr = iris_logistic_regression()
+    dep = sca.Deployment(_spec({"devices": [-1, -1, -1]}), components={"clf": lr}, device=-1,
+                         batcher={"cpu_batching": cpu_batching, "cooldown_ms": 60000})
+    try:
+        rep = dep.batched["clf"]
+        bad = rep.replicas[0]
+        bad.inject_fault(fail_after=0)  # replica 0 fails every batch from now on
+        X = np.random.default_rng(0).normal(size=(3, 4))
+        for _ in range(40):  # every request still succeeds: device faults are re-run elsewhere
+            out = dep.predict(_payload(X))
+            np.testing.assert_allclose(out["data"]["ndarray"], lr.predict_proba(X), rtol=1e-12)
+        h = bad.health()
+        assert h["trips"] >= 1 and not h["healthy"] and h["injected"] >= 3
+        assert rep.retries == h["injected"]
+        # once tripped it gets no more traffic; the set stays ready (degraded)
+        before = rep.requests_per_replica()[0]
+        for _ in range(20):
+            dep.predict(_payload(X))
+        assert rep.requests_per_replica()[0] == before
+        assert dep.ready()
+        text = dep.metrics()
+        assert 'seldon_gpu_healthy{' in text and "seldon_replica_retries" in text
+        assert any(line.startswith("seldon_gpu_healthy{") and line.endswith(" 0.0") for line in text.splitlines())
+    finally:
+        dep.close()
+
+
+def test_single_unit_trips_then_recovers_half_open():
+    C = sca.native()
+    rm = to_row_model(iris_logistic_regression())
+    u = C.BatchedUnit(rm, -1, fail_threshold=2, cooldown_ms=150)
+    X = np.random.default_rng(1).normal(size=(2, 4))
+    ref = u.run(X)
+    u.inject_fault(fail_after=0, fail_count=2)
+    for _ in range(2):
+        with pytest.raises(RuntimeError, match="injected device fault"):
+            u.run(X)
+    assert not u.health()["healthy"] and not u.ready
+    time.sleep(0.2)  # cooldown over: half-open, the next batch probes the unit
+    assert u.ready
+    np.testing.assert_array_equal(u.run(X), ref)
+    h = u.health()
+    assert h["healthy"] and h["consecutive_failures"] == 0 and h["trips"] == 1
+    u.stop()
+
+
+def test_unready_unit_flips_engine_readiness():
+    lr = iris_logistic_regression()
+    dep = sca.Deployment(_spec({}), components={"clf": lr}, device=-1,
+                         batcher={"fail_threshold": 1, "cooldown_ms": 60000})
+    try:
+        assert dep.ready()
+        dep.batched["clf"].inject_fault(fail_after=0, fail_count=1)
+        with pytest.raises(EngineError) as ei:
+            dep.predict(_payload(np.ones((1, 4))))
+        assert ei.value.body["code"] == 206 and ei.value.body["status"] == "FAILURE"
+        assert not dep.ready()  # /ready goes false: a load balancer drains this engine
+    finally:
+        dep.close()
+
+
+def test_hang_watchdog_answers_requests_and_trips():
+    C = sca.native()
+    rm = to_row_model(iris_logistic_regression())
+    u = C.BatchedUnit(rm, -1, cpu_batching=True, slots=1, hang_timeout_ms=100, cooldown_ms=100)
+    X = np.ones((1, 4))
+    u.inject_fault(hang_ms=600)  # completions held on the host: a slow / hung device
+    t0 = time.perf_counter()
+    with pytest.raises(RuntimeError, match="hang watchdog"):
+        u.run(X)
+    assert time.perf_counter() - t0 < 0.5  # answered by the watchdog, not by the device
+    # the only slot is parked until the "device" lets go: new work fails fast
+    with pytest.raises(RuntimeError, match="wedged"):
+        u.run(X)
+    h = u.health()
+    assert h["hangs"] == 1 and h["trips"] >= 1
+    u.inject_fault()  # clear
+    time.sleep(0.7)
+    np.testing.assert_allclose(u.run(X), iris_logistic_regression().predict_proba(X), rtol=1e-12)
+    assert u.health()["healthy"]
+    u.stop()
+
+
+def test_sca_fault_env(monkeypatch):
+    monkeypatch.setenv("SCA_FAULT", "gpu:*:fail_after=0;cpu:*:fail_after=2,fail_count=1")
+    C = sca.native()
+    u = C.BatchedUnit(to_row_model(iris_logistic_regression()), -1)
+    X = np.ones((1, 4))
+    u.run(X)
+    u.run(X)
+    with pytest.raises(RuntimeError, match="injected"):
+        u.run(X)
+    u.run(X)  # fail_count=1: recovered
+    assert u.health()["injected"] == 1
+    u.stop()
+
+
+def test_fault_env_device_filter(monkeypatch):
+    monkeypatch.setenv("SCA_FAULT", "gpu:3:fail_after=0")
+    u = sca.native().BatchedUnit(to_row_model(iris_logistic_regression()), -1)
+    u.run(np.ones((1, 4)))  # a gpu:3 entry does not apply to the CPU unit
+    assert u.health()["injected"] == 0
+    u.stop()
+
+
+@pytest.mark.gpu
+def test_gpu_replica_failover():
+    import torch
+
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    lr = iris_logistic_regression()
+    dep = sca.Deployment(_spec({"devices": [0, 0]}), components={"clf": lr}, device=0,
+                         batcher={"cooldown_ms": 60000})
+    try:
+        rep = dep.batched["clf"]
+        rep.replicas[1].inject_fault(fail_after=0)
+        X = np.random.default_rng(2).normal(size=(5, 4))
+        for _ in range(30):
+            out = dep.predict(_payload(X))
+            np.testing.assert_allclose(out["data"]["ndarray"], lr.predict_proba(X), rtol=1e-12)
+        assert not rep.replicas[1].health()["healthy"] and rep.replicas[0].health()["healthy"]
+        assert rep.retries >= 1
+    finally:
+        dep.close()
