@@ -26,6 +26,7 @@ reference vae/OutlierVAE.py:29-116 and utils.py:106-142) is shared in
 """
 from __future__ import annotations
 
+import copy
 import json
 import logging
 import math
@@ -106,6 +107,20 @@ class _FeedbackMetrics:
     """Labels arrive through send_feedback; metrics lag one prediction."""
     roll_window = 100
     score_key = "score"
+    # Online state checkpointed by state_dict() (SURVEY §5.4; the reference
+    # pickles the whole detector into Redis, persistence.py:21-85).  Model
+    # weights and device handles are construction inputs, not state.
+    _STATE = ("_predictions", "_labels", "_scores", "metric", "label", "nb_outliers")
+
+    def state_dict(self) -> Dict[str, Any]:
+        keys: List[str] = []
+        for cls in type(self).__mro__:
+            keys += [k for k in cls.__dict__.get("_STATE", ()) if k not in keys]
+        return {k: copy.deepcopy(getattr(self, k)) for k in keys if hasattr(self, k)}
+
+    def load_state_dict(self, state: Dict[str, Any]) -> None:
+        for k, v in state.items():
+            setattr(self, k, copy.deepcopy(v))
 
     def _init_feedback(self):
         self._predictions: List[int] = []
@@ -172,6 +187,7 @@ class _FeedbackMetrics:
 
 class _Reservoir:
     """Reservoir sampling + scaling statistics (CoreVAE.py:59-77)."""
+    _STATE = ("batch", "N", "mu", "sigma", "xmin", "xmax")
 
     def _init_scaling(self, preprocess: Optional[Dict], reservoir_size: int, n_features: int):
         self.reservoir_size = reservoir_size
@@ -215,6 +231,7 @@ class _Reservoir:
 @register("MAHALANOBIS_OD")
 class OutlierMahalanobis(_FeedbackMetrics):
     score_key = "outlier_score"
+    _STATE = ("mean", "C", "n", "clip")
     _EPSILON = 1e-8
 
     def __init__(self, threshold=25, n_components=3, n_stdev=3, start_clip=50, max_n=-1, device=None,
@@ -310,6 +327,7 @@ class OutlierMahalanobis(_FeedbackMetrics):
 @register("ISOLATION_FOREST_OD")
 class OutlierIsolationForest(_FeedbackMetrics):
     score_key = "anomaly_score"
+    _STATE = ("N",)
 
     def __init__(self, threshold=0.0, model=None, model_name="if", load_path="./models/", train_data=None,
                  n_estimators=100, max_samples="auto", contamination="auto", random_state=0, device=None):

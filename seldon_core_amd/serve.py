@@ -55,6 +55,10 @@ def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
     ap.add_argument("--log-level", default=os.environ.get("SELDON_LOG_LEVEL", "INFO"))
     ap.add_argument("--explainer-port", type=int, default=None,
                     help="port of the predictor's explainer (default: explainer.endpoint.service_port or 9000)")
+    ap.add_argument("--persistence", nargs="?", default=0, const=1, type=int,
+                    help="checkpoint stateful nodes (routers, detectors) and restore them at start "
+                         "(SELDON_PERSISTENCE_BACKEND=file|redis)")
+    ap.add_argument("--push-frequency", type=float, default=None, help="seconds between checkpoints (default 60)")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -92,6 +96,9 @@ def run_worker(args: argparse.Namespace) -> int:
         comps[node] = cls
     dep = Deployment(sdep, components=comps, predictor=args.predictor, deployment_name=cfg.deployment_name,
                      device=args.device, fuse=False if args.no_fuse else None, config=cfg)
+    if args.persistence:
+        dep.restore_checkpoint()
+        dep.start_checkpointing(args.push_frequency)
     h = dep.serve(http_port=cfg.http_port, grpc_port=cfg.grpc_port, admin_port=cfg.admin_port,
                   threads=cfg.threads, grpc_threads=cfg.grpc_threads, host=cfg.host)
     rank = os.environ.get("SCA_WORKER_RANK", "0")
@@ -142,6 +149,7 @@ class Supervisor:
         env = dict(os.environ)
         env["HIP_VISIBLE_DEVICES"] = str(rank)
         env["SCA_WORKER_RANK"] = str(rank)
+        env["SCA_WORKERS"] = str(self.n)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         self.procs[rank] = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--worker", *self.argv],
                                             env=env)

@@ -400,6 +400,71 @@ class Deployment:
             out.update({f"{pn}/{k}": v for k, v in p.batcher_stats().items()})
         return out
 
+    # -------------------------------------------------------- checkpoint
+    # the reference snapshots a component's state (the pickled
+    # user object) into Redis every push_frequency seconds and restores it at
+    # start (python/seldon_core/persistence.py:21-85, microservice.py:227-230).
+    # Here every stateful node of the graph -- native bandit routers (JSON),
+    # Python components and outlier detectors (state_dict / pickle) --
+    # checkpoints under persistence_<deployment>_<predictor>_<node>[_w<rank>].
+    def checkpoint_key(self, node: str, worker: Optional[str] = None) -> str:
+        from ..utils.persistence import state_key
+
+        key = state_key(self.deployment_name, self.predictor.get("name", "0"), node)
+        worker = os.environ.get("SCA_WORKER_RANK") if worker is None else worker
+        world = int(os.environ.get("SCA_WORKERS", "1") or 1)
+        return f"{key}_w{worker}" if worker and world > 1 else key
+
+    def checkpoint(self, store=None) -> int:
+        """Write every stateful node's snapshot; returns how many were written."""
+        from ..utils.persistence import default_store
+
+        store = store or default_store()
+        n = 0
+        for node in self.engine.node_names():
+            try:
+                blob = self.engine.snapshot(node)
+                if blob:
+                    store.set(self.checkpoint_key(node), blob)
+                    n += 1
+            except Exception as e:  # one unpicklable component must not stop the others
+                logger.warning("checkpoint of node %s failed: %s", node, e)
+        return n
+
+    def restore_checkpoint(self, store=None) -> int:
+        """Restore nodes from their snapshots; returns how many were restored."""
+        from ..utils.persistence import default_store
+
+        store = store or default_store()
+        n = 0
+        for node in self.engine.node_names():
+            try:
+                blob = store.get(self.checkpoint_key(node))
+            except Exception as e:  # store unreachable: start fresh like the reference
+                logger.warning("checkpoint restore of %s failed: %s", node, e)
+                continue
+            if blob:
+                self.engine.restore(node, blob)
+                n += 1
+        if n:
+            logger.info("restored %d node state(s) of %s", n, self.deployment_name)
+        return n
+
+    def start_checkpointing(self, push_frequency: Optional[float] = None, store=None):
+        """Periodic checkpoints on a daemon thread; close() writes a last one."""
+        from ..utils.persistence import Persister, default_store
+
+        store = store or default_store()
+        self._ckpt_store = store
+
+        class _Pusher(Persister):
+            def push(inner) -> None:  # noqa: N805
+                self.checkpoint(store)
+
+        self._persister = _Pusher(lambda: b"", push_frequency, store, key="-")
+        self._persister.start()
+        return self._persister
+
     # ----------------------------------------------------------- serving
     def serve(self, http_port: int = 8000, grpc_port: Optional[int] = 5001, admin_port: Optional[int] = None,
               threads: int = 4, grpc_threads: Optional[int] = None, host: str = "0.0.0.0",
@@ -421,6 +486,10 @@ class Deployment:
         for s in self._servers:
             s.stop()
         self._servers = []
+        if getattr(self, "_persister", None) is not None:
+            self._persister.stop()
+            self.checkpoint(self._ckpt_store)  # final snapshot after the drain
+            self._persister = None
         for u in list(self.batched.values()) + list(self.native_units.values()):
             u.stop()
         for p in getattr(self, "peers", {}).values():

@@ -118,10 +118,10 @@ class Persister(threading.Thread):
         self.freq = float(push_frequency or DEFAULT_PUSH_FREQUENCY)
         self.store = store or default_store()
         self.key = key or state_key()
-        self._stop = threading.Event()
+        self._halt = threading.Event()
 
     def run(self) -> None:
-        while not self._stop.wait(self.freq):
+        while not self._halt.wait(self.freq):
             self.push()
 
     def push(self) -> None:
@@ -131,7 +131,7 @@ class Persister(threading.Thread):
             logger.warning("persistence push failed: %s", e)
 
     def stop(self) -> None:
-        self._stop.set()
+        self._halt.set()
 
 
 def persist(user_object: Any, push_frequency: Optional[float] = None, store=None, key: Optional[str] = None):
