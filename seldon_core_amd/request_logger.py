@@ -7,14 +7,22 @@ Receives the engine's CloudEvents ``seldon.message.pair`` POSTs
 (tabular / text / image), and prints one line per row to stdout for a log
 shipper (fluentd / Elasticsearch in the reference setup).
 
-    python -m seldon_core_amd.request_logger --port 8080
+With ``--kafka host:port --kafka-topic T`` every pair is also published as a
+``RequestResponse`` proto to the legacy prediction stream (the
+reference reader is kafka/tests/src/read_predictions.py), batched off the
+request thread by :class:`KafkaSink`.
+
+    python -m seldon_core_amd.request_logger --port 8080 [--kafka localhost:9093 --kafka-topic predictions]
 """
 from __future__ import annotations
 
 import argparse
 import json
+import logging
+import queue
 import sys
 import threading
+import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional, TextIO, Tuple
 
@@ -84,9 +92,78 @@ def flatten_pair(content: Dict) -> List[Dict]:
     return docs
 
 
+logger = logging.getLogger(__name__)
+
+
+def pair_to_proto(content: Dict) -> bytes:
+    """CloudEvents pair content -> serialized seldon.protos.RequestResponse."""
+    from google.protobuf import json_format
+
+    from .proto import prediction_pb2
+
+    m = prediction_pb2.RequestResponse()
+    for k in ("request", "response"):
+        if isinstance(content.get(k), dict):
+            json_format.ParseDict(content[k], getattr(m, k), ignore_unknown_fields=True)
+    return m.SerializeToString()
+
+
+class KafkaSink:
+    """Publishes pairs to a topic from one background thread.
+
+    Records queued while a produce is in flight go out together as one
+    RecordBatch (``linger_s`` bounds how long the first one waits)."""
+
+    def __init__(self, bootstrap: str, topic: str, linger_s: float = 0.02, max_batch: int = 500, producer=None):
+        from .utils.kafka import KafkaProducer
+
+        self.topic, self.linger_s, self.max_batch = topic, linger_s, max_batch
+        self.producer = producer or KafkaProducer(bootstrap, client_id="seldon-request-logger")
+        self.q: "queue.Queue" = queue.Queue()
+        self.sent = self.dropped = 0
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def publish(self, content: Dict) -> None:
+        puid = ((content.get("response") or {}).get("meta") or {}).get("puid") or content.get("id")
+        self.q.put(((puid or "").encode() or None, pair_to_proto(content)))
+
+    def _run(self) -> None:
+        while True:
+            first = self.q.get()
+            if first is None:
+                return
+            batch, stop = [first], False
+            deadline = time.monotonic() + self.linger_s
+            while len(batch) < self.max_batch:
+                try:
+                    item = self.q.get(timeout=max(0.0, deadline - time.monotonic()))
+                except queue.Empty:
+                    break
+                if item is None:
+                    stop = True
+                    break
+                batch.append(item)
+            try:
+                self.producer.send_batch(self.topic, [(k, v, [("content-type", b"application/x-protobuf")])
+                                                      for k, v in batch])
+                self.sent += len(batch)
+            except Exception as e:  # broker down: drop, keep the HTTP sink alive
+                self.dropped += len(batch)
+                logger.warning("kafka publish of %d pairs failed: %s", len(batch), e)
+            if stop:
+                return
+
+    def close(self, timeout: float = 5.0) -> None:
+        self.q.put(None)
+        self._t.join(timeout)
+        self.producer.close()
+
+
 class _Handler(BaseHTTPRequestHandler):
     out: TextIO = sys.stdout
     lock = threading.Lock()
+    sink: Optional[KafkaSink] = None
 
     def _handle(self):
         n = int(self.headers.get("Content-Length") or 0)
@@ -97,6 +174,8 @@ class _Handler(BaseHTTPRequestHandler):
                 for d in docs:
                     self.out.write(json.dumps(d, default=str) + "\n")
                 self.out.flush()
+            if self.sink is not None:
+                self.sink.publish(content)
             body, code = b"{}", 200
         except Exception as e:  # malformed event: report, keep serving
             body, code = json.dumps({"error": str(e)}).encode(), 400
@@ -113,8 +192,9 @@ class _Handler(BaseHTTPRequestHandler):
         pass
 
 
-def serve(host: str = "0.0.0.0", port: int = 8080, out: TextIO = sys.stdout) -> ThreadingHTTPServer:
-    handler = type("Handler", (_Handler,), {"out": out})
+def serve(host: str = "0.0.0.0", port: int = 8080, out: TextIO = sys.stdout,
+          sink: Optional[KafkaSink] = None) -> ThreadingHTTPServer:
+    handler = type("Handler", (_Handler,), {"out": out, "sink": sink})
     srv = ThreadingHTTPServer((host, port), handler)
     threading.Thread(target=srv.serve_forever, daemon=True).start()
     return srv
@@ -124,8 +204,11 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="seldon-amd-request-logger")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--kafka", default=None, help="also publish RequestResponse protos to this broker")
+    ap.add_argument("--kafka-topic", default="predictions")
     args = ap.parse_args(argv)
-    srv = serve(args.host, args.port)
+    sink = KafkaSink(args.kafka, args.kafka_topic) if args.kafka else None
+    srv = serve(args.host, args.port, sink=sink)
     try:
         threading.Event().wait()
     except KeyboardInterrupt:

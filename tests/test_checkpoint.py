@@ -10,6 +10,7 @@ import pickle
 import time
 
 import numpy as np
+import pytest
 
 import seldon_core_amd as sca
 from seldon_core_amd.components.outlier import OutlierMahalanobis
@@ -128,3 +129,41 @@ def test_worker_keys_are_per_rank(monkeypatch):
         assert d.checkpoint_key("router") == "persistence_ck_mab_router"
     finally:
         d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_bandit_router_checkpoint_roundtrip(tmp_path):
+    """Device-side bandit state (pinned tries/values) survives a restart."""
+    store = FileStore(str(tmp_path))
+
+    def gpu_mab():
+        params = [{"name": "n_branches", "value": "3", "type": "INT"}, {"name": "seed", "value": "7", "type": "INT"},
+                  {"name": "epsilon", "value": "0.1", "type": "FLOAT"},
+                  {"name": "best_branch", "value": "0", "type": "INT"}]
+        spec = {"name": "mab", "graph": {"name": "router", "type": "ROUTER", "implementation": "EPSILON_GREEDY",
+                                         "parameters": params,
+                                         "children": [{"name": f"m{i}", "type": "MODEL"} for i in range(3)]}}
+        return sca.Deployment(spec, components={f"m{i}": Const(i) for i in range(3)}, device=0,
+                              deployment_name="gck")
+
+    d = gpu_mab()
+    try:
+        assert d.engine.unit_kind("router") == "gpu:epsilon_greedy"
+        for _ in range(200):
+            out = d.predict({"data": {"ndarray": [[1.0]]}})
+            b = out["meta"]["routing"]["router"]
+            d.feedback({"request": {"data": {"ndarray": [[1.0]]}}, "response": out, "reward": float(b == 1)})
+        assert d.checkpoint(store) >= 1
+        before = json.loads(d.engine.snapshot("router"))
+    finally:
+        d.close()
+    assert before["best"] == 1
+    d2 = gpu_mab()
+    try:
+        assert d2.restore_checkpoint(store) >= 1
+        after = json.loads(d2.engine.snapshot("router"))
+        assert after["tries"] == before["tries"] and after["best"] == 1
+        picks = [d2.predict({"data": {"ndarray": [[1.0]]}})["meta"]["routing"]["router"] for _ in range(400)]
+        assert np.mean(np.array(picks) == 1) > 0.85  # exploits the restored best branch at once
+    finally:
+        d2.close()
