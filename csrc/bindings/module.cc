@@ -225,6 +225,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("mlp_model", [to_layers](py::list layers, int out_mode) {
     return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MlpModel>(to_layers(layers), out_mode));
   }, py::arg("layers"), py::arg("out_mode") = 0);
+  m.def("mlp_layerwise", [](std::shared_ptr<gpu::RowModel> m, int rows) {
+    auto p = std::dynamic_pointer_cast<gpu::MlpModel>(m);
+    if (!p) throw std::runtime_error("not an MLP model");
+    return p->layerwise(rows);
+  });
+  m.def("mlp_workspace_bytes", [](std::shared_ptr<gpu::RowModel> m, int rows) {
+    return m->workspace_bytes(rows, m->in_cols());
+  });
   m.def("vae_model", [to_layers](py::list encoder, int latent, py::list decoder, int samples, uint64_t seed) {
     return std::static_pointer_cast<gpu::RowModel>(
         gpu::MlpModel::vae(to_layers(encoder), latent, to_layers(decoder), samples, seed));

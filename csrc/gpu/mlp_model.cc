@@ -2,6 +2,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 namespace sca::gpu {
@@ -9,6 +11,7 @@ namespace sca::gpu {
 namespace {
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
+constexpr size_t kSlack = 4 * 16 + 64;  // workspace floats past each buffer (A look-ahead)
 
 // Host twin of kern::Philox (csrc/kernels/philox.h): identical streams, so the
 // CPU reference path draws the same reparameterisation noise as the GPU.
@@ -109,14 +112,22 @@ int MlpModel::add_layer(const DenseLayer& L, int type, int in_buf, int out_buf) 
   op.in_buf = in_buf;
   op.out_buf = out_buf;
   op.K = L.K;
-  op.Kp = round_up(L.K, 4);
+  op.Kp = round_up(L.K, 16);
   op.N = L.N;
   op.Np = round_up(L.N, 16);
-  // Wt [Kp][Np] + b [Np], zero padded
+  // fragment-major Wt: [Np/16 tiles][Kp/16 blocks][64 lanes][4]; lane (kq, n)
+  // of block kb holds Wt[16 kb + 4 kq + j][16 t + n], j = 0..3 (kernels.h)
   op.w_off = (long long)params_.size();
   params_.resize(params_.size() + size_t(op.Kp) * op.Np, 0.f);
-  for (int nn = 0; nn < L.N; ++nn)
-    for (int k = 0; k < L.K; ++k) params_[size_t(op.w_off) + size_t(k) * op.Np + nn] = L.W[size_t(nn) * L.K + k];
+  const int KB = op.Kp / 16;
+  float* w = params_.data() + op.w_off;
+  for (int t = 0; t < op.Np / 16; ++t)
+    for (int kb = 0; kb < KB; ++kb)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 4; ++j) {
+          const int nn = t * 16 + (lane & 15), k = kb * 16 + (lane >> 4) * 4 + j;
+          w[((size_t(t) * KB + kb) * 64 + lane) * 4 + j] = (nn < L.N && k < L.K) ? L.W[size_t(nn) * L.K + k] : 0.f;
+        }
   op.b_off = (long long)params_.size();
   params_.resize(params_.size() + size_t(op.Np), 0.f);
   for (int nn = 0; nn < L.N; ++nn) params_[size_t(op.b_off) + nn] = L.b[size_t(nn)];
@@ -124,11 +135,13 @@ int MlpModel::add_layer(const DenseLayer& L, int type, int in_buf, int out_buf) 
 }
 
 void MlpModel::build() {
+  if (const char* m = std::getenv("SCA_MLP_MODE"))
+    mode_ = !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "layer") ? 2 : 0;
   prog_ = kern::MlpProgram();
   params_.clear();
   auto& p = prog_;
   p.F = F_;
-  p.Fp = round_up(F_, 4);
+  p.Fp = round_up(F_, 16);
   int width[kern::kMlpMaxBufs] = {};
   width[0] = p.Fp;
   auto use = [&](int b, int w) { width[b] = std::max(width[b], w); };
@@ -185,11 +198,19 @@ void MlpModel::build() {
   int off = 0;
   for (int b = 0; b < kern::kMlpMaxBufs; ++b) {
     if (!width[b]) continue;
-    p.buf_ld[b] = width[b] | 1;  // odd stride: the 16 rows of a fragment land in distinct banks
+    // ld = 8 (mod 16): ds_read_b128 A fragments (16 rows x 16 B per k quad)
+    // are conflict-free in each of the instruction's four 16-lane groups
+    p.buf_ld[b] = (width[b] + 15 - 8) / 16 * 16 + 8;
     p.buf_off[b] = off;
     off += kern::kMlpRows * p.buf_ld[b];
   }
   p.lds_floats = off;
+  // 8 waves when a layer has >= 8 column tiles (more MFMA chains per tile of
+  // rows at small batches; LDS-bound occupancy keeps ~1-2 workgroups per CU)
+  int max_tiles = 0;
+  for (int o = 0; o < p.n_pre + p.n_loop; ++o) max_tiles = std::max(max_tiles, p.ops[o].Np / 16);
+  p.waves = max_tiles >= 8 ? 8 : 4;
+  params_.resize(params_.size() + 4 * 64 * 4, 0.f);  // B look-ahead pad (4 blocks, mlp.hip dense())
   if ((size_t(off) + kern::kMlpRows) * sizeof(float) > 160 * 1024)
     throw std::runtime_error("MlpModel: layer widths exceed the 160 KiB LDS budget of one workgroup");
 }
@@ -199,8 +220,132 @@ void MlpModel::to_device(int device) {
   d_params_.upload(params_.data(), params_.size() * sizeof(float));
 }
 
-void MlpModel::launch(const double* X, int rows, int, double* out, void*, hipStream_t s) {
-  kern::mlp_forward(X, rows, prog_, d_params_.as<float>(), seed_, offset_.fetch_add(1), out, s);
+// ------------------------------------------------------------ dispatch
+// Cost model in CU-cycles (MI355X: 256 CUs x 4 MFMA pipes, one
+// v_mfma_f32_16x16x4_f32 = 32 pipe cycles).  Fused: one workgroup per 16-row
+// tile runs every layer, so a batch of few tiles leaves most CUs idle and
+// the tile's MFMAs share one CU's 4 pipes.  Layer-wise: each layer spreads
+// (row tiles x column tiles) single-wave tasks over all 1024 pipes, paying
+// a launch gap and an L2 round trip per layer.
+bool MlpModel::layerwise(int rows) const {
+  if (mode_ == 1) return false;
+  if (mode_ == 2) return true;
+  const double row_tiles = std::ceil(rows / 16.0);
+  const int S = vae_ ? samples_ : 1;
+  double per_tile = 0, layer = 8000;  // convert + finish kernels
+  for (int o = 0; o < prog_.n_pre + prog_.n_loop; ++o) {
+    const auto& op = prog_.ops[o];
+    if (op.type == kern::kMlpReparam) continue;
+    const bool loop = o >= prog_.n_pre;
+    const double mf = double(op.Np / 16) * (op.Kp / 16) * 4;
+    per_tile += mf * (loop ? prog_.loops : 1);
+    const double tasks = (loop ? std::ceil(rows * double(S) / 16.0) : row_tiles) * (op.Np / 16);
+    layer += std::ceil(tasks / 1024.0) * (op.Kp / 16) * 4 * 32 + 1500 + 4000;
+  }
+  const double fused = std::max(1.0, row_tiles / 256.0) * per_tile * 8 + 2000;
+  return layer < 0.9 * fused;
+}
+
+int MlpModel::max_np() const {
+  int w = 16;
+  for (int o = 0; o < prog_.n_pre + prog_.n_loop; ++o) w = std::max(w, prog_.ops[o].Np);
+  return w;
+}
+
+size_t MlpModel::workspace_bytes(int max_rows, int) const {
+  if (mode_ == 1) return 0;
+  const size_t R = size_t(round_up(std::max(max_rows, 1), 16)), S = vae_ ? size_t(samples_) : 1;
+  const size_t W = size_t(max_np()), K0 = size_t(prog_.ops[0].Kp);
+  // [X fp32 R x K0][buf0 R*S x W][buf1 R*S x W]([head R x W][mse R]), kSlack
+  // floats after each: the layer kernel's A look-ahead reads up to 4 K-blocks
+  // past the end of a row
+  return (R * K0 + kSlack + 2 * (R * S * W + kSlack) + (vae_ ? R * W + kSlack + R : 0)) * sizeof(float);
+}
+
+void MlpModel::launch(const double* X, int rows, int, double* out, void* ws, hipStream_t s) {
+  const uint64_t off = offset_.fetch_add(1);
+  if (ws && layerwise(rows)) {
+    launch_layerwise(X, rows, out, static_cast<float*>(ws), seed_ ^ (off * 0x9E3779B97F4A7C15ULL), s);
+    return;
+  }
+  kern::mlp_forward(X, rows, prog_, d_params_.as<float>(), seed_, off, out, s);
+}
+
+void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* ws, uint64_t key, hipStream_t s) {
+  const float* P = d_params_.as<float>();
+  const size_t R = size_t(round_up(rows, 16)), S = vae_ ? size_t(samples_) : 1, W = size_t(max_np());
+  const size_t K0 = size_t(prog_.ops[0].Kp);
+  float* x32 = ws;
+  float* buf[2] = {x32 + R * K0 + kSlack, x32 + R * K0 + kSlack + R * S * W + kSlack};
+  float* head = buf[1] + R * S * W + kSlack;
+  float* mse = head + R * W + kSlack;
+  auto args = [&](const kern::MlpOp& op) {
+    kern::MlpLayerArgs a;
+    a.W = P + op.w_off;
+    a.bias = P + op.b_off;
+    a.K = op.K;
+    a.Kp = op.Kp;
+    a.N = op.N;
+    a.Np = op.Np;
+    a.act = op.act;
+    a.rows = rows;
+    a.rows_eff = rows;
+    return a;
+  };
+  // encoder / plain stack: X -> x32 -> buf0 -> buf1 -> ...
+  kern::mlp_convert(X, rows, F_, int(K0), x32, s);
+  const float* cur = x32;
+  int cur_ld = int(K0), flip = 0;
+  for (int o = 0; o < prog_.n_pre; ++o) {
+    const auto& op = prog_.ops[o];
+    kern::MlpLayerArgs a = args(op);
+    a.A = cur;
+    a.lda = cur_ld;
+    const bool head_out = vae_ && o + 1 == prog_.n_pre;
+    a.O = head_out ? head : buf[flip];
+    a.ldo = op.Np;
+    kern::mlp_layer(a, s);
+    cur = a.O;
+    cur_ld = op.Np;
+    flip ^= 1;
+  }
+  if (!vae_) {
+    kern::mlp_finish(cur, cur_ld, rows, prog_.out_dim, prog_.out_softmax, out, s);
+    return;
+  }
+  // decoder over rows x samples: reparam fused into the first layer's A, MSE into the last's epilogue
+  (void)hipMemsetAsync(mse, 0, size_t(rows) * sizeof(float), s);
+  const float* dcur = nullptr;
+  int dld = 0;
+  flip = 0;
+  for (int o = prog_.n_pre; o < prog_.n_pre + prog_.n_loop; ++o) {
+    const auto& op = prog_.ops[o];
+    if (op.type == kern::kMlpReparam) continue;
+    kern::MlpLayerArgs a = args(op);
+    a.rows_eff = rows * int(S);
+    if (!dcur) {
+      a.H = head;
+      a.ldh = prog_.ops[prog_.n_pre - 1].Np;
+      a.latent = latent_;
+      a.key = key;
+    } else {
+      a.A = dcur;
+      a.lda = dld;
+    }
+    if (op.type == kern::kMlpDenseMse) {
+      a.mse = mse;
+      a.xref = x32;  // the fp32 input, as the fused kernel's LDS copy
+      a.ldx = int(K0);
+    } else {
+      a.O = buf[flip];
+      a.ldo = op.Np;
+      dcur = a.O;
+      dld = op.Np;
+      flip ^= 1;
+    }
+    kern::mlp_layer(a, s);
+  }
+  kern::mlp_mse_finish(mse, rows, 1.0 / (double(F_) * samples_), out, s);
 }
 
 void MlpModel::cpu_dense(const DenseLayer& L, const std::vector<float>& in, std::vector<float>& out, int rows) const {

@@ -39,6 +39,10 @@ class MlpModel : public RowModel {
   int out_cols(int) const override { return out_dim_; }
   void to_device(int device) override;
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  // Layer-wise path (one launch per layer over rows x column tiles) for
+  // batches whose 16-row tiles cannot fill the chip; needs the workspace.
+  size_t workspace_bytes(int max_rows, int cols) const override;
+  bool layerwise(int rows) const;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
   std::shared_ptr<RowModel> clone() const override;
   const kern::MlpProgram& program() const { return prog_; }
@@ -49,6 +53,8 @@ class MlpModel : public RowModel {
   void build();
   int add_layer(const DenseLayer& L, int type, int in_buf, int out_buf);
   void cpu_dense(const DenseLayer& L, const std::vector<float>& in, std::vector<float>& out, int rows) const;
+  void launch_layerwise(const double* X, int rows, double* out, float* ws, uint64_t key, hipStream_t s);
+  int max_np() const;
 
   std::vector<DenseLayer> enc_, dec_;  // plain: enc_ = all layers
   bool vae_ = false;
@@ -56,6 +62,7 @@ class MlpModel : public RowModel {
   int F_ = 0, out_dim_ = 0;
   uint64_t seed_ = 0;
   std::atomic<uint64_t> offset_{0};  // advances per launch: fresh MC draws per request
+  int mode_ = 0;                     // SCA_MLP_MODE: 0 auto, 1 fused, 2 layer-wise
   kern::MlpProgram prog_;
   std::vector<float> params_;
   DeviceBuffer d_params_;

@@ -107,12 +107,13 @@ void crop_resize_chw_u8(const uint8_t* img, int H, int W, int C, int crop, float
 // ------------------------------------------------------------ fused MLP
 // A whole dense network (and the VAE outlier detector's encoder -> MC
 // reparameterised decoder -> reconstruction-MSE loop) in one launch: a
-// 256-thread workgroup owns a 16-row tile, keeps every activation in LDS and
-// runs each Dense layer on f32-input MFMA (v_mfma_f32_16x16x4_f32: exact fp32
-// products, i.e. Keras/torch float32 numerics) with bias + activation fused
-// into the epilogue.  Weights are stored transposed and zero-padded
-// (Wt [Kp][Np], Kp % 4 == 0, Np % 16 == 0) so B-fragment loads are coalesced
-// and the K loop has no bounds checks.
+// A workgroup of 4 or 8 waves owns a 16-row tile, keeps every activation in
+// LDS and runs each Dense layer on f32-input MFMA (v_mfma_f32_16x16x4_f32:
+// exact fp32 products, i.e. Keras/torch float32 numerics) with bias +
+// activation fused into the epilogue.  Weights are transposed, zero-padded to
+// Kp % 16 == 0, Np % 16 == 0 and packed fragment-major
+// ([Np/16][Kp/16][64][4] floats: one 16-byte load per lane feeds four MFMAs),
+// so the K loop has no bounds checks and every B load is a coalesced 1 KiB.
 enum MlpOpType : int { kMlpDense = 0, kMlpDenseMse = 1, kMlpReparam = 2 };
 enum MlpAct : int { kMlpIdentity = 0, kMlpRelu = 1, kMlpSigmoid = 2, kMlpTanh = 3 };
 struct MlpOp {
@@ -131,10 +132,44 @@ struct MlpProgram {
   int out_buf = 0, out_dim = 0, out_softmax = 0;
   int mse_mode = 0, mse_dim = 0;         // 1: out[r] = mean over loops of mean_c (recon - x)^2
   int lds_floats = 0;
+  int waves = 4;                         // workgroup = 64 * waves threads
   MlpOp ops[kMlpMaxOps];
 };
 void mlp_forward(const double* X, int rows, const MlpProgram& prog, const float* params, uint64_t seed,
                  uint64_t offset, double* out, hipStream_t stream);
+
+// Layer-wise path for batches too small to fill the chip with one workgroup
+// per 16-row tile: one launch per Dense layer, one wave per 16x16 output tile
+// (grid = row tiles x column tiles), activations round-trip through an
+// L2-resident fp32 workspace (the fp64 request rows are converted once).  Same packed weights and k permutation as the
+// fused kernel.  A VAE's MC decodes run as one batch of rows x samples rows
+// (sample-major): the first decoder layer draws z = mu + exp(lv / 2) eps on
+// the fly from the same Philox streams as the fused kernel, the last one
+// reduces (act(y) - x)^2 into per-row sums.
+struct MlpLayerArgs {
+  const float* W = nullptr;  // packed fragment-major [Np/16][Kp/16][64][4]
+  const float* bias = nullptr;
+  int K = 0, Kp = 0, N = 0, Np = 0, act = 0;
+  const float* A = nullptr;  // A = fp32 activations [rows_eff][lda] ...
+  int lda = 0;
+  const float* H = nullptr;  // ... or a VAE head [rows][ldh] = [mu | log_var] (reparameterised A)
+  int ldh = 0, latent = 0;
+  uint64_t key = 0;
+  int rows = 0;      // request rows (X, H)
+  int rows_eff = 0;  // rows x samples on decoder layers, else rows
+  float* O = nullptr;    // fp32 out [rows_eff][ldo], columns >= N zeroed
+  int ldo = 0;
+  float* mse = nullptr;  // if set: MSE epilogue against xref [rows][ldx], sums into mse[row % rows]
+  const float* xref = nullptr;
+  int ldx = 0;
+};
+void mlp_layer(const MlpLayerArgs& a, hipStream_t stream);
+// fp64 rows [rows][F] -> fp32 [rows][ld], zero-padded columns
+void mlp_convert(const double* X, int rows, int F, int ld, float* out, hipStream_t stream);
+// logits [rows][ld] -> out: mode 0 plain [rows][n], 1 row softmax, 2 binary [1 - p, p]
+void mlp_finish(const float* logits, int ld, int rows, int n, int mode, double* out, hipStream_t stream);
+// out[r] = mse[r] * scale
+void mlp_mse_finish(const float* mse, int rows, double scale, double* out, hipStream_t stream);
 
 // Mahalanobis detector: Sherman-Morrison recurrence + scores over a batch
 // (B [nb][k][k], cov0 [k][k], xd [nb][k]); false if k > 16.

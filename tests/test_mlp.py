@@ -95,6 +95,15 @@ def test_vae_cpu_is_stochastic_and_positive():
     assert (a > 0).all() and not np.array_equal(a, b)  # fresh MC draws per call
 
 
+def test_mlp_dispatch_cost_model():
+    """Few 16-row tiles of a wide network -> layer-wise; many tiles of a narrow one -> fused."""
+    C = sca.native()
+    wide = C.mlp_model(random_dense_stack([784, 512, 256, 10], ["relu", "relu", "identity"]), 1)
+    narrow = C.mlp_model(random_dense_stack([13, 37, 19, 3], ["relu", "relu", "identity"]), 1)
+    assert C.mlp_layerwise(wide, 64) and not C.mlp_layerwise(narrow, 64)
+    assert C.mlp_workspace_bytes(wide, 64) >= 2 * 64 * 512 * 4
+
+
 def test_lds_budget_error():
     C = sca.native()
     with pytest.raises(Exception, match="LDS"):
@@ -103,11 +112,13 @@ def test_lds_budget_error():
 
 # ------------------------------------------------------------------ GPU
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["fused", "layer"])
 @pytest.mark.parametrize("dims", [(13, 37, 19, 3), (784, 256, 64, 10), (5, 1, 2), (64, 128, 128, 64, 33)])
 @pytest.mark.parametrize("rows", [1, 16, 37, 300])
-def test_mlp_gpu_matches_torch_fp32(dims, rows):
+def test_mlp_gpu_matches_torch_fp32(dims, rows, mode, monkeypatch):
     import torch
 
+    monkeypatch.setenv("SCA_MLP_MODE", mode)  # read when the model is built
     layers = random_dense_stack(list(dims), ["relu"] * (len(dims) - 2) + ["identity"], seed=len(dims))
     rm = mlp_row_model(layers, OUT_SOFTMAX)
     X = np.random.default_rng(rows).normal(size=(rows, dims[0]))
@@ -126,7 +137,9 @@ def test_mlp_gpu_matches_torch_fp32(dims, rows):
 
 
 @pytest.mark.gpu
-def test_vae_gpu_matches_cpu_reference():
+@pytest.mark.parametrize("mode", ["fused", "layer"])
+def test_vae_gpu_matches_cpu_reference(mode, monkeypatch):
+    monkeypatch.setenv("SCA_MLP_MODE", mode)
     C = sca.native()
     enc, dec = _vae_layers(F=30, hidden=(20, 10), latent=3)
     gpu_m = C.vae_model(enc, 3, dec, 10, 11)

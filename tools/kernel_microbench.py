@@ -1,0 +1,278 @@
+"""Hot serving kernels at throughput batch sizes, for timing and PMC passes (GPU only).
+
+    python tools/kernel_microbench.py [--only tree,vae,mlp,linear] [--iters 50]
+
+Each case launches its kernel `iters` times on one stream after a warmup and
+prints one JSON line (microseconds per launch from HIP events for the raw
+tree kernels; wall time per BatchedUnit.run and the batcher's GPU-busy time
+for the model kernels, which includes the H2D/D2H of the batch).  Used under
+`rocprofv3 --pmc ...` by tools/gpu_pmc.sh so every dispatch of the same
+kernel reports the same counters; tools/pmc_summary.py turns the CSVs into
+profiles/*/pmc_summary.md.
+
+Cases (shapes are the serving configs of BASELINE.json, at a large batch):
+  tree    xgboost 1000 trees x depth 8, 32 features, 4096 rows (tree_perfect_partial + tree_reduce)
+  vae     VAE outlier detector 64 -> 256 -> 128 -> z16 -> 128 -> 256 -> 64, 10 MC decodes, 4096 rows
+  mlp     MNIST-shaped classifier 784 -> 512 -> 256 -> 10 softmax, 8192 and 64 rows
+  mlp_torch / vae_torch  the same networks in PyTorch eager fp32 (hipBLASLt GEMMs), as the library baseline
+  linear  iris logistic regression 4 -> 3 softmax, 65536 rows
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _time_unit(name, unit, X, iters, extra):
+    unit.run(X[: min(len(X), 64)])
+    unit.run(X)
+    unit.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        unit.run(X)
+    dt = time.perf_counter() - t0
+    st = unit.stats()
+    rec = {"case": name, "rows": len(X), "iters": iters, "wall_us_per_run": round(dt / iters * 1e6, 1),
+           "gpu_busy_us_per_run": round(st["gpu_busy_s"] / iters * 1e6, 1), "batches": st["batches"], **extra}
+    print(json.dumps(rec), flush=True)
+    return rec
+
+
+def case_tree(iters):
+    import torch
+
+    from seldon_core_amd import native
+
+    K = native().kernels
+    T, D, F, rows = 1000, 8, 32, 4096
+    ni = (1 << D) - 1
+    g = torch.Generator().manual_seed(0)
+    thr = torch.randn(T * ni, generator=g)
+    feat = torch.randint(0, F, (T * ni,), generator=g, dtype=torch.int32)
+    nodes = torch.stack([thr.view(torch.int32), feat], 1).contiguous().cuda()
+    leaves = (torch.randn(T * (ni + 1), generator=g) * 0.01).cuda()
+    X = torch.randn(rows, F, dtype=torch.float64, generator=g).cuda()
+    rb, chunk = 64, 32  # measured best two-pass geometry at >= 2048 rows (profiles/r01g_tree_variants)
+    begin = torch.unique_consecutive(torch.arange(0, T + chunk, chunk, dtype=torch.int32).clamp_(max=T)).cuda()
+    nc = begin.numel() - 1
+    group = torch.zeros(nc, dtype=torch.int32, device="cuda")
+    partial = torch.empty(nc * rows, dtype=torch.float32, device="cuda")
+    out = torch.empty(rows, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    def launch():
+        K.tree_perfect_partial(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0, begin.data_ptr(), nc,
+                               rb, partial.data_ptr(), s, 0)
+        K.tree_reduce(partial.data_ptr(), rows, nc, group.data_ptr(), 1, 0, 1.0, 0, out.data_ptr(), 1, s)
+
+    for _ in range(5):
+        launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000 / iters
+    # reference: the same ensemble on the CPU twin
+    ref = torch.zeros(rows, dtype=torch.float64)
+    Xc, thr_c, feat_c, leaves_c = X.cpu()[:256].float().double(), thr, feat, leaves.cpu()  # kernel compares in fp32
+    for t in range(T):
+        idx = torch.zeros(256, dtype=torch.long)
+        for _ in range(D):
+            n = t * ni + idx
+            go_right = Xc[torch.arange(256), feat_c[n].long()] >= thr_c[n].double()
+            idx = 2 * idx + 1 + go_right.long()
+        ref[:256] += leaves_c[t * (ni + 1) + idx - ni].double()
+    err = float((out.cpu()[:256] - ref[:256]).abs().max())
+    visits = rows * T * D
+    rec = {"case": "tree", "rows": rows, "trees": T, "depth": D, "iters": iters, "us_per_batch": round(us, 2),
+           "rows_per_s": round(rows / us * 1e6), "node_visits_per_s": round(visits / us * 1e6),
+           "max_err_vs_cpu": err}
+    print(json.dumps(rec), flush=True)
+    return rec
+
+
+def case_vae(iters):
+    from seldon_core_amd import native
+    from seldon_core_amd.models.mlp import random_dense_stack
+
+    C = native()
+    F, latent, rows = 64, 16, 4096
+    enc = random_dense_stack([F, 256, 128, 2 * latent], ["relu", "relu", "identity"], seed=1)
+    dec = random_dense_stack([latent, 128, 256, F], ["relu", "relu", "sigmoid"], seed=2)
+    unit = C.BatchedUnit(C.vae_model(enc, latent, dec, 10, 3), 0)
+    X = np.random.default_rng(0).random(size=(rows, F))
+    try:
+        flops = 2 * rows * (F * 256 + 256 * 128 + 128 * 2 * latent + 10 * (latent * 128 + 128 * 256 + 256 * F))
+        rec = _time_unit("vae", unit, X, iters, {"gflop_per_run": round(flops / 1e9, 3)})
+        rec["tflops_gpu_busy"] = round(flops / (rec["gpu_busy_us_per_run"] * 1e-6) / 1e12, 2)
+        print(json.dumps({"case": "vae_derived", "tflops_fp32_mfma": rec["tflops_gpu_busy"]}), flush=True)
+    finally:
+        unit.stop()
+
+
+MLP_DIMS = [784, 512, 256, 10]
+
+
+def case_mlp(iters, rows_list=(8192, 64)):
+    from seldon_core_amd import native
+    from seldon_core_amd.models.mlp import OUT_SOFTMAX, mlp_row_model, random_dense_stack
+
+    C = native()
+    dims = MLP_DIMS
+    unit = C.BatchedUnit(mlp_row_model(random_dense_stack(dims, ["relu", "relu", "identity"], seed=4), OUT_SOFTMAX), 0)
+    try:
+        for rows in rows_list:
+            X = np.random.default_rng(1).normal(size=(rows, dims[0]))
+            flops = 2 * rows * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+            rec = _time_unit("mlp", unit, X, iters, {"gflop_per_run": round(flops / 1e9, 4),
+                                                     "input_mb_fp64": round(X.nbytes / 2**20, 2)})
+            print(json.dumps({"case": "mlp_derived", "rows": rows,
+                              "tflops_fp32_mfma_incl_h2d": round(flops / (rec["gpu_busy_us_per_run"] * 1e-6) / 1e12, 2)}),
+                  flush=True)
+    finally:
+        unit.stop()
+
+
+def case_mlp_modes(iters):
+    """Fused vs layer-wise MLP / VAE at serving batch sizes (GPU-busy time per batch incl. H2D)."""
+    import os
+
+    from seldon_core_amd import native
+    from seldon_core_amd.models.mlp import OUT_SOFTMAX, mlp_row_model, random_dense_stack
+
+    C = native()
+    nets = {"mlp784": lambda: mlp_row_model(random_dense_stack(MLP_DIMS, ["relu", "relu", "identity"], seed=4),
+                                            OUT_SOFTMAX),
+            "vae64": lambda: C.vae_model(random_dense_stack([64, 256, 128, 32], ["relu", "relu", "identity"], seed=1), 16,
+                                         random_dense_stack([16, 128, 256, 64], ["relu", "relu", "sigmoid"], seed=2),
+                                         10, 3)}
+    for net, make in nets.items():
+        for rows in (1, 16, 64, 256, 1024, 4096):
+            rec = {"case": "mlp_modes", "net": net, "rows": rows}
+            for mode in ("fused", "layer", "auto"):
+                os.environ["SCA_MLP_MODE"] = mode
+                m = make()
+                if mode == "auto":
+                    rec["auto_layerwise"] = bool(C.mlp_layerwise(m, rows))
+                unit = C.BatchedUnit(m, 0)
+                X = np.random.default_rng(rows).random(size=(rows, 784 if net == "mlp784" else 64))
+                try:
+                    y = unit.run(X)
+                    unit.reset_stats()
+                    for _ in range(iters):
+                        y2 = unit.run(X)
+                    rec[mode + "_us"] = round(unit.stats()["gpu_busy_s"] / iters * 1e6, 1)
+                    if mode == "fused":
+                        ref = y2
+                    else:
+                        rec[mode + "_maxdiff"] = float(np.abs(y2 - ref).max()) if net == "mlp784" else None
+                finally:
+                    unit.stop()
+            os.environ.pop("SCA_MLP_MODE", None)
+            print(json.dumps(rec), flush=True)
+
+
+def _torch_time(fn, iters):
+    import torch
+
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000 / iters
+
+
+def case_mlp_torch(iters, rows_list=(8192, 64)):
+    """Same MLP in PyTorch eager fp32 (hipBLASLt GEMMs + elementwise), input already fp32 on device."""
+    import torch
+
+    from seldon_core_amd.models.mlp import random_dense_stack
+
+    layers = random_dense_stack(MLP_DIMS, ["relu", "relu", "identity"], seed=4)
+    Ws = [torch.tensor(L["W"], device="cuda") for L in layers]
+    bs = [torch.tensor(L["b"], device="cuda") for L in layers]
+    for rows in rows_list:
+        x = torch.randn(rows, MLP_DIMS[0], device="cuda")
+
+        def fwd():
+            h = x
+            for i, (W, b) in enumerate(zip(Ws, bs)):
+                h = torch.nn.functional.linear(h, W, b)
+                if i + 1 < len(Ws):
+                    h = torch.relu(h)
+            return torch.softmax(h, 1)
+
+        us = _torch_time(fwd, iters)
+        flops = 2 * rows * sum(a * b for a, b in zip(MLP_DIMS[:-1], MLP_DIMS[1:]))
+        print(json.dumps({"case": "mlp_torch_fp32", "rows": rows, "us_per_run": round(us, 2),
+                          "tflops": round(flops / (us * 1e-6) / 1e12, 2)}), flush=True)
+
+
+def case_vae_torch(iters):
+    import torch
+
+    from seldon_core_amd.models.mlp import random_dense_stack
+
+    F, latent, rows = 64, 16, 4096
+    enc = random_dense_stack([F, 256, 128, 2 * latent], ["relu", "relu", "identity"], seed=1)
+    dec = random_dense_stack([latent, 128, 256, F], ["relu", "relu", "sigmoid"], seed=2)
+    E = [(torch.tensor(L["W"], device="cuda"), torch.tensor(L["b"], device="cuda")) for L in enc]
+    D = [(torch.tensor(L["W"], device="cuda"), torch.tensor(L["b"], device="cuda")) for L in dec]
+    x = torch.rand(rows, F, device="cuda")
+    F_ = torch.nn.functional
+
+    def fwd():
+        h = F_.relu(F_.linear(F_.relu(F_.linear(x, *E[0])), *E[1]))
+        h = F_.linear(h, *E[2])
+        mu, logvar = h[:, :latent], h[:, latent:]
+        err = torch.zeros(rows, device="cuda")
+        for _ in range(10):
+            z = mu + torch.exp(0.5 * logvar) * torch.randn_like(mu)
+            y = torch.sigmoid(F_.linear(F_.relu(F_.linear(F_.relu(F_.linear(z, *D[0])), *D[1])), *D[2]))
+            err += ((y - x) ** 2).mean(1)
+        return err / 10
+
+    us = _torch_time(fwd, iters)
+    print(json.dumps({"case": "vae_torch_fp32", "rows": rows, "us_per_run": round(us, 2)}), flush=True)
+
+
+def case_linear(iters):
+    from seldon_core_amd import native
+
+    C = native()
+    rows = 65536
+    rng = np.random.default_rng(2)
+    unit = C.BatchedUnit(C.linear_model(rng.normal(size=(3, 4)), rng.normal(size=3), 1), 0)
+    X = rng.normal(size=(rows, 4))
+    try:
+        _time_unit("linear", unit, X, iters, {"bytes_in_out": rows * (4 + 3) * 8})
+    finally:
+        unit.stop()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="tree,vae,mlp,linear")
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    cases = {"tree": case_tree, "vae": case_vae, "mlp": case_mlp, "linear": case_linear,
+             "mlp_torch": case_mlp_torch, "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes}
+    for c in a.only.split(","):
+        cases[c](a.iters)
+
+
+if __name__ == "__main__":
+    main()
