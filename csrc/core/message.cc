@@ -150,7 +150,13 @@ double half_to_double(uint16_t h) {
 bool TfTensor::to_dense(std::vector<int64_t>& shape, std::vector<double>& v, std::string* err) const {
   shape = dims;
   int64_t n = 1;
-  for (auto d : dims) n *= d;
+  for (auto d : dims) {
+    if (d < 0) {
+      if (err) *err = "negative dimension in tftensor shape";
+      return false;
+    }
+    n *= d;
+  }
   v.clear();
   if (!content.empty()) {
     const char* p = content.data();
@@ -221,7 +227,13 @@ bool DefaultData::dense(std::vector<int64_t>& shp, std::vector<double>& vals, st
     case DataKind::Tensor: {
       shp = shape;
       int64_t n = 1;
-      for (auto d : shape) n *= d;
+      for (auto d : shape) {
+        if (d < 0) {
+          if (err) *err = "negative dimension in tensor shape";
+          return false;
+        }
+        n *= d;
+      }
       if (n != int64_t(values.size())) {
         if (err) *err = "tensor values do not match shape";
         return false;
@@ -425,6 +437,7 @@ void parse_tftensor(const Json& j, TfTensor& t) {
       for (const auto& x : d->items()) {
         int64_t sz = 0;
         if (auto* s = field(x, "size")) sz = get_int(*s, "dim.size");
+        if (sz < 0) bad("negative dimension in tensorShape");
         t.dims.push_back(sz);
       }
     }
@@ -469,7 +482,11 @@ void parse_default_data(const Json& j, DefaultData& d) {
     check_known(*f, {"shape", "values"}, "seldon.protos.Tensor");
     if (auto* s = field(*f, "shape")) {
       if (!s->is_array()) bad("expected array for Tensor.shape");
-      for (const auto& x : s->items()) d.shape.push_back(get_int(x, "Tensor.shape"));
+      for (const auto& x : s->items()) {
+        int64_t dim = get_int(x, "Tensor.shape");
+        if (dim < 0) bad("negative dimension in Tensor.shape");
+        d.shape.push_back(dim);
+      }
     }
     if (auto* v = field(*f, "values")) {
       if (!v->is_array()) bad("expected array for Tensor.values");

@@ -461,6 +461,7 @@ bool dec_tftensor(std::string_view buf, TfTensor& t) {
                 if ((dt >> 3) == 1 && (dt & 7) == 0) size = int64_t(dr.varint());
                 else dr.skip(uint32_t(dt & 7));
               }
+              if (size < 0) { sr.ok = false; break; }
               t.dims.push_back(size);
             } else if ((st >> 3) == 3 && (st & 7) == 0) {
               t.unknown_rank = sr.varint() != 0;
@@ -505,7 +506,10 @@ bool dec_default_data(std::string_view buf, DefaultData& d) {
         if (ff == 1) {
           std::vector<int32_t> s;
           read_packed_varint(tr, ww, s);
-          for (auto x : s) d.shape.push_back(x);
+          for (auto x : s) {
+            if (x < 0) return false;  // numpy rejects negative dims
+            d.shape.push_back(x);
+          }
         } else if (ff == 2) {
           read_packed_fixed(tr, ww, d.values);
         } else {

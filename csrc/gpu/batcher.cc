@@ -194,7 +194,11 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
     it.cols = int(cc);
   }
   const int want = model_->in_cols();
-  if (it.rows == 0 || (want > 0 && it.cols != want)) {
+  if (it.rows <= 0 || it.cols <= 0) {
+    k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, model_->name() + " expects a non-empty 2-D numeric payload")));
+    return;
+  }
+  if (want > 0 && it.cols != want) {
     k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR,
                                "X has " + std::to_string(it.cols) + " features, but " + model_->name() +
                                    " is expecting " + std::to_string(want) + " features as input.")));

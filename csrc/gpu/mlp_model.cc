@@ -211,8 +211,10 @@ void MlpModel::build() {
   for (int o = 0; o < p.n_pre + p.n_loop; ++o) max_tiles = std::max(max_tiles, p.ops[o].Np / 16);
   p.waves = max_tiles >= 8 ? 8 : 4;
   params_.resize(params_.size() + 4 * 64 * 4, 0.f);  // B look-ahead pad (4 blocks, mlp.hip dense())
-  if ((size_t(off) + kern::kMlpRows) * sizeof(float) > 160 * 1024)
-    throw std::runtime_error("MlpModel: layer widths exceed the 160 KiB LDS budget of one workgroup");
+  // A network whose activations do not fit one workgroup's 160 KiB of LDS
+  // cannot use the fused kernel; it runs layer-wise (activations in HBM).
+  fused_ok_ = (size_t(off) + kern::kMlpRows) * sizeof(float) <= 160 * 1024;
+  if (!fused_ok_) mode_ = 2;
 }
 
 void MlpModel::to_device(int device) {
@@ -254,6 +256,11 @@ int MlpModel::max_np() const {
 
 size_t MlpModel::workspace_bytes(int max_rows, int) const {
   if (mode_ == 1) return 0;
+  if (mode_ == 0) {  // auto: only models the cost model ever sends layer-wise need one
+    bool any = false;
+    for (int r = 1; r <= std::max(max_rows, 1) && !any; r += (r < 64 ? 1 : 16)) any = layerwise(r);
+    if (!any) return 0;
+  }
   const size_t R = size_t(round_up(std::max(max_rows, 1), 16)), S = vae_ ? size_t(samples_) : 1;
   const size_t W = size_t(max_np()), K0 = size_t(prog_.ops[0].Kp);
   // [X fp32 R x K0][buf0 R*S x W][buf1 R*S x W]([head R x W][mse R]), kSlack
@@ -264,6 +271,7 @@ size_t MlpModel::workspace_bytes(int max_rows, int) const {
 
 void MlpModel::launch(const double* X, int rows, int, double* out, void* ws, hipStream_t s) {
   const uint64_t off = offset_.fetch_add(1);
+  if (!fused_ok_ && !ws) throw std::runtime_error("MlpModel: layer-wise network launched without a workspace");
   if (ws && layerwise(rows)) {
     launch_layerwise(X, rows, out, static_cast<float*>(ws), seed_ ^ (off * 0x9E3779B97F4A7C15ULL), s);
     return;

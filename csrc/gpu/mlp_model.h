@@ -63,6 +63,7 @@ class MlpModel : public RowModel {
   uint64_t seed_ = 0;
   std::atomic<uint64_t> offset_{0};  // advances per launch: fresh MC draws per request
   int mode_ = 0;                     // SCA_MLP_MODE: 0 auto, 1 fused, 2 layer-wise
+  bool fused_ok_ = true;             // activations fit one workgroup's LDS
   kern::MlpProgram prog_;
   std::vector<float> params_;
   DeviceBuffer d_params_;

@@ -340,7 +340,22 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
   }
 
   // Parse as many complete requests as possible (one in flight at a time).
+  // Nothing thrown while parsing one client's bytes may reach the epoll loop:
+  // answer 400 and drop that connection instead.
   void process(Conn* c) {
+    try {
+      process_requests(c);
+    } catch (const std::exception& e) {
+      if (c->dead) return;
+      c->busy = false;
+      c->in.clear();
+      c->in_off = 0;
+      write_response(c, 400, "text/plain", std::string("bad request: ") + e.what(), false);
+      flush(c);
+    }
+  }
+
+  void process_requests(Conn* c) {
     while (!c->busy && !c->dead) {
       std::string_view buf(c->in.data() + c->in_off, c->in.size() - c->in_off);
       if (buf.empty()) break;
@@ -394,10 +409,20 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
       if (chunked) {
         size_t p = body_start;
         bool complete = false;
+        bool bad = false, too_large = false;
         while (true) {
           size_t ce = buf.find("\r\n", p);
           if (ce == std::string_view::npos) break;
-          size_t sz = strtoull(std::string(buf.substr(p, ce - p)).c_str(), nullptr, 16);
+          // chunk-size = 1*HEXDIG [ ";" chunk-ext ]; reject anything else and
+          // compare without adding to the untrusted size (no wrap-around).
+          std::string_view szs = buf.substr(p, ce - p);
+          size_t semi = szs.find(';');
+          if (semi != std::string_view::npos) szs = szs.substr(0, semi);
+          szs = trim(szs);
+          if (szs.empty() || szs.size() > 15 ||
+              szs.find_first_not_of("0123456789abcdefABCDEF") != std::string_view::npos) { bad = true; break; }
+          size_t sz = size_t(strtoull(std::string(szs).c_str(), nullptr, 16));
+          if (sz > srv->opts_.max_body || chunk_body.size() > srv->opts_.max_body - sz) { too_large = true; break; }
           if (sz == 0) {
             size_t te = buf.find("\r\n", ce + 2);
             if (te == std::string_view::npos) break;
@@ -405,11 +430,19 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
             complete = true;
             break;
           }
-          if (buf.size() < ce + 2 + sz + 2) break;
+          if (buf.size() - (ce + 2) < sz + 2) break;
+          if (buf.substr(ce + 2 + sz, 2) != "\r\n") { bad = true; break; }
           chunk_body.append(buf.data() + ce + 2, sz);
           p = ce + 2 + sz + 2;
         }
+        if (bad) { write_response(c, 400, "text/plain", "bad chunked encoding", false); break; }
+        if (too_large) { write_response(c, 413, "text/plain", "payload too large", false); break; }
         if (!complete) {
+          // an incomplete chunked body may not grow past the body limit
+          if (buf.size() - body_start > srv->opts_.max_body + 65536) {
+            write_response(c, 413, "text/plain", "payload too large", false);
+            break;
+          }
           if (expect_continue && !c->sent_continue) { c->out += "HTTP/1.1 100 Continue\r\n\r\n"; c->sent_continue = true; flush(c); }
           break;
         }

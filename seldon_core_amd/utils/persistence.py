@@ -33,22 +33,42 @@ def state_key(deployment: str = DEPLOYMENT_ID, predictor: str = PREDICTOR_ID, un
     return f"persistence_{deployment}_{predictor}_{unit}"
 
 
+def _default_dir() -> str:
+    """Per-user state directory (never a shared world-writable path)."""
+    base = os.environ.get("XDG_STATE_HOME") or os.path.join(os.path.expanduser("~"), ".local", "state")
+    return os.path.join(base, "seldon-persistence")
+
+
 class FileStore:
+    """Snapshots are unpickled on restore, so only files this user owns, in a
+    directory no one else can write, are ever read."""
+
     def __init__(self, root: Optional[str] = None):
-        self.root = root or os.environ.get("SELDON_PERSISTENCE_DIR", "/tmp/seldon-persistence")
-        os.makedirs(self.root, exist_ok=True)
+        self.root = root or os.environ.get("SELDON_PERSISTENCE_DIR") or _default_dir()
+        os.makedirs(self.root, mode=0o700, exist_ok=True)
+        self._check_owned(self.root, directory=True)
+
+    @staticmethod
+    def _check_owned(path: str, directory: bool = False) -> None:
+        st = os.stat(path)
+        if st.st_uid != os.getuid():
+            raise PermissionError(f"{path} is owned by uid {st.st_uid}, not the current user")
+        if st.st_mode & 0o022:
+            raise PermissionError(f"{path} is group/world-writable (mode {oct(st.st_mode & 0o777)})")
 
     def get(self, key: str) -> Optional[bytes]:
         p = os.path.join(self.root, key + ".pkl")
         if not os.path.exists(p):
             return None
+        self._check_owned(p)
         with open(p, "rb") as f:
             return f.read()
 
     def set(self, key: str, value: bytes) -> None:
         p = os.path.join(self.root, key + ".pkl")
         tmp = p + ".tmp"
-        with open(tmp, "wb") as f:
+        fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+        with os.fdopen(fd, "wb") as f:
             f.write(value)
         os.replace(tmp, p)
 

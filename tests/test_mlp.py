@@ -104,10 +104,28 @@ def test_mlp_dispatch_cost_model():
     assert C.mlp_workspace_bytes(wide, 64) >= 2 * 64 * 512 * 4
 
 
-def test_lds_budget_error():
+def test_wide_network_falls_back_to_layerwise():
+    """Activations wider than one workgroup's LDS: no fused plan, every batch
+    size goes layer-wise and always gets a workspace."""
     C = sca.native()
-    with pytest.raises(Exception, match="LDS"):
-        C.mlp_model(random_dense_stack([2048, 2048, 10], ["relu", "identity"]), 0)
+    layers = random_dense_stack([784, 2048, 10], ["relu", "identity"])
+    m = C.mlp_model(layers, 1)
+    for rows in (1, 64, 4096):
+        assert C.mlp_layerwise(m, rows)
+        assert C.mlp_workspace_bytes(m, rows) >= rows * 2048 * 4
+    X = np.random.default_rng(0).normal(size=(5, 784))
+    h = np.maximum(X @ np.asarray(layers[0]["W"]).T + layers[0]["b"], 0)
+    z = h @ np.asarray(layers[1]["W"]).T + layers[1]["b"]
+    ref = np.exp(z - z.max(1, keepdims=True))
+    ref /= ref.sum(1, keepdims=True)
+    np.testing.assert_allclose(m.run_cpu(X), ref, rtol=1e-4, atol=1e-6)
+
+
+def test_narrow_network_needs_no_workspace():
+    C = sca.native()
+    narrow = C.mlp_model(random_dense_stack([13, 37, 19, 3], ["relu", "relu", "identity"]), 1)
+    assert not any(C.mlp_layerwise(narrow, r) for r in (1, 16, 256, 4096))
+    assert C.mlp_workspace_bytes(narrow, 4096) == 0
 
 
 # ------------------------------------------------------------------ GPU
