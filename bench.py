@@ -14,29 +14,49 @@ through the native HTTP/1.1 front end, and drives it with the native
 closed-loop load generator (256 concurrent users per rank, no think time, the
 locust REST payload shape).  Weak scaling: per-GPU load is fixed as N grows.
 
+Launch: ``python bench.py --gpus N`` spawns N rank processes itself (fresh
+processes, before anything touches a GPU); under ``torch.distributed.run`` the
+ranks come from the environment and ``--gpus`` must equal ``WORLD_SIZE``.
+
 A "step" is ``--step-requests`` completed predictions per rank.  W warmup steps
 run untimed; K steps are timed between a barrier + device synchronize on both
 sides; ms_per_step is the max over ranks; ``value`` is the whole-job
-predictions/s.  ``--api grpc`` measures the gRPC front end instead
-(``seldon.protos.Seldon/Predict``, Tensor [3,2]-style payload).
+predictions/s.
+
+After the timed headline (never inside it) every rank:
+
+* checks a sample of responses, sent through the same front end, against a CPU
+  oracle (scikit-learn for iris, the host tree walker for xgboost) and exits
+  non-zero on a mismatch;
+* measures the gRPC API (``seldon.protos.Seldon/Predict``, Tensor payload);
+* with N >= 2, measures BASELINE.json's multi-GPU graph configs with their
+  nodes placed on distinct GPUs of the rank's GPU group: ``abtest`` (RANDOM_ABTEST
+  over 2 model replicas on 2 GPUs), ``pipeline`` (transformer -> combiner over 2
+  models, 4 GPUs, N >= 4) and ``mab`` (epsilon-greedy router over one replica per
+  GPU of the job, with concurrent feedback traffic so the bandit learns), each
+  self-checked the same way and reporting its per-GPU batch counts.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
+import threading
 import time
+import urllib.request
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 REST_BASELINE = 12088.95
 GRPC_BASELINE = 28256.39
+VARIANT_SPAN = {"abtest": 2, "pipeline": 4}  # GPUs a variant's graph spans (mab: all of the job's)
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -50,11 +70,48 @@ def parse_args():
     ap.add_argument("--slots", type=int, default=4, help="GPU batches in flight per unit")
     ap.add_argument("--no-spin", action="store_true", help="block on events instead of spinning")
     ap.add_argument("--graph", choices=["single", "abtest", "pipeline", "mab"], default="single",
-                    help="graph shape (single = the headline single-model graph)")
-    ap.add_argument("--extra-grpc", action="store_true", help="also report the gRPC API (untimed extra)")
-    return ap.parse_args()
+                    help="graph of the timed region (single = the headline single-model graph)")
+    ap.add_argument("--extras", choices=["auto", "none"], default="auto",
+                    help="after the timed region: gRPC + multi-GPU graph variants (auto) or nothing")
+    ap.add_argument("--extra-steps", type=int, default=2, help="steps per extra measurement")
+    ap.add_argument("--extra-grpc", action="store_true", help="(kept for old command lines; gRPC is an auto extra)")
+    return ap.parse_args(argv)
 
 
+# ------------------------------------------------------------------ launch
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Direct launch with --gpus N: start N fresh rank processes (no GPU has
+    been touched in this one) and exit with the first failing rank's code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    pending = set(range(n))
+    while pending:
+        for r in list(pending):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            pending.discard(r)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # a failed rank would leave the others in a collective
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ------------------------------------------------------------------ sizing
 def cpu_budget() -> float:
     """CPUs this process may use: cgroup v2 quota (cpu.max) or affinity."""
     try:
@@ -69,7 +126,7 @@ def cpu_budget() -> float:
         return float(os.cpu_count() or 8)
 
 
-def size_threads(args, local_world: int) -> None:
+def size_threads(args, local_world: int) -> float:
     """Split the CPU share of one rank between the front end (~60%), the
     closed-loop load generator (~32%) and the GPU device thread (measured on
     a 16-CPU MI355X share: 10 front-end / 5 generator threads was the best
@@ -79,36 +136,105 @@ def size_threads(args, local_world: int) -> None:
         args.server_threads = max(1, min(16, int(round(per_rank * 0.6))))
     if args.client_threads is None:
         args.client_threads = max(1, min(10, int(round(per_rank * 0.32))))
+    return per_rank
 
 
-def build_deployment(model: str, device: int, graph_kind: str = "single", slots: int = 4, spin: bool = True):
-    import numpy as np  # noqa: F401
+# ------------------------------------------------------------------ graphs
+class Workload:
+    """The benchmark model: component, payload row, names and a CPU oracle."""
+
+    def __init__(self, model: str):
+        from seldon_core_amd.servers import SKLearnServer, XGBoostServer
+
+        self.model = model
+        if model == "iris":
+            from seldon_core_amd.models import iris_logistic_regression
+
+            self.clf = iris_logistic_regression()
+            self.comp = SKLearnServer(model=self.clf)
+            self.names = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
+            self.row = [5.1, 3.5, 1.4, 0.2]
+            self.label = "sklearn-iris-LogisticRegression (linear_softmax HIP kernel, fp64)"
+            self.impl = "SKLEARN_SERVER"
+        else:
+            from seldon_core_amd.models import synthetic_xgboost
+
+            self.ens = synthetic_xgboost(1000, 8, 32, seed=0)
+            self.comp = XGBoostServer(ensemble=self.ens)
+            self.names = [f"f{i}" for i in range(32)]
+            self.row = [0.1 * ((i * 7) % 13 - 6) for i in range(32)]
+            self.label = "xgboost-1000trees-depth8 regressor (tree_perfect HIP kernel, random-init)"
+            self.impl = "XGBOOST_SERVER"
+
+    def oracle(self, X):
+        import numpy as np
+
+        if self.model == "iris":
+            return self.clf.predict_proba(X)
+        return np.asarray(self.ens.predict(X), dtype=np.float64).reshape(len(X), -1)
+
+    def sample(self, n: int, seed: int):
+        import numpy as np
+
+        rng = np.random.default_rng(seed)
+        base = np.asarray(self.row)
+        return base + rng.normal(scale=0.5, size=(n, len(base)))
+
+
+def group_devices(rank: int, span: int, ngpu: int):
+    """GPUs of a variant graph on `rank`: the rank's group of `span` GPUs,
+    rotated so the graph's first node sits on the rank's own GPU."""
+    if ngpu <= 0:
+        return [-1] * span
+    base = (rank // span) * span
+    return [(base + (rank + i) % span) % ngpu for i in range(span)]
+
+
+def build_graph(wl: Workload, kind: str, devs):
+    """SeldonDeployment graph + components for one graph kind on devices `devs`."""
+    import numpy as np
 
     import seldon_core_amd as sca
-    from seldon_core_amd.servers import SKLearnServer, XGBoostServer
+    from seldon_core_amd.models import to_row_model
 
-    if model == "iris":
-        from seldon_core_amd.models import iris_logistic_regression
+    if kind == "single":
+        g = {"name": "classifier", "type": "MODEL", "implementation": wl.impl, "modelUri": "memory://bench",
+             "children": [], "device": devs[0]}
+        return g, {"classifier": wl.comp}, wl.oracle, wl.label
+    C = sca.native()
+    rm_a = wl.comp.row_model() if hasattr(wl.comp, "row_model") else to_row_model(wl.comp)
+    if kind == "abtest":  # seldon-abtest: RANDOM_ABTEST router over 2 model replicas on 2 GPUs
+        g = {"name": "ab", "type": "ROUTER", "implementation": "RANDOM_ABTEST", "device": devs[0],
+             "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
+             "children": [{"name": "a", "type": "MODEL", "device": devs[0]},
+                          {"name": "b", "type": "MODEL", "device": devs[1]}]}
+        return g, {"a": rm_a, "b": rm_a.clone()}, wl.oracle, f"RANDOM_ABTEST(2 replicas on GPUs {devs[:2]})"
+    if kind == "pipeline":  # transformer -> combiner over 2 models, one stage per GPU (device graph)
+        F = len(wl.row)
+        scale = 1.0 + 0.01 * np.random.default_rng(0).random(F)
+        tr = C.linear_model(np.diag(scale), np.zeros(F), 0)  # standard-scaler-style affine transform
+        g = {"name": "scaler", "type": "TRANSFORMER", "device": devs[0], "children": [
+            {"name": "combiner", "type": "COMBINER", "implementation": "AVERAGE_COMBINER", "device": devs[3],
+             "children": [{"name": "a", "type": "MODEL", "device": devs[1]},
+                          {"name": "b", "type": "MODEL", "device": devs[2]}]}]}
+        return (g, {"scaler": tr, "a": rm_a, "b": rm_a.clone()}, lambda X: wl.oracle(np.asarray(X) * scale),
+                f"TRANSFORMER->COMBINER(2 models) device graph on GPUs {devs[:4]}")
+    if kind == "mab":  # epsilon-greedy router over one model replica per GPU
+        from seldon_core_amd.components.routers import EpsilonGreedy
 
-        comp = SKLearnServer(model=iris_logistic_regression())
-        names = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
-        row = [5.1, 3.5, 1.4, 0.2]
-        label = "sklearn-iris-LogisticRegression (linear_softmax HIP kernel, fp64)"
-    else:
-        from seldon_core_amd.models import synthetic_xgboost
+        n = len(devs)
+        kids = [{"name": f"m{i}", "type": "MODEL", "device": devs[i]} for i in range(n)]
+        comps = {f"m{i}": (rm_a if i == 0 else rm_a.clone()) for i in range(n)}
+        comps["mab"] = EpsilonGreedy(n_branches=n, epsilon=0.1, seed=1)
+        g = {"name": "mab", "type": "ROUTER", "device": devs[0], "children": kids}
+        return g, comps, wl.oracle, f"EPSILON_GREEDY router over {n} replicas on GPUs {devs}"
+    raise ValueError(kind)
 
-        ens = synthetic_xgboost(1000, 8, 32, seed=0)
-        comp = XGBoostServer(ensemble=ens)
-        names = [f"f{i}" for i in range(32)]
-        row = [0.1 * ((i * 7) % 13 - 6) for i in range(32)]
-        label = "xgboost-1000trees-depth8 regressor (tree_perfect HIP kernel, random-init)"
-    impl = "SKLEARN_SERVER" if model == "iris" else "XGBOOST_SERVER"
-    graph = {"name": "classifier", "type": "MODEL", "implementation": impl,
-             "modelUri": "memory://bench", "children": [], "device": device}
-    comps = {"classifier": comp}
-    if graph_kind != "single":
-        graph, comps, glabel = _graph_variant(graph_kind, comp, model, device, len(row))
-        label = f"{glabel} [{label}]"
+
+def make_deployment(wl: Workload, kind: str, devs, device: int, slots: int, spin: bool):
+    import seldon_core_amd as sca
+
+    graph, comps, oracle, label = build_graph(wl, kind, devs)
     spec = {"apiVersion": "machinelearning.seldon.io/v1alpha2", "kind": "SeldonDeployment",
             "metadata": {"name": "bench"},
             "spec": {"name": "bench", "predictors": [{
@@ -116,61 +242,23 @@ def build_deployment(model: str, device: int, graph_kind: str = "single", slots:
                 "graph": graph}]}}
     dep = sca.Deployment(spec, components=comps, device=device,
                          batcher={"max_batch": 4096, "slots": slots, "spin_wait": spin})
-    return dep, names, row, label
+    return dep, oracle, label
 
 
-def _graph_variant(kind: str, comp, model: str, device: int, n_features: int):
-    """Multi-node graphs of BASELINE.json's other configs (extra measurements,
-    not the headline): GPU placement spreads nodes over the visible GPUs."""
-    import numpy as np
-
-    import seldon_core_amd as sca
-    from seldon_core_amd.models import to_row_model
-
-    C = sca.native()
-    ngpu = max(1, sca.gpu_count()) if device >= 0 else 1
-    dev = (lambda i: (device + i) % ngpu) if device >= 0 else (lambda i: -1)
-    rm_a = comp.row_model() if hasattr(comp, "row_model") else to_row_model(comp)
-    rm_b = rm_a.clone()
-    if kind == "abtest":  # seldon-abtest: RANDOM_ABTEST router over 2 model replicas on 2 GPUs
-        g = {"name": "ab", "type": "ROUTER", "implementation": "RANDOM_ABTEST", "device": dev(0),
-             "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
-             "children": [{"name": "a", "type": "MODEL", "device": dev(0)},
-                          {"name": "b", "type": "MODEL", "device": dev(1)}]}
-        return g, {"a": rm_a, "b": rm_b}, "RANDOM_ABTEST(2 replicas)"
-    if kind == "pipeline":  # transformer -> combiner over 2 models, one stage per GPU (device graph)
-        rng = np.random.default_rng(0)
-        scale = np.diag(1.0 + 0.01 * rng.random(n_features))
-        tr = C.linear_model(scale, np.zeros(n_features), 0)  # standard-scaler-style affine transform
-        g = {"name": "scaler", "type": "TRANSFORMER", "device": dev(0), "children": [
-            {"name": "combiner", "type": "COMBINER", "implementation": "AVERAGE_COMBINER", "device": dev(3),
-             "children": [{"name": "a", "type": "MODEL", "device": dev(1)},
-                          {"name": "b", "type": "MODEL", "device": dev(2)}]}]}
-        return g, {"scaler": tr, "a": rm_a, "b": rm_b}, "TRANSFORMER->COMBINER(2 models) device graph"
-    if kind == "mab":  # epsilon-greedy router over one model replica per GPU
-        from seldon_core_amd.components.routers import EpsilonGreedy
-
-        n = max(2, ngpu)
-        kids = [{"name": f"m{i}", "type": "MODEL", "device": dev(i)} for i in range(n)]
-        comps = {f"m{i}": (rm_a if i == 0 else rm_a.clone()) for i in range(n)}
-        comps["mab"] = EpsilonGreedy(n_branches=n, epsilon=0.1, seed=1)
-        g = {"name": "mab", "type": "ROUTER", "device": dev(0), "children": kids}
-        return g, comps, f"EPSILON_GREEDY router over {n} replicas"
-    raise ValueError(kind)
-
-
-def run_loadgen(args, port: int, steps: int, warmup: int, api: str, body: bytes | str) -> dict:
+# ------------------------------------------------------------------ load
+def run_loadgen(args, port: int, steps: int, warmup: int, api: str, body, path: str = "/api/v0.1/predictions",
+                users: int | None = None, step_requests: int | None = None, threads: int | None = None) -> dict:
     lg = os.path.join(ROOT, "seldon_core_amd", "bin", "sca_loadgen")
-    cmd = [lg, "--host", "127.0.0.1", "--port", str(port), "--users", str(args.users),
-           "--threads", str(args.client_threads), "--steps", str(steps), "--warmup", str(warmup),
-           "--step-requests", str(args.step_requests)]
+    cmd = [lg, "--host", "127.0.0.1", "--port", str(port), "--users", str(users or args.users),
+           "--threads", str(threads or args.client_threads), "--steps", str(steps), "--warmup", str(warmup),
+           "--step-requests", str(step_requests or args.step_requests)]
     if api == "rest":
-        cmd += ["--mode", "rest", "--path", "/api/v0.1/predictions", "--body", body]
+        cmd += ["--mode", "rest", "--path", path, "--body", body]
     else:
-        path = f"/tmp/sca_bench_req_{os.getpid()}.pb"
-        with open(path, "wb") as f:
+        bpath = f"/tmp/sca_bench_req_{os.getpid()}.pb"
+        with open(bpath, "wb") as f:
             f.write(body)
-        cmd += ["--mode", "grpc", "--path", "/seldon.protos.Seldon/Predict", "--body-file", path,
+        cmd += ["--mode", "grpc", "--path", "/seldon.protos.Seldon/Predict", "--body-file", bpath,
                 "--streams-per-conn", "8"]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
     if res.returncode not in (0, 1) or not res.stdout.strip():
@@ -181,113 +269,284 @@ def run_loadgen(args, port: int, steps: int, warmup: int, api: str, body: bytes 
     return out
 
 
-def main() -> None:
-    args = parse_args()
-    import torch
+def self_check(port: int, wl: Workload, oracle, seed: int, n: int = 24) -> dict:
+    """Send distinct rows through the REST front end (one-row requests and one
+    batch) and compare with the CPU oracle."""
+    import numpy as np
 
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    has_gpu = torch.cuda.is_available()
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # noqa: F811
+    X = wl.sample(n, seed)
+    got = []
 
-        if has_gpu:
-            torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl" if has_gpu else "gloo")
-    device = local_rank if has_gpu else -1
+    def post(rows):
+        body = json.dumps({"data": {"names": wl.names, "ndarray": rows.tolist()}}).encode()
+        req = urllib.request.Request(f"http://127.0.0.1:{port}/api/v0.1/predictions", data=body,
+                                     headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=30) as r:
+            out = np.asarray(json.loads(r.read())["data"]["ndarray"], dtype=np.float64)
+            return out.reshape(len(rows), -1)  # regressors answer one flat value per row
 
-    def barrier():
-        if dist is not None:
-            if has_gpu:
-                dist.barrier(device_ids=[local_rank])
+    for i in range(n // 2):
+        got.append(post(X[i:i + 1]))
+    got.append(post(X[n // 2:]))
+    got = np.vstack(got)
+    ref = np.asarray(oracle(X), dtype=np.float64).reshape(got.shape)
+    err = float(np.abs(got - ref).max())
+    tol = 1e-9 if wl.model == "iris" else 1e-4 * max(1.0, float(np.abs(ref).max()))
+    return {"rows": n, "max_abs_err": err, "tol": tol, "ok": bool(err <= tol)}
+
+
+def unit_stats(dep) -> dict:
+    per_dev: dict = {}
+    total = {"batches": 0, "rows": 0, "gpu_busy_s": 0.0}
+    for name, st in dep.batcher_stats().items():
+        if not isinstance(st, dict):
+            continue
+        for k in total:
+            total[k] += st.get(k, 0)
+        entries = st.get("per_device") or [{"device": st.get("device", -1), "batches": st.get("batches", 0),
+                                            "rows": st.get("rows", 0)}]
+        for e in entries:
+            d = per_dev.setdefault(str(e["device"]), {"batches": 0, "rows": 0, "units": []})
+            d["batches"] += e["batches"]
+            d["rows"] += e["rows"]
+            d["units"].append(name)
+    total["per_device"] = per_dev
+    return total
+
+
+class Dist:
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_world = int(os.environ.get("LOCAL_WORLD_SIZE", self.world))
+        import torch
+
+        self.torch = torch
+        self.has_gpu = torch.cuda.is_available()
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            if self.has_gpu:
+                torch.cuda.set_device(self.local_rank)
+            dist.init_process_group(backend="nccl" if self.has_gpu else "gloo")
+            self.dist = dist
+        self.device = self.local_rank if self.has_gpu else -1
+
+    def barrier(self):
+        if self.dist is not None:
+            if self.has_gpu:
+                self.dist.barrier(device_ids=[self.local_rank])
             else:
-                dist.barrier()
+                self.dist.barrier()
 
-    def sync():
-        if has_gpu:
-            torch.cuda.synchronize()
+    def sync(self):
+        if self.has_gpu:
+            self.torch.cuda.synchronize()
 
-    size_threads(args, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
-    dep, names, row, label = build_deployment(args.model, device, args.graph, args.slots, not args.no_spin)
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def timed(d: Dist, fn):
+    d.barrier()
+    d.sync()
+    t0 = time.perf_counter()
+    out = fn()
+    d.sync()
+    d.barrier()
+    return out, time.perf_counter() - t0
+
+
+def measure_variant(args, d: Dist, wl: Workload, kind: str, spin: bool) -> dict:
+    """One multi-GPU graph config, untimed by the driver contract but timed the
+    same way (barrier + sync around the loadgen window, max over ranks)."""
+    import seldon_core_amd as sca
+
+    ngpu = sca.gpu_count() if d.has_gpu else 0
+    span = max(2, d.world) if kind == "mab" else VARIANT_SPAN[kind]
+    devs = group_devices(d.rank, span, ngpu)
+    dep, oracle, label = make_deployment(wl, kind, devs, d.device, args.slots, spin)
+    h = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
+    body = json.dumps({"data": {"names": wl.names, "ndarray": [wl.row]}})
+    sreq = max(1000, args.step_requests // 2)
+    fb = None
+    try:
+        run_loadgen(args, h.http_port, 1, 0, "rest", body, step_requests=sreq)  # warm every replica
+        for u in dep.batched.values():
+            u.reset_stats()
+        fb_out = {}
+        if kind == "mab":
+            # feedback traffic next to the predictions (reference MAB loadtest:
+            # util/loadtester/scripts/predict_rest_locust.py sends feedback):
+            # branch 0 is rewarded, so the bandit must keep routing to it.
+            fbody = json.dumps({"request": {"data": {"names": wl.names, "ndarray": [wl.row]}},
+                                "response": {"meta": {"routing": {"mab": 0}}, "data": {"ndarray": [[0.0]]}},
+                                "reward": 1.0})
+            fb = threading.Thread(target=lambda: fb_out.update(run_loadgen(
+                args, h.http_port, args.extra_steps, 0, "rest", fbody, path="/api/v0.1/feedback",
+                users=max(4, args.users // 16), step_requests=max(200, sreq // 16),
+                threads=max(1, args.client_threads // 4))))
+            fb.start()
+        lg, wall = timed(d, lambda: run_loadgen(args, h.http_port, args.extra_steps, 0, "rest", body,
+                                                step_requests=sreq))
+        if fb is not None:
+            fb.join()
+        check = self_check(h.http_port, wl, oracle, seed=100 + d.rank)
+        st = unit_stats(dep)
+        res = {"ok": lg["ok"], "wall": wall, "p50": lg["p50_ms"], "p99": lg["p99_ms"], "check": check,
+               "devices": devs, "label": label, "stats": st}
+        if fb_out:
+            res["feedback_rps"] = fb_out.get("rps")
+            routed = {k: v["rows"] for k, v in st["per_device"].items()}
+            res["rows_per_device"] = routed
+        return res
+    finally:
+        h.stop()
+        dep.close()
+
+
+def main() -> None:
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, argv))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        sys.exit(2)
+
+    d = Dist()
+    per_rank_cpus = size_threads(args, d.local_world)
+    spin = not args.no_spin
+    import seldon_core_amd as sca
+
+    wl = Workload(args.model)
+    ngpu = sca.gpu_count() if d.has_gpu else 0
+    devs = [d.device] if args.graph == "single" else group_devices(
+        d.rank, max(2, d.world) if args.graph == "mab" else VARIANT_SPAN[args.graph], ngpu)
+    dep, oracle, label = make_deployment(wl, args.graph, devs, d.device, args.slots, spin)
+    if args.graph != "single":
+        label = f"{label} [{wl.label}]"
     handle = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
-    payload = json.dumps({"data": {"names": names, "ndarray": [row]}})
     C = dep.C
+    payload = json.dumps({"data": {"names": wl.names, "ndarray": [wl.row]}})
+    pb = C.json_to_pb(json.dumps({"data": {"names": wl.names,
+                                           "tensor": {"shape": [1, len(wl.row)], "values": wl.row}}}))
     if args.api == "rest":
         body, port = payload, handle.http_port
     else:
-        body, port = C.json_to_pb(json.dumps({"data": {"names": names, "tensor": {"shape": [1, len(row)],
-                                                                                   "values": row}}})), handle.grpc_port
-    # warmup (untimed)
-    if args.warmup > 0:
+        body, port = pb, handle.grpc_port
+    if args.warmup > 0:  # untimed
         run_loadgen(args, port, args.warmup, 0, args.api, body)
     for u in dep.batched.values():
         u.reset_stats()
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    lg = run_loadgen(args, port, args.steps, 0, args.api, body)
-    sync()
-    barrier()
-    t1 = time.perf_counter()
-    wall = t1 - t0
-    stats = {k: v.stats() for k, v in dep.batched.items()}
-    mine = {"ok": lg["ok"], "wall": wall, "rps": lg["ok"] / wall, "p50": lg["p50_ms"], "p99": lg["p99_ms"],
-            "p90": lg["p90_ms"], "lg_rps": lg["rps"], "batch": stats}
-    extra = None
-    if args.extra_grpc and args.api == "rest":
-        gbody = C.json_to_pb(json.dumps({"data": {"names": names, "tensor": {"shape": [1, len(row)], "values": row}}}))
-        g = run_loadgen(args, handle.grpc_port, max(2, args.steps // 2), 1, "grpc", gbody)
-        extra = {"rps": g["rps"], "p50": g["p50_ms"], "p99": g["p99_ms"]}
-    results = [mine]
-    extras = [extra]
-    if dist is not None:
-        results = [None] * world
-        dist.all_gather_object(results, mine)
-        extras = [None] * world
-        dist.all_gather_object(extras, extra)
+    lg, wall = timed(d, lambda: run_loadgen(args, port, args.steps, 0, args.api, body))
+    st = unit_stats(dep)
+    mine = {"rank": d.rank, "device": d.device, "ok": lg["ok"], "wall": wall, "p50": lg["p50_ms"],
+            "p99": lg["p99_ms"], "stats": st, "cpu_budget": round(per_rank_cpus, 2)}
+    extras: dict = {}
+    failures = []
+    # ---- after the timed region: correctness + extra configs
+    chk = self_check(handle.http_port, wl, oracle, seed=d.rank)
+    mine["check"] = chk
+    if not chk["ok"]:
+        failures.append(f"rank {d.rank} headline self-check: {chk}")
+    if args.extras == "auto" and args.graph == "single":
+        g, gwall = timed(d, lambda: run_loadgen(args, handle.grpc_port, args.extra_steps, 0, "grpc", pb))
+        extras["grpc"] = {"ok": g["ok"], "wall": gwall, "p50": g["p50_ms"], "p99": g["p99_ms"]}
     handle.stop()
     dep.close()
-    if rank == 0:
-        # whole-job throughput: every rank's completed predictions over the
-        # slowest rank's timed window
-        wall_max = max(r["wall"] for r in results)
-        value = sum(r["ok"] for r in results) / wall_max
-        ms_per_step = wall_max / args.steps * 1000.0
-        base = REST_BASELINE if args.api == "rest" else GRPC_BASELINE
-        batch = next(iter(results[0]["batch"].values()), {}) if results[0]["batch"] else {}
-        mean_rows = batch.get("rows", 0) / max(1, batch.get("batches", 1))
-        line = {
-            "metric": "predictions/sec (%s graph, %s)" % ("single-model" if args.graph == "single" else args.graph,
-                                                          args.api.upper()),
-            "value": round(value, 2), "unit": "predictions/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": round(value / base, 3), "dtype": "fp64",
-            "data": ("synthetic (locust-shaped JSON payload, iris feature row); model fit on sklearn's bundled iris"
-                     if args.model == "iris" else
-                     f"synthetic (locust-shaped JSON payload, {len(row)}-feature random row); random-init model"),
-            "p50_ms": round(max(r["p50"] for r in results), 4), "p99_ms": round(max(r["p99"] for r in results), 4),
-            "baseline": {"rest_rps": REST_BASELINE, "rest_p50_ms": 4, "rest_p99_ms": 69, "grpc_rps": GRPC_BASELINE,
-                         "grpc_p50_ms": 1, "grpc_p99_ms": 6},
-            "config": {"model": label, "global_batch": args.users * world, "seq_len": len(row),
-                       "parallelism": f"dp{world}", "graph": args.graph, "api": args.api,
-                       "users_per_gpu": args.users, "requests_per_step_per_gpu": args.step_requests,
-                       "device": "gpu" if has_gpu else "cpu", "gpu_batches": batch.get("batches", 0),
-                       "mean_rows_per_gpu_batch": round(mean_rows, 2),
-                       "gpu_busy_frac_per_slot": round(batch.get("gpu_busy_s", 0.0) /
-                                                       max(1e-9, results[0]["wall"] * args.slots), 3),
-                       "slots": args.slots, "server_threads": args.server_threads,
-                       "client_threads": args.client_threads, "host_cpus": os.cpu_count(),
-                       "cpu_budget": round(cpu_budget(), 2)},
+    if args.extras == "auto" and args.graph == "single" and d.world >= 2:
+        kinds = ["abtest"] + (["pipeline"] if d.world >= 4 else []) + ["mab"]
+        for kind in kinds:
+            r = measure_variant(args, d, wl, kind, spin=False)
+            if not r["check"]["ok"]:
+                failures.append(f"rank {d.rank} {kind} self-check: {r['check']}")
+            extras[kind] = r
+    results = d.gather({"mine": mine, "extras": extras, "failures": failures})
+    if d.rank == 0:
+        print(json.dumps(summarize(args, d, results, label, wl)), flush=True)
+    bad = [f for r in results for f in r["failures"]]
+    d.close()
+    if bad:
+        print("bench.py: self-check FAILED: " + "; ".join(bad), file=sys.stderr)
+        sys.exit(3)
+
+
+def summarize(args, d: Dist, results, label: str, wl: Workload) -> dict:
+    mines = [r["mine"] for r in results]
+    # whole-job throughput: every rank's completed predictions over the
+    # slowest rank's timed window
+    wall_max = max(m["wall"] for m in mines)
+    value = sum(m["ok"] for m in mines) / wall_max
+    base = REST_BASELINE if args.api == "rest" else GRPC_BASELINE
+    st0 = mines[0]["stats"]
+    per_rank = [{"rank": m["rank"], "device": m["device"], "cpu_budget": m["cpu_budget"],
+                 "rps": round(m["ok"] / m["wall"], 1), "p50_ms": m["p50"], "p99_ms": m["p99"],
+                 "gpu_batches": m["stats"]["batches"],
+                 "mean_rows_per_batch": round(m["stats"]["rows"] / max(1, m["stats"]["batches"]), 2),
+                 "check_max_abs_err": m["check"]["max_abs_err"]} for m in mines]
+    line = {
+        "metric": "predictions/sec (%s graph, %s)" % ("single-model" if args.graph == "single" else args.graph,
+                                                      args.api.upper()),
+        "value": round(value, 2), "unit": "predictions/s", "n_gpus": d.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1000.0, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": round(value / base, 3), "dtype": "fp64",
+        "data": ("synthetic (locust-shaped JSON payload, iris feature row); model fit on sklearn's bundled iris"
+                 if args.model == "iris" else
+                 f"synthetic (locust-shaped JSON payload, {len(wl.row)}-feature random row); random-init model"),
+        "p50_ms": round(max(m["p50"] for m in mines), 4), "p99_ms": round(max(m["p99"] for m in mines), 4),
+        "baseline": {"rest_rps": REST_BASELINE, "rest_p50_ms": 4, "rest_p99_ms": 69, "grpc_rps": GRPC_BASELINE,
+                     "grpc_p50_ms": 1, "grpc_p99_ms": 6},
+        "self_check": {"ok": all(m["check"]["ok"] for m in mines),
+                       "max_abs_err": max(m["check"]["max_abs_err"] for m in mines)},
+        "config": {"model": label, "global_batch": args.users * d.world, "seq_len": len(wl.row),
+                   "parallelism": f"dp{d.world}", "graph": args.graph, "api": args.api,
+                   "users_per_gpu": args.users, "requests_per_step_per_gpu": args.step_requests,
+                   "device": "gpu" if d.has_gpu else "cpu", "gpu_batches": st0["batches"],
+                   "mean_rows_per_gpu_batch": round(st0["rows"] / max(1, st0["batches"]), 2),
+                   "gpu_busy_frac_per_slot": round(st0["gpu_busy_s"] / max(1e-9, mines[0]["wall"] * args.slots), 3),
+                   "slots": args.slots, "server_threads": args.server_threads,
+                   "client_threads": args.client_threads, "host_cpus": os.cpu_count(),
+                   "cpu_budget": round(cpu_budget(), 2), "per_rank": per_rank},
+    }
+    ex = [r["extras"] for r in results]
+    if ex[0].get("grpc"):
+        gw = max(e["grpc"]["wall"] for e in ex)
+        g = sum(e["grpc"]["ok"] for e in ex) / gw
+        line["grpc"] = {"value": round(g, 2), "vs_baseline": round(g / GRPC_BASELINE, 3),
+                        "p50_ms": max(e["grpc"]["p50"] for e in ex), "p99_ms": max(e["grpc"]["p99"] for e in ex)}
+    variants = {}
+    for kind in ("abtest", "pipeline", "mab"):
+        if kind not in ex[0]:
+            continue
+        rs = [e[kind] for e in ex]
+        w = max(r["wall"] for r in rs)
+        v = sum(r["ok"] for r in rs) / w
+        variants[kind] = {
+            "graph": rs[0]["label"], "gpus_per_graph": len(rs[0]["devices"]), "n_gpus": d.world,
+            "value": round(v, 2), "unit": "predictions/s", "vs_rest_baseline": round(v / REST_BASELINE, 3),
+            "p50_ms": max(r["p50"] for r in rs), "p99_ms": max(r["p99"] for r in rs),
+            "self_check": {"ok": all(r["check"]["ok"] for r in rs),
+                           "max_abs_err": max(r["check"]["max_abs_err"] for r in rs)},
+            "rank0_batches_per_device": {k: v2["batches"] for k, v2 in rs[0]["stats"]["per_device"].items()},
         }
-        if extras[0] is not None:
-            g_rps = sum(e["rps"] for e in extras if e)
-            line["grpc"] = {"value": round(g_rps, 2), "vs_baseline": round(g_rps / GRPC_BASELINE, 3),
-                            "p50_ms": max(e["p50"] for e in extras if e), "p99_ms": max(e["p99"] for e in extras if e)}
-        print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        if "feedback_rps" in rs[0]:
+            variants[kind]["feedback_rps"] = round(sum(r.get("feedback_rps") or 0 for r in rs), 1)
+            variants[kind]["rank0_rows_per_device"] = rs[0].get("rows_per_device")
+    if variants:
+        line["variants"] = variants
+    return line
 
 
 if __name__ == "__main__":

@@ -333,6 +333,7 @@ PYBIND11_MODULE(_C, m) {
         d["requests"] = s.requests;
         d["max_rows"] = s.max_rows;
         d["gpu_busy_s"] = s.gpu_busy_s;
+        d["device"] = u.options().device;
         return d;
       })
       .def("reset_stats", &gpu::BatchedUnit::reset_stats)
@@ -365,6 +366,16 @@ PYBIND11_MODULE(_C, m) {
         d["max_rows"] = mx;
         d["gpu_busy_s"] = busy;
         d["per_replica"] = u.requests_per_replica();
+        py::list per_dev;
+        for (const auto& rep : u.replicas()) {
+          auto s = rep->stats();
+          py::dict e;
+          e["device"] = rep->options().device;
+          e["batches"] = s.batches;
+          e["rows"] = s.rows;
+          per_dev.append(e);
+        }
+        d["per_device"] = per_dev;
         return d;
       })
       .def("reset_stats", [](gpu::ReplicaUnit& u) {

@@ -32,45 +32,34 @@ __device__ __forceinline__ bool go_left(float x, float thr, int32_t feat, int cm
   return cmp_le ? (x <= thr) : (x < thr);
 }
 
-template <int D>
-__device__ __forceinline__ int descend_fixed(const TreeNode* __restrict__ tn, const float* __restrict__ xs,
-                                             int cmp_le) {
-  int idx = 0;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    const TreeNode nd = tn[idx];
-    const float x = xs[nd.feat & 0x7fffffff];
-    idx = 2 * idx + (go_left(x, nd.thr, nd.feat, cmp_le) ? 1 : 2);
-  }
-  return idx;
+// Feature-major LDS tile: feature f of tile row r lives at tile[f * RB + r]
+// (RB = rows per block, a power of two; lrb = log2 RB).  A ds_read_b32 banks
+// on (addr / 4) % 32 per 32-lane half, and the lanes of a half read 32
+// different rows, so a level's reads hit 32 distinct banks whatever feature
+// each lane's node tests.  (A row-major tile with F = 32 folded every lane
+// onto one bank at the root and stayed 2..32-way below it: 92.9% of LDS
+// cycles were bank conflicts, profiles/r01l_pmc.)
+__device__ __forceinline__ float tile_x(const float* xs, int32_t feat, int lrb) {
+  return xs[(feat & 0x7fffffff) << lrb];
 }
 
-__device__ __forceinline__ int descend_any(const TreeNode* __restrict__ tn, const float* __restrict__ xs, int D,
-                                           int cmp_le) {
-  int idx = 0;
-  for (int d = 0; d < D; ++d) {
-    const TreeNode nd = tn[idx];
-    const float x = xs[nd.feat & 0x7fffffff];
-    idx = 2 * idx + (go_left(x, nd.thr, nd.feat, cmp_le) ? 1 : 2);
-  }
-  return idx;
-}
-
-// Stage the RB x F feature tile (fp64 -> fp32) into LDS; rows past `rows`
-// are zero-filled so every thread can traverse unconditionally.  Loads are
-// issued kU at a time into registers before any LDS write, so the tile costs
-// one memory round trip, not one per loop trip.
+// Stage the RB x F feature tile (fp64 -> fp32) into LDS, feature-major.
+// Consecutive threads take consecutive rows of one feature, so the LDS
+// writes are consecutive addresses (conflict-free); rows past `rows` are
+// zero-filled so every thread can traverse unconditionally.  Loads are issued
+// kU at a time into registers before any LDS write (one round trip).
 __device__ __forceinline__ void stage_tile(float* tile, const double* __restrict__ X, int row0, int rows, int RB,
-                                           int F) {
+                                           int lrb, int F) {
   constexpr int kU = 8;
-  const int n = RB * F, valid = (rows - row0) * F;  // elements of real rows
+  const int n = RB * F, nrow = min(RB, rows - row0);
   for (int i0 = threadIdx.x; i0 < n; i0 += kBlock * kU) {
     double v[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {  // branch-free: clamped address, select after the load
-      const int i = i0 + u * kBlock;
-      const double x = X[size_t(row0) * F + min(i, valid - 1)];
-      v[u] = i < valid ? x : 0.0;
+      const int i = min(i0 + u * kBlock, n - 1);
+      const int r = i & (RB - 1), f = i >> lrb;
+      const double x = X[size_t(row0 + min(r, nrow - 1)) * F + f];
+      v[u] = r < nrow ? x : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -78,6 +67,54 @@ __device__ __forceinline__ void stage_tile(float* tile, const double* __restrict
       if (i < n) tile[i] = float(v[u]);
     }
   }
+}
+
+// U perfect-tree descents interleaved: the U node loads of a level are
+// independent, so a lane keeps U L2 (or LDS) round trips in flight instead of
+// one.  The descent is a chain of D dependent loads per tree -- at 4096 rows x
+// 1000 trees x depth 8 a lane walking its 8 trees one after the other spent
+// 85% of its cycles waiting on that chain (profiles/r02a_tree).  Invalid
+// slots (past the chunk end) walk tree t0 and contribute 0.
+template <int D, int U, bool STAGED>
+__device__ __forceinline__ float descend_perfect(const TreeNode* __restrict__ nodes, const float* __restrict__ leaves,
+                                                 int n_internal, int depth, int t, int t1, int tstride, int tfirst,
+                                                 const float* xs, int lrb, const double* __restrict__ xg, int cmp_le) {
+  const TreeNode* tn[U];
+  const float* lf[U];
+  bool ok[U];
+  int idx[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int tu = t + u * tstride;
+    ok[u] = tu < t1;
+    const int tt = ok[u] ? tu : tfirst;
+    tn[u] = nodes + size_t(tt) * n_internal;
+    lf[u] = leaves + size_t(tt) * (n_internal + 1);
+    idx[u] = 0;
+  }
+  auto level = [&]() {
+    TreeNode nd[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) nd[u] = tn[u][idx[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float x = STAGED ? tile_x(xs, nd[u].feat, lrb) : float(xg[nd[u].feat & 0x7fffffff]);
+      idx[u] = 2 * idx[u] + (go_left(x, nd[u].thr, nd[u].feat, cmp_le) ? 1 : 2);
+    }
+  };
+  if constexpr (D > 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) level();
+  } else {
+    for (int d = 0; d < depth; ++d) level();
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float v = lf[u][idx[u] - n_internal];
+    acc += ok[u] ? v : 0.f;
+  }
+  return acc;
 }
 
 // Contiguous global -> LDS copy with gfx950 direct-to-LDS loads
@@ -242,48 +279,39 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
                                                           int lds_trees, TreeReduceArgs red) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* red_lds = lds;        // [kBlock]
-  float* tile = lds + kBlock;  // [RB * F] when staged
+  float* tile = lds + kBlock;  // [F][RB] when staged
   const int tile_floats = stage_lds ? ((RB * F + 3) & ~3) : 0;
   const int n_internal = (1 << depth) - 1;
   TreeNode* s_nodes = reinterpret_cast<TreeNode*>(lds + kBlock + tile_floats);  // [lds_trees][n_internal]
   float* s_leaves = reinterpret_cast<float*>(reinterpret_cast<char*>(s_nodes) +
                                             ((size_t(lds_trees) * n_internal * sizeof(TreeNode) + 15) & ~size_t(15)));
+  const int lrb = __builtin_ctz(unsigned(RB));
   const int row0 = blockIdx.x * RB;
   const int chunk = blockIdx.y;
   const int r_local = threadIdx.x & (RB - 1);
-  const int slot = threadIdx.x / RB;
-  const int tpr = kBlock / RB;
+  const int slot = threadIdx.x >> lrb;
+  const int tpr = kBlock >> lrb;
   const int t0 = chunk_begin[chunk], t1 = chunk_begin[chunk + 1];
   if constexpr (TREES_LDS) {  // issued first: in flight while the feature tile loads
     copy_to_lds(s_nodes, nodes + size_t(t0) * n_internal, (t1 - t0) * n_internal * int(sizeof(TreeNode)));
     copy_to_lds(s_leaves, leaves + size_t(t0) * (n_internal + 1), (t1 - t0) * (n_internal + 1) * int(sizeof(float)));
   }
-  if (stage_lds) stage_tile(tile, X, row0, rows, RB, F);
+  if (stage_lds) stage_tile(tile, X, row0, rows, RB, lrb, F);
   if constexpr (TREES_LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (stage_lds || TREES_LDS) __syncthreads();
-  const float* xs = stage_lds ? tile + r_local * F : nullptr;
-  float acc = 0.f;
+  const float* xs = tile + r_local;
   const bool row_ok = row0 + r_local < rows;
-  if (stage_lds || row_ok) {
-    for (int t = t0 + slot; t < t1; t += tpr) {
-      const TreeNode* tn = TREES_LDS ? s_nodes + size_t(t - t0) * n_internal : nodes + size_t(t) * n_internal;
-      int idx;
-      if (stage_lds) {
-        idx = D > 0 ? descend_fixed<D>(tn, xs, cmp_le) : descend_any(tn, xs, depth, cmp_le);
-      } else {
-        // Wide feature vectors: read fp64 features straight from global.
-        const double* xg = X + size_t(row0 + r_local) * F;
-        idx = 0;
-        for (int d = 0; d < depth; ++d) {
-          const TreeNode nd = tn[idx];
-          const float x = float(xg[nd.feat & 0x7fffffff]);
-          idx = 2 * idx + (go_left(x, nd.thr, nd.feat, cmp_le) ? 1 : 2);
-        }
-      }
-      const float* lf = TREES_LDS ? s_leaves + size_t(t - t0) * (n_internal + 1)
-                                  : leaves + size_t(t) * (n_internal + 1);
-      acc += lf[idx - n_internal];
-    }
+  const double* xg = X + size_t(min(row0 + r_local, rows - 1)) * F;
+  const TreeNode* nbase = TREES_LDS ? s_nodes - size_t(t0) * n_internal : nodes;
+  const float* lbase = TREES_LDS ? s_leaves - size_t(t0) * (n_internal + 1) : leaves;
+  constexpr int U = 4;
+  float acc = 0.f;
+  if (stage_lds) {
+    for (int t = t0 + slot; t < t1; t += tpr * U)
+      acc += descend_perfect<D, U, true>(nbase, lbase, n_internal, depth, t, t1, tpr, t0, xs, lrb, xg, cmp_le);
+  } else if (row_ok) {  // wide feature vectors: fp64 features straight from global
+    for (int t = t0 + slot; t < t1; t += tpr * U)
+      acc += descend_perfect<D, U, false>(nbase, lbase, n_internal, depth, t, t1, tpr, t0, xs, lrb, xg, cmp_le);
   }
   if (!row_ok) acc = 0.f;
   if (stage_lds) __syncthreads();  // tile no longer needed; `red` is disjoint anyway
@@ -291,6 +319,8 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
   if constexpr (FUSED) fused_tail(partial, rows, n_chunks, red);
 }
 
+// Sparse (pointer) trees: U descents interleaved as above; each runs until it
+// reaches a leaf (left < 0), the others idle through the remaining trips.
 template <bool FUSED>
 __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restrict__ X, int rows, int F,
                                                          const SparseNode* __restrict__ nodes,
@@ -301,33 +331,48 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* red_lds = lds;
   float* tile = lds + kBlock;
+  const int lrb = __builtin_ctz(unsigned(RB));
   const int row0 = blockIdx.x * RB;
   const int chunk = blockIdx.y;
   const int r_local = threadIdx.x & (RB - 1);
-  const int slot = threadIdx.x / RB;
-  const int tpr = kBlock / RB;
+  const int slot = threadIdx.x >> lrb;
+  const int tpr = kBlock >> lrb;
   if (stage_lds) {
-    stage_tile(tile, X, row0, rows, RB, F);
+    stage_tile(tile, X, row0, rows, RB, lrb, F);
     __syncthreads();
   }
   const bool row_ok = row0 + r_local < rows;
   const int t0 = chunk_begin[chunk], t1 = chunk_begin[chunk + 1];
+  constexpr int U = 4;
   float acc = 0.f;
   if (row_ok) {
-    const float* xs = tile + r_local * F;
+    const float* xs = tile + r_local;
     const double* xg = X + size_t(row0 + r_local) * F;
-    for (int t = t0 + slot; t < t1; t += tpr) {
-      int i = tree_root[t];
-      SparseNode nd = nodes[i];
-      int guard = 0;
-      while (nd.left >= 0 && guard < 4096) {
-        const int f = nd.feat & 0x7fffffff;
-        const float x = stage_lds ? xs[f] : float(xg[f]);
-        i = go_left(x, nd.thr, nd.feat, cmp_le) ? nd.left : nd.right;
-        nd = nodes[i];
-        ++guard;
+    for (int t = t0 + slot; t < t1; t += tpr * U) {
+      SparseNode nd[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ok[u] = t + u * tpr < t1;
+        nd[u] = nodes[tree_root[ok[u] ? t + u * tpr : t0]];
       }
-      acc += nd.thr;
+      for (int guard = 0; guard < 4096; ++guard) {
+        bool any = false;
+        int nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool inner = nd[u].left >= 0;
+          any |= inner;
+          const float x = stage_lds ? tile_x(xs, nd[u].feat, lrb) : float(xg[nd[u].feat & 0x7fffffff]);
+          nxt[u] = inner ? (go_left(x, nd[u].thr, nd[u].feat, cmp_le) ? nd[u].left : nd[u].right) : -1;
+        }
+        if (!any) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (nxt[u] >= 0) nd[u] = nodes[nxt[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += ok[u] ? nd[u].thr : 0.f;
     }
   }
   if (stage_lds) __syncthreads();
