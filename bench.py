@@ -62,7 +62,12 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--api", choices=["rest", "grpc"], default="rest")
-    ap.add_argument("--model", choices=["iris", "xgb1000"], default="iris")
+    ap.add_argument("--model", choices=["iris", "xgb1000", "python-iris", "python-noop"], default="iris",
+                    help="iris/xgb1000: prepackaged servers on HIP kernels; python-*: user Python classes "
+                         "(the reference's wrapper-microservice workload)")
+    ap.add_argument("--py-batching", type=int, default=4096,
+                    help="python-* models: stack concurrent requests up to this many rows (0 = off)")
+    ap.add_argument("--py-workers", type=int, default=0, help="python-* models: worker processes (0 = in-process)")
     ap.add_argument("--users", type=int, default=256, help="concurrent clients per GPU")
     ap.add_argument("--step-requests", type=int, default=40000, help="predictions per step per GPU")
     ap.add_argument("--server-threads", type=int, default=None, help="default: sized from the CPU quota per rank")
@@ -156,6 +161,19 @@ class Workload:
             self.row = [5.1, 3.5, 1.4, 0.2]
             self.label = "sklearn-iris-LogisticRegression (linear_softmax HIP kernel, fp64)"
             self.impl = "SKLEARN_SERVER"
+        elif model in ("python-iris", "python-noop"):
+            from seldon_core_amd.components.examples import EchoModel, IrisClassifier
+
+            self.names = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
+            self.row = [5.1, 3.5, 1.4, 0.2]
+            if model == "python-iris":
+                self.comp = IrisClassifier()
+                self.clf = self.comp.model
+                self.label = "user Python class IrisClassifier (sklearn LogisticRegression.predict_proba)"
+            else:
+                self.comp = EchoModel()
+                self.label = "user Python class EchoModel (no-op predict)"
+            self.impl = None
         else:
             from seldon_core_amd.models import synthetic_xgboost
 
@@ -169,8 +187,10 @@ class Workload:
     def oracle(self, X):
         import numpy as np
 
-        if self.model == "iris":
+        if self.model in ("iris", "python-iris"):
             return self.clf.predict_proba(X)
+        if self.model == "python-noop":
+            return np.asarray(X, dtype=np.float64)
         return np.asarray(self.ens.predict(X), dtype=np.float64).reshape(len(X), -1)
 
     def sample(self, n: int, seed: int):
@@ -198,9 +218,15 @@ def build_graph(wl: Workload, kind: str, devs):
     from seldon_core_amd.models import to_row_model
 
     if kind == "single":
-        g = {"name": "classifier", "type": "MODEL", "implementation": wl.impl, "modelUri": "memory://bench",
-             "children": [], "device": devs[0]}
-        return g, {"classifier": wl.comp}, wl.oracle, wl.label
+        g = {"name": "classifier", "type": "MODEL", "children": [], "device": devs[0]}
+        if wl.impl:
+            g.update(implementation=wl.impl, modelUri="memory://bench")
+        else:  # a user Python class
+            g.update(batching=wl.py_batching, workers=wl.py_workers)
+        label = wl.label
+        if not wl.impl:
+            label += f" [batching={wl.py_batching}, workers={wl.py_workers}]"
+        return g, {"classifier": wl.comp}, wl.oracle, label
     C = sca.native()
     rm_a = wl.comp.row_model() if hasattr(wl.comp, "row_model") else to_row_model(wl.comp)
     if kind == "abtest":  # seldon-abtest: RANDOM_ABTEST router over 2 model replicas on 2 GPUs
@@ -291,7 +317,7 @@ def self_check(port: int, wl: Workload, oracle, seed: int, n: int = 24) -> dict:
     got = np.vstack(got)
     ref = np.asarray(oracle(X), dtype=np.float64).reshape(got.shape)
     err = float(np.abs(got - ref).max())
-    tol = 1e-9 if wl.model == "iris" else 1e-4 * max(1.0, float(np.abs(ref).max()))
+    tol = 1e-4 * max(1.0, float(np.abs(ref).max())) if wl.model == "xgb1000" else 1e-9
     return {"rows": n, "max_abs_err": err, "tol": tol, "ok": bool(err <= tol)}
 
 
@@ -431,11 +457,14 @@ def main() -> None:
     import seldon_core_amd as sca
 
     wl = Workload(args.model)
+    wl.py_batching, wl.py_workers = args.py_batching, args.py_workers
     ngpu = sca.gpu_count() if d.has_gpu else 0
     devs = [d.device] if args.graph == "single" else group_devices(
         d.rank, max(2, d.world) if args.graph == "mab" else VARIANT_SPAN[args.graph], ngpu)
     dep, oracle, label = make_deployment(wl, args.graph, devs, d.device, args.slots, spin)
     if args.graph != "single":
+        if not wl.impl:
+            raise SystemExit("multi-node --graph variants use the kernel models (iris / xgb1000)")
         label = f"{label} [{wl.label}]"
     handle = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
     C = dep.C
@@ -466,7 +495,7 @@ def main() -> None:
         extras["grpc"] = {"ok": g["ok"], "wall": gwall, "p50": g["p50_ms"], "p99": g["p99_ms"]}
     handle.stop()
     dep.close()
-    if args.extras == "auto" and args.graph == "single" and d.world >= 2:
+    if args.extras == "auto" and args.graph == "single" and d.world >= 2 and wl.impl:
         kinds = ["abtest"] + (["pipeline"] if d.world >= 4 else []) + ["mab"]
         for kind in kinds:
             r = measure_variant(args, d, wl, kind, spin=False)
@@ -503,7 +532,7 @@ def summarize(args, d: Dist, results, label: str, wl: Workload) -> dict:
         "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1000.0, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": round(value / base, 3), "dtype": "fp64",
         "data": ("synthetic (locust-shaped JSON payload, iris feature row); model fit on sklearn's bundled iris"
-                 if args.model == "iris" else
+                 if args.model in ("iris", "python-iris", "python-noop") else
                  f"synthetic (locust-shaped JSON payload, {len(wl.row)}-feature random row); random-init model"),
         "p50_ms": round(max(m["p50"] for m in mines), 4), "p99_ms": round(max(m["p99"] for m in mines), 4),
         "baseline": {"rest_rps": REST_BASELINE, "rest_p50_ms": 4, "rest_p99_ms": 69, "grpc_rps": GRPC_BASELINE,

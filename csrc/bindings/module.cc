@@ -279,6 +279,22 @@ PYBIND11_MODULE(_C, m) {
       .def("snapshot", [](const Unit& u) { return py::bytes(u.snapshot()); })
       .def("restore", [](Unit& u, const py::bytes& b) { u.restore(std::string(b)); });
 
+  py::class_<PyUnit, Unit, std::shared_ptr<PyUnit>>(m, "PyUnit")
+      .def("stop", &PyUnit::stop)
+      .def("stats", [](const PyUnit& u) {
+        auto s = u.stats();
+        py::dict d;
+        d["jobs"] = s.jobs;
+        d["calls"] = s.calls;
+        d["rows"] = s.rows;
+        d["batched_calls"] = s.batched_calls;
+        d["pool_calls"] = s.pool_calls;
+        d["workers"] = u.options().worker_fds.size();
+        d["alive_workers"] = u.alive_workers();
+        d["batch_rows"] = u.options().batch_rows;
+        return d;
+      });
+
   py::class_<gpu::BatchedUnit, Unit, std::shared_ptr<gpu::BatchedUnit>>(m, "BatchedUnit")
       .def(py::init([](std::shared_ptr<gpu::RowModel> model, int device, int max_batch, int max_wait_us, int slots,
                        bool zero_copy, size_t zc_bytes, bool spin, bool cpu_batching, int fail_threshold,
@@ -471,10 +487,17 @@ PYBIND11_MODULE(_C, m) {
       .def("add_header_route", &Engine::add_header_route, py::arg("name"), py::arg("value"), py::arg("regex"),
            py::arg("target"))
       .def("bind_python",
-           [](Engine& e, const std::string& node, py::object adapter, uint32_t builtin_methods) {
-             e.bind(node, std::make_shared<PyUnit>(std::move(adapter), builtin_methods));
+           [](Engine& e, const std::string& node, py::object adapter, uint32_t builtin_methods, int batch_rows,
+              std::vector<int> worker_fds) {
+             PyUnitOptions o;
+             o.batch_rows = batch_rows;
+             o.worker_fds = std::move(worker_fds);
+             auto u = std::make_shared<PyUnit>(std::move(adapter), builtin_methods, std::move(o));
+             e.bind(node, u);
+             return u;
            },
-           py::arg("node"), py::arg("adapter"), py::arg("builtin_methods") = 0)
+           py::arg("node"), py::arg("adapter"), py::arg("builtin_methods") = 0, py::arg("batch_rows") = 0,
+           py::arg("worker_fds") = std::vector<int>{})
       .def("bind_batched", [](Engine& e, const std::string& node,
                               std::shared_ptr<gpu::BatchedUnit> u) { e.bind(node, u); })
       .def("bind_unit", [](Engine& e, const std::string& node, std::shared_ptr<Unit> u) { e.bind(node, u); })

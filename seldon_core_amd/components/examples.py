@@ -169,3 +169,29 @@ class ImageNetOutputTransformer:
             result = np.asarray(data.get("ndarray"), dtype=float)
         result = np.reshape(result, (1, self.classes))
         return {"strData": self.cnames[int(np.argmax(result[0]))]}
+
+
+class IrisClassifier:
+    """The reference's user-class example (examples/models/sklearn_iris/
+    IrisClassifier.py:3-10): a plain Python class whose ``predict`` calls a
+    scikit-learn LogisticRegression.  It stays a *Python* component (the
+    wrapper-microservice workload), unlike ``SKLearnServer`` which compiles the
+    model to a kernel.  ``model`` defaults to the iris fit from sklearn's
+    bundled dataset (no joblib file or network needed)."""
+
+    def __init__(self, model=None):
+        if model is None:
+            from ..models import iris_logistic_regression
+
+            model = iris_logistic_regression()
+        self.model = model
+
+    def predict(self, X, features_names):
+        return self.model.predict_proba(X)
+
+
+class EchoModel:
+    """No-op user component: returns its input (Python-runtime overhead probe)."""
+
+    def predict(self, X, features_names):
+        return X

@@ -4,7 +4,7 @@ python/seldon_core/microservice.py:177-322).
     python -m seldon_core_amd.microservice <Interface> REST|GRPC \
         [--service-type MODEL|ROUTER|TRANSFORMER|COMBINER|OUTLIER_DETECTOR] \
         [--persistence] [--parameters '<json list>'] [--log-level INFO] \
-        [--tracing] [--workers N]
+        [--tracing] [--workers N] [--batching ROWS]
 
 The user class is imported exactly as the reference does (``Module`` ->
 ``Module.Module``, ``pkg.mod.Class`` -> ``pkg.mod.Class``), built from the
@@ -79,8 +79,11 @@ def import_user_class(interface_name: str):
     return getattr(mod, parts[1])
 
 
-def build_microservice(user_object: Any, service_type: str = "MODEL", name: str = None, device: int = None):
-    """A one-node deployment wrapping the component (graph-equivalent)."""
+def build_microservice(user_object: Any, service_type: str = "MODEL", name: str = None, device: int = None,
+                       workers: int = 0, batching: int = 0):
+    """A one-node deployment wrapping the component (graph-equivalent).
+    ``workers`` > 0 runs the component in that many worker processes (the
+    reference's gunicorn workers); ``batching`` stacks concurrent requests."""
     from .serving.deployment import Deployment
 
     name = name or os.environ.get("PREDICTIVE_UNIT_ID", "model")
@@ -91,6 +94,10 @@ def build_microservice(user_object: Any, service_type: str = "MODEL", name: str 
         spec["graph"] = {"name": name, "type": "UNKNOWN_TYPE", "methods": ["ROUTE", "SEND_FEEDBACK"]}
     elif node_type == "COMBINER":
         spec["graph"] = {"name": name, "type": "UNKNOWN_TYPE", "methods": ["AGGREGATE"]}
+    if workers > 0:
+        spec["graph"]["workers"] = int(workers)
+    if batching > 0:
+        spec["graph"]["batching"] = int(batching)
     return Deployment(spec, components={name: user_object}, device=device)
 
 
@@ -108,7 +115,10 @@ def main(argv=None) -> None:
     ap.add_argument("--log-level", type=str, default="INFO")
     ap.add_argument("--tracing", nargs="?", default=int(os.environ.get("TRACING", "0")), const=1, type=int)
     ap.add_argument("--workers", type=int, default=int(os.environ.get("GUNICORN_WORKERS", "4")),
-                    help="native front-end I/O threads")
+                    help="component worker processes when > 1 (the reference's gunicorn workers); "
+                         "the native front end uses max(workers, 4) I/O threads")
+    ap.add_argument("--batching", type=int, default=int(os.environ.get("SELDON_BATCHING", "0")),
+                    help="stack concurrent requests to a row-wise component, up to this many rows (0 = off)")
     ap.add_argument("--port", type=int, default=int(os.environ.get(SERVICE_PORT_ENV_NAME, DEFAULT_PORT)))
     ap.add_argument("--device", type=int, default=None, help="GPU for native units (-1 = CPU)")
     args = ap.parse_args(argv)
@@ -141,18 +151,25 @@ def main(argv=None) -> None:
 
         configure_tracing(args.interface_name)
 
-    dep = build_microservice(user_object, args.service_type, device=args.device)
+    workers = args.workers if args.workers > 1 else 0
+    if workers and args.persistence:
+        logger.warning("--persistence keeps one copy of the component: running it in-process, not in %d workers",
+                       workers)
+        workers = 0
+    dep = build_microservice(user_object, args.service_type, device=args.device, workers=workers,
+                             batching=args.batching)
+    io_threads = max(args.workers, 4)
     node = dep.predictor["graph"]["name"]
     from .serving.openapi import wrapper_spec_json
 
     if args.api_type == "REST":
-        http = dep.C.HttpServer(dep.engine, "0.0.0.0", [args.port], args.workers, node, True, wrapper_spec_json())
+        http = dep.C.HttpServer(dep.engine, "0.0.0.0", [args.port], io_threads, node, True, wrapper_spec_json())
         http.start()
         servers = [http]
         logger.info("REST microservice running on port %i", http.ports[0])
     else:
         max_msg = int(annotations.get("seldon.io/grpc-max-message-size", 64 << 20))
-        grpc = dep.C.GrpcServer(dep.engine, "0.0.0.0", args.port, args.workers, node, max_msg)
+        grpc = dep.C.GrpcServer(dep.engine, "0.0.0.0", args.port, io_threads, node, max_msg)
         grpc.start()
         servers = [grpc]
         logger.info("GRPC microservice running on port %i", grpc.port)

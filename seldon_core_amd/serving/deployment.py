@@ -24,6 +24,7 @@ from __future__ import annotations
 import importlib
 import json
 import logging
+import pickle
 import os
 from typing import Any, Dict, Optional, Union
 
@@ -96,6 +97,7 @@ class Deployment:
         self.engine = self.C.Engine(json.dumps(self.predictor), self.deployment_name, "",
                                     share_metrics_with=_metrics_from, **ekw)
         self.units: Dict[str, Any] = {}
+        self.python_units: Dict[str, PythonUnit] = {}
         self.batched: Dict[str, Any] = {}
         self.native_units: Dict[str, Any] = {}
         self.fused: Dict[str, Any] = {}
@@ -248,8 +250,39 @@ class Deployment:
         if unit_type in (None, "UNKNOWN_TYPE"):
             unit_type = "UNKNOWN_TYPE"
         adapter = PythonUnit(obj, unit_type, node["name"])
-        self.engine.bind_python(node["name"], adapter, 0)
+        batch_rows, workers = self._python_options(node, obj)
+        fds = []
+        if workers > 0:
+            try:
+                fds = adapter.start_pool(workers)
+            except (pickle.PicklingError, TypeError, AttributeError, RuntimeError) as e:
+                logger.warning("node %s: cannot run the component in %d worker processes (%s); serving it in-process",
+                               node["name"], workers, e)
+        adapter.native = self.engine.bind_python(node["name"], adapter, 0, batch_rows, fds)
         self.units[node["name"]] = adapter
+        self.__dict__.setdefault("python_units", {})[node["name"]] = adapter
+
+    def _python_options(self, node: Dict, obj: Any):
+        """(batch_rows, workers) of a Python node.  Precedence: node extension
+        fields ``batching`` / ``workers`` > component attributes
+        ``seldon_batching`` / ``seldon_workers`` > annotations
+        ``seldon.io/python-batching`` / ``seldon.io/python-workers``
+        (the reference's ``--workers`` / GUNICORN_WORKERS)."""
+        ann = self.annotations()
+
+        def pick(field: str, attr: str, key: str):
+            if node.get(field) is not None:
+                return node[field]
+            if getattr(obj, attr, None) is not None:
+                return getattr(obj, attr)
+            return ann.get(key)
+
+        b = pick("batching", "seldon_batching", "seldon.io/python-batching")
+        if isinstance(b, str):
+            b = {"true": 4096, "false": 0}.get(b.lower(), b)
+        batch_rows = 4096 if b is True else int(b or 0)
+        workers = int(pick("workers", "seldon_workers", "seldon.io/python-workers") or 0)
+        return max(0, batch_rows), max(0, workers)
 
     def _instantiate(self, node: Dict, obj: Any) -> Any:
         if isinstance(obj, str):
@@ -492,6 +525,10 @@ class Deployment:
             self._persister = None
         for u in list(self.batched.values()) + list(self.native_units.values()):
             u.stop()
+        for a in getattr(self, "python_units", {}).values():
+            if getattr(a, "native", None) is not None:
+                a.native.stop()  # closes the pool sockets: workers exit on EOF
+            a.stop_pool()
         for p in getattr(self, "peers", {}).values():
             p.close()
         if getattr(self, "_span_exporter", None) is not None:
