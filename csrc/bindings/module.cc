@@ -12,6 +12,7 @@
 #include "../core/msglog.h"
 #include "../gpu/batcher.h"
 #include "../gpu/graph.h"
+#include "../gpu/lstm_model.h"
 #include "../gpu/mlp_model.h"
 #include "../gpu/replica.h"
 #include "../gpu/models.h"
@@ -237,6 +238,46 @@ PYBIND11_MODULE(_C, m) {
     return std::static_pointer_cast<gpu::RowModel>(
         gpu::MlpModel::vae(to_layers(encoder), latent, to_layers(decoder), samples, seed));
   }, py::arg("encoder"), py::arg("latent"), py::arg("decoder"), py::arg("samples") = 10, py::arg("seed") = 0);
+  auto to_lstm = [](py::handle h) {
+    py::dict d = h.cast<py::dict>();
+    auto Wi = d["W_ih"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+    auto Wh = d["W_hh"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+    auto b = d["b"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+    if (Wi.ndim() != 2 || Wh.ndim() != 2) throw std::runtime_error("LSTM W_ih / W_hh must be 2-D [4H, in] / [4H, H]");
+    gpu::LstmWeights w;
+    w.H = int(Wh.shape(1));
+    w.in = int(Wi.shape(1));
+    w.W_ih = to_vec(Wi);
+    w.W_hh = to_vec(Wh);
+    w.b = to_vec(b);
+    return w;
+  };
+  m.def("lstm_seq2seq_model",
+        [to_lstm](int T, int F, py::list enc, py::list dec, py::array_t<float, py::array::c_style | py::array::forcecast> W,
+                  py::array_t<float, py::array::c_style | py::array::forcecast> b, int out_act) {
+          std::vector<std::pair<gpu::LstmWeights, gpu::LstmWeights>> e;
+          for (auto h : enc) {
+            py::sequence pair = h.cast<py::sequence>();
+            if (pair.size() != 2) throw std::runtime_error("encoder layer = (forward, backward)");
+            e.emplace_back(to_lstm(pair[0]), to_lstm(pair[1]));
+          }
+          std::vector<gpu::LstmWeights> d;
+          for (auto h : dec) d.push_back(to_lstm(h));
+          return std::static_pointer_cast<gpu::RowModel>(
+              std::make_shared<gpu::LstmSeqModel>(T, F, std::move(e), std::move(d), to_vec(W), to_vec(b), out_act));
+        },
+        py::arg("T"), py::arg("F"), py::arg("encoder"), py::arg("decoder"), py::arg("dense_W"), py::arg("dense_b"),
+        py::arg("out_act") = 1);
+  m.def("lstm_program", [](std::shared_ptr<gpu::RowModel> m) {
+    auto p = std::dynamic_pointer_cast<gpu::LstmSeqModel>(m);
+    if (!p) throw std::runtime_error("not an LSTM model");
+    const auto& g = p->program();
+    py::dict d;
+    d["w_lds"] = g.w_lds;
+    d["lds_bytes"] = g.lds_floats * 4;
+    d["workspace_floats_per_wg"] = g.seq_ws_floats;
+    return d;
+  });
   m.def("minmax_model", [] { return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MinMaxModel>()); });
   m.def("mean_sigmoid_model", [](double thr) {
     return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MeanSigmoidModel>(thr));

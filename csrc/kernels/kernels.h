@@ -195,4 +195,41 @@ void eg_route(const int32_t* best_branch, int n_branches, float epsilon, uint64_
 void ts_route(const float* alpha, const float* beta, int n_branches, uint64_t seed, uint64_t offset, int n,
               double* branch_out, hipStream_t stream);
 
+// ------------------------------------------------------------------ LSTM
+// Seq2seq LSTM reconstruction error (seq2seq outlier detector, reference
+// components/outlier-detection/seq2seq-lstm/model.py:6-92 and
+// CoreSeq2SeqLSTM.py:107-174): bidirectional LSTM encoder stack, LSTM decoder
+// stack initialised with the concatenated final encoder states, Dense output,
+// T-1 step greedy decode, per-sequence MSE.  One persistent kernel per batch
+// (csrc/kernels/lstm.hip).
+constexpr int kLstmMaxLayers = 4;
+constexpr int kLstmRows = 16;  // sequences per workgroup (one MFMA tile)
+struct LstmCell {              // one direction of one layer
+  int w_off = 0, b_off = 0;    // floats, relative to the phase blob: B fragments [Np/16][Kp/4][64], bias [Np]
+  int in = 0, H = 0, Kp = 0, Np = 0;
+  int lda = 0, ldg = 0;        // LDS strides of its A [16][lda] and gate [16][ldg] buffers
+  int a_off = 0, g_off = 0, c_off = 0;  // LDS offsets (floats) of A, gates, cell state [16][H]
+};
+struct LstmProgram {
+  int T = 0, F = 0, n_enc = 0, n_dec = 0;
+  LstmCell enc[kLstmMaxLayers][2];
+  LstmCell dec[kLstmMaxLayers];
+  long long enc_phase[kLstmMaxLayers] = {};  // global offsets (floats) of each encoder layer's blob
+  int enc_phase_floats[kLstmMaxLayers] = {};
+  long long dec_phase = 0;
+  int dec_phase_floats = 0;
+  int dense_w = 0, dense_b = 0;  // relative to the decoder blob: W fragments [Np/16][Kp/4][64], b [F]
+  int dense_kp = 0, dense_np = 0;
+  int D = 0, out_act = 0;        // decoder top units; 0 linear, 1 sigmoid, 2 tanh, 3 relu
+  int w_lds = 0;                 // stage each phase's weights in LDS
+  int w_region = 0;              // LDS floats reserved for weights (0 when !w_lds)
+  int y_off = 0, mse_off = 0;    // LDS offsets: dense inputs staged, mse [16]
+  int x_lds = 0, x_off = 0;      // input tile [16][T][F] (fp32) staged in LDS when it fits
+  int lds_floats = 0;
+  long long seq_ws_floats = 0;   // per-workgroup global workspace (encoder sequences, ping-pong)
+  int Hmax2 = 0;                 // 2 x widest encoder layer
+};
+void lstm_seq2seq_mse(const double* X, int rows, const LstmProgram& prog, const float* params, float* ws,
+                      double* out, hipStream_t stream);
+
 }  // namespace sca::kern

@@ -467,7 +467,9 @@ def load_vae_weights(path: str) -> Dict:
 class Seq2SeqLSTMNet:
     """BiLSTM encoder (stack), LSTM decoder (stack) initialised with the
     concatenated final encoder states, Dense output (seq2seq-lstm/model.py:6-92).
-    torch-ROCm; weights random-init or a state_dict (safetensors / weights-only)."""
+    Weights live in torch modules (random-init or a state_dict from safetensors);
+    on a GPU the scoring runs as the native MFMA kernel (``native_model``), on
+    the CPU as torch eager."""
 
     def __init__(self, n_features: int, encoder_dim=(20,), decoder_dim=(20,), output_activation="sigmoid",
                  device: int = -1, seed: int = 0):
@@ -491,8 +493,9 @@ class Seq2SeqLSTMNet:
         self.out = nn.Linear(d_in, n_features)
         self.act = {"sigmoid": torch.sigmoid, "linear": lambda t: t, "tanh": torch.tanh,
                     "relu": torch.relu}[output_activation]
+        self.act_name = output_activation
         self.modules = nn.ModuleList([self.enc, self.dec, self.out]).to(self.dev).eval()
-        self._graphs: Dict[tuple, Any] = {}
+        self._units: Dict[int, Any] = {}  # timesteps -> native BatchedUnit (GPU)
 
     def load_state_dict(self, sd):
         self.modules.load_state_dict(sd)
@@ -523,29 +526,56 @@ class Seq2SeqLSTMNet:
         return out
 
     def reconstruct(self, X: np.ndarray) -> np.ndarray:
+        """Greedy T-1 step decode (torch, eager) -- the CPU path and the test
+        oracle of the native kernel."""
         import torch
 
         x = torch.as_tensor(np.ascontiguousarray(X), dtype=torch.float32, device=self.dev)
         with torch.no_grad():
-            if self.dev.type != "cuda":
-                return self._decode(x).double().cpu().numpy()
-            key = tuple(x.shape)
-            g = self._graphs.get(key)
-            if g is None:  # capture the T-step decode once per shape into a HIP graph
-                static_in = x.clone()
-                s = torch.cuda.Stream(self.dev)
-                s.wait_stream(torch.cuda.current_stream(self.dev))
-                with torch.cuda.stream(s):
-                    self._decode(static_in)  # warm-up (MIOpen plans, allocator)
-                torch.cuda.current_stream(self.dev).wait_stream(s)
-                graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
-                    static_out = self._decode(static_in)
-                g = self._graphs[key] = (graph, static_in, static_out)
-            graph, static_in, static_out = g
-            static_in.copy_(x)
-            graph.replay()
-            return static_out.double().cpu().numpy()
+            return self._decode(x).double().cpu().numpy()
+
+    # ------------------------------------------------------------ native
+    _ACTS = {"linear": 0, "sigmoid": 1, "tanh": 2, "relu": 3}
+
+    def native_model(self, timesteps: int):
+        """The same network as a native RowModel: one row = a flattened [T, F]
+        sequence -> its reconstruction MSE, computed on the GPU by one
+        persistent MFMA kernel per batch (csrc/kernels/lstm.hip)."""
+        from .._native import native
+
+        def cell(w_ih, w_hh, b_ih, b_hh):
+            t = lambda v: v.detach().float().cpu().numpy()  # noqa: E731
+            return {"W_ih": t(w_ih), "W_hh": t(w_hh), "b": t(b_ih) + t(b_hh)}
+
+        enc = []
+        for m in self.enc:
+            enc.append((cell(m.weight_ih_l0, m.weight_hh_l0, m.bias_ih_l0, m.bias_hh_l0),
+                        cell(m.weight_ih_l0_reverse, m.weight_hh_l0_reverse, m.bias_ih_l0_reverse,
+                             m.bias_hh_l0_reverse)))
+        dec = [cell(c.weight_ih, c.weight_hh, c.bias_ih, c.bias_hh) for c in self.dec]
+        W = self.out.weight.detach().float().cpu().numpy()
+        b = self.out.bias.detach().float().cpu().numpy()
+        return native().lstm_seq2seq_model(int(timesteps), int(W.shape[0]), enc, dec, W, b,
+                                           self._ACTS[self.act_name])
+
+    def mse(self, X: np.ndarray) -> np.ndarray:
+        """Per-sequence reconstruction MSE of X [B, T, F]."""
+        B, T, F = X.shape
+        if self.dev.type == "cuda":
+            unit = self._units.get(T)
+            if unit is None:
+                from .._native import native
+
+                unit = self._units[T] = native().BatchedUnit(self.native_model(T), self.dev.index or 0,
+                                                             max_batch=4096)
+            return np.asarray(unit.run(np.ascontiguousarray(X, dtype=np.float64).reshape(B, T * F)))[:, 0]
+        rec = self.reconstruct(X)
+        return np.mean((X - rec) ** 2, axis=(1, 2))
+
+    def close(self) -> None:
+        for u in self._units.values():
+            u.stop()
+        self._units = {}
 
 
 @register("SEQ2SEQ_OD")
@@ -585,8 +615,7 @@ class OutlierSeq2SeqLSTM(_FeedbackMetrics, _Reservoir):
             X[:, :, col] = np.clip(X[:, :, col], -c, c)
         self.reservoir_sampling(X, update_stand=self.N >= self.reservoir_size)
         X = self._scale(X)
-        rec = self.net.reconstruct(X)
-        self.mse = np.mean((X - rec) ** 2, axis=(1, 2))
+        self.mse = self.net.mse(X)
         self.prediction = (self.mse > self.threshold).astype(int)
         return self.prediction
 

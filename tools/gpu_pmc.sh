@@ -10,6 +10,7 @@ cd "$ROOT"
 OUT="$ROOT/gpurun_out/pmc"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+export SCA_PMC=1
 ONLY="${ONLY:-tree,vae,mlp,linear}"
 ITERS="${ITERS:-20}"
 

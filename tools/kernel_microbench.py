@@ -263,13 +263,47 @@ def case_linear(iters):
         unit.stop()
 
 
+def case_lstm(iters):
+    """seq2seq LSTM detector (ECG-shaped: T=140, F=1, BiLSTM 20 -> LSTM 40 -> Dense),
+    one persistent kernel per batch, vs the torch eager decode loop."""
+    import torch
+
+    from seldon_core_amd import native
+    from seldon_core_amd.components.outlier import Seq2SeqLSTMNet
+
+    C = native()
+    T, F = 140, 1
+    net = Seq2SeqLSTMNet(F, (20,), (40,), "sigmoid", 0, 0)
+    for rows in (16, 1024):
+        X = np.random.default_rng(3).random((rows, T, F))
+        unit = C.BatchedUnit(net.native_model(T), 0, max_batch=4096)
+        try:
+            got = np.asarray(unit.run(X.reshape(rows, -1)))[:, 0]
+            if os.environ.get("SCA_PMC"):  # counter passes: only the kernel (torch's eager loop floods the trace)
+                ref, torch_us = got, 0.0
+            else:
+                ref = np.mean((X - net.reconstruct(X)) ** 2, axis=(1, 2))
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(3):
+                    net.reconstruct(X)
+                torch.cuda.synchronize()
+                torch_us = (time.perf_counter() - t0) / 3 * 1e6
+            _time_unit("lstm", unit, X.reshape(rows, -1), iters,
+                       {"T": T, "F": F, "enc": 20, "dec": 40, "torch_eager_us": round(torch_us, 1),
+                        "max_rel_err_vs_torch": float(np.max(np.abs(got - ref) / np.abs(ref)))})
+        finally:
+            unit.stop()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="tree,vae,mlp,linear")
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     cases = {"tree": case_tree, "vae": case_vae, "mlp": case_mlp, "linear": case_linear,
-             "mlp_torch": case_mlp_torch, "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes}
+             "mlp_torch": case_mlp_torch, "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes,
+             "lstm": case_lstm}
     for c in a.only.split(","):
         cases[c](a.iters)
 
