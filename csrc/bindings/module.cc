@@ -13,6 +13,7 @@
 #include "../gpu/batcher.h"
 #include "../gpu/graph.h"
 #include "../gpu/lstm_model.h"
+#include "../gpu/maha_device.h"
 #include "../gpu/mlp_model.h"
 #include "../gpu/replica.h"
 #include "../gpu/models.h"
@@ -278,6 +279,26 @@ PYBIND11_MODULE(_C, m) {
     d["workspace_floats_per_wg"] = g.seq_ws_floats;
     return d;
   });
+  py::class_<gpu::MahalanobisDevice, std::shared_ptr<gpu::MahalanobisDevice>>(m, "MahalanobisDevice")
+      .def(py::init<int, int, double, double, double, double, int>(), py::arg("p"), py::arg("k"),
+           py::arg("n_stdev") = 3.0, py::arg("start_clip") = 50.0, py::arg("max_n") = -1.0, py::arg("eps") = 1e-8,
+           py::arg("device") = 0)
+      .def("step", [](gpu::MahalanobisDevice& d, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
+        if (X.ndim() != 2 || X.shape(1) != d.p()) throw std::runtime_error("X must be [rows, p]");
+        std::vector<double> s;
+        {
+          py::gil_scoped_release nogil;
+          s = d.step(X.data(), int(X.shape(0)));
+        }
+        return py::array_t<double>(py::ssize_t(s.size()), s.data());
+      })
+      .def("state", [](const gpu::MahalanobisDevice& d) {
+        auto s = d.state();
+        return py::array_t<double>(py::ssize_t(s.size()), s.data());
+      })
+      .def("set_state", [](gpu::MahalanobisDevice& d, std::vector<double> s) { d.set_state(s); })
+      .def_property_readonly("p", &gpu::MahalanobisDevice::p)
+      .def_property_readonly("k", &gpu::MahalanobisDevice::k);
   m.def("minmax_model", [] { return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MinMaxModel>()); });
   m.def("mean_sigmoid_model", [](double thr) {
     return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MeanSigmoidModel>(thr));

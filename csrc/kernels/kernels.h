@@ -173,6 +173,22 @@ void mlp_mse_finish(const float* mse, int rows, double scale, double* out, hipSt
 
 // Mahalanobis detector: Sherman-Morrison recurrence + scores over a batch
 // (B [nb][k][k], cov0 [k][k], xd [nb][k]); false if k > 16.
+// Whole Mahalanobis detector step on the device (CoreMahalanobis.py:68-151):
+// clip, running mean / covariance update, top-k eigenvectors (parallel cyclic
+// Jacobi in LDS), projections, Sherman-Morrison scores, state update -- one
+// single-workgroup launch per request batch, state resident in HBM.
+constexpr int kMahaMaxP = 64;
+constexpr int kMahaMaxK = 16;
+struct MahaParams {
+  int p = 0, k = 0;
+  double n_stdev = 3.0, start_clip = 50.0, max_n = -1.0, eps = 1e-8;
+};
+// state layout (doubles): mean[p] | C[p*p] | clip_lo[p] | clip_hi[p] | n | c_zero | has_clip
+inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
+// workspace doubles for a batch of nb rows
+inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (3 * size_t(p) + 2 * size_t(k)); }
+void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* ws, double* scores,
+               hipStream_t stream);
 bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd, int nb, int k, double n, double* out,
                            hipStream_t stream);
 

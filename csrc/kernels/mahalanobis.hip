@@ -128,6 +128,296 @@ __global__ __launch_bounds__(64) void maha_sm_kernel(const double* __restrict__ 
   }
 }
 
+
+// ------------------------------------------------------------ full detector step
+// One 256-thread workgroup runs CoreMahalanobis._get_preds (:68-151) for one
+// request batch against the device-resident state.  p <= 64 features, k <= 16
+// components; p x p matrices live in LDS (row stride kLd = 65 doubles).
+constexpr int kT = 256;
+constexpr int kLd = kMahaMaxP + 1;
+constexpr int kMaxSweeps = 40;
+
+__device__ double block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+// Gauss-Jordan with partial pivoting; M and inv are caller-provided (LDS)
+// k x k buffers, so nothing spills to scratch.  Returns det(A).
+__device__ double invert_into(const double* A, double* M, double* inv, int k) {
+  for (int e = 0; e < k * k; ++e) {
+    M[e] = A[e];
+    inv[e] = (e / k == e % k) ? 1.0 : 0.0;
+  }
+  double det = 1.0;
+  for (int c = 0; c < k; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < k; ++r)
+      if (fabs(M[r * k + c]) > fabs(M[piv * k + c])) piv = r;
+    if (M[piv * k + c] == 0.0) return 0.0;
+    if (piv != c) {
+      for (int j = 0; j < k; ++j) {
+        double t = M[c * k + j]; M[c * k + j] = M[piv * k + j]; M[piv * k + j] = t;
+        t = inv[c * k + j]; inv[c * k + j] = inv[piv * k + j]; inv[piv * k + j] = t;
+      }
+      det = -det;
+    }
+    const double d = M[c * k + c];
+    det *= d;
+    const double id = 1.0 / d;
+    for (int j = 0; j < k; ++j) { M[c * k + j] *= id; inv[c * k + j] *= id; }
+    for (int r = 0; r < k; ++r) {
+      if (r == c) continue;
+      const double f = M[r * k + c];
+      if (f == 0.0) continue;
+      for (int j = 0; j < k; ++j) { M[r * k + j] -= f * M[c * k + j]; inv[r * k + j] -= f * inv[c * k + j]; }
+    }
+  }
+  return det;
+}
+
+__global__ __launch_bounds__(kT) void maha_step_kernel(const double* __restrict__ X, int nb, MahaParams prm,
+                                                       double* __restrict__ state, double* __restrict__ ws,
+                                                       double* __restrict__ scores) {
+  __shared__ double Cold[kMahaMaxP * kLd], A[kMahaMaxP * kLd], V[kMahaMaxP * kLd];
+  __shared__ double mean0[kMahaMaxP];
+  __shared__ double rc[kMahaMaxP / 2], rs[kMahaMaxP / 2];
+  __shared__ int rp[kMahaMaxP / 2], rq[kMahaMaxP / 2];
+  __shared__ double red[4];
+  __shared__ int sel[kMahaMaxK];
+  __shared__ double P[kMahaMaxK * kMahaMaxK], Cp[kMahaMaxK * kMahaMaxK], T1[kMahaMaxK * kMahaMaxK],
+      T2[kMahaMaxK * kMahaMaxK];
+  __shared__ int valid, inverted;
+  __shared__ double scal;
+  const int tid = threadIdx.x;
+  const int p = prm.p, k = prm.k, kk = k * k;
+  double* s_mean = state;
+  double* s_C = state + p;
+  double* s_lo = s_C + p * p;
+  double* s_hi = s_lo + p;
+  double* s_tail = s_hi + p;  // n, c_zero, has_clip
+  const double n_state = s_tail[0];
+  const bool c_zero = s_tail[1] != 0.0;
+  const bool do_clip = n_state > prm.start_clip && s_tail[2] != 0.0;
+  const double n = prm.max_n > 0 ? fmin(n_state, prm.max_n) : n_state;
+  double* XC = ws;                          // [nb][p] clipped rows
+  double* MO = XC + size_t(nb) * p;         // [nb][p] means_offset
+  double* D = MO + size_t(nb) * p;          // [nb][p] Xc - means_offset
+  double* DPC = D + size_t(nb) * p;         // [nb][k] projected (Xc - m)
+  double* XD = DPC + size_t(nb) * k;        // [nb][k] projected (X - m)
+
+  for (int e = tid; e < p * p; e += kT) Cold[(e / p) * kLd + e % p] = c_zero ? 0.0 : s_C[e];
+  for (int j = tid; j < p; j += kT) mean0[j] = s_mean[j];
+  __syncthreads();
+
+  // ---- clip + running means (sequential in rows, parallel in features)
+  for (int j = tid; j < p; j += kT) {
+    const double m0 = mean0[j];
+    double cum = 0.0, prev = m0;
+    for (int i = 0; i < nb; ++i) {
+      double x = X[size_t(i) * p + j];
+      if (do_clip) x = fmin(fmax(x, s_lo[j]), s_hi[j]);
+      cum += x;
+      const double roll = cum / double(i + 1);
+      const double nm = m0 + (double(i + 1) / (double(i) + n + 1.0)) * (roll - m0);
+      XC[size_t(i) * p + j] = x;
+      MO[size_t(i) * p + j] = prev;
+      D[size_t(i) * p + j] = x - prev;
+      prev = nm;
+    }
+    s_mean[j] = prev;  // new_means[-1] (mean0 keeps the old value for this step)
+  }
+  __syncthreads();
+
+  // ---- covariance update: cov = (n-1)/(n+max(1,nb-1)) C + 1/(n+max(1,nb-1)) sum_i coef_i d_i d_i^T
+  const double den = n + fmax(1.0, double(nb) - 1.0);
+  for (int e = tid; e < p * p; e += kT) {
+    const int a = e / p, b = e - a * p;
+    double acc = 0.0;
+    for (int i = 0; i < nb; ++i)
+      acc += ((n + i) / (n + i + 1.0)) * (D[size_t(i) * p + a] * D[size_t(i) * p + b]);
+    const double cov = (n - 1.0) / den * Cold[a * kLd + b] + 1.0 / den * acc;
+    A[a * kLd + b] = cov;
+    s_C[e] = cov;
+  }
+  // ---- eigenvectors: parallel cyclic Jacobi (round-robin pairs, m = p rounded up to even)
+  const int m = p + (p & 1);
+  for (int e = tid; e < m * m; e += kT) {
+    const int a = e / m, b = e - a * m;
+    V[a * kLd + b] = a == b ? 1.0 : 0.0;
+    if (a >= p || b >= p) A[a * kLd + b] = 0.0;  // dummy index of an odd p
+  }
+  __syncthreads();
+  const int half = m / 2;
+  for (int sweep = 0; sweep < kMaxSweeps && m > 1; ++sweep) {
+    double off = 0.0, all = 0.0;
+    for (int e = tid; e < m * m; e += kT) {
+      const int a = e / m, b = e - a * m;
+      const double v = A[a * kLd + b];
+      all += v * v;
+      if (a != b) off += v * v;
+    }
+    off = block_sum(off, red);
+    all = block_sum(all, red);
+    if (off <= 1e-30 * all || off == 0.0) break;
+    for (int r = 0; r < m - 1; ++r) {
+      for (int i = tid; i < half; i += kT) {
+        const int a = i == 0 ? 0 : 1 + (i + r) % (m - 1);
+        const int b = 1 + ((i == 0 ? 0 : m - 1 - i) + r) % (m - 1);
+        const int pp = min(a, b), qq = max(a, b);
+        const double app = A[pp * kLd + pp], aqq = A[qq * kLd + qq], apq = A[pp * kLd + qq];
+        double c = 1.0, sn = 0.0;
+        if (apq != 0.0 && fabs(apq) > 1e-18 * (fabs(app) + fabs(aqq))) {
+          const double th = (aqq - app) / (2.0 * apq);
+          const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+          c = 1.0 / sqrt(t * t + 1.0);
+          sn = t * c;
+        }
+        rc[i] = c;
+        rs[i] = sn;
+        rp[i] = pp;
+        rq[i] = qq;
+      }
+      __syncthreads();
+      for (int e = tid; e < m * half; e += kT) {  // columns: A <- A J, V <- V J
+        const int row = e / half, i = e - row * half;
+        const int pp = rp[i], qq = rq[i];
+        const double c = rc[i], sn = rs[i];
+        const double ap = A[row * kLd + pp], aq = A[row * kLd + qq];
+        A[row * kLd + pp] = c * ap - sn * aq;
+        A[row * kLd + qq] = sn * ap + c * aq;
+        const double vp = V[row * kLd + pp], vq = V[row * kLd + qq];
+        V[row * kLd + pp] = c * vp - sn * vq;
+        V[row * kLd + qq] = sn * vp + c * vq;
+      }
+      __syncthreads();
+      for (int e = tid; e < m * half; e += kT) {  // rows: A <- J^T A
+        const int col = e / half, i = e - col * half;
+        const int pp = rp[i], qq = rq[i];
+        const double c = rc[i], sn = rs[i];
+        const double ap = A[pp * kLd + col], aq = A[qq * kLd + col];
+        A[pp * kLd + col] = c * ap - sn * aq;
+        A[qq * kLd + col] = sn * ap + c * aq;
+      }
+      __syncthreads();
+    }
+  }
+  // ---- top-k eigenpairs (any order: the scores are invariant to it)
+  if (tid == 0) {
+    for (int a = 0; a < k; ++a) {
+      int best = -1;
+      for (int j = 0; j < p; ++j) {
+        bool taken = false;
+        for (int b = 0; b < a; ++b) taken |= sel[b] == j;
+        if (!taken && (best < 0 || A[j * kLd + j] > A[best * kLd + best])) best = j;
+      }
+      sel[a] = best;
+    }
+  }
+  __syncthreads();
+  // ---- projections; proj_cov = V^T C_old V
+  for (int e = tid; e < kk; e += kT) {
+    const int a = e / k, b = e - a * k;
+    double acc = 0.0;
+    if (!c_zero)
+      for (int r = 0; r < p; ++r) {
+        double t = 0.0;
+        for (int c = 0; c < p; ++c) t += Cold[r * kLd + c] * V[c * kLd + sel[b]];
+        acc += V[r * kLd + sel[a]] * t;
+      }
+    P[e] = acc;
+  }
+  for (int e = tid; e < nb * k; e += kT) {
+    const int i = e / k, a = e - i * k;
+    const double* v = V + sel[a];
+    double px = 0.0, pxc = 0.0, pm = 0.0;
+    for (int j = 0; j < p; ++j) {
+      const double w = v[j * kLd];
+      px += X[size_t(i) * p + j] * w;
+      pxc += XC[size_t(i) * p + j] * w;
+      pm += MO[size_t(i) * p + j] * w;
+    }
+    DPC[e] = pxc - pm;
+    XD[e] = px - pm;
+  }
+  if (tid == 0) valid = 0;
+  __syncthreads();
+  // ---- Sherman-Morrison scores (sequential in rows)
+  for (int i = 0; i < nb; ++i) {
+    const double* d = XD + size_t(i) * k;
+    if (!valid) {
+      if (tid == 0) {  // Gauss-Jordan in LDS (T1 = working copy of P, T2 = inverse)
+        inverted = 0;
+        const double det = invert_into(P, T1, T2, k);
+        if (fabs(det) > prm.eps) {
+          for (int e = 0; e < kk; ++e) Cp[e] = T2[e];
+          inverted = 1;
+          valid = 1;
+        }
+      }
+      __syncthreads();
+      if (!inverted) {
+        if (n + i != 0.0) {
+          const double a = (n + i - 1.0) / (n + i), cb = 1.0 / (n + i + 1.0);
+          const double* dp = DPC + size_t(i) * k;
+          for (int e = tid; e < kk; e += kT) P[e] = a * P[e] + cb * dp[e / k] * dp[e % k];
+        }
+        if (tid == 0) scores[i] = 0.0;
+        __syncthreads();
+        continue;
+      }
+    } else {
+      const double a = (n + i - 1.0) / (n + i - 2.0), cb = 1.0 / (n + i);  // B_{i-1} = dpc dpc^T / (n + i)
+      const double* dp = DPC + size_t(i - 1) * k;
+      for (int e = tid; e < kk; e += kT) T1[e] = a * Cp[e];
+      __syncthreads();
+      for (int e = tid; e < kk; e += kT) {  // BC1 = B_{i-1} c_inv
+        const int r = e / k, c = e - r * k;
+        double sacc = 0.0;
+        for (int j = 0; j < k; ++j) sacc += (cb * dp[r] * dp[j]) * T1[j * k + c];
+        T2[e] = sacc;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        double tr = 0.0;
+        for (int j = 0; j < k; ++j) tr += T2[j * k + j];
+        scal = 1.0 / (1.0 + tr);
+      }
+      __syncthreads();
+      for (int e = tid; e < kk; e += kT) {
+        const int r = e / k, c = e - r * k;
+        double sacc = 0.0;
+        for (int j = 0; j < k; ++j) sacc += T1[r * k + j] * T2[j * k + c];
+        Cp[e] = T1[e] - scal * sacc;
+      }
+      __syncthreads();
+    }
+    double part = 0.0;
+    for (int e = tid; e < kk; e += kT) part += d[e / k] * Cp[e] * d[e % k];
+    part = block_sum(part, red);
+    if (tid == 0) scores[i] = part;
+    __syncthreads();
+  }
+  // ---- state update: n, clip bounds from the new covariance diagonal
+  const double n_new = n_state + nb;
+  for (int j = tid; j < p; j += kT) {
+    if (n_new > prm.start_clip) {
+      const double sd = sqrt(s_C[j * p + j]);
+      s_lo[j] = s_mean[j] - prm.n_stdev * sd;
+      s_hi[j] = s_mean[j] + prm.n_stdev * sd;
+    }
+  }
+  if (tid == 0) {
+    s_tail[0] = n_new;
+    s_tail[1] = 0.0;
+    if (n_new > prm.start_clip) s_tail[2] = 1.0;
+  }
+}
+
 }  // namespace
 
 bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd, int nb, int k, double n,
@@ -136,6 +426,12 @@ bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd
   if (nb <= 0) return true;
   hipLaunchKernelGGL(maha_sm_kernel, dim3(1), dim3(64), 0, s, B, cov0, xd, nb, k, n, 1e-8, out);
   return true;
+}
+
+void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* ws, double* scores,
+               hipStream_t s) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(maha_step_kernel, dim3(1), dim3(kT), 0, s, X, nb, prm, state, ws, scores);
 }
 
 }  // namespace sca::kern

@@ -4,10 +4,12 @@ scoring on the MI355X:
 
 * ``OutlierMahalanobis`` -- mahalanobis/CoreMahalanobis.py:68-151 (online mean /
   covariance, top-k PCA via ``eigh``, Sherman-Morrison inverse updates,
-  Mahalanobis score).  The state update is inherently sequential per request
-  and tiny (p x p, k x k); it runs in fp64 numpy for exact parity, and the
-  per-row Sherman-Morrison recurrence + quadratic forms run in one HIP kernel
-  (``mahalanobis_sm_scores``) when a batch is large enough to pay for a launch.
+  Mahalanobis score).  On a GPU the state (mean, covariance, clip bounds, n)
+  stays in HBM and each request is one single-workgroup kernel launch that
+  runs the whole step -- clip, running moments, top-k eigenvectors by
+  parallel cyclic Jacobi in LDS, projections, Sherman-Morrison recurrence,
+  state update (``MahalanobisDevice``, csrc/kernels/mahalanobis.hip); on the
+  CPU it is fp64 numpy (the parity oracle).
 * ``OutlierIsolationForest`` -- isolation-forest/CoreIsolationForest.py:62-76:
   ``decision_function < threshold``; the forest runs on the tree-ensemble HIP
   kernel (isolation transform: 2^(-mean path / c(n)) - offset).
@@ -15,14 +17,9 @@ scoring on the MI355X:
   10 MC reconstructions -> row MSE; the whole VAE + MC loop + MSE is one fused
   MFMA kernel launch (csrc/kernels/mlp.hip, ``vae_model``).
 * ``OutlierSeq2SeqLSTM`` -- seq2seq-lstm/CoreSeq2SeqLSTM.py:107-174: BiLSTM
-  encoder, step-by-step LSTM decoder fed its own outputs, row MSE; batched over
-  observations on the GPU with torch-ROCm (MIOpen LSTM) and the fixed-length
-  decode loop captured once per batch size into a HIP graph.
-
-The ``Outlier*`` wrappers' feedback loop (labels via ``send_feedback``,
-confusion matrix + total / rolling accuracy, precision, recall, F1, F2,
-reference vae/OutlierVAE.py:29-116 and utils.py:106-142) is shared in
-:class:`_FeedbackMetrics`.
+  encoder, step-by-step LSTM decoder fed its own outputs, row MSE; on a GPU the
+  whole model + T-1 step decode + MSE is one persistent MFMA kernel per batch
+  (csrc/kernels/lstm.hip), on the CPU torch eager.
 """
 from __future__ import annotations
 
@@ -235,7 +232,7 @@ class OutlierMahalanobis(_FeedbackMetrics):
     _EPSILON = 1e-8
 
     def __init__(self, threshold=25, n_components=3, n_stdev=3, start_clip=50, max_n=-1, device=None,
-                 gpu_min_rows: int = 256):
+                 gpu_min_rows: int = 0):
         self.threshold = threshold
         self.n_components = n_components
         self.max_n = max_n
@@ -247,22 +244,61 @@ class OutlierMahalanobis(_FeedbackMetrics):
         self.n = 0
         self.nb_outliers = 0
         self.device = _default_device(device)
-        self.gpu_min_rows = gpu_min_rows
+        self._dev = None  # native MahalanobisDevice: state resident in HBM (created at the first request)
         self._init_feedback()
 
     def _last_scores(self):
         return self.score
 
+    # ------------------------------------------------------------ device path
+    def _device_for(self, p: int):
+        """The whole _get_preds runs as one kernel launch per request on a GPU
+        (csrc/kernels/mahalanobis.hip: maha_step); p <= 64, k <= 16."""
+        if self.device < 0 or p > 64 or min(self.n_components, p) > 16:
+            return None
+        if self._dev is None or self._dev.p != p:
+            from .._native import native
+
+            self._dev = native().MahalanobisDevice(p, min(self.n_components, p), float(self.n_stdev),
+                                                   float(self.start_clip), float(self.max_n), self._EPSILON,
+                                                   self.device)
+            if self.n:  # state restored / accumulated on the host before the device existed
+                self._push_state(p)
+        return self._dev
+
+    def _push_state(self, p: int) -> None:
+        c_zero = isinstance(self.C, int) and self.C == 0
+        mean = np.broadcast_to(np.asarray(self.mean, float), (p,))
+        C = np.zeros((p, p)) if c_zero else np.asarray(self.C, float)
+        lo, hi = (np.zeros(p), np.zeros(p)) if self.clip is None else (np.asarray(self.clip[0], float),
+                                                                        np.asarray(self.clip[1], float))
+        st = np.concatenate([mean, C.ravel(), lo, hi, [float(self.n), 1.0 if c_zero else 0.0,
+                                                      0.0 if self.clip is None else 1.0]])
+        self._dev.set_state(st.tolist())
+
+    def _pull_state(self) -> None:
+        if self._dev is None:
+            return
+        p = self._dev.p
+        st = np.asarray(self._dev.state())
+        self.mean = st[:p].copy()
+        self.C = 0 if st[-2] != 0 else st[p:p + p * p].reshape(p, p).copy()
+        self.clip = [st[p + p * p:2 * p + p * p].copy(), st[2 * p + p * p:3 * p + p * p].copy()] if st[-1] else None
+        self.n = int(st[-3])
+
+    def state_dict(self):
+        self._pull_state()
+        return super().state_dict()
+
+    def load_state_dict(self, state):
+        super().load_state_dict(state)
+        if self._dev is not None:
+            self._push_state(self._dev.p)
+
     def _sm_scores(self, B, proj_cov, x_diff, n):
         """Sherman-Morrison inverse recurrence over the batch rows + quadratic
-        forms (CoreMahalanobis.py:118-146)."""
+        forms (CoreMahalanobis.py:118-146) -- host path."""
         nb, k = x_diff.shape
-        if self.device >= 0 and nb >= self.gpu_min_rows:
-            from ..ops import mahalanobis_sm_scores
-
-            out = mahalanobis_sm_scores(B, proj_cov, x_diff, n, self.device)
-            if out is not None:
-                return out
         all_C_inv = np.zeros_like(B)
         c_inv = None
         for i, b in enumerate(B):
@@ -281,9 +317,18 @@ class OutlierMahalanobis(_FeedbackMetrics):
         return np.matmul(x_diff[:, None, :], np.matmul(all_C_inv, x_diff[:, :, None])).reshape(nb)
 
     def _get_preds(self, X):
+        X = np.asarray(X, dtype=float)
+        if X.ndim == 2 and self._device_for(X.shape[1]) is not None:
+            self.score = np.asarray(self._dev.step(X))
+            self.n += X.shape[0]
+            self.prediction = (self.score > self.threshold).astype(int)
+            return self.prediction
+        return self._get_preds_host(X)
+
+    def _get_preds_host(self, X):
+        """numpy path (CPU placement; the parity oracle of the device kernel)."""
         from scipy.linalg import eigh
 
-        X = np.asarray(X, dtype=float)
         nb, p = X.shape
         k = min(self.n_components, p)
         n = min(self.n, self.max_n) if self.max_n > 0 else self.n
