@@ -224,9 +224,21 @@ PYBIND11_MODULE(_C, m) {
     }
     return out;
   };
-  m.def("mlp_model", [to_layers](py::list layers, int out_mode) {
-    return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MlpModel>(to_layers(layers), out_mode));
-  }, py::arg("layers"), py::arg("out_mode") = 0);
+  auto prec = [](const std::string& p) {
+    if (p == "fp32" || p == "float32") return 0;
+    if (p == "bf16" || p == "bfloat16") return 1;
+    throw std::runtime_error("precision must be 'fp32' or 'bf16'");
+  };
+  m.def("mlp_model", [to_layers, prec](py::list layers, int out_mode, const std::string& precision) {
+    auto mm = std::make_shared<gpu::MlpModel>(to_layers(layers), out_mode);
+    if (prec(precision)) mm->set_precision(prec(precision));
+    return std::static_pointer_cast<gpu::RowModel>(mm);
+  }, py::arg("layers"), py::arg("out_mode") = 0, py::arg("precision") = "fp32");
+  m.def("mlp_precision", [](std::shared_ptr<gpu::RowModel> m) {
+    auto p = std::dynamic_pointer_cast<gpu::MlpModel>(m);
+    if (!p) throw std::runtime_error("not an MLP model");
+    return std::string(p->precision() ? "bf16" : "fp32");
+  });
   m.def("mlp_layerwise", [](std::shared_ptr<gpu::RowModel> m, int rows) {
     auto p = std::dynamic_pointer_cast<gpu::MlpModel>(m);
     if (!p) throw std::runtime_error("not an MLP model");
@@ -235,10 +247,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("mlp_workspace_bytes", [](std::shared_ptr<gpu::RowModel> m, int rows) {
     return m->workspace_bytes(rows, m->in_cols());
   });
-  m.def("vae_model", [to_layers](py::list encoder, int latent, py::list decoder, int samples, uint64_t seed) {
-    return std::static_pointer_cast<gpu::RowModel>(
-        gpu::MlpModel::vae(to_layers(encoder), latent, to_layers(decoder), samples, seed));
-  }, py::arg("encoder"), py::arg("latent"), py::arg("decoder"), py::arg("samples") = 10, py::arg("seed") = 0);
+  m.def("vae_model", [to_layers, prec](py::list encoder, int latent, py::list decoder, int samples, uint64_t seed,
+                                       const std::string& precision) {
+    auto mm = gpu::MlpModel::vae(to_layers(encoder), latent, to_layers(decoder), samples, seed);
+    if (prec(precision)) mm->set_precision(prec(precision));
+    return std::static_pointer_cast<gpu::RowModel>(mm);
+  }, py::arg("encoder"), py::arg("latent"), py::arg("decoder"), py::arg("samples") = 10, py::arg("seed") = 0,
+     py::arg("precision") = "fp32");
   auto to_lstm = [](py::handle h) {
     py::dict d = h.cast<py::dict>();
     auto Wi = d["W_ih"].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();

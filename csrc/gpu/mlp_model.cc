@@ -12,6 +12,15 @@ namespace {
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 constexpr size_t kSlack = 4 * 16 + 64;  // workspace floats past each buffer (A look-ahead)
+constexpr int kGemmRows = 512;          // rows_eff from which fp32 layers use the register-tiled GEMM
+
+uint16_t to_bf16(float f) {  // round to nearest even
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
 
 // Host twin of kern::Philox (csrc/kernels/philox.h): identical streams, so the
 // CPU reference path draws the same reparameterisation noise as the GPU.
@@ -131,7 +140,22 @@ int MlpModel::add_layer(const DenseLayer& L, int type, int in_buf, int out_buf) 
   op.b_off = (long long)params_.size();
   params_.resize(params_.size() + size_t(op.Np), 0.f);
   for (int nn = 0; nn < L.N; ++nn) params_[size_t(op.b_off) + nn] = L.b[size_t(nn)];
+  op.Kpb = round_up(L.K, 64);
+  op.Npb = round_up(L.N, 64);
+  op.wb_off = (long long)pbf_.size();
+  if (precision_ == 1) {  // bf16 row-major [Npb][Kpb], zero padded (gemm_bf16_lds_kernel)
+    pbf_.resize(pbf_.size() + size_t(op.Npb) * op.Kpb, 0);
+    uint16_t* wb = pbf_.data() + op.wb_off;
+    for (int nn = 0; nn < L.N; ++nn)
+      for (int k = 0; k < L.K; ++k) wb[size_t(nn) * op.Kpb + k] = to_bf16(L.W[size_t(nn) * L.K + k]);
+  }
   return n;
+}
+
+void MlpModel::set_precision(int p) {
+  if (p != 0 && p != 1) throw std::runtime_error("MlpModel: precision must be fp32 (0) or bf16 (1)");
+  precision_ = p;
+  build();
 }
 
 void MlpModel::build() {
@@ -139,6 +163,7 @@ void MlpModel::build() {
     mode_ = !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "layer") ? 2 : 0;
   prog_ = kern::MlpProgram();
   params_.clear();
+  pbf_.clear();
   auto& p = prog_;
   p.F = F_;
   p.Fp = round_up(F_, 16);
@@ -213,13 +238,17 @@ void MlpModel::build() {
   params_.resize(params_.size() + 4 * 64 * 4, 0.f);  // B look-ahead pad (4 blocks, mlp.hip dense())
   // A network whose activations do not fit one workgroup's 160 KiB of LDS
   // cannot use the fused kernel; it runs layer-wise (activations in HBM).
-  fused_ok_ = (size_t(off) + kern::kMlpRows) * sizeof(float) <= 160 * 1024;
-  if (!fused_ok_) mode_ = 2;
+  fused_ok_ = (size_t(off) + kern::kMlpRows) * sizeof(float) <= 160 * 1024 && precision_ == 0;
+  if (!fused_ok_) mode_ = 2;  // bf16 runs on the layer-wise GEMMs only
 }
 
 void MlpModel::to_device(int device) {
   d_params_.alloc(params_.size() * sizeof(float), device);
   d_params_.upload(params_.data(), params_.size() * sizeof(float));
+  if (!pbf_.empty()) {
+    d_pbf_.alloc(pbf_.size() * sizeof(uint16_t) + 64 * 16, device);  // + look-ahead pad
+    d_pbf_.upload(pbf_.data(), pbf_.size() * sizeof(uint16_t));
+  }
 }
 
 // ------------------------------------------------------------ dispatch
@@ -255,6 +284,14 @@ int MlpModel::max_np() const {
 }
 
 size_t MlpModel::workspace_bytes(int max_rows, int) const {
+  if (precision_ == 1) {
+    const size_t R = size_t(round_up(std::max(max_rows, 1), 128)), S = vae_ ? size_t(samples_) : 1;
+    size_t Wb = 64;
+    for (int o = 0; o < prog_.n_pre + prog_.n_loop; ++o) Wb = std::max(Wb, size_t(prog_.ops[o].Npb));
+    const size_t K0 = size_t(prog_.ops[0].Kpb), K0f = size_t(prog_.ops[0].Kp);
+    // [x bf16 R x K0][buf0 bf16 R*S x Wb][buf1 bf16 R*S x Wb][x fp32 R x K0f][head/logits fp32 R x Wb][mse R]
+    return (R * K0 + 2 * R * S * Wb) * 2 + (R * K0f + R * Wb + R) * 4 + 4 * 256;
+  }
   if (mode_ == 1) return 0;
   if (mode_ == 0) {  // auto: only models the cost model ever sends layer-wise need one
     bool any = false;
@@ -271,6 +308,11 @@ size_t MlpModel::workspace_bytes(int max_rows, int) const {
 
 void MlpModel::launch(const double* X, int rows, int, double* out, void* ws, hipStream_t s) {
   const uint64_t off = offset_.fetch_add(1);
+  if (precision_ == 1) {
+    if (!ws) throw std::runtime_error("MlpModel: bf16 network launched without a workspace");
+    launch_layerwise_bf16(X, rows, out, static_cast<char*>(ws), seed_ ^ (off * 0x9E3779B97F4A7C15ULL), s);
+    return;
+  }
   if (!fused_ok_ && !ws) throw std::runtime_error("MlpModel: layer-wise network launched without a workspace");
   if (ws && layerwise(rows)) {
     launch_layerwise(X, rows, out, static_cast<float*>(ws), seed_ ^ (off * 0x9E3779B97F4A7C15ULL), s);
@@ -312,7 +354,7 @@ void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* w
     const bool head_out = vae_ && o + 1 == prog_.n_pre;
     a.O = head_out ? head : buf[flip];
     a.ldo = op.Np;
-    kern::mlp_layer(a, s);
+    run_layer(a, s);
     cur = a.O;
     cur_ld = op.Np;
     flip ^= 1;
@@ -351,7 +393,127 @@ void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* w
       dld = op.Np;
       flip ^= 1;
     }
+    run_layer(a, s);
+  }
+  kern::mlp_mse_finish(mse, rows, 1.0 / (double(F_) * samples_), out, s);
+}
+
+// Large batches: the register-tiled GEMM (64 rows x up to 64 columns per
+// wave); small ones: one 16x16 tile per wave (more waves for the chip).
+void MlpModel::run_layer(const kern::MlpLayerArgs& a, hipStream_t s) const {
+  if (a.rows_eff < kGemmRows) {
     kern::mlp_layer(a, s);
+    return;
+  }
+  kern::DenseGemmArgs g;
+  g.W = a.W;
+  g.bias = a.bias;
+  g.K = a.K;
+  g.Kp = a.Kp;
+  g.N = a.N;
+  g.Np = a.Np;
+  g.act = a.act;
+  g.A = a.A;
+  g.lda = a.lda;
+  g.H = a.H;
+  g.ldh = a.ldh;
+  g.latent = a.latent;
+  g.key = a.key;
+  g.rows = a.rows;
+  g.rows_eff = a.rows_eff;
+  g.O = a.O;
+  g.ldo = a.ldo;
+  g.o_f32 = 1;
+  g.mse = a.mse;
+  g.xref = a.xref;
+  g.ldx = a.ldx;
+  kern::dense_gemm(g, s);
+}
+
+void MlpModel::launch_layerwise_bf16(const double* X, int rows, double* out, char* ws, uint64_t key, hipStream_t s) {
+  const float* P = d_params_.as<float>();
+  const uint16_t* Wb = d_pbf_.as<uint16_t>();
+  const size_t R = size_t(round_up(rows, 128)), S = vae_ ? size_t(samples_) : 1;
+  size_t Wmax = 64;
+  for (int o = 0; o < prog_.n_pre + prog_.n_loop; ++o) Wmax = std::max(Wmax, size_t(prog_.ops[o].Npb));
+  const size_t K0 = size_t(prog_.ops[0].Kpb), K0f = size_t(prog_.ops[0].Kp);
+  uint16_t* xb = reinterpret_cast<uint16_t*>(ws);
+  uint16_t* buf[2] = {xb + R * K0, xb + R * K0 + R * S * Wmax};
+  float* x32 = reinterpret_cast<float*>(buf[1] + R * S * Wmax);
+  float* head = x32 + R * K0f;
+  float* mse = head + R * Wmax;
+  auto args = [&](const kern::MlpOp& op) {
+    kern::DenseGemmArgs a;
+    a.bf16 = 1;
+    a.W = Wb + op.wb_off;
+    a.bias = P + op.b_off;
+    a.K = op.K;
+    a.Kp = op.Kpb;
+    a.N = op.N;
+    a.Np = op.Npb;
+    a.act = op.act;
+    a.rows = rows;
+    a.rows_eff = rows;
+    return a;
+  };
+  kern::convert_bf16(X, rows, F_, int(K0), xb, s);
+  const void* cur = xb;
+  int cur_ld = int(K0), flip = 0;
+  for (int o = 0; o < prog_.n_pre; ++o) {
+    const auto& op = prog_.ops[o];
+    kern::DenseGemmArgs a = args(op);
+    a.A = cur;
+    a.lda = cur_ld;
+    const bool last = o + 1 == prog_.n_pre;
+    if (last) {  // plain MLP logits / VAE head [mu | log_var] in fp32
+      a.O = head;
+      a.o_f32 = 1;
+    } else {
+      a.O = buf[flip];
+      a.o_f32 = 0;
+      flip ^= 1;
+    }
+    a.ldo = op.Npb;
+    kern::dense_gemm(a, s);
+    cur = a.O;
+    cur_ld = op.Npb;
+  }
+  if (!vae_) {
+    kern::mlp_finish(head, cur_ld, rows, prog_.out_dim, prog_.out_softmax, out, s);
+    return;
+  }
+  kern::mlp_convert(X, rows, F_, int(K0f), x32, s);  // fp32 reference rows for the MSE
+  (void)hipMemsetAsync(mse, 0, size_t(rows) * sizeof(float), s);
+  const void* dcur = nullptr;
+  int dld = 0;
+  flip = 0;
+  for (int o = prog_.n_pre; o < prog_.n_pre + prog_.n_loop; ++o) {
+    const auto& op = prog_.ops[o];
+    if (op.type == kern::kMlpReparam) continue;
+    kern::DenseGemmArgs a = args(op);
+    a.rows_eff = rows * int(S);
+    if (!dcur) {
+      a.H = head;
+      a.ldh = prog_.ops[prog_.n_pre - 1].Npb;
+      a.latent = latent_;
+      a.key = key;
+    } else {
+      a.A = dcur;
+      a.lda = dld;
+    }
+    if (op.type == kern::kMlpDenseMse) {
+      a.mse = mse;
+      a.xref = x32;
+      a.ldx = int(K0f);
+    } else {
+      a.O = buf[flip];
+      a.o_f32 = 0;
+      a.ldo = op.Npb;
+      dcur = a.O;
+      dld = op.Npb;
+      flip ^= 1;
+    }
+    kern::dense_gemm(a, s);
   }
   kern::mlp_mse_finish(mse, rows, 1.0 / (double(F_) * samples_), out, s);
 }
@@ -420,11 +582,10 @@ void MlpModel::run_cpu(const double* X, int rows, int, double* out) const {
 }
 
 std::shared_ptr<RowModel> MlpModel::clone() const {
-  if (vae_) {
-    auto m = vae(enc_, latent_, dec_, samples_, seed_);
-    return with_meta(m);
-  }
-  return with_meta(std::make_shared<MlpModel>(enc_, out_mode_));
+  std::shared_ptr<MlpModel> m = vae_ ? vae(enc_, latent_, dec_, samples_, seed_)
+                                     : std::make_shared<MlpModel>(enc_, out_mode_);
+  if (precision_) m->set_precision(precision_);
+  return with_meta(m);
 }
 
 }  // namespace sca::gpu

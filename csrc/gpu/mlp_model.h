@@ -46,6 +46,10 @@ class MlpModel : public RowModel {
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
   std::shared_ptr<RowModel> clone() const override;
   const kern::MlpProgram& program() const { return prog_; }
+  // 0 = fp32 (exact f32 MFMA products, Keras / torch float32 numerics);
+  // 1 = bf16 operands, fp32 accumulation (per-model opt-in, ~1e-2 relative).
+  void set_precision(int p);
+  int precision() const { return precision_; }
   void set_seed(uint64_t seed) { seed_ = seed; }
 
  private:
@@ -54,6 +58,8 @@ class MlpModel : public RowModel {
   int add_layer(const DenseLayer& L, int type, int in_buf, int out_buf);
   void cpu_dense(const DenseLayer& L, const std::vector<float>& in, std::vector<float>& out, int rows) const;
   void launch_layerwise(const double* X, int rows, double* out, float* ws, uint64_t key, hipStream_t s);
+  void launch_layerwise_bf16(const double* X, int rows, double* out, char* ws, uint64_t key, hipStream_t s);
+  void run_layer(const kern::MlpLayerArgs& a, hipStream_t s) const;
   int max_np() const;
 
   std::vector<DenseLayer> enc_, dec_;  // plain: enc_ = all layers
@@ -64,6 +70,9 @@ class MlpModel : public RowModel {
   std::atomic<uint64_t> offset_{0};  // advances per launch: fresh MC draws per request
   int mode_ = 0;                     // SCA_MLP_MODE: 0 auto, 1 fused, 2 layer-wise
   bool fused_ok_ = true;             // activations fit one workgroup's LDS
+  int precision_ = 0;
+  std::vector<uint16_t> pbf_;        // bf16 weights (precision_ == 1)
+  DeviceBuffer d_pbf_;
   kern::MlpProgram prog_;
   std::vector<float> params_;
   DeviceBuffer d_params_;

@@ -1,0 +1,359 @@
+// Large-batch Dense layer GEMM with fused epilogue (SURVEY K10 / dense models;
+// reference: the Keras / sklearn dense layers of vae/model.py:23-91 and the
+// MLP servers).  See DenseGemmArgs in kernels.h for the layouts.
+//
+// One wave per workgroup owns a 64-row x 16*TN-column output tile: 4 x TN
+// independent 16x16 accumulators.  Operands come straight from global memory
+// in MFMA fragment order (A rows are contiguous along K, W is pre-packed), so
+// there is no LDS staging and no barrier; the next K block's fragments are
+// loaded before the current block's MFMAs issue (register double buffering),
+// and with 4 x TN accumulators consecutive MFMAs never depend on each other.
+// Per 16-B B fragment the wave issues 4 MFMAs (one per row tile) and per A
+// fragment TN -- the layer kernel with 16x16 per wave issued 1 per B load.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+#include "philox.h"
+
+namespace sca::kern {
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+constexpr int kTM = 4;  // row tiles (of 16) per wave
+
+__device__ __forceinline__ float act_f(float v, int a) {
+  switch (a) {
+    case kMlpRelu: return fmaxf(v, 0.f);
+    case kMlpSigmoid: return 1.f / (1.f + expf(-v));
+    case kMlpTanh: return tanhf(v);
+    default: return v;
+  }
+}
+
+// VAE reparameterised input value z[row][k] (same Philox streams as the fused
+// kernel's reparam() and mlp_layer's AMODE 2)
+__device__ __forceinline__ float reparam_z(const DenseGemmArgs& a, int row, int k) {
+  const int r = row % a.rows, smp = row / a.rows;
+  const int kk = min(k, a.latent - 1);
+  const float* h = a.H + size_t(r) * a.ldh;
+  Philox rng(a.key, (uint64_t(r) << 24) ^ (uint64_t(smp) << 14) ^ uint64_t(kk));
+  const float z = h[kk] + expf(0.5f * h[a.latent + kk]) * rng.normal();
+  return k < a.latent ? z : 0.f;
+}
+
+// ---- operand fragments
+template <int BF16> struct Frag;
+template <> struct Frag<0> {  // fp32: one 16-k block = 4 MFMAs (16x16x4), 4 floats per lane
+  using T = f32x4;
+  static constexpr int kK = 16;
+};
+template <> struct Frag<1> {  // bf16: one 32-k block = 1 MFMA (16x16x32), 8 bf16 per lane
+  using T = bf16x8;
+  static constexpr int kK = 32;
+};
+
+template <int BF16, int AMODE>
+__device__ __forceinline__ typename Frag<BF16>::T load_a(const DenseGemmArgs& a, int row, int kb, int kq) {
+  row = min(row, a.rows_eff - 1);
+  if constexpr (AMODE == 0) {
+    if constexpr (BF16) {
+      return *reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(a.A) + size_t(row) * a.lda + kb * 32 + kq * 8);
+    } else {
+      return *reinterpret_cast<const f32x4*>(static_cast<const float*>(a.A) + size_t(row) * a.lda + kb * 16 + kq * 4);
+    }
+  } else {
+    typename Frag<BF16>::T v;
+    constexpr int n = BF16 ? 8 : 4;
+    const int k0 = kb * Frag<BF16>::kK + kq * n;
+#pragma unroll
+    for (int j = 0; j < n; ++j) {
+      if constexpr (BF16) v[j] = __bf16(reparam_z(a, row, k0 + j));
+      else v[j] = reparam_z(a, row, k0 + j);
+    }
+    return v;
+  }
+}
+
+template <int BF16>
+__device__ __forceinline__ f32x4 mma(const typename Frag<BF16>::T& x, const typename Frag<BF16>::T& y, f32x4 acc,
+                                     int j) {
+  if constexpr (BF16) {
+    (void)j;
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, acc, 0, 0, 0);
+  } else {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], y[j], acc, 0, 0, 0);
+  }
+}
+
+template <int BF16, int AMODE, int TN>
+__global__ __launch_bounds__(64) void dense_gemm_kernel(const DenseGemmArgs a) {
+  using T = typename Frag<BF16>::T;
+  const int lane = threadIdx.x, r16 = lane & 15, kq = lane >> 4;
+  const int m0 = blockIdx.y * (16 * kTM);
+  const int t0 = blockIdx.x * TN;  // first column tile
+  const int ntiles = a.Np >> 4;
+  const int KB = a.Kp / Frag<BF16>::kK;
+  const T* W = static_cast<const T*>(a.W);
+  const T* wt[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) wt[tn] = W + size_t(min(t0 + tn, ntiles - 1)) * KB * 64 + lane;
+  f32x4 acc[kTM][TN];
+#pragma unroll
+  for (int tm = 0; tm < kTM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  T av[kTM], bv[TN];
+#pragma unroll
+  for (int tm = 0; tm < kTM; ++tm) av[tm] = load_a<BF16, AMODE>(a, m0 + 16 * tm + r16, 0, kq);
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) bv[tn] = wt[tn][0];
+  for (int kb = 0; kb < KB; ++kb) {
+    T an[kTM], bn[TN];
+    const int kn = min(kb + 1, KB - 1);  // the last block reloads itself (never used)
+#pragma unroll
+    for (int tm = 0; tm < kTM; ++tm) an[tm] = load_a<BF16, AMODE>(a, m0 + 16 * tm + r16, kn, kq);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) bn[tn] = wt[tn][size_t(kn) * 64];
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int J = BF16 ? 1 : 4;
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int tm = 0; tm < kTM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma<BF16>(av[tm], bv[tn], acc[tm][tn], j);
+#pragma unroll
+    for (int tm = 0; tm < kTM; ++tm) av[tm] = an[tm];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) bv[tn] = bn[tn];
+  }
+  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int t = t0 + tn;
+    if (t >= ntiles) break;
+    const int col = t * 16 + r16;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < kTM; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + 16 * tm + kq * 4 + i;
+        if (!a.mse) {
+          if (row < a.rows_eff) {
+            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
+            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+          }
+        } else {
+          const bool ok = live && row < a.rows_eff;
+          const int r = row % a.rows;
+          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
+          d *= d;
+          d += __shfl_xor(d, 1, 64);
+          d += __shfl_xor(d, 2, 64);
+          d += __shfl_xor(d, 4, 64);
+          d += __shfl_xor(d, 8, 64);
+          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+        }
+      }
+    }
+  }
+}
+
+// ---- bf16: LDS-tiled GEMM.  A 256-thread workgroup (2 x 2 waves) owns a
+// 128 x BN output tile (BN = 64 is launched: two resident workgroups per CU).  Per 64-wide K stage the A and W panels (128 B per row) are
+// staged in LDS with full-line 16-B loads; each wave reads its 4 + BN/32
+// fragments with ds_read_b128 and issues 8 * BN/32 MFMAs (16x16x32 bf16).
+// The LDS row stride is 144 B (128 + 16): the 16 lanes of a ds_read_b128
+// group read 16 rows at one k-chunk, which land on 16 distinct 16-B slots of
+// the 256-B bank row (row * 9 mod 16) -- conflict-free.  Global loads run two
+// stages ahead (two register sets) into two LDS buffers: the L2 / HBM round
+// trip of stage k+2 overlaps the MFMAs of stages k and k+1 (one stage of
+// ~512 MFMA cycles alone does not cover it: profiles/r02d_dense).  W is
+// row-major [Npb][Kpb] bf16 (Kpb, Npb multiples of 64, zero padded).
+constexpr int kBM = 128, kBK = 64, kLdr = kBK + 8;  // row stride in bf16 elements
+
+template <int AMODE>
+__device__ __forceinline__ bf16x8 stage_a(const DenseGemmArgs& a, int row, int k) {
+  row = min(row, a.rows_eff - 1);
+  if constexpr (AMODE == 0) {
+    return *reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(a.A) + size_t(row) * a.lda + k);
+  } else {
+    bf16x8 v;
+    if (k >= a.latent) {  // K padding past the latent width: no draws
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __bf16(0.f);
+      return v;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = __bf16(reparam_z(a, row, k + j));
+    return v;
+  }
+}
+
+template <int AMODE, int BN>
+__global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs a) {
+  constexpr int TN = BN / 32;                 // 16-col tiles per wave (2 waves along N)
+  constexpr int CA = kBM * 8 / 256;           // A staging chunks per thread (128 rows x 8 chunks)
+  constexpr int CW = BN * 8 / 256;            // W staging chunks per thread
+  constexpr int kBuf = (kBM + BN) * kLdr;     // one LDS buffer: A panel then W panel
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * kBuf];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 1, wc = wave & 1, r16 = lane & 15, kq = lane >> 4;
+  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * BN;
+  const __bf16* W = static_cast<const __bf16*>(a.W);
+  const int KS = a.Kp / kBK;
+  // two stages of staging registers; every index below is a compile-time
+  // constant (the K loop is unrolled by two), so they stay in VGPRs
+  bf16x8 ra0[CA], rw0[CW], ra1[CA], rw1[CW];
+  auto gload = [&](int ks, bf16x8* ra, bf16x8* rw) {
+#pragma unroll
+    for (int j = 0; j < CA; ++j) {
+      const int c = tid + 256 * j;
+      ra[j] = stage_a<AMODE>(a, m0 + (c >> 3), ks * kBK + (c & 7) * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const int c = tid + 256 * j;
+      rw[j] = *reinterpret_cast<const bf16x8*>(W + size_t(min(n0 + (c >> 3), a.Np - 1)) * a.Kp + ks * kBK +
+                                               (c & 7) * 8);
+    }
+  };
+  auto lstore = [&](int buf, const bf16x8* ra, const bf16x8* rw) {
+    __bf16* As = smem + buf * kBuf;
+    __bf16* Ws = As + kBM * kLdr;
+#pragma unroll
+    for (int j = 0; j < CA; ++j) {
+      const int c = tid + 256 * j;
+      *reinterpret_cast<bf16x8*>(As + (c >> 3) * kLdr + (c & 7) * 8) = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const int c = tid + 256 * j;
+      *reinterpret_cast<bf16x8*>(Ws + (c >> 3) * kLdr + (c & 7) * 8) = rw[j];
+    }
+  };
+  f32x4 acc[4][TN];
+#pragma unroll
+  for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) {
+    const __bf16* As = smem + buf * kBuf;
+    const __bf16* Ws = As + kBM * kLdr;
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; ++kk) {
+      bf16x8 af[4], bf[TN];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        af[t] = *reinterpret_cast<const bf16x8*>(As + (wr * 64 + t * 16 + r16) * kLdr + kk * 32 + kq * 8);
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        bf[t] = *reinterpret_cast<const bf16x8*>(Ws + (wc * (BN / 2) + t * 16 + r16) * kLdr + kk * 32 + kq * 8);
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+  gload(0, ra0, rw0);
+  if (KS > 1) gload(1, ra1, rw1);
+  lstore(0, ra0, rw0);
+  __syncthreads();
+  for (int ks = 0; ks < KS; ks += 2) {
+    // even stage: buffer 0 holds it, set 1 holds ks + 1, set 0 is free for ks + 2
+    if (ks + 2 < KS) gload(ks + 2, ra0, rw0);
+    compute(0);
+    if (ks + 1 < KS) lstore(1, ra1, rw1);
+    __syncthreads();
+    if (ks + 1 >= KS) break;
+    // odd stage: buffer 1, set 0 holds ks + 2, set 1 free for ks + 3
+    if (ks + 3 < KS) gload(ks + 3, ra1, rw1);
+    compute(1);
+    if (ks + 2 < KS) lstore(0, ra0, rw0);
+    __syncthreads();
+  }
+  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int col = n0 + wc * (BN / 2) + tn * 16 + r16;
+    if (col >= a.Np) continue;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 4; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 64 + tm * 16 + kq * 4 + i;
+        if (!a.mse) {
+          if (row < a.rows_eff) {
+            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
+            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+          }
+        } else {
+          const bool ok = live && row < a.rows_eff;
+          const int r = row % a.rows;
+          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
+          d *= d;
+          d += __shfl_xor(d, 1, 64);
+          d += __shfl_xor(d, 2, 64);
+          d += __shfl_xor(d, 4, 64);
+          d += __shfl_xor(d, 8, 64);
+          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+        }
+      }
+    }
+  }
+}
+
+__global__ void convert_bf16_kernel(const double* __restrict__ X, int rows, int F, int ld, __bf16* __restrict__ out) {
+  const size_t n = size_t(rows) * ld;
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+    const int r = int(i / ld), c = int(i - size_t(r) * ld);
+    out[i] = __bf16(c < F ? float(X[size_t(r) * F + c]) : 0.f);
+  }
+}
+
+template <int BF16, int AMODE>
+void launch_tn(const DenseGemmArgs& a, hipStream_t s) {
+  const int ntiles = a.Np >> 4;
+  const int row_blocks = (a.rows_eff + 16 * kTM - 1) / (16 * kTM);
+  // TN: as wide as the layer allows, narrower when that leaves the chip's
+  // 1024 SIMDs short of waves
+  int tn = ntiles >= 4 ? 4 : ntiles >= 2 ? 2 : 1;
+  while (tn > 1 && row_blocks * ((ntiles + tn - 1) / tn) < 1024) tn >>= 1;
+  const dim3 grid((ntiles + tn - 1) / tn, row_blocks);
+  if (tn == 4) hipLaunchKernelGGL((dense_gemm_kernel<BF16, AMODE, 4>), grid, dim3(64), 0, s, a);
+  else if (tn == 2) hipLaunchKernelGGL((dense_gemm_kernel<BF16, AMODE, 2>), grid, dim3(64), 0, s, a);
+  else hipLaunchKernelGGL((dense_gemm_kernel<BF16, AMODE, 1>), grid, dim3(64), 0, s, a);
+}
+
+}  // namespace
+
+void dense_gemm(const DenseGemmArgs& a, hipStream_t s) {
+  if (a.rows_eff <= 0) return;
+  if (a.bf16) {
+    // 128 x 64 tiles: two resident workgroups per CU (the 128 x 128 variant
+    // needs 230 VGPRs -> one, and measured 2.5x slower on the VAE decoder)
+    const dim3 grid((a.Np + 63) / 64, (a.rows_eff + kBM - 1) / kBM);
+    if (a.H) hipLaunchKernelGGL((gemm_bf16_lds_kernel<2, 64>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((gemm_bf16_lds_kernel<0, 64>), grid, dim3(256), 0, s, a);
+  } else {
+    if (a.H) launch_tn<0, 2>(a, s);
+    else launch_tn<0, 0>(a, s);
+  }
+}
+
+void convert_bf16(const double* X, int rows, int F, int ld, void* out, hipStream_t s) {
+  if (rows <= 0) return;
+  const size_t n = size_t(rows) * ld;
+  const int blocks = int((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+  hipLaunchKernelGGL(convert_bf16_kernel, dim3(blocks), dim3(256), 0, s, X, rows, F, ld, static_cast<__bf16*>(out));
+}
+
+}  // namespace sca::kern

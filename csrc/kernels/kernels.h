@@ -121,6 +121,8 @@ struct MlpOp {
   int in_buf, out_buf;
   int K, Kp, N, Np;        // Reparam: N = latent dim (input holds [mean | log_var])
   long long w_off, b_off;  // float offsets into the parameter blob
+  long long wb_off;        // bf16 precision: offset (elements) into the bf16 weight blob
+  int Kpb, Npb;            //   its K / N padded to 32
 };
 constexpr int kMlpMaxOps = 24;
 constexpr int kMlpMaxBufs = 6;
@@ -164,6 +166,37 @@ struct MlpLayerArgs {
   int ldx = 0;
 };
 void mlp_layer(const MlpLayerArgs& a, hipStream_t stream);
+
+// Large-batch layer GEMM (csrc/kernels/gemm.hip): one wave per 64 x (16 TN)
+// output tile straight from L2 -- no LDS -- so each 16-B B fragment feeds 4
+// MFMAs (4 row tiles) and each A fragment TN: 4x the operand reuse of the
+// 16x16-per-wave layer kernel.  Two operand types:
+//   fp32: A fp32 [rows][lda], W packed as for mlp_layer (v_mfma_f32_16x16x4_f32)
+//   bf16: A bf16 [rows][lda], W bf16 row-major [Np][Kp], Kp % 64 == 0 and
+//         Np % 64 == 0 (zero padded); LDS-tiled 128 x 128 workgroup tiles on
+//         v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+// Epilogue: + bias, activation, store fp32 or bf16 (columns >= N zeroed), or
+// the VAE's MSE reduction.  AMODE 2 = VAE reparameterised A (as mlp_layer).
+struct DenseGemmArgs {
+  int bf16 = 0;
+  const void* W = nullptr;
+  const float* bias = nullptr;
+  int K = 0, Kp = 0, N = 0, Np = 0, act = 0;
+  const void* A = nullptr;
+  int lda = 0;
+  const float* H = nullptr;
+  int ldh = 0, latent = 0;
+  uint64_t key = 0;
+  int rows = 0, rows_eff = 0;
+  void* O = nullptr;
+  int ldo = 0, o_f32 = 1;
+  float* mse = nullptr;
+  const float* xref = nullptr;
+  int ldx = 0;
+};
+void dense_gemm(const DenseGemmArgs& a, hipStream_t stream);
+// fp64 rows [rows][F] -> bf16 [rows][ld], zero-padded columns
+void convert_bf16(const double* X, int rows, int F, int ld, void* out, hipStream_t stream);
 // fp64 rows [rows][F] -> fp32 [rows][ld], zero-padded columns
 void mlp_convert(const double* X, int rows, int F, int ld, float* out, hipStream_t stream);
 // logits [rows][ld] -> out: mode 0 plain [rows][n], 1 row softmax, 2 binary [1 - p, p]

@@ -428,7 +428,7 @@ class OutlierVAE(_FeedbackMetrics, _Reservoir):
     score_key = "mse"
 
     def __init__(self, threshold=10, reservoir_size=50000, model_name="vae", load_path="./models/", weights=None,
-                 preprocess=None, samples: int = 10, seed: int = 0, device=None):
+                 preprocess=None, samples: int = 10, seed: int = 0, device=None, precision: str = "fp32"):
         self.threshold = threshold
         self.nb_outliers = 0
         if weights is None:
@@ -441,7 +441,9 @@ class OutlierVAE(_FeedbackMetrics, _Reservoir):
         self._init_scaling(preprocess, reservoir_size, n_features)
         from .._native import native
 
-        rm = native().vae_model(weights["encoder"], int(weights["latent"]), weights["decoder"], samples, seed)
+        # precision="bf16": bf16 MFMA operands, fp32 accumulation (opt-in; scores within ~1e-2 relative)
+        rm = native().vae_model(weights["encoder"], int(weights["latent"]), weights["decoder"], samples, seed,
+                                precision)
         self._scorer = _NativeScorer(rm, _default_device(device))
         self._init_feedback()
 

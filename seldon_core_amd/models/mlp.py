@@ -26,10 +26,15 @@ def layer(W_out_in, b, act="identity") -> dict:
     return {"W": W, "b": np.ascontiguousarray(b, dtype=np.float32).reshape(-1), "act": ACTS[act]}
 
 
-def mlp_row_model(layers: Sequence[dict], out_mode: int = OUT_PLAIN, class_names: Optional[List[str]] = None):
+def mlp_row_model(layers: Sequence[dict], out_mode: int = OUT_PLAIN, class_names: Optional[List[str]] = None,
+                  precision: str = "fp32"):
+    """Native dense network.  ``precision="bf16"`` is an explicit per-model
+    opt-in: bf16 operands with fp32 accumulation on v_mfma_f32_16x16x32_bf16
+    (expect ~1e-2 relative error on the logits vs float32; tests/test_mlp.py
+    states the tolerance), the default keeps exact fp32 products."""
     from .._native import native
 
-    m = native().mlp_model(list(layers), out_mode)
+    m = native().mlp_model(list(layers), out_mode, precision)
     if class_names:
         m.set_class_names([str(c) for c in class_names])
     return m

@@ -169,3 +169,81 @@ def test_vae_gpu_matches_cpu_reference(mode, monkeypatch):
     finally:
         unit.stop()
     np.testing.assert_allclose(got[:, 0], cpu_m.run_cpu(X)[:, 0], rtol=2e-4)
+
+
+# ------------------------------------------------------------------ bf16 / large-batch GEMM
+def test_bf16_precision_is_an_explicit_opt_in():
+    C = sca.native()
+    layers = random_dense_stack([20, 32, 5], ["relu", "identity"])
+    assert C.mlp_precision(C.mlp_model(layers, 1)) == "fp32"
+    m = C.mlp_model(layers, 1, "bf16")
+    assert C.mlp_precision(m) == "bf16" and C.mlp_layerwise(m, 4096)  # bf16 runs on the GEMM path only
+    assert C.mlp_precision(m.clone()) == "bf16"
+    with pytest.raises(Exception):
+        C.mlp_model(layers, 1, "fp8")
+
+
+def _torch_mlp(layers, X, softmax=True):
+    import torch
+
+    x = torch.tensor(X, dtype=torch.float32)
+    for L in layers:
+        x = x @ torch.tensor(L["W"]).T + torch.tensor(L["b"])
+        if L["act"] == 1:
+            x = torch.relu(x)
+    return (torch.softmax(x, 1) if softmax else x).double().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [1, 300, 1024, 8192])
+@pytest.mark.parametrize("dims", [(784, 512, 256, 10), (13, 37, 19, 3)])
+def test_mlp_large_batch_gemm_fp32_matches_torch(dims, rows, monkeypatch):
+    """Layer-wise fp32 path (register-tiled GEMM from 512 rows) vs torch fp32."""
+    monkeypatch.setenv("SCA_MLP_MODE", "layer")
+    layers = random_dense_stack(list(dims), ["relu"] * (len(dims) - 2) + ["identity"], seed=3)
+    X = np.random.default_rng(rows).normal(size=(rows, dims[0]))
+    unit = sca.native().BatchedUnit(mlp_row_model(layers, OUT_SOFTMAX), 0, max_batch=8192)
+    try:
+        got = unit.run(X)
+    finally:
+        unit.stop()
+    np.testing.assert_allclose(got, _torch_mlp(layers, X), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [1, 64, 1000, 8192])
+@pytest.mark.parametrize("dims", [(784, 512, 256, 10), (13, 37, 19, 3), (64, 128, 128, 64, 33)])
+def test_mlp_bf16_matches_torch_fp32_within_stated_tolerance(dims, rows):
+    """bf16 operands / fp32 accumulation: stated tolerance 2e-2 absolute on
+    softmax probabilities and 3e-2 relative on logits vs torch float32."""
+    layers = random_dense_stack(list(dims), ["relu"] * (len(dims) - 2) + ["identity"], seed=4)
+    X = np.random.default_rng(rows).normal(size=(rows, dims[0]))
+    for out_mode, softmax in ((OUT_SOFTMAX, True), (0, False)):
+        unit = sca.native().BatchedUnit(mlp_row_model(layers, out_mode, precision="bf16"), 0, max_batch=8192)
+        try:
+            got = unit.run(X)
+        finally:
+            unit.stop()
+        ref = _torch_mlp(layers, X, softmax)
+        if softmax:
+            np.testing.assert_allclose(got, ref, atol=2e-2)
+        else:
+            scale = np.abs(ref).max()
+            np.testing.assert_allclose(got, ref, atol=3e-2 * scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision,rtol", [("fp32", 2e-4), ("bf16", 5e-2)])
+def test_vae_large_batch_paths_match_cpu(precision, rtol, monkeypatch):
+    monkeypatch.setenv("SCA_MLP_MODE", "layer")
+    C = sca.native()
+    enc, dec = _vae_layers(F=64, hidden=(256, 128), latent=16)
+    gpu_m = C.vae_model(enc, 16, dec, 10, 11, precision)
+    cpu_m = C.vae_model(enc, 16, dec, 10, 11)
+    X = np.random.default_rng(5).random(size=(1000, 64))
+    unit = C.BatchedUnit(gpu_m, 0, max_batch=4096)
+    try:
+        got = unit.run(X)[:, 0]
+    finally:
+        unit.stop()
+    np.testing.assert_allclose(got, cpu_m.run_cpu(X)[:, 0], rtol=rtol)

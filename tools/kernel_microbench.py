@@ -180,6 +180,65 @@ def case_mlp_modes(iters):
             print(json.dumps(rec), flush=True)
 
 
+def case_dense_prec(iters):
+    """MLP 784-512-256-10 @ 8192 rows and VAE 64-256-128-z16 x10 @ 4096 rows:
+    fused fp32 / layer-wise fp32 (register-tiled GEMM) / bf16 GEMM.  Kernel
+    time comes from the rocprofv3 kernel trace (gpu-busy here includes the
+    fp64 H2D of the batch); run with torch cases for the library baseline."""
+    import os
+
+    from seldon_core_amd import native
+    from seldon_core_amd.models.mlp import OUT_SOFTMAX, mlp_row_model, random_dense_stack
+
+    C = native()
+    mlp_layers = random_dense_stack(MLP_DIMS, ["relu", "relu", "identity"], seed=4)
+    enc = random_dense_stack([64, 256, 128, 32], ["relu", "relu", "identity"], seed=1)
+    dec = random_dense_stack([16, 128, 256, 64], ["relu", "relu", "sigmoid"], seed=2)
+    for net, rows in (("mlp784", 8192), ("vae64", 4096)):
+        X = np.random.default_rng(0).random(size=(rows, 784 if net == "mlp784" else 64))
+        ref = None
+        for label, mode, prec in (("fused_fp32", "fused", "fp32"), ("layer_fp32", "layer", "fp32"),
+                                  ("bf16", "layer", "bf16")):
+            os.environ["SCA_MLP_MODE"] = mode
+            m = (mlp_row_model(mlp_layers, OUT_SOFTMAX, precision=prec) if net == "mlp784"
+                 else C.vae_model(enc, 16, dec, 10, 3, prec))
+            unit = C.BatchedUnit(m, 0, max_batch=8192)
+            try:
+                y = unit.run(X)
+                ref = y if ref is None else ref
+                rec = _time_unit(f"dense_{net}_{label}", unit, X, iters,
+                                 {"max_abs_diff_vs_fused_fp32": float(np.abs(y - ref).max())})
+            finally:
+                unit.stop()
+        os.environ.pop("SCA_MLP_MODE", None)
+
+
+def case_mlp_torch_bf16(iters, rows_list=(8192,)):
+    """The MLP in PyTorch eager bf16 (hipBLASLt bf16 GEMMs)."""
+    import torch
+
+    from seldon_core_amd.models.mlp import random_dense_stack
+
+    layers = random_dense_stack(MLP_DIMS, ["relu", "relu", "identity"], seed=4)
+    Ws = [torch.tensor(L["W"], device="cuda", dtype=torch.bfloat16) for L in layers]
+    bs = [torch.tensor(L["b"], device="cuda", dtype=torch.bfloat16) for L in layers]
+    for rows in rows_list:
+        x = torch.randn(rows, MLP_DIMS[0], device="cuda", dtype=torch.bfloat16)
+
+        def fwd():
+            h = x
+            for i, (W, b) in enumerate(zip(Ws, bs)):
+                h = torch.nn.functional.linear(h, W, b)
+                if i + 1 < len(Ws):
+                    h = torch.relu(h)
+            return torch.softmax(h.float(), 1)
+
+        us = _torch_time(fwd, iters)
+        flops = 2 * rows * sum(a * b for a, b in zip(MLP_DIMS[:-1], MLP_DIMS[1:]))
+        print(json.dumps({"case": "mlp_torch_bf16", "rows": rows, "us_per_run": round(us, 2),
+                          "tflops": round(flops / (us * 1e-6) / 1e12, 2)}), flush=True)
+
+
 def _torch_time(fn, iters):
     import torch
 
@@ -303,7 +362,7 @@ def main():
     a = ap.parse_args()
     cases = {"tree": case_tree, "vae": case_vae, "mlp": case_mlp, "linear": case_linear,
              "mlp_torch": case_mlp_torch, "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes,
-             "lstm": case_lstm}
+             "lstm": case_lstm, "dense_prec": case_dense_prec, "mlp_torch_bf16": case_mlp_torch_bf16}
     for c in a.only.split(","):
         cases[c](a.iters)
 
