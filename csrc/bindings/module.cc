@@ -407,11 +407,10 @@ PYBIND11_MODULE(_C, m) {
       .def("run", [](gpu::BatchedUnit& u, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
         if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
         const int rows = int(X.shape(0)), cols = int(X.shape(1));
-        std::vector<double> x(X.data(), X.data() + X.size());
         std::vector<double> out;
         {
-          py::gil_scoped_release nogil;
-          out = u.run_dense(x, rows, cols);
+          py::gil_scoped_release nogil;  // X (held by this frame) is read in place: no host copy
+          out = u.run_ptr(X.data(), rows, cols);
         }
         const int oc = int(out.size() / size_t(rows));
         py::array_t<double> r({rows, oc});

@@ -126,6 +126,8 @@ void BatchedUnit::stop() {
   for (auto& it : rest) it.k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "GPU unit stopped")));
 }
 
+constexpr size_t kDirectH2DBytes = size_t(1) << 20;
+
 void BatchedUnit::ensure_capacity(Slot& s, int rows, int cols) {
   const int oc = model_->out_cols(cols);
   const size_t need_in = size_t(rows) * cols * sizeof(double);
@@ -177,13 +179,32 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
   Item it;
   std::vector<int64_t> shape;
   std::string err;
-  if (!in->data.dense(shape, it.x, &err)) {
-    k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, err)));
-    return;
+  size_t nvals = 0;
+  const DefaultData& dd = in->data;
+  bool flat = (dd.kind == DataKind::Tensor || (dd.kind == DataKind::NdArray && dd.nd_dense)) && !dd.shape.empty();
+  if (flat) {  // rows read in place from the message (it stays alive in it.req)
+    int64_t n = 1;
+    for (auto d : dd.shape) {
+      if (d < 0) flat = false;
+      n *= d;
+    }
+    flat = flat && n == int64_t(dd.values.size());
+  }
+  if (flat) {
+    shape = dd.shape;
+    it.xp = dd.values.data();
+    nvals = dd.values.size();
+  } else {
+    if (!dd.dense(shape, it.x, &err)) {
+      k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, err)));
+      return;
+    }
+    it.xp = it.x.data();
+    nvals = it.x.size();
   }
   if (shape.empty()) {
-    it.rows = it.x.empty() ? 0 : 1;
-    it.cols = int(it.x.size());
+    it.rows = nvals == 0 ? 0 : 1;
+    it.cols = int(nvals);
   } else if (shape.size() == 1) {
     it.rows = 1;
     it.cols = int(shape[0]);
@@ -207,6 +228,10 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
   it.req = std::move(in);
   it.k = std::move(k);
   if (c.exec) it.exec = *c.exec;
+  submit_item(std::move(it));
+}
+
+void BatchedUnit::submit_item(Item it) {
   if (opts_.device < 0 && !cpu_) {
     if (fault_armed_.load(std::memory_order_relaxed) && take_injected_failure()) {
       note_failure();
@@ -216,7 +241,7 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
     note_success();
     const int oc = model_->out_cols(it.cols);
     std::vector<double> out(size_t(it.rows) * oc);
-    model_->run_cpu(it.x.data(), it.rows, it.cols, out.data());
+    model_->run_cpu(it.xp, it.rows, it.cols, out.data());
     MsgPtr r = make_response(*resp_, it, out.data(), oc);
     {
       std::lock_guard<std::mutex> g(stats_mu_);
@@ -264,7 +289,7 @@ bool BatchedUnit::launch(Slot* s) {
       s->cpu_out.assign(size_t(rows) * s->out_cols, 0.0);
       size_t row = 0;
       for (const auto& it : s->items) {
-        model_->run_cpu(it.x.data(), it.rows, cols, s->cpu_out.data() + row * s->out_cols);
+        model_->run_cpu(it.xp, it.rows, cols, s->cpu_out.data() + row * s->out_cols);
         row += size_t(it.rows);
       }
       return true;
@@ -281,12 +306,19 @@ bool BatchedUnit::launch(Slot* s) {
   try {
     ensure_capacity(*s, rows, cols);
     double* hin = s->h_in.host<double>();
-    size_t off = 0;
-    for (const auto& it : s->items) {
-      memcpy(hin + off, it.x.data(), it.x.size() * sizeof(double));
-      off += it.x.size();
-    }
     const size_t bin = size_t(rows) * cols * sizeof(double), bout = size_t(rows) * s->out_cols * sizeof(double);
+    // A lone large request is DMA'd straight from its own memory (the
+    // message's tensor, or the caller's buffer for run_ptr): no host copy
+    // into the pinned slot first (8192 x 784 fp64: 51 MB).
+    const bool direct = s->items.size() == 1 && bin >= kDirectH2DBytes;
+    if (!direct) {
+      size_t off = 0;
+      for (const auto& it : s->items) {
+        const size_t n = size_t(it.rows) * it.cols;
+        memcpy(hin + off, it.xp, n * sizeof(double));
+        off += n;
+      }
+    }
     hipStream_t st = s->stream.get();
     const int32_t* seg = nullptr;
     const int nseg = int(s->items.size());
@@ -302,7 +334,7 @@ bool BatchedUnit::launch(Slot* s) {
       if (seg) model_->launch_segments(x, rows, cols, y, s->ws.get(), seg, nseg, st);
       else model_->launch(x, rows, cols, y, s->ws.get(), st);
     };
-    if (opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes) {
+    if (!direct && opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes) {
       // Output always zero-copy (written once); input zero-copy only if the
       // kernel reads each element once -- models that re-read X from many
       // workgroups (tree chunks) get one DMA into HBM first.
@@ -313,7 +345,8 @@ bool BatchedUnit::launch(Slot* s) {
       }
       if (err == hipSuccess) run(xin, s->h_out.dev<double>());
     } else {
-      err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
+      err = hipMemcpyAsync(s->d_in.get(), direct ? static_cast<const void*>(s->items[0].xp) : hin, bin,
+                           hipMemcpyHostToDevice, st);
       if (err == hipSuccess) {
         run(s->d_in.as<double>(), s->d_out.as<double>());
         err = hipMemcpyAsync(s->h_out.host<double>(), s->d_out.get(), bout, hipMemcpyDeviceToHost, st);
@@ -366,13 +399,14 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     std::vector<Group> groups;
     size_t row = 0;
     for (auto& it : items) {
-      std::vector<double> y(out + row * oc, out + (row + size_t(it.rows)) * oc);
+      const double* yp = out + row * oc;
       row += size_t(it.rows);
-      if (!it.exec) {
+      if (!it.exec) {  // answered before the slot is reused: build the response from the slot directly
         Done k = std::move(it.k);
-        k(Outcome::ok(make_response(*resp_, it, y.data(), oc)));
+        k(Outcome::ok(make_response(*resp_, it, yp, oc)));
         continue;
       }
+      std::vector<double> y(yp, yp + size_t(it.rows) * oc);
       Group* g = nullptr;
       for (auto& gg : groups)
         if (gg.ex.get() == it.exec.get()) { g = &gg; break; }
@@ -603,6 +637,30 @@ void BatchedUnit::reset_stats() {
   stats_ = BatcherStats();
 }
 
+std::vector<double> BatchedUnit::run_ptr(const double* X, int rows, int cols) {
+  if (rows <= 0 || cols <= 0) throw std::runtime_error("run_ptr: empty input");
+  const int want = model_->in_cols();
+  if (want > 0 && cols != want)
+    throw std::runtime_error("X has " + std::to_string(cols) + " features, but " + model_->name() + " is expecting " +
+                             std::to_string(want) + " features as input.");
+  auto msg = std::make_shared<SeldonMessage>();
+  msg->payload = Payload::Data;
+  msg->data.kind = DataKind::Tensor;
+  msg->data.shape = {rows, cols};
+  std::promise<Outcome> p;
+  auto f = p.get_future();
+  Item it;
+  it.req = std::move(msg);
+  it.xp = X;
+  it.rows = rows;
+  it.cols = cols;
+  it.k = [&p](Outcome o) { p.set_value(std::move(o)); };
+  submit_item(std::move(it));
+  Outcome o = f.get();
+  if (o.err) throw std::runtime_error(o.err->info);
+  return std::move(o.msg->data.values);
+}
+
 std::vector<double> BatchedUnit::run_dense(const std::vector<double>& X, int rows, int cols) {
   auto msg = std::make_shared<SeldonMessage>();
   msg->payload = Payload::Data;
@@ -615,7 +673,7 @@ std::vector<double> BatchedUnit::run_dense(const std::vector<double>& X, int row
   transform_input(c, msg, [&p](Outcome o) { p.set_value(std::move(o)); });
   Outcome o = f.get();
   if (o.err) throw std::runtime_error(o.err->info);
-  return o.msg->data.values;
+  return std::move(o.msg->data.values);
 }
 
 }  // namespace sca::gpu

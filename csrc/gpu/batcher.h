@@ -114,6 +114,9 @@ class BatchedUnit : public Unit {
 
   // Synchronous dense call (tests / python ops): X [rows, cols] -> out.
   std::vector<double> run_dense(const std::vector<double>& X, int rows, int cols);
+  // Same, reading the rows straight from caller memory (kept alive by the
+  // caller until the call returns): no copy before the GPU staging / DMA.
+  std::vector<double> run_ptr(const double* X, int rows, int cols);
 
   void stop();
 
@@ -127,7 +130,8 @@ class BatchedUnit : public Unit {
  private:
   struct Item {
     MsgPtr req;
-    std::vector<double> x;
+    std::vector<double> x;     // decoded rows, when the message holds no flat fp64 array
+    const double* xp = nullptr;  // the rows: into req's tensor values, `x`, or caller memory (run_ptr)
     int rows = 0;
     int cols = 0;
     Done k;
@@ -158,6 +162,7 @@ class BatchedUnit : public Unit {
   void note_success();
   static ErrPtr device_error(ApiError kind, std::string info);
   static MsgPtr make_response(const RespInfo& info, const Item& it, const double* out, int out_cols);
+  void submit_item(Item it);
 
   RowModelPtr model_;
   BatcherOptions opts_;
