@@ -481,12 +481,13 @@ PYBIND11_MODULE(_C, m) {
   // ------------------------------------------------------- RCCL fabric
   m.def("rccl_unique_id", [] { return py::bytes(par::rccl_unique_id()); });
   py::class_<par::Fabric, std::shared_ptr<par::Fabric>>(m, "Fabric")
-      .def(py::init([](int rank, int world, const py::bytes& uid, int device) {
+      .def(py::init([](int rank, int world, const py::bytes& uid, int device, std::vector<int> ctrl_fds) {
              std::string id(uid);
              py::gil_scoped_release nogil;  // collective: blocks until every rank joins
-             return std::make_shared<par::Fabric>(rank, world, id, device);
+             return std::make_shared<par::Fabric>(rank, world, id, device, std::move(ctrl_fds));
            }),
-           py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"))
+           py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"), py::arg("ctrl_fds"))
+      .def_property_readonly("gpu", &par::Fabric::gpu)
       .def_property_readonly("rank", &par::Fabric::rank)
       .def_property_readonly("world", &par::Fabric::world)
       .def_property_readonly("device", &par::Fabric::device)
@@ -518,6 +519,7 @@ PYBIND11_MODULE(_C, m) {
       })
       .def_property_readonly("batches", &par::PeerServer::batches)
       .def_property_readonly("rows", &par::PeerServer::rows)
+      .def_property_readonly("host_syncs", &par::PeerServer::host_syncs)
       .def("error", &par::PeerServer::error);
 
   // ------------------------------------------------------------- engine

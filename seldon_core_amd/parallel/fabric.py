@@ -1,4 +1,4 @@
-"""Cross-process graph placement over RCCL (one engine process per MI355X).
+"""Cross-process graph placement (one engine process per MI355X).
 
 Spec extension: a graph node may carry ``rank: r`` -- the torch.distributed
 rank (= GPU) whose process hosts that node's row model.  Rank 0 runs the front
@@ -26,22 +26,61 @@ from __future__ import annotations
 import os
 from typing import Any, Dict, List, Optional
 
-from .._native import native
+from .._native import gpu_count, native
 from ..serving.spec import SpecError, iter_nodes, load_spec, select_predictor
 
 
+def _control_links(rank: int, world: int, host: str = "127.0.0.1") -> List[int]:
+    """Star of host sockets rank 0 <-> every worker (the fabric's control
+    plane: batch headers).  Workers listen on an ephemeral port and publish it
+    over the default process group; rank 0 connects.  fds[r] = socket to rank r
+    (-1 where there is no link)."""
+    import socket
+
+    import torch.distributed as dist
+
+    lst = None
+    port = 0
+    if rank != 0:
+        lst = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        lst.bind((host, 0))
+        lst.listen(1)
+        port = lst.getsockname()[1]
+    ports = [None] * world
+    dist.all_gather_object(ports, port)
+    fds = [-1] * world
+    if rank == 0:
+        for r in range(1, world):
+            c = socket.create_connection((host, int(ports[r])))
+            c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            fds[r] = c.detach()
+    else:
+        c, _ = lst.accept()
+        c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        fds[0] = c.detach()
+        lst.close()
+    return fds
+
+
 def init_fabric(device: Optional[int] = None):
-    """Create the RCCL communicator for the current torch.distributed job
-    (the unique id is broadcast over the default process group)."""
+    """Create the fabric for the current torch.distributed job: control
+    sockets between rank 0 and every worker, plus (GPU ranks) an RCCL
+    communicator whose unique id is broadcast over the default process group.
+    ``device < 0`` (or no GPU) gives a CPU fabric: the same peer protocol with
+    the payloads on the sockets."""
     import torch.distributed as dist
 
     C = native()
     rank, world = dist.get_rank(), dist.get_world_size()
-    box = [C.rccl_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(box, src=0)
     if device is None:
-        device = int(os.environ.get("LOCAL_RANK", rank))
-    return C.Fabric(rank, world, box[0], device)
+        device = int(os.environ.get("LOCAL_RANK", rank)) if gpu_count() > 0 else -1
+    fds = _control_links(rank, world)
+    uid = b""
+    if device >= 0:
+        box = [C.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    return C.Fabric(rank, world, uid, int(device), fds)
 
 
 def node_rank(node: Dict) -> Optional[int]:

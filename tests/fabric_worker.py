@@ -1,0 +1,63 @@
+"""Rank process for tests/test_fabric.py (gloo + CPU fabric, device -1).
+
+Rank 0 serves a graph with nodes placed on other ranks (``rank: r``) through
+the native PeerRowModel, workers run the native PeerServer loop; rank 0 checks
+every answer against sklearn and prints one JSON line."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import numpy as np
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    import seldon_core_amd as sca
+    from seldon_core_amd.models import iris_logistic_regression
+    from seldon_core_amd.parallel.fabric import init_fabric, serve_peer
+
+    lr = iris_logistic_regression()
+    mode = sys.argv[1]
+    if mode == "combiner":  # K-way gather: one model per rank, averaged on rank 0
+        kids = [{"name": f"m{r}", "type": "MODEL", "rank": r} for r in range(world)]
+        graph = {"name": "comb", "type": "COMBINER", "implementation": "AVERAGE_COMBINER", "children": kids}
+        comps = {f"m{r}": lr for r in range(world)}
+    else:  # a single remote MODEL node on the last rank behind a local router
+        graph = {"name": "m", "type": "MODEL", "rank": world - 1}
+        comps = {"m": lr}
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}], "graph": graph}
+    fabric = init_fabric(device=-1)
+    assert not fabric.gpu
+    if rank != 0:
+        srv = serve_peer(spec, fabric, comps)
+        srv.join()
+        print(json.dumps({"rank": rank, "batches": srv.batches, "rows": srv.rows, "host_syncs": srv.host_syncs,
+                          "error": srv.error()}), flush=True)
+        fabric.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    dep = sca.Deployment(spec, components=comps, device=-1, fabric=fabric)
+    rng = np.random.default_rng(0)
+    worst = 0.0
+    n = 0
+    for i in range(40):
+        X = rng.normal(loc=4.0, scale=1.5, size=(1 + i % 5, 4))
+        out = dep.predict({"data": {"ndarray": X.tolist()}})
+        got = np.asarray(out["data"]["ndarray"])
+        worst = max(worst, float(np.abs(got - lr.predict_proba(X)).max()))
+        n += len(X)
+    kinds = {name: dep.engine.unit_kind(name) for name in dep.engine.node_names()}
+    dep.close()  # stops the workers' loops
+    fabric.close()
+    print(json.dumps({"rank": 0, "worst": worst, "rows": n, "kinds": kinds}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,6 +1,13 @@
-"""Cross-rank placement (RCCL fabric) -- the parts checkable without GPUs.
-The end-to-end RCCL path is exercised by tools/fabric_probe.py under torchrun
-on GPU boxes (one process per GPU)."""
+"""Cross-rank placement (fabric).  The peer protocol runs here end to end on
+CPU fabrics (gloo rendezvous, control + data over sockets, device -1) through
+the real native PeerRowModel / PeerServer state machines; the RCCL data plane
+is exercised by tools/fabric_probe.py under torchrun on GPU boxes."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
 import pytest
 
 import seldon_core_amd as sca
@@ -45,6 +52,53 @@ def test_worker_resolver_builds_row_models():
     kind, obj = res._resolve(spec["graph"]["children"][1])
     rm = res._row_model_of(res._instantiate(spec["graph"]["children"][1], obj))
     assert kind == "object" and rm is not None and rm.in_cols == 4 and rm.out_cols(4) == 3
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(world, mode):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "fabric_worker.py"), mode],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=180)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, e[-3000:]
+        outs.append(json.loads([line for line in o.splitlines() if line.startswith("{")][-1]))
+    return outs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_remote_model_node_cpu_fabric(world):
+    outs = _run_ranks(world, "single")
+    front = outs[0]
+    assert front["worst"] < 1e-12 and front["rows"] > 0
+    last = outs[-1]
+    assert last["error"] == "" and last["rows"] == front["rows"] and last["batches"] >= 1
+    assert last["host_syncs"] == 0  # CPU loop never waits on a device
+
+
+def test_combiner_gathers_from_every_rank_cpu_fabric():
+    outs = _run_ranks(3, "combiner")
+    assert outs[0]["worst"] < 1e-12
+    for w in outs[1:]:
+        assert w["error"] == "" and w["rows"] == outs[0]["rows"]
 
 
 def test_native_fabric_api_present():
