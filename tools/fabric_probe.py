@@ -6,7 +6,10 @@
 Rank 0 serves a graph whose MODEL children live on ranks 1..N-1 (plus one on
 rank 0), sends batches through the engine and checks every answer against the
 CPU reference of the same model; ranks > 0 run PeerServer loops.
-``--same-device`` puts every rank on GPU 0 (single-GPU rehearsal).
+``--same-device`` puts every rank on GPU 0: RCCL rejects two ranks on one
+device (ncclCommInitRank -> invalid usage, seen on the 1-GPU box), so it only
+checks the control-plane rendezvous; the CPU fabric tests (tests/test_fabric.py)
+run the whole peer protocol without GPUs.
 """
 import argparse
 import json
