@@ -1,5 +1,7 @@
 #include "engine.h"
 
+#include "roctx.h"
+
 #include "msglog.h"
 
 #include <algorithm>
@@ -364,6 +366,13 @@ std::vector<TraceSpan> Engine::drain_spans() {
 }
 
 Done Engine::traced(const std::shared_ptr<ReqCtx>& ctx, const Node* n, const char* what, Done k) {
+  if (trace::roctx_on()) {  // marker range around the node call, closed on whichever thread finishes it
+    const uint64_t id = trace::range_start((n->name + ":" + what).c_str());
+    k = [id, k = std::move(k)](Outcome o) {
+      trace::range_stop(id);
+      k(std::move(o));
+    };
+  }
   if (!ctx->traced) return k;
   const int64_t t0 = wall_us();
   std::string name = n->name + ":" + what;
@@ -502,10 +511,12 @@ void Engine::predict_local(MsgPtr req, Done k, ExecPtr exec) {
       ctx->t0_us = wall_us();
     }
   }
+  const uint64_t roctx_id = trace::roctx_on() ? trace::range_start("predictions") : 0;
   const bool log_pair = msglog_ && msglog_->wants_pairs();
   MsgPtr request_copy = (pair_hook_ || log_pair ? req : nullptr);
   const auto t_req = log_pair ? std::chrono::system_clock::now() : std::chrono::system_clock::time_point();
-  eval(root_, req, ctx, [this, ctx, k = std::move(k), request_copy, t_req, log_pair](Outcome o) {
+  eval(root_, req, ctx, [this, ctx, k = std::move(k), request_copy, t_req, log_pair, roctx_id](Outcome o) {
+    if (roctx_id) trace::range_stop(roctx_id);
     if (ctx->traced) {
       TraceSpan s;
       s.trace_id = ctx->trace_id;

@@ -75,6 +75,13 @@ uint64_t Histogram::count_le(double s) const {
   return acc;
 }
 
+void Histogram::copy_from(const Histogram& o) {
+  for (int b = 0; b < kBuckets; ++b) buckets_[b].store(o.buckets_[b].load(std::memory_order_relaxed));
+  count_.store(o.count_.load(std::memory_order_relaxed));
+  sum_bits_.store(o.sum_bits_.load(std::memory_order_relaxed));
+  max_bits_.store(o.max_bits_.load(std::memory_order_relaxed));
+}
+
 void Histogram::reset() {
   for (auto& b : buckets_) b.store(0);
   count_.store(0);

@@ -30,6 +30,7 @@ class Histogram {
   double sum() const;
   double max() const;
   uint64_t count_le(double seconds) const;
+  void copy_from(const Histogram& o);  // snapshot (scrape-time export of a unit's own histogram)
   void reset();
 
  private:

@@ -1,5 +1,7 @@
 #include "batcher.h"
 
+#include "../core/roctx.h"
+
 #include <immintrin.h>
 
 #include <algorithm>
@@ -359,7 +361,11 @@ bool BatchedUnit::launch(Slot* s) {
     launch_error = ex.what();
   }
   s->t_launch = std::chrono::steady_clock::now();
-  if (err == hipSuccess) return true;
+  if (err == hipSuccess) {
+    if (trace::roctx_on())
+      s->roctx = trace::range_start((model_->name() + " batch rows=" + std::to_string(rows)).c_str());
+    return true;
+  }
   auto e = device_error(ApiError::EXECUTION_FAILURE,
                         "GPU launch failed: " + (launch_error.empty() ? std::string(hipGetErrorString(err)) : launch_error));
   note_failure();
@@ -371,6 +377,12 @@ bool BatchedUnit::launch(Slot* s) {
 
 void BatchedUnit::complete(Slot* s, hipError_t st) {
   const double busy = std::chrono::duration<double>(std::chrono::steady_clock::now() - s->t_launch).count();
+  if (s->roctx) {
+    trace::range_stop(s->roctx);
+    s->roctx = 0;
+  }
+  batch_hist_.observe(busy);
+  rows_hist_.observe(double(s->rows) * 1e-6);
   if (s->abandoned) {  // the watchdog already answered these requests
     s->abandoned = false;
     abandoned_slots_.fetch_sub(1, std::memory_order_relaxed);
@@ -630,6 +642,12 @@ void BatchedUnit::collect_metrics(MetricsRegistry& m, const Labels& labels) cons
   m.counter("seldon_gpu_failed_batches", l)->set(double(h.failed_batches));
   m.counter("seldon_gpu_hangs", l)->set(double(h.hangs));
   m.counter("seldon_gpu_unhealthy_trips", l)->set(double(h.trips));
+  // per-unit kernel-time histogram (launch -> completion event of each batch)
+  // and batch-size distribution
+  m.timer("seldon_gpu_batch_device", l, true)->hist.copy_from(batch_hist_);
+  Series* rows = m.gauge("seldon_gpu_batch_rows_p50", l);
+  rows->set(rows_hist_.quantile(0.5) * 1e6);
+  m.gauge("seldon_gpu_batch_rows_p99", l)->set(rows_hist_.quantile(0.99) * 1e6);
 }
 
 void BatchedUnit::reset_stats() {

@@ -149,6 +149,7 @@ class BatchedUnit : public Unit {
     int cols = 0;
     int out_cols = 0;
     bool abandoned = false;  // watchdog answered its requests; waiting for the device to finish
+    uint64_t roctx = 0;      // marker range of the batch (SCA_ROCTX=1)
     std::chrono::steady_clock::time_point t_launch;
   };
 
@@ -166,6 +167,8 @@ class BatchedUnit : public Unit {
 
   RowModelPtr model_;
   BatcherOptions opts_;
+  Histogram batch_hist_;  // device time per batch (launch -> completion event), exported at scrape time
+  Histogram rows_hist_;   // rows per batch (observed as "seconds" = rows * 1e-6 for the shared bucket grid)
   std::shared_ptr<const RespInfo> resp_;
   std::vector<std::unique_ptr<Slot>> slots_;
   std::mutex mu_;

@@ -96,3 +96,13 @@ def test_device_graph_through_batched_cpu_path():
     finally:
         fused.close()
         plain.close()
+
+
+def test_batch_device_time_histogram_exported(served):
+    """Per-unit kernel-time histogram + batch-size quantiles on /prometheus."""
+    dep, h, clf = served
+    for _ in range(3):
+        dep.predict({"data": {"ndarray": [[5.1, 3.5, 1.4, 0.2]]}})
+    body = urllib.request.urlopen(f"http://127.0.0.1:{h.http_port}/prometheus", timeout=10).read().decode()
+    assert "# TYPE seldon_gpu_batch_device_seconds histogram" in body
+    assert 'seldon_gpu_batch_device_seconds_bucket{' in body and "seldon_gpu_batch_rows_p99" in body

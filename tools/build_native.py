@@ -32,7 +32,7 @@ NGHTTP2_LIB = Path("/opt/conda/lib/libnghttp2.so.14")
 
 LIB_SOURCES = [
     "core/json.cc", "core/message.cc", "core/pbwire.cc", "core/spec.cc", "core/metrics.cc",
-    "core/engine.cc", "core/units.cc", "core/msglog.cc",
+    "core/engine.cc", "core/units.cc", "core/msglog.cc", "core/roctx.cc",
     "server/http_server.cc", "server/grpc_server.cc", "server/remote_unit.cc",
     "gpu/models.cc", "gpu/batcher.cc", "gpu/router.cc", "gpu/graph.cc", "gpu/replica.cc", "gpu/mlp_model.cc", "gpu/lstm_model.cc", "gpu/maha_device.cc", "parallel/fabric.cc",
     "kernels/linear.hip", "kernels/tree.hip", "kernels/combine.hip", "kernels/bandit.hip", "kernels/image.hip", "kernels/mlp.hip", "kernels/mahalanobis.hip", "kernels/lstm.hip", "kernels/gemm.hip",
@@ -130,7 +130,7 @@ def build(jobs: int = 8, verbose: bool = False) -> Path:
     newest = max(o.stat().st_mtime for o in objs)
     if not out.exists() or out.stat().st_mtime < newest:
         cmd = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
-               "-o", str(out), f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", str(ng),
+               "-o", str(out), f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", str(ng),
                "-Wl,-rpath,$ORIGIN/lib", f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"]
         if verbose:
             print(" ".join(cmd), flush=True)
