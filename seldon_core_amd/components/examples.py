@@ -12,7 +12,8 @@ backed by the engine's GPU kernels when they sit in a graph:
 * ``ImageNetTransformer`` / ``ImageNetCombiner`` / ``ImageNetOutputTransformer``
   -- examples/models/openvino_imagenet_ensemble/resources/{transformer,combiner}:
   JPEG decode on the host, centre crop / resize / HWC->CHW on the GPU
-  (``crop_resize_chw`` kernel), average of two model outputs, argmax -> class name.
+  (``crop_resize_chw`` kernel), average of two model outputs
+  (``combine_mean_f64``), argmax -> class name (``argmax_rows_f64``).
 """
 from __future__ import annotations
 
@@ -143,15 +144,46 @@ class ImageNetTransformer:
         return {"data": {"names": ["x"], "tftensor": _tftensor_json(X)}}
 
 
+def _gpu_device(device: Optional[int]) -> Optional[int]:
+    """GPU ordinal for a component's kernels, or None (CPU placement / no GPU)."""
+    if device is not None and device < 0:
+        return None
+    try:
+        import torch
+
+        return (device or 0) if torch.cuda.is_available() else None
+    except Exception:
+        return None
+
+
 @register("IMAGENET_COMBINER")
 class ImageNetCombiner:
+    """Average of the two model outputs (resources/combiner: (Xs[0] + Xs[1]) / 2)
+    -- on a GPU the ``combine_mean_f64`` kernel (csrc/kernels/combine.hip)."""
+
+    def __init__(self, device: Optional[int] = None):
+        self.device = device
+        self.gpu_calls = 0
+
     def aggregate(self, Xs, features_names):
+        dev = _gpu_device(self.device)
+        if dev is not None:
+            import torch
+
+            from .. import ops
+
+            ts = [torch.as_tensor(np.reshape(np.asarray(x, dtype=np.float64), (1, -1)), device=f"cuda:{dev}")
+                  for x in Xs[:2]]
+            self.gpu_calls += 1
+            return ops.combine_mean(ts).cpu().numpy()
         return (np.reshape(Xs[0], (1, -1)) + np.reshape(Xs[1], (1, -1))) / 2.0
 
 
 @register("IMAGENET_OUTPUT_TRANSFORMER")
 class ImageNetOutputTransformer:
-    def __init__(self, classes: int = 1000, class_names_path: str = ""):
+    def __init__(self, classes: int = 1000, class_names_path: str = "", device: Optional[int] = None):
+        self.device = device
+        self.gpu_calls = 0
         self.classes = int(os.environ.get("CLASSES", classes))
         self.cnames: List[str] = [str(i) for i in range(self.classes)]
         if class_names_path and os.path.exists(class_names_path):
@@ -167,8 +199,18 @@ class ImageNetOutputTransformer:
             result = np.asarray(data["tensor"]["values"], dtype=float)
         else:
             result = np.asarray(data.get("ndarray"), dtype=float)
-        result = np.reshape(result, (1, self.classes))
-        return {"strData": self.cnames[int(np.argmax(result[0]))]}
+        result = np.reshape(np.asarray(result, dtype=np.float64), (1, self.classes))
+        dev = _gpu_device(self.device)
+        if dev is not None:  # argmax_rows_f64 kernel (first maximum, as np.argmax)
+            import torch
+
+            from .. import ops
+
+            self.gpu_calls += 1
+            idx = int(ops.argmax_rows(torch.as_tensor(result, device=f"cuda:{dev}")).cpu()[0])
+        else:
+            idx = int(np.argmax(result[0]))
+        return {"strData": self.cnames[idx]}
 
 
 class IrisClassifier:

@@ -92,10 +92,23 @@ def test_imagenet_transformer_cpu(hw):
 def test_imagenet_combiner_and_output():
     x0, x1 = np.zeros((1, 10)), np.zeros((1, 10))
     x0[0, 3], x1[0, 3] = 1.0, 0.5
-    avg = ImageNetCombiner().aggregate([x0, x1], [])
+    avg = ImageNetCombiner(device=-1).aggregate([x0, x1], [])
     assert avg.shape == (1, 10) and avg[0, 3] == 0.75
-    o = ImageNetOutputTransformer(classes=10)
+    o = ImageNetOutputTransformer(classes=10, device=-1)
     assert o.transform_output_raw({"data": {"ndarray": avg.tolist()}}) == {"strData": "3"}
+
+
+@pytest.mark.gpu
+def test_imagenet_combiner_and_output_on_kernels():
+    rng = np.random.default_rng(1)
+    x0, x1 = rng.normal(size=(1, 1000)), rng.normal(size=(1, 1000))
+    comb = ImageNetCombiner(device=0)
+    avg = comb.aggregate([x0, x1], [])
+    np.testing.assert_allclose(avg, (x0 + x1) / 2, rtol=0, atol=1e-15)
+    o = ImageNetOutputTransformer(classes=1000, device=0)
+    out = o.transform_output_raw({"data": {"tensor": {"shape": [1, 1000], "values": avg.ravel().tolist()}}})
+    assert out == {"strData": str(int(np.argmax(avg[0])))}
+    assert comb.gpu_calls == 1 and o.gpu_calls == 1
 
 
 @pytest.mark.gpu
