@@ -194,7 +194,40 @@ SERVICES = {
     "Seldon": {"Predict": ("SeldonMessage", "SeldonMessage"), "SendFeedback": ("Feedback", "SeldonMessage")},
 }
 
+def _build_tfserving(pool):
+    """``tensorflow_serving/apis/{model,predict,prediction_service}.proto``:
+    the subset the TF-Serving gRPC proxy speaks (Predict)."""
+    try:
+        pool.FindMessageTypeByName("tensorflow.serving.PredictRequest")
+        return
+    except KeyError:
+        pass
+    from google.protobuf import wrappers_pb2  # noqa: F401  (registers wrappers.proto in the default pool)
+
+    _map.pkg = "tensorflow.serving"
+    fd = descriptor_pb2.FileDescriptorProto(name="tensorflow_serving/apis/predict.proto",
+                                            package="tensorflow.serving", syntax="proto3",
+                                            dependency=["google/protobuf/wrappers.proto",
+                                                        "tensorflow/core/framework/tensor.proto"])
+    m = fd.message_type.add(name="ModelSpec")
+    _field(m, "name", 1, T_STRING)
+    _field(m, "version", 2, T_MESSAGE, type_name=".google.protobuf.Int64Value")
+    _field(m, "signature_name", 3, T_STRING)
+    m = fd.message_type.add(name="PredictRequest")
+    _field(m, "model_spec", 1, T_MESSAGE, type_name=".tensorflow.serving.ModelSpec")
+    _map(m, "inputs", 2, T_STRING, T_MESSAGE, ".tensorflow.TensorProto")
+    _field(m, "output_filter", 3, T_STRING, REP)
+    m = fd.message_type.add(name="PredictResponse")
+    _field(m, "model_spec", 2, T_MESSAGE, type_name=".tensorflow.serving.ModelSpec")
+    _map(m, "outputs", 1, T_STRING, T_MESSAGE, ".tensorflow.TensorProto")
+    s = fd.service.add(name="PredictionService")
+    s.method.add(name="Predict", input_type=".tensorflow.serving.PredictRequest",
+                 output_type=".tensorflow.serving.PredictResponse")
+    pool.Add(fd)
+
+
 _pool = _build()
+_build_tfserving(_pool)
 
 
 def _cls(full_name: str):
@@ -214,5 +247,9 @@ prediction_pb2 = SimpleNamespace(
     DESCRIPTOR=_pool.FindFileByName("prediction.proto"),
 )
 tensor_pb2 = SimpleNamespace(TensorProto=_cls("tensorflow.TensorProto"))
+predict_pb2 = SimpleNamespace(ModelSpec=_cls("tensorflow.serving.ModelSpec"),
+                              PredictRequest=_cls("tensorflow.serving.PredictRequest"),
+                              PredictResponse=_cls("tensorflow.serving.PredictResponse"))
+TFSERVING_PREDICT = "/tensorflow.serving.PredictionService/Predict"
 
-__all__ = ["prediction_pb2", "tensor_pb2", "SERVICES"]
+__all__ = ["prediction_pb2", "tensor_pb2", "predict_pb2", "SERVICES", "TFSERVING_PREDICT"]

@@ -187,6 +187,11 @@ def load_prepackaged(impl: str, model_uri: str, params: Dict[str, Any]):
         s = XGBoostServer(model_uri)
     elif impl == "MLFLOW_SERVER":
         s = MLFlowServer(model_uri)
+    elif impl == "TENSORFLOW_SERVER" and p.get("grpc_endpoint"):
+        from .proxies import TfServingGrpcProxy
+
+        kw = {k: p[k] for k in ("signature_name", "model_input", "model_output") if k in p}
+        return TfServingGrpcProxy(p["grpc_endpoint"], p.get("model_name", "model"), **kw)
     elif impl == "TENSORFLOW_SERVER":
         s = TFServingProxy(model_uri, rest_endpoint=p.get("rest_endpoint", ""), model_name=p.get("model_name", ""))
     else:

@@ -27,6 +27,10 @@ _TF_DTYPES = {
     "DT_BOOL": np.bool_, "DT_UINT16": np.uint16, "DT_HALF": np.float16, "DT_UINT32": np.uint32,
     "DT_UINT64": np.uint64, "DT_COMPLEX64": np.complex64, "DT_COMPLEX128": np.complex128,
 }
+_TF_ENUM = ["DT_INVALID", "DT_FLOAT", "DT_DOUBLE", "DT_INT32", "DT_UINT8", "DT_INT16", "DT_INT8", "DT_STRING",
+            "DT_COMPLEX64", "DT_INT64", "DT_BOOL", "DT_QINT8", "DT_QUINT8", "DT_QINT32", "DT_BFLOAT16", "DT_QINT16",
+            "DT_QUINT16", "DT_UINT16", "DT_COMPLEX128", "DT_HALF", "DT_RESOURCE", "DT_VARIANT", "DT_UINT32",
+            "DT_UINT64"]
 _TF_VALS = {
     "DT_FLOAT": "floatVal", "DT_DOUBLE": "doubleVal", "DT_INT32": "intVal", "DT_UINT8": "intVal",
     "DT_INT16": "intVal", "DT_INT8": "intVal", "DT_UINT16": "intVal", "DT_INT64": "int64Val",
@@ -46,8 +50,8 @@ def _camel_get(d: Dict, camel: str):
 
 def tftensor_to_array(t: Dict) -> np.ndarray:
     dtype_name = t.get("dtype", "DT_FLOAT")
-    if isinstance(dtype_name, int):
-        dtype_name = {v: k for k, v in enumerate(_TF_DTYPES)}.get(dtype_name, "DT_FLOAT")
+    if isinstance(dtype_name, int):  # enum number (tensorflow/core/framework/types.proto)
+        dtype_name = _TF_ENUM[dtype_name] if 0 <= dtype_name < len(_TF_ENUM) else "DT_INVALID"
     np_dtype = _TF_DTYPES.get(dtype_name)
     if np_dtype is None:
         raise SeldonMicroserviceException(f"Unsupported tftensor dtype {dtype_name}")

@@ -122,3 +122,13 @@ def test_number_formatting(C):
     vals = [0.1, 1e-300, 123456789.125, 1e22, -0.0, 5e-324, 2 ** 53]
     out = rt(C, {"data": {"tensor": {"shape": [len(vals)], "values": vals}}})
     assert out["data"]["tensor"]["values"] == vals
+
+
+def test_tftensor_enum_number_dtype():
+    """protobuf JSON may carry the DataType as its enum number (types.proto)."""
+    from seldon_core_amd.serving.codec import tftensor_to_array
+
+    shape = {"dim": [{"size": "2"}]}
+    assert tftensor_to_array({"dtype": 2, "tensorShape": shape, "doubleVal": [1.5, 2.5]}).dtype == np.float64
+    assert tftensor_to_array({"dtype": 9, "tensorShape": shape, "int64Val": ["3", "4"]}).tolist() == [3, 4]
+    assert tftensor_to_array({"dtype": 1, "tensorShape": shape, "floatVal": [1, 2]}).dtype == np.float32
