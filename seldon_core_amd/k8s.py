@@ -2,7 +2,10 @@
 P2; reference operator/controllers/seldondeployment_controller.go:253-636 --
 createComponents / createContainerService / createDeploymentWithoutEngine --,
 seldondeployment_engine.go:101-214 (engine container), ambassador.go:50-260
-(Mapping annotations) and seldondeployment_explainers.go:32-184).
+(Mapping annotations), seldondeployment_explainers.go:32-184 and, with
+``ISTIO_ENABLED=true`` / ``--istio``, the Istio VirtualServices +
+DestinationRules of seldondeployment_controller.go:111-225 and
+seldondeployment_explainers.go:196-290).
 
     python -m seldon_core_amd.k8s sdep.json [--namespace ns] > manifests.yaml
 
@@ -22,7 +25,12 @@ traffic zeroed, probes ``/ready`` / ``/live`` on the admin port, preStop
 annotations, 10% maxUnavailable, 20 s grace), predictor Service with the
 Ambassador REST + gRPC Mappings (weight, shadow, header / regex-header,
 ambassador-id, custom config), component Deployments / Services, HPAs from
-``hpaSpec``, explainer Deployment + Service.
+``hpaSpec``, explainer Deployment + Service; with Istio one ``-http`` and
+one ``-grpc`` VirtualService per deployment whose routes split traffic over
+the predictors (weight = ``traffic``, destination subset = predictor name on
+the engine's REST / gRPC port) and an ISTIO_MUTUAL DestinationRule per
+predictor Service selecting its ``version`` label; explainers get their own
+unsplit pair under ``/seldon/<ns>/<name>/<predictor>/explainer/``.
 """
 from __future__ import annotations
 
@@ -123,6 +131,45 @@ def _ambassador(sdep: Dict, predictor: Dict, svc: str, ns: str) -> str:
     return "".join("---\n" + d for d in docs)
 
 
+def istio_enabled() -> bool:
+    return os.environ.get("ISTIO_ENABLED", "false") == "true"
+
+
+def _vs_name(name: str) -> str:
+    return name[:63].rstrip("-")
+
+
+def _istio(sdep: Dict, ns: str, seldon_id: str, targets: List[Dict], prefix: str, mtls: bool = True) -> List[Dict]:
+    """VirtualServices (REST + gRPC) routing ``prefix`` / the Seldon gRPC
+    service to ``targets`` (``{"host", "subset", "weight", "version"}``), and
+    one DestinationRule per target host."""
+    ann = _annotations(sdep)
+    gateway = ann.get("seldon.io/istio-gateway", os.environ.get("ISTIO_GATEWAY", "seldon-gateway"))
+    name = sdep["metadata"]["name"]
+    base = targets[0]["vs"]
+
+    def route(port: int) -> List[Dict]:
+        return [{"destination": {"host": t["host"], "subset": t["subset"], "port": {"number": port}},
+                 "weight": t["weight"]} for t in targets]
+
+    http = {"match": [{"uri": {"prefix": prefix}}], "rewrite": {"uri": "/"}, "route": route(HTTP_PORT)}
+    grpc = {"match": [{"uri": {"prefix": "/seldon.protos.Seldon/"},
+                       "headers": {"seldon": {"exact": name}, "namespace": {"exact": ns}}}],
+            "route": route(GRPC_PORT)}
+    out = []
+    for suffix, rt in (("http", http), ("grpc", grpc)):
+        out.append({"apiVersion": "networking.istio.io/v1alpha3", "kind": "VirtualService",
+                    "metadata": _meta(_vs_name(f"{base}-{suffix}"), ns, {LABEL_ID: seldon_id}),
+                    "spec": {"hosts": ["*"], "gateways": [gateway], "http": [rt]}})
+    for t in targets:
+        spec = {"host": t["host"], "subsets": [{"name": t["subset"], "labels": {"version": t["version"]}}]}
+        if mtls:
+            spec["trafficPolicy"] = {"tls": {"mode": "ISTIO_MUTUAL"}}
+        out.append({"apiVersion": "networking.istio.io/v1alpha3", "kind": "DestinationRule",
+                    "metadata": _meta(t["host"], ns, {LABEL_ID: seldon_id}), "spec": spec})
+    return out
+
+
 def _meta(name: str, ns: str, labels: Dict[str, str], annotations: Optional[Dict[str, str]] = None) -> Dict:
     m = {"name": name, "namespace": ns, "labels": dict(labels)}
     if annotations:
@@ -205,12 +252,17 @@ def _unit_env(sdep: Dict, predictor: Dict, node: Dict, port: int) -> List[Dict]:
             {"name": "SELDON_DEPLOYMENT_ID", "value": sdep["metadata"]["name"]}]
 
 
-def render(sdep_in: Any, namespace: Optional[str] = None, bound: Optional[set] = None) -> List[Dict]:
-    """All objects for a SeldonDeployment (dict / JSON / YAML path)."""
+def render(sdep_in: Any, namespace: Optional[str] = None, bound: Optional[set] = None,
+           istio: Optional[bool] = None) -> List[Dict]:
+    """All objects for a SeldonDeployment (dict / JSON / YAML path).
+    ``istio`` defaults to the operator's ``ISTIO_ENABLED`` environment flag."""
     sdep = apply_defaults(copy.deepcopy(load_spec(sdep_in)))
     ns = namespace or (sdep.get("metadata") or {}).get("namespace") or "default"
     seldon_id = naming.sdep_name(sdep)
+    istio = istio_enabled() if istio is None else istio
     out: List[Dict] = []
+    routes: List[Dict] = []
+    n_pred = len(predictors(sdep))
     for p in predictors(sdep):
         ann = _annotations(sdep, p)
         version = (p.get("labels") or {}).get("version", p["name"])
@@ -237,6 +289,8 @@ def render(sdep_in: Any, namespace: Optional[str] = None, bound: Optional[set] =
                             [{"protocol": "TCP", "port": HTTP_PORT, "targetPort": HTTP_PORT, "name": "http"},
                              {"protocol": "TCP", "port": GRPC_PORT, "targetPort": GRPC_PORT, "name": "grpc"}],
                             svc_ann, headless=ann.get("seldon.io/headless-svc", "false") != "false"))
+        routes.append({"vs": seldon_id, "host": svc, "subset": p["name"], "version": version,
+                       "weight": 100 if n_pred <= 1 else int(p.get("traffic", 0) or 0)})
         # ---- external component containers (reference layout)
         for cs in p.get("componentSpecs") or []:
             containers = [c for c in ((cs.get("spec") or {}).get("containers") or []) if c.get("name") in ext]
@@ -295,13 +349,20 @@ def render(sdep_in: Any, namespace: Optional[str] = None, bound: Optional[set] =
             tcp = {"tcpSocket": {"port": port}, "periodSeconds": 5, "timeoutSeconds": 1, "successThreshold": 1}
             c.setdefault("readinessProbe", dict(tcp, initialDelaySeconds=20, failureThreshold=7))
             c.setdefault("livenessProbe", dict(tcp, initialDelaySeconds=60, failureThreshold=5))
-            xl = {LABEL_APP: xname, LABEL_ID: seldon_id, "app.kubernetes.io/managed-by": "seldon-core-amd"}
+            xl = {LABEL_APP: xname, LABEL_ID: seldon_id, "version": version,
+                  "app.kubernetes.io/managed-by": "seldon-core-amd"}
             out.append(_deployment(xname, ns, xl, {"containers": [c]}, 1))
             out.append(_service(xname, ns, {LABEL_APP: xname, LABEL_ID: seldon_id}, xname,
                                 [{"protocol": "TCP", "port": port, "targetPort": port, "name": "http"}],
                                 {AMBASSADOR_ANNOTATION: _ambassador(
                                     {**sdep, "metadata": {**sdep["metadata"], "name": sdep["metadata"]["name"] +
                                                           "-explainer"}}, p, xname, ns)}))
+            if istio:
+                out += _istio(sdep, ns, seldon_id,
+                              [{"vs": xname, "host": xname, "subset": p["name"], "version": version, "weight": 100}],
+                              f"/seldon/{ns}/{sdep['metadata']['name']}/{p['name']}/explainer/", mtls=False)
+    if istio and routes:
+        out += _istio(sdep, ns, seldon_id, routes, f"/seldon/{ns}/{sdep['metadata']['name']}/")
     return out
 
 
@@ -309,8 +370,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap = argparse.ArgumentParser(prog="seldon-amd-k8s")
     ap.add_argument("spec")
     ap.add_argument("--namespace", default=None)
+    ap.add_argument("--istio", action="store_true", default=None,
+                    help="also render Istio VirtualServices / DestinationRules (default: $ISTIO_ENABLED)")
     a = ap.parse_args(argv)
-    sys.stdout.write(yaml.safe_dump_all(render(a.spec, a.namespace), sort_keys=False))
+    sys.stdout.write(yaml.safe_dump_all(render(a.spec, a.namespace, istio=a.istio), sort_keys=False))
     return 0
 
 

@@ -133,3 +133,48 @@ def test_examples_render_and_cli(capsys):
     assert k8s.main([os.path.join(ROOT, "examples", "abtest.json"), "--namespace", "x"]) == 0
     docs = [d for d in yaml.safe_load_all(capsys.readouterr().out) if d]
     assert all(d["metadata"]["namespace"] == "x" for d in docs)
+
+
+def test_istio_virtual_services_split_traffic(monkeypatch):
+    """createIstioResources (seldondeployment_controller.go:111-225): one REST
+    and one gRPC VirtualService, a weighted route per predictor, one
+    ISTIO_MUTUAL DestinationRule per predictor Service selecting its version."""
+    sd = _sdep([_pred("a", 75, labels={"version": "v1"}), _pred("b", 25, labels={"version": "v2"})])
+    assert not _by_kind(k8s.render(sd), "VirtualService")  # ISTIO_ENABLED unset
+    monkeypatch.setenv("ISTIO_ENABLED", "true")
+    objs = k8s.render(sd, namespace="ns1")
+    vs = {v["metadata"]["name"]: v["spec"] for v in _by_kind(objs, "VirtualService")}
+    assert set(vs) == {"mymodel-mymodel-http", "mymodel-mymodel-grpc"}  # seldonId + suffix
+    http, grpc = vs["mymodel-mymodel-http"], vs["mymodel-mymodel-grpc"]
+    assert http["gateways"] == ["seldon-gateway"] and http["hosts"] == ["*"]
+    assert http["http"][0]["match"][0]["uri"]["prefix"] == "/seldon/ns1/mymodel/"
+    assert http["http"][0]["rewrite"] == {"uri": "/"}
+    assert grpc["http"][0]["match"][0]["headers"] == {"seldon": {"exact": "mymodel"}, "namespace": {"exact": "ns1"}}
+    svcs = {s["metadata"]["name"] for s in _by_kind(objs, "Service")}
+    for rt, port in ((http, 8000), (grpc, 5001)):
+        r = rt["http"][0]["route"]
+        assert [(d["destination"]["subset"], d["weight"]) for d in r] == [("a", 75), ("b", 25)]
+        assert all(d["destination"]["port"]["number"] == port and d["destination"]["host"] in svcs for d in r)
+    drs = _by_kind(objs, "DestinationRule")
+    assert sorted(d["spec"]["subsets"][0]["labels"]["version"] for d in drs) == ["v1", "v2"]
+    assert all(d["spec"]["trafficPolicy"]["tls"]["mode"] == "ISTIO_MUTUAL" for d in drs)
+    # the subset's version label is what the engine pods carry
+    deps = {d["metadata"]["name"]: d for d in _by_kind(objs, "Deployment")}
+    versions = {d["spec"]["template"]["metadata"]["labels"].get("version") for d in deps.values()}
+    assert {"v1", "v2"} <= versions
+
+
+def test_istio_gateway_annotation_and_explainer(monkeypatch):
+    monkeypatch.setenv("ISTIO_ENABLED", "true")
+    monkeypatch.setenv("ISTIO_GATEWAY", "envgw")
+    p = _pred(explainer={"type": "anchor_tabular"})
+    objs = k8s.render(_sdep([p]), namespace="s")
+    vs = {v["metadata"]["name"]: v["spec"] for v in _by_kind(objs, "VirtualService")}
+    assert vs["mymodel-mymodel-http"]["gateways"] == ["envgw"]
+    assert vs["mymodel-mymodel-http"]["http"][0]["route"][0]["weight"] == 100  # single predictor
+    xhttp = [v for n, v in vs.items() if "explainer" in n and n.endswith("-http")][0]
+    assert xhttp["http"][0]["match"][0]["uri"]["prefix"] == "/seldon/s/mymodel/p/explainer/"
+    xdr = [d for d in _by_kind(objs, "DestinationRule") if "explainer" in d["metadata"]["name"]][0]
+    assert "trafficPolicy" not in xdr["spec"]
+    objs = k8s.render(_sdep([_pred()], {"seldon.io/istio-gateway": "ns/gw"}), istio=True)
+    assert _by_kind(objs, "VirtualService")[0]["spec"]["gateways"] == ["ns/gw"]
