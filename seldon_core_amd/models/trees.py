@@ -21,7 +21,6 @@ components/outlier-detection/isolation-forest/CoreIsolationForest.py:62-76.
 """
 from __future__ import annotations
 
-import json
 import math
 from dataclasses import dataclass, field
 from pathlib import Path
@@ -200,15 +199,20 @@ def _avg_path_length(n: np.ndarray) -> np.ndarray:
 
 
 # ------------------------------------------------------------------ XGBoost
-def from_xgboost_json(model: Union[str, Path, Dict]) -> TreeEnsemble:
-    """Import an XGBoost JSON model (``Booster.save_model('model.json')``)."""
+def from_xgboost_json(model: Union[str, Path, bytes, Dict]) -> TreeEnsemble:
+    """Import an XGBoost model: JSON (``Booster.save_model('model.json')``),
+    or -- decoded to the same schema by :mod:`.xgb_binary` -- UBJSON
+    (``model.ubj``) and the legacy binary ``model.bst``."""
     if not isinstance(model, dict):
-        model = json.loads(Path(model).read_text())
+        from .xgb_binary import load_xgboost_model
+
+        model = load_xgboost_model(model)
     learner = model["learner"]
     lmp = learner.get("learner_model_param", {})
     n_features = int(lmp.get("num_feature", 0))
     num_class = int(lmp.get("num_class", 0) or 0)
-    base_score = float(lmp.get("base_score", 0.5))
+    bs = lmp.get("base_score", 0.5)
+    base_score = float(bs.strip("[]").split(",")[0]) if isinstance(bs, str) else float(bs)  # 2.x: "[5E-1]"
     objective = learner.get("objective", {}).get("name", "reg:squarederror")
     gb = learner["gradient_booster"]
     if gb.get("name") not in ("gbtree", "dart"):

@@ -21,7 +21,7 @@ from ..utils.storage import Storage
 logger = logging.getLogger(__name__)
 
 JOBLIB_FILE = "model.joblib"
-XGB_JSON_FILES = ("model.json", "model.bst.json")
+XGB_JSON_FILES = ("model.json", "model.bst.json", "model.ubj", "model.bst")
 
 
 class SKLearnServer:
@@ -56,11 +56,9 @@ class SKLearnServer:
 
 
 class XGBoostServer:
-    """XGBoost booster from ``<modelUri>/model.json`` (XGBoost JSON schema).
-
-    The binary ``model.bst`` format needs the xgboost library (not available
-    on this platform); save models with ``Booster.save_model('model.json')``.
-    """
+    """XGBoost booster from ``<modelUri>/model.{json,ubj,bst}``: XGBoost JSON,
+    UBJSON or the legacy binary format (decoded without the xgboost library,
+    ``models/xgb_binary.py``)."""
 
     def __init__(self, model_uri: str = "", ensemble=None):
         self.model_uri = model_uri
@@ -76,7 +74,7 @@ class XGBoostServer:
             if os.path.isdir(root):
                 cands = [os.path.join(root, f) for f in XGB_JSON_FILES if os.path.exists(os.path.join(root, f))]
                 if not cands:
-                    raise FileNotFoundError(f"no XGBoost JSON model ({', '.join(XGB_JSON_FILES)}) in {root}")
+                    raise FileNotFoundError(f"no XGBoost model ({', '.join(XGB_JSON_FILES)}) in {root}")
                 path = cands[0]
             self._ens = from_xgboost_json(path)
         self.ready = True
