@@ -40,7 +40,6 @@ import logging
 import os
 import ssl
 import threading
-import time
 import urllib.error
 import urllib.request
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
@@ -48,7 +47,7 @@ from typing import Any, Dict, Iterable, List, Optional, Tuple
 
 from . import k8s
 from .serving import naming
-from .serving.spec import apply_defaults, predictors, validate
+from .serving.spec import apply_defaults, validate
 
 logger = logging.getLogger(__name__)
 
@@ -339,11 +338,17 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--webhook-port", type=int, default=0)
     ap.add_argument("--cert", default=None)
     ap.add_argument("--key", default=None)
+    ap.add_argument("--usage-database", default=None,
+                    help="opt-in anonymous usage reports (spartakus format) to this URL")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     client = KubeClient(a.api) if a.api else KubeClient.in_cluster()
     if a.webhook_port:
         webhook_server(port=a.webhook_port, cert=a.cert, key=a.key)
+    if a.usage_database:
+        from .usage import UsageReporter
+
+        UsageReporter(client, a.usage_database).start()
     Reconciler(client, a.namespace).run(a.resync)
     return 0
 

@@ -177,3 +177,43 @@ def test_webhook_server_paths():
             assert json.loads(urllib.request.urlopen(req, timeout=10).read())["response"]["uid"] == "x"
     finally:
         srv.shutdown()
+
+
+def test_usage_report_spartakus_format(api):
+    import http.server
+
+    from seldon_core_amd.usage import UsageReporter
+
+    fa, client = api
+    fa.objs[("nodes", None, "n1")] = {"metadata": {"name": "n1", "uid": "u1"},
+                                      "status": {"nodeInfo": {"operatingSystem": "linux", "architecture": "amd64",
+                                                              "kernelVersion": "6.8"},
+                                                 "capacity": {"cpu": "256", "memory": "2Ti", "amd.com/gpu": "8",
+                                                              "pods": "110"}}}
+    fa.objs[("seldondeployments", "ns1", "m")] = _sdep([_pred("a", 100)], name="m")
+    got = []
+
+    class Collector(http.server.BaseHTTPRequestHandler):
+        def do_POST(self):
+            got.append(json.loads(self.rfile.read(int(self.headers["Content-Length"]))))
+            self.send_response(201)
+            self.send_header("Content-Length", "0")
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.HTTPServer(("127.0.0.1", 0), Collector)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        r = UsageReporter(client, f"http://127.0.0.1:{srv.server_port}")
+        assert r.report_once()
+    finally:
+        srv.shutdown()
+    rep, = got
+    assert rep["version"] == "v1" and rep["clusterID"] == r.cluster_id
+    node, = rep["nodes"]
+    assert node["architecture"] == "amd64" and {"resource": "amd.com/gpu", "value": "8"} in node["capacity"]
+    assert "n1" not in json.dumps(rep) and "ns1" not in json.dumps(rep)  # anonymous
+    assert {"name": "seldondeployments", "value": "1"} in rep["extensions"]
+    assert not UsageReporter(client, "http://127.0.0.1:9").report_once()  # unreachable: no exception
