@@ -29,7 +29,7 @@ CSRC = ROOT / "csrc"
 BUILD = ROOT / "build" / "san"
 SOURCES = [
     "core/json.cc", "core/message.cc", "core/pbwire.cc", "core/spec.cc", "core/metrics.cc",
-    "core/engine.cc", "core/units.cc", "core/msglog.cc",
+    "core/engine.cc", "core/units.cc", "core/msglog.cc", "core/roctx.cc",
     "server/http_server.cc", "server/grpc_server.cc", "server/remote_unit.cc",
     "tests/core_stress.cc",
 ]
@@ -57,7 +57,7 @@ def _compile(kind: str, src_rel: str, inc: Path) -> Path:
     if fresh:
         return obj
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Wall", "-Wno-unused-function",
-           *FLAGS[kind], f"-I{CSRC}", f"-I{inc}", "-MMD", "-MF", str(dep), "-c", str(src), "-o", str(obj)]
+           *FLAGS[kind], f"-I{CSRC}", f"-I{inc}", "-I/opt/rocm/include", "-MMD", "-MF", str(dep), "-c", str(src), "-o", str(obj)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"[{kind}] compile failed: {src_rel}\n{res.stderr}")
@@ -70,7 +70,8 @@ def build(kind: str, jobs: int = 8) -> Path:
         objs = list(ex.map(lambda s: _compile(kind, s, inc), SOURCES))
     out = BUILD / kind / "core_stress"
     if not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
-        cmd = ["g++", *FLAGS[kind], *map(str, objs), str(ng), f"-Wl,-rpath,{ng.parent}", "-lpthread", "-o", str(out)]
+        cmd = ["g++", *FLAGS[kind], *map(str, objs), str(ng), f"-Wl,-rpath,{ng.parent}",
+               "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lpthread", "-o", str(out)]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"[{kind}] link failed\n{res.stderr}")
