@@ -383,14 +383,30 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed(d: Dist, fn):
+def cpu_seconds() -> tuple:
+    """(this process: front end + device thread + Python, reaped children:
+    the load generator) user+sys CPU seconds."""
+    import resource
+
+    me = resource.getrusage(resource.RUSAGE_SELF)
+    ch = resource.getrusage(resource.RUSAGE_CHILDREN)
+    return me.ru_utime + me.ru_stime, ch.ru_utime + ch.ru_stime
+
+
+def timed(d: Dist, fn, cpu: dict | None = None):
     d.barrier()
     d.sync()
+    c0 = cpu_seconds()
     t0 = time.perf_counter()
     out = fn()
     d.sync()
+    wall = time.perf_counter() - t0
+    if cpu is not None:  # CPUs busy over the window, server side vs load generator
+        c1 = cpu_seconds()
+        cpu["server_cpus"] = round((c1[0] - c0[0]) / wall, 2)
+        cpu["loadgen_cpus"] = round((c1[1] - c0[1]) / wall, 2)
     d.barrier()
-    return out, time.perf_counter() - t0
+    return out, wall
 
 
 def measure_variant(args, d: Dist, wl: Workload, kind: str, spin: bool) -> dict:
@@ -479,10 +495,11 @@ def main() -> None:
         run_loadgen(args, port, args.warmup, 0, args.api, body)
     for u in dep.batched.values():
         u.reset_stats()
-    lg, wall = timed(d, lambda: run_loadgen(args, port, args.steps, 0, args.api, body))
+    cpu: dict = {}
+    lg, wall = timed(d, lambda: run_loadgen(args, port, args.steps, 0, args.api, body), cpu)
     st = unit_stats(dep)
     mine = {"rank": d.rank, "device": d.device, "ok": lg["ok"], "wall": wall, "p50": lg["p50_ms"],
-            "p99": lg["p99_ms"], "stats": st, "cpu_budget": round(per_rank_cpus, 2)}
+            "p99": lg["p99_ms"], "stats": st, "cpu_budget": round(per_rank_cpus, 2), "cpu": cpu}
     extras: dict = {}
     failures = []
     # ---- after the timed region: correctness + extra configs
@@ -520,7 +537,7 @@ def summarize(args, d: Dist, results, label: str, wl: Workload) -> dict:
     value = sum(m["ok"] for m in mines) / wall_max
     base = REST_BASELINE if args.api == "rest" else GRPC_BASELINE
     st0 = mines[0]["stats"]
-    per_rank = [{"rank": m["rank"], "device": m["device"], "cpu_budget": m["cpu_budget"],
+    per_rank = [{"rank": m["rank"], "device": m["device"], "cpu_budget": m["cpu_budget"], **m["cpu"],
                  "rps": round(m["ok"] / m["wall"], 1), "p50_ms": m["p50"], "p99_ms": m["p99"],
                  "gpu_batches": m["stats"]["batches"],
                  "mean_rows_per_batch": round(m["stats"]["rows"] / max(1, m["stats"]["batches"]), 2),

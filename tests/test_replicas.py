@@ -71,5 +71,12 @@ def test_gpu_replica_matches_sklearn():
         for _ in range(8):
             out = dep.predict({"data": {"ndarray": X.tolist()}})
             np.testing.assert_allclose(np.array(out["data"]["ndarray"]), lr.predict_proba(X), rtol=1e-12)
+        st = dep.batched["clf"].stats()
+        devs = [e["device"] for e in st["per_device"]]
+        # replicas land on N consecutive GPUs: distinct devices whenever the box has them
+        assert devs == [i % n for i in range(max(2, n))], devs
+        assert len(set(devs)) == min(n, max(2, n))
+        # sequential requests take turns over idle replicas, so every GPU served some
+        assert all(e["batches"] > 0 for e in st["per_device"]), st["per_device"]
     finally:
         dep.close()
