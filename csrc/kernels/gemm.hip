@@ -12,6 +12,8 @@
 // fragment TN -- the layer kernel with 16x16 per wave issued 1 per B load.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 #include "philox.h"
 
@@ -164,17 +166,34 @@ __global__ __launch_bounds__(64) void dense_gemm_kernel(const DenseGemmArgs a) {
 }
 
 // ---- bf16: LDS-tiled GEMM.  A 256-thread workgroup (2 x 2 waves) owns a
-// 128 x BN output tile (BN = 64 is launched: two resident workgroups per CU).  Per 64-wide K stage the A and W panels (128 B per row) are
-// staged in LDS with full-line 16-B loads; each wave reads its 4 + BN/32
-// fragments with ds_read_b128 and issues 8 * BN/32 MFMAs (16x16x32 bf16).
+// BM x BN output tile (BM = 128 or 32, BN = 64).  Per 64-wide K stage the A and
+// W panels (128 B per row) are staged in LDS with full-line 16-B loads; each
+// wave reads its BM/32 + BN/32 fragments with ds_read_b128 and issues
+// (BM/32) * (BN/32) MFMAs (16x16x32 bf16) per 32-deep step.
 // The LDS row stride is 144 B (128 + 16): the 16 lanes of a ds_read_b128
 // group read 16 rows at one k-chunk, which land on 16 distinct 16-B slots of
 // the 256-B bank row (row * 9 mod 16) -- conflict-free.  Global loads run two
 // stages ahead (two register sets) into two LDS buffers: the L2 / HBM round
-// trip of stage k+2 overlaps the MFMAs of stages k and k+1 (one stage of
-// ~512 MFMA cycles alone does not cover it: profiles/r02d_dense).  W is
-// row-major [Npb][Kpb] bf16 (Kpb, Npb multiples of 64, zero padded).
-constexpr int kBM = 128, kBK = 64, kLdr = kBK + 8;  // row stride in bf16 elements
+// trip of stage k+2 overlaps the MFMAs of stages k and k+1.
+//
+// Grid: 1-D, remapped XCD-aware.  Workgroups are dealt round-robin over the 8
+// XCDs (each with its own L2), so with a 2-D (N, M) grid the N tiles that share
+// one A panel landed on 8 different XCDs and every A panel came from HBM 8
+// times (r02d: 27 us for 8192 x 784 x 512 at ~6 TB/s of mostly redundant
+// traffic).  The remap gives each XCD a contiguous run of tiles in (m, n)
+// order, n fastest: an A panel is fetched from HBM once and then hit in that
+// XCD's L2 by its other N tiles; W (<= 1 MB) stays L2-resident everywhere.
+//
+// Measured on MI355X (profiles/r02h_gemm): MLP 784-512-256-10 @ 8192 rows,
+// layer 1 26.9 -> 23.7 us, layer 2 15.7 -> 14.6 us with the remap
+// (SCA_GEMM_REMAP=0 restores the plain order for A/B runs); the 10-wide head
+// 9.4 -> 6.0 us on 32 x 64 tiles.  Converting the fp64 batch while staging
+// layer 1 (instead of the separate convert pass) measured 71-79 us vs 24 + 19:
+// 4x the staging loads per chunk serialise the two-stage register pipeline.
+//
+// AMODE 0: A is bf16 [rows][lda]; 2: VAE reparameterised z from H.
+// W is row-major [Npb][Kpb] bf16 (Kpb, Npb multiples of 64, zero padded).
+constexpr int kBK = 64, kLdr = kBK + 8;  // row stride in bf16 elements
 
 template <int AMODE>
 __device__ __forceinline__ bf16x8 stage_a(const DenseGemmArgs& a, int row, int k) {
@@ -194,16 +213,26 @@ __device__ __forceinline__ bf16x8 stage_a(const DenseGemmArgs& a, int row, int k
   }
 }
 
-template <int AMODE, int BN>
+// bijective XCD-aware tile index for workgroup `L` of `nwg` (cdna guide §5)
+__device__ __forceinline__ int xcd_tile(int L, int nwg) {
+  const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+}
+
+template <int AMODE, int BM, int BN>
 __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs a) {
+  constexpr int TM = BM / 32;                 // 16-row tiles per wave (2 waves along M)
   constexpr int TN = BN / 32;                 // 16-col tiles per wave (2 waves along N)
-  constexpr int CA = kBM * 8 / 256;           // A staging chunks per thread (128 rows x 8 chunks)
+  constexpr int CA = BM * 8 / 256;            // A staging chunks per thread (BM rows x 8 chunks)
   constexpr int CW = BN * 8 / 256;            // W staging chunks per thread
-  constexpr int kBuf = (kBM + BN) * kLdr;     // one LDS buffer: A panel then W panel
+  constexpr int kBuf = (BM + BN) * kLdr;      // one LDS buffer: A panel then W panel
+  static_assert(CA >= 1 && CW >= 1, "tile too small for 256 stagers");
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * kBuf];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 1, wc = wave & 1, r16 = lane & 15, kq = lane >> 4;
-  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * BN;
+  const int nN = (a.Np + BN - 1) / BN;
+  const int t = a.xcd_remap ? xcd_tile(blockIdx.x, gridDim.x) : int(blockIdx.x);
+  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
   const __bf16* W = static_cast<const __bf16*>(a.W);
   const int KS = a.Kp / kBK;
   // two stages of staging registers; every index below is a compile-time
@@ -224,7 +253,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
   };
   auto lstore = [&](int buf, const bf16x8* ra, const bf16x8* rw) {
     __bf16* As = smem + buf * kBuf;
-    __bf16* Ws = As + kBM * kLdr;
+    __bf16* Ws = As + BM * kLdr;
 #pragma unroll
     for (int j = 0; j < CA; ++j) {
       const int c = tid + 256 * j;
@@ -236,25 +265,25 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
       *reinterpret_cast<bf16x8*>(Ws + (c >> 3) * kLdr + (c & 7) * 8) = rw[j];
     }
   };
-  f32x4 acc[4][TN];
+  f32x4 acc[TM][TN];
 #pragma unroll
-  for (int tm = 0; tm < 4; ++tm)
+  for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int buf) {
     const __bf16* As = smem + buf * kBuf;
-    const __bf16* Ws = As + kBM * kLdr;
+    const __bf16* Ws = As + BM * kLdr;
 #pragma unroll
     for (int kk = 0; kk < kBK / 32; ++kk) {
-      bf16x8 af[4], bf[TN];
+      bf16x8 af[TM], bf[TN];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        af[t] = *reinterpret_cast<const bf16x8*>(As + (wr * 64 + t * 16 + r16) * kLdr + kk * 32 + kq * 8);
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (wr * (BM / 2) + i * 16 + r16) * kLdr + kk * 32 + kq * 8);
 #pragma unroll
-      for (int t = 0; t < TN; ++t)
-        bf[t] = *reinterpret_cast<const bf16x8*>(Ws + (wc * (BN / 2) + t * 16 + r16) * kLdr + kk * 32 + kq * 8);
+      for (int i = 0; i < TN; ++i)
+        bf[i] = *reinterpret_cast<const bf16x8*>(Ws + (wc * (BN / 2) + i * 16 + r16) * kLdr + kk * 32 + kq * 8);
 #pragma unroll
-      for (int tm = 0; tm < 4; ++tm)
+      for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
@@ -285,10 +314,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
     const bool live = col < a.N;
     const float bias = live ? a.bias[col] : 0.f;
 #pragma unroll
-    for (int tm = 0; tm < 4; ++tm) {
+    for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wr * 64 + tm * 16 + kq * 4 + i;
+        const int row = m0 + wr * (BM / 2) + tm * 16 + kq * 4 + i;
         if (!a.mse) {
           if (row < a.rows_eff) {
             const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
@@ -311,11 +340,43 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
   }
 }
 
+template <int AMODE>
+void launch_bf16(const DenseGemmArgs& a, hipStream_t s) {
+  // 128 x 64 tiles (two resident workgroups per CU) when they fill the chip;
+  // 32 x 64 otherwise (narrow layers such as a 10-class head: 4x the
+  // workgroups, so the A stream is spread over every CU)
+  const int nN = (a.Np + 63) / 64;
+  const int big = nN * ((a.rows_eff + 127) / 128);
+  if (big >= 256) {
+    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 128, 64>), dim3(big), dim3(256), 0, s, a);
+  } else {
+    const int small = nN * ((a.rows_eff + 31) / 32);
+    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 32, 64>), dim3(small), dim3(256), 0, s, a);
+  }
+}
+
+// fp64 [rows][F] -> bf16 [rows][ld] (zero-padded): 8 outputs per thread, one
+// 16-B store; 16-B loads when the 8 inputs are in one aligned row run
 __global__ void convert_bf16_kernel(const double* __restrict__ X, int rows, int F, int ld, __bf16* __restrict__ out) {
-  const size_t n = size_t(rows) * ld;
+  const int per_row = ld >> 3;  // ld % 8 == 0 (Kpb is a multiple of 64)
+  const size_t n = size_t(rows) * per_row;
+  using f64x2 = __attribute__((ext_vector_type(2))) double;
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
-    const int r = int(i / ld), c = int(i - size_t(r) * ld);
-    out[i] = __bf16(c < F ? float(X[size_t(r) * F + c]) : 0.f);
+    const int r = int(i / per_row), c0 = int(i - size_t(r) * per_row) * 8;
+    const double* x = X + size_t(r) * F + c0;
+    bf16x8 v;
+    if (c0 + 8 <= F && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f64x2 d = reinterpret_cast<const f64x2*>(x)[j];
+        v[2 * j] = __bf16(float(d[0]));
+        v[2 * j + 1] = __bf16(float(d[1]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __bf16(c0 + j < F ? float(x[j]) : 0.f);
+    }
+    reinterpret_cast<bf16x8*>(out)[i] = v;
   }
 }
 
@@ -338,11 +399,13 @@ void launch_tn(const DenseGemmArgs& a, hipStream_t s) {
 void dense_gemm(const DenseGemmArgs& a, hipStream_t s) {
   if (a.rows_eff <= 0) return;
   if (a.bf16) {
-    // 128 x 64 tiles: two resident workgroups per CU (the 128 x 128 variant
-    // needs 230 VGPRs -> one, and measured 2.5x slower on the VAE decoder)
-    const dim3 grid((a.Np + 63) / 64, (a.rows_eff + kBM - 1) / kBM);
-    if (a.H) hipLaunchKernelGGL((gemm_bf16_lds_kernel<2, 64>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((gemm_bf16_lds_kernel<0, 64>), grid, dim3(256), 0, s, a);
+    static const int remap = [] { const char* v = getenv("SCA_GEMM_REMAP"); return v ? atoi(v) : 1; }();
+    DenseGemmArgs b = a;
+    b.xcd_remap = remap;
+    // (the 128 x 128 variant needs 230 VGPRs -> one workgroup per CU, and
+    // measured 2.5x slower on the VAE decoder)
+    if (b.H) launch_bf16<2>(b, s);
+    else launch_bf16<0>(b, s);
   } else {
     if (a.H) launch_tn<0, 2>(a, s);
     else launch_tn<0, 0>(a, s);
@@ -351,9 +414,10 @@ void dense_gemm(const DenseGemmArgs& a, hipStream_t s) {
 
 void convert_bf16(const double* X, int rows, int F, int ld, void* out, hipStream_t s) {
   if (rows <= 0) return;
-  const size_t n = size_t(rows) * ld;
-  const int blocks = int((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
-  hipLaunchKernelGGL(convert_bf16_kernel, dim3(blocks), dim3(256), 0, s, X, rows, F, ld, static_cast<__bf16*>(out));
+  const size_t n = size_t(rows) * (ld / 8);
+  const int bs = n < (size_t(256) << 10) ? 64 : 256;  // small batches: more, narrower workgroups
+  const int blocks = int((n + bs - 1) / bs < 4096 ? (n + bs - 1) / bs : 4096);
+  hipLaunchKernelGGL(convert_bf16_kernel, dim3(blocks), dim3(bs), 0, s, X, rows, F, ld, static_cast<__bf16*>(out));
 }
 
 }  // namespace sca::kern

@@ -184,6 +184,8 @@ struct DenseGemmArgs {
   int K = 0, Kp = 0, N = 0, Np = 0, act = 0;
   const void* A = nullptr;
   int lda = 0;
+  int a_f64 = 0;
+  int xcd_remap = 1;  // bf16 path: XCD-aware tile order (set by dense_gemm)  // bf16 path: A is the fp64 request batch [rows][lda], K = lda (converted while staging)
   const float* H = nullptr;
   int ldh = 0, latent = 0;
   uint64_t key = 0;
