@@ -79,6 +79,9 @@ def parse_args(argv=None):
     ap.add_argument("--extras", choices=["auto", "none"], default="auto",
                     help="after the timed region: gRPC + multi-GPU graph variants (auto) or nothing")
     ap.add_argument("--extra-steps", type=int, default=2, help="steps per extra measurement")
+    ap.add_argument("--fabric-probe", choices=["auto", "none"], default="auto",
+                    help="N >= 2: after everything else, run tools/fabric_probe.py in child processes "
+                         "(rank-placed graph nodes over the RCCL p2p fabric) under a time limit")
     ap.add_argument("--extra-grpc", action="store_true", help="(kept for old command lines; gRPC is an auto extra)")
     return ap.parse_args(argv)
 
@@ -457,6 +460,50 @@ def measure_variant(args, d: Dist, wl: Workload, kind: str, spin: bool) -> dict:
         dep.close()
 
 
+def fabric_probe(d: Dist, timeout_s: float = 150.0, requests: int = 200):
+    """Cross-process graph placement over the p2p fabric: every
+    rank starts ``tools/fabric_probe.py`` as a child process in a fresh
+    process group (rank 0 hosts an AVERAGE_COMBINER whose MODEL children live
+    on every rank; batches and replies travel as RCCL send/recv on GPUs).  It
+    runs after the measurements, in children under a time limit, so a hang or
+    fault there is recorded instead of costing the benchmark line.  Returns
+    rank 0's summary (None on other ranks)."""
+    import signal
+
+    box = [_free_port() if d.rank == 0 else None]
+    if d.dist is not None:
+        d.dist.broadcast_object_list(box, src=0)
+    env = dict(os.environ, RANK=str(d.rank), LOCAL_RANK=str(d.local_rank), WORLD_SIZE=str(d.world),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(box[0]))
+    t0 = time.perf_counter()
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "fabric_probe.py"), "--requests", str(requests)],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout_s)
+        status = "ok" if p.returncode == 0 else f"rc={p.returncode}"
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        status = f"timeout after {timeout_s:.0f}s"
+    res = {"rank": d.rank, "status": status, "wall_s": round(time.perf_counter() - t0, 2)}
+    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+    if lines:
+        try:
+            res["probe"] = json.loads(lines[-1])
+        except ValueError:
+            pass
+    if status != "ok":
+        res["stderr_tail"] = (err or "")[-600:]
+    allr = d.gather(res)
+    if d.rank != 0:
+        return None
+    top = allr[0].get("probe") or {}
+    return {"ok": all(r["status"] == "ok" for r in allr), "world": d.world,
+            "data_plane": top.get("data_plane"), "requests": top.get("requests"),
+            "max_abs_err": top.get("max_abs_err"), "req_per_s": round(top.get("req_per_s", 0.0), 1),
+            "units": top.get("units"), "ranks": [{k: r[k] for k in r if k != "probe"} for r in allr]}
+
+
 def main() -> None:
     argv = sys.argv[1:]
     args = parse_args(argv)
@@ -520,8 +567,14 @@ def main() -> None:
                 failures.append(f"rank {d.rank} {kind} self-check: {r['check']}")
             extras[kind] = r
     results = d.gather({"mine": mine, "extras": extras, "failures": failures})
+    fabric = None
+    if args.extras == "auto" and args.fabric_probe == "auto" and d.world >= 2:
+        fabric = fabric_probe(d)
     if d.rank == 0:
-        print(json.dumps(summarize(args, d, results, label, wl)), flush=True)
+        line = summarize(args, d, results, label, wl)
+        if fabric is not None:
+            line["rccl_fabric"] = fabric
+        print(json.dumps(line), flush=True)
     bad = [f for r in results for f in r["failures"]]
     d.close()
     if bad:

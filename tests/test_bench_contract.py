@@ -24,7 +24,7 @@ def _json_lines(out):
 def test_bench_two_ranks_cpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--step-requests", "1000", "--users", "16"]
+           "--steps", "2", "--warmup", "1", "--step-requests", "1000", "--users", "16", "--fabric-probe", "none"]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert res.returncode == 0, res.stderr[-3000:]
@@ -61,6 +61,10 @@ def test_bench_direct_launch_spawns_ranks_and_runs_variants():
     assert v["abtest"]["gpus_per_graph"] == 2 and v["mab"]["gpus_per_graph"] == 2
     assert all(x["self_check"]["ok"] for x in v.values())
     assert v["mab"]["feedback_rps"] > 0
+    # rank-placed graph over the p2p fabric (child processes, sockets data plane on CPU)
+    fab = line["rccl_fabric"]
+    assert fab["ok"] and fab["world"] == 2 and fab["data_plane"] == "sockets", fab
+    assert fab["max_abs_err"] < 1e-12 and [r["status"] for r in fab["ranks"]] == ["ok", "ok"]
 
 
 def test_bench_rejects_gpus_world_mismatch():

@@ -31,8 +31,11 @@ def main():
 
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
-    dev = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(dev)
+    if torch.cuda.is_available():
+        dev = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", rank))
+        torch.cuda.set_device(dev)
+    else:  # CPU fabric: the same peer protocol with the payloads on the control sockets
+        dev = -1
     dist.init_process_group("gloo")
     import seldon_core_amd as sca
     from seldon_core_amd.models import iris_logistic_regression
@@ -68,8 +71,9 @@ def main():
     dt = time.perf_counter() - t0
     dep.close()  # stops the peers
     fabric.close()
-    print(json.dumps({"rank": 0, "world": world, "units": kinds, "requests": args.requests,
-                      "max_abs_err": worst, "req_per_s": args.requests / dt}), flush=True)
+    print(json.dumps({"rank": 0, "world": world, "device": dev, "data_plane": "rccl" if dev >= 0 else "sockets",
+                      "units": kinds, "requests": args.requests, "max_abs_err": worst,
+                      "req_per_s": args.requests / dt}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
     sys.exit(0 if worst < 1e-12 else 2)
