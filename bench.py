@@ -79,6 +79,8 @@ def parse_args(argv=None):
     ap.add_argument("--extras", choices=["auto", "none"], default="auto",
                     help="after the timed region: gRPC + multi-GPU graph variants (auto) or nothing")
     ap.add_argument("--extra-steps", type=int, default=2, help="steps per extra measurement")
+    ap.add_argument("--cpu-profile", default=None,
+                    help="write a sampling CPU profile of the serving process over the timed window to this JSON file")
     ap.add_argument("--fabric-probe", choices=["auto", "none"], default="auto",
                     help="N >= 2: after everything else, run tools/fabric_probe.py in child processes "
                          "(rank-placed graph nodes over the RCCL p2p fabric) under a time limit")
@@ -326,7 +328,7 @@ def self_check(port: int, wl: Workload, oracle, seed: int, n: int = 24) -> dict:
 
 def unit_stats(dep) -> dict:
     per_dev: dict = {}
-    total = {"batches": 0, "rows": 0, "gpu_busy_s": 0.0}
+    total = {"batches": 0, "rows": 0, "gpu_busy_s": 0.0, "launch_cpu_s": 0.0, "complete_cpu_s": 0.0}
     for name, st in dep.batcher_stats().items():
         if not isinstance(st, dict):
             continue
@@ -543,7 +545,16 @@ def main() -> None:
     for u in dep.batched.values():
         u.reset_stats()
     cpu: dict = {}
+    if args.cpu_profile:
+        from seldon_core_amd.utils import cpuprof
+
+        cpuprof.start()
     lg, wall = timed(d, lambda: run_loadgen(args, port, args.steps, 0, args.api, body), cpu)
+    if args.cpu_profile:
+        prof = cpuprof.stop()
+        prof.update(rps=round(lg["ok"] / wall, 1), server_cpus=cpu.get("server_cpus"), rank=d.rank)
+        with open(args.cpu_profile if d.world == 1 else f"{args.cpu_profile}.rank{d.rank}", "w") as f:
+            json.dump(prof, f, indent=1)
     st = unit_stats(dep)
     mine = {"rank": d.rank, "device": d.device, "ok": lg["ok"], "wall": wall, "p50": lg["p50_ms"],
             "p99": lg["p99_ms"], "stats": st, "cpu_budget": round(per_rank_cpus, 2), "cpu": cpu}
@@ -594,6 +605,9 @@ def summarize(args, d: Dist, results, label: str, wl: Workload) -> dict:
                  "rps": round(m["ok"] / m["wall"], 1), "p50_ms": m["p50"], "p99_ms": m["p99"],
                  "gpu_batches": m["stats"]["batches"],
                  "mean_rows_per_batch": round(m["stats"]["rows"] / max(1, m["stats"]["batches"]), 2),
+                 # share of the window the GPU device thread spent launching / handing off responses
+                 "device_thread_launch_frac": round(m["stats"]["launch_cpu_s"] / m["wall"], 3),
+                 "device_thread_complete_frac": round(m["stats"]["complete_cpu_s"] / m["wall"], 3),
                  "check_max_abs_err": m["check"]["max_abs_err"]} for m in mines]
     line = {
         "metric": "predictions/sec (%s graph, %s)" % ("single-model" if args.graph == "single" else args.graph,

@@ -6,6 +6,7 @@
 
 #include <future>
 
+#include "../core/cpuprof.h"
 #include "../core/engine.h"
 #include "../core/json.h"
 #include "../core/message.h"
@@ -82,6 +83,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("gpu_device_count", [] { return gpu::device_count(); });
 
   // ------------------------------------------------------------- codecs
+  m.def("cpu_profile_start", [](int hz) { return prof::start(hz); }, py::arg("hz") = 997,
+        "Start sampling this process's CPU time (SIGPROF at `hz` per CPU-second).");
+  m.def("cpu_profile_stop", [] {
+    py::list out;
+    for (const auto& kv : prof::stop()) out.append(py::make_tuple(kv.first.first, kv.first.second, kv.second));
+    return out;
+  }, "Stop sampling: [(module, offset, samples)], most frequent first.");
   m.def("json_roundtrip", [](const std::string& text) {
     SeldonMessage msg;
     message_from_json(parse_json(text), msg);
@@ -425,6 +433,8 @@ PYBIND11_MODULE(_C, m) {
         d["requests"] = s.requests;
         d["max_rows"] = s.max_rows;
         d["gpu_busy_s"] = s.gpu_busy_s;
+        d["launch_cpu_s"] = s.launch_cpu_s;
+        d["complete_cpu_s"] = s.complete_cpu_s;
         d["device"] = u.options().device;
         return d;
       })

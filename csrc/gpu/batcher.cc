@@ -88,6 +88,7 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
     if (opts_.cpu_batching) {
       cpu_ = true;
       for (int i = 0; i < opts_.slots; ++i) slots_.push_back(std::make_unique<Slot>());
+      handoff_th_ = std::thread([this] { handoff_loop(); });
       device_th_ = std::thread([this] { device_loop(); });
     }
     return;
@@ -106,6 +107,7 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
     slots_.push_back(std::move(s));
   }
   running_.store(true);
+  handoff_th_ = std::thread([this] { handoff_loop(); });
   device_th_ = std::thread([this] { device_loop(); });
 }
 
@@ -118,6 +120,12 @@ void BatchedUnit::stop() {
   }
   cv_submit_.notify_all();
   if (device_th_.joinable()) device_th_.join();  // completes everything in flight
+  {
+    std::lock_guard<std::mutex> g(ho_mu_);
+    ho_stop_ = true;
+  }
+  ho_cv_.notify_all();
+  if (handoff_th_.joinable()) handoff_th_.join();  // posts what the device thread handed over
   std::deque<Item> rest;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -375,6 +383,58 @@ bool BatchedUnit::launch(Slot* s) {
   return false;
 }
 
+void BatchedUnit::handoff_loop() {
+  std::vector<Handoff> batch;
+  while (true) {
+    {
+      std::unique_lock<std::mutex> lk(ho_mu_);
+      if (ho_q_.empty()) {
+        if (ho_stop_) return;
+        ho_sleeping_ = true;
+        ho_cv_.wait(lk, [&] { return ho_stop_ || !ho_q_.empty(); });
+        ho_sleeping_ = false;
+        if (ho_q_.empty()) return;  // stopping with nothing left
+      }
+      batch.swap(ho_q_);
+    }
+    for (auto& h : batch) post_responses(h);
+    batch.clear();
+  }
+}
+
+// One task per front-end executor: it builds its requests' responses from the
+// shared output block and runs their continuations on that thread.
+void BatchedUnit::post_responses(Handoff& h) {
+  struct Req {
+    Item item;
+    size_t off;
+  };
+  struct Group {
+    ExecPtr ex;
+    std::shared_ptr<std::vector<Req>> reqs;
+  };
+  std::vector<Group> groups;
+  for (size_t i = 0; i < h.items.size(); ++i) {
+    Item& it = h.items[i];
+    Group* g = nullptr;
+    for (auto& gg : groups)
+      if (gg.ex.get() == it.exec.get()) { g = &gg; break; }
+    if (!g) {
+      groups.push_back(Group{it.exec, std::make_shared<std::vector<Req>>()});
+      g = &groups.back();
+    }
+    g->reqs->push_back(Req{std::move(it), h.offs[i]});
+  }
+  for (auto& g : groups) {
+    g.ex->post([info = resp_, reqs = g.reqs, out = h.out, oc = h.out_cols]() {
+      for (auto& r : *reqs) {
+        Done k = std::move(r.item.k);
+        k(Outcome::ok(make_response(*info, r.item, out->data() + r.off, oc)));
+      }
+    });
+  }
+}
+
 void BatchedUnit::complete(Slot* s, hipError_t st) {
   const double busy = std::chrono::duration<double>(std::chrono::steady_clock::now() - s->t_launch).count();
   if (s->roctx) {
@@ -399,42 +459,34 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     for (auto& it : items) it.k(Outcome::fail(e));
   } else {
     note_success();
-    // Copy each request's rows out of the slot (it is reused at once), then
-    // hand the requests to their front-end threads, one task per thread.
+    // Requests with a front-end executor go to the hand-off thread with one
+    // copy of the output block; synchronous callers (no executor) are
+    // answered here, before the slot is reused.
     const int oc = s->out_cols;
     const double* out = cpu_ ? s->cpu_out.data() : s->h_out.host<double>();
-    using Req = std::pair<Item, std::vector<double>>;
-    struct Group {
-      ExecPtr ex;
-      std::shared_ptr<std::vector<Req>> reqs;
-    };
-    std::vector<Group> groups;
+    Handoff h;
+    h.out_cols = oc;
     size_t row = 0;
     for (auto& it : items) {
-      const double* yp = out + row * oc;
-      row += size_t(it.rows);
-      if (!it.exec) {  // answered before the slot is reused: build the response from the slot directly
+      const size_t r = size_t(it.rows);
+      if (!it.exec) {
         Done k = std::move(it.k);
-        k(Outcome::ok(make_response(*resp_, it, yp, oc)));
-        continue;
+        k(Outcome::ok(make_response(*resp_, it, out + row * oc, oc)));
+      } else {
+        h.offs.push_back(row * oc);
+        h.items.push_back(std::move(it));
       }
-      std::vector<double> y(yp, yp + size_t(it.rows) * oc);
-      Group* g = nullptr;
-      for (auto& gg : groups)
-        if (gg.ex.get() == it.exec.get()) { g = &gg; break; }
-      if (!g) {
-        groups.push_back(Group{it.exec, std::make_shared<std::vector<Req>>()});
-        g = &groups.back();
-      }
-      g->reqs->emplace_back(std::move(it), std::move(y));
+      row += r;
     }
-    for (auto& g : groups) {
-      g.ex->post([info = resp_, reqs = g.reqs, oc]() {
-        for (auto& r : *reqs) {
-          Done k = std::move(r.first.k);
-          k(Outcome::ok(make_response(*info, r.first, r.second.data(), oc)));
-        }
-      });
+    if (!h.items.empty()) {
+      h.out = std::make_shared<std::vector<double>>(out, out + size_t(s->rows) * oc);
+      bool wake;
+      {
+        std::lock_guard<std::mutex> g(ho_mu_);
+        ho_q_.push_back(std::move(h));
+        wake = ho_sleeping_;
+      }
+      if (wake) ho_cv_.notify_one();
     }
   }
   std::lock_guard<std::mutex> g(stats_mu_);
@@ -483,7 +535,11 @@ void BatchedUnit::device_loop() {
         s->rows = rows;
         s->cols = cols;
         lk.unlock();
+        const auto t0 = clk::now();
         const bool ok = launch(s);
+        launch_cpu_s_.store(launch_cpu_s_.load(std::memory_order_relaxed) +
+                                std::chrono::duration<double>(clk::now() - t0).count(),
+                            std::memory_order_relaxed);
         lk.lock();
         (ok ? inflight : free_list).push_back(s);
       }
@@ -505,7 +561,11 @@ void BatchedUnit::device_loop() {
         ++i;
         continue;
       }
+      const auto t0 = clk::now();
       complete(s, st);
+      complete_cpu_s_.store(complete_cpu_s_.load(std::memory_order_relaxed) +
+                                std::chrono::duration<double>(clk::now() - t0).count(),
+                            std::memory_order_relaxed);
       inflight.erase(inflight.begin() + long(i));
       free_list.push_back(s);
       progress = true;
@@ -623,7 +683,10 @@ UnitHealth BatchedUnit::health() const {
 
 BatcherStats BatchedUnit::stats() const {
   std::lock_guard<std::mutex> g(stats_mu_);
-  return stats_;
+  BatcherStats s = stats_;
+  s.launch_cpu_s = launch_cpu_s_.load(std::memory_order_relaxed);
+  s.complete_cpu_s = complete_cpu_s_.load(std::memory_order_relaxed);
+  return s;
 }
 
 void BatchedUnit::collect_metrics(MetricsRegistry& m, const Labels& labels) const {
@@ -653,6 +716,8 @@ void BatchedUnit::collect_metrics(MetricsRegistry& m, const Labels& labels) cons
 void BatchedUnit::reset_stats() {
   std::lock_guard<std::mutex> g(stats_mu_);
   stats_ = BatcherStats();
+  launch_cpu_s_.store(0.0, std::memory_order_relaxed);
+  complete_cpu_s_.store(0.0, std::memory_order_relaxed);
 }
 
 std::vector<double> BatchedUnit::run_ptr(const double* X, int rows, int cols) {

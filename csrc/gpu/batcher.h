@@ -88,6 +88,8 @@ struct BatcherStats {
   uint64_t requests = 0;
   uint64_t max_rows = 0;
   double gpu_busy_s = 0;     // sum over batches of launch -> completion observed
+  double launch_cpu_s = 0;   // device thread: staging + kernel launch + event record
+  double complete_cpu_s = 0; // device thread: response hand-off to the front-end threads
 };
 
 class BatchedUnit : public Unit {
@@ -153,8 +155,19 @@ class BatchedUnit : public Unit {
     std::chrono::steady_clock::time_point t_launch;
   };
 
+  // One completed batch on its way to the front-end threads: the requests and
+  // one copy of the slot's output rows (the slot is reused at once).
+  struct Handoff {
+    std::vector<Item> items;
+    std::vector<size_t> offs;  // each item's first output value in `out`
+    std::shared_ptr<std::vector<double>> out;
+    int out_cols = 0;
+  };
+
   void ensure_capacity(Slot& s, int rows, int cols);
   void device_loop();
+  void handoff_loop();
+  void post_responses(Handoff& h);
   bool launch(Slot* s);
   void complete(Slot* s, hipError_t st);
   void abandon(Slot* s);
@@ -183,8 +196,19 @@ class BatchedUnit : public Unit {
   bool segmented_ = false;
   bool cpu_ = false;        // device -1 with cpu_batching
   std::thread device_th_;
+  // Response hand-off thread: groups a completed batch's requests by front-end
+  // executor and posts them (eventfd wake-ups), off the device thread, which
+  // only launches and reaps batches.
+  std::thread handoff_th_;
+  std::mutex ho_mu_;
+  std::condition_variable ho_cv_;
+  std::vector<Handoff> ho_q_;   // guarded by ho_mu_
+  bool ho_sleeping_ = false;    // guarded by ho_mu_
+  bool ho_stop_ = false;        // guarded by ho_mu_
   mutable std::mutex stats_mu_;
   BatcherStats stats_;
+  // device-thread CPU time (single writer: the device thread; relaxed reads)
+  std::atomic<double> launch_cpu_s_{0.0}, complete_cpu_s_{0.0};
   // health / fault injection
   std::atomic<int> consec_fail_{0};
   std::atomic<int64_t> open_until_ns_{0};  // steady_clock ns; unhealthy before this

@@ -322,6 +322,37 @@ def case_linear(iters):
         unit.stop()
 
 
+def case_latency(iters):
+    """Round trip of one micro-batch through BatchedUnit (submit -> launch ->
+    completion seen -> response rows) for serving-size batches, spin vs
+    blocking completion, next to torch's launch + synchronize floor."""
+    import torch
+
+    from seldon_core_amd import native
+
+    C = native()
+    rng = np.random.default_rng(2)
+    n = max(iters, 2000)
+    for spin in (True, False):
+        unit = C.BatchedUnit(C.linear_model(rng.normal(size=(3, 4)), rng.normal(size=3), 1), 0, spin_wait=spin)
+        try:
+            for rows in (1, 20):
+                _time_unit(f"latency_linear_spin{int(spin)}", unit, rng.normal(size=(rows, 4)), n, {})
+        finally:
+            unit.stop()
+    x = torch.zeros(4, device="cuda")
+    for _ in range(100):
+        x.add_(1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        x.add_(1)
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"case": "latency_torch_launch_sync", "iters": n, "wall_us_per_run": round(dt / n * 1e6, 2)}),
+          flush=True)
+
+
 def case_lstm(iters):
     """seq2seq LSTM detector (ECG-shaped: T=140, F=1, BiLSTM 20 -> LSTM 40 -> Dense),
     one persistent kernel per batch, vs the torch eager decode loop."""
@@ -362,7 +393,7 @@ def main():
     a = ap.parse_args()
     cases = {"tree": case_tree, "vae": case_vae, "mlp": case_mlp, "linear": case_linear,
              "mlp_torch": case_mlp_torch, "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes,
-             "lstm": case_lstm, "dense_prec": case_dense_prec, "mlp_torch_bf16": case_mlp_torch_bf16}
+             "lstm": case_lstm, "latency": case_latency, "dense_prec": case_dense_prec, "mlp_torch_bf16": case_mlp_torch_bf16}
     for c in a.only.split(","):
         cases[c](a.iters)
 
