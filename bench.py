@@ -81,6 +81,7 @@ def parse_args(argv=None):
     ap.add_argument("--extra-steps", type=int, default=2, help="steps per extra measurement")
     ap.add_argument("--cpu-profile", default=None,
                     help="write a sampling CPU profile of the serving process over the timed window to this JSON file")
+    ap.add_argument("--cpu-profile-depth", type=int, default=1, help="frames per CPU-profile sample (>1: call paths)")
     ap.add_argument("--fabric-probe", choices=["auto", "none"], default="auto",
                     help="N >= 2: after everything else, run tools/fabric_probe.py in child processes "
                          "(rank-placed graph nodes over the RCCL p2p fabric) under a time limit")
@@ -548,7 +549,7 @@ def main() -> None:
     if args.cpu_profile:
         from seldon_core_amd.utils import cpuprof
 
-        cpuprof.start()
+        cpuprof.start(depth=args.cpu_profile_depth)
     lg, wall = timed(d, lambda: run_loadgen(args, port, args.steps, 0, args.api, body), cpu)
     if args.cpu_profile:
         prof = cpuprof.stop()

@@ -83,13 +83,18 @@ PYBIND11_MODULE(_C, m) {
   m.def("gpu_device_count", [] { return gpu::device_count(); });
 
   // ------------------------------------------------------------- codecs
-  m.def("cpu_profile_start", [](int hz) { return prof::start(hz); }, py::arg("hz") = 997,
-        "Start sampling this process's CPU time (SIGPROF at `hz` per CPU-second).");
+  m.def("cpu_profile_start", [](int hz, int depth) { return prof::start(hz, size_t(1) << 20, depth); },
+        py::arg("hz") = 997, py::arg("depth") = 1,
+        "Start sampling this process's CPU time (SIGPROF per thread at `hz` per CPU-second).");
   m.def("cpu_profile_stop", [] {
     py::list out;
-    for (const auto& kv : prof::stop()) out.append(py::make_tuple(kv.first.first, kv.first.second, kv.second));
+    for (const auto& s : prof::stop().samples) {
+      py::list frames;
+      for (const auto& f : s.frames) frames.append(py::make_tuple(f.module, f.offset));
+      out.append(py::make_tuple(frames, s.count));
+    }
     return out;
-  }, "Stop sampling: [(module, offset, samples)], most frequent first.");
+  }, "Stop sampling: [([(module, offset), ...], samples)], most frequent first.");
   m.def("json_roundtrip", [](const std::string& text) {
     SeldonMessage msg;
     message_from_json(parse_json(text), msg);

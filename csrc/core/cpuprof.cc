@@ -2,6 +2,7 @@
 
 #include <dirent.h>
 #include <dlfcn.h>
+#include <execinfo.h>
 #include <signal.h>
 #include <sys/time.h>
 #include <time.h>
@@ -22,6 +23,7 @@ uintptr_t* g_pcs = nullptr;      // samples (program counters)
 size_t g_cap = 0;
 std::atomic<size_t> g_n{0};
 std::atomic<bool> g_on{false};
+int g_depth = 1;                 // frames per sample: 1 = the interrupted PC only
 struct sigaction g_old {};
 std::vector<timer_t> g_timers;   // one CPU-time timer per thread alive at start()
 
@@ -33,22 +35,35 @@ void on_sigprof(int, siginfo_t*, void* uc) {
   if (!g_on.load(std::memory_order_relaxed)) return;
   const size_t i = g_n.fetch_add(1, std::memory_order_relaxed);
   if (i >= g_cap) return;
+  uintptr_t* rec = g_pcs + i * size_t(g_depth);
   const auto* ctx = static_cast<const ucontext_t*>(uc);
 #if defined(__x86_64__)
-  g_pcs[i] = uintptr_t(ctx->uc_mcontext.gregs[REG_RIP]);
+  rec[0] = uintptr_t(ctx->uc_mcontext.gregs[REG_RIP]);
 #else
   (void)ctx;
-  g_pcs[i] = 0;
+  rec[0] = 0;
 #endif
+  if (g_depth > 1) {
+    // Callers through the DWARF unwinder (libgcc, preloaded by start()):
+    // frames [0, 1] are this handler and the signal trampoline.
+    void* fr[34];
+    const int n = backtrace(fr, std::min(34, g_depth + 2));
+    for (int d = 1; d < g_depth; ++d) rec[d] = d + 1 < n ? uintptr_t(fr[d + 1]) - 1 : 0;
+  }
 }
 
 }  // namespace
 
-bool start(int hz, size_t max_samples) {
+bool start(int hz, size_t max_samples, int depth) {
   std::lock_guard<std::mutex> g(g_mu);
   if (g_on.load() || hz <= 0) return false;
+  g_depth = std::max(1, std::min(depth, 32));
+  if (g_depth > 1) {  // load the unwinder outside signal context
+    void* fr[4];
+    (void)backtrace(fr, 4);
+  }
   delete[] g_pcs;
-  g_pcs = new uintptr_t[max_samples];
+  g_pcs = new uintptr_t[max_samples * size_t(g_depth)];
   g_cap = max_samples;
   g_n.store(0);
   struct sigaction sa {};
@@ -89,27 +104,42 @@ bool start(int hz, size_t max_samples) {
   return true;
 }
 
-std::vector<std::pair<std::pair<std::string, uint64_t>, uint64_t>> stop() {
+Profile stop() {
   std::lock_guard<std::mutex> g(g_mu);
-  std::vector<std::pair<std::pair<std::string, uint64_t>, uint64_t>> out;
+  Profile out;
   if (!g_on.load()) return out;
   for (timer_t t : g_timers) timer_delete(t);
   g_timers.clear();
   g_on.store(false);
   sigaction(SIGPROF, &g_old, nullptr);
   const size_t n = std::min(g_n.load(), g_cap);
-  std::map<uintptr_t, uint64_t> by_pc;
-  for (size_t i = 0; i < n; ++i) by_pc[g_pcs[i]]++;
-  std::map<std::pair<std::string, uint64_t>, uint64_t> agg;
-  for (const auto& kv : by_pc) {
+  out.depth = g_depth;
+  std::map<uintptr_t, Loc> locs;
+  auto loc = [&](uintptr_t pc) -> const Loc& {
+    auto it = locs.find(pc);
+    if (it != locs.end()) return it->second;
+    Loc l;
     Dl_info info{};
-    if (kv.first && dladdr(reinterpret_cast<void*>(kv.first), &info) && info.dli_fname)
-      agg[{info.dli_fname, uint64_t(kv.first - uintptr_t(info.dli_fbase))}] += kv.second;
-    else
-      agg[{"", uint64_t(kv.first)}] += kv.second;
+    if (pc && dladdr(reinterpret_cast<void*>(pc), &info) && info.dli_fname) {
+      l.module = info.dli_fname;
+      l.offset = uint64_t(pc - uintptr_t(info.dli_fbase));
+    } else {
+      l.offset = uint64_t(pc);
+    }
+    return locs.emplace(pc, std::move(l)).first->second;
+  };
+  std::map<std::vector<uintptr_t>, uint64_t> stacks;
+  for (size_t i = 0; i < n; ++i) {
+    const uintptr_t* rec = g_pcs + i * size_t(g_depth);
+    stacks[std::vector<uintptr_t>(rec, rec + g_depth)]++;
   }
-  out.assign(agg.begin(), agg.end());
-  std::sort(out.begin(), out.end(), [](const auto& a, const auto& b) { return a.second > b.second; });
+  for (const auto& kv : stacks) {
+    Sample smp;
+    smp.count = kv.second;
+    for (uintptr_t pc : kv.first) smp.frames.push_back(loc(pc));
+    out.samples.push_back(std::move(smp));
+  }
+  std::sort(out.samples.begin(), out.samples.end(), [](const Sample& a, const Sample& b) { return a.count > b.count; });
   return out;
 }
 

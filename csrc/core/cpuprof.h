@@ -17,8 +17,21 @@
 
 namespace sca::prof {
 
-bool start(int hz, size_t max_samples = size_t(1) << 21);
-// (module, offset) -> samples, most frequent first; empty module = unknown.
-std::vector<std::pair<std::pair<std::string, uint64_t>, uint64_t>> stop();
+struct Loc {
+  std::string module;  // empty: unknown
+  uint64_t offset = 0; // in module (or the raw address)
+};
+struct Sample {
+  std::vector<Loc> frames;  // [0] = interrupted PC, then callers (depth > 1)
+  uint64_t count = 0;
+};
+struct Profile {
+  int depth = 1;
+  std::vector<Sample> samples;  // distinct stacks, most frequent first
+};
+
+// depth > 1 also records depth - 1 callers through the DWARF unwinder.
+bool start(int hz, size_t max_samples = size_t(1) << 20, int depth = 1);
+Profile stop();
 
 }  // namespace sca::prof

@@ -127,13 +127,33 @@ void BatchedUnit::stop() {
   ho_cv_.notify_all();
   if (handoff_th_.joinable()) handoff_th_.join();  // posts what the device thread handed over
   std::deque<Item> rest;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    rest.swap(queue_);
-    queued_rows_ = 0;
-    queued_n_.store(0);
-  }
+  drain_shards(rest);
   for (auto& it : rest) it.k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "GPU unit stopped")));
+}
+
+namespace {
+std::atomic<int> g_next_shard{0};
+int shard_of_this_thread(int shards) {
+  thread_local const int idx = g_next_shard.fetch_add(1, std::memory_order_relaxed);
+  return idx % shards;
+}
+}  // namespace
+
+void BatchedUnit::drain_shards(std::deque<Item>& into) {
+  for (auto& sh : shards_) {
+    if (sh.n.load(std::memory_order_acquire) == 0) continue;
+    std::deque<Item> got;
+    {
+      std::lock_guard<std::mutex> g(sh.mu);
+      got.swap(sh.q);
+      sh.n.fetch_sub(int(got.size()), std::memory_order_relaxed);
+      queued_n_.fetch_sub(int(got.size()), std::memory_order_relaxed);
+    }
+    for (auto& it : got) {
+      queued_rows_.fetch_sub(it.rows, std::memory_order_relaxed);
+      into.push_back(std::move(it));
+    }
+  }
 }
 
 constexpr size_t kDirectH2DBytes = size_t(1) << 20;
@@ -270,16 +290,22 @@ void BatchedUnit::submit_item(Item it) {
     it.k(Outcome::fail(device_error(ApiError::UNAVAILABLE, "every batch slot of this GPU is wedged")));
     return;
   }
-  inflight_rows_.fetch_add(it.rows, std::memory_order_relaxed);
-  bool wake;
+  const int rows = it.rows;
+  inflight_rows_.fetch_add(rows, std::memory_order_relaxed);
+  queued_rows_.fetch_add(rows, std::memory_order_relaxed);
+  Shard& sh = shards_[shard_of_this_thread(kShards)];
   {
-    std::lock_guard<std::mutex> g(mu_);
-    queued_rows_ += size_t(it.rows);
-    wake = queue_.empty();
-    queue_.push_back(std::move(it));
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.q.push_back(std::move(it));
+    sh.n.fetch_add(1, std::memory_order_release);
+    queued_n_.fetch_add(1, std::memory_order_seq_cst);
   }
-  queued_n_.fetch_add(1, std::memory_order_release);
-  if (wake) cv_submit_.notify_one();  // the device thread sleeps only with an empty queue
+  // Pairs with the device thread's dev_sleeping_ store + queued_n_ re-check
+  // under mu_: either it sees this item or we see it asleep and wake it.
+  if (dev_sleeping_.load(std::memory_order_seq_cst)) {
+    { std::lock_guard<std::mutex> g(mu_); }
+    cv_submit_.notify_one();
+  }
 }
 
 bool BatchedUnit::launch(Slot* s) {
@@ -501,48 +527,47 @@ void BatchedUnit::device_loop() {
   if (!cpu_) (void)hipSetDevice(opts_.device);
   std::vector<Slot*> free_list, inflight;
   for (auto& s : slots_) free_list.push_back(s.get());
+  std::deque<Item> pending;  // taken from the shards, not yet in a slot (device thread only)
   using clk = std::chrono::steady_clock;
   clk::time_point wait_start{};
   int spins = 0;
   while (true) {
-    // ---- launch everything that fits into the free slots
-    {
+    // ---- take what the front ends queued (O(1) under the lock: producers
+    // never wait behind batch formation), then launch everything that fits
+    // into the free slots from the device thread's own backlog
+    if (inflight.empty() && pending.empty()) {
       std::unique_lock<std::mutex> lk(mu_);
-      if (inflight.empty()) {
-        cv_submit_.wait(lk, [&] { return !running_.load() || !queue_.empty(); });
-        if (!running_.load()) break;
-        if (opts_.max_wait_us > 0 && queued_rows_ < size_t(opts_.max_batch)) {
-          const auto deadline = clk::now() + std::chrono::microseconds(opts_.max_wait_us);
-          cv_submit_.wait_until(lk, deadline, [&] { return !running_.load() || queued_rows_ >= size_t(opts_.max_batch); });
-          if (!running_.load()) break;
-        }
+      dev_sleeping_.store(true, std::memory_order_seq_cst);
+      cv_submit_.wait(lk, [&] { return !running_.load() || queued_n_.load(std::memory_order_seq_cst) > 0; });
+      if (running_.load() && opts_.max_wait_us > 0 && queued_rows_.load() < opts_.max_batch) {
+        const auto deadline = clk::now() + std::chrono::microseconds(opts_.max_wait_us);
+        cv_submit_.wait_until(lk, deadline,
+                              [&] { return !running_.load() || queued_rows_.load() >= opts_.max_batch; });
       }
-      while (!queue_.empty() && !free_list.empty()) {
-        Slot* s = free_list.back();
-        free_list.pop_back();
-        int rows = 0, n = 0;
-        const int cols = queue_.front().cols;
-        while (!queue_.empty()) {
-          Item& it = queue_.front();
-          if (!s->items.empty() && (it.cols != cols || rows + it.rows > opts_.max_batch)) break;
-          rows += it.rows;
-          queued_rows_ -= size_t(it.rows);
-          s->items.push_back(std::move(it));
-          queue_.pop_front();
-          ++n;
-        }
-        queued_n_.fetch_sub(n, std::memory_order_relaxed);
-        s->rows = rows;
-        s->cols = cols;
-        lk.unlock();
-        const auto t0 = clk::now();
-        const bool ok = launch(s);
-        launch_cpu_s_.store(launch_cpu_s_.load(std::memory_order_relaxed) +
-                                std::chrono::duration<double>(clk::now() - t0).count(),
-                            std::memory_order_relaxed);
-        lk.lock();
-        (ok ? inflight : free_list).push_back(s);
+      dev_sleeping_.store(false, std::memory_order_relaxed);
+      if (!running_.load()) break;
+    }
+    if (!free_list.empty() && queued_n_.load(std::memory_order_acquire) > 0) drain_shards(pending);
+    while (!pending.empty() && !free_list.empty()) {
+      Slot* s = free_list.back();
+      free_list.pop_back();
+      int rows = 0;
+      const int cols = pending.front().cols;
+      while (!pending.empty()) {
+        Item& it = pending.front();
+        if (!s->items.empty() && (it.cols != cols || rows + it.rows > opts_.max_batch)) break;
+        rows += it.rows;
+        s->items.push_back(std::move(it));
+        pending.pop_front();
       }
+      s->rows = rows;
+      s->cols = cols;
+      const auto t0 = clk::now();
+      const bool ok = launch(s);
+      launch_cpu_s_.store(launch_cpu_s_.load(std::memory_order_relaxed) +
+                              std::chrono::duration<double>(clk::now() - t0).count(),
+                          std::memory_order_relaxed);
+      (ok ? inflight : free_list).push_back(s);
     }
     if (inflight.empty()) continue;
     // ---- reap finished batches
@@ -574,12 +599,9 @@ void BatchedUnit::device_loop() {
     if (abandoned_slots_.load(std::memory_order_relaxed) >= int(slots_.size())) {
       // Wedged device: answer what is still queued instead of letting it wait.
       std::deque<Item> rest;
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        rest.swap(queue_);
-        queued_rows_ = 0;
-        queued_n_.store(0);
-      }
+      drain_shards(rest);
+      for (auto& it : pending) rest.push_back(std::move(it));
+      pending.clear();
       if (!rest.empty()) {
         auto e = device_error(ApiError::UNAVAILABLE, "every batch slot of this GPU is wedged");
         for (auto& it : rest) {
@@ -595,7 +617,8 @@ void BatchedUnit::device_loop() {
         (void)hipEventSynchronize(inflight.front()->ev.get());
       continue;
     }
-    if (!free_list.empty() && queued_n_.load(std::memory_order_acquire) > 0) continue;  // new work: launch it
+    if (!free_list.empty() && (!pending.empty() || queued_n_.load(std::memory_order_acquire) > 0))
+      continue;  // new work: launch it
     // Spin through the usual 10-50 us round trip; back off if the GPU is slow
     // so a long kernel does not burn a core (and CPU quota) for nothing.
     if (spins++ == 0) wait_start = clk::now();

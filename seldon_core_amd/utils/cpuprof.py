@@ -24,8 +24,9 @@ _SYMBOLIZER = next((p for p in ("/opt/rocm/lib/llvm/bin/llvm-symbolizer", shutil
                     if p and os.path.exists(p)), None)
 
 
-def start(hz: int = 997) -> bool:
-    return bool(native().cpu_profile_start(int(hz)))
+def start(hz: int = 997, depth: int = 1) -> bool:
+    """depth > 1 also records depth - 1 callers per sample (DWARF unwinder)."""
+    return bool(native().cpu_profile_start(int(hz), int(depth)))
 
 
 def _symbolize(module: str, offsets: List[int]) -> Dict[int, str]:
@@ -43,22 +44,50 @@ def _symbolize(module: str, offsets: List[int]) -> Dict[int, str]:
             for o, b in zip(offsets, blocks)}
 
 
-def stop(top: int = 40) -> List[Dict]:
+def _short(fn: str) -> str:
+    """Drop argument lists: 'ns::f(int, std::string)' -> 'ns::f'."""
+    depth, out = 0, []
+    for ch in fn:
+        if ch == "(":
+            depth += 1
+        if depth == 0:
+            out.append(ch)
+        if ch == ")":
+            depth -= 1
+    return "".join(out).strip() or fn
+
+
+def stop(top: int = 40) -> Dict:
+    """Leaf-function table (``functions``), module shares, and with depth > 1
+    the hottest call paths (``paths``: leaf <- caller <- ...)."""
     samples = native().cpu_profile_stop()
-    by_mod: Dict[str, List] = collections.defaultdict(list)
-    for mod, off, n in samples:
-        by_mod[mod].append((off, n))
-    total = sum(n for _, _, n in samples) or 1
+    pcs: Dict[str, set] = collections.defaultdict(set)
+    for frames, _ in samples:
+        for mod, off in frames:
+            pcs[mod].add(off)
+    names: Dict[tuple, str] = {}
+    for mod, offs in pcs.items():
+        offs = sorted(offs)
+        sym = _symbolize(mod, offs)
+        for o in offs:
+            names[(mod, o)] = sym.get(o) or (f"{os.path.basename(mod)}+{hex(o)}" if mod else "[unknown]")
+    total = sum(n for _, n in samples) or 1
     funcs: Dict[tuple, int] = collections.Counter()
-    for mod, items in by_mod.items():
-        names = _symbolize(mod, [o for o, _ in items])
-        for off, n in items:
-            fn = names.get(off) or (f"{os.path.basename(mod)}+{hex(off)}" if mod else "[unknown]")
-            funcs[(fn, os.path.basename(mod) if mod else "?")] += n
+    paths: Dict[tuple, int] = collections.Counter()
+    for frames, n in samples:
+        mod, off = frames[0]
+        funcs[(names[(mod, off)], os.path.basename(mod) if mod else "?")] += n
+        if len(frames) > 1:
+            st = [_short(names[f])[:90] for f in frames if f[0] or f[1]]
+            st = [x for i, x in enumerate(st) if i == 0 or x != st[i - 1]]  # the unwinder repeats the leaf
+            paths[tuple(st)] += n
     rows = [{"function": fn[:160], "module": mod, "samples": n, "frac": round(n / total, 4)}
             for (fn, mod), n in funcs.most_common(top)]
-    mods = collections.Counter()
+    mods: Dict[str, int] = collections.Counter()
     for (fn, mod), n in funcs.items():
         mods[mod] += n
-    return {"total_samples": total, "functions": rows,
-            "modules": [{"module": m, "frac": round(n / total, 4)} for m, n in mods.most_common(12)]}
+    out = {"total_samples": total, "functions": rows,
+           "modules": [{"module": m, "frac": round(n / total, 4)} for m, n in mods.most_common(12)]}
+    if paths:
+        out["paths"] = [{"stack": list(p), "samples": n, "frac": round(n / total, 4)} for p, n in paths.most_common(top)]
+    return out
