@@ -26,7 +26,7 @@ const double kGrowth = std::pow(2.0, 1.0 / 8.0);
 
 inline int bucket_of(double s) {
   if (!(s > kBase)) return 0;
-  int b = int(std::log(s / kBase) / std::log(kGrowth)) + 1;
+  int b = int(8.0 * std::log2(s / kBase)) + 1;  // 2^(1/8) growth
   return std::min(b, Histogram::kBuckets - 1);
 }
 inline double bucket_upper(int b) { return kBase * std::pow(kGrowth, b); }
@@ -43,15 +43,45 @@ std::string sanitize(const std::string& n) {
 }
 }  // namespace
 
+namespace {
+int stripe_of_this_thread() {
+  static std::atomic<int> next{0};
+  thread_local const int idx = next.fetch_add(1, std::memory_order_relaxed) % Histogram::kStripes;
+  return idx;
+}
+}  // namespace
+
 void Histogram::observe(double s) {
-  buckets_[bucket_of(s)].fetch_add(1, std::memory_order_relaxed);
-  count_.fetch_add(1, std::memory_order_relaxed);
-  atomic_add_double(sum_bits_, s);
-  atomic_max_double(max_bits_, s);
+  Stripe& st = stripes_[stripe_of_this_thread()];
+  st.buckets[bucket_of(s)].fetch_add(1, std::memory_order_relaxed);
+  st.count.fetch_add(1, std::memory_order_relaxed);
+  atomic_add_double(st.sum_bits, s);
+  atomic_max_double(st.max_bits, s);
 }
 
-double Histogram::sum() const { return bits_to_d(sum_bits_.load(std::memory_order_relaxed)); }
-double Histogram::max() const { return bits_to_d(max_bits_.load(std::memory_order_relaxed)); }
+uint64_t Histogram::count() const {
+  uint64_t n = 0;
+  for (const auto& st : stripes_) n += st.count.load(std::memory_order_relaxed);
+  return n;
+}
+
+double Histogram::sum() const {
+  double v = 0.0;
+  for (const auto& st : stripes_) v += bits_to_d(st.sum_bits.load(std::memory_order_relaxed));
+  return v;
+}
+
+double Histogram::max() const {
+  double v = 0.0;
+  for (const auto& st : stripes_) v = std::max(v, bits_to_d(st.max_bits.load(std::memory_order_relaxed)));
+  return v;
+}
+
+uint64_t Histogram::bucket_total(int b) const {
+  uint64_t n = 0;
+  for (const auto& st : stripes_) n += st.buckets[b].load(std::memory_order_relaxed);
+  return n;
+}
 
 double Histogram::quantile(double q) const {
   uint64_t n = count();
@@ -60,7 +90,7 @@ double Histogram::quantile(double q) const {
   if (target == 0) target = 1;
   uint64_t acc = 0;
   for (int b = 0; b < kBuckets; ++b) {
-    acc += buckets_[b].load(std::memory_order_relaxed);
+    acc += bucket_total(b);
     if (acc >= target) return std::min(bucket_upper(b), max());
   }
   return max();
@@ -70,23 +100,29 @@ uint64_t Histogram::count_le(double s) const {
   uint64_t acc = 0;
   for (int b = 0; b < kBuckets; ++b) {
     if (bucket_upper(b) > s * (1 + 1e-9)) break;
-    acc += buckets_[b].load(std::memory_order_relaxed);
+    acc += bucket_total(b);
   }
   return acc;
 }
 
 void Histogram::copy_from(const Histogram& o) {
-  for (int b = 0; b < kBuckets; ++b) buckets_[b].store(o.buckets_[b].load(std::memory_order_relaxed));
-  count_.store(o.count_.load(std::memory_order_relaxed));
-  sum_bits_.store(o.sum_bits_.load(std::memory_order_relaxed));
-  max_bits_.store(o.max_bits_.load(std::memory_order_relaxed));
+  for (int i = 0; i < kStripes; ++i) {
+    Stripe& d = stripes_[i];
+    const Stripe& src = o.stripes_[i];
+    for (int b = 0; b < kBuckets; ++b) d.buckets[b].store(src.buckets[b].load(std::memory_order_relaxed));
+    d.count.store(src.count.load(std::memory_order_relaxed));
+    d.sum_bits.store(src.sum_bits.load(std::memory_order_relaxed));
+    d.max_bits.store(src.max_bits.load(std::memory_order_relaxed));
+  }
 }
 
 void Histogram::reset() {
-  for (auto& b : buckets_) b.store(0);
-  count_.store(0);
-  sum_bits_.store(0);
-  max_bits_.store(0);
+  for (auto& st : stripes_) {
+    for (auto& b : st.buckets) b.store(0);
+    st.count.store(0);
+    st.sum_bits.store(0);
+    st.max_bits.store(0);
+  }
 }
 
 void Series::inc(double v) { atomic_add_double(value_bits, v); }

@@ -21,12 +21,17 @@ namespace sca {
 
 using Labels = std::vector<std::pair<std::string, std::string>>;
 
+// Log-bucketed latency histogram.  Observations go to one of kStripes
+// cache-line-aligned stripes chosen by the observing thread, so the front-end
+// workers that time every request do not bounce one set of counters between
+// cores; readers (scrapes) sum the stripes.
 class Histogram {
  public:
   static constexpr int kBuckets = 240;  // 2^(1/8) spaced from 1us
+  static constexpr int kStripes = 8;
   void observe(double seconds);
   double quantile(double q) const;
-  uint64_t count() const { return count_.load(std::memory_order_relaxed); }
+  uint64_t count() const;
   double sum() const;
   double max() const;
   uint64_t count_le(double seconds) const;
@@ -34,10 +39,14 @@ class Histogram {
   void reset();
 
  private:
-  std::atomic<uint64_t> buckets_[kBuckets] = {};
-  std::atomic<uint64_t> count_{0};
-  std::atomic<uint64_t> sum_bits_{0};
-  std::atomic<uint64_t> max_bits_{0};
+  struct alignas(64) Stripe {
+    std::atomic<uint64_t> buckets[kBuckets] = {};
+    std::atomic<uint64_t> count{0};
+    std::atomic<uint64_t> sum_bits{0};
+    std::atomic<uint64_t> max_bits{0};
+  };
+  uint64_t bucket_total(int b) const;
+  Stripe stripes_[kStripes];
 };
 
 struct Series {

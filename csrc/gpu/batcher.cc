@@ -409,56 +409,101 @@ bool BatchedUnit::launch(Slot* s) {
   return false;
 }
 
-void BatchedUnit::handoff_loop() {
-  std::vector<Handoff> batch;
-  while (true) {
-    {
-      std::unique_lock<std::mutex> lk(ho_mu_);
-      if (ho_q_.empty()) {
-        if (ho_stop_) return;
-        ho_sleeping_ = true;
-        ho_cv_.wait(lk, [&] { return ho_stop_ || !ho_q_.empty(); });
-        ho_sleeping_ = false;
-        if (ho_q_.empty()) return;  // stopping with nothing left
-      }
-      batch.swap(ho_q_);
-    }
-    for (auto& h : batch) post_responses(h);
-    batch.clear();
+BatchedUnit::ParcelPool::~ParcelPool() {
+  for (Parcel* p = head.load(); p;) {
+    Parcel* n = p->next;
+    delete p;
+    p = n;
   }
 }
 
-// One task per front-end executor: it builds its requests' responses from the
-// shared output block and runs their continuations on that thread.
-void BatchedUnit::post_responses(Handoff& h) {
-  struct Req {
-    Item item;
-    size_t off;
+void BatchedUnit::ParcelPool::put(Parcel* p) {
+  Parcel* h = head.load(std::memory_order_relaxed);
+  do {
+    p->next = h;
+  } while (!head.compare_exchange_weak(h, p, std::memory_order_release, std::memory_order_relaxed));
+}
+
+void BatchedUnit::Parcel::run() {
+  size_t off = 0;
+  for (auto& it : items) {
+    Done k = std::move(it.k);
+    k(Outcome::ok(make_response(*info, it, y.data() + off, oc)));
+    off += size_t(it.rows) * size_t(oc);
+  }
+  items.clear();  // destroys the Items on the thread that created them
+  y.clear();
+  std::shared_ptr<ParcelPool> keep = std::move(pool);  // the pool may go with the last reference
+  keep->put(this);
+}
+
+void BatchedUnit::handoff_loop() {
+  std::vector<Handoff> batch;
+  std::vector<Parcel*> spare;
+  while (true) {
+    {
+      std::unique_lock<std::mutex> lk(ho_mu_);
+      for (auto& h : batch) ho_free_.push_back(std::move(h));  // emptied below: capacity goes back
+      batch.clear();
+      if (ho_q_.empty()) {
+        if (ho_stop_) break;
+        ho_sleeping_ = true;
+        ho_cv_.wait(lk, [&] { return ho_stop_ || !ho_q_.empty(); });
+        ho_sleeping_ = false;
+        if (ho_q_.empty()) break;  // stopping with nothing left
+      }
+      batch.swap(ho_q_);
+    }
+    for (auto& h : batch) post_responses(h, spare);
+  }
+  for (Parcel* p : spare) delete p;
+}
+
+// One parcel per front-end executor: its task builds the responses and runs
+// the continuations on that thread.
+void BatchedUnit::post_responses(Handoff& h, std::vector<Parcel*>& spare) {
+  Parcel* groups[32];
+  int ng = 0;
+  auto fresh = [&]() -> Parcel* {
+    if (spare.empty())
+      for (Parcel* p = parcels_->take_all(); p; p = p->next) spare.push_back(p);
+    Parcel* p;
+    if (spare.empty()) {
+      p = new Parcel();
+    } else {
+      p = spare.back();
+      spare.pop_back();
+    }
+    p->pool = parcels_;
+    p->info = resp_;
+    p->oc = h.out_cols;
+    return p;
   };
-  struct Group {
-    ExecPtr ex;
-    std::shared_ptr<std::vector<Req>> reqs;
+  auto flush = [&](Parcel* p) {
+    ExecPtr ex = p->items.front().exec;
+    ex->post([p] { p->run(); });
   };
-  std::vector<Group> groups;
+  const int oc = h.out_cols;
   for (size_t i = 0; i < h.items.size(); ++i) {
     Item& it = h.items[i];
-    Group* g = nullptr;
-    for (auto& gg : groups)
-      if (gg.ex.get() == it.exec.get()) { g = &gg; break; }
+    Parcel* g = nullptr;
+    for (int j = 0; j < ng; ++j)
+      if (groups[j]->items.front().exec.get() == it.exec.get()) { g = groups[j]; break; }
     if (!g) {
-      groups.push_back(Group{it.exec, std::make_shared<std::vector<Req>>()});
-      g = &groups.back();
-    }
-    g->reqs->push_back(Req{std::move(it), h.offs[i]});
-  }
-  for (auto& g : groups) {
-    g.ex->post([info = resp_, reqs = g.reqs, out = h.out, oc = h.out_cols]() {
-      for (auto& r : *reqs) {
-        Done k = std::move(r.item.k);
-        k(Outcome::ok(make_response(*info, r.item, out->data() + r.off, oc)));
+      if (ng == 32) {  // more executors than the table holds: ship what we have
+        for (int j = 0; j < ng; ++j) flush(groups[j]);
+        ng = 0;
       }
-    });
+      g = groups[ng++] = fresh();
+    }
+    const double* src = h.out.data() + h.offs[i];
+    g->y.insert(g->y.end(), src, src + size_t(it.rows) * oc);
+    g->items.push_back(std::move(it));
   }
+  for (int j = 0; j < ng; ++j) flush(groups[j]);
+  h.items.clear();
+  h.offs.clear();
+  h.out.clear();
 }
 
 void BatchedUnit::complete(Slot* s, hipError_t st) {
@@ -491,6 +536,13 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     const int oc = s->out_cols;
     const double* out = cpu_ ? s->cpu_out.data() : s->h_out.host<double>();
     Handoff h;
+    {
+      std::lock_guard<std::mutex> g(ho_mu_);
+      if (!ho_free_.empty()) {  // reuse a drained hand-off's buffers
+        h = std::move(ho_free_.back());
+        ho_free_.pop_back();
+      }
+    }
     h.out_cols = oc;
     size_t row = 0;
     for (auto& it : items) {
@@ -505,7 +557,7 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
       row += r;
     }
     if (!h.items.empty()) {
-      h.out = std::make_shared<std::vector<double>>(out, out + size_t(s->rows) * oc);
+      h.out.assign(out, out + size_t(s->rows) * oc);
       bool wake;
       {
         std::lock_guard<std::mutex> g(ho_mu_);

@@ -160,14 +160,37 @@ class BatchedUnit : public Unit {
   struct Handoff {
     std::vector<Item> items;
     std::vector<size_t> offs;  // each item's first output value in `out`
-    std::shared_ptr<std::vector<double>> out;
+    std::vector<double> out;
     int out_cols = 0;
+  };
+
+  // One batch's requests bound for one front-end executor, with their output
+  // rows.  Parcels are recycled: the worker that ran one returns it to the
+  // pool, the hand-off thread refills it, so in steady state no buffer is
+  // allocated on one thread and freed on another (cross-thread frees took the
+  // allocator's arena locks in the r02i CPU profiles).  The Items themselves
+  // were created by the worker that finally destroys them.
+  struct Parcel;
+  struct ParcelPool {
+    std::atomic<Parcel*> head{nullptr};
+    ~ParcelPool();
+    void put(Parcel* p);  // lock-free push (any thread)
+    Parcel* take_all() { return head.exchange(nullptr, std::memory_order_acquire); }  // single consumer
+  };
+  struct Parcel {
+    std::shared_ptr<ParcelPool> pool;  // set while out of the pool
+    std::shared_ptr<const RespInfo> info;
+    std::vector<Item> items;
+    std::vector<double> y;  // the items' output rows, back to back
+    int oc = 0;
+    Parcel* next = nullptr;
+    void run();  // on the executor: respond to every item, then go back to the pool
   };
 
   void ensure_capacity(Slot& s, int rows, int cols);
   void device_loop();
   void handoff_loop();
-  void post_responses(Handoff& h);
+  void post_responses(Handoff& h, std::vector<Parcel*>& spare);
   bool launch(Slot* s);
   void complete(Slot* s, hipError_t st);
   void abandon(Slot* s);
@@ -216,6 +239,8 @@ class BatchedUnit : public Unit {
   std::mutex ho_mu_;
   std::condition_variable ho_cv_;
   std::vector<Handoff> ho_q_;   // guarded by ho_mu_
+  std::vector<Handoff> ho_free_;  // emptied hand-offs, reused by the device thread (guarded by ho_mu_)
+  std::shared_ptr<ParcelPool> parcels_ = std::make_shared<ParcelPool>();
   bool ho_sleeping_ = false;    // guarded by ho_mu_
   bool ho_stop_ = false;        // guarded by ho_mu_
   mutable std::mutex stats_mu_;

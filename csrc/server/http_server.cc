@@ -209,6 +209,9 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
   bool wake_pending = false;                // eventfd written and not yet drained (guarded by qmu)
   std::atomic<bool> stop{false};
   std::unordered_map<std::string, Series*> timers;
+  Series* last_timer = nullptr;
+  int last_status = 0;
+  std::string last_uri;
 
   ~Worker() {
     for (auto& kv : conns)
@@ -219,9 +222,16 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
   }
 
   Series* server_timer(const std::string& uri, int status) {
+    // hot path: the last (uri, status) seen by this worker, without building a key
+    if (last_timer && status == last_status && uri == last_uri) return last_timer;
     std::string key = uri + "#" + std::to_string(status);
     auto it = timers.find(key);
-    if (it != timers.end()) return it->second;
+    if (it != timers.end()) {
+      last_timer = it->second;
+      last_status = status;
+      last_uri = uri;
+      return it->second;
+    }
     Labels l = {{"deployment_name", srv->engine_->options().deployment_name},
                 {"predictor_name", srv->engine_->spec().name.empty() ? "unknown" : srv->engine_->spec().name},
                 {"predictor_version", [&] {
