@@ -429,6 +429,7 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
       if (r > 0) {
         ssize_t rv = nghttp2_session_mem_recv(c->session, buf, size_t(r));
         if (rv < 0) { close_conn(c); return; }
+        if (size_t(r) < sizeof buf) break;  // drained (edge-triggered: the next arrival is reported)
         continue;
       }
       if (r == 0) { close_conn(c); return; }

@@ -304,6 +304,10 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
       if (r > 0) {
         if (c->in_off > 0 && c->in_off == c->in.size()) { c->in.clear(); c->in_off = 0; }
         c->in.append(buf, size_t(r));
+        // A short read drained the socket: edge-triggered epoll reports the
+        // next arrival (or the peer's FIN), so skip the read that would
+        // only return EAGAIN -- one syscall less per request.
+        if (size_t(r) < sizeof buf) break;
         continue;
       }
       if (r == 0) {  // peer closed: finish in-flight work, then close

@@ -187,7 +187,11 @@ struct Worker {
         if (evs[i].events & EPOLLIN) {
           while (true) {
             ssize_t r = ::recv(c.fd, buf, sizeof buf, 0);
-            if (r > 0) { c.in.append(buf, size_t(r)); continue; }
+            if (r > 0) {
+              c.in.append(buf, size_t(r));
+              if (size_t(r) < sizeof buf) break;  // drained (edge-triggered epoll)
+              continue;
+            }
             if (r == 0) { fprintf(stderr, "server closed connection\n"); exit(4); }
             break;
           }
@@ -339,6 +343,7 @@ struct Worker {
             ssize_t r = ::recv(c.fd, buf, sizeof buf, 0);
             if (r > 0) {
               if (nghttp2_session_mem_recv(c.s, buf, size_t(r)) < 0) { fprintf(stderr, "h2 recv error\n"); exit(4); }
+              if (size_t(r) < sizeof buf) break;  // drained (edge-triggered epoll)
               continue;
             }
             if (r == 0) { fprintf(stderr, "server closed connection\n"); exit(4); }

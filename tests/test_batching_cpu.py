@@ -106,3 +106,36 @@ def test_batch_device_time_histogram_exported(served):
     body = urllib.request.urlopen(f"http://127.0.0.1:{h.http_port}/prometheus", timeout=10).read().decode()
     assert "# TYPE seldon_gpu_batch_device_seconds histogram" in body
     assert 'seldon_gpu_batch_device_seconds_bucket{' in body and "seldon_gpu_batch_rows_p99" in body
+
+
+def test_loadgen_storm_through_shards_handoff_and_parcels():
+    """Closed-loop storm (native load generator, 128 users over 4 front-end
+    threads) through the sharded submission queue, the hand-off thread and
+    the recycled response parcels: no failed request, every request counted
+    once, batches shared, and answers still correct afterwards."""
+    import os
+    import subprocess
+
+    clf = iris_logistic_regression()
+    dep = sca.Deployment(_spec({"name": "clf", "type": "MODEL"}), components={"clf": clf}, device=-1,
+                         batcher={"cpu_batching": True, "slots": 3})
+    h = dep.serve(http_port=0, grpc_port=0, threads=4, host="127.0.0.1")
+    try:
+        lg = os.path.join(os.path.dirname(sca.__file__), "bin", "sca_loadgen")
+        body = json.dumps({"data": {"names": ["a", "b", "c", "d"], "ndarray": [[5.1, 3.5, 1.4, 0.2]]}})
+        dep.batched["clf"].reset_stats()
+        res = subprocess.run([lg, "--host", "127.0.0.1", "--port", str(h.http_port), "--users", "128", "--threads", "2",
+                              "--steps", "2", "--warmup", "0", "--step-requests", "3000", "--mode", "rest",
+                              "--path", "/api/v0.1/predictions", "--body", body],
+                             capture_output=True, text=True, timeout=240)
+        out = json.loads(res.stdout.strip().splitlines()[-1])
+        assert out["errors"] == 0 and out["ok"] == 6000, out
+        st = dep.batched["clf"].stats()
+        assert st["requests"] == 6000 and st["rows"] == 6000, st
+        assert st["batches"] < st["requests"]  # concurrent requests shared batches
+        X = np.random.default_rng(7).uniform(0, 8, (5, 4))
+        got = dep.predict({"data": {"ndarray": X.tolist()}})
+        np.testing.assert_allclose(np.array(got["data"]["ndarray"]), clf.predict_proba(X), rtol=1e-12)
+    finally:
+        h.stop()
+        dep.close()
