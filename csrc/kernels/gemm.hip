@@ -219,17 +219,19 @@ __device__ __forceinline__ int xcd_tile(int L, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
 }
 
-template <int AMODE, int BM, int BN>
-__global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs a) {
-  constexpr int TM = BM / 32;                 // 16-row tiles per wave (2 waves along M)
-  constexpr int TN = BN / 32;                 // 16-col tiles per wave (2 waves along N)
-  constexpr int CA = BM * 8 / 256;            // A staging chunks per thread (BM rows x 8 chunks)
-  constexpr int CW = BN * 8 / 256;            // W staging chunks per thread
+template <int AMODE, int BM, int BN, int NT>
+__global__ __launch_bounds__(NT) void gemm_bf16_lds_kernel(const DenseGemmArgs a) {
+  constexpr int WN = NT / 128;                // waves along N (2 along M); each wave owns BM/2 x 32
+  constexpr int TM = BM / 32;                 // 16-row tiles per wave
+  constexpr int TN = 2;                       // 16-col tiles per wave
+  static_assert(BN == 32 * WN, "BN must be 32 x waves along N");
+  constexpr int CA = BM * 8 / NT;             // A staging chunks per thread (BM rows x 8 chunks)
+  constexpr int CW = BN * 8 / NT;             // W staging chunks per thread
   constexpr int kBuf = (BM + BN) * kLdr;      // one LDS buffer: A panel then W panel
-  static_assert(CA >= 1 && CW >= 1, "tile too small for 256 stagers");
+  static_assert(CA >= 1 && CW >= 1, "tile too small for the stagers");
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * kBuf];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave >> 1, wc = wave & 1, r16 = lane & 15, kq = lane >> 4;
+  const int wr = wave / WN, wc = wave % WN, r16 = lane & 15, kq = lane >> 4;
   const int nN = (a.Np + BN - 1) / BN;
   const int t = a.xcd_remap ? xcd_tile(blockIdx.x, gridDim.x) : int(blockIdx.x);
   const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
@@ -241,12 +243,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
   auto gload = [&](int ks, bf16x8* ra, bf16x8* rw) {
 #pragma unroll
     for (int j = 0; j < CA; ++j) {
-      const int c = tid + 256 * j;
+      const int c = tid + NT * j;
       ra[j] = stage_a<AMODE>(a, m0 + (c >> 3), ks * kBK + (c & 7) * 8);
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
-      const int c = tid + 256 * j;
+      const int c = tid + NT * j;
       rw[j] = *reinterpret_cast<const bf16x8*>(W + size_t(min(n0 + (c >> 3), a.Np - 1)) * a.Kp + ks * kBK +
                                                (c & 7) * 8);
     }
@@ -256,12 +258,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
     __bf16* Ws = As + BM * kLdr;
 #pragma unroll
     for (int j = 0; j < CA; ++j) {
-      const int c = tid + 256 * j;
+      const int c = tid + NT * j;
       *reinterpret_cast<bf16x8*>(As + (c >> 3) * kLdr + (c & 7) * 8) = ra[j];
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
-      const int c = tid + 256 * j;
+      const int c = tid + NT * j;
       *reinterpret_cast<bf16x8*>(Ws + (c >> 3) * kLdr + (c & 7) * 8) = rw[j];
     }
   };
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
         af[i] = *reinterpret_cast<const bf16x8*>(As + (wr * (BM / 2) + i * 16 + r16) * kLdr + kk * 32 + kq * 8);
 #pragma unroll
       for (int i = 0; i < TN; ++i)
-        bf[i] = *reinterpret_cast<const bf16x8*>(Ws + (wc * (BN / 2) + i * 16 + r16) * kLdr + kk * 32 + kq * 8);
+        bf[i] = *reinterpret_cast<const bf16x8*>(Ws + (wc * 32 + i * 16 + r16) * kLdr + kk * 32 + kq * 8);
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -309,7 +311,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
   // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
-    const int col = n0 + wc * (BN / 2) + tn * 16 + r16;
+    const int col = n0 + wc * 32 + tn * 16 + r16;
     if (col >= a.Np) continue;
     const bool live = col < a.N;
     const float bias = live ? a.bias[col] : 0.f;
@@ -342,41 +344,48 @@ __global__ __launch_bounds__(256) void gemm_bf16_lds_kernel(const DenseGemmArgs 
 
 template <int AMODE>
 void launch_bf16(const DenseGemmArgs& a, hipStream_t s) {
-  // 128 x 64 tiles (two resident workgroups per CU) when they fill the chip;
+  // 128 x 64 tiles (two resident workgroups per CU) when they fill the chip,
   // 32 x 64 otherwise (narrow layers such as a 10-class head: 4x the
-  // workgroups, so the A stream is spread over every CU)
+  // workgroups, so the A stream is spread over every CU).  The VAE decoder's
+  // first layer (AMODE 2) recomputes its reparameterised A panel per N tile,
+  // so it takes 128 x 128 tiles on 8 waves: half the draws, 71.5 -> 44 us at
+  // 40960 x 128 (profiles/r02h_gemm); for plain A the 128 x 128 variant and
+  // a global_load_lds 3-stage ring at one workgroup per CU measured slower.
   const int nN = (a.Np + 63) / 64;
   const int big = nN * ((a.rows_eff + 127) / 128);
-  if (big >= 256) {
-    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 128, 64>), dim3(big), dim3(256), 0, s, a);
+  const int wide = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
+  if (AMODE == 2 && wide >= 256) {
+    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 128, 128, 512>), dim3(wide), dim3(512), 0, s, a);
+  } else if (big >= 256) {
+    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 128, 64, 256>), dim3(big), dim3(256), 0, s, a);
   } else {
     const int small = nN * ((a.rows_eff + 31) / 32);
-    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 32, 64>), dim3(small), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 32, 64, 256>), dim3(small), dim3(256), 0, s, a);
   }
 }
 
-// fp64 [rows][F] -> bf16 [rows][ld] (zero-padded): 8 outputs per thread, one
-// 16-B store; 16-B loads when the 8 inputs are in one aligned row run
+// fp64 [rows][F] -> bf16 [rows][ld] (zero-padded).  Each lane converts one
+// pair of adjacent columns per step: the wave's 16-B loads and 4-B stores are
+// lane-contiguous.
 __global__ void convert_bf16_kernel(const double* __restrict__ X, int rows, int F, int ld, __bf16* __restrict__ out) {
-  const int per_row = ld >> 3;  // ld % 8 == 0 (Kpb is a multiple of 64)
-  const size_t n = size_t(rows) * per_row;
+  const int half = ld >> 1;  // ld is even (a multiple of 64)
+  const size_t n = size_t(rows) * half;
   using f64x2 = __attribute__((ext_vector_type(2))) double;
+  using bf16x2 = __attribute__((ext_vector_type(2))) __bf16;
+  const bool vec = (F & 1) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
-    const int r = int(i / per_row), c0 = int(i - size_t(r) * per_row) * 8;
-    const double* x = X + size_t(r) * F + c0;
-    bf16x8 v;
-    if (c0 + 8 <= F && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f64x2 d = reinterpret_cast<const f64x2*>(x)[j];
-        v[2 * j] = __bf16(float(d[0]));
-        v[2 * j + 1] = __bf16(float(d[1]));
-      }
+    const int r = int(i / half), c = int(i - size_t(r) * half) * 2;
+    const double* x = X + size_t(r) * F + c;
+    bf16x2 v;
+    if (c + 2 <= F && vec) {
+      const f64x2 d = *reinterpret_cast<const f64x2*>(x);
+      v[0] = __bf16(float(d[0]));
+      v[1] = __bf16(float(d[1]));
     } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = __bf16(c0 + j < F ? float(x[j]) : 0.f);
+      v[0] = __bf16(c < F ? float(x[0]) : 0.f);
+      v[1] = __bf16(c + 1 < F ? float(x[1]) : 0.f);
     }
-    reinterpret_cast<bf16x8*>(out)[i] = v;
+    reinterpret_cast<bf16x2*>(out)[i] = v;
   }
 }
 
@@ -414,9 +423,9 @@ void dense_gemm(const DenseGemmArgs& a, hipStream_t s) {
 
 void convert_bf16(const double* X, int rows, int F, int ld, void* out, hipStream_t s) {
   if (rows <= 0) return;
-  const size_t n = size_t(rows) * (ld / 8);
-  const int bs = n < (size_t(256) << 10) ? 64 : 256;  // small batches: more, narrower workgroups
-  const int blocks = int((n + bs - 1) / bs < 4096 ? (n + bs - 1) / bs : 4096);
+  const size_t n = size_t(rows) * (ld / 2);
+  const int bs = 256;
+  const int blocks = int((n + bs - 1) / bs < 8192 ? (n + bs - 1) / bs : 8192);
   hipLaunchKernelGGL(convert_bf16_kernel, dim3(blocks), dim3(bs), 0, s, X, rows, F, ld, static_cast<__bf16*>(out));
 }
 

@@ -6,7 +6,7 @@ for d in sorted(glob.glob('gpurun_out/ab_*/')):
     acc = collections.defaultdict(list)
     for r in rows:
         n = r['Kernel_Name']
-        m = re.search(r'(gemm_bf16_lds_kernel<[^>]*>|convert_bf16_kernel|mlp_finish_kernel|mlp_convert_kernel)', n)
+        m = re.search(r'(gemm_bf16_g?lds_kernel<[^>]*>|convert_bf16_kernel|mlp_finish_kernel|mlp_convert_kernel)', n)
         if m:
             key = m.group(1) + ' wgs=' + str(int(r['Grid_Size_X'])//int(r['Workgroup_Size_X']))
             acc[key].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1000)
