@@ -12,6 +12,10 @@
 //   core_stress engine <requests>  concurrent predict / feedback / metrics / tracing
 //   core_stress serve              HTTP + gRPC front ends; prints "PORTS <http> <grpc>",
 //                                  serves until stdin closes (the test drives sca_loadgen)
+//   core_stress batcher <requests> the GPU micro-batcher's host machinery on its CPU
+//                                  path (cpu_batching): per-thread submission shards,
+//                                  device thread, hand-off thread, recycled response
+//                                  parcels posted to 8 executors by 8 producer threads
 //
 // Exit status 0 = every check passed; sanitizer reports make it non-zero.
 #include <unistd.h>
@@ -26,7 +30,13 @@
 #include <thread>
 #include <vector>
 
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+
 #include "core/engine.h"
+#include "gpu/batcher.h"
 #include "core/json.h"
 #include "core/message.h"
 #include "core/spec.h"
@@ -227,6 +237,123 @@ void serve_mode() {
   std::cout << "served " << http.requests_served() << std::endl;
 }
 
+// ---------------------------------------------------------------- batcher
+// y = [sum(x), 2 * x0, rows_in_batch-independent id]: each request can check
+// its own answer.
+class FakeRowModel : public gpu::RowModel {
+ public:
+  std::string name() const override { return "fake"; }
+  int in_cols() const override { return 4; }
+  int out_cols(int) const override { return 3; }
+  void to_device(int) override {}
+  void launch(const double*, int, int, double*, void*, hipStream_t) override {
+    throw std::runtime_error("fake model has no device path");
+  }
+  void run_cpu(const double* X, int rows, int cols, double* out) const override {
+    for (int r = 0; r < rows; ++r) {
+      const double* x = X + size_t(r) * cols;
+      out[r * 3 + 0] = x[0] + x[1] + x[2] + x[3];
+      out[r * 3 + 1] = 2.0 * x[0];
+      out[r * 3 + 2] = x[3];
+    }
+  }
+};
+
+// One thread draining posted continuations (a front-end worker stand-in).
+class ThreadExecutor : public Executor {
+ public:
+  ThreadExecutor() : th_([this] { run(); }) {}
+  ~ThreadExecutor() override {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void post(std::function<void()> fn) override {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(std::move(fn));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  void run() {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (true) {
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;
+      auto fn = std::move(q_.front());
+      q_.pop_front();
+      lk.unlock();
+      fn();
+      lk.lock();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+  std::thread th_;
+};
+
+void batcher_mode(int n) {
+  gpu::BatcherOptions o;
+  o.device = -1;
+  o.cpu_batching = true;
+  o.slots = 3;
+  o.max_batch = 64;
+  auto unit = std::make_shared<gpu::BatchedUnit>(std::make_shared<FakeRowModel>(), o);
+  constexpr int kThreads = 8;
+  std::vector<ExecPtr> execs;
+  for (int i = 0; i < kThreads; ++i) execs.push_back(std::make_shared<ThreadExecutor>());
+  std::atomic<int> done{0}, wrong{0};
+  std::vector<std::thread> producers;
+  const std::string puid = "stress";
+  for (int t = 0; t < kThreads; ++t) {
+    producers.emplace_back([&, t] {
+      std::mt19937 rng(1234 + t);
+      for (int i = 0; i < n; ++i) {
+        const int rows = 1 + int(rng() % 3);
+        auto m = std::make_shared<SeldonMessage>();
+        m->payload = Payload::Data;
+        std::vector<double> vals;
+        for (int r = 0; r < rows; ++r) {
+          const double id = double(t) * 1e6 + i * 10 + r;
+          vals.insert(vals.end(), {1.0 * r, 0.5, 0.25, id});
+        }
+        m->data.set_dense(DataKind::Tensor, {int64_t(rows), 4}, std::move(vals));
+        // a third of the requests finish on the completing thread (no executor)
+        const ExecPtr* ex = (i % 3 == 0) ? nullptr : &execs[size_t((t + i) % kThreads)];
+        CallCtx c{nullptr, &puid, ex};
+        unit->transform_input(c, m, [&, t, i, rows](Outcome o) {
+          bool ok = !o.err && o.msg && o.msg->data.values.size() == size_t(rows) * 3;
+          if (ok)
+            for (int r = 0; r < rows; ++r) {
+              const double id = double(t) * 1e6 + i * 10 + r;
+              const double* y = o.msg->data.values.data() + r * 3;
+              ok = ok && y[0] == 1.0 * r + 0.75 + id && y[1] == 2.0 * r && y[2] == id;
+            }
+          if (!ok) wrong.fetch_add(1);
+          done.fetch_add(1);
+        });
+      }
+    });
+  }
+  for (auto& p : producers) p.join();
+  for (int spin = 0; done.load() < kThreads * n && spin < 30000; ++spin) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  const auto st = unit->stats();
+  unit->stop();
+  execs.clear();
+  check(done.load() == kThreads * n, "every batched request answered exactly once");
+  check(wrong.load() == 0, "every batched request got its own rows back");
+  check(st.requests == uint64_t(kThreads) * n, "batcher counted every request");
+  check(st.batches < st.requests, "requests shared batches");
+  std::cout << "batches " << st.batches << " requests " << st.requests << std::endl;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -240,8 +367,10 @@ int main(int argc, char** argv) {
     engine_mode(n);
   } else if (mode == "serve") {
     serve_mode();
+  } else if (mode == "batcher") {
+    batcher_mode(n);
   } else {
-    std::cerr << "usage: core_stress fuzz|engine|serve [n]\n";
+    std::cerr << "usage: core_stress fuzz|engine|serve|batcher [n]\n";
     return 2;
   }
   if (fails) {

@@ -1,5 +1,5 @@
 """Sanitizer runs of the native host core: ASan+UBSan and TSan
-builds of the codecs, graph executor and HTTP/gRPC front ends
+builds of the codecs, graph executor, HTTP/gRPC front ends and the micro-batcher host machinery
 (tools/build_sanitizers.py, csrc/tests/core_stress.cc).  Device kernels are
 not sanitizer-built: GPU ASan is unavailable on the MI355X pool."""
 import json
@@ -30,7 +30,7 @@ def _clean(stderr: str) -> bool:
             and "WARNING: ThreadSanitizer" not in stderr and "ERROR: LeakSanitizer" not in stderr)
 
 
-@pytest.mark.parametrize("mode,n", [("fuzz", "2000"), ("engine", "3000")])
+@pytest.mark.parametrize("mode,n", [("fuzz", "2000"), ("engine", "3000"), ("batcher", "2000")])
 def test_core_stress(stress_exe, mode, n):
     exe, kind = stress_exe
     r = subprocess.run([exe, mode, n], capture_output=True, text=True, timeout=600, env=SAN_ENV)

@@ -7,7 +7,9 @@ gRPC front ends -- plus ``csrc/tests/core_stress.cc``, with
 
 * ``asan``: ``-fsanitize=address,undefined`` (heap/stack misuse, leaks, UB)
 * ``tsan``: ``-fsanitize=thread`` (data races in continuations, executors,
-  front-end workers, metrics registry, traffic split)
+  front-end workers, metrics registry, traffic split, the micro-batcher's
+  submission shards / device thread / hand-off thread / response parcels on
+  its CPU path)
 
 GPU code is not part of these builds: GPU AddressSanitizer / XNACK runs are
 not available on the MI355X pool, so device kernels are checked by numerics
@@ -31,6 +33,7 @@ SOURCES = [
     "core/json.cc", "core/message.cc", "core/pbwire.cc", "core/spec.cc", "core/metrics.cc",
     "core/engine.cc", "core/units.cc", "core/msglog.cc", "core/roctx.cc",
     "server/http_server.cc", "server/grpc_server.cc", "server/remote_unit.cc",
+    "gpu/batcher.cc",  # host machinery only: the stress driver runs it on its CPU path
     "tests/core_stress.cc",
 ]
 FLAGS = {
@@ -57,7 +60,7 @@ def _compile(kind: str, src_rel: str, inc: Path) -> Path:
     if fresh:
         return obj
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Wall", "-Wno-unused-function",
-           *FLAGS[kind], f"-I{CSRC}", f"-I{inc}", "-I/opt/rocm/include", "-MMD", "-MF", str(dep), "-c", str(src), "-o", str(obj)]
+           *FLAGS[kind], f"-I{CSRC}", f"-I{inc}", "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-MMD", "-MF", str(dep), "-c", str(src), "-o", str(obj)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"[{kind}] compile failed: {src_rel}\n{res.stderr}")
@@ -71,7 +74,7 @@ def build(kind: str, jobs: int = 8) -> Path:
     out = BUILD / kind / "core_stress"
     if not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
         cmd = ["g++", *FLAGS[kind], *map(str, objs), str(ng), f"-Wl,-rpath,{ng.parent}",
-               "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lpthread", "-o", str(out)]
+               "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lamdhip64", "-lpthread", "-o", str(out)]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"[{kind}] link failed\n{res.stderr}")
