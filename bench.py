@@ -404,7 +404,11 @@ def timed(d: Dist, fn, cpu: dict | None = None):
     d.sync()
     c0 = cpu_seconds()
     t0 = time.perf_counter()
-    out = fn()
+    err = None
+    try:
+        out = fn()
+    except Exception as e:  # still meet the closing barrier, or the other ranks would wait forever
+        out, err = None, e
     d.sync()
     wall = time.perf_counter() - t0
     if cpu is not None:  # CPUs busy over the window, server side vs load generator
@@ -412,6 +416,8 @@ def timed(d: Dist, fn, cpu: dict | None = None):
         cpu["server_cpus"] = round((c1[0] - c0[0]) / wall, 2)
         cpu["loadgen_cpus"] = round((c1[1] - c0[1]) / wall, 2)
     d.barrier()
+    if err is not None:
+        raise err
     return out, wall
 
 
@@ -423,13 +429,23 @@ def measure_variant(args, d: Dist, wl: Workload, kind: str, spin: bool) -> dict:
     ngpu = sca.gpu_count() if d.has_gpu else 0
     span = max(2, d.world) if kind == "mab" else VARIANT_SPAN[kind]
     devs = group_devices(d.rank, span, ngpu)
-    dep, oracle, label = make_deployment(wl, kind, devs, d.device, args.slots, spin)
-    h = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
     body = json.dumps({"data": {"names": wl.names, "ndarray": [wl.row]}})
     sreq = max(1000, args.step_requests // 2)
+    dep = h = None
+    setup_error = None
+    try:  # everything rank-local first: a rank that fails here must not skip a collective alone
+        if os.environ.get("SCA_BENCH_FAULT") == f"{kind}:{d.rank}":  # fault injection (tests)
+            raise RuntimeError(f"injected {kind} setup fault")
+        dep, oracle, label = make_deployment(wl, kind, devs, d.device, args.slots, spin)
+        h = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
+        run_loadgen(args, h.http_port, 1, 0, "rest", body, step_requests=sreq)  # warm every replica
+    except Exception as e:
+        setup_error = f"rank {d.rank}: {type(e).__name__}: {e}"[:400]
+    errors = [e for e in d.gather(setup_error) if e]
     fb = None
     try:
-        run_loadgen(args, h.http_port, 1, 0, "rest", body, step_requests=sreq)  # warm every replica
+        if errors:  # every rank skips the variant together
+            raise RuntimeError("; ".join(errors))
         for u in dep.batched.values():
             u.reset_stats()
         fb_out = {}
@@ -459,8 +475,10 @@ def measure_variant(args, d: Dist, wl: Workload, kind: str, spin: bool) -> dict:
             res["rows_per_device"] = routed
         return res
     finally:
-        h.stop()
-        dep.close()
+        if h is not None:
+            h.stop()
+        if dep is not None:
+            dep.close()
 
 
 def fabric_probe(d: Dist, timeout_s: float = 150.0, requests: int = 200):
@@ -567,14 +585,21 @@ def main() -> None:
     if not chk["ok"]:
         failures.append(f"rank {d.rank} headline self-check: {chk}")
     if args.extras == "auto" and args.graph == "single":
-        g, gwall = timed(d, lambda: run_loadgen(args, handle.grpc_port, args.extra_steps, 0, "grpc", pb))
-        extras["grpc"] = {"ok": g["ok"], "wall": gwall, "p50": g["p50_ms"], "p99": g["p99_ms"]}
+        try:
+            g, gwall = timed(d, lambda: run_loadgen(args, handle.grpc_port, args.extra_steps, 0, "grpc", pb))
+            extras["grpc"] = {"ok": g["ok"], "wall": gwall, "p50": g["p50_ms"], "p99": g["p99_ms"]}
+        except Exception as e:  # reported; the headline stands
+            extras["grpc"] = {"error": f"{type(e).__name__}: {e}"[:600]}
     handle.stop()
     dep.close()
     if args.extras == "auto" and args.graph == "single" and d.world >= 2 and wl.impl:
         kinds = ["abtest"] + (["pipeline"] if d.world >= 4 else []) + ["mab"]
         for kind in kinds:
-            r = measure_variant(args, d, wl, kind, spin=False)
+            try:
+                r = measure_variant(args, d, wl, kind, spin=False)
+            except Exception as e:  # reported in the JSON line; the headline stands
+                extras[kind] = {"error": f"{type(e).__name__}: {e}"[:600]}
+                continue
             if not r["check"]["ok"]:
                 failures.append(f"rank {d.rank} {kind} self-check: {r['check']}")
             extras[kind] = r
@@ -635,7 +660,9 @@ def summarize(args, d: Dist, results, label: str, wl: Workload) -> dict:
                    "cpu_budget": round(cpu_budget(), 2), "per_rank": per_rank},
     }
     ex = [r["extras"] for r in results]
-    if ex[0].get("grpc"):
+    if any("error" in e.get("grpc", {}) for e in ex):
+        line["grpc"] = {"error": next(e["grpc"]["error"] for e in ex if "error" in e.get("grpc", {}))}
+    elif ex[0].get("grpc"):
         gw = max(e["grpc"]["wall"] for e in ex)
         g = sum(e["grpc"]["ok"] for e in ex) / gw
         line["grpc"] = {"value": round(g, 2), "vs_baseline": round(g / GRPC_BASELINE, 3),
@@ -645,6 +672,10 @@ def summarize(args, d: Dist, results, label: str, wl: Workload) -> dict:
         if kind not in ex[0]:
             continue
         rs = [e[kind] for e in ex]
+        errs = [r["error"] for r in rs if "error" in r]
+        if errs:
+            variants[kind] = {"error": errs[0], "ranks_failed": len(errs)}
+            continue
         w = max(r["wall"] for r in rs)
         v = sum(r["ok"] for r in rs) / w
         variants[kind] = {

@@ -85,3 +85,20 @@ def test_group_devices_places_variant_nodes_on_distinct_gpus():
         devs = bench.group_devices(r, 8, 8)
         assert devs[0] == r and sorted(devs) == list(range(8))
     assert bench.group_devices(3, 2, 1) == [0, 0]  # one visible GPU: fold
+
+
+def test_variant_failure_on_one_rank_is_reported_not_fatal():
+    """A variant that fails on one rank (SCA_BENCH_FAULT=abtest:1) is skipped by
+    every rank together -- no rank waits alone in a collective -- and shows up
+    as an error in the line; the headline and the other variants stand."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--step-requests", "1000",
+           "--users", "16", "--fabric-probe", "none"]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", SCA_BENCH_FAULT="abtest:1")
+    env.pop("WORLD_SIZE", None)
+    res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = _json_lines(res.stdout)[0]
+    assert line["value"] > 0 and line["self_check"]["ok"]
+    ab = line["variants"]["abtest"]
+    assert "injected abtest setup fault" in ab["error"] and ab["ranks_failed"] == 2, ab
+    assert line["variants"]["mab"]["self_check"]["ok"]
