@@ -82,6 +82,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-profile", default=None,
                     help="write a sampling CPU profile of the serving process over the timed window to this JSON file")
     ap.add_argument("--cpu-profile-depth", type=int, default=1, help="frames per CPU-profile sample (>1: call paths)")
+    ap.add_argument("--variants-child", default=None, help=argparse.SUPPRESS)  # internal: isolated variant runner
     ap.add_argument("--fabric-probe", choices=["auto", "none"], default="auto",
                     help="N >= 2: after everything else, run tools/fabric_probe.py in child processes "
                          "(rank-placed graph nodes over the RCCL p2p fabric) under a time limit")
@@ -347,7 +348,7 @@ def unit_stats(dep) -> dict:
 
 
 class Dist:
-    def __init__(self):
+    def __init__(self, backend: str | None = None):
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -362,13 +363,14 @@ class Dist:
 
             if self.has_gpu:
                 torch.cuda.set_device(self.local_rank)
-            dist.init_process_group(backend="nccl" if self.has_gpu else "gloo")
+            self.backend = backend or ("nccl" if self.has_gpu else "gloo")
+            dist.init_process_group(backend=self.backend)
             self.dist = dist
         self.device = self.local_rank if self.has_gpu else -1
 
     def barrier(self):
         if self.dist is not None:
-            if self.has_gpu:
+            if self.backend == "nccl":
                 self.dist.barrier(device_ids=[self.local_rank])
             else:
                 self.dist.barrier()
@@ -481,6 +483,72 @@ def measure_variant(args, d: Dist, wl: Workload, kind: str, spin: bool) -> dict:
             dep.close()
 
 
+def child_env(d: "Dist", port: int) -> dict:
+    """Environment of a per-rank child that forms its own process group on
+    `port`.  Under torch.distributed.run the ranks carry
+    TORCHELASTIC_USE_AGENT_STORE=True (connect to the launcher's store instead
+    of hosting one): a child must not inherit that, or every rank would wait
+    for a store nobody serves on the new port."""
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(RANK=str(d.rank), LOCAL_RANK=str(d.local_rank), WORLD_SIZE=str(d.world),
+               LOCAL_WORLD_SIZE=str(d.local_world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return env
+
+
+def run_variants_isolated(args, d: Dist, argv, kinds, timeout_s: float = 900.0) -> dict:
+    """Run the multi-GPU graph variants in a child process per rank (a fresh
+    gloo process group on a new port): a device fault or hang while nodes of
+    a graph talk across GPUs ends the child, which is recorded, instead of the
+    rank that still has to print the headline line."""
+    import signal
+
+    box = [_free_port() if d.rank == 0 else None]
+    if d.dist is not None:
+        d.dist.broadcast_object_list(box, src=0)
+    env = child_env(d, box[0])
+    child_argv = [a for a in argv if a != "--variants-child"]
+    cmd = [sys.executable, os.path.abspath(__file__), *child_argv, "--variants-child", ",".join(kinds),
+           "--server-threads", str(args.server_threads), "--client-threads", str(args.client_threads)]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout_s)
+        status = None if p.returncode == 0 else f"variant runner rc={p.returncode}: {(err or '')[-400:]}"
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        status = f"variant runner timed out after {timeout_s:.0f}s"
+    res = {}
+    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+    if lines:
+        try:
+            res = json.loads(lines[-1])
+        except ValueError:
+            pass
+    for kind in kinds:
+        if kind not in res:
+            res[kind] = {"error": status or "variant runner printed no result"}
+    return res
+
+
+def variants_child(args) -> None:
+    """Entry of the isolated variant runner: measure each kind, print one JSON
+    line {kind: result} for this rank."""
+    d = Dist(backend="gloo")
+    import seldon_core_amd  # noqa: F401
+
+    wl = Workload(args.model)
+    wl.py_batching, wl.py_workers = args.py_batching, args.py_workers
+    out = {}
+    for kind in args.variants_child.split(","):
+        try:
+            out[kind] = measure_variant(args, d, wl, kind, spin=False)
+        except Exception as e:
+            out[kind] = {"error": f"{type(e).__name__}: {e}"[:600]}
+    print(json.dumps(out), flush=True)
+    d.close()
+
+
 def fabric_probe(d: Dist, timeout_s: float = 150.0, requests: int = 200):
     """Cross-process graph placement over the p2p fabric: every
     rank starts ``tools/fabric_probe.py`` as a child process in a fresh
@@ -494,8 +562,7 @@ def fabric_probe(d: Dist, timeout_s: float = 150.0, requests: int = 200):
     box = [_free_port() if d.rank == 0 else None]
     if d.dist is not None:
         d.dist.broadcast_object_list(box, src=0)
-    env = dict(os.environ, RANK=str(d.rank), LOCAL_RANK=str(d.local_rank), WORLD_SIZE=str(d.world),
-               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(box[0]))
+    env = child_env(d, box[0])
     t0 = time.perf_counter()
     p = subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "fabric_probe.py"), "--requests", str(requests)],
                          env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
@@ -535,6 +602,9 @@ def main() -> None:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
         sys.exit(2)
 
+    if args.variants_child:
+        variants_child(args)
+        return
     d = Dist()
     per_rank_cpus = size_threads(args, d.local_world)
     spin = not args.no_spin
@@ -594,13 +664,8 @@ def main() -> None:
     dep.close()
     if args.extras == "auto" and args.graph == "single" and d.world >= 2 and wl.impl:
         kinds = ["abtest"] + (["pipeline"] if d.world >= 4 else []) + ["mab"]
-        for kind in kinds:
-            try:
-                r = measure_variant(args, d, wl, kind, spin=False)
-            except Exception as e:  # reported in the JSON line; the headline stands
-                extras[kind] = {"error": f"{type(e).__name__}: {e}"[:600]}
-                continue
-            if not r["check"]["ok"]:
+        for kind, r in run_variants_isolated(args, d, argv, kinds).items():
+            if "error" not in r and not r["check"]["ok"]:
                 failures.append(f"rank {d.rank} {kind} self-check: {r['check']}")
             extras[kind] = r
     results = d.gather({"mine": mine, "extras": extras, "failures": failures})

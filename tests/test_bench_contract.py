@@ -24,7 +24,7 @@ def _json_lines(out):
 def test_bench_two_ranks_cpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--step-requests", "1000", "--users", "16", "--fabric-probe", "none"]
+           "--steps", "2", "--warmup", "1", "--step-requests", "1000", "--users", "16", "--extra-steps", "1"]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert res.returncode == 0, res.stderr[-3000:]
@@ -37,6 +37,10 @@ def test_bench_two_ranks_cpu():
     # value = both ranks' predictions over the slowest rank's window
     assert abs(line["value"] - 2 * 2 * 1000 / (line["ms_per_step"] * 2 / 1000.0)) / line["value"] < 0.01
     assert line["vs_baseline"] > 0 and line["higher_is_better"] is True
+    # the driver's launch path (torch.distributed.run): the isolated variant
+    # runner and the fabric probe form their own process groups from the ranks
+    assert line["variants"]["abtest"]["self_check"]["ok"] and line["variants"]["mab"]["self_check"]["ok"]
+    assert line["rccl_fabric"]["ok"], line["rccl_fabric"]
 
 
 def test_bench_direct_launch_spawns_ranks_and_runs_variants():
