@@ -521,8 +521,7 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     return;
   }
   inflight_rows_.fetch_sub(s->rows, std::memory_order_relaxed);
-  std::vector<Item> items;
-  items.swap(s->items);
+  std::vector<Item>& items = s->items;  // cleared below; the slot keeps the capacity
   const size_t n_items = items.size();
   if (st != hipSuccess) {
     auto e = device_error(ApiError::EXECUTION_FAILURE, std::string("GPU execution failed: ") + hipGetErrorString(st));
@@ -567,6 +566,7 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
       if (wake) ho_cv_.notify_one();
     }
   }
+  items.clear();
   std::lock_guard<std::mutex> g(stats_mu_);
   stats_.batches++;
   stats_.rows += uint64_t(s->rows);
