@@ -18,6 +18,14 @@ The supervisor never touches a GPU itself; it restarts a worker that dies
 (bounded restart rate) and, on SIGTERM/SIGINT, forwards SIGTERM so every
 worker drains: readiness off, wait for in-flight requests, stop.
 
+SIGHUP is a rolling update (the Deployment's RollingUpdate strategy,
+``seldondeployment_controller.go:565``, exercised upstream by
+``testing/scripts/test_rolling_updates.py``): worker by worker, a new worker
+is started from the current ``--spec`` file next to the old one (same GPU,
+same ports through ``SO_REUSEPORT``), and only once it reports ready is the
+old one drained -- one extra worker at a time, never fewer than N serving.
+A new worker that fails to come up stops the rollout and the old one stays.
+
 Configuration precedence: defaults < ``/etc/podinfo/annotations`` < spec
 annotations < environment (``ENGINE_SERVER_PORT``, ``SELDON_LOG_*``, ...) < flags.
 """
@@ -102,6 +110,10 @@ def run_worker(args: argparse.Namespace) -> int:
     h = dep.serve(http_port=cfg.http_port, grpc_port=cfg.grpc_port, admin_port=cfg.admin_port,
                   threads=cfg.threads, grpc_threads=cfg.grpc_threads, host=cfg.host)
     rank = os.environ.get("SCA_WORKER_RANK", "0")
+    ready_file = os.environ.get("SCA_READY_FILE")
+    if ready_file:  # the supervisor's rolling update waits for this before draining the old worker
+        with open(ready_file, "w") as f:
+            f.write(str(os.getpid()))
     logger.info("worker %s serving %s: REST :%s gRPC :%s admin :%s (device %s, units %s)", rank,
                 dep.predictor.get("name"), h.http_port, h.grpc_port, cfg.admin_port, dep.device,
                 {n: dep.engine.unit_kind(n) for n in dep.engine.node_names()})
@@ -137,23 +149,79 @@ def run_worker(args: argparse.Namespace) -> int:
 class Supervisor:
     """Keeps one worker process per GPU alive."""
 
-    def __init__(self, n: int, worker_argv: List[str], max_restarts: int = 5):
+    def __init__(self, n: int, worker_argv: List[str], max_restarts: int = 5, ready_timeout: float = 120.0,
+                 drain_timeout: float = 60.0):
         self.n = n
         self.argv = worker_argv
         self.max_restarts = max_restarts
+        self.ready_timeout = ready_timeout
+        self.drain_timeout = drain_timeout
         self.procs: Dict[int, subprocess.Popen] = {}
         self.restarts: Dict[int, List[float]] = {i: [] for i in range(n)}
         self.stopping = False
+        self.roll_requested = False
+        self.generation = 0
+        self.rollouts: List[Dict] = []
 
-    def spawn(self, rank: int) -> None:
+    def _start(self, rank: int, ready_file: Optional[str] = None) -> subprocess.Popen:
         env = dict(os.environ)
         env["HIP_VISIBLE_DEVICES"] = str(rank)
         env["SCA_WORKER_RANK"] = str(rank)
         env["SCA_WORKERS"] = str(self.n)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        self.procs[rank] = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--worker", *self.argv],
-                                            env=env)
-        logger.info("started worker %d (pid %d) on GPU %d", rank, self.procs[rank].pid, rank)
+        if ready_file:
+            env["SCA_READY_FILE"] = ready_file
+        else:
+            env.pop("SCA_READY_FILE", None)
+        p = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--worker", *self.argv], env=env)
+        logger.info("started worker %d (pid %d) on GPU %d", rank, p.pid, rank)
+        return p
+
+    def spawn(self, rank: int) -> None:
+        self.procs[rank] = self._start(rank)
+
+    def rolling_update(self) -> bool:
+        """Replace every worker, one at a time, surge 1: start the new one,
+        wait for its ready marker, then drain the old one.  Returns False (and
+        keeps the old worker) if a new worker does not come up."""
+        import tempfile
+
+        self.generation += 1
+        record = {"generation": self.generation, "replaced": [], "ok": True}
+        with tempfile.TemporaryDirectory(prefix="sca-rollout-") as tmp:
+            for rank in range(self.n):
+                if self.stopping:
+                    record["ok"] = False
+                    break
+                ready = os.path.join(tmp, f"worker-{rank}.ready")
+                new = self._start(rank, ready)
+                deadline = time.monotonic() + self.ready_timeout
+                while not os.path.exists(ready) and new.poll() is None and time.monotonic() < deadline:
+                    time.sleep(0.05)
+                if not os.path.exists(ready):
+                    logger.error("rollout %d: new worker %d did not become ready; keeping the old one",
+                                 self.generation, rank)
+                    if new.poll() is None:
+                        new.send_signal(signal.SIGTERM)
+                        try:
+                            new.wait(timeout=self.drain_timeout)
+                        except subprocess.TimeoutExpired:
+                            new.kill()
+                    record["ok"] = False
+                    break
+                old = self.procs[rank]
+                self.procs[rank] = new  # from here on the new one is the supervised worker
+                if old.poll() is None:
+                    old.send_signal(signal.SIGTERM)  # drain: readiness off, in-flight requests finish
+                    try:
+                        old.wait(timeout=self.drain_timeout)
+                    except subprocess.TimeoutExpired:
+                        old.kill()
+                        old.wait()
+                record["replaced"].append({"rank": rank, "old_pid": old.pid, "new_pid": new.pid})
+                logger.info("rollout %d: worker %d replaced (pid %d -> %d)", self.generation, rank, old.pid, new.pid)
+        self.rollouts.append(record)
+        return record["ok"]
 
     def status(self) -> Dict:
         return {"workers": {r: {"pid": p.pid, "alive": p.poll() is None, "restarts": len(self.restarts[r])}
@@ -170,9 +238,13 @@ class Supervisor:
             self.spawn(r)
         signal.signal(signal.SIGTERM, lambda *_: self.terminate())
         signal.signal(signal.SIGINT, lambda *_: self.terminate())
+        signal.signal(signal.SIGHUP, lambda *_: setattr(self, "roll_requested", True))
         rc = 0
         while True:
             time.sleep(0.2)
+            if self.roll_requested and not self.stopping:
+                self.roll_requested = False
+                self.rolling_update()
             alive = 0
             for r, p in list(self.procs.items()):
                 code = p.poll()

@@ -191,3 +191,74 @@ def test_native_tracing_spans(tmp_path):
     assert names == {"ab:route", f"{branch}:predict"}
     assert all(s["traceId"] == root[0]["traceId"] for s in kids)
     assert all(s["localEndpoint"]["serviceName"] == "seldon-svc-orch" for s in spans)
+
+
+def test_rolling_update_swaps_model_version_without_failed_requests(tmp_path):
+    """SIGHUP to the supervisor = rolling update (the reference's
+    testing/scripts/test_rolling_updates.py with fixed-model images v1/v2):
+    while clients keep sending, every worker is replaced by one built from the
+    new spec, no request fails (beyond the reference's connect retries), every
+    answer is v1 or v2, and the deployment ends on v2."""
+    (tmp_path / "fixed_model.py").write_text(
+        "class FixedModel:\n"
+        "    def __init__(self, version='1'):\n"
+        "        self.v = float(version)\n"
+        "    def predict(self, X, names=None, meta=None):\n"
+        "        return [[self.v] * 4 for _ in range(len(X))]\n")
+
+    def write_spec(version):
+        spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+                "graph": {"name": "m", "type": "MODEL",
+                          "parameters": [{"name": "version", "value": str(version), "type": "STRING"}]}}
+        (tmp_path / "spec.json").write_text(json.dumps(spec))
+
+    write_spec(1)
+    hp, gp = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=f"{ROOT}:{tmp_path}")
+    p = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--spec", str(tmp_path / "spec.json"),
+                          "--gpus", "2", "--device", "-1", "--component", "m=fixed_model.FixedModel",
+                          "--http-port", str(hp), "--grpc-port", str(gp), "--admin-port", "0", "--threads", "1",
+                          "--log-level", "WARNING"], env=env, cwd=ROOT, start_new_session=True)
+    seen, failed = [], []
+    stop = threading.Event()
+
+    def client():
+        while not stop.is_set():
+            for attempt in range(4):  # connect retries, as the reference's e2e helpers do
+                try:
+                    req = urllib.request.Request(f"http://127.0.0.1:{hp}/api/v0.1/predictions",
+                                                 data=b'{"data":{"ndarray":[[1.0, 2.0]]}}',
+                                                 headers={"Content-Type": "application/json", "Connection": "close"})
+                    out = json.loads(urllib.request.urlopen(req, timeout=10).read())
+                    seen.append(out["data"]["ndarray"][0][0])
+                    break
+                except Exception as e:  # noqa: BLE001
+                    if attempt == 3:
+                        failed.append(repr(e))
+                    time.sleep(0.05)
+
+    try:
+        assert _wait_ready(hp), "engine did not become ready"
+        th = [threading.Thread(target=client) for _ in range(3)]
+        for t in th:
+            t.start()
+        time.sleep(1.0)
+        assert seen and set(seen) == {1.0}
+        write_spec(2)
+        p.send_signal(signal.SIGHUP)
+        deadline = time.monotonic() + 120
+        while time.monotonic() < deadline and not (len(seen) > 30 and set(seen[-30:]) == {2.0}):
+            time.sleep(0.2)
+        stop.set()
+        for t in th:
+            t.join(timeout=30)
+        assert not failed, failed[:5]
+        assert set(seen) <= {1.0, 2.0}
+        assert set(seen[-30:]) == {2.0}, seen[-40:]
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 0
+    finally:
+        stop.set()
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
