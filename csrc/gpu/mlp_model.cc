@@ -465,6 +465,13 @@ void MlpModel::launch_layerwise_bf16(const double* X, int rows, double* out, cha
     a.A = cur;
     a.lda = cur_ld;
     const bool last = o + 1 == prog_.n_pre;
+    if (last && !vae_ && op.N <= 16 &&
+        (prog_.out_softmax == 2 ? op.N == 1 && prog_.out_dim == 2 : prog_.out_dim == op.N)) {
+      a.out64 = out;  // the epilogue writes the model output (mlp_finish fused)
+      a.out_mode = prog_.out_softmax;
+      kern::dense_gemm(a, s);
+      return;
+    }
     if (last) {  // plain MLP logits / VAE head [mu | log_var] in fp32
       a.O = head;
       a.o_f32 = 1;

@@ -309,6 +309,41 @@ __global__ __launch_bounds__(NT) void gemm_bf16_lds_kernel(const DenseGemmArgs a
     __syncthreads();
   }
   // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
+  if (a.out64) {  // N <= 16: wave wc = 0, tile tn = 0 holds a row's every column (16 lanes of one kq)
+    if (wc != 0 || n0 != 0) return;
+    const bool live = r16 < a.N;
+    const float bias = live ? a.bias[r16] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * (BM / 2) + tm * 16 + kq * 4 + i;
+        const float v = act_f(acc[tm][0][i] + bias, a.act);
+        if (a.out_mode == 1) {  // softmax over the row's N lanes
+          float m = live ? v : -3.4e38f;
+          m = fmaxf(m, __shfl_xor(m, 1, 64));
+          m = fmaxf(m, __shfl_xor(m, 2, 64));
+          m = fmaxf(m, __shfl_xor(m, 4, 64));
+          m = fmaxf(m, __shfl_xor(m, 8, 64));
+          const float e = live ? expf(v - m) : 0.f;
+          float sum = e;
+          sum += __shfl_xor(sum, 1, 64);
+          sum += __shfl_xor(sum, 2, 64);
+          sum += __shfl_xor(sum, 4, 64);
+          sum += __shfl_xor(sum, 8, 64);
+          if (live && row < a.rows_eff) a.out64[size_t(row) * a.N + r16] = double(e / sum);
+        } else if (a.out_mode == 2) {
+          if (r16 == 0 && row < a.rows_eff) {
+            a.out64[size_t(row) * 2] = 1.0 - double(v);
+            a.out64[size_t(row) * 2 + 1] = double(v);
+          }
+        } else if (live && row < a.rows_eff) {
+          a.out64[size_t(row) * a.N + r16] = double(v);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int col = n0 + wc * 32 + tn * 16 + r16;

@@ -185,7 +185,12 @@ struct DenseGemmArgs {
   const void* A = nullptr;
   int lda = 0;
   int a_f64 = 0;
-  int xcd_remap = 1;  // bf16 path: XCD-aware tile order (set by dense_gemm)  // bf16 path: A is the fp64 request batch [rows][lda], K = lda (converted while staging)
+  int xcd_remap = 1;  // bf16 path: XCD-aware tile order (set by dense_gemm)
+  // bf16 path, N <= 16: write the model output (fp64) straight from the
+  // epilogue -- mode 0 plain [rows][N], 1 row softmax, 2 binary [1 - p, p] --
+  // instead of fp32 logits + mlp_finish (one launch and a round trip less)
+  double* out64 = nullptr;
+  int out_mode = 0;  // bf16 path: A is the fp64 request batch [rows][lda], K = lda (converted while staging)
   const float* H = nullptr;
   int ldh = 0, latent = 0;
   uint64_t key = 0;

@@ -247,3 +247,27 @@ def test_vae_large_batch_paths_match_cpu(precision, rtol, monkeypatch):
     finally:
         unit.stop()
     np.testing.assert_allclose(got, cpu_m.run_cpu(X)[:, 0], rtol=rtol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [1, 700, 4096])
+def test_mlp_bf16_binary_output_fused_epilogue(rows):
+    """Binary classifier head (1 sigmoid unit -> [1 - p, p]) written by the bf16
+    GEMM epilogue: stated tolerance 2e-2 absolute vs torch float32."""
+    import torch
+
+    from seldon_core_amd.models.mlp import OUT_BINARY
+
+    layers = random_dense_stack([20, 48, 1], ["relu", "sigmoid"], seed=9)
+    X = np.random.default_rng(rows).normal(size=(rows, 20))
+    unit = sca.native().BatchedUnit(mlp_row_model(layers, OUT_BINARY, precision="bf16"), 0, max_batch=8192)
+    try:
+        got = unit.run(X)
+    finally:
+        unit.stop()
+    x = torch.tensor(X, dtype=torch.float32)
+    h = torch.relu(x @ torch.tensor(layers[0]["W"]).T + torch.tensor(layers[0]["b"]))
+    p = torch.sigmoid(h @ torch.tensor(layers[1]["W"]).T + torch.tensor(layers[1]["b"])).double().numpy()[:, 0]
+    assert got.shape == (rows, 2)
+    np.testing.assert_allclose(got[:, 1], p, atol=2e-2)
+    np.testing.assert_allclose(got[:, 0] + got[:, 1], 1.0, atol=1e-12)
