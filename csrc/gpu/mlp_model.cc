@@ -13,6 +13,7 @@ namespace {
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 constexpr size_t kSlack = 4 * 16 + 64;  // workspace floats past each buffer (A look-ahead)
 constexpr int kGemmRows = 512;          // rows_eff from which fp32 layers use the register-tiled GEMM
+constexpr int kLdsGemmRows = 2048;      // ... and from which the LDS-tiled one (row-major weights)
 
 uint16_t to_bf16(float f) {  // round to nearest even
   uint32_t u;
@@ -143,7 +144,16 @@ int MlpModel::add_layer(const DenseLayer& L, int type, int in_buf, int out_buf) 
   op.Kpb = round_up(L.K, 64);
   op.Npb = round_up(L.N, 64);
   op.wb_off = (long long)pbf_.size();
-  if (precision_ == 1) {  // bf16 row-major [Npb][Kpb], zero padded (gemm_bf16_lds_kernel)
+  if (precision_ == 0) {  // fp32 row-major [Npb][Kq], zero padded (gemm_lds_kernel<float>)
+    const int Kq = round_up(L.K, 32);
+    wr_off_[size_t(n)] = (long long)prm_.size();
+    kq_[size_t(n)] = Kq;
+    prm_.resize(prm_.size() + size_t(op.Npb) * Kq, 0.f);
+    float* wr = prm_.data() + wr_off_[size_t(n)];
+    for (int nn = 0; nn < L.N; ++nn)
+      for (int k = 0; k < L.K; ++k) wr[size_t(nn) * Kq + k] = L.W[size_t(nn) * L.K + k];
+  }
+  if (precision_ == 1) {  // bf16 row-major [Npb][Kpb], zero padded (gemm_lds_kernel<__bf16>)
     pbf_.resize(pbf_.size() + size_t(op.Npb) * op.Kpb, 0);
     uint16_t* wb = pbf_.data() + op.wb_off;
     for (int nn = 0; nn < L.N; ++nn)
@@ -164,6 +174,9 @@ void MlpModel::build() {
   prog_ = kern::MlpProgram();
   params_.clear();
   pbf_.clear();
+  prm_.clear();
+  wr_off_.assign(kern::kMlpMaxOps, -1);
+  kq_.assign(kern::kMlpMaxOps, 0);
   auto& p = prog_;
   p.F = F_;
   p.Fp = round_up(F_, 16);
@@ -249,6 +262,10 @@ void MlpModel::to_device(int device) {
     d_pbf_.alloc(pbf_.size() * sizeof(uint16_t) + 64 * 16, device);  // + look-ahead pad
     d_pbf_.upload(pbf_.data(), pbf_.size() * sizeof(uint16_t));
   }
+  if (!prm_.empty()) {
+    d_prm_.alloc(prm_.size() * sizeof(float), device);
+    d_prm_.upload(prm_.data(), prm_.size() * sizeof(float));
+  }
 }
 
 // ------------------------------------------------------------ dispatch
@@ -299,7 +316,7 @@ size_t MlpModel::workspace_bytes(int max_rows, int) const {
     if (!any) return 0;
   }
   const size_t R = size_t(round_up(std::max(max_rows, 1), 16)), S = vae_ ? size_t(samples_) : 1;
-  const size_t W = size_t(max_np()), K0 = size_t(prog_.ops[0].Kp);
+  const size_t W = size_t(max_np()), K0 = size_t(round_up(prog_.ops[0].Kp, 32));
   // [X fp32 R x K0][buf0 R*S x W][buf1 R*S x W]([head R x W][mse R]), kSlack
   // floats after each: the layer kernel's A look-ahead reads up to 4 K-blocks
   // past the end of a row
@@ -324,7 +341,7 @@ void MlpModel::launch(const double* X, int rows, int, double* out, void* ws, hip
 void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* ws, uint64_t key, hipStream_t s) {
   const float* P = d_params_.as<float>();
   const size_t R = size_t(round_up(rows, 16)), S = vae_ ? size_t(samples_) : 1, W = size_t(max_np());
-  const size_t K0 = size_t(prog_.ops[0].Kp);
+  const size_t K0 = size_t(round_up(prog_.ops[0].Kp, 32));  // rows hold Kq readable floats (LDS-tiled GEMM)
   float* x32 = ws;
   float* buf[2] = {x32 + R * K0 + kSlack, x32 + R * K0 + kSlack + R * S * W + kSlack};
   float* head = buf[1] + R * S * W + kSlack;
@@ -354,7 +371,7 @@ void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* w
     const bool head_out = vae_ && o + 1 == prog_.n_pre;
     a.O = head_out ? head : buf[flip];
     a.ldo = op.Np;
-    run_layer(a, s);
+    run_layer(a, o, s);
     cur = a.O;
     cur_ld = op.Np;
     flip ^= 1;
@@ -393,25 +410,35 @@ void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* w
       dld = op.Np;
       flip ^= 1;
     }
-    run_layer(a, s);
+    run_layer(a, o, s);
   }
   kern::mlp_mse_finish(mse, rows, 1.0 / (double(F_) * samples_), out, s);
 }
 
 // Large batches: the register-tiled GEMM (64 rows x up to 64 columns per
 // wave); small ones: one 16x16 tile per wave (more waves for the chip).
-void MlpModel::run_layer(const kern::MlpLayerArgs& a, hipStream_t s) const {
+void MlpModel::run_layer(const kern::MlpLayerArgs& a, int op, hipStream_t s) const {
   if (a.rows_eff < kGemmRows) {
     kern::mlp_layer(a, s);
     return;
   }
   kern::DenseGemmArgs g;
-  g.W = a.W;
+  const long long wr = wr_off_[size_t(op)];
+  if (a.rows_eff >= kLdsGemmRows && !a.H && wr >= 0 && kq_[size_t(op)] <= a.lda && a.lda % 4 == 0) {
+    // A rows hold Kq floats (zeros past K), W row-major [Npb][Kq]: LDS-tiled exact-fp32 MFMA GEMM
+    g.lds_f32 = 1;
+    g.W = d_prm_.as<float>() + wr;
+    g.Kp = kq_[size_t(op)];
+    g.Np = prog_.ops[op].Npb;
+    g.n_store = a.Np;  // the activation buffers are Np (16-padded) wide
+  } else {
+    g.W = a.W;
+    g.Kp = a.Kp;
+    g.Np = a.Np;
+  }
   g.bias = a.bias;
   g.K = a.K;
-  g.Kp = a.Kp;
   g.N = a.N;
-  g.Np = a.Np;
   g.act = a.act;
   g.A = a.A;
   g.lda = a.lda;

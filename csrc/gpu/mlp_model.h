@@ -59,7 +59,7 @@ class MlpModel : public RowModel {
   void cpu_dense(const DenseLayer& L, const std::vector<float>& in, std::vector<float>& out, int rows) const;
   void launch_layerwise(const double* X, int rows, double* out, float* ws, uint64_t key, hipStream_t s);
   void launch_layerwise_bf16(const double* X, int rows, double* out, char* ws, uint64_t key, hipStream_t s);
-  void run_layer(const kern::MlpLayerArgs& a, hipStream_t s) const;
+  void run_layer(const kern::MlpLayerArgs& a, int op, hipStream_t s) const;
   int max_np() const;
 
   std::vector<DenseLayer> enc_, dec_;  // plain: enc_ = all layers
@@ -73,6 +73,12 @@ class MlpModel : public RowModel {
   int precision_ = 0;
   std::vector<uint16_t> pbf_;        // bf16 weights (precision_ == 1)
   DeviceBuffer d_pbf_;
+  // fp32 weights row-major [Npb][Kq] (Kq = K rounded to 32) for the LDS-tiled
+  // exact-fp32 GEMM of large batches; per op index, -1 = none
+  std::vector<float> prm_;
+  std::vector<long long> wr_off_;
+  std::vector<int> kq_;
+  DeviceBuffer d_prm_;
   kern::MlpProgram prog_;
   std::vector<float> params_;
   DeviceBuffer d_params_;

@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64) void dense_gemm_kernel(const DenseGemmArgs a) {
 //
 // AMODE 0: A is bf16 [rows][lda]; 2: VAE reparameterised z from H.
 // W is row-major [Npb][Kpb] bf16 (Kpb, Npb multiples of 64, zero padded).
-constexpr int kBK = 64, kLdr = kBK + 8;  // row stride in bf16 elements
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;  // one 16-B staging chunk
 
 template <int AMODE>
 __device__ __forceinline__ bf16x8 stage_a(const DenseGemmArgs& a, int row, int k) {
@@ -213,14 +213,33 @@ __device__ __forceinline__ bf16x8 stage_a(const DenseGemmArgs& a, int row, int k
   }
 }
 
+// One 16-B chunk of the A panel (row `row`, elements [k, k + 16 / sizeof(T))).
+template <typename T, int AMODE>
+__device__ __forceinline__ u32x4 stage_a_chunk(const DenseGemmArgs& a, int row, int k) {
+  if constexpr (AMODE == 0) {
+    row = min(row, a.rows_eff - 1);
+    return *reinterpret_cast<const u32x4*>(static_cast<const T*>(a.A) + size_t(row) * a.lda + k);
+  } else {
+    static_assert(sizeof(T) == 2, "reparameterised A is staged as bf16");
+    return __builtin_bit_cast(u32x4, stage_a<AMODE>(a, row, k));
+  }
+}
+
 // bijective XCD-aware tile index for workgroup `L` of `nwg` (cdna guide §5)
 __device__ __forceinline__ int xcd_tile(int L, int nwg) {
   const int xcd = L & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
 }
 
-template <int AMODE, int BM, int BN, int NT>
-__global__ __launch_bounds__(NT) void gemm_bf16_lds_kernel(const DenseGemmArgs a) {
+// T = __bf16: v_mfma_f32_16x16x32_bf16, 64-deep K stages; T = float: exact
+// fp32 products on v_mfma_f32_16x16x4_f32 (four per 16-B fragment), 32-deep
+// stages.  The LDS image is the same in bytes either way: 128-B rows padded to
+// 144 B, one 16-B chunk per (row, k-chunk).
+template <typename T, int AMODE, int BM, int BN, int NT>
+__global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
+  constexpr int kEl = 16 / int(sizeof(T));    // elements per 16-B chunk
+  constexpr int kBKe = 8 * kEl;               // K elements per stage (128 B per row)
+  constexpr int kLdr = kBKe + kEl;            // LDS row stride in elements (144 B)
   constexpr int WN = NT / 128;                // waves along N (2 along M); each wave owns BM/2 x 32
   constexpr int TM = BM / 32;                 // 16-row tiles per wave
   constexpr int TN = 2;                       // 16-col tiles per wave
@@ -229,42 +248,42 @@ __global__ __launch_bounds__(NT) void gemm_bf16_lds_kernel(const DenseGemmArgs a
   constexpr int CW = BN * 8 / NT;             // W staging chunks per thread
   constexpr int kBuf = (BM + BN) * kLdr;      // one LDS buffer: A panel then W panel
   static_assert(CA >= 1 && CW >= 1, "tile too small for the stagers");
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * kBuf];
+  __shared__ __attribute__((aligned(16))) T smem[2 * kBuf];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave / WN, wc = wave % WN, r16 = lane & 15, kq = lane >> 4;
   const int nN = (a.Np + BN - 1) / BN;
   const int t = a.xcd_remap ? xcd_tile(blockIdx.x, gridDim.x) : int(blockIdx.x);
   const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
-  const __bf16* W = static_cast<const __bf16*>(a.W);
-  const int KS = a.Kp / kBK;
+  const T* W = static_cast<const T*>(a.W);
+  const int KS = a.Kp / kBKe;
   // two stages of staging registers; every index below is a compile-time
   // constant (the K loop is unrolled by two), so they stay in VGPRs
-  bf16x8 ra0[CA], rw0[CW], ra1[CA], rw1[CW];
-  auto gload = [&](int ks, bf16x8* ra, bf16x8* rw) {
+  u32x4 ra0[CA], rw0[CW], ra1[CA], rw1[CW];
+  auto gload = [&](int ks, u32x4* ra, u32x4* rw) {
 #pragma unroll
     for (int j = 0; j < CA; ++j) {
       const int c = tid + NT * j;
-      ra[j] = stage_a<AMODE>(a, m0 + (c >> 3), ks * kBK + (c & 7) * 8);
+      ra[j] = stage_a_chunk<T, AMODE>(a, m0 + (c >> 3), ks * kBKe + (c & 7) * kEl);
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
       const int c = tid + NT * j;
-      rw[j] = *reinterpret_cast<const bf16x8*>(W + size_t(min(n0 + (c >> 3), a.Np - 1)) * a.Kp + ks * kBK +
-                                               (c & 7) * 8);
+      rw[j] = *reinterpret_cast<const u32x4*>(W + size_t(min(n0 + (c >> 3), a.Np - 1)) * a.Kp + ks * kBKe +
+                                              (c & 7) * kEl);
     }
   };
-  auto lstore = [&](int buf, const bf16x8* ra, const bf16x8* rw) {
-    __bf16* As = smem + buf * kBuf;
-    __bf16* Ws = As + BM * kLdr;
+  auto lstore = [&](int buf, const u32x4* ra, const u32x4* rw) {
+    T* As = smem + buf * kBuf;
+    T* Ws = As + BM * kLdr;
 #pragma unroll
     for (int j = 0; j < CA; ++j) {
       const int c = tid + NT * j;
-      *reinterpret_cast<bf16x8*>(As + (c >> 3) * kLdr + (c & 7) * 8) = ra[j];
+      *reinterpret_cast<u32x4*>(As + (c >> 3) * kLdr + (c & 7) * kEl) = ra[j];
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
       const int c = tid + NT * j;
-      *reinterpret_cast<bf16x8*>(Ws + (c >> 3) * kLdr + (c & 7) * 8) = rw[j];
+      *reinterpret_cast<u32x4*>(Ws + (c >> 3) * kLdr + (c & 7) * kEl) = rw[j];
     }
   };
   f32x4 acc[TM][TN];
@@ -273,22 +292,30 @@ __global__ __launch_bounds__(NT) void gemm_bf16_lds_kernel(const DenseGemmArgs a
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int buf) {
-    const __bf16* As = smem + buf * kBuf;
-    const __bf16* Ws = As + BM * kLdr;
+    const T* As = smem + buf * kBuf;
+    const T* Ws = As + BM * kLdr;
 #pragma unroll
-    for (int kk = 0; kk < kBK / 32; ++kk) {
-      bf16x8 af[TM], bf[TN];
+    for (int kk = 0; kk < 2; ++kk) {  // two 16-B fragments per row per stage (bytes kk * 64 + kq * 16)
+      u32x4 af[TM], bf[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (wr * (BM / 2) + i * 16 + r16) * kLdr + kk * 32 + kq * 8);
+        af[i] = *reinterpret_cast<const u32x4*>(As + (wr * (BM / 2) + i * 16 + r16) * kLdr + kk * 4 * kEl + kq * kEl);
 #pragma unroll
       for (int i = 0; i < TN; ++i)
-        bf[i] = *reinterpret_cast<const bf16x8*>(Ws + (wc * 32 + i * 16 + r16) * kLdr + kk * 32 + kq * 8);
+        bf[i] = *reinterpret_cast<const u32x4*>(Ws + (wc * 32 + i * 16 + r16) * kLdr + kk * 4 * kEl + kq * kEl);
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
+        for (int tn = 0; tn < TN; ++tn) {
+          if constexpr (sizeof(T) == 2) {
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[tm]),
+                                                                  __builtin_bit_cast(bf16x8, bf[tn]), acc[tm][tn], 0, 0, 0);
+          } else {  // lane (r16, kq) holds k = kk * 16 + 4 kq + j of MFMA j: every k once per stage
+            const f32x4 x = __builtin_bit_cast(f32x4, af[tm]), y = __builtin_bit_cast(f32x4, bf[tn]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], y[j], acc[tm][tn], 0, 0, 0);
+          }
+        }
     }
   };
   gload(0, ra0, rw0);
@@ -344,10 +371,11 @@ __global__ __launch_bounds__(NT) void gemm_bf16_lds_kernel(const DenseGemmArgs a
     }
     return;
   }
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int col = n0 + wc * 32 + tn * 16 + r16;
-    if (col >= a.Np) continue;
+    if (col >= n_store) continue;
     const bool live = col < a.N;
     const float bias = live ? a.bias[col] : 0.f;
 #pragma unroll
@@ -377,8 +405,8 @@ __global__ __launch_bounds__(NT) void gemm_bf16_lds_kernel(const DenseGemmArgs a
   }
 }
 
-template <int AMODE>
-void launch_bf16(const DenseGemmArgs& a, hipStream_t s) {
+template <typename T, int AMODE>
+void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
   // 128 x 64 tiles (two resident workgroups per CU) when they fill the chip,
   // 32 x 64 otherwise (narrow layers such as a 10-class head: 4x the
   // workgroups, so the A stream is spread over every CU).  The VAE decoder's
@@ -389,13 +417,17 @@ void launch_bf16(const DenseGemmArgs& a, hipStream_t s) {
   const int nN = (a.Np + 63) / 64;
   const int big = nN * ((a.rows_eff + 127) / 128);
   const int wide = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
-  if (AMODE == 2 && wide >= 256) {
-    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 128, 128, 512>), dim3(wide), dim3(512), 0, s, a);
-  } else if (big >= 256) {
-    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 128, 64, 256>), dim3(big), dim3(256), 0, s, a);
+  if constexpr (AMODE == 2) {
+    if (wide >= 256) {
+      hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 128, 512>), dim3(wide), dim3(512), 0, s, a);
+      return;
+    }
+  }
+  if (big >= 256) {
+    hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 64, 256>), dim3(big), dim3(256), 0, s, a);
   } else {
     const int small = nN * ((a.rows_eff + 31) / 32);
-    hipLaunchKernelGGL((gemm_bf16_lds_kernel<AMODE, 32, 64, 256>), dim3(small), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 32, 64, 256>), dim3(small), dim3(256), 0, s, a);
   }
 }
 
@@ -448,8 +480,12 @@ void dense_gemm(const DenseGemmArgs& a, hipStream_t s) {
     b.xcd_remap = remap;
     // (the 128 x 128 variant needs 230 VGPRs -> one workgroup per CU, and
     // measured 2.5x slower on the VAE decoder)
-    if (b.H) launch_bf16<2>(b, s);
-    else launch_bf16<0>(b, s);
+    if (b.H) launch_lds<__bf16, 2>(b, s);
+    else launch_lds<__bf16, 0>(b, s);
+  } else if (a.lds_f32 && !a.H) {  // large fp32 layer: LDS-tiled exact-fp32 MFMA GEMM
+    DenseGemmArgs b = a;
+    b.xcd_remap = 1;
+    launch_lds<float, 0>(b, s);
   } else {
     if (a.H) launch_tn<0, 2>(a, s);
     else launch_tn<0, 0>(a, s);

@@ -190,7 +190,11 @@ struct DenseGemmArgs {
   // epilogue -- mode 0 plain [rows][N], 1 row softmax, 2 binary [1 - p, p] --
   // instead of fp32 logits + mlp_finish (one launch and a round trip less)
   double* out64 = nullptr;
-  int out_mode = 0;  // bf16 path: A is the fp64 request batch [rows][lda], K = lda (converted while staging)
+  int out_mode = 0;
+  // fp32: W is row-major [Np][Kp] (Kp % 32 == 0, Np % 64 == 0, zero padded) and A rows hold Kp
+  // readable floats -- the LDS-tiled exact-fp32 MFMA kernel instead of the fragment-packed one
+  int lds_f32 = 0;
+  int n_store = 0;  // LDS-tiled paths: output columns to store (0 = Np); the rest of the padded tile is dropped  // bf16 path: A is the fp64 request batch [rows][lda], K = lda (converted while staging)
   const float* H = nullptr;
   int ldh = 0, latent = 0;
   uint64_t key = 0;
