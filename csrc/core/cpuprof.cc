@@ -24,7 +24,6 @@ size_t g_cap = 0;
 std::atomic<size_t> g_n{0};
 std::atomic<bool> g_on{false};
 int g_depth = 1;                 // frames per sample: 1 = the interrupted PC only
-struct sigaction g_old {};
 std::vector<timer_t> g_timers;   // one CPU-time timer per thread alive at start()
 
 // Per-thread CPU-time clock of thread `tid` (linux/posix-timers.h:
@@ -62,15 +61,24 @@ bool start(int hz, size_t max_samples, int depth) {
     void* fr[4];
     (void)backtrace(fr, 4);
   }
-  delete[] g_pcs;
-  g_pcs = new uintptr_t[max_samples * size_t(g_depth)];
+  // Reuse the sample buffer (grow only): a handler of the previous session
+  // still finishing its store must not write into freed memory.
+  static size_t words = 0;
+  if (max_samples * size_t(g_depth) > words) {
+    delete[] g_pcs;
+    words = max_samples * size_t(g_depth);
+    g_pcs = new uintptr_t[words];
+  }
   g_cap = max_samples;
   g_n.store(0);
   struct sigaction sa {};
   sa.sa_sigaction = on_sigprof;
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
   sigemptyset(&sa.sa_mask);
-  if (sigaction(SIGPROF, &sa, &g_old) != 0) return false;
+  // The handler stays installed after stop() (a no-op while g_on is false):
+  // restoring SIGPROF's default action could let a sample signal still pending
+  // at stop() terminate the process.
+  if (sigaction(SIGPROF, &sa, nullptr) != 0) return false;
   g_on.store(true);
   // A process-wide ITIMER_PROF coalesces expirations while its signal is
   // pending, so with many busy threads most samples are lost: arm one
@@ -98,7 +106,6 @@ bool start(int hz, size_t max_samples, int depth) {
   }
   if (g_timers.empty()) {
     g_on.store(false);
-    sigaction(SIGPROF, &g_old, nullptr);
     return false;
   }
   return true;
@@ -111,7 +118,6 @@ Profile stop() {
   for (timer_t t : g_timers) timer_delete(t);
   g_timers.clear();
   g_on.store(false);
-  sigaction(SIGPROF, &g_old, nullptr);
   const size_t n = std::min(g_n.load(), g_cap);
   out.depth = g_depth;
   std::map<uintptr_t, Loc> locs;
