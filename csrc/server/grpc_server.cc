@@ -99,6 +99,18 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
   std::vector<GCompletion> q;
   std::vector<std::function<void()>> tasks;  // continuations posted by GPU units
   bool running_tasks = false;                // worker thread only
+  // Wake-ups: an enqueue writes the eventfd only while the worker is (about to
+  // be) blocked in epoll_wait; an awake worker picks the work up at the top of
+  // its loop.  polling / has_work pair up seq_cst (no lost wake-up), which
+  // saves an eventfd write + epoll wake + read per hand-off under load.
+  std::atomic<bool> polling{false};
+  std::atomic<bool> has_work{false};
+  bool need_wake() {  // caller holds qmu, has just queued work
+    has_work.store(true, std::memory_order_seq_cst);
+    if (wake_pending || !polling.load(std::memory_order_seq_cst)) return false;
+    wake_pending = true;
+    return true;
+  }
   bool wake_pending = false;                 // eventfd written and not yet drained (guarded by qmu)
   nghttp2_session_callbacks* cbs = nullptr;
 
@@ -108,14 +120,13 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
       fn();
       return;
     }
-    bool was_empty;
+    bool wake;
     {
       std::lock_guard<std::mutex> g(qmu);
-      was_empty = !wake_pending;
-      wake_pending = true;
       tasks.push_back(std::move(fn));
+      wake = need_wake();
     }
-    if (was_empty) {
+    if (wake) {
       uint64_t one = 1;
       ssize_t w = ::write(evfd, &one, 8);
       (void)w;
@@ -227,14 +238,13 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
       complete(std::move(d), false);
       return;
     }
-    bool was_empty;
+    bool wake;
     {
       std::lock_guard<std::mutex> g(qmu);
-      was_empty = !wake_pending;
-      wake_pending = true;
       q.push_back(std::move(d));
+      wake = need_wake();
     }
-    if (was_empty) {  // one wakeup per drained batch of completions
+    if (wake) {  // one wakeup per drained batch of completions
       uint64_t one = 1;
       ssize_t w = ::write(evfd, &one, 8);
       (void)w;
@@ -251,15 +261,18 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
     if (flush_now) flush(c);
   }
 
-  void drain_queue() {
-    uint64_t v;
-    ssize_t r = ::read(evfd, &v, 8);
-    (void)r;
+  void drain_queue(bool evfd_ready) {
+    if (evfd_ready) {
+      uint64_t v;
+      ssize_t r = ::read(evfd, &v, 8);
+      (void)r;
+    }
     std::vector<GCompletion> items;
     std::vector<std::function<void()>> run;
     {
       std::lock_guard<std::mutex> g(qmu);
-      wake_pending = false;  // anything queued from now on signals again
+      if (evfd_ready) wake_pending = false;  // anything queued from now on signals again
+      has_work.store(false, std::memory_order_relaxed);
       run.swap(tasks);
     }
     running_tasks = true;
@@ -372,11 +385,18 @@ struct GrpcServer::Worker : Executor, std::enable_shared_from_this<GrpcServer::W
     tid = std::this_thread::get_id();
     epoll_event evs[256];
     while (!stop.load(std::memory_order_relaxed)) {
+      if (has_work.load(std::memory_order_acquire)) drain_queue(false);
+      polling.store(true, std::memory_order_seq_cst);
+      if (has_work.load(std::memory_order_seq_cst)) {  // queued after the check above
+        polling.store(false, std::memory_order_relaxed);
+        continue;
+      }
       int n = epoll_wait(epfd, evs, 256, 200);
+      polling.store(false, std::memory_order_relaxed);
       for (int i = 0; i < n; ++i) {
         int fd = evs[i].data.fd;
         uint32_t e = evs[i].events;
-        if (fd == evfd) { drain_queue(); continue; }
+        if (fd == evfd) { drain_queue(true); continue; }
         if (fd == lfd) { accept_all(); continue; }
         auto it = conns.find(fd);
         if (it == conns.end()) continue;
