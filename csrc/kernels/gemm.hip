@@ -165,16 +165,15 @@ __global__ __launch_bounds__(64) void dense_gemm_kernel(const DenseGemmArgs a) {
   }
 }
 
-// ---- bf16: LDS-tiled GEMM.  A 256-thread workgroup (2 x 2 waves) owns a
-// BM x BN output tile (BM = 128 or 32, BN = 64).  Per 64-wide K stage the A and
-// W panels (128 B per row) are staged in LDS with full-line 16-B loads; each
-// wave reads its BM/32 + BN/32 fragments with ds_read_b128 and issues
-// (BM/32) * (BN/32) MFMAs (16x16x32 bf16) per 32-deep step.
-// The LDS row stride is 144 B (128 + 16): the 16 lanes of a ds_read_b128
-// group read 16 rows at one k-chunk, which land on 16 distinct 16-B slots of
-// the 256-B bank row (row * 9 mod 16) -- conflict-free.  Global loads run two
-// stages ahead (two register sets) into two LDS buffers: the L2 / HBM round
-// trip of stage k+2 overlaps the MFMAs of stages k and k+1.
+// ---- LDS-tiled GEMM (bf16 or exact fp32).  A 256-thread workgroup (2 x 2
+// waves) owns a BM x BN output tile (BM = 128 or 32, BN = 64).  Per K stage the
+// A and W panels (128 B per row) are staged in LDS with full-line 16-B loads;
+// each wave reads its BM/32 + BN/32 fragments with ds_read_b128 and issues
+// (BM/32) * (BN/32) MFMAs per fragment step.  The LDS rows are XOR-swizzled
+// (gemm_lds_kernel's sw()): fragment reads and staging stores are both
+// bank-conflict-free.  Global loads run two stages ahead (two register sets)
+// into two LDS buffers: the L2 / HBM round trip of stage k+2 overlaps the
+// MFMAs of stages k and k+1.
 //
 // Grid: 1-D, remapped XCD-aware.  Workgroups are dealt round-robin over the 8
 // XCDs (each with its own L2), so with a 2-D (N, M) grid the N tiles that share
@@ -233,13 +232,13 @@ __device__ __forceinline__ int xcd_tile(int L, int nwg) {
 
 // T = __bf16: v_mfma_f32_16x16x32_bf16, 64-deep K stages; T = float: exact
 // fp32 products on v_mfma_f32_16x16x4_f32 (four per 16-B fragment), 32-deep
-// stages.  The LDS image is the same in bytes either way: 128-B rows padded to
-// 144 B, one 16-B chunk per (row, k-chunk).
+// stages.  The LDS image is the same in bytes either way: 128-B rows of eight
+// 16-B chunks, XOR-swizzled per row pair.
 template <typename T, int AMODE, int BM, int BN, int NT>
 __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   constexpr int kEl = 16 / int(sizeof(T));    // elements per 16-B chunk
   constexpr int kBKe = 8 * kEl;               // K elements per stage (128 B per row)
-  constexpr int kLdr = kBKe + kEl;            // LDS row stride in elements (144 B)
+  constexpr int kLdr = kBKe;                  // LDS row = the 128-B panel row, XOR-swizzled (see sw())
   constexpr int WN = NT / 128;                // waves along N (2 along M); each wave owns BM/2 x 32
   constexpr int TM = BM / 32;                 // 16-row tiles per wave
   constexpr int TN = 2;                       // 16-col tiles per wave
@@ -248,6 +247,13 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   constexpr int CW = BN * 8 / NT;             // W staging chunks per thread
   constexpr int kBuf = (BM + BN) * kLdr;      // one LDS buffer: A panel then W panel
   static_assert(CA >= 1 && CW >= 1, "tile too small for the stagers");
+  // Element offset of 16-B chunk `ch` (0..7) of panel row `r`: chunk ch ^ ((r >> 1) & 7).
+  // A ds_read_b128 lane group (16 rows, one chunk) then hits 16 distinct
+  // 16-B slots of the 256-B bank row, and a staging store group (2 rows x 8
+  // chunks) fills the two halves -- both conflict-free (the 144-B padded rows
+  // this replaces left the stores 2-way conflicted: 33% of LDS-active cycles,
+  // profiles/r02h_gemm/pmc_summary.md).
+  auto sw = [](int r, int ch) { return r * kLdr + ((ch ^ ((r >> 1) & 7)) * kEl); };
   __shared__ __attribute__((aligned(16))) T smem[2 * kBuf];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave / WN, wc = wave % WN, r16 = lane & 15, kq = lane >> 4;
@@ -278,12 +284,12 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
 #pragma unroll
     for (int j = 0; j < CA; ++j) {
       const int c = tid + NT * j;
-      *reinterpret_cast<u32x4*>(As + (c >> 3) * kLdr + (c & 7) * kEl) = ra[j];
+      *reinterpret_cast<u32x4*>(As + sw(c >> 3, c & 7)) = ra[j];
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
       const int c = tid + NT * j;
-      *reinterpret_cast<u32x4*>(Ws + (c >> 3) * kLdr + (c & 7) * kEl) = rw[j];
+      *reinterpret_cast<u32x4*>(Ws + sw(c >> 3, c & 7)) = rw[j];
     }
   };
   f32x4 acc[TM][TN];
@@ -299,10 +305,10 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
       u32x4 af[TM], bf[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const u32x4*>(As + (wr * (BM / 2) + i * 16 + r16) * kLdr + kk * 4 * kEl + kq * kEl);
+        af[i] = *reinterpret_cast<const u32x4*>(As + sw(wr * (BM / 2) + i * 16 + r16, kk * 4 + kq));
 #pragma unroll
       for (int i = 0; i < TN; ++i)
-        bf[i] = *reinterpret_cast<const u32x4*>(Ws + (wc * 32 + i * 16 + r16) * kLdr + kk * 4 * kEl + kq * kEl);
+        bf[i] = *reinterpret_cast<const u32x4*>(Ws + sw(wc * 32 + i * 16 + r16, kk * 4 + kq));
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
