@@ -234,7 +234,7 @@ __device__ __forceinline__ int xcd_tile(int L, int nwg) {
 // fp32 products on v_mfma_f32_16x16x4_f32 (four per 16-B fragment), 32-deep
 // stages.  The LDS image is the same in bytes either way: 128-B rows of eight
 // 16-B chunks, XOR-swizzled per row pair.
-template <typename T, int AMODE, int BM, int BN, int NT>
+template <typename T, int AMODE, int BM, int BN, int NT, int NS = 2>
 __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   constexpr int kEl = 16 / int(sizeof(T));    // elements per 16-B chunk
   constexpr int kBKe = 8 * kEl;               // K elements per stage (128 B per row)
@@ -262,14 +262,19 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
   const T* W = static_cast<const T*>(a.W);
   const int KS = a.Kp / kBKe;
-  // two stages of staging registers; every index below is a compile-time
-  // constant (the K loop is unrolled by two), so they stay in VGPRs
-  u32x4 ra0[CA], rw0[CW], ra1[CA], rw1[CW];
-  auto gload = [&](int ks, u32x4* ra, u32x4* rw) {
+  // NS sets of staging registers; every set index below is a compile-time
+  // constant (the K loop is unrolled by NS), so they stay in VGPRs
+  u32x4 ra[NS][CA], rw[NS][CW];
+  auto gload = [&](int ks, bool live, u32x4* ra, u32x4* rw) {
+    // A computed on the fly (AMODE 2: reparameterised draws, no memory loads)
+    // is skipped for the clamped stages past the end; loaded operands are not
+    // (see the unconditional ring below)
+    if (AMODE == 0 || live) {
 #pragma unroll
-    for (int j = 0; j < CA; ++j) {
-      const int c = tid + NT * j;
-      ra[j] = stage_a_chunk<T, AMODE>(a, m0 + (c >> 3), ks * kBKe + (c & 7) * kEl);
+      for (int j = 0; j < CA; ++j) {
+        const int c = tid + NT * j;
+        ra[j] = stage_a_chunk<T, AMODE>(a, m0 + (c >> 3), ks * kBKe + (c & 7) * kEl);
+      }
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
@@ -324,22 +329,27 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
         }
     }
   };
-  gload(0, ra0, rw0);
-  if (KS > 1) gload(1, ra1, rw1);
-  lstore(0, ra0, rw0);
+  // NS register sets: the global loads of stage ks + NS are issued as stage ks
+  // starts (its set was stored to LDS one stage earlier), so NS stages of
+  // L2 / HBM latency are in flight behind the MFMAs; LDS is double-buffered.
+  // Loads and LDS stores are issued unconditionally (stage indices clamped to
+  // the last stage, the K loop padded to a multiple of NS with the compute
+  // skipped): a load inside a branch makes the compiler's vmcnt bookkeeping
+  // wait for every outstanding load at the join, which drains the ring.
+#pragma unroll
+  for (int st = 0; st < NS; ++st) gload(min(st, KS - 1), st < KS, ra[st], rw[st]);
+  lstore(0, ra[0], rw[0]);
   __syncthreads();
-  for (int ks = 0; ks < KS; ks += 2) {
-    // even stage: buffer 0 holds it, set 1 holds ks + 1, set 0 is free for ks + 2
-    if (ks + 2 < KS) gload(ks + 2, ra0, rw0);
-    compute(0);
-    if (ks + 1 < KS) lstore(1, ra1, rw1);
-    __syncthreads();
-    if (ks + 1 >= KS) break;
-    // odd stage: buffer 1, set 0 holds ks + 2, set 1 free for ks + 3
-    if (ks + 3 < KS) gload(ks + 3, ra1, rw1);
-    compute(1);
-    if (ks + 2 < KS) lstore(0, ra0, rw0);
-    __syncthreads();
+  const int KSr = (KS + NS - 1) / NS * NS;
+  for (int ks0 = 0; ks0 < KSr; ks0 += NS) {
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      const int ks = ks0 + st;
+      gload(min(ks + NS, KS - 1), ks + NS < KS, ra[st], rw[st]);
+      if (ks < KS) compute(ks & 1);
+      lstore((ks + 1) & 1, ra[(st + 1) % NS], rw[(st + 1) % NS]);  // past the last stage: never read
+      __syncthreads();
+    }
   }
   // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
   if (a.out64) {  // N <= 16: wave wc = 0, tile tn = 0 holds a row's every column (16 lanes of one kq)

@@ -6,7 +6,10 @@ for d in sorted(glob.glob('gpurun_out/ab_*/')):
     acc = collections.defaultdict(list)
     for r in rows:
         n = r['Kernel_Name']
-        m = re.search(r'(gemm_bf16_g?lds_kernel<[^>]*>|convert_bf16_kernel|mlp_finish_kernel|mlp_convert_kernel)', n)
+        mm = re.search(r'gemm_lds_kernelIDF16bLi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)', n)  # undemangled __bf16
+        if mm:
+            n = "gemm_lds_kernel<__bf16, %s, %s, %s, %s, %s>" % mm.groups()
+        m = re.search(r'(gemm_(?:bf16_g?)?lds_kernel<[^>]*>|convert_bf16_kernel|mlp_finish_kernel|mlp_convert_kernel)', n)
         if m:
             key = m.group(1) + ' wgs=' + str(int(r['Grid_Size_X'])//int(r['Workgroup_Size_X']))
             acc[key].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1000)
