@@ -83,6 +83,8 @@ def parse_args(argv=None):
                     help="write a sampling CPU profile of the serving process over the timed window to this JSON file")
     ap.add_argument("--cpu-profile-depth", type=int, default=1, help="frames per CPU-profile sample (>1: call paths)")
     ap.add_argument("--variants-child", default=None, help=argparse.SUPPRESS)  # internal: isolated variant runner
+    ap.add_argument("--pin", choices=["auto", "none"], default="auto",
+                    help="pin each rank (front end, device thread, load generator) to whole CCDs local to its GPU")
     ap.add_argument("--fabric-probe", choices=["auto", "none"], default="auto",
                     help="N >= 2: after everything else, run tools/fabric_probe.py in child processes "
                          "(rank-placed graph nodes over the RCCL p2p fabric) under a time limit")
@@ -125,30 +127,58 @@ def spawn_ranks(n: int, argv) -> int:
 
 # ------------------------------------------------------------------ sizing
 def cpu_budget() -> float:
-    """CPUs this process may use: cgroup v2 quota (cpu.max) or affinity."""
+    """CPUs this process may use: the smaller of the cgroup v2 quota (cpu.max)
+    and the CPU affinity mask."""
+    limits = []
     try:
         quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
         if quota != "max":
-            return float(quota) / float(period)
+            limits.append(float(quota) / float(period))
     except (OSError, ValueError):
         pass
     try:
-        return float(len(os.sched_getaffinity(0)))
+        limits.append(float(len(os.sched_getaffinity(0))))
     except AttributeError:
-        return float(os.cpu_count() or 8)
+        limits.append(float(os.cpu_count() or 8))
+    return min(limits)
 
 
-def size_threads(args, local_world: int) -> float:
+def size_threads(args, per_rank: float) -> float:
     """Split the CPU share of one rank between the front end (~60%), the
     closed-loop load generator (~32%) and the GPU device thread (measured on
     a 16-CPU MI355X share: 10 front-end / 5 generator threads was the best
-    split, profiles/r01f_sweep_executor)."""
-    per_rank = max(2.0, cpu_budget() / max(1, local_world))
+    split unpinned, profiles/r01f_sweep_executor)."""
+    per_rank = max(2.0, per_rank)
     if args.server_threads is None:
         args.server_threads = max(1, min(16, int(round(per_rank * 0.6))))
     if args.client_threads is None:
         args.client_threads = max(1, min(10, int(round(per_rank * 0.32))))
     return per_rank
+
+
+def place_rank(args, d) -> tuple:
+    """(per-rank CPU budget, pinned CPUs): with --pin auto each rank is pinned
+    to whole CCDs local to its GPU (seldon_core_amd.utils.topology), so its
+    front end, device thread and load generator share one L3."""
+    per_rank = cpu_budget() / max(1, d.local_world)
+    if args.pin != "auto" or not d.has_gpu:
+        return per_rank, []
+    from seldon_core_amd.utils import topology
+
+    cpus = topology.pin(d.local_rank, int(round(per_rank)))
+    return per_rank, cpus
+
+
+def cpu_ranges(cpus) -> str:
+    out, i = [], 0
+    cpus = sorted(cpus)
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
 
 
 # ------------------------------------------------------------------ graphs
@@ -606,7 +636,8 @@ def main() -> None:
         variants_child(args)
         return
     d = Dist()
-    per_rank_cpus = size_threads(args, d.local_world)
+    per_rank_budget, pinned = place_rank(args, d)
+    per_rank_cpus = size_threads(args, per_rank_budget)
     spin = not args.no_spin
     import seldon_core_amd as sca
 
@@ -646,7 +677,8 @@ def main() -> None:
             json.dump(prof, f, indent=1)
     st = unit_stats(dep)
     mine = {"rank": d.rank, "device": d.device, "ok": lg["ok"], "wall": wall, "p50": lg["p50_ms"],
-            "p99": lg["p99_ms"], "stats": st, "cpu_budget": round(per_rank_cpus, 2), "cpu": cpu}
+            "p99": lg["p99_ms"], "stats": st, "cpu_budget": round(per_rank_cpus, 2), "cpu": cpu,
+            "pinned_cpus": cpu_ranges(pinned) if pinned else None}
     extras: dict = {}
     failures = []
     # ---- after the timed region: correctness + extra configs
@@ -692,7 +724,8 @@ def summarize(args, d: Dist, results, label: str, wl: Workload) -> dict:
     value = sum(m["ok"] for m in mines) / wall_max
     base = REST_BASELINE if args.api == "rest" else GRPC_BASELINE
     st0 = mines[0]["stats"]
-    per_rank = [{"rank": m["rank"], "device": m["device"], "cpu_budget": m["cpu_budget"], **m["cpu"],
+    per_rank = [{"rank": m["rank"], "device": m["device"], "cpu_budget": m["cpu_budget"],
+                 "pinned_cpus": m.get("pinned_cpus"), **m["cpu"],
                  "rps": round(m["ok"] / m["wall"], 1), "p50_ms": m["p50"], "p99_ms": m["p99"],
                  "gpu_batches": m["stats"]["batches"],
                  "mean_rows_per_batch": round(m["stats"]["rows"] / max(1, m["stats"]["batches"]), 2),
