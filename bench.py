@@ -165,6 +165,10 @@ def place_rank(args, d) -> tuple:
         return per_rank, []
     from seldon_core_amd.utils import topology
 
+    # One CCD (16 logical CPUs on MI355X hosts) is the measured sweet spot
+    # (profiles/r02m_pinning): a rank with a larger share still takes one, so
+    # N = 1 and N = 8 on an unconstrained node run the same per-rank setup.
+    per_rank = min(per_rank, 16.0)
     cpus = topology.pin(d.local_rank, int(round(per_rank)))
     return per_rank, cpus
 

@@ -67,6 +67,8 @@ def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
                     help="checkpoint stateful nodes (routers, detectors) and restore them at start "
                          "(SELDON_PERSISTENCE_BACKEND=file|redis)")
     ap.add_argument("--push-frequency", type=float, default=None, help="seconds between checkpoints (default 60)")
+    ap.add_argument("--pin-cpus", type=int, default=0,
+                    help="pin each worker to whole CCDs of its GPU's socket covering this many CPUs (0 = off)")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -88,6 +90,13 @@ def _n_workers(arg: str) -> int:
 
 # ------------------------------------------------------------------ worker
 def run_worker(args: argparse.Namespace) -> int:
+    if args.pin_cpus > 0 and (args.device is None or args.device >= 0):
+        # before the front end and the GPU units start their threads (they inherit it)
+        from .utils.topology import pin
+
+        cpus = pin(args.device or 0, args.pin_cpus)
+        if cpus:
+            logger.info("worker pinned to CPUs %s", cpus)
     from .serving.config import EngineConfig
     from .serving.deployment import Deployment
     from .serving.spec import load_spec, predictors
