@@ -366,6 +366,7 @@ bool BatchedUnit::launch(Slot* s) {
       for (size_t i = 0; i < s->items.size(); ++i) o[i + 1] = o[i] + s->items[i].rows;
       seg = s->h_seg.dev<int32_t>();
     }
+    bool signalled = false;  // the model's last kernel completes s->ev itself
     auto run = [&](const double* x, double* y) {
       if (seg) model_->launch_segments(x, rows, cols, y, s->ws.get(), seg, nseg, st);
       else model_->launch(x, rows, cols, y, s->ws.get(), st);
@@ -379,7 +380,13 @@ bool BatchedUnit::launch(Slot* s) {
         err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
         xin = s->d_in.as<double>();
       }
-      if (err == hipSuccess) run(xin, s->h_out.dev<double>());
+      if (err == hipSuccess) {
+        // zero-copy output: nothing follows the kernel on the stream, so a
+        // model that can lets its kernel's own dispatch complete the event
+        signalled = !seg && model_->launch_signal(xin, rows, cols, s->h_out.dev<double>(), s->ws.get(), st,
+                                                  s->ev.get());
+        if (!signalled) run(xin, s->h_out.dev<double>());
+      }
     } else {
       err = hipMemcpyAsync(s->d_in.get(), direct ? static_cast<const void*>(s->items[0].xp) : hin, bin,
                            hipMemcpyHostToDevice, st);
@@ -389,7 +396,7 @@ bool BatchedUnit::launch(Slot* s) {
       }
     }
     if (err == hipSuccess) err = hipGetLastError();
-    if (err == hipSuccess) err = hipEventRecord(s->ev.get(), st);
+    if (err == hipSuccess && !signalled) err = hipEventRecord(s->ev.get(), st);
   } catch (const std::exception& ex) {
     err = hipErrorUnknown;
     launch_error = ex.what();

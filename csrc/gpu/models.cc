@@ -26,6 +26,12 @@ void LinearModel::launch(const double* X, int rows, int cols, double* out, void*
   kern::linear_f64(X, rows, K_, dW_.as<double>(), db_.as<double>(), C_, act_, out, s);
 }
 
+bool LinearModel::launch_signal(const double* X, int rows, int, double* out, void*, hipStream_t s, hipEvent_t done) {
+  if (rows <= 0) return false;  // nothing would be launched to complete `done`
+  kern::linear_f64(X, rows, K_, dW_.as<double>(), db_.as<double>(), C_, act_, out, s, done);
+  return true;
+}
+
 void LinearModel::run_cpu(const double* X, int rows, int, double* out) const {
   std::vector<double> z(static_cast<size_t>(C_));
   const int oc = out_cols(K_);

@@ -51,6 +51,14 @@ class RowModel {
   }
   virtual size_t workspace_bytes(int max_rows, int cols) const { (void)max_rows; (void)cols; return 0; }
   virtual void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) = 0;
+  // launch() whose last kernel completes `done` from its own dispatch
+  // (hipExtLaunchKernelGGL) -- the batcher then skips its hipEventRecord.
+  // Returns false (nothing launched) if the model cannot.
+  virtual bool launch_signal(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
+                             hipEvent_t done) {
+    (void)X; (void)rows; (void)cols; (void)out; (void)ws; (void)s; (void)done;
+    return false;
+  }
   virtual void run_cpu(const double* X, int rows, int cols, double* out) const = 0;
   // Independent copy (host parameters only; call to_device on it) -- one per
   // GPU replica.
@@ -76,6 +84,8 @@ class LinearModel : public RowModel {
   int out_cols(int) const override { return act_ == kern::kActBinaryLogistic ? 2 : C_; }
   void to_device(int device) override;
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  bool launch_signal(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
+                     hipEvent_t done) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
   std::shared_ptr<RowModel> clone() const override {
     return with_meta(std::make_shared<LinearModel>(W_, b_, C_, K_, act_));

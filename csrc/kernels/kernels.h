@@ -24,8 +24,10 @@ enum LinearAct : int {
   kActSigmoid = 4,       // independent sigmoid per column
 };
 // fp64 I/O, fp64 accumulate (parity with sklearn to ~1e-15).
+// `stop` (optional): completed by the kernel's own dispatch, replacing a
+// hipEventRecord after it.
 void linear_f64(const double* X, int rows, int K, const double* W, const double* b, int C, int act,
-                double* out, hipStream_t stream);
+                double* out, hipStream_t stream, hipEvent_t stop = nullptr);
 
 // ------------------------------------------------------------ tree ensemble
 // Perfect (complete) binary trees of fixed depth D, breadth-first.  Node i of

@@ -8,6 +8,7 @@
 //  * wave-per-row: larger K.  Lanes stride K (coalesced row reads), each
 //    class logit is a 64-lane shuffle reduction; logits staged in LDS.
 // fp64 throughout so results match sklearn bit-for-bit up to summation order.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -103,32 +104,42 @@ __global__ __launch_bounds__(kBlock) void linear_wave_rows(const double* __restr
   }
 }
 
+// `stop` (optional) is completed by the kernel's own dispatch packet
+// (hipExtLaunchKernelGGL): one HIP call per batch instead of launch +
+// hipEventRecord (2.1 + 2.6 us of host time, tools/micro/launch_cost.hip).
+template <class... Args, class... P>
+void launch_maybe_ext(void (*k)(Args...), dim3 grid, dim3 block, size_t lds, hipStream_t s, hipEvent_t stop,
+                      P... args) {
+  if (stop) hipExtLaunchKernelGGL(k, grid, block, uint32_t(lds), s, nullptr, stop, 0, args...);
+  else hipLaunchKernelGGL(k, grid, block, lds, s, args...);
+}
+
 template <int ACT>
 void launch_linear(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
-                   hipStream_t s) {
+                   hipStream_t s, hipEvent_t stop) {
   if (rows <= 0) return;
   if (C <= kMaxThreadC && C * K + C <= kMaxLdsDoubles) {
     const size_t lds = size_t(C * K + C + kBlock * C) * sizeof(double);
-    hipLaunchKernelGGL(linear_thread_rows<ACT>, dim3((rows + kBlock - 1) / kBlock), dim3(kBlock), lds, s, X, rows,
-                       K, W, b, C, out);
+    launch_maybe_ext(linear_thread_rows<ACT>, dim3((rows + kBlock - 1) / kBlock), dim3(kBlock), lds, s, stop, X, rows,
+                     K, W, b, C, out);
   } else {
     const int rows_per_block = kBlock / 64;
     const size_t lds = size_t(rows_per_block * C) * sizeof(double);
-    hipLaunchKernelGGL(linear_wave_rows<ACT>, dim3((rows + rows_per_block - 1) / rows_per_block), dim3(kBlock), lds,
-                       s, X, rows, K, W, b, C, out);
+    launch_maybe_ext(linear_wave_rows<ACT>, dim3((rows + rows_per_block - 1) / rows_per_block), dim3(kBlock), lds, s,
+                     stop, X, rows, K, W, b, C, out);
   }
 }
 
 }  // namespace
 
 void linear_f64(const double* X, int rows, int K, const double* W, const double* b, int C, int act, double* out,
-                hipStream_t s) {
+                hipStream_t s, hipEvent_t stop) {
   switch (act) {
-    case kActIdentity: launch_linear<kActIdentity>(X, rows, K, W, b, C, out, s); break;
-    case kActSoftmax: launch_linear<kActSoftmax>(X, rows, K, W, b, C, out, s); break;
-    case kActBinaryLogistic: launch_linear<kActBinaryLogistic>(X, rows, K, W, b, C, out, s); break;
-    case kActOvr: launch_linear<kActOvr>(X, rows, K, W, b, C, out, s); break;
-    default: launch_linear<kActSigmoid>(X, rows, K, W, b, C, out, s); break;
+    case kActIdentity: launch_linear<kActIdentity>(X, rows, K, W, b, C, out, s, stop); break;
+    case kActSoftmax: launch_linear<kActSoftmax>(X, rows, K, W, b, C, out, s, stop); break;
+    case kActBinaryLogistic: launch_linear<kActBinaryLogistic>(X, rows, K, W, b, C, out, s, stop); break;
+    case kActOvr: launch_linear<kActOvr>(X, rows, K, W, b, C, out, s, stop); break;
+    default: launch_linear<kActSigmoid>(X, rows, K, W, b, C, out, s, stop); break;
   }
 }
 
