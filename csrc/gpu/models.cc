@@ -193,6 +193,25 @@ bool TreeEnsembleModel::zero_copy_input_for(int rows, int cols) const {
 }
 
 void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) {
+  launch_impl(X, rows, cols, out, ws, s, nullptr);
+}
+
+bool TreeEnsembleModel::launch_signal(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
+                                      hipEvent_t done) {
+  if (rows <= 0 || uses_fused(rows)) return false;  // contract: false = nothing launched
+  return launch_impl(X, rows, cols, out, ws, s, done);
+}
+
+bool TreeEnsembleModel::uses_fused(int rows) const {
+  int rb, pi, lt;
+  plan_for(rows, &rb, &pi, &lt);
+  const Plan& p = *plans_[size_t(pi)];
+  return fused_reduce_ && spec_.groups <= kern::kTreeFusedMaxGroups && size_t(rows) * p.n_chunks <= 4096;
+}
+
+// `done` (optional): completed by the batch's last kernel; returns whether it was
+bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
+                                    hipEvent_t done) {
   (void)cols;
   int rb, pi, lt;
   plan_for(rows, &rb, &pi, &lt);
@@ -202,8 +221,7 @@ void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out,
   // Small slabs may fold in the partial kernel's last workgroup (one launch
   // per batch; the tail does <= 16 slab loads per thread) -- off by default,
   // see plan_for.
-  const bool fused = fused_reduce_ && spec_.groups <= kern::kTreeFusedMaxGroups && size_t(rows) * p.n_chunks <= 4096;
-  if (fused) {
+  if (uses_fused(rows)) {
     const kern::TreeReduceArgs red{counter, p.group.as<int>(), spec_.groups, d_base_.as<float>(), spec_.scale,
                                    spec_.transform, out, spec_.out_cols};
     if (spec_.depth > 0)
@@ -212,7 +230,7 @@ void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out,
     else
       kern::tree_sparse_fused(X, rows, spec_.n_features, d_sparse_.as<kern::SparseNode>(), d_roots_.as<int>(),
                               spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s);
-    return;
+    return false;  // the fused launchers record no event
   }
   if (spec_.depth > 0)
     kern::tree_perfect_partial(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
@@ -221,7 +239,8 @@ void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out,
     kern::tree_sparse_partial(X, rows, spec_.n_features, d_sparse_.as<kern::SparseNode>(), d_roots_.as<int>(),
                               spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, s);
   kern::tree_reduce(partial, rows, p.n_chunks, p.group.as<int>(), spec_.groups, d_base_.as<float>(), spec_.scale,
-                    spec_.transform, out, spec_.out_cols, s);
+                    spec_.transform, out, spec_.out_cols, s, done);
+  return done != nullptr;
 }
 
 float TreeEnsembleModel::tree_value_cpu(int t, const float* x) const {

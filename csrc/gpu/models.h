@@ -128,6 +128,8 @@ class TreeEnsembleModel : public RowModel {
   void to_device(int device) override;
   size_t workspace_bytes(int max_rows, int cols) const override;
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
+  bool launch_signal(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
+                     hipEvent_t done) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
   const TreeEnsembleSpec& spec() const { return spec_; }
   bool zero_copy_input() const override { return false; }  // every tree-chunk block stages the X tile
@@ -141,6 +143,8 @@ class TreeEnsembleModel : public RowModel {
   void set_fused_reduce(bool on) { fused_reduce_ = on; }
 
  private:
+  bool launch_impl(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s, hipEvent_t done);
+  bool uses_fused(int rows) const;
   struct Plan {
     int chunk_trees;
     int n_chunks;

@@ -73,7 +73,7 @@ enum TreeTransform : int {
 };
 void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,
                  const float* base_margin, float scale, int transform, double* out, int out_cols,
-                 hipStream_t stream);
+                 hipStream_t stream, hipEvent_t stop = nullptr);
 // Fused variant: the partial kernel's last workgroup to finish (device-scope
 // counter, reset by that workgroup) folds the slab and writes `out` -- one
 // launch per batch instead of two.  Used for small slabs (rows x chunks) and

@@ -14,6 +14,7 @@
 // each XCD's 4 MiB L2 across batches.  Per-row partial sums over the thread's
 // trees are reduced through LDS and written to a [chunk, row] slab that
 // tree_reduce folds (deterministic, no float atomics).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -499,7 +500,8 @@ void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes
 }
 
 void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,
-                 const float* base_margin, float scale, int transform, double* out, int out_cols, hipStream_t s) {
+                 const float* base_margin, float scale, int transform, double* out, int out_cols, hipStream_t s,
+                 hipEvent_t stop) {
   if (rows <= 0) return;
   if (groups > kMaxGroups) groups = kMaxGroups;
   // Keep LDS <= 64 KB per block: 256 threads up to 32 groups, 64 beyond.
@@ -511,8 +513,13 @@ void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_
   while (L < nthr && L * 4 < n_chunks) L <<= 1;
   const int RB = nthr / L;
   const size_t lds = size_t(nthr) * groups * sizeof(double);
-  hipLaunchKernelGGL(reduce_transform, dim3((rows + RB - 1) / RB), dim3(nthr), lds, s, partial, rows, n_chunks,
-                     chunk_group, groups, base_margin, scale, transform, out, out_cols, RB);
+  if (stop)  // the batch's last kernel completes the batcher's event from its own dispatch
+    hipExtLaunchKernelGGL(reduce_transform, dim3((rows + RB - 1) / RB), dim3(nthr), uint32_t(lds), s, nullptr, stop, 0,
+                          partial, rows, n_chunks, chunk_group, groups, base_margin, scale, transform, out, out_cols,
+                          RB);
+  else
+    hipLaunchKernelGGL(reduce_transform, dim3((rows + RB - 1) / RB), dim3(nthr), lds, s, partial, rows, n_chunks,
+                       chunk_group, groups, base_margin, scale, transform, out, out_cols, RB);
 }
 
 }  // namespace sca::kern

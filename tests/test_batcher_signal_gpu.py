@@ -25,3 +25,23 @@ def test_signalled_linear_batches_are_exact_under_concurrency():
         assert st["requests"] >= 1200 and st["batches"] >= 1
     finally:
         unit.stop()
+
+
+@pytest.mark.gpu
+def test_signalled_tree_batches_are_exact_under_concurrency():
+    """Tree ensembles: the two-pass plan's reduce kernel completes the event
+    (the partial kernel before it on the same stream), the fused plan falls
+    back to launch + hipEventRecord; both must hand back complete answers."""
+    from seldon_core_amd.models import synthetic_xgboost
+
+    ens = synthetic_xgboost(300, 6, 16, seed=9)
+    unit = sca.native().BatchedUnit(to_row_model(ens), 0, slots=4)
+    rng = np.random.default_rng(7)
+    Xs = [rng.standard_normal((1 + i % 29, 16)) for i in range(600)] + [rng.standard_normal((700, 16))]
+    try:
+        with cf.ThreadPoolExecutor(8) as ex:
+            outs = list(ex.map(unit.run, Xs))
+        for X, got in zip(Xs, outs):
+            np.testing.assert_allclose(np.asarray(got).reshape(-1), ens.predict(X).reshape(-1), rtol=2e-5, atol=2e-5)
+    finally:
+        unit.stop()
