@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace sca::gpu {
 
@@ -71,6 +72,8 @@ void LinearModel::run_cpu(const double* X, int rows, int, double* out) const {
 static const int kPlanSizes[] = {4, 8, 16, 32, 64, 128, 256, 512};
 
 TreeEnsembleModel::TreeEnsembleModel(TreeEnsembleSpec spec) : spec_(std::move(spec)) {
+  // SCA_TREE_FUSED=0/1 forces the single-launch fused-fold plan off / on (A/B runs)
+  if (const char* f = std::getenv("SCA_TREE_FUSED")) fused_reduce_ = f[0] == '1';
   const int T = spec_.n_trees;
   if (T <= 0) throw std::runtime_error("TreeEnsembleModel: no trees");
   if (int(spec_.tree_group.size()) != T) spec_.tree_group.assign(size_t(T), 0);
@@ -198,7 +201,7 @@ void TreeEnsembleModel::launch(const double* X, int rows, int cols, double* out,
 
 bool TreeEnsembleModel::launch_signal(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
                                       hipEvent_t done) {
-  if (rows <= 0 || uses_fused(rows)) return false;  // contract: false = nothing launched
+  if (rows <= 0) return false;  // contract: false = nothing launched
   return launch_impl(X, rows, cols, out, ws, s, done);
 }
 
@@ -226,11 +229,12 @@ bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double*
                                    spec_.transform, out, spec_.out_cols};
     if (spec_.depth > 0)
       kern::tree_perfect_fused(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
-                               spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s, lt);
+                               spec_.depth, spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s, lt,
+                               done);
     else
       kern::tree_sparse_fused(X, rows, spec_.n_features, d_sparse_.as<kern::SparseNode>(), d_roots_.as<int>(),
-                              spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s);
-    return false;  // the fused launchers record no event
+                              spec_.cmp_le, p.begin.as<int>(), p.n_chunks, rb, partial, red, s, done);
+    return done != nullptr;
   }
   if (spec_.depth > 0)
     kern::tree_perfect_partial(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),

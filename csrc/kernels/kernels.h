@@ -92,10 +92,11 @@ struct TreeReduceArgs {
 };
 void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
-                        const TreeReduceArgs& red, hipStream_t stream, int lds_trees = 0);
+                        const TreeReduceArgs& red, hipStream_t stream, int lds_trees = 0,
+                        hipEvent_t stop = nullptr);
 void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
                        const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
-                       const TreeReduceArgs& red, hipStream_t stream);
+                       const TreeReduceArgs& red, hipStream_t stream, hipEvent_t stop = nullptr);
 
 // ------------------------------------------------------------ combiners
 // out = mean over N inputs (each [n] fp64). inputs: device array of pointers.

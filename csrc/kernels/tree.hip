@@ -423,16 +423,23 @@ constexpr int kTreeLdsPad = 16;  // leaves slab rounded up to 16 B
 template <bool FUSED>
 void launch_perfect(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                     int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
-                    int lds_trees, hipStream_t s) {
+                    int lds_trees, hipStream_t s, hipEvent_t stop = nullptr) {
   bool stage;
   int lds = lds_bytes_for(RB, F, &stage);
   if (stage) lds = int((kBlock + ((RB * F + 3) & ~3)) * sizeof(float));
   if (depth > kMaxTreeLdsDepth || lds + lds_trees * tree_bytes(depth) + kTreeLdsPad > kMaxLdsBytes) lds_trees = 0;
   if (lds_trees) lds += lds_trees * tree_bytes(depth) + kTreeLdsPad;
   dim3 grid((rows + RB - 1) / RB, n_chunks);
-#define SCA_TREE_LAUNCH(DD, TL)                                                                                  \
-  hipLaunchKernelGGL((perfect_partial<DD, FUSED, TL>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves,   \
-                     depth, cmp_le, chunk_begin, RB, int(stage), partial, n_chunks, lds_trees, red)
+#define SCA_TREE_LAUNCH(DD, TL)                                                                                    \
+  do {                                                                                                            \
+    if (stop)                                                                                                     \
+      hipExtLaunchKernelGGL((perfect_partial<DD, FUSED, TL>), grid, dim3(kBlock), uint32_t(lds), s, nullptr, stop, \
+                            0, X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, RB, int(stage), partial,    \
+                            n_chunks, lds_trees, red);                                                            \
+    else                                                                                                          \
+      hipLaunchKernelGGL((perfect_partial<DD, FUSED, TL>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, \
+                         depth, cmp_le, chunk_begin, RB, int(stage), partial, n_chunks, lds_trees, red);          \
+  } while (0)
 #define SCA_TREE_CASE(DD)                                  \
   case DD:                                                 \
     if (lds_trees) SCA_TREE_LAUNCH(DD, true);              \
@@ -452,12 +459,16 @@ void launch_perfect(const double* X, int rows, int F, const TreeNode* nodes, con
 template <bool FUSED>
 void launch_sparse(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
                    const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
-                   hipStream_t s) {
+                   hipStream_t s, hipEvent_t stop = nullptr) {
   bool stage;
   const int lds = lds_bytes_for(RB, F, &stage);
   dim3 grid((rows + RB - 1) / RB, n_chunks);
-  hipLaunchKernelGGL((sparse_partial<FUSED>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, tree_root, cmp_le,
-                     chunk_begin, RB, int(stage), partial, n_chunks, red);
+  if (stop)
+    hipExtLaunchKernelGGL((sparse_partial<FUSED>), grid, dim3(kBlock), uint32_t(lds), s, nullptr, stop, 0, X, rows, F,
+                          nodes, tree_root, cmp_le, chunk_begin, RB, int(stage), partial, n_chunks, red);
+  else
+    hipLaunchKernelGGL((sparse_partial<FUSED>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, tree_root, cmp_le,
+                       chunk_begin, RB, int(stage), partial, n_chunks, red);
 }
 
 }  // namespace
@@ -486,17 +497,17 @@ void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nod
 
 void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial,
-                        const TreeReduceArgs& red, hipStream_t s, int lds_trees) {
+                        const TreeReduceArgs& red, hipStream_t s, int lds_trees, hipEvent_t stop) {
   if (rows <= 0 || n_chunks <= 0) return;
   launch_perfect<true>(X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, n_chunks, RB, partial, red, lds_trees,
-                       s);
+                       s, stop);
 }
 
 void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
                        const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
-                       hipStream_t s) {
+                       hipStream_t s, hipEvent_t stop) {
   if (rows <= 0 || n_chunks <= 0) return;
-  launch_sparse<true>(X, rows, F, nodes, tree_root, cmp_le, chunk_begin, n_chunks, RB, partial, red, s);
+  launch_sparse<true>(X, rows, F, nodes, tree_root, cmp_le, chunk_begin, n_chunks, RB, partial, red, s, stop);
 }
 
 void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,

@@ -28,14 +28,18 @@ def test_signalled_linear_batches_are_exact_under_concurrency():
 
 
 @pytest.mark.gpu
-def test_signalled_tree_batches_are_exact_under_concurrency():
-    """Tree ensembles: the two-pass plan's reduce kernel completes the event
-    (the partial kernel before it on the same stream), the fused plan falls
-    back to launch + hipEventRecord; both must hand back complete answers."""
+@pytest.mark.parametrize("fused", [False, True])
+def test_signalled_tree_batches_are_exact_under_concurrency(fused):
+    """Tree ensembles: the batch's last kernel completes the event -- the
+    reduce kernel of the two-pass plan (the partial kernel before it on the
+    same stream), or the fused plan's partial kernel whose last workgroup
+    folds the slab; both must hand back complete answers."""
     from seldon_core_amd.models import synthetic_xgboost
 
     ens = synthetic_xgboost(300, 6, 16, seed=9)
-    unit = sca.native().BatchedUnit(to_row_model(ens), 0, slots=4)
+    d = ens.device_spec()
+    d["fused_reduce"] = fused
+    unit = sca.native().BatchedUnit(sca.native().tree_model(d), 0, slots=4)
     rng = np.random.default_rng(7)
     Xs = [rng.standard_normal((1 + i % 29, 16)) for i in range(600)] + [rng.standard_normal((700, 16))]
     try:
