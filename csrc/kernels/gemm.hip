@@ -314,19 +314,29 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
 #pragma unroll
       for (int i = 0; i < TN; ++i)
         bf[i] = *reinterpret_cast<const u32x4*>(Ws + sw(wc * 32 + i * 16 + r16, kk * 4 + kq));
+      if constexpr (sizeof(T) == 2) {
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
+        for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          if constexpr (sizeof(T) == 2) {
+          for (int tn = 0; tn < TN; ++tn)
             acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[tm]),
                                                                   __builtin_bit_cast(bf16x8, bf[tn]), acc[tm][tn], 0, 0, 0);
-          } else {  // lane (r16, kq) holds k = kk * 16 + 4 kq + j of MFMA j: every k once per stage
-            const f32x4 x = __builtin_bit_cast(f32x4, af[tm]), y = __builtin_bit_cast(f32x4, bf[tn]);
+      } else {
+        // lane (r16, kq) holds k = kk * 16 + 4 kq + j of MFMA j: every k once
+        // per stage.  j outermost: consecutive MFMAs go to the TM x TN
+        // independent accumulators, so the 16x16x4 f32 MFMA's 40-cycle
+        // dependent latency (32-cycle issue) is never exposed; each
+        // accumulator still sees j = 0..3 in order (bit-identical sums).
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], y[j], acc[tm][tn], 0, 0, 0);
-          }
-        }
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+              acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(__builtin_bit_cast(f32x4, af[tm])[j],
+                                                                 __builtin_bit_cast(f32x4, bf[tn])[j], acc[tm][tn], 0,
+                                                                 0, 0);
+      }
     }
   };
   // NS register sets: the global loads of stage ks + NS are issued as stage ks
@@ -429,7 +439,9 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
   // first layer (AMODE 2) recomputes its reparameterised A panel per N tile,
   // so it takes 128 x 128 tiles on 8 waves: half the draws, 71.5 -> 44 us at
   // 40960 x 128 (profiles/r02h_gemm); for plain A the 128 x 128 variant and
-  // a global_load_lds 3-stage ring at one workgroup per CU measured slower.
+  // a global_load_lds 3-stage ring at one workgroup per CU measured slower,
+  // and so did 128 x 128 tiles for fp32 (layer 784->512: 74.6 vs 71.4 us,
+  // profiles/r02r_gemm_fp32).
   const int nN = (a.Np + 63) / 64;
   const int big = nN * ((a.rows_eff + 127) / 128);
   const int wide = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
