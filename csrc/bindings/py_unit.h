@@ -592,6 +592,8 @@ class PyUnit : public Unit {
     std::string rtext;
     bool ok = write_all(fd, &h, sizeof h) && (h.x_bytes == 0 || write_all(fd, x, h.x_bytes)) &&
               write_all(fd, text.data(), text.size()) && read_all(fd, &r, sizeof r) && r.magic == PoolFrame::kMagic;
+    // a reply frame must describe whole doubles and sane sizes (1 GiB each)
+    ok = ok && r.x_bytes % sizeof(double) == 0 && r.x_bytes <= (1ull << 30) && r.text_bytes <= (1ull << 30);
     if (ok) {
       y.resize(r.x_bytes / sizeof(double));
       rtext.resize(r.text_bytes);
