@@ -359,8 +359,12 @@ void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* w
     a.rows_eff = rows;
     return a;
   };
-  // encoder / plain stack: X -> x32 -> buf0 -> buf1 -> ...
-  kern::mlp_convert(X, rows, F_, int(K0), x32, s);
+  // encoder / plain stack: X -> x32 -> buf0 -> buf1 -> ...  A plain stack on
+  // the LDS-tiled GEMM reads X (fp64) straight into its first layer's staging
+  // (no convert pass; the VAE keeps x32 as its MSE reference) and writes the
+  // model output from its last layer's epilogue (no mlp_finish).
+  const bool direct_in = !vae_ && lds_layer(0, rows);
+  if (!direct_in) kern::mlp_convert(X, rows, F_, int(K0), x32, s);
   const float* cur = x32;
   int cur_ld = int(K0), flip = 0;
   for (int o = 0; o < prog_.n_pre; ++o) {
@@ -368,10 +372,15 @@ void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* w
     kern::MlpLayerArgs a = args(op);
     a.A = cur;
     a.lda = cur_ld;
-    const bool head_out = vae_ && o + 1 == prog_.n_pre;
-    a.O = head_out ? head : buf[flip];
+    const bool last = o + 1 == prog_.n_pre;
+    a.O = vae_ && last ? head : buf[flip];
     a.ldo = op.Np;
-    run_layer(a, o, s);
+    if (!vae_ && last && op.N <= 16 && lds_layer(o, rows) &&
+        (prog_.out_softmax == 2 ? op.N == 1 && prog_.out_dim == 2 : prog_.out_dim == op.N)) {
+      run_layer(a, o, s, o == 0 && direct_in ? X : nullptr, out);
+      return;
+    }
+    run_layer(a, o, s, o == 0 && direct_in ? X : nullptr);
     cur = a.O;
     cur_ld = op.Np;
     flip ^= 1;
@@ -417,14 +426,21 @@ void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* w
 
 // Large batches: the register-tiled GEMM (64 rows x up to 64 columns per
 // wave); small ones: one 16x16 tile per wave (more waves for the chip).
-void MlpModel::run_layer(const kern::MlpLayerArgs& a, int op, hipStream_t s) const {
+bool MlpModel::lds_layer(int op, int rows_eff) const {
+  return rows_eff >= kLdsGemmRows && wr_off_[size_t(op)] >= 0;
+}
+
+void MlpModel::run_layer(const kern::MlpLayerArgs& a, int op, hipStream_t s, const double* a64,
+                         double* out64) const {
+  if ((a64 || out64) && !lds_layer(op, a.rows_eff))
+    throw std::logic_error("MlpModel::run_layer: fp64 A / fp64 output need the LDS-tiled GEMM");
   if (a.rows_eff < kGemmRows) {
     kern::mlp_layer(a, s);
     return;
   }
   kern::DenseGemmArgs g;
   const long long wr = wr_off_[size_t(op)];
-  if (a.rows_eff >= kLdsGemmRows && !a.H && wr >= 0 && kq_[size_t(op)] <= a.lda && a.lda % 4 == 0) {
+  if (a.rows_eff >= kLdsGemmRows && !a.H && wr >= 0 && (a64 || (kq_[size_t(op)] <= a.lda && a.lda % 4 == 0))) {
     // A rows hold Kq floats (zeros past K), W row-major [Npb][Kq]: LDS-tiled exact-fp32 MFMA GEMM
     g.lds_f32 = 1;
     g.W = d_prm_.as<float>() + wr;
@@ -454,6 +470,15 @@ void MlpModel::run_layer(const kern::MlpLayerArgs& a, int op, hipStream_t s) con
   g.mse = a.mse;
   g.xref = a.xref;
   g.ldx = a.ldx;
+  if (a64) {  // fp64 rows [rows][K]: masked past K, converted to fp32 while staging
+    g.A = a64;
+    g.lda = F_;
+    g.a_f64 = 1;
+  }
+  if (out64) {
+    g.out64 = out64;
+    g.out_mode = prog_.out_softmax;
+  }
   kern::dense_gemm(g, s);
 }
 

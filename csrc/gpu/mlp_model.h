@@ -59,7 +59,11 @@ class MlpModel : public RowModel {
   void cpu_dense(const DenseLayer& L, const std::vector<float>& in, std::vector<float>& out, int rows) const;
   void launch_layerwise(const double* X, int rows, double* out, float* ws, uint64_t key, hipStream_t s);
   void launch_layerwise_bf16(const double* X, int rows, double* out, char* ws, uint64_t key, hipStream_t s);
-  void run_layer(const kern::MlpLayerArgs& a, int op, hipStream_t s) const;
+  // a64: fp64 request rows [rows][F] as A (converted while staging; LDS path only);
+  // out64: write the model output from the epilogue (LDS path, N <= 16)
+  void run_layer(const kern::MlpLayerArgs& a, int op, hipStream_t s, const double* a64 = nullptr,
+                 double* out64 = nullptr) const;
+  bool lds_layer(int op, int rows_eff) const;
   int max_np() const;
 
   std::vector<DenseLayer> enc_, dec_;  // plain: enc_ = all layers

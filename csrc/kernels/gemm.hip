@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernels.h"
 #include "philox.h"
@@ -21,6 +22,7 @@ namespace sca::kern {
 namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f64x2 = __attribute__((ext_vector_type(2))) double;
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 constexpr int kTM = 4;  // row tiles (of 16) per wave
 
@@ -212,6 +214,26 @@ __device__ __forceinline__ bf16x8 stage_a(const DenseGemmArgs& a, int row, int k
   }
 }
 
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+
+// AMODE 3: four fp64 request values (row `row`, [k, k + 4)) for one fp32
+// staging chunk, kept raw in the register ring and converted at the LDS store
+// (converting here would make the load wait at issue and drain the ring);
+// elements past K (the Kp padding) are zero.  Two 16-B loads when in range
+// and 16-B aligned (K even), else masked scalar loads.
+__device__ __forceinline__ f64x4 stage_a64(const DenseGemmArgs& a, int row, int k) {
+  row = min(row, a.rows_eff - 1);
+  const double* x = static_cast<const double*>(a.A) + size_t(row) * a.lda + k;
+  if (k + 3 < a.K && (a.lda & 1) == 0) {
+    const f64x2 lo = *reinterpret_cast<const f64x2*>(x), hi = *reinterpret_cast<const f64x2*>(x + 2);
+    return f64x4{lo[0], lo[1], hi[0], hi[1]};
+  }
+  f64x4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = k + j < a.K ? x[j] : 0.0;
+  return v;
+}
+
 // One 16-B chunk of the A panel (row `row`, elements [k, k + 16 / sizeof(T))).
 template <typename T, int AMODE>
 __device__ __forceinline__ u32x4 stage_a_chunk(const DenseGemmArgs& a, int row, int k) {
@@ -264,16 +286,19 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   const int KS = a.Kp / kBKe;
   // NS sets of staging registers; every set index below is a compile-time
   // constant (the K loop is unrolled by NS), so they stay in VGPRs
-  u32x4 ra[NS][CA], rw[NS][CW];
-  auto gload = [&](int ks, bool live, u32x4* ra, u32x4* rw) {
+  using RA = std::conditional_t<AMODE == 3, f64x4, u32x4>;  // A ring element (raw fp64 for AMODE 3)
+  RA ra[NS][CA];
+  u32x4 rw[NS][CW];
+  auto gload = [&](int ks, bool live, RA* ra, u32x4* rw) {
     // A computed on the fly (AMODE 2: reparameterised draws, no memory loads)
     // is skipped for the clamped stages past the end; loaded operands are not
     // (see the unconditional ring below)
-    if (AMODE == 0 || live) {
+    if (AMODE != 2 || live) {
 #pragma unroll
       for (int j = 0; j < CA; ++j) {
         const int c = tid + NT * j;
-        ra[j] = stage_a_chunk<T, AMODE>(a, m0 + (c >> 3), ks * kBKe + (c & 7) * kEl);
+        if constexpr (AMODE == 3) ra[j] = stage_a64(a, m0 + (c >> 3), ks * kBKe + (c & 7) * kEl);
+        else ra[j] = stage_a_chunk<T, AMODE>(a, m0 + (c >> 3), ks * kBKe + (c & 7) * kEl);
       }
     }
 #pragma unroll
@@ -283,13 +308,17 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
                                               (c & 7) * kEl);
     }
   };
-  auto lstore = [&](int buf, const u32x4* ra, const u32x4* rw) {
+  auto lstore = [&](int buf, const RA* ra, const u32x4* rw) {
     T* As = smem + buf * kBuf;
     T* Ws = As + BM * kLdr;
 #pragma unroll
     for (int j = 0; j < CA; ++j) {
       const int c = tid + NT * j;
-      *reinterpret_cast<u32x4*>(As + sw(c >> 3, c & 7)) = ra[j];
+      if constexpr (AMODE == 3)
+        *reinterpret_cast<f32x4*>(As + sw(c >> 3, c & 7)) =
+            f32x4{float(ra[j][0]), float(ra[j][1]), float(ra[j][2]), float(ra[j][3])};
+      else
+        *reinterpret_cast<u32x4*>(As + sw(c >> 3, c & 7)) = ra[j];
     }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
@@ -465,7 +494,7 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
 __global__ void convert_bf16_kernel(const double* __restrict__ X, int rows, int F, int ld, __bf16* __restrict__ out) {
   const int half = ld >> 1;  // ld is even (a multiple of 64)
   const size_t n = size_t(rows) * half;
-  using f64x2 = __attribute__((ext_vector_type(2))) double;
+
   using bf16x2 = __attribute__((ext_vector_type(2))) __bf16;
   const bool vec = (F & 1) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
   for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
@@ -513,7 +542,8 @@ void dense_gemm(const DenseGemmArgs& a, hipStream_t s) {
   } else if (a.lds_f32 && !a.H) {  // large fp32 layer: LDS-tiled exact-fp32 MFMA GEMM
     DenseGemmArgs b = a;
     b.xcd_remap = 1;
-    launch_lds<float, 0>(b, s);
+    if (b.a_f64) launch_lds<float, 3>(b, s);
+    else launch_lds<float, 0>(b, s);
   } else {
     if (a.H) launch_tn<0, 2>(a, s);
     else launch_tn<0, 0>(a, s);

@@ -271,3 +271,38 @@ def test_mlp_bf16_binary_output_fused_epilogue(rows):
     assert got.shape == (rows, 2)
     np.testing.assert_allclose(got[:, 1], p, atol=2e-2)
     np.testing.assert_allclose(got[:, 0] + got[:, 1], 1.0, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,out_mode", [((784, 512, 256, 10), 1), ((13, 37, 19, 3), 0), ((50, 64, 1), 2),
+                                           ((31, 33), 1), ((30, 7), 0), ((37, 40, 20), 1)])
+def test_mlp_lds_gemm_fp64_input_and_fused_output(dims, out_mode, monkeypatch):
+    """LDS-tiled fp32 layer-wise path (>= 2048 rows): the first layer stages the
+    fp64 request rows itself (odd widths take the masked scalar loads) and a
+    last layer with N <= 16 writes the softmax / plain / binary output from its
+    epilogue; wider heads (N = 33, 20) keep the fp32 logits + finish kernel."""
+    import torch
+
+    monkeypatch.setenv("SCA_MLP_MODE", "layer")
+    acts = ["relu"] * (len(dims) - 2) + ["sigmoid" if out_mode == 2 else "identity"]
+    layers = random_dense_stack(list(dims), acts, seed=len(dims) + dims[0])
+    X = np.random.default_rng(dims[0]).normal(size=(4096 + 37, dims[0]))
+    unit = sca.native().BatchedUnit(mlp_row_model(layers, out_mode), 0, max_batch=8192)
+    try:
+        got = np.asarray(unit.run(X))
+    finally:
+        unit.stop()
+    x = torch.tensor(X, dtype=torch.float32)
+    for L in layers:
+        x = x @ torch.tensor(L["W"]).T + torch.tensor(L["b"])
+        if L["act"] == 1:
+            x = torch.relu(x)
+        elif L["act"] == 2:
+            x = torch.sigmoid(x)
+    if out_mode == 1:
+        x = torch.softmax(x, 1)
+    elif out_mode == 2:
+        x = torch.cat([1 - x, x], 1)
+    ref = x.double().numpy()
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5)

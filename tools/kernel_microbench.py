@@ -254,8 +254,10 @@ def _torch_time(fn, iters):
     return e0.elapsed_time(e1) * 1000 / iters
 
 
-def case_mlp_torch(iters, rows_list=(8192, 64)):
-    """Same MLP in PyTorch eager fp32 (hipBLASLt GEMMs + elementwise), input already fp32 on device."""
+def case_mlp_torch(iters, rows_list=(8192, 64), fp64_io=False):
+    """Same MLP in PyTorch eager fp32 (hipBLASLt GEMMs + elementwise), input already fp32 on device.
+    fp64_io: the serving contract of our kernels -- fp64 rows in, fp64 probabilities out (the
+    fp64 -> fp32 cast and the fp64 output are part of the timed work, as in mlp_kernel)."""
     import torch
 
     from seldon_core_amd.models.mlp import random_dense_stack
@@ -264,19 +266,21 @@ def case_mlp_torch(iters, rows_list=(8192, 64)):
     Ws = [torch.tensor(L["W"], device="cuda") for L in layers]
     bs = [torch.tensor(L["b"], device="cuda") for L in layers]
     for rows in rows_list:
-        x = torch.randn(rows, MLP_DIMS[0], device="cuda")
+        x = torch.randn(rows, MLP_DIMS[0], device="cuda", dtype=torch.float64 if fp64_io else torch.float32)
 
         def fwd():
-            h = x
+            h = x.float() if fp64_io else x
             for i, (W, b) in enumerate(zip(Ws, bs)):
                 h = torch.nn.functional.linear(h, W, b)
                 if i + 1 < len(Ws):
                     h = torch.relu(h)
-            return torch.softmax(h, 1)
+            out = torch.softmax(h, 1)
+            return out.double() if fp64_io else out
 
         us = _torch_time(fwd, iters)
         flops = 2 * rows * sum(a * b for a, b in zip(MLP_DIMS[:-1], MLP_DIMS[1:]))
-        print(json.dumps({"case": "mlp_torch_fp32", "rows": rows, "us_per_run": round(us, 2),
+        print(json.dumps({"case": "mlp_torch_fp32" + ("_fp64io" if fp64_io else ""), "rows": rows,
+                          "us_per_run": round(us, 2),
                           "tflops": round(flops / (us * 1e-6) / 1e12, 2)}), flush=True)
 
 
@@ -392,7 +396,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     cases = {"tree": case_tree, "vae": case_vae, "mlp": case_mlp, "linear": case_linear,
-             "mlp_torch": case_mlp_torch, "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes,
+             "mlp_torch": case_mlp_torch,
+             "mlp_torch_fp64io": lambda it: case_mlp_torch(it, fp64_io=True), "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes,
              "lstm": case_lstm, "latency": case_latency, "dense_prec": case_dense_prec, "mlp_torch_bf16": case_mlp_torch_bf16}
     for c in a.only.split(","):
         cases[c](a.iters)
