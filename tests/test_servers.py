@@ -91,6 +91,10 @@ def test_rest_multipart(engine_server):
 
 def test_feedback_and_prometheus(engine_server):
     _, h = engine_server
+    # one prediction of its own: the predictions series must not depend on
+    # which other tests of this module ran first on this worker
+    st, _ = http(h.http_port, "/api/v0.1/predictions", json.dumps({"data": {"ndarray": [[1.0]]}}).encode())
+    assert st == 200
     st, body = http(h.http_port, "/api/v0.1/feedback", json.dumps({"reward": 1.0, "request": {"data": {"ndarray": [[1]]}}}).encode())
     assert (st, body) == (200, "{}")
     st, text = http(h.http_port, "/prometheus")
