@@ -145,14 +145,16 @@ def cpu_budget() -> float:
 
 def size_threads(args, per_rank: float) -> float:
     """Split the CPU share of one rank between the front end (~60%), the
-    closed-loop load generator (~32%) and the GPU device thread (measured on
-    a 16-CPU MI355X share: 10 front-end / 5 generator threads was the best
-    split unpinned, profiles/r01f_sweep_executor)."""
+    closed-loop load generator (~25%) and the GPU device / hand-off threads
+    (measured on a 16-CPU MI355X share: 10 front-end / 5 generator threads
+    was the best split unpinned, profiles/r01f_sweep_executor; pinned to one
+    CCD, 10 / 4 serves 1.44M vs 1.38M REST pred/s with p99 0.29-0.35 vs
+    0.46-1.08 ms, and gRPC 2.10M vs 1.99M, profiles/r02v_threads)."""
     per_rank = max(2.0, per_rank)
     if args.server_threads is None:
         args.server_threads = max(1, min(16, int(round(per_rank * 0.6))))
     if args.client_threads is None:
-        args.client_threads = max(1, min(10, int(round(per_rank * 0.32))))
+        args.client_threads = max(1, min(10, int(round(per_rank * 0.25))))
     return per_rank
 
 
