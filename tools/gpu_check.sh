@@ -26,7 +26,7 @@ run() {  # name timeout cmd...
 rocm-smi --showproductname > "$OUT/rocm_smi.log" 2>&1 || true
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 180 python __graft_entry__.py smoke ;;
     bench) run bench 400 python bench.py --extra-grpc ;;
     bench_grpc) run bench_grpc 400 python bench.py --api grpc ;;
