@@ -6,54 +6,77 @@ Reference numbers (doc/source/reference/benchmarking.md:31-64):
 REST 12,088.95 req/s (p50 4 ms, p99 69 ms), gRPC 28,256.39 req/s (p50 1 ms,
 p99 6 ms), 256 locust users, one engine replica.
 
-Here: one process per GPU (torch.distributed over RCCL for the job-level
-barrier / result gather).  Each rank serves one replica of the graph -- the
-reference's sklearn-iris LogisticRegression model (BASELINE config
-1) executed by the GPU micro-batcher + linear_softmax HIP kernel on its GPU --
+Headline: one process per GPU.  Each rank serves one replica of the graph --
+the reference's sklearn-iris LogisticRegression model (BASELINE config 1)
+executed by the GPU micro-batcher + linear_softmax HIP kernel on its GPU --
 through the native HTTP/1.1 front end, and drives it with the native
 closed-loop load generator (256 concurrent users per rank, no think time, the
-locust REST payload shape).  Weak scaling: per-GPU load is fixed as N grows.
+locust REST payload shape, a sampled reply-body check).  Weak scaling: per-GPU
+load is fixed as N grows.  A "step" is ``--step-requests`` completed
+predictions per rank (default: calibrated so the K timed steps last >= 5 s);
+W warmup steps run untimed; K steps are timed between a barrier + device
+synchronize on both sides; ms_per_step is the max over ranks; ``value`` is
+the whole-job predictions/s.
 
-Launch: ``python bench.py --gpus N`` spawns N rank processes itself (fresh
-processes, before anything touches a GPU); under ``torch.distributed.run`` the
-ranks come from the environment and ``--gpus`` must equal ``WORLD_SIZE``.
+After the headline (never inside it):
 
-A "step" is ``--step-requests`` completed predictions per rank.  W warmup steps
-run untimed; K steps are timed between a barrier + device synchronize on both
-sides; ms_per_step is the max over ranks; ``value`` is the whole-job
-predictions/s.
+* every rank checks sampled replies against a CPU oracle (scikit-learn for
+  iris, the host tree walker for xgboost) and measures the gRPC API;
+* with N >= 2, rank 0 measures BASELINE.json's multi-GPU graphs as ONE graph
+  over the node's GPUs, each in a child process with its own deadline:
+  ``abtest`` (RANDOM_ABTEST over replicas on 2 GPUs), ``pipeline``
+  (transformer -> combiner over 2 models, 4 GPUs), ``mab`` (epsilon-greedy
+  over one replica per GPU, with concurrent feedback traffic) and
+  ``replicas`` (one endpoint over a replica per GPU);
+* then every rank starts a fabric child: the same graphs with their nodes
+  placed on ranks (``abtest_rccl``, ``pipeline_rccl``, ``mab_rccl``), batches
+  travelling between the rank processes as RCCL send/recv over xGMI.
 
-After the timed headline (never inside it) every rank:
+Robustness: the whole run has one budget (``BUDGET_S``); every child and load
+generator call gets a timeout from what is left; ranks hand results to rank 0
+through files (no collective after the headline); a rank-0 watchdog prints
+the JSON line when the budget runs out, marking what did not finish as
+``"timeout"``, and kills every child process group.
 
-* checks a sample of responses, sent through the same front end, against a CPU
-  oracle (scikit-learn for iris, the host tree walker for xgboost) and exits
-  non-zero on a mismatch;
-* measures the gRPC API (``seldon.protos.Seldon/Predict``, Tensor payload);
-* with N >= 2, measures BASELINE.json's multi-GPU graph configs with their
-  nodes placed on distinct GPUs of the rank's GPU group: ``abtest`` (RANDOM_ABTEST
-  over 2 model replicas on 2 GPUs), ``pipeline`` (transformer -> combiner over 2
-  models, 4 GPUs, N >= 4) and ``mab`` (epsilon-greedy router over one replica per
-  GPU of the job, with concurrent feedback traffic so the bandit learns), each
-  self-checked the same way and reporting its per-GPU batch counts.
+Launch: ``python bench.py --gpus N`` spawns N rank processes itself; under
+``torch.distributed.run`` the ranks come from the environment and ``--gpus``
+must equal ``WORLD_SIZE``.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import socket
+import shutil
 import subprocess
 import sys
+import tempfile
 import threading
 import time
-import urllib.request
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from seldon_core_amd.utils import benchkit as bk  # noqa: E402  (no GPU, no torch import)
+
 REST_BASELINE = 12088.95
 GRPC_BASELINE = 28256.39
-VARIANT_SPAN = {"abtest": 2, "pipeline": 4}  # GPUs a variant's graph spans (mab: all of the job's)
+BUDGET_S = float(os.environ.get("SCA_BENCH_BUDGET_S", "420"))  # whole run, well under the driver's 600 s lease
+VARIANT_CAP_S = float(os.environ.get("SCA_BENCH_VARIANT_CAP_S", "75"))  # one in-process variant child
+TARGET_TIMED_S = 5.0  # headline timed region when --step-requests is calibrated
+EXTRA_WINDOW_S = 1.2  # gRPC / variant timed windows
+REPORT_RESERVE_S = 8.0  # rank 0 keeps this much of the budget to write the line
+HEAD_RESERVE_S = min(45.0, 0.25 * BUDGET_S)  # left for the report + extras when the headline starts a step
+FABRIC_RESERVE_S = min(75.0, 0.3 * BUDGET_S)
+EXTRA_RESERVE_S = min(30.0, 0.15 * BUDGET_S)  # left when the gRPC extra starts  # kept for the rank-placed (RCCL) phase while in-process variants run
+T_START = time.time()
+try:
+    ORIG_AFFINITY = sorted(os.sched_getaffinity(0))
+except AttributeError:
+    ORIG_AFFINITY = []
+VARIANTS = ("abtest", "pipeline", "mab", "replicas")
+RANK_VARIANTS = ("abtest", "pipeline", "mab")
+SPAN = {"abtest": 2, "pipeline": 4}  # GPUs a graph spans (mab / replicas: all of the job's)
 
 
 def parse_args(argv=None):
@@ -69,31 +92,55 @@ def parse_args(argv=None):
                     help="python-* models: stack concurrent requests up to this many rows (0 = off)")
     ap.add_argument("--py-workers", type=int, default=0, help="python-* models: worker processes (0 = in-process)")
     ap.add_argument("--users", type=int, default=256, help="concurrent clients per GPU")
-    ap.add_argument("--step-requests", type=int, default=40000, help="predictions per step per GPU")
+    ap.add_argument("--step-requests", type=int, default=None,
+                    help="predictions per step per GPU (default: calibrated so the timed steps last >= 5 s)")
     ap.add_argument("--server-threads", type=int, default=None, help="default: sized from the CPU quota per rank")
     ap.add_argument("--client-threads", type=int, default=None, help="default: sized from the CPU quota per rank")
     ap.add_argument("--slots", type=int, default=4, help="GPU batches in flight per unit")
     ap.add_argument("--no-spin", action="store_true", help="block on events instead of spinning")
-    ap.add_argument("--graph", choices=["single", "abtest", "pipeline", "mab"], default="single",
+    ap.add_argument("--graph", choices=["single", "abtest", "pipeline", "mab", "replicas"], default="single",
                     help="graph of the timed region (single = the headline single-model graph)")
     ap.add_argument("--extras", choices=["auto", "none"], default="auto",
                     help="after the timed region: gRPC + multi-GPU graph variants (auto) or nothing")
-    ap.add_argument("--extra-steps", type=int, default=2, help="steps per extra measurement")
+    ap.add_argument("--variants", default=",".join(VARIANTS), help="in-process variants to run (N >= 2)")
+    ap.add_argument("--rank-variants", default=",".join(RANK_VARIANTS),
+                    help="rank-placed (RCCL fabric) variants to run (N >= 2); empty = none")
     ap.add_argument("--cpu-profile", default=None,
                     help="write a sampling CPU profile of the serving process over the timed window to this JSON file")
     ap.add_argument("--cpu-profile-depth", type=int, default=1, help="frames per CPU-profile sample (>1: call paths)")
-    ap.add_argument("--variants-child", default=None, help=argparse.SUPPRESS)  # internal: isolated variant runner
     ap.add_argument("--pin", choices=["auto", "none"], default="auto",
                     help="pin each rank (front end, device thread, load generator) to whole CCDs local to its GPU")
-    ap.add_argument("--fabric-probe", choices=["auto", "none"], default="auto",
-                    help="N >= 2: after everything else, run tools/fabric_probe.py in child processes "
-                         "(rank-placed graph nodes over the RCCL p2p fabric) under a time limit")
-    ap.add_argument("--extra-grpc", action="store_true", help="(kept for old command lines; gRPC is an auto extra)")
-    return ap.parse_args(argv)
+    # kept for old command lines
+    ap.add_argument("--extra-grpc", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--extra-steps", type=int, default=2, help=argparse.SUPPRESS)
+    ap.add_argument("--fabric-probe", choices=["auto", "none"], default="auto", help=argparse.SUPPRESS)
+    # internal: child processes
+    ap.add_argument("--variant-child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--fabric-child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--span", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--deadline", type=float, default=None, help=argparse.SUPPRESS)
+    args = ap.parse_args(argv)
+    if args.fabric_probe == "none":
+        args.rank_variants = ""
+    return args
+
+
+def fault(kind: str, rank: int) -> None:
+    """Fault injection for tests: SCA_BENCH_FAULT is a comma list of
+    "<kind>:<rank>" (setup error) or "hang:<kind>:<rank>" (sleep forever at
+    that point)."""
+    faults = os.environ.get("SCA_BENCH_FAULT", "").split(",")
+    if f"{kind}:{rank}" in faults:
+        raise RuntimeError(f"injected {kind} setup fault")
+    if f"hang:{kind}:{rank}" in faults:
+        while True:
+            time.sleep(3600)
 
 
 # ------------------------------------------------------------------ launch
 def _free_port() -> int:
+    import socket
+
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
@@ -101,48 +148,30 @@ def _free_port() -> int:
 
 def spawn_ranks(n: int, argv) -> int:
     """Direct launch with --gpus N: start N fresh rank processes (no GPU has
-    been touched in this one) and exit with the first failing rank's code."""
+    been touched in this one), all sharing one deadline; exit with rank 0's
+    code (rank 0 reports every other rank's failures in its line).  A rank
+    still running past the deadline is killed."""
     port = _free_port()
+    deadline = T_START + BUDGET_S
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
-    rc = 0
-    pending = set(range(n))
-    while pending:
-        for r in list(pending):
-            code = procs[r].poll()
-            if code is None:
-                continue
-            pending.discard(r)
-            if code != 0 and rc == 0:
-                rc = code
-                for q in pending:  # a failed rank would leave the others in a collective
-                    procs[q].terminate()
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SCA_BENCH_DEADLINE=str(deadline))
+        procs.append(bk.CHILDREN.popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                       stdout=None if r == 0 else subprocess.DEVNULL))
+    while any(p.poll() is None for p in procs) and time.time() < deadline + 20:
+        if procs[0].poll() is not None and procs[0].returncode != 0:
+            break  # rank 0 failed: the others would wait for it
         time.sleep(0.05)
-    return rc
+    for p in procs:
+        if p.poll() is None:
+            bk.Children.kill(p)
+            p.wait()
+    rc0 = procs[0].returncode
+    return 124 if rc0 is None or rc0 < 0 else rc0
 
 
 # ------------------------------------------------------------------ sizing
-def cpu_budget() -> float:
-    """CPUs this process may use: the smaller of the cgroup v2 quota (cpu.max)
-    and the CPU affinity mask."""
-    limits = []
-    try:
-        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if quota != "max":
-            limits.append(float(quota) / float(period))
-    except (OSError, ValueError):
-        pass
-    try:
-        limits.append(float(len(os.sched_getaffinity(0))))
-    except AttributeError:
-        limits.append(float(os.cpu_count() or 8))
-    return min(limits)
-
-
 def size_threads(args, per_rank: float) -> float:
     """Split the CPU share of one rank between the front end (~60%), the
     closed-loop load generator (~25%) and the GPU device / hand-off threads
@@ -162,7 +191,7 @@ def place_rank(args, d) -> tuple:
     """(per-rank CPU budget, pinned CPUs): with --pin auto each rank is pinned
     to whole CCDs local to its GPU (seldon_core_amd.utils.topology), so its
     front end, device thread and load generator share one L3."""
-    per_rank = cpu_budget() / max(1, d.local_world)
+    per_rank = bk.cpu_budget() / max(1, d.local_world)
     if args.pin != "auto" or not d.has_gpu:
         return per_rank, []
     from seldon_core_amd.utils import topology
@@ -175,216 +204,9 @@ def place_rank(args, d) -> tuple:
     return per_rank, cpus
 
 
-def cpu_ranges(cpus) -> str:
-    out, i = [], 0
-    cpus = sorted(cpus)
-    while i < len(cpus):
-        j = i
-        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
-            j += 1
-        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
-        i = j + 1
-    return ",".join(out)
-
-
-# ------------------------------------------------------------------ graphs
-class Workload:
-    """The benchmark model: component, payload row, names and a CPU oracle."""
-
-    def __init__(self, model: str):
-        from seldon_core_amd.servers import SKLearnServer, XGBoostServer
-
-        self.model = model
-        if model == "iris":
-            from seldon_core_amd.models import iris_logistic_regression
-
-            self.clf = iris_logistic_regression()
-            self.comp = SKLearnServer(model=self.clf)
-            self.names = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
-            self.row = [5.1, 3.5, 1.4, 0.2]
-            self.label = "sklearn-iris-LogisticRegression (linear_softmax HIP kernel, fp64)"
-            self.impl = "SKLEARN_SERVER"
-        elif model in ("python-iris", "python-noop"):
-            from seldon_core_amd.components.examples import EchoModel, IrisClassifier
-
-            self.names = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
-            self.row = [5.1, 3.5, 1.4, 0.2]
-            if model == "python-iris":
-                self.comp = IrisClassifier()
-                self.clf = self.comp.model
-                self.label = "user Python class IrisClassifier (sklearn LogisticRegression.predict_proba)"
-            else:
-                self.comp = EchoModel()
-                self.label = "user Python class EchoModel (no-op predict)"
-            self.impl = None
-        else:
-            from seldon_core_amd.models import synthetic_xgboost
-
-            self.ens = synthetic_xgboost(1000, 8, 32, seed=0)
-            self.comp = XGBoostServer(ensemble=self.ens)
-            self.names = [f"f{i}" for i in range(32)]
-            self.row = [0.1 * ((i * 7) % 13 - 6) for i in range(32)]
-            self.label = "xgboost-1000trees-depth8 regressor (tree_perfect HIP kernel, random-init)"
-            self.impl = "XGBOOST_SERVER"
-
-    def oracle(self, X):
-        import numpy as np
-
-        if self.model in ("iris", "python-iris"):
-            return self.clf.predict_proba(X)
-        if self.model == "python-noop":
-            return np.asarray(X, dtype=np.float64)
-        return np.asarray(self.ens.predict(X), dtype=np.float64).reshape(len(X), -1)
-
-    def sample(self, n: int, seed: int):
-        import numpy as np
-
-        rng = np.random.default_rng(seed)
-        base = np.asarray(self.row)
-        return base + rng.normal(scale=0.5, size=(n, len(base)))
-
-
-def group_devices(rank: int, span: int, ngpu: int):
-    """GPUs of a variant graph on `rank`: the rank's group of `span` GPUs,
-    rotated so the graph's first node sits on the rank's own GPU."""
-    if ngpu <= 0:
-        return [-1] * span
-    base = (rank // span) * span
-    return [(base + (rank + i) % span) % ngpu for i in range(span)]
-
-
-def build_graph(wl: Workload, kind: str, devs):
-    """SeldonDeployment graph + components for one graph kind on devices `devs`."""
-    import numpy as np
-
-    import seldon_core_amd as sca
-    from seldon_core_amd.models import to_row_model
-
-    if kind == "single":
-        g = {"name": "classifier", "type": "MODEL", "children": [], "device": devs[0]}
-        if wl.impl:
-            g.update(implementation=wl.impl, modelUri="memory://bench")
-        else:  # a user Python class
-            g.update(batching=wl.py_batching, workers=wl.py_workers)
-        label = wl.label
-        if not wl.impl:
-            label += f" [batching={wl.py_batching}, workers={wl.py_workers}]"
-        return g, {"classifier": wl.comp}, wl.oracle, label
-    C = sca.native()
-    rm_a = wl.comp.row_model() if hasattr(wl.comp, "row_model") else to_row_model(wl.comp)
-    if kind == "abtest":  # seldon-abtest: RANDOM_ABTEST router over 2 model replicas on 2 GPUs
-        g = {"name": "ab", "type": "ROUTER", "implementation": "RANDOM_ABTEST", "device": devs[0],
-             "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
-             "children": [{"name": "a", "type": "MODEL", "device": devs[0]},
-                          {"name": "b", "type": "MODEL", "device": devs[1]}]}
-        return g, {"a": rm_a, "b": rm_a.clone()}, wl.oracle, f"RANDOM_ABTEST(2 replicas on GPUs {devs[:2]})"
-    if kind == "pipeline":  # transformer -> combiner over 2 models, one stage per GPU (device graph)
-        F = len(wl.row)
-        scale = 1.0 + 0.01 * np.random.default_rng(0).random(F)
-        tr = C.linear_model(np.diag(scale), np.zeros(F), 0)  # standard-scaler-style affine transform
-        g = {"name": "scaler", "type": "TRANSFORMER", "device": devs[0], "children": [
-            {"name": "combiner", "type": "COMBINER", "implementation": "AVERAGE_COMBINER", "device": devs[3],
-             "children": [{"name": "a", "type": "MODEL", "device": devs[1]},
-                          {"name": "b", "type": "MODEL", "device": devs[2]}]}]}
-        return (g, {"scaler": tr, "a": rm_a, "b": rm_a.clone()}, lambda X: wl.oracle(np.asarray(X) * scale),
-                f"TRANSFORMER->COMBINER(2 models) device graph on GPUs {devs[:4]}")
-    if kind == "mab":  # epsilon-greedy router over one model replica per GPU
-        from seldon_core_amd.components.routers import EpsilonGreedy
-
-        n = len(devs)
-        kids = [{"name": f"m{i}", "type": "MODEL", "device": devs[i]} for i in range(n)]
-        comps = {f"m{i}": (rm_a if i == 0 else rm_a.clone()) for i in range(n)}
-        comps["mab"] = EpsilonGreedy(n_branches=n, epsilon=0.1, seed=1)
-        g = {"name": "mab", "type": "ROUTER", "device": devs[0], "children": kids}
-        return g, comps, wl.oracle, f"EPSILON_GREEDY router over {n} replicas on GPUs {devs}"
-    raise ValueError(kind)
-
-
-def make_deployment(wl: Workload, kind: str, devs, device: int, slots: int, spin: bool):
-    import seldon_core_amd as sca
-
-    graph, comps, oracle, label = build_graph(wl, kind, devs)
-    spec = {"apiVersion": "machinelearning.seldon.io/v1alpha2", "kind": "SeldonDeployment",
-            "metadata": {"name": "bench"},
-            "spec": {"name": "bench", "predictors": [{
-                "name": "default", "replicas": 1, "componentSpecs": [{"spec": {"containers": []}}],
-                "graph": graph}]}}
-    dep = sca.Deployment(spec, components=comps, device=device,
-                         batcher={"max_batch": 4096, "slots": slots, "spin_wait": spin})
-    return dep, oracle, label
-
-
-# ------------------------------------------------------------------ load
-def run_loadgen(args, port: int, steps: int, warmup: int, api: str, body, path: str = "/api/v0.1/predictions",
-                users: int | None = None, step_requests: int | None = None, threads: int | None = None) -> dict:
-    lg = os.path.join(ROOT, "seldon_core_amd", "bin", "sca_loadgen")
-    cmd = [lg, "--host", "127.0.0.1", "--port", str(port), "--users", str(users or args.users),
-           "--threads", str(threads or args.client_threads), "--steps", str(steps), "--warmup", str(warmup),
-           "--step-requests", str(step_requests or args.step_requests)]
-    if api == "rest":
-        cmd += ["--mode", "rest", "--path", path, "--body", body]
-    else:
-        bpath = f"/tmp/sca_bench_req_{os.getpid()}.pb"
-        with open(bpath, "wb") as f:
-            f.write(body)
-        cmd += ["--mode", "grpc", "--path", "/seldon.protos.Seldon/Predict", "--body-file", bpath,
-                "--streams-per-conn", "8"]
-    res = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
-    if res.returncode not in (0, 1) or not res.stdout.strip():
-        raise RuntimeError(f"loadgen failed rc={res.returncode}: {res.stderr[-2000:]}")
-    out = json.loads(res.stdout.strip().splitlines()[-1])
-    if out["errors"]:
-        raise RuntimeError(f"loadgen saw {out['errors']} failed requests")
-    return out
-
-
-def self_check(port: int, wl: Workload, oracle, seed: int, n: int = 24) -> dict:
-    """Send distinct rows through the REST front end (one-row requests and one
-    batch) and compare with the CPU oracle."""
-    import numpy as np
-
-    X = wl.sample(n, seed)
-    got = []
-
-    def post(rows):
-        body = json.dumps({"data": {"names": wl.names, "ndarray": rows.tolist()}}).encode()
-        req = urllib.request.Request(f"http://127.0.0.1:{port}/api/v0.1/predictions", data=body,
-                                     headers={"Content-Type": "application/json"})
-        with urllib.request.urlopen(req, timeout=30) as r:
-            out = np.asarray(json.loads(r.read())["data"]["ndarray"], dtype=np.float64)
-            return out.reshape(len(rows), -1)  # regressors answer one flat value per row
-
-    for i in range(n // 2):
-        got.append(post(X[i:i + 1]))
-    got.append(post(X[n // 2:]))
-    got = np.vstack(got)
-    ref = np.asarray(oracle(X), dtype=np.float64).reshape(got.shape)
-    err = float(np.abs(got - ref).max())
-    tol = 1e-4 * max(1.0, float(np.abs(ref).max())) if wl.model == "xgb1000" else 1e-9
-    return {"rows": n, "max_abs_err": err, "tol": tol, "ok": bool(err <= tol)}
-
-
-def unit_stats(dep) -> dict:
-    per_dev: dict = {}
-    total = {"batches": 0, "rows": 0, "gpu_busy_s": 0.0, "launch_cpu_s": 0.0, "complete_cpu_s": 0.0}
-    for name, st in dep.batcher_stats().items():
-        if not isinstance(st, dict):
-            continue
-        for k in total:
-            total[k] += st.get(k, 0)
-        entries = st.get("per_device") or [{"device": st.get("device", -1), "batches": st.get("batches", 0),
-                                            "rows": st.get("rows", 0)}]
-        for e in entries:
-            d = per_dev.setdefault(str(e["device"]), {"batches": 0, "rows": 0, "units": []})
-            d["batches"] += e["batches"]
-            d["rows"] += e["rows"]
-            d["units"].append(name)
-    total["per_device"] = per_dev
-    return total
-
-
+# ------------------------------------------------------------------ ranks
 class Dist:
-    def __init__(self, backend: str | None = None):
+    def __init__(self, budget: bk.Budget, backend: str | None = None):
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -394,13 +216,17 @@ class Dist:
         self.torch = torch
         self.has_gpu = torch.cuda.is_available()
         self.dist = None
+        self.backend = None
         if self.world > 1:
+            import datetime
+
             import torch.distributed as dist
 
             if self.has_gpu:
                 torch.cuda.set_device(self.local_rank)
             self.backend = backend or ("nccl" if self.has_gpu else "gloo")
-            dist.init_process_group(backend=self.backend)
+            dist.init_process_group(backend=self.backend,
+                                    timeout=datetime.timedelta(seconds=max(30.0, budget.left())))
             self.dist = dist
         self.device = self.local_rank if self.has_gpu else -1
 
@@ -422,9 +248,12 @@ class Dist:
         self.dist.all_gather_object(out, obj)
         return out
 
-    def close(self):
-        if self.dist is not None:
-            self.dist.destroy_process_group()
+    def bcast(self, obj):
+        if self.dist is None:
+            return obj
+        box = [obj if self.rank == 0 else None]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
 
 
 def cpu_seconds() -> tuple:
@@ -437,89 +266,7 @@ def cpu_seconds() -> tuple:
     return me.ru_utime + me.ru_stime, ch.ru_utime + ch.ru_stime
 
 
-def timed(d: Dist, fn, cpu: dict | None = None):
-    d.barrier()
-    d.sync()
-    c0 = cpu_seconds()
-    t0 = time.perf_counter()
-    err = None
-    try:
-        out = fn()
-    except Exception as e:  # still meet the closing barrier, or the other ranks would wait forever
-        out, err = None, e
-    d.sync()
-    wall = time.perf_counter() - t0
-    if cpu is not None:  # CPUs busy over the window, server side vs load generator
-        c1 = cpu_seconds()
-        cpu["server_cpus"] = round((c1[0] - c0[0]) / wall, 2)
-        cpu["loadgen_cpus"] = round((c1[1] - c0[1]) / wall, 2)
-    d.barrier()
-    if err is not None:
-        raise err
-    return out, wall
-
-
-def measure_variant(args, d: Dist, wl: Workload, kind: str, spin: bool) -> dict:
-    """One multi-GPU graph config, untimed by the driver contract but timed the
-    same way (barrier + sync around the loadgen window, max over ranks)."""
-    import seldon_core_amd as sca
-
-    ngpu = sca.gpu_count() if d.has_gpu else 0
-    span = max(2, d.world) if kind == "mab" else VARIANT_SPAN[kind]
-    devs = group_devices(d.rank, span, ngpu)
-    body = json.dumps({"data": {"names": wl.names, "ndarray": [wl.row]}})
-    sreq = max(1000, args.step_requests // 2)
-    dep = h = None
-    setup_error = None
-    try:  # everything rank-local first: a rank that fails here must not skip a collective alone
-        if os.environ.get("SCA_BENCH_FAULT") == f"{kind}:{d.rank}":  # fault injection (tests)
-            raise RuntimeError(f"injected {kind} setup fault")
-        dep, oracle, label = make_deployment(wl, kind, devs, d.device, args.slots, spin)
-        h = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
-        run_loadgen(args, h.http_port, 1, 0, "rest", body, step_requests=sreq)  # warm every replica
-    except Exception as e:
-        setup_error = f"rank {d.rank}: {type(e).__name__}: {e}"[:400]
-    errors = [e for e in d.gather(setup_error) if e]
-    fb = None
-    try:
-        if errors:  # every rank skips the variant together
-            raise RuntimeError("; ".join(errors))
-        for u in dep.batched.values():
-            u.reset_stats()
-        fb_out = {}
-        if kind == "mab":
-            # feedback traffic next to the predictions (reference MAB loadtest:
-            # util/loadtester/scripts/predict_rest_locust.py sends feedback):
-            # branch 0 is rewarded, so the bandit must keep routing to it.
-            fbody = json.dumps({"request": {"data": {"names": wl.names, "ndarray": [wl.row]}},
-                                "response": {"meta": {"routing": {"mab": 0}}, "data": {"ndarray": [[0.0]]}},
-                                "reward": 1.0})
-            fb = threading.Thread(target=lambda: fb_out.update(run_loadgen(
-                args, h.http_port, args.extra_steps, 0, "rest", fbody, path="/api/v0.1/feedback",
-                users=max(4, args.users // 16), step_requests=max(200, sreq // 16),
-                threads=max(1, args.client_threads // 4))))
-            fb.start()
-        lg, wall = timed(d, lambda: run_loadgen(args, h.http_port, args.extra_steps, 0, "rest", body,
-                                                step_requests=sreq))
-        if fb is not None:
-            fb.join()
-        check = self_check(h.http_port, wl, oracle, seed=100 + d.rank)
-        st = unit_stats(dep)
-        res = {"ok": lg["ok"], "wall": wall, "p50": lg["p50_ms"], "p99": lg["p99_ms"], "check": check,
-               "devices": devs, "label": label, "stats": st}
-        if fb_out:
-            res["feedback_rps"] = fb_out.get("rps")
-            routed = {k: v["rows"] for k, v in st["per_device"].items()}
-            res["rows_per_device"] = routed
-        return res
-    finally:
-        if h is not None:
-            h.stop()
-        if dep is not None:
-            dep.close()
-
-
-def child_env(d: "Dist", port: int) -> dict:
+def child_env(d: "Dist", port: int, deadline: float) -> dict:
     """Environment of a per-rank child that forms its own process group on
     `port`.  Under torch.distributed.run the ranks carry
     TORCHELASTIC_USE_AGENT_STORE=True (connect to the launcher's store instead
@@ -527,147 +274,189 @@ def child_env(d: "Dist", port: int) -> dict:
     for a store nobody serves on the new port."""
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     env.update(RANK=str(d.rank), LOCAL_RANK=str(d.local_rank), WORLD_SIZE=str(d.world),
-               LOCAL_WORLD_SIZE=str(d.local_world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+               LOCAL_WORLD_SIZE=str(d.local_world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               SCA_BENCH_DEADLINE=str(deadline))
     return env
 
 
-def run_variants_isolated(args, d: Dist, argv, kinds, timeout_s: float = 900.0) -> dict:
-    """Run the multi-GPU graph variants in a child process per rank (a fresh
-    gloo process group on a new port): a device fault or hang while nodes of
-    a graph talk across GPUs ends the child, which is recorded, instead of the
-    rank that still has to print the headline line."""
-    import signal
+# ------------------------------------------------------------------ report
+class Reporter:
+    """Rank 0's single JSON line.  emit() is called once, either at the end
+    of a normal run or by the watchdog when the budget runs out (what has not
+    finished is reported as "timeout"); it then kills every child."""
 
-    box = [_free_port() if d.rank == 0 else None]
-    if d.dist is not None:
-        d.dist.broadcast_object_list(box, src=0)
-    env = child_env(d, box[0])
-    child_argv = [a for a in argv if a != "--variants-child"]
-    cmd = [sys.executable, os.path.abspath(__file__), *child_argv, "--variants-child", ",".join(kinds),
-           "--server-threads", str(args.server_threads), "--client-threads", str(args.client_threads)]
-    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                         start_new_session=True)
-    try:
-        out, err = p.communicate(timeout=timeout_s)
-        status = None if p.returncode == 0 else f"variant runner rc={p.returncode}: {(err or '')[-400:]}"
-    except subprocess.TimeoutExpired:
-        os.killpg(p.pid, signal.SIGKILL)
-        out, err = p.communicate()
-        status = f"variant runner timed out after {timeout_s:.0f}s"
-    res = {}
-    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
-    if lines:
-        try:
-            res = json.loads(lines[-1])
-        except ValueError:
-            pass
-    for kind in kinds:
-        if kind not in res:
-            res[kind] = {"error": status or "variant runner printed no result"}
-    return res
+    def __init__(self, args, d: Dist, ex: bk.Exchange, budget: bk.Budget):
+        self.args, self.d, self.ex, self.budget = args, d, ex, budget
+        self.lock = threading.Lock()
+        self.emitted = False
+        self.label = ""
+        self.wl = None
+        self.variants: dict = {}
+        self.pending: list = []
+        self.rc = 0
 
+    def start_watchdog(self):
+        def run():
+            while self.budget.left() > 0:
+                time.sleep(min(1.0, max(0.05, self.budget.left())))
+            if self.d.rank == 0:
+                self.emit(watchdog=True)
+            bk.CHILDREN.kill_all()
+            sys.stdout.flush()
+            os._exit(self.rc if self.d.rank == 0 else 0)
 
-def variants_child(args) -> None:
-    """Entry of the isolated variant runner: measure each kind, print one JSON
-    line {kind: result} for this rank."""
-    d = Dist(backend="gloo")
-    import seldon_core_amd  # noqa: F401
+        threading.Thread(target=run, daemon=True, name="bench-watchdog").start()
 
-    wl = Workload(args.model)
-    wl.py_batching, wl.py_workers = args.py_batching, args.py_workers
-    out = {}
-    for kind in args.variants_child.split(","):
-        try:
-            out[kind] = measure_variant(args, d, wl, kind, spin=False)
-        except Exception as e:
-            out[kind] = {"error": f"{type(e).__name__}: {e}"[:600]}
-    print(json.dumps(out), flush=True)
-    d.close()
+    def emit(self, watchdog: bool = False):
+        with self.lock:
+            if self.emitted:
+                return
+            self.emitted = True
+            try:
+                line, failures = summarize(self, watchdog)
+            except Exception as e:  # the line must come out whatever happened
+                line, failures = {"metric": metric_name(self.args), "value": 0.0, "unit": "predictions/s",
+                                  "n_gpus": self.d.world, "steps": self.args.steps, "warmup": self.args.warmup,
+                                  "error": f"report failed: {type(e).__name__}: {e}"}, ["report"]
+            print(json.dumps(line), flush=True)
+            if failures:
+                print("bench.py: FAILED: " + "; ".join(failures), file=sys.stderr, flush=True)
+                self.rc = 3
 
 
-def fabric_probe(d: Dist, timeout_s: float = 150.0, requests: int = 200):
-    """Cross-process graph placement over the p2p fabric: every
-    rank starts ``tools/fabric_probe.py`` as a child process in a fresh
-    process group (rank 0 hosts an AVERAGE_COMBINER whose MODEL children live
-    on every rank; batches and replies travel as RCCL send/recv on GPUs).  It
-    runs after the measurements, in children under a time limit, so a hang or
-    fault there is recorded instead of costing the benchmark line.  Returns
-    rank 0's summary (None on other ranks)."""
-    import signal
-
-    box = [_free_port() if d.rank == 0 else None]
-    if d.dist is not None:
-        d.dist.broadcast_object_list(box, src=0)
-    env = child_env(d, box[0])
-    t0 = time.perf_counter()
-    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "fabric_probe.py"), "--requests", str(requests)],
-                         env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
-    try:
-        out, err = p.communicate(timeout=timeout_s)
-        status = "ok" if p.returncode == 0 else f"rc={p.returncode}"
-    except subprocess.TimeoutExpired:
-        os.killpg(p.pid, signal.SIGKILL)
-        out, err = p.communicate()
-        status = f"timeout after {timeout_s:.0f}s"
-    res = {"rank": d.rank, "status": status, "wall_s": round(time.perf_counter() - t0, 2)}
-    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
-    if lines:
-        try:
-            res["probe"] = json.loads(lines[-1])
-        except ValueError:
-            pass
-    if status != "ok":
-        res["stderr_tail"] = (err or "")[-600:]
-    allr = d.gather(res)
-    if d.rank != 0:
-        return None
-    top = allr[0].get("probe") or {}
-    return {"ok": all(r["status"] == "ok" for r in allr), "world": d.world,
-            "data_plane": top.get("data_plane"), "requests": top.get("requests"),
-            "max_abs_err": top.get("max_abs_err"), "req_per_s": round(top.get("req_per_s", 0.0), 1),
-            "units": top.get("units"), "ranks": [{k: r[k] for k in r if k != "probe"} for r in allr]}
+def metric_name(args) -> str:
+    return "predictions/sec (%s graph, %s)" % ("single-model" if args.graph == "single" else args.graph,
+                                               args.api.upper())
 
 
-def main() -> None:
-    argv = sys.argv[1:]
-    args = parse_args(argv)
-    env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus, argv))
-    if env_world is not None and int(env_world) != args.gpus:
-        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
-        sys.exit(2)
+def summarize(rep: Reporter, watchdog: bool):
+    args, d, ex = rep.args, rep.d, rep.ex
+    failures = []
+    heads = {r: ex.get("headline", r) for r in range(d.world)}
+    missing = [r for r, h in heads.items() if h is None]
+    mines = [h for h in heads.values() if h is not None]
+    if missing:
+        failures.append(f"no headline result from ranks {missing}")
+    for m in mines:
+        if not m["check"]["ok"]:
+            failures.append(f"rank {m['rank']} headline self-check: {m['check']}")
+    base = REST_BASELINE if args.api == "rest" else GRPC_BASELINE
+    line = {"metric": metric_name(args), "value": 0.0, "unit": "predictions/s", "n_gpus": d.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp64"}
+    if mines:
+        # whole-job throughput: every rank's completed predictions over the
+        # slowest rank's timed window
+        wall_max = max(m["wall"] for m in mines)
+        value = sum(m["ok"] for m in mines) / wall_max if not missing else 0.0
+        line.update(value=round(value, 2), ms_per_step=round(wall_max / args.steps * 1000.0, 3),
+                    vs_baseline=round(value / base, 3), timed_region_s=round(wall_max, 3),
+                    p50_ms=round(max(m["p50"] for m in mines), 4), p99_ms=round(max(m["p99"] for m in mines), 4),
+                    step_ms=bk.step_spread([s for m in mines for s in m["step_ms"]]))
+    wl = rep.wl
+    line["data"] = ("synthetic (locust-shaped JSON payload, iris feature row); model fit on sklearn's bundled iris"
+                    if args.model in ("iris", "python-iris", "python-noop") else
+                    f"synthetic (locust-shaped JSON payload, {len(wl.row) if wl else '?'}-feature random row); "
+                    "random-init model")
+    line["baseline"] = {"rest_rps": REST_BASELINE, "rest_p50_ms": 4, "rest_p99_ms": 69, "grpc_rps": GRPC_BASELINE,
+                        "grpc_p50_ms": 1, "grpc_p99_ms": 6}
+    if mines:
+        line["self_check"] = {"ok": all(m["check"]["ok"] for m in mines) and not missing,
+                              "max_abs_err": max(m["check"]["max_abs_err"] for m in mines),
+                              "sampled_replies_checked": sum(m.get("checked", 0) for m in mines)}
+    st0 = mines[0]["stats"] if mines else {"batches": 0, "rows": 0, "gpu_busy_s": 0.0}
+    wall0 = mines[0]["wall"] if mines else 1.0
+    per_rank = [{"rank": m["rank"], "device": m["device"], "cpu_budget": m["cpu_budget"],
+                 "pinned_cpus": m.get("pinned_cpus"), **m["cpu"], "step_requests": m["step_requests"],
+                 "rps": round(m["ok"] / m["wall"], 1), "p50_ms": m["p50"], "p99_ms": m["p99"],
+                 "step_ms": bk.step_spread(m["step_ms"]),
+                 "gpu_batches": m["stats"]["batches"],
+                 "mean_rows_per_batch": round(m["stats"]["rows"] / max(1, m["stats"]["batches"]), 2),
+                 # share of the window the GPU device thread spent launching / handing off responses
+                 "device_thread_launch_frac": round(m["stats"]["launch_cpu_s"] / m["wall"], 3),
+                 "device_thread_complete_frac": round(m["stats"]["complete_cpu_s"] / m["wall"], 3),
+                 "check_max_abs_err": m["check"]["max_abs_err"]} for m in mines]
+    line["config"] = {"model": rep.label, "global_batch": args.users * d.world, "seq_len": len(wl.row) if wl else 0,
+                      "parallelism": f"dp{d.world}", "graph": args.graph, "api": args.api,
+                      "users_per_gpu": args.users,
+                      "requests_per_step_per_gpu": mines[0]["step_requests"] if mines else args.step_requests,
+                      "device": "gpu" if d.has_gpu else "cpu", "gpu_batches": st0["batches"],
+                      "mean_rows_per_gpu_batch": round(st0["rows"] / max(1, st0["batches"]), 2),
+                      "gpu_busy_frac_per_slot": round(st0["gpu_busy_s"] / max(1e-9, wall0 * args.slots), 3),
+                      "slots": args.slots, "server_threads": args.server_threads,
+                      "client_threads": args.client_threads, "host_cpus": os.cpu_count(),
+                      "cpu_budget": round(bk.cpu_budget(), 2), "per_rank": per_rank}
+    # ---- extras
+    if args.extras == "auto" and args.graph == "single":
+        gr = {r: ex.get("grpc", r) for r in range(d.world)}
+        errs = [g["error"] for g in gr.values() if g and "error" in g]
+        if errs:
+            line["grpc"] = {"error": errs[0]}
+        elif all(g is not None for g in gr.values()):
+            gs = list(gr.values())
+            gw = max(g["wall"] for g in gs)
+            v = sum(g["ok"] for g in gs) / gw
+            line["grpc"] = {"value": round(v, 2), "vs_baseline": round(v / GRPC_BASELINE, 3),
+                            "p50_ms": max(g["p50"] for g in gs), "p99_ms": max(g["p99"] for g in gs),
+                            "window_s": round(gw, 3), "step_ms": bk.step_spread([s for g in gs for s in g["step_ms"]])}
+        else:
+            line["grpc"] = {"error": "timeout" if watchdog else "missing"}
+    variants = dict(rep.variants)
+    for k in rep.pending:
+        variants.setdefault(k, {"error": "timeout" if watchdog else "not run"})
+    for k, v in variants.items():
+        if "error" not in v and not v.get("self_check", {}).get("ok", True):
+            failures.append(f"{k} self-check: {v['self_check']}")
+    if variants:
+        line["variants"] = variants
+    line["budget"] = {"budget_s": BUDGET_S, "used_s": round(time.time() - T_START, 1), "watchdog_fired": watchdog}
+    return line, failures
 
-    if args.variants_child:
-        variants_child(args)
-        return
-    d = Dist()
-    per_rank_budget, pinned = place_rank(args, d)
-    per_rank_cpus = size_threads(args, per_rank_budget)
-    spin = not args.no_spin
+
+# ---------------------------------------------------------------- headline
+def calibrate(args, d: Dist, port: int, body, budget: bk.Budget) -> int:
+    """Step size so the K timed steps last >= TARGET_TIMED_S on the slowest
+    rank: a short probe run per rank, min rate over ranks (one collective,
+    before the timed region)."""
+    probe = bk.run_loadgen(port, 1, 1, args.api, body, args.users, args.client_threads,
+                           max(2000, args.users * 16), budget.timeout(cap=120, reserve=HEAD_RESERVE_S))
+    rate = d.gather(float(probe["rps"]))
+    per_step = max(0.2, TARGET_TIMED_S / max(1, args.steps))
+    return int(min(5_000_000, max(2000, min(rate) * per_step)))
+
+
+def headline(args, d: Dist, rep: Reporter, budget: bk.Budget, per_rank_cpus: float, pinned) -> tuple:
     import seldon_core_amd as sca
 
-    wl = Workload(args.model)
-    wl.py_batching, wl.py_workers = args.py_batching, args.py_workers
+    wl = bk.Workload(args.model, args.py_batching, args.py_workers)
+    rep.wl = wl
     ngpu = sca.gpu_count() if d.has_gpu else 0
-    devs = [d.device] if args.graph == "single" else group_devices(
-        d.rank, max(2, d.world) if args.graph == "mab" else VARIANT_SPAN[args.graph], ngpu)
-    dep, oracle, label = make_deployment(wl, args.graph, devs, d.device, args.slots, spin)
+    if args.graph == "single":
+        devs = [d.device]
+    else:
+        span = SPAN.get(args.graph, max(2, d.world))
+        devs = [(d.device + i) % ngpu for i in range(span)] if ngpu else [-1] * span
+    dep, oracle, label = bk.make_deployment(wl, args.graph, devs, d.device, args.slots, not args.no_spin)
     if args.graph != "single":
         if not wl.impl:
             raise SystemExit("multi-node --graph variants use the kernel models (iris / xgb1000)")
         label = f"{label} [{wl.label}]"
+    rep.label = label
     handle = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
-    C = dep.C
-    payload = json.dumps({"data": {"names": wl.names, "ndarray": [wl.row]}})
-    pb = C.json_to_pb(json.dumps({"data": {"names": wl.names,
-                                           "tensor": {"shape": [1, len(wl.row)], "values": wl.row}}}))
+    body_rest = wl.rest_body()
+    pb = dep.C.json_to_pb(json.dumps({"data": {"names": wl.names,
+                                               "tensor": {"shape": [1, len(wl.row)], "values": wl.row}}}))
+    expect_rest = bk.rest_expect(handle.http_port, body_rest)
+    expect_pb = bk.pb_data_suffix(dep.predict_pb(pb)[1])
     if args.api == "rest":
-        body, port = payload, handle.http_port
+        body, port, expect = body_rest, handle.http_port, expect_rest
     else:
-        body, port = pb, handle.grpc_port
+        body, port, expect = pb, handle.grpc_port, expect_pb
+    if args.step_requests is None:
+        args.step_requests = calibrate(args, d, port, body, budget)
     if args.warmup > 0:  # untimed
-        run_loadgen(args, port, args.warmup, 0, args.api, body)
+        bk.run_loadgen(port, args.warmup, 0, args.api, body, args.users, args.client_threads, args.step_requests,
+                       budget.timeout(reserve=HEAD_RESERVE_S), expect=expect)
     for u in dep.batched.values():
         u.reset_stats()
     cpu: dict = {}
@@ -675,127 +464,417 @@ def main() -> None:
         from seldon_core_amd.utils import cpuprof
 
         cpuprof.start(depth=args.cpu_profile_depth)
-    lg, wall = timed(d, lambda: run_loadgen(args, port, args.steps, 0, args.api, body), cpu)
+    tmo = budget.timeout(reserve=HEAD_RESERVE_S)
+    d.barrier()
+    d.sync()
+    c0 = cpu_seconds()
+    t0 = time.perf_counter()
+    err = None
+    try:
+        lg = bk.run_loadgen(port, args.steps, 0, args.api, body, args.users, args.client_threads, args.step_requests,
+                            tmo, expect=expect)
+    except Exception as e:  # still meet the closing barrier, or the other ranks would wait forever
+        lg, err = None, e
+    d.sync()
+    wall = time.perf_counter() - t0
+    c1 = cpu_seconds()
+    cpu["server_cpus"] = round((c1[0] - c0[0]) / wall, 2)
+    cpu["loadgen_cpus"] = round((c1[1] - c0[1]) / wall, 2)
+    d.barrier()
+    if err is not None:
+        raise err
     if args.cpu_profile:
         prof = cpuprof.stop()
         prof.update(rps=round(lg["ok"] / wall, 1), server_cpus=cpu.get("server_cpus"), rank=d.rank)
         with open(args.cpu_profile if d.world == 1 else f"{args.cpu_profile}.rank{d.rank}", "w") as f:
             json.dump(prof, f, indent=1)
-    st = unit_stats(dep)
+    st = bk.unit_stats(dep)
+    chk = bk.self_check(handle.http_port, wl, oracle, seed=d.rank)
     mine = {"rank": d.rank, "device": d.device, "ok": lg["ok"], "wall": wall, "p50": lg["p50_ms"],
-            "p99": lg["p99_ms"], "stats": st, "cpu_budget": round(per_rank_cpus, 2), "cpu": cpu,
-            "pinned_cpus": cpu_ranges(pinned) if pinned else None}
-    extras: dict = {}
-    failures = []
-    # ---- after the timed region: correctness + extra configs
-    chk = self_check(handle.http_port, wl, oracle, seed=d.rank)
-    mine["check"] = chk
-    if not chk["ok"]:
-        failures.append(f"rank {d.rank} headline self-check: {chk}")
-    if args.extras == "auto" and args.graph == "single":
+            "p99": lg["p99_ms"], "step_ms": lg["step_ms"], "checked": lg.get("checked", 0), "stats": st,
+            "cpu_budget": round(per_rank_cpus, 2), "cpu": cpu, "step_requests": args.step_requests,
+            "pinned_cpus": bk.cpu_ranges(pinned) if pinned else None, "check": chk}
+    rep.ex.put("headline", mine)
+    return dep, handle, pb, expect_pb, lg
+
+
+def grpc_extra(args, d: Dist, rep: Reporter, budget: bk.Budget, handle, pb, expect_pb, head_lg) -> None:
+    """gRPC API (seldon.protos.Seldon/Predict, Tensor payload) on every rank,
+    started together (soft file barrier), window >= EXTRA_WINDOW_S."""
+    try:
+        fault("grpc", d.rank)
+        rep.ex.barrier("grpc_go", timeout=budget.timeout(cap=60, reserve=EXTRA_RESERVE_S))
+        sreq = int(max(2000, head_lg["rps"] * EXTRA_WINDOW_S / 2))
+        t0 = time.perf_counter()
+        g = bk.run_loadgen(handle.grpc_port, 2, 1, "grpc", pb, args.users, args.client_threads, sreq,
+                           budget.timeout(cap=120, reserve=EXTRA_RESERVE_S), expect=expect_pb)
+        res = {"ok": g["ok"], "wall": g["seconds"], "p50": g["p50_ms"], "p99": g["p99_ms"],
+               "step_ms": g["step_ms"], "call_s": round(time.perf_counter() - t0, 2)}
+    except Exception as e:  # reported; the headline stands
+        res = {"error": f"{type(e).__name__}: {e}"[:600]}
+    rep.ex.put("grpc", res)
+
+
+# ---------------------------------------------------------------- variants
+def variant_cmd(args, kind: str, span: int, deadline: float, extra=()):
+    return [sys.executable, os.path.abspath(__file__), "--model", args.model, "--slots", str(args.slots),
+            "--users", str(args.users), "--variant-child", kind, "--span", str(span), "--deadline", str(deadline),
+            *extra]
+
+
+def run_inprocess_variants(args, d: Dist, rep: Reporter, budget: bk.Budget, kinds) -> None:
+    """Rank 0: each multi-GPU graph as ONE deployment over the node's GPUs,
+    in a child process (a fault or hang there is recorded, not fatal) with
+    its own deadline; results go into the line as soon as they exist."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK")
+           and not k.startswith("TORCHELASTIC_")}
+    env["SCA_BENCH_AFFINITY"] = bk.cpu_ranges(ORIG_AFFINITY) if ORIG_AFFINITY else ""
+    reserve = REPORT_RESERVE_S + (FABRIC_RESERVE_S if args.rank_variants else 0.0)
+    for kind in kinds:
+        span = SPAN.get(kind, d.world)
         try:
-            g, gwall = timed(d, lambda: run_loadgen(args, handle.grpc_port, args.extra_steps, 0, "grpc", pb))
-            extras["grpc"] = {"ok": g["ok"], "wall": gwall, "p50": g["p50_ms"], "p99": g["p99_ms"]}
-        except Exception as e:  # reported; the headline stands
-            extras["grpc"] = {"error": f"{type(e).__name__}: {e}"[:600]}
-    handle.stop()
-    dep.close()
-    if args.extras == "auto" and args.graph == "single" and d.world >= 2 and wl.impl:
-        kinds = ["abtest"] + (["pipeline"] if d.world >= 4 else []) + ["mab"]
-        for kind, r in run_variants_isolated(args, d, argv, kinds).items():
-            if "error" not in r and not r["check"]["ok"]:
-                failures.append(f"rank {d.rank} {kind} self-check: {r['check']}")
-            extras[kind] = r
-    results = d.gather({"mine": mine, "extras": extras, "failures": failures})
-    fabric = None
-    if args.extras == "auto" and args.fabric_probe == "auto" and d.world >= 2:
-        fabric = fabric_probe(d)
+            tmo = budget.timeout(cap=VARIANT_CAP_S, reserve=reserve, floor=10.0)
+        except bk.BudgetExpired as e:
+            rep.variants[kind] = {"error": f"skipped: {e}"}
+            continue
+        res = bk.CHILDREN.run(variant_cmd(args, kind, span, time.time() + tmo), tmo + 5, env=env)
+        out = bk.last_json(res["stdout"])
+        if res["timed_out"]:
+            out = {"error": "timeout", "after_s": round(tmo, 1), "stderr_tail": res["stderr"][-600:]}
+        elif out is None or res["rc"] != 0:
+            out = dict(out or {}, error=(out or {}).get("error") or f"variant child rc={res['rc']}",
+                       stderr_tail=res["stderr"][-600:])
+        out["child_wall_s"] = res["wall_s"]
+        rep.variants[kind] = out
+        if kind in rep.pending:
+            rep.pending.remove(kind)
+
+
+def variant_child(args) -> None:
+    """One in-process variant: build it on GPUs 0..span-1, serve, calibrate,
+    time a >= EXTRA_WINDOW_S window (mab: with concurrent feedback that
+    rewards the last branch), self-check, report placement; one JSON line."""
+    budget = bk.Budget(args.deadline)
+    aff = os.environ.get("SCA_BENCH_AFFINITY")
+    if aff:  # the parent rank was pinned to one CCD; one process now drives every GPU
+        from seldon_core_amd.utils.topology import _parse_cpulist
+
+        try:
+            os.sched_setaffinity(0, _parse_cpulist(aff))
+        except OSError:
+            pass
+    kind = args.variant_child
+    out = {"error": "unfinished"}
+    dep = h = None
+    try:
+        fault(kind, 0)
+        import seldon_core_amd as sca
+
+        ngpu = sca.gpu_count()
+        devs = list(range(args.span)) if ngpu > 0 else [-1] * args.span
+        if ngpu and args.span > ngpu:
+            if not os.environ.get("SCA_BENCH_FOLD"):
+                raise RuntimeError(f"{kind} needs {args.span} GPUs, {ngpu} visible")
+            devs = [i % ngpu for i in devs]  # rehearsal on a smaller box: nodes fold onto the GPUs present
+        cpus = bk.cpu_budget()
+        server_threads = max(2, min(32, int(cpus * 0.55)))
+        client_threads = max(1, min(16, int(cpus * 0.3)))
+        wl = bk.Workload(args.model)
+        dep, oracle, label = bk.make_deployment(wl, kind, devs, devs[0], args.slots, spin=False)
+        h = dep.serve(http_port=0, grpc_port=0, threads=server_threads, host="127.0.0.1")
+        body = wl.rest_body()
+        expect = bk.rest_expect(h.http_port, body)
+        cal = bk.run_loadgen(h.http_port, 1, 1, "rest", body, args.users, client_threads, 4000,
+                             budget.timeout(reserve=3), expect=expect)
+        sreq = int(max(2000, cal["rps"] * EXTRA_WINDOW_S / 2))
+        for u in dep.batched.values():
+            u.reset_stats()
+        fb_out, fb = {}, None
+        n = len(devs)
+        if kind == "mab":
+            # feedback next to the predictions (reference MAB loadtest sends
+            # feedback: util/loadtester/scripts/predict_rest_locust.py); the
+            # last branch (the farthest GPU) is rewarded, so the bandit must
+            # learn to send most traffic there.
+            fbody = json.dumps({"request": {"data": {"names": wl.names, "ndarray": [wl.row]}},
+                                "response": {"meta": {"routing": {"mab": n - 1}}, "data": {"ndarray": [[0.0]]}},
+                                "reward": 1.0})
+
+            def feedback():
+                try:
+                    fb_out.update(bk.run_loadgen(h.http_port, 2, 0, "rest", fbody, max(4, args.users // 16),
+                                                 max(1, client_threads // 4), max(200, sreq // 16),
+                                                 budget.timeout(reserve=3), path="/api/v0.1/feedback"))
+                except Exception as e:
+                    fb_out["error"] = f"{type(e).__name__}: {e}"[:300]
+
+            fb = threading.Thread(target=feedback)
+            fb.start()
+        lg = bk.run_loadgen(h.http_port, 2, 0, "rest", body, args.users, client_threads, sreq,
+                            budget.timeout(reserve=3), expect=expect)
+        if fb is not None:
+            fb.join()
+        check = bk.self_check(h.http_port, wl, oracle, seed=100)
+        st = bk.unit_stats(dep)
+        pl = bk.placement(dep)
+        used = sorted({x for v in pl.values() if isinstance(v, list) for x in v})
+        out = {"graph": label, "model": wl.label, "gpus_per_graph": len(set(devs)), "value": round(lg["rps"], 2),
+               "unit": "predictions/s", "vs_rest_baseline": round(lg["rps"] / REST_BASELINE, 3),
+               "p50_ms": lg["p50_ms"], "p99_ms": lg["p99_ms"], "window_s": round(lg["seconds"], 3),
+               "step_ms": bk.step_spread(lg["step_ms"]), "sampled_replies_checked": lg.get("checked", 0),
+               "self_check": check, "placement": pl, "peer_access": bk.peer_access(used),
+               "batches_per_device": {k: v["batches"] for k, v in st["per_device"].items()},
+               "rows_per_device": {k: v["rows"] for k, v in st["per_device"].items()},
+               "server_threads": server_threads, "client_threads": client_threads, "cpu_budget": cpus}
+        if kind == "mab":
+            out["feedback"] = {"rewarded_branch": n - 1, "rps": fb_out.get("rps"), "error": fb_out.get("error")}
+    except Exception as e:
+        out = {"error": f"{type(e).__name__}: {e}"[:600]}
+    finally:
+        try:
+            if h is not None:
+                h.stop()
+            if dep is not None:
+                dep.close()
+        except Exception:
+            pass
+    print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------------ fabric
+def run_fabric_phase(args, d: Dist, rep: Reporter, budget: bk.Budget, kinds) -> None:
+    """Every rank: start a fabric child (fresh gloo group on a port rank 0
+    publishes through the exchange); rank 0's child serves the rank-placed
+    graphs, the others run PeerServer loops.  Each rank files its child's
+    result; rank 0 merges them into the line."""
+    ex = rep.ex
     if d.rank == 0:
-        line = summarize(args, d, results, label, wl)
-        if fabric is not None:
-            line["rccl_fabric"] = fabric
-        print(json.dumps(line), flush=True)
-    bad = [f for r in results for f in r["failures"]]
-    d.close()
-    if bad:
-        print("bench.py: self-check FAILED: " + "; ".join(bad), file=sys.stderr)
-        sys.exit(3)
+        try:
+            tmo = budget.timeout(reserve=REPORT_RESERVE_S, floor=20.0)
+            ex.put("fabric_go", {"port": _free_port(), "deadline": time.time() + tmo})
+        except bk.BudgetExpired as e:
+            ex.put("fabric_go", {"skip": str(e)})
+    go = ex.wait("fabric_go", [0], timeout=max(0.0, budget.left(REPORT_RESERVE_S))).get(0)
+    if not go or "skip" in go:
+        if d.rank == 0:
+            for k in kinds:
+                rep.variants[f"{k}_rccl"] = {"error": (go or {}).get("skip", "not run")}
+                if f"{k}_rccl" in rep.pending:
+                    rep.pending.remove(f"{k}_rccl")
+        return
+    deadline = float(go["deadline"])
+    cmd = [sys.executable, os.path.abspath(__file__), "--model", args.model, "--slots", str(args.slots),
+           "--users", str(args.users), "--fabric-child", ",".join(kinds), "--deadline", str(deadline),
+           "--server-threads", str(args.server_threads), "--client-threads", str(args.client_threads)]
+    res = bk.CHILDREN.run(cmd, max(1.0, deadline - time.time()) + 3, env=child_env(d, int(go["port"]), deadline))
+    out = {"graphs": {}}
+    for ln in res["stdout"].splitlines():  # one line per finished graph, then a summary
+        if ln.startswith("{"):
+            try:
+                o = json.loads(ln)
+            except ValueError:
+                continue
+            if "kind" in o:
+                out["graphs"][o["kind"]] = o["result"]
+            else:
+                out.update({k: v for k, v in o.items() if k != "graphs"})
+    status = "timeout" if res["timed_out"] else ("ok" if res["rc"] == 0 else f"rc={res['rc']}")
+    mine = {"rank": d.rank, "status": status, "wall_s": res["wall_s"], "result": out}
+    if status != "ok":
+        mine["stderr_tail"] = res["stderr"][-600:]
+    ex.put("fabric", mine)
+    if d.rank != 0:
+        return
+    peers = ex.wait("fabric", list(range(1, d.world)), timeout=max(0.0, budget.left(REPORT_RESERVE_S)))
+    for k in kinds:
+        key = f"{k}_rccl"
+        r0 = out["graphs"].get(k)
+        if r0 is None:
+            r0 = {"error": "timeout" if status == "timeout" else f"fabric child {status}: no result",
+                  "stderr_tail": res["stderr"][-400:]}
+        r0 = dict(r0)
+        r0["data_plane"] = out.get("data_plane", "rccl" if d.has_gpu else "sockets")
+        r0["fabric_world"] = d.world
+        r0["worker_ranks"] = {str(r): ((p.get("result") or {}).get("graphs") or {}).get(k, {"status": p["status"]})
+                              for r, p in sorted(peers.items())}
+        missing = [r for r in range(1, d.world) if r not in peers]
+        if missing:
+            r0["workers_missing"] = missing
+        rep.variants[key] = r0
+        if key in rep.pending:
+            rep.pending.remove(key)
 
 
-def summarize(args, d: Dist, results, label: str, wl: Workload) -> dict:
-    mines = [r["mine"] for r in results]
-    # whole-job throughput: every rank's completed predictions over the
-    # slowest rank's timed window
-    wall_max = max(m["wall"] for m in mines)
-    value = sum(m["ok"] for m in mines) / wall_max
-    base = REST_BASELINE if args.api == "rest" else GRPC_BASELINE
-    st0 = mines[0]["stats"]
-    per_rank = [{"rank": m["rank"], "device": m["device"], "cpu_budget": m["cpu_budget"],
-                 "pinned_cpus": m.get("pinned_cpus"), **m["cpu"],
-                 "rps": round(m["ok"] / m["wall"], 1), "p50_ms": m["p50"], "p99_ms": m["p99"],
-                 "gpu_batches": m["stats"]["batches"],
-                 "mean_rows_per_batch": round(m["stats"]["rows"] / max(1, m["stats"]["batches"]), 2),
-                 # share of the window the GPU device thread spent launching / handing off responses
-                 "device_thread_launch_frac": round(m["stats"]["launch_cpu_s"] / m["wall"], 3),
-                 "device_thread_complete_frac": round(m["stats"]["complete_cpu_s"] / m["wall"], 3),
-                 "check_max_abs_err": m["check"]["max_abs_err"]} for m in mines]
-    line = {
-        "metric": "predictions/sec (%s graph, %s)" % ("single-model" if args.graph == "single" else args.graph,
-                                                      args.api.upper()),
-        "value": round(value, 2), "unit": "predictions/s", "n_gpus": d.world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1000.0, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": round(value / base, 3), "dtype": "fp64",
-        "data": ("synthetic (locust-shaped JSON payload, iris feature row); model fit on sklearn's bundled iris"
-                 if args.model in ("iris", "python-iris", "python-noop") else
-                 f"synthetic (locust-shaped JSON payload, {len(wl.row)}-feature random row); random-init model"),
-        "p50_ms": round(max(m["p50"] for m in mines), 4), "p99_ms": round(max(m["p99"] for m in mines), 4),
-        "baseline": {"rest_rps": REST_BASELINE, "rest_p50_ms": 4, "rest_p99_ms": 69, "grpc_rps": GRPC_BASELINE,
-                     "grpc_p50_ms": 1, "grpc_p99_ms": 6},
-        "self_check": {"ok": all(m["check"]["ok"] for m in mines),
-                       "max_abs_err": max(m["check"]["max_abs_err"] for m in mines)},
-        "config": {"model": label, "global_batch": args.users * d.world, "seq_len": len(wl.row),
-                   "parallelism": f"dp{d.world}", "graph": args.graph, "api": args.api,
-                   "users_per_gpu": args.users, "requests_per_step_per_gpu": args.step_requests,
-                   "device": "gpu" if d.has_gpu else "cpu", "gpu_batches": st0["batches"],
-                   "mean_rows_per_gpu_batch": round(st0["rows"] / max(1, st0["batches"]), 2),
-                   "gpu_busy_frac_per_slot": round(st0["gpu_busy_s"] / max(1e-9, mines[0]["wall"] * args.slots), 3),
-                   "slots": args.slots, "server_threads": args.server_threads,
-                   "client_threads": args.client_threads, "host_cpus": os.cpu_count(),
-                   "cpu_budget": round(cpu_budget(), 2), "per_rank": per_rank},
-    }
-    ex = [r["extras"] for r in results]
-    if any("error" in e.get("grpc", {}) for e in ex):
-        line["grpc"] = {"error": next(e["grpc"]["error"] for e in ex if "error" in e.get("grpc", {}))}
-    elif ex[0].get("grpc"):
-        gw = max(e["grpc"]["wall"] for e in ex)
-        g = sum(e["grpc"]["ok"] for e in ex) / gw
-        line["grpc"] = {"value": round(g, 2), "vs_baseline": round(g / GRPC_BASELINE, 3),
-                        "p50_ms": max(e["grpc"]["p50"] for e in ex), "p99_ms": max(e["grpc"]["p99"] for e in ex)}
-    variants = {}
-    for kind in ("abtest", "pipeline", "mab"):
-        if kind not in ex[0]:
+def fabric_child(args) -> None:
+    """Rank-placed graphs over the RCCL p2p fabric.
+    Rank 0 hosts the front end, router/combiner and the micro-batchers; the
+    nodes placed on rank r run in rank r's PeerServer on its GPU; batches and
+    replies are RCCL send/recv on GPUs (sockets on CPU).  Every rank walks the
+    same graph list in the same order."""
+    import datetime
+
+    import torch
+    import torch.distributed as dist
+
+    budget = bk.Budget(args.deadline)
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = int(os.environ.get("LOCAL_RANK", rank)) if torch.cuda.is_available() else -1
+    if dev >= 0:
+        torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(10.0, budget.left())))
+    from seldon_core_amd.parallel.fabric import init_fabric, serve_peer
+    from seldon_core_amd.serving.deployment import Deployment
+
+    fabric = init_fabric(device=dev)
+    wl = bk.Workload(args.model)
+    graphs = {}
+    for kind in [k for k in args.fabric_child.split(",") if k]:
+        if (kind == "pipeline" and world < 4) or world < 2:
             continue
-        rs = [e[kind] for e in ex]
-        errs = [r["error"] for r in rs if "error" in r]
-        if errs:
-            variants[kind] = {"error": errs[0], "ranks_failed": len(errs)}
+        g, comps, oracle, label = bk.build_rank_graph(wl, kind, world)
+        spec = bk.sdep(g)
+        if rank != 0:
+            t0 = time.perf_counter()
+            try:
+                fault(f"{kind}_rccl", rank)
+                srv = serve_peer(spec, fabric, comps)
+                srv.join()
+                graphs[kind] = {"batches": srv.batches, "rows": srv.rows, "host_syncs": srv.host_syncs,
+                                "max_inflight": getattr(srv, "max_inflight", None), "error": srv.error(),
+                                "device": dev, "wall_s": round(time.perf_counter() - t0, 2)}
+            except Exception as e:
+                graphs[kind] = {"error": f"{type(e).__name__}: {e}"[:400]}
+            print(json.dumps({"kind": kind, "result": graphs[kind]}), flush=True)
             continue
-        w = max(r["wall"] for r in rs)
-        v = sum(r["ok"] for r in rs) / w
-        variants[kind] = {
-            "graph": rs[0]["label"], "gpus_per_graph": len(rs[0]["devices"]), "n_gpus": d.world,
-            "value": round(v, 2), "unit": "predictions/s", "vs_rest_baseline": round(v / REST_BASELINE, 3),
-            "p50_ms": max(r["p50"] for r in rs), "p99_ms": max(r["p99"] for r in rs),
-            "self_check": {"ok": all(r["check"]["ok"] for r in rs),
-                           "max_abs_err": max(r["check"]["max_abs_err"] for r in rs)},
-            "rank0_batches_per_device": {k: v2["batches"] for k, v2 in rs[0]["stats"]["per_device"].items()},
-        }
-        if "feedback_rps" in rs[0]:
-            variants[kind]["feedback_rps"] = round(sum(r.get("feedback_rps") or 0 for r in rs), 1)
-            variants[kind]["rank0_rows_per_device"] = rs[0].get("rows_per_device")
-    if variants:
-        line["variants"] = variants
-    return line
+        dep = h = None
+        try:
+            fault(f"{kind}_rccl", 0)
+            dep = Deployment(spec, components=comps, device=dev, fabric=fabric, fuse=False,
+                             batcher={"max_batch": 4096, "slots": args.slots, "spin_wait": False})
+            h = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
+            body = wl.rest_body()
+            expect = bk.rest_expect(h.http_port, body)
+            cal = bk.run_loadgen(h.http_port, 1, 1, "rest", body, args.users, args.client_threads, 4000,
+                                 budget.timeout(reserve=5), expect=expect)
+            sreq = int(max(2000, cal["rps"] * EXTRA_WINDOW_S / 2))
+            for u in dep.batched.values():
+                u.reset_stats()
+            fb_out, fb = {}, None
+            if kind == "mab":  # reward the last rank's replica: most batches must cross the fabric
+                fbody = json.dumps({"request": {"data": {"names": wl.names, "ndarray": [wl.row]}},
+                                    "response": {"meta": {"routing": {"mab": world - 1}},
+                                                 "data": {"ndarray": [[0.0]]}}, "reward": 1.0})
+
+                def feedback():
+                    try:
+                        fb_out.update(bk.run_loadgen(h.http_port, 2, 0, "rest", fbody, max(4, args.users // 16),
+                                                     max(1, args.client_threads // 4), max(200, sreq // 16),
+                                                     budget.timeout(reserve=5), path="/api/v0.1/feedback"))
+                    except Exception as e:
+                        fb_out["error"] = f"{type(e).__name__}: {e}"[:300]
+
+                fb = threading.Thread(target=feedback)
+                fb.start()
+            lg = bk.run_loadgen(h.http_port, 2, 0, "rest", body, args.users, args.client_threads, sreq,
+                                budget.timeout(reserve=5), expect=expect)
+            if fb is not None:
+                fb.join()
+            check = bk.self_check(h.http_port, wl, oracle, seed=200)
+            st = bk.unit_stats(dep)
+            r = {"graph": label, "value": round(lg["rps"], 2), "unit": "predictions/s",
+                 "p50_ms": lg["p50_ms"], "p99_ms": lg["p99_ms"], "window_s": round(lg["seconds"], 3),
+                 "step_ms": bk.step_spread(lg["step_ms"]), "sampled_replies_checked": lg.get("checked", 0),
+                 "self_check": check, "placement": bk.placement(dep),
+                 "unit_kinds": {n: dep.engine.unit_kind(n) for n in dep.engine.node_names()},
+                 "rank0_batches_per_unit": {k: v.get("batches", 0) for k, v in dep.batcher_stats().items()
+                                            if isinstance(v, dict)},
+                 "rank0_device_batches": {k: v["batches"] for k, v in st["per_device"].items()}}
+            if kind == "mab":
+                r["feedback"] = {"rewarded_branch": world - 1, "rps": fb_out.get("rps"), "error": fb_out.get("error")}
+            graphs[kind] = r
+        except Exception as e:
+            graphs[kind] = {"error": f"{type(e).__name__}: {e}"[:600]}
+        finally:
+            try:
+                if h is not None:
+                    h.stop()
+                if dep is not None:
+                    dep.close()  # stops the peers' loops for this graph
+                else:
+                    fabric.stop_peers()  # keep the workers in step with the graph list
+            except Exception:
+                pass
+        print(json.dumps({"kind": kind, "result": graphs[kind]}), flush=True)
+    fabric.close()
+    print(json.dumps({"rank": rank, "world": world, "device": dev,
+                      "data_plane": "rccl" if dev >= 0 else "sockets"}), flush=True)
+    sys.stdout.flush()
+    os._exit(0)  # no teardown collective: a peer that failed must not hold this child
+
+
+# -------------------------------------------------------------------- main
+def main() -> None:
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if args.variant_child:
+        variant_child(args)
+        return
+    if args.fabric_child:
+        fabric_child(args)
+        return
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, argv))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        sys.exit(2)
+
+    deadline = float(os.environ.get("SCA_BENCH_DEADLINE", T_START + BUDGET_S))
+    budget = bk.Budget(deadline)
+    d = Dist(budget)
+    rep = Reporter(args, d, None, budget)
+    rep.start_watchdog()
+    ex_dir = d.bcast(tempfile.mkdtemp(prefix="sca_bench_") if d.rank == 0 else None)
+    rep.ex = ex = bk.Exchange(ex_dir, d.rank, d.world)
+    per_rank_budget, pinned = place_rank(args, d)
+    per_rank_cpus = size_threads(args, per_rank_budget)
+    extras = args.extras == "auto" and args.graph == "single"
+    inproc, rccl = [], []
+    if extras and d.world >= 2 and args.model in ("iris", "xgb1000"):  # same lists on every rank
+        inproc = [k for k in args.variants.split(",") if k and (k != "pipeline" or d.world >= 4)]
+        rccl = [k for k in args.rank_variants.split(",") if k and (k != "pipeline" or d.world >= 4)]
+    rep.pending = inproc + [f"{k}_rccl" for k in rccl]
+    dep = handle = None
+    try:
+        dep, handle, pb, expect_pb, head_lg = headline(args, d, rep, budget, per_rank_cpus, pinned)
+        if extras:
+            grpc_extra(args, d, rep, budget, handle, pb, expect_pb, head_lg)
+    except Exception as e:
+        rep.ex.put("headline_error", f"rank {d.rank}: {type(e).__name__}: {e}"[:600])
+        if d.rank == 0:
+            print(f"bench.py: rank 0 headline failed: {e}", file=sys.stderr, flush=True)
+    finally:
+        if handle is not None:
+            handle.stop()
+        if dep is not None:
+            dep.close()
+    if inproc or rccl:
+        ex.put("idle", True)
+        if d.rank == 0 and inproc:
+            # others' gRPC windows must be over before rank 0 drives every GPU
+            ex.wait("idle", list(range(d.world)), timeout=max(0.0, min(60.0, budget.left(REPORT_RESERVE_S))))
+            run_inprocess_variants(args, d, rep, budget, inproc)
+        if rccl:
+            run_fabric_phase(args, d, rep, budget, rccl)
+    if d.rank != 0:
+        ex.put("done", True)
+        sys.stdout.flush()
+        os._exit(0)
+    rep.emit()
+    shutil.rmtree(ex_dir, ignore_errors=True)
+    sys.stdout.flush()
+    os._exit(rep.rc)
 
 
 if __name__ == "__main__":

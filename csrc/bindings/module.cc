@@ -81,6 +81,14 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native Seldon-compatible inference graph engine (native core)";
   m.def("version", [] { return std::string("0.1.0"); });
   m.def("gpu_device_count", [] { return gpu::device_count(); });
+  m.def("can_access_peer", [](int dev, int peer) {
+    // hipDeviceCanAccessPeer: whether `dev` can map `peer`'s HBM over xGMI
+    // (recorded per graph placement by bench.py).
+    if (dev == peer) return true;
+    int ok = 0;
+    if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess) return false;
+    return ok != 0;
+  });
 
   // ------------------------------------------------------------- codecs
   m.def("cpu_profile_start", [](int hz, int depth) { return prof::start(hz, size_t(1) << 20, depth); },

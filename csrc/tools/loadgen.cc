@@ -53,6 +53,12 @@ struct Args {
   int warmup = 1;
   long step_requests = 10000;
   bool keepalive = true;
+  // Sampled reply check: every `check_every`-th reply of a worker must contain
+  // `expect` (e.g. the DefaultData bytes of a reference reply); a 200 whose
+  // body differs counts as an error, so a wrong answer inside the timed
+  // region fails the run instead of counting as a prediction.
+  std::string expect;
+  long check_every = 16;
 };
 
 static std::string read_file(const std::string& p) {
@@ -94,6 +100,8 @@ struct StepCtl {
   long limit = 0;
   std::atomic<long> errors{0};
   std::atomic<long> completed{0};
+  std::atomic<long> checked{0};
+  std::atomic<long> bad_body{0};
   bool try_issue() { return issued.fetch_add(1, std::memory_order_relaxed) < limit; }
 };
 
@@ -111,6 +119,16 @@ struct Worker {
   std::string request;  // full HTTP request bytes (REST)
   std::vector<float> lat_us;
   bool record = false;
+  long replies = 0;  // this worker's replies so far (check sampling)
+
+  // true when this reply is sampled and its body lacks the expected bytes
+  bool body_bad(const char* p, size_t n, StepCtl& st) {
+    if (a->expect.empty() || (replies++ % a->check_every) != 0) return false;
+    st.checked.fetch_add(1, std::memory_order_relaxed);
+    if (memmem(p, n, a->expect.data(), a->expect.size()) != nullptr) return false;
+    st.bad_body.fetch_add(1, std::memory_order_relaxed);
+    return true;
+  }
 
   // REST
   std::vector<RestConn> rconns;
@@ -153,8 +171,9 @@ struct Worker {
     if (p != std::string::npos && p < he) cl = size_t(strtoul(c.in.c_str() + p + 15, nullptr, 10));
     if (c.in.size() < he + 4 + cl) return false;
     int status = atoi(c.in.c_str() + 9);
+    const bool bad = status == 200 && body_bad(c.in.data() + he + 4, cl, st);
     c.in.erase(0, he + 4 + cl);
-    if (status != 200) st.errors.fetch_add(1, std::memory_order_relaxed);
+    if (status != 200 || bad) st.errors.fetch_add(1, std::memory_order_relaxed);
     st.completed.fetch_add(1, std::memory_order_relaxed);
     if (record) lat_us.push_back(float(std::chrono::duration<double, std::micro>(Clock::now() - c.t0).count()));
     c.busy = false;
@@ -215,6 +234,7 @@ struct Worker {
     Clock::time_point t0;
     int grpc_status = -1;
     size_t off = 0;
+    std::string body;  // reply bytes (only while checking bodies)
   };
   struct GConn {
     int fd;
@@ -246,11 +266,21 @@ struct Worker {
     if (nl == 11 && !memcmp(name, "grpc-status", 11)) c->streams[f->hd.stream_id].grpc_status = atoi(std::string((const char*)v, vl).c_str());
     return 0;
   }
+  static int g_chunk(nghttp2_session*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* ud) {
+    auto* c = static_cast<GConn*>(ud);
+    if (!c->w->a->expect.empty()) {
+      auto it = c->streams.find(sid);
+      if (it != c->streams.end()) it->second.body.append(reinterpret_cast<const char*>(data), len);
+    }
+    return 0;
+  }
   static int g_close(nghttp2_session*, int32_t sid, uint32_t, void* ud) {
     auto* c = static_cast<GConn*>(ud);
     auto it = c->streams.find(sid);
     if (it == c->streams.end()) return 0;
-    if (it->second.grpc_status != 0) c->st->errors.fetch_add(1, std::memory_order_relaxed);
+    const bool bad = it->second.grpc_status == 0 &&
+                     c->w->body_bad(it->second.body.data(), it->second.body.size(), *c->st);
+    if (it->second.grpc_status != 0 || bad) c->st->errors.fetch_add(1, std::memory_order_relaxed);
     c->st->completed.fetch_add(1, std::memory_order_relaxed);
     if (c->w->record)
       c->w->lat_us.push_back(float(std::chrono::duration<double, std::micro>(Clock::now() - it->second.t0).count()));
@@ -303,6 +333,7 @@ struct Worker {
     nghttp2_session_callbacks_new(&cbs);
     nghttp2_session_callbacks_set_on_header_callback(cbs, g_header);
     nghttp2_session_callbacks_set_on_stream_close_callback(cbs, g_close);
+    nghttp2_session_callbacks_set_on_data_chunk_recv_callback(cbs, g_chunk);
     for (int i = 0; i < nconn; ++i) {
       auto c = std::make_unique<GConn>();
       c->fd = connect_to(a->host, a->port);
@@ -385,6 +416,9 @@ int main(int argc, char** argv) {
     else if (k == "--steps") a.steps = std::stoi(v());
     else if (k == "--warmup") a.warmup = std::stoi(v());
     else if (k == "--step-requests") a.step_requests = std::stol(v());
+    else if (k == "--expect") a.expect = v();
+    else if (k == "--expect-file") a.expect = read_file(v());
+    else if (k == "--check-every") a.check_every = std::max(1L, std::stol(v()));
     else { fprintf(stderr, "unknown arg %s\n", k.c_str()); return 2; }
   }
   if (!body_file.empty()) a.body = read_file(body_file);
@@ -399,7 +433,7 @@ int main(int argc, char** argv) {
     else workers[size_t(t)].init_rest(std::max(1, nc));
   }
   std::vector<double> step_ms;
-  long total_ok = 0, total_err = 0;
+  long total_ok = 0, total_err = 0, total_checked = 0, total_bad = 0;
   double timed_s = 0;
   for (int step = 0; step < a.warmup + a.steps; ++step) {
     const bool timed = step >= a.warmup;
@@ -417,6 +451,8 @@ int main(int argc, char** argv) {
       total_ok += st.completed.load() - st.errors.load();
       total_err += st.errors.load();
     }
+    total_checked += st.checked.load();  // warmup replies are checked too
+    total_bad += st.bad_body.load();
   }
   std::vector<float> lat;
   for (auto& w : workers) lat.insert(lat.end(), w.lat_us.begin(), w.lat_us.end());
@@ -425,11 +461,11 @@ int main(int argc, char** argv) {
   mean = lat.empty() ? 0 : mean / double(lat.size()) / 1000.0;
   printf("{\"mode\":\"%s\",\"users\":%d,\"threads\":%d,\"steps\":%d,\"step_requests\":%ld,\"ok\":%ld,\"errors\":%ld,"
          "\"seconds\":%.6f,\"rps\":%.2f,\"p50_ms\":%.4f,\"p90_ms\":%.4f,\"p99_ms\":%.4f,\"p999_ms\":%.4f,"
-         "\"mean_ms\":%.4f,\"max_ms\":%.4f,\"step_ms\":[",
+         "\"mean_ms\":%.4f,\"max_ms\":%.4f,\"checked\":%ld,\"bad_body\":%ld,\"step_ms\":[",
          a.mode.c_str(), a.users, nthreads, a.steps, a.step_requests, total_ok, total_err, timed_s,
          timed_s > 0 ? double(total_ok) / timed_s : 0.0, pct(lat, 0.5), pct(lat, 0.9), pct(lat, 0.99),
-         pct(lat, 0.999), mean, mx / 1000.0);
+         pct(lat, 0.999), mean, mx / 1000.0, total_checked, total_bad);
   for (size_t i = 0; i < step_ms.size(); ++i) printf("%s%.4f", i ? "," : "", step_ms[i]);
   printf("]}\n");
-  return total_err > 0 ? 1 : 0;
+  return (total_err > 0 || total_bad > 0) ? 1 : 0;
 }
