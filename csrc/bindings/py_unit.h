@@ -330,8 +330,15 @@ class PyUnit : public Unit {
       }
       std::vector<Outcome> res;
       std::vector<ErrPtr> fb_res;
-      if (worker < 0) run_inproc(jobs, res, fb_res);
-      else run_pool(worker, jobs, res, fb_res);
+      try {
+        if (worker < 0) run_inproc(jobs, res, fb_res);
+        else run_pool(worker, jobs, res, fb_res);
+      } catch (const std::exception& e) {  // backstop: a request error must never end the serving thread
+        auto err = make_error(ApiError::MICROSERVICE_ERROR, e.what());
+        res.assign(jobs.size(), Outcome::fail(err));
+        fb_res.assign(1, err);
+      }
+      if (res.size() != jobs.size()) res.resize(jobs.size(), Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "no result")));
       complete(jobs, res, fb_res);
     }
   }
@@ -632,16 +639,34 @@ class PyUnit : public Unit {
       return;
     }
     // dense: text = {"names":[...],"meta":{...}|null,"meta_first":{...}|null}
-    Json info = parse_json(rtext);
-    std::vector<std::string> names;
-    if (const Json* n = info.find("names"))
-      for (const auto& s : n->items()) names.push_back(s.as_string());
-    auto meta_of = [&](const char* key) {
-      const Json* m = info.find(key);
-      return m && !m->is_null() ? m->dump() : std::string();
-    };
-    std::vector<int64_t> yshape(r.shape, r.shape + r.ndim);
-    split_dense(jobs, res, y.data(), yshape, names, meta_of("meta"), meta_of("meta_first"), total);
+    // A worker's reply is untrusted input: its shape must fit the frame and
+    // describe exactly the doubles sent, and a malformed names/meta document
+    // (e.g. a metric with an unknown key) fails these jobs, not the server.
+    try {
+      constexpr uint32_t kMaxDims = sizeof(r.shape) / sizeof(r.shape[0]);
+      if (r.ndim == 0 || r.ndim > kMaxDims) throw std::runtime_error("reply has " + std::to_string(r.ndim) + " dims");
+      uint64_t n = 1;
+      for (uint32_t i = 0; i < r.ndim; ++i) {
+        if (r.shape[i] < 0) throw std::runtime_error("reply has a negative dimension");
+        n *= uint64_t(r.shape[i]);
+      }
+      if (n * sizeof(double) != r.x_bytes)
+        throw std::runtime_error("reply shape holds " + std::to_string(n) + " values but " +
+                                 std::to_string(r.x_bytes / sizeof(double)) + " were sent");
+      Json info = parse_json(rtext);
+      std::vector<std::string> names;
+      if (const Json* nm = info.find("names"))
+        for (const auto& s : nm->items()) names.push_back(s.as_string());
+      auto meta_of = [&](const char* key) {
+        const Json* m = info.find(key);
+        return m && !m->is_null() ? m->dump() : std::string();
+      };
+      std::vector<int64_t> yshape(r.shape, r.shape + r.ndim);
+      split_dense(jobs, res, y.data(), yshape, names, meta_of("meta"), meta_of("meta_first"), total);
+    } catch (const std::exception& e) {
+      auto err = make_error(ApiError::MICROSERVICE_ERROR, std::string("bad reply from python worker: ") + e.what());
+      for (auto& o : res) o = Outcome::fail(err);
+    }
   }
 
   py::object adapter_;

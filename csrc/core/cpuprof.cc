@@ -19,11 +19,16 @@ namespace sca::prof {
 namespace {
 
 std::mutex g_mu;                 // start / stop
-uintptr_t* g_pcs = nullptr;      // samples (program counters)
-size_t g_cap = 0;
+// Sample buffer: allocated once at its maximum size and never freed or
+// resized, so a SIGPROF handler still running from a previous session can
+// only ever write inside it.  The handler bounds every store by kMaxWords
+// with the depth it read itself, whatever start() publishes meanwhile.
+constexpr size_t kMaxWords = size_t(1) << 22;  // 32 MiB of program counters
+std::atomic<uintptr_t*> g_pcs{nullptr};
+std::atomic<size_t> g_cap{0};
 std::atomic<size_t> g_n{0};
 std::atomic<bool> g_on{false};
-int g_depth = 1;                 // frames per sample: 1 = the interrupted PC only
+std::atomic<int> g_depth{1};     // frames per sample: 1 = the interrupted PC only
 std::vector<timer_t> g_timers;   // one CPU-time timer per thread alive at start()
 
 // Per-thread CPU-time clock of thread `tid` (linux/posix-timers.h:
@@ -31,10 +36,12 @@ std::vector<timer_t> g_timers;   // one CPU-time timer per thread alive at start
 clockid_t thread_cpu_clock(pid_t tid) { return clockid_t((~unsigned(tid) << 3) | 4 | 2); }
 
 void on_sigprof(int, siginfo_t*, void* uc) {
-  if (!g_on.load(std::memory_order_relaxed)) return;
+  if (!g_on.load(std::memory_order_acquire)) return;
+  uintptr_t* pcs = g_pcs.load(std::memory_order_relaxed);
+  const size_t depth = size_t(g_depth.load(std::memory_order_relaxed));
   const size_t i = g_n.fetch_add(1, std::memory_order_relaxed);
-  if (i >= g_cap) return;
-  uintptr_t* rec = g_pcs + i * size_t(g_depth);
+  if (pcs == nullptr || i >= g_cap.load(std::memory_order_relaxed) || (i + 1) * depth > kMaxWords) return;
+  uintptr_t* rec = pcs + i * depth;
   const auto* ctx = static_cast<const ucontext_t*>(uc);
 #if defined(__x86_64__)
   rec[0] = uintptr_t(ctx->uc_mcontext.gregs[REG_RIP]);
@@ -42,12 +49,12 @@ void on_sigprof(int, siginfo_t*, void* uc) {
   (void)ctx;
   rec[0] = 0;
 #endif
-  if (g_depth > 1) {
+  if (depth > 1) {
     // Callers through the DWARF unwinder (libgcc, preloaded by start()):
     // frames [0, 1] are this handler and the signal trampoline.
     void* fr[34];
-    const int n = backtrace(fr, std::min(34, g_depth + 2));
-    for (int d = 1; d < g_depth; ++d) rec[d] = d + 1 < n ? uintptr_t(fr[d + 1]) - 1 : 0;
+    const int n = backtrace(fr, std::min(34, int(depth) + 2));
+    for (int d = 1; d < int(depth); ++d) rec[d] = d + 1 < n ? uintptr_t(fr[d + 1]) - 1 : 0;
   }
 }
 
@@ -56,20 +63,14 @@ void on_sigprof(int, siginfo_t*, void* uc) {
 bool start(int hz, size_t max_samples, int depth) {
   std::lock_guard<std::mutex> g(g_mu);
   if (g_on.load() || hz <= 0) return false;
-  g_depth = std::max(1, std::min(depth, 32));
-  if (g_depth > 1) {  // load the unwinder outside signal context
+  depth = std::max(1, std::min(depth, 32));
+  if (depth > 1) {  // load the unwinder outside signal context
     void* fr[4];
     (void)backtrace(fr, 4);
   }
-  // Reuse the sample buffer (grow only): a handler of the previous session
-  // still finishing its store must not write into freed memory.
-  static size_t words = 0;
-  if (max_samples * size_t(g_depth) > words) {
-    delete[] g_pcs;
-    words = max_samples * size_t(g_depth);
-    g_pcs = new uintptr_t[words];
-  }
-  g_cap = max_samples;
+  if (g_pcs.load() == nullptr) g_pcs.store(new uintptr_t[kMaxWords]);  // once; never freed
+  g_depth.store(depth);
+  g_cap.store(std::min(max_samples, kMaxWords / size_t(depth)));
   g_n.store(0);
   struct sigaction sa {};
   sa.sa_sigaction = on_sigprof;
@@ -79,7 +80,7 @@ bool start(int hz, size_t max_samples, int depth) {
   // restoring SIGPROF's default action could let a sample signal still pending
   // at stop() terminate the process.
   if (sigaction(SIGPROF, &sa, nullptr) != 0) return false;
-  g_on.store(true);
+  g_on.store(true, std::memory_order_release);  // publishes buffer, depth and cap to the handler
   // A process-wide ITIMER_PROF coalesces expirations while its signal is
   // pending, so with many busy threads most samples are lost: arm one
   // CPU-time timer per thread instead, each signalling its own thread.
@@ -118,8 +119,10 @@ Profile stop() {
   for (timer_t t : g_timers) timer_delete(t);
   g_timers.clear();
   g_on.store(false);
-  const size_t n = std::min(g_n.load(), g_cap);
-  out.depth = g_depth;
+  const size_t n = std::min(g_n.load(), g_cap.load());
+  const int depth = g_depth.load();
+  out.depth = depth;
+  const uintptr_t* pcs = g_pcs.load();
   std::map<uintptr_t, Loc> locs;
   auto loc = [&](uintptr_t pc) -> const Loc& {
     auto it = locs.find(pc);
@@ -136,8 +139,8 @@ Profile stop() {
   };
   std::map<std::vector<uintptr_t>, uint64_t> stacks;
   for (size_t i = 0; i < n; ++i) {
-    const uintptr_t* rec = g_pcs + i * size_t(g_depth);
-    stacks[std::vector<uintptr_t>(rec, rec + g_depth)]++;
+    const uintptr_t* rec = pcs + i * size_t(depth);
+    stacks[std::vector<uintptr_t>(rec, rec + depth)]++;
   }
   for (const auto& kv : stacks) {
     Sample smp;

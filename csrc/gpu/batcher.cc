@@ -347,6 +347,7 @@ bool BatchedUnit::launch(Slot* s) {
     // message's tensor, or the caller's buffer for run_ptr): no host copy
     // into the pinned slot first (8192 x 784 fp64: 51 MB).
     const bool direct = s->items.size() == 1 && bin >= kDirectH2DBytes;
+    s->direct = direct;
     if (!direct) {
       size_t off = 0;
       for (const auto& it : s->items) {
@@ -525,6 +526,11 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     s->abandoned = false;
     abandoned_slots_.fetch_sub(1, std::memory_order_relaxed);
     if (st != hipSuccess) note_failure();
+    // the device is done with the direct-path source: release / answer it now
+    for (auto& it : s->parked)
+      if (it.caller_mem) it.k(Outcome::fail(s->parked_err));
+    s->parked.clear();
+    s->parked_err.reset();
     return;
   }
   inflight_rows_.fetch_sub(s->rows, std::memory_order_relaxed);
@@ -729,7 +735,15 @@ void BatchedUnit::abandon(Slot* s) {
   note_failure();
   auto e = device_error(ApiError::DEADLINE_EXCEEDED, "GPU batch exceeded the hang watchdog (" +
                                                          std::to_string(opts_.hang_timeout_ms) + " ms)");
-  for (auto& it : items) it.k(Outcome::fail(e));
+  for (auto& it : items) {
+    if (s->direct && it.caller_mem) {  // its buffer is the DMA source: answer once the device lets go
+      s->parked_err = e;
+      s->parked.push_back(std::move(it));
+      continue;
+    }
+    it.k(Outcome::fail(e));
+    if (s->direct) s->parked.push_back(std::move(it));  // keep the request (DMA source) alive
+  }
 }
 
 bool BatchedUnit::take_injected_failure() {
@@ -817,6 +831,7 @@ std::vector<double> BatchedUnit::run_ptr(const double* X, int rows, int cols) {
   Item it;
   it.req = std::move(msg);
   it.xp = X;
+  it.caller_mem = true;
   it.rows = rows;
   it.cols = cols;
   it.k = [&p](Outcome o) { p.set_value(std::move(o)); };

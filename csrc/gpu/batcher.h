@@ -138,6 +138,7 @@ class BatchedUnit : public Unit {
     int cols = 0;
     Done k;
     ExecPtr exec;
+    bool caller_mem = false;  // xp is the run_ptr caller's buffer (freed once the caller is answered)
   };
   struct Slot {
     PinnedBuffer h_in, h_out, h_seg;
@@ -151,6 +152,13 @@ class BatchedUnit : public Unit {
     int cols = 0;
     int out_cols = 0;
     bool abandoned = false;  // watchdog answered its requests; waiting for the device to finish
+    // Direct path (one request >= kDirectH2DBytes DMA'd from its own memory):
+    // a watchdog-abandoned batch keeps the request alive here until the slot's
+    // event completes, since that copy may still be reading it; run_ptr callers
+    // are answered only then (their buffer is the DMA source).
+    bool direct = false;
+    std::vector<Item> parked;
+    ErrPtr parked_err;
     uint64_t roctx = 0;      // marker range of the batch (SCA_ROCTX=1)
     std::chrono::steady_clock::time_point t_launch;
   };

@@ -69,6 +69,8 @@ def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
     ap.add_argument("--push-frequency", type=float, default=None, help="seconds between checkpoints (default 60)")
     ap.add_argument("--pin-cpus", type=int, default=0,
                     help="pin each worker to whole CCDs of its GPU's socket covering this many CPUs (0 = off)")
+    ap.add_argument("--supervise", action="store_true",
+                    help="run even a single worker under the supervisor (SIGHUP rolling updates, restarts)")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -142,8 +144,15 @@ def run_worker(args: argparse.Namespace) -> int:
     def on_signal(signum, frame):  # noqa: ARG001
         stop.set()
 
+    def on_hup(signum, frame):  # noqa: ARG001
+        # SIGHUP's default action would kill the only serving process: a
+        # rolling update needs a supervisor to start the replacement first.
+        if not os.environ.get("SCA_WORKER_RANK"):
+            logger.warning("SIGHUP ignored: rolling updates need the supervisor (--supervise or --gpus > 1)")
+
     signal.signal(signal.SIGTERM, on_signal)
     signal.signal(signal.SIGINT, on_signal)
+    signal.signal(signal.SIGHUP, on_hup)
     stop.wait()
     if explainer is not None:
         explainer.stop()
@@ -171,6 +180,7 @@ class Supervisor:
         self.roll_requested = False
         self.generation = 0
         self.rollouts: List[Dict] = []
+        self._surge: Optional[subprocess.Popen] = None  # the rollout's new worker before it is swapped in
 
     def _start(self, rank: int, ready_file: Optional[str] = None) -> subprocess.Popen:
         env = dict(os.environ)
@@ -204,22 +214,26 @@ class Supervisor:
                     break
                 ready = os.path.join(tmp, f"worker-{rank}.ready")
                 new = self._start(rank, ready)
+                self._surge = new  # terminate() must reach it too
                 deadline = time.monotonic() + self.ready_timeout
-                while not os.path.exists(ready) and new.poll() is None and time.monotonic() < deadline:
+                while (not os.path.exists(ready) and new.poll() is None and time.monotonic() < deadline
+                       and not self.stopping):
                     time.sleep(0.05)
+                if self.stopping:  # SIGTERM arrived mid-rollout: stop the new worker, keep nothing half-done
+                    self._stop_proc(new)
+                    self._surge = None
+                    record["ok"] = False
+                    break
                 if not os.path.exists(ready):
                     logger.error("rollout %d: new worker %d did not become ready; keeping the old one",
                                  self.generation, rank)
-                    if new.poll() is None:
-                        new.send_signal(signal.SIGTERM)
-                        try:
-                            new.wait(timeout=self.drain_timeout)
-                        except subprocess.TimeoutExpired:
-                            new.kill()
+                    self._stop_proc(new)
+                    self._surge = None
                     record["ok"] = False
                     break
                 old = self.procs[rank]
                 self.procs[rank] = new  # from here on the new one is the supervised worker
+                self._surge = None
                 if old.poll() is None:
                     old.send_signal(signal.SIGTERM)  # drain: readiness off, in-flight requests finish
                     try:
@@ -236,9 +250,18 @@ class Supervisor:
         return {"workers": {r: {"pid": p.pid, "alive": p.poll() is None, "restarts": len(self.restarts[r])}
                             for r, p in self.procs.items()}}
 
+    def _stop_proc(self, p: subprocess.Popen) -> None:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+            try:
+                p.wait(timeout=self.drain_timeout)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
     def terminate(self) -> None:
         self.stopping = True
-        for p in self.procs.values():
+        for p in list(self.procs.values()) + ([self._surge] if self._surge is not None else []):
             if p.poll() is None:
                 p.send_signal(signal.SIGTERM)
 
@@ -284,7 +307,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     if args.worker:
         return run_worker(args)
     n = _n_workers(args.gpus)
-    if n == 1:
+    if n == 1 and not args.supervise:
         return run_worker(args)
     raw = list(sys.argv[1:] if argv is None else argv)
     worker_argv: List[str] = []

@@ -333,3 +333,52 @@ def test_unpicklable_component_falls_back_in_process():
         assert dep.predict(PAYLOADS[0])["data"]["ndarray"][0] == [1.0, 2.0, 3.0, 4.0]
     finally:
         dep.close()
+
+
+def test_process_pool_rejects_malformed_worker_replies(monkeypatch):
+    """A worker's reply is untrusted: more dims than the frame holds, a shape
+    that does not match the doubles sent, or a metric the codec rejects fail
+    that request with an error response -- the serving thread survives and
+    the next good reply is served (run_pool decoding)."""
+    import socket
+    import threading
+
+    from seldon_core_amd.serving import adapter as am
+
+    good_txt = json.dumps({"names": ["y"], "meta": None, "meta_first": None}).encode()
+    bad_metric = json.dumps({"names": ["y"], "meta": {"metrics": [{"key": "k", "type": "COUNTER", "value": 1,
+                                                                   "extra": 5}]}, "meta_first": None}).encode()
+    one = np.array([42.0]).tobytes()
+    replies = [
+        am.FRAME.pack(am.MAGIC, 0, 9, 0, *([1] * 8), 8, len(good_txt)) + one + good_txt,  # ndim 9 > 8 slots
+        am.FRAME.pack(am.MAGIC, 0, 2, 0, 5, 5, *([0] * 6), 8, len(good_txt)) + one + good_txt,  # 25 values, 1 sent
+        am.FRAME.pack(am.MAGIC, 0, 2, 0, 1, 1, *([0] * 6), 8, len(bad_metric)) + one + bad_metric,
+        am.FRAME.pack(am.MAGIC, 0, 2, 0, 1, 1, *([0] * 6), 8, len(good_txt)) + one + good_txt,
+    ]
+
+    def rogue_pool(self, n, timeout=120.0):
+        parent, child = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+
+        def serve():
+            for rep in replies:
+                try:
+                    am.recv_frame(child)
+                except Exception:
+                    return
+                child.sendall(rep)
+
+        threading.Thread(target=serve, daemon=True).start()
+        self._rogue = child
+        return [parent.detach()]
+
+    monkeypatch.setattr(am.PythonUnit, "start_pool", rogue_pool)
+    dep = _dep(Plain(), {"workers": 1, "batching": 0})
+    try:
+        for _ in range(3):
+            with pytest.raises(EngineError) as ei:
+                dep.predict({"data": {"ndarray": [[1.0]]}})
+            assert "python worker" in json.dumps(ei.value.args[-1]) or ei.value.args
+        out = dep.predict({"data": {"ndarray": [[1.0]]}})
+        assert out["data"]["ndarray"] == [[42.0]]
+    finally:
+        dep.close()

@@ -262,3 +262,79 @@ def test_rolling_update_swaps_model_version_without_failed_requests(tmp_path):
         if p.poll() is None:
             os.killpg(p.pid, signal.SIGKILL)
             p.wait()
+
+
+def _pgroup_alive(pgid):
+    try:
+        os.killpg(pgid, 0)
+        return True
+    except ProcessLookupError:
+        return False
+
+
+def test_sigterm_during_rollout_stops_the_new_worker(tmp_path):
+    """SIGTERM while a rollout waits for its new worker: the
+    supervisor signals the not-yet-swapped-in worker too and exits; no
+    process of the group outlives it."""
+    (tmp_path / "slow_model.py").write_text(
+        "import time\n"
+        "class SlowModel:\n"
+        "    def __init__(self, version='1'):\n"
+        "        self.v = float(version)\n"
+        "        if self.v > 1:\n"
+        "            time.sleep(4.0)\n"
+        "    def predict(self, X, names=None, meta=None):\n"
+        "        return [[self.v] for _ in range(len(X))]\n")
+
+    def write_spec(version):
+        spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+                "graph": {"name": "m", "type": "MODEL",
+                          "parameters": [{"name": "version", "value": str(version), "type": "STRING"}]}}
+        (tmp_path / "spec.json").write_text(json.dumps(spec))
+
+    write_spec(1)
+    hp, gp = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=f"{ROOT}:{tmp_path}")
+    p = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--spec", str(tmp_path / "spec.json"),
+                          "--gpus", "1", "--supervise", "--device", "-1", "--component", "m=slow_model.SlowModel",
+                          "--http-port", str(hp), "--grpc-port", str(gp), "--admin-port", "0", "--threads", "1",
+                          "--log-level", "WARNING"], env=env, cwd=ROOT, start_new_session=True)
+    try:
+        assert _wait_ready(hp), "engine did not become ready"
+        write_spec(2)
+        p.send_signal(signal.SIGHUP)
+        time.sleep(1.5)  # the new worker is still in its 4 s __init__
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 0
+        deadline = time.monotonic() + 20
+        while _pgroup_alive(p.pid) and time.monotonic() < deadline:
+            time.sleep(0.1)
+        assert not _pgroup_alive(p.pid), "a worker outlived the supervisor"
+    finally:
+        if _pgroup_alive(p.pid):
+            os.killpg(p.pid, signal.SIGKILL)
+        if p.poll() is None:
+            p.wait()
+
+
+def test_single_worker_survives_sighup():
+    """Without a supervisor SIGHUP is logged and ignored (its default action
+    would kill the only serving process)."""
+    hp, gp = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("SCA_WORKER_RANK", None)
+    p = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--gpus", "1", "--device", "-1",
+                          "--http-port", str(hp), "--grpc-port", str(gp), "--admin-port", "0", "--threads", "1",
+                          "--log-level", "WARNING"], env=env, cwd=ROOT, start_new_session=True)
+    try:
+        assert _wait_ready(hp), "engine did not become ready"
+        p.send_signal(signal.SIGHUP)
+        time.sleep(0.5)
+        assert p.poll() is None
+        assert _wait_ready(hp)
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 0
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
