@@ -196,7 +196,12 @@ PYBIND11_MODULE(_C, m) {
         const int rows = int(X.shape(0)), cols = int(X.shape(1));
         const int oc = mdl.out_cols(cols);
         py::array_t<double> out({rows, oc});
-        mdl.run_cpu(X.data(), rows, cols, out.mutable_data());
+        const double* x = X.data();
+        double* y = out.mutable_data();
+        {
+          py::gil_scoped_release nogil;  // concurrent callers (e.g. several batches over one fabric)
+          mdl.run_cpu(x, rows, cols, y);
+        }
         return out;
       });
   m.def("linear_model",
@@ -543,6 +548,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("batches", &par::PeerServer::batches)
       .def_property_readonly("rows", &par::PeerServer::rows)
       .def_property_readonly("host_syncs", &par::PeerServer::host_syncs)
+      .def_property_readonly("max_inflight", &par::PeerServer::max_inflight)
+      .def_property_readonly("slots", &par::PeerServer::slots)
       .def("error", &par::PeerServer::error);
 
   // ------------------------------------------------------------- engine

@@ -6,33 +6,46 @@
 // With one engine process per GPU, the front-end rank keeps the graph and the
 // request queue; children placed on other ranks are reached per micro-batch:
 //
-//   rank 0 (front end)                        rank r (worker)
-//   ------------------                        ---------------
-//   header {op, model, rows, cols} --ctrl-->  blocking read of the header (host)
-//   X [rows, cols] fp64 ---------data------>  posted recv X (stream-ordered)
-//                                             model.launch(X) on the worker's GPU
-//   Y [rows, out_cols] <--------data-------   posted send Y (stream-ordered)
+//   rank 0 (front end)                          rank r (worker)
+//   ------------------                          ---------------
+//   header {seq, op, model, rows, cols} ------> header ring (shared memory,
+//     into the worker's header ring,             sequence-number doorbell)
+//     no syscall                                 polled by the worker thread
+//   X [rows, cols] fp64 --- comm_x / stream_x -> recv into slot k = seq % K
+//                                                model.launch(slot k) on the
+//                                                compute stream
+//   Y [rows, out_cols] <--- comm_y / stream_y -- send from slot k
 //
-// Two planes behind one Transport:
-//  * control: a host socket per (rank 0, worker) pair carries the 16-byte
-//    headers, so the worker learns the batch geometry without a device round
-//    trip -- it posts the payload receive, the kernel and the reply send on its
-//    stream back to back and never waits for the GPU between batches;
-//  * data: RCCL point-to-point on the fabric stream (GPU memory to GPU memory
-//    over xGMI) for GPU fabrics, or the same sockets for CPU fabrics (device -1:
-//    multi-process tests and CPU serving run the identical state machines).
+// Pipelining: the worker owns K batch slots; slot k's receive, kernel and
+// reply are chained with events across three streams, and a slot is reused
+// only once its previous reply has left (device-side waits -- the worker
+// thread never blocks on the GPU).  X travels on one RCCL communicator and Y
+// on a second one, each on its own stream, so the receive of batch k+1
+// overlaps the kernel and reply of batch k, and the front end's send of the
+// next batch is not queued behind the receive of the previous reply.
 //
-// A fan-out to K ranks (COMBINER over replicas on K GPUs) is one RCCL group:
-// the K sends are the broadcast, the K receives the gather, and the combine
-// kernel runs on rank 0's GPU.  All fabric operations of a rank are issued
-// from one thread at a time in one order (a per-fabric mutex), so the sequence
-// each worker observes is exactly header, payload, reply.
+// Two planes:
+//  * control: a shared-memory ring per (rank 0, worker) pair carries the
+//    headers (the ranks share one host); the socket pair made at rendezvous
+//    carries only the ring's name and serves as a liveness check;
+//  * data: RCCL point-to-point (GPU memory to GPU memory over xGMI) for GPU
+//    fabrics, or the sockets for CPU fabrics (device -1: multi-process tests
+//    and CPU serving run the same header ring; a receiver thread per peer
+//    hands replies to concurrent callers in order, and the worker reads
+//    batches ahead of its compute thread, so K batches are in flight too).
+//
+// A fan-out to K ranks (COMBINER over replicas on K GPUs) is one RCCL group
+// per direction: the sends are the broadcast, the receives the gather, and the
+// combine kernel runs on rank 0's GPU.  All issues of a rank happen under one
+// mutex, so every worker sees headers and payloads in one order.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -44,12 +57,26 @@
 
 namespace sca::par {
 
-std::string rccl_unique_id();  // 128 opaque bytes; rank 0 creates, everyone receives it out of band
+// Two 128-byte RCCL ids (X and Y communicators); rank 0 creates, everyone
+// receives them out of band.
+std::string rccl_unique_id();
 
 struct PeerHeader {
   int32_t op = 0, model = 0, rows = 0, cols = 0;
 };
 enum PeerOp : int32_t { kPeerStop = 0, kPeerRun = 1 };
+
+// Single-producer (rank 0) / single-consumer (one worker) header ring in a
+// shared mapping.  Slot i holds header seq when slots[i].seq == seq + 1.
+struct HeaderRing {
+  static constexpr uint32_t kSlots = 256;
+  struct alignas(64) Slot {
+    std::atomic<uint64_t> seq;
+    PeerHeader h;
+  };
+  alignas(64) std::atomic<uint64_t> consumed;  // headers taken by the worker
+  Slot slots[kSlots];
+};
 
 class Fabric {
  public:
@@ -63,29 +90,61 @@ class Fabric {
   int world() const { return world_; }
   int device() const { return device_; }
   bool gpu() const { return device_ >= 0; }
-  ncclComm_t comm() const { return comm_; }
-  hipStream_t stream() const { return stream_.get(); }
+  hipStream_t stream_x() const { return sx_.get(); }
+  hipStream_t stream_y() const { return sy_.get(); }
   std::mutex& issue_mutex() { return mu_; }
-  bool open() const { return open_; }
+  bool open() const { return open_.load(); }
   void close();
 
-  // control plane (host, blocking)
-  void send_header(int peer, const PeerHeader& h);
-  PeerHeader recv_header(int peer);
-  // data plane: GPU fabrics enqueue on stream(); CPU fabrics block
-  void send(const void* p, size_t bytes, int peer);
-  void recv(void* p, size_t bytes, int peer);
+  // control plane: rank 0 publishes, the worker takes (spin, then back off;
+  // throws once the peer's socket is gone)
+  void publish(int peer, const PeerHeader& h);
+  PeerHeader take();
+  // data plane: GPU fabrics enqueue on stream_x (X) / stream_y (Y); CPU
+  // fabrics write / read the sockets
+  void send_x(const void* p, size_t bytes, int peer);
+  void recv_x(void* p, size_t bytes, int peer);
+  void send_y(const void* p, size_t bytes, int peer);
+  void recv_y(void* p, size_t bytes, int peer);
   void group_start();
   void group_end();
 
+  // CPU fabrics, rank 0: queue a reply read (bytes into `dst`) on the peer's
+  // receiver thread; replies arrive in issue order.
+  struct Waiter {
+    std::mutex mu;
+    std::condition_variable cv;
+    int pending = 0;
+    std::string error;
+  };
+  void expect_reply(int peer, void* dst, size_t bytes, std::shared_ptr<Waiter> w);
+
  private:
   int fd(int peer) const;
+  void map_rings();
+  bool peer_gone(int peer) const;
+  void receiver(int peer);
   int rank_, world_, device_;
-  ncclComm_t comm_ = nullptr;
-  gpu::Stream stream_;
+  ncclComm_t comm_x_ = nullptr, comm_y_ = nullptr;
+  gpu::Stream sx_, sy_;
   std::vector<int> fds_;
+  std::vector<HeaderRing*> rings_;  // rank 0: one per worker; worker: rings_[0]
+  std::vector<uint64_t> next_;      // rank 0: next seq per worker; worker: next_[0] to take
   std::mutex mu_;
-  bool open_ = true;
+  std::atomic<bool> open_{true};
+  // CPU reply receivers (rank 0)
+  struct Pending {
+    void* dst;
+    size_t bytes;
+    std::shared_ptr<Waiter> w;
+  };
+  struct RecvQ {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Pending> q;
+    std::thread th;
+  };
+  std::vector<std::unique_ptr<RecvQ>> rq_;
 };
 using FabricPtr = std::shared_ptr<Fabric>;
 
@@ -118,7 +177,7 @@ class PeerRowModel : public gpu::RowModel {
 };
 
 // Worker side: serves the row models placed on this rank until rank 0 sends
-// a stop header.
+// a stop header.  K = SCA_FABRIC_SLOTS (default 4) batches in flight.
 class PeerServer {
  public:
   explicit PeerServer(FabricPtr fabric);
@@ -129,15 +188,19 @@ class PeerServer {
   uint64_t batches() const { return batches_.load(); }
   uint64_t rows() const { return rows_.load(); }
   uint64_t host_syncs() const { return host_syncs_.load(); }  // device waits (buffer growth only)
+  uint64_t max_inflight() const { return max_inflight_.load(); }  // most batches received but not yet answered
+  int slots() const { return slots_; }
   std::string error() const;
 
  private:
   void loop();
   void loop_cpu();
+  void note_inflight(uint64_t n);
   FabricPtr f_;
   std::vector<gpu::RowModelPtr> models_;
   std::thread th_;
-  std::atomic<uint64_t> batches_{0}, rows_{0}, host_syncs_{0};
+  int slots_ = 4;
+  std::atomic<uint64_t> batches_{0}, rows_{0}, host_syncs_{0}, max_inflight_{0};
   mutable std::mutex err_mu_;
   std::string err_;
 };

@@ -63,12 +63,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(world, mode):
+def _run_ranks(world, mode, **extra_env):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", **extra_env)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "fabric_worker.py"), mode],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = []
@@ -105,3 +105,23 @@ def test_native_fabric_api_present():
     C = sca.native()
     for name in ("rccl_unique_id", "Fabric", "PeerServer", "peer_row_model"):
         assert hasattr(C, name)
+
+
+def test_concurrent_senders_keep_k_batches_in_flight_cpu_fabric():
+    """4 concurrent senders x 3 ranks, K = 4 slots per worker: every answer
+    (single peers and the broadcast/gather fan-out) matches sklearn to 1e-12,
+    and the workers really held more than one batch in flight (headers come
+    through the shared-memory ring, payloads are read ahead of compute)."""
+    outs = _run_ranks(3, "concurrent", SCA_FABRIC_SLOTS="4", SCA_FABRIC_WORKER_DELAY_US="3000")
+    front = outs[0]
+    assert front["errors"] == [] and front["worst"] < 1e-12 and front["rows"] > 0, front
+    for w in outs[1:]:
+        assert w["error"] == "" and w["slots"] == 4 and w["batches"] > 0, w
+        assert 2 <= w["max_inflight"] <= 4, w
+
+
+def test_header_ring_liveness_worker_exits_when_front_end_dies():
+    """A worker polling its header ring notices rank 0's death (control
+    socket EOF) and leaves with an error instead of spinning forever."""
+    outs = _run_ranks(2, "orphan")
+    assert "gone" in outs[1]["error"] or "closed" in outs[1]["error"], outs[1]
