@@ -8,6 +8,14 @@ from .serving import (Deployment, EngineError, SeldonComponent, SeldonMicroservi
                       SeldonNotImplementedError)
 from .utils.storage import Storage
 
+
+def __getattr__(name):  # the client pulls in protobuf / grpc: import it on first use
+    if name in ("SeldonClient", "SeldonChannelCredentials", "SeldonCallCredentials"):
+        from . import client
+
+        return getattr(client, name)
+    raise AttributeError(name)
+
 __version__ = "0.1.0"
 
 __all__ = ["Deployment", "EngineError", "SeldonComponent", "SeldonMicroserviceException",

@@ -35,6 +35,55 @@ class SeldonClientException(Exception):
         self.message = message
 
 
+class SeldonChannelCredentials:
+    """TLS for the gateway connection (reference seldon_client.py:27-39).
+
+    Field meanings follow the reference exactly, so existing client code keeps
+    working: ``certificate_chain_file`` is the CA bundle the server is checked
+    against (REST ``verify=``; gRPC ``root_certificates``), ``verify=False``
+    skips server verification (REST), and ``root_certificates_file`` +
+    ``private_key_file`` are the client's own certificate and key (mutual TLS;
+    REST ``cert=(root_certificates_file, private_key_file)``, gRPC
+    ``certificate_chain`` / ``private_key``)."""
+
+    def __init__(self, verify: bool = True, root_certificates_file: Optional[str] = None,
+                 private_key_file: Optional[str] = None, certificate_chain_file: Optional[str] = None):
+        self.verify = verify
+        self.root_certificates_file = root_certificates_file
+        self.private_key_file = private_key_file
+        self.certificate_chain_file = certificate_chain_file
+
+
+class SeldonCallCredentials:
+    """Per-call credentials: a token sent as ``X-Auth-Token`` (REST header /
+    gRPC metadata) on TLS connections (reference seldon_client.py:42-48)."""
+
+    def __init__(self, token: Optional[str] = None):
+        self.token = token
+
+
+def _ssl_context(cc: SeldonChannelCredentials):
+    import ssl
+
+    if cc.certificate_chain_file:
+        ctx = ssl.create_default_context(cafile=cc.certificate_chain_file)
+    else:
+        ctx = ssl.create_default_context()
+        if not cc.verify:
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+    if cc.private_key_file:
+        ctx.load_cert_chain(certfile=cc.root_certificates_file, keyfile=cc.private_key_file)
+    return ctx
+
+
+def _read(path: Optional[str]) -> Optional[bytes]:
+    if not path:
+        return None
+    with open(path, "rb") as f:
+        return f.read()
+
+
 class SeldonClientPrediction:
     def __init__(self, request, response, success: bool = True, msg: str = ""):
         self.request, self.response, self.success, self.msg = request, response, success, msg
@@ -81,7 +130,9 @@ class SeldonClient:
                  gateway_endpoint: str = "localhost:8003", microservice_endpoint: str = "localhost:5000",
                  grpc_max_send_message_length: int = 4 * 1024 * 1024,
                  grpc_max_receive_message_length: int = 4 * 1024 * 1024,
-                 client_return_type: str = "proto", timeout: float = 30.0):
+                 client_return_type: str = "proto", timeout: float = 30.0,
+                 channel_credentials: Optional[SeldonChannelCredentials] = None,
+                 call_credentials: Optional[SeldonCallCredentials] = None):
         self.config = dict(locals())
         del self.config["self"]
 
@@ -100,41 +151,72 @@ class SeldonClient:
     def _ret(self, c, d: Dict, cls=None):
         return d if c["client_return_type"] == "dict" else _to_proto(d, cls)
 
-    def _rest(self, url: str, body: Dict, headers: Optional[Dict] = None, form: bool = False, timeout=30.0) -> Dict:
+    def _rest(self, url: str, body: Dict, headers: Optional[Dict] = None, form: bool = False, timeout=30.0,
+              c: Optional[Dict] = None) -> Dict:
         if form:
             data = ("json=" + urllib.request.quote(json.dumps(body))).encode()
             ctype = "application/x-www-form-urlencoded"
         else:
             data = json.dumps(body).encode()
             ctype = "application/json"
-        req = urllib.request.Request(url, data=data, headers={"Content-Type": ctype, **(headers or {})})
+        hdrs = {"Content-Type": ctype, **self._token_headers(c), **(headers or {})}
+        req = urllib.request.Request(url, data=data, headers=hdrs)
+        cc = (c or {}).get("channel_credentials")
         try:
-            with urllib.request.urlopen(req, timeout=timeout) as r:
+            with urllib.request.urlopen(req, timeout=timeout, context=_ssl_context(cc) if cc else None) as r:
                 return json.loads(r.read())
         except urllib.error.HTTPError as e:
             raise SeldonClientException(e.read().decode())
+        except urllib.error.URLError as e:
+            raise SeldonClientException(f"{url}: {e.reason}")
+
+    @staticmethod
+    def _token_headers(c: Optional[Dict]) -> Dict[str, str]:
+        # the reference sends the call token only on TLS connections
+        if c and c.get("channel_credentials") is not None and c.get("call_credentials") is not None \
+                and c["call_credentials"].token is not None:
+            return {"X-Auth-Token": c["call_credentials"].token}
+        return {}
 
     def _grpc(self, c, endpoint: str, path: str, req_bytes: bytes, metadata=None) -> bytes:
         import grpc
 
         opts = [("grpc.max_send_message_length", c["grpc_max_send_message_length"]),
                 ("grpc.max_receive_message_length", c["grpc_max_receive_message_length"])]
-        with grpc.insecure_channel(endpoint, options=opts) as ch:
+        cc = c.get("channel_credentials")
+        if cc is None:
+            ch = grpc.insecure_channel(endpoint, options=opts)
+        else:  # reference seldon_client.py:1380-1395 (secure channel + X-Auth-Token metadata)
+            creds = grpc.ssl_channel_credentials(root_certificates=_read(cc.certificate_chain_file),
+                                                 private_key=_read(cc.private_key_file),
+                                                 certificate_chain=_read(cc.root_certificates_file))
+            call = c.get("call_credentials")
+            if call is not None and call.token is not None:
+                tok = call.token
+                creds = grpc.composite_channel_credentials(creds, grpc.metadata_call_credentials(
+                    lambda context, callback: callback((("x-auth-token", tok),), None)))
+            ch = grpc.secure_channel(endpoint, creds, options=opts)
+        with ch:
             try:
                 return ch.unary_unary(path)(req_bytes, timeout=c["timeout"], metadata=metadata)
             except grpc.RpcError as e:
                 raise SeldonClientException(f"{e.code()}: {e.details()}")
 
+    @staticmethod
+    def _scheme(c) -> str:
+        return "https://" if c.get("channel_credentials") is not None else "http://"
+
     def _gateway_base(self, c) -> str:
+        sch = self._scheme(c)
         if c["gateway"] == "seldon":
-            return "http://" + c["seldon_rest_endpoint"]
+            return sch + c["seldon_rest_endpoint"]
         dep, ns = c.get("deployment_name"), c.get("namespace")
         prefix = c.get("gateway_prefix")
         if prefix:
-            return "http://" + c["gateway_endpoint"] + prefix
+            return sch + c["gateway_endpoint"] + prefix
         if not dep:
-            return "http://" + c["gateway_endpoint"]
-        return "http://" + c["gateway_endpoint"] + ("/seldon/" + (ns + "/" if ns else "") + dep)
+            return sch + c["gateway_endpoint"]
+        return sch + c["gateway_endpoint"] + ("/seldon/" + (ns + "/" if ns else "") + dep)
 
     def _oauth_headers(self, c) -> Dict[str, str]:
         if c["gateway"] != "seldon" or not c.get("oauth_key"):
@@ -152,7 +234,7 @@ class SeldonClient:
         try:
             if c["transport"] == "rest":
                 url = self._gateway_base(c) + (http_path or "/api/v0.1/predictions")
-                resp = self._rest(url, req, {**self._oauth_headers(c), **(headers or {})}, timeout=c["timeout"])
+                resp = self._rest(url, req, {**self._oauth_headers(c), **(headers or {})}, timeout=c["timeout"], c=c)
             else:
                 endpoint = c["seldon_grpc_endpoint"] if c["gateway"] == "seldon" else c["gateway_endpoint"]
                 md = [("seldon", c.get("deployment_name") or ""), ("namespace", c.get("namespace") or "")]
@@ -175,7 +257,7 @@ class SeldonClient:
         try:
             if c["transport"] == "rest":
                 resp = self._rest(self._gateway_base(c) + "/api/v0.1/feedback", fb, self._oauth_headers(c),
-                                  timeout=c["timeout"])
+                                  timeout=c["timeout"], c=c)
             else:
                 endpoint = c["seldon_grpc_endpoint"] if c["gateway"] == "seldon" else c["gateway_endpoint"]
                 raw = self._grpc(c, endpoint, "/seldon.protos.Seldon/SendFeedback",
@@ -197,7 +279,7 @@ class SeldonClient:
             raise SeldonClientException("gRPC not supported for explain")
         req = _payload(data, bin_data, str_data, None, names, c["payload_type"], shape, None)
         dep, ns = c.get("deployment_name"), c.get("namespace")
-        base = "http://" + c["gateway_endpoint"]
+        base = self._scheme(c) + c["gateway_endpoint"]
         if http_path is not None:
             url = f"{base}/seldon/{ns}/{dep}{http_path}"
         elif gateway_prefix is not None:
@@ -205,9 +287,11 @@ class SeldonClient:
         else:
             url = base + "/seldon/" + (ns + "/" if ns else "") + f"{dep}-explainer/models/{dep}:explain"
         body = json.dumps(req).encode()
-        r = urllib.request.Request(url, data=body, headers={"Content-Type": "application/json", **(headers or {})})
+        r = urllib.request.Request(url, data=body, headers={"Content-Type": "application/json",
+                                                            **self._token_headers(c), **(headers or {})})
+        cc = c.get("channel_credentials")
         try:
-            with urllib.request.urlopen(r, timeout=c["timeout"]) as resp:
+            with urllib.request.urlopen(r, timeout=c["timeout"], context=_ssl_context(cc) if cc else None) as resp:
                 return json.loads(resp.read())
         except urllib.error.HTTPError as e:
             return {"success": False, "response_code": e.code}
