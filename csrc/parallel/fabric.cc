@@ -561,7 +561,7 @@ void PeerServer::loop_cpu() {
           f_->recv_x(b.x.data(), b.x.size() * sizeof(double), 0);
         }
         std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return q.size() < size_t(slots_) || done; });
+        cv.wait(lk, [&] { return q.size() + (computing ? 1 : 0) < size_t(slots_) || done; });  // K slots incl. the one computing
         if (done) return;  // the compute side failed
         const bool stop = b.h.op == kPeerStop;
         q.push_back(std::move(b));
@@ -603,6 +603,7 @@ void PeerServer::loop_cpu() {
     {
       std::lock_guard<std::mutex> lk(mu);
       computing = false;
+      cv.notify_all();
     }
     batches_++;
     rows_ += uint64_t(b.h.rows);

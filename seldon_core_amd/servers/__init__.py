@@ -11,7 +11,6 @@ from __future__ import annotations
 import json
 import logging
 import os
-import pickle
 from typing import Any, Dict, Optional
 
 import numpy as np
@@ -93,9 +92,11 @@ class XGBoostServer:
 
 
 class MLFlowServer:
-    """MLflow-style model directory.  Without the mlflow package the supported
-    flavours are TorchScript (``model.pt``, executed on the GPU by PyTorch-ROCm)
-    and scikit-learn (``model.pkl``/``model.joblib``)."""
+    """MLflow model directory (reference servers/mlflowserver/mlflowserver/
+    MLFlowServer.py:17-45).  With an ``MLmodel`` file the flavour and its
+    artifact come from it and the logged input signature is enforced
+    (``servers/mlflow_model.py``).  Directories without ``MLmodel`` fall back to
+    ``model.pt`` (TorchScript on the GPU) or ``model.joblib``/``model.pkl``."""
 
     def __init__(self, model_uri: str = "", device: Optional[str] = None):
         self.model_uri = model_uri
@@ -103,50 +104,46 @@ class MLFlowServer:
         self.ready = False
         self._fn = None
         self._model = None
+        self.flavour: Optional[str] = None
+        self.signature = None
 
     def load(self) -> None:
+        from .mlflow_model import MLMODEL_FILE, load_mlmodel, load_pytorch, load_sklearn
+
         root = Storage.download(self.model_uri)
-        pt = os.path.join(root, "model.pt")
-        if os.path.exists(pt):
-            import torch
-
-            dev = self.device or ("cuda" if torch.cuda.is_available() else "cpu")
-            mod = torch.jit.load(pt, map_location=dev).eval()
-
-            def fn(X):
-                with torch.no_grad():
-                    t = torch.as_tensor(np.asarray(X, dtype=np.float32), device=dev)
-                    return mod(t).float().cpu().numpy()
-
-            self._fn = fn
+        if os.path.isfile(os.path.join(root, MLMODEL_FILE)):
+            mm, lf = load_mlmodel(root, self.device)
+            self.signature = mm.signature
+        elif os.path.exists(os.path.join(root, "model.pt")):
+            lf = load_pytorch(os.path.join(root, "model.pt"), self.device)
         else:
-            import joblib
-
+            lf = None
             for f in ("model.joblib", "model.pkl"):
                 p = os.path.join(root, f)
                 if os.path.exists(p):
-                    m = joblib.load(p)
-                    self._model = m
-                    self._fn = getattr(m, "predict")
+                    lf = load_sklearn(p)
                     break
-        if self._fn is None:
-            raise FileNotFoundError(f"no supported model flavour in {root}")
+            if lf is None:
+                raise FileNotFoundError(f"no MLmodel file and no supported model flavour in {root}")
+        self.flavour, self._fn, self._model = lf.flavour, lf.predict, lf.model
         self.ready = True
 
-    def predict(self, X, names, meta=None):
+    def predict(self, X, names=None, meta=None):
         if not self.ready:
             self.load()
+        if self.signature is not None:
+            X = self.signature.enforce(X, list(names or ()))
         return self._fn(X)
 
     def row_model(self):
-        """scikit-learn flavour with a native kernel (linear, trees, MLP): the
-        pyfunc ``predict`` is served by the GPU micro-batcher."""
-        m = getattr(self, "_model", None)
+        """sklearn / xgboost flavours with a native kernel (linear, trees, MLP):
+        the pyfunc ``predict`` is served by the GPU micro-batcher."""
+        m = self._model
         if m is None:
             return None
         from ..models import to_row_model
 
-        return to_row_model(m, "predict")
+        return to_row_model(m, "predict") if self.flavour == "sklearn" else to_row_model(m)
 
 
 class TFServingProxy:

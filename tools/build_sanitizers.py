@@ -68,16 +68,27 @@ def _compile(kind: str, src_rel: str, inc: Path) -> Path:
 
 
 def build(kind: str, jobs: int = 8) -> Path:
-    inc, ng = _nghttp2()
-    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(kind, s, inc), SOURCES))
-    out = BUILD / kind / "core_stress"
-    if not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
-        cmd = ["g++", *FLAGS[kind], *map(str, objs), str(ng), f"-Wl,-rpath,{ng.parent}",
-               "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lamdhip64", "-lpthread", "-o", str(out)]
-        res = subprocess.run(cmd, capture_output=True, text=True)
-        if res.returncode != 0:
-            raise RuntimeError(f"[{kind}] link failed\n{res.stderr}")
+    """Compile + link under an exclusive file lock (pytest-xdist workers build
+    the same tree concurrently); the executable is linked to a temporary name
+    and renamed into place so a running copy is never overwritten."""
+    import fcntl
+
+    (BUILD / kind).mkdir(parents=True, exist_ok=True)
+    with open(BUILD / kind / ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        inc, ng = _nghttp2()
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            objs = list(ex.map(lambda s: _compile(kind, s, inc), SOURCES))
+        out = BUILD / kind / "core_stress"
+        if not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+            tmp = out.with_name(f"core_stress.{os.getpid()}.tmp")
+            cmd = ["g++", *FLAGS[kind], *map(str, objs), str(ng), f"-Wl,-rpath,{ng.parent}",
+                   "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lamdhip64", "-lpthread",
+                   "-o", str(tmp)]
+            res = subprocess.run(cmd, capture_output=True, text=True)
+            if res.returncode != 0:
+                raise RuntimeError(f"[{kind}] link failed\n{res.stderr}")
+            os.replace(tmp, out)
     return out
 
 
