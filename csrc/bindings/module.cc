@@ -338,8 +338,32 @@ PYBIND11_MODULE(_C, m) {
         return py::array_t<double>(py::ssize_t(s.size()), s.data());
       })
       .def("set_state", [](gpu::MahalanobisDevice& d, std::vector<double> s) { d.set_state(s); })
+      .def("predict_view", [](const gpu::MahalanobisDevice& d, double threshold) {
+        return std::static_pointer_cast<gpu::RowModel>(d.predict_view(threshold));
+      }, py::arg("threshold"), "RowModel of predictions (score > threshold) over this detector's state")
+      .def("batches", [](const gpu::MahalanobisDevice& d) {
+        const auto st = d.stats();
+        py::dict r;
+        r["batches"] = st.batches;
+        r["requests"] = st.requests;
+        r["rows"] = st.rows;
+        return r;
+      })
       .def_property_readonly("p", &gpu::MahalanobisDevice::p)
       .def_property_readonly("k", &gpu::MahalanobisDevice::k);
+  m.def("mahalanobis_model", [](int p, int k, double n_stdev, double start_clip, double max_n, double eps, int out_mode,
+                                double threshold) {
+    return std::static_pointer_cast<gpu::RowModel>(
+        std::make_shared<gpu::MahalanobisModel>(p, k, n_stdev, start_clip, max_n, eps, out_mode, threshold));
+  }, py::arg("p"), py::arg("k"), py::arg("n_stdev") = 3.0, py::arg("start_clip") = 50.0, py::arg("max_n") = -1.0,
+        py::arg("eps") = 1e-8, py::arg("out_mode") = 1, py::arg("threshold") = 25.0,
+        "Segmented, state-chained Mahalanobis detector RowModel (out_mode 0 scores, 1 predictions)");
+  m.def("mahalanobis_state", [](std::shared_ptr<gpu::RowModel> rm) {
+    auto mm = std::dynamic_pointer_cast<gpu::MahalanobisModel>(rm);
+    if (!mm) throw std::runtime_error("not a Mahalanobis model");
+    auto s = mm->state();
+    return py::array_t<double>(py::ssize_t(s.size()), s.data());
+  });
   m.def("minmax_model", [] { return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MinMaxModel>()); });
   m.def("mean_sigmoid_model", [](double thr) {
     return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::MeanSigmoidModel>(thr));
@@ -831,6 +855,23 @@ PYBIND11_MODULE(_C, m) {
                                      uintptr_t s) {
     return kern::mahalanobis_sm_scores(P<const double>(B), P<const double>(cov0), P<const double>(xd), nb, k_, n,
                                        P<double>(out), as_stream(s));
+  });
+  k.def("maha_step_segments", [](uintptr_t X, uintptr_t seg, int nseg, int p, int k_, double n_stdev, double start_clip,
+                                  double max_n, double eps, int out_mode, double threshold, uintptr_t state,
+                                  uintptr_t ws, uintptr_t out, uintptr_t s) {
+    if (p < 1 || p > kern::kMahaMaxP || k_ < 1 || k_ > std::min(p, kern::kMahaMaxK))
+      throw std::runtime_error("maha_step_segments: 1 <= k <= min(p, 16), p <= 64");
+    kern::MahaParams prm;
+    prm.p = p;
+    prm.k = k_;
+    prm.n_stdev = n_stdev;
+    prm.start_clip = start_clip;
+    prm.max_n = max_n;
+    prm.eps = eps;
+    prm.out_mode = out_mode;
+    prm.threshold = threshold;
+    kern::maha_step_segments(P<const double>(X), P<const int32_t>(seg), nseg, prm, P<double>(state), P<double>(ws),
+                             P<double>(out), as_stream(s));
   });
   k.def("mean_sigmoid_rows_f64", [](uintptr_t in, int rows, int F, double thr, uintptr_t out, uintptr_t s) {
     kern::mean_sigmoid_rows_f64(P<const double>(in), rows, F, thr, P<double>(out), as_stream(s));

@@ -229,6 +229,8 @@ constexpr int kMahaMaxK = 16;
 struct MahaParams {
   int p = 0, k = 0;
   double n_stdev = 3.0, start_clip = 50.0, max_n = -1.0, eps = 1e-8;
+  int out_mode = 0;        // 0: scores, 1: predictions (score > threshold ? 1 : 0)
+  double threshold = 25.0;
 };
 // state layout (doubles): mean[p] | C[p*p] | clip_lo[p] | clip_hi[p] | n | c_zero | has_clip
 inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
@@ -236,6 +238,11 @@ inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
 inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (3 * size_t(p) + 2 * size_t(k)); }
 void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* ws, double* scores,
                hipStream_t stream);
+// Several request batches in order (seg: nseg + 1 row offsets, device-visible):
+// one launch steps the state through each request exactly as nseg maha_step
+// calls would; ws is sized for the largest segment.
+void maha_step_segments(const double* X, const int32_t* seg, int nseg, const MahaParams& prm, double* state,
+                        double* ws, double* out, hipStream_t stream);
 bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd, int nb, int k, double n, double* out,
                            hipStream_t stream);
 

@@ -180,9 +180,12 @@ __device__ double invert_into(const double* A, double* M, double* inv, int k) {
   return det;
 }
 
-__global__ __launch_bounds__(kT) void maha_step_kernel(const double* __restrict__ X, int nb, MahaParams prm,
-                                                       double* __restrict__ state, double* __restrict__ ws,
-                                                       double* __restrict__ scores) {
+// One request's step (CoreMahalanobis._get_preds for X [nb][p]) against the
+// state in HBM; called once per segment by maha_step_kernel.  Callers
+// __syncthreads() between calls: the next segment reads the state this one
+// wrote (same workgroup, same CU: its L1 is coherent at workgroup scope).
+__device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams& prm, double* __restrict__ state,
+                         double* __restrict__ ws, double* __restrict__ scores) {
   __shared__ double Cold[kMahaMaxP * kLd], A[kMahaMaxP * kLd], V[kMahaMaxP * kLd];
   __shared__ double mean0[kMahaMaxP];
   __shared__ double rc[kMahaMaxP / 2], rs[kMahaMaxP / 2];
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(kT) void maha_step_kernel(const double* __restrict_
           const double* dp = DPC + size_t(i) * k;
           for (int e = tid; e < kk; e += kT) P[e] = a * P[e] + cb * dp[e / k] * dp[e % k];
         }
-        if (tid == 0) scores[i] = 0.0;
+        if (tid == 0) scores[i] = prm.out_mode == 1 ? (0.0 > prm.threshold ? 1.0 : 0.0) : 0.0;
         __syncthreads();
         continue;
       }
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(kT) void maha_step_kernel(const double* __restrict_
     double part = 0.0;
     for (int e = tid; e < kk; e += kT) part += d[e / k] * Cp[e] * d[e % k];
     part = block_sum(part, red);
-    if (tid == 0) scores[i] = part;
+    if (tid == 0) scores[i] = prm.out_mode == 1 ? (part > prm.threshold ? 1.0 : 0.0) : part;
     __syncthreads();
   }
   // ---- state update: n, clip bounds from the new covariance diagonal
@@ -418,6 +421,20 @@ __global__ __launch_bounds__(kT) void maha_step_kernel(const double* __restrict_
   }
 }
 
+__global__ __launch_bounds__(kT) void maha_step_kernel(const double* __restrict__ X, const int32_t* __restrict__ seg,
+                                                       int nseg, int nb, MahaParams prm, double* __restrict__ state,
+                                                       double* __restrict__ ws, double* __restrict__ out) {
+  if (seg == nullptr) {
+    maha_one(X, nb, prm, state, ws, out);
+    return;
+  }
+  for (int r = 0; r < nseg; ++r) {
+    const int b = seg[r], e = seg[r + 1];
+    if (e > b) maha_one(X + size_t(b) * prm.p, e - b, prm, state, ws, out + b);
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd, int nb, int k, double n,
@@ -431,7 +448,14 @@ bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd
 void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* ws, double* scores,
                hipStream_t s) {
   if (nb <= 0) return;
-  hipLaunchKernelGGL(maha_step_kernel, dim3(1), dim3(kT), 0, s, X, nb, prm, state, ws, scores);
+  hipLaunchKernelGGL(maha_step_kernel, dim3(1), dim3(kT), 0, s, X, static_cast<const int32_t*>(nullptr), 0, nb, prm,
+                     state, ws, scores);
+}
+
+void maha_step_segments(const double* X, const int32_t* seg, int nseg, const MahaParams& prm, double* state,
+                        double* ws, double* out, hipStream_t s) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(maha_step_kernel, dim3(1), dim3(kT), 0, s, X, seg, nseg, 0, prm, state, ws, out);
 }
 
 }  // namespace sca::kern

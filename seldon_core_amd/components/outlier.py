@@ -232,7 +232,7 @@ class OutlierMahalanobis(_FeedbackMetrics):
     _EPSILON = 1e-8
 
     def __init__(self, threshold=25, n_components=3, n_stdev=3, start_clip=50, max_n=-1, device=None,
-                 gpu_min_rows: int = 0):
+                 gpu_min_rows: int = 0, n_features: Optional[int] = None):
         self.threshold = threshold
         self.n_components = n_components
         self.max_n = max_n
@@ -244,6 +244,7 @@ class OutlierMahalanobis(_FeedbackMetrics):
         self.n = 0
         self.nb_outliers = 0
         self.device = _default_device(device)
+        self.n_features = int(n_features) if n_features else None
         self._dev = None  # native MahalanobisDevice: state resident in HBM (created at the first request)
         self._init_feedback()
 
@@ -252,19 +253,38 @@ class OutlierMahalanobis(_FeedbackMetrics):
 
     # ------------------------------------------------------------ device path
     def _device_for(self, p: int):
-        """The whole _get_preds runs as one kernel launch per request on a GPU
-        (csrc/kernels/mahalanobis.hip: maha_step); p <= 64, k <= 16."""
+        """The whole _get_preds runs on the GPU through the native micro-batcher
+        (csrc/gpu/maha_device.cc): concurrent requests share one
+        single-workgroup launch that steps the HBM-resident state through them
+        in order (csrc/kernels/mahalanobis.hip: maha_step_segments); p <= 64,
+        k <= 16."""
+        if self._dev is not None and self._dev.p == p:
+            return self._dev
         if self.device < 0 or p > 64 or min(self.n_components, p) > 16:
             return None
-        if self._dev is None or self._dev.p != p:
-            from .._native import native
+        return self._make_device(p, self.device)
 
-            self._dev = native().MahalanobisDevice(p, min(self.n_components, p), float(self.n_stdev),
-                                                   float(self.start_clip), float(self.max_n), self._EPSILON,
-                                                   self.device)
-            if self.n:  # state restored / accumulated on the host before the device existed
-                self._push_state(p)
+    def _make_device(self, p: int, device: int):
+        from .._native import native
+
+        self._dev = native().MahalanobisDevice(p, min(self.n_components, p), float(self.n_stdev),
+                                               float(self.start_clip), float(self.max_n), self._EPSILON, device)
+        if self.n:  # state restored / accumulated on the host before the device existed
+            self._push_state(p)
         return self._dev
+
+    def row_model(self):
+        """Native graph node (MODEL): predictions ``score > threshold`` -- the
+        reference's predict() output (CoreMahalanobis.py:148-151) -- served by
+        the micro-batcher with no Python per request.  Needs ``n_features``
+        (the reference learns p from the first request; a native unit is bound
+        before any arrives).  The node shares this object's detector state, so
+        state_dict()/load_state_dict() checkpoint it."""
+        p = self.n_features
+        if not p or p > 64 or min(self.n_components, p) > 16:
+            return None
+        dev = self._dev if (self._dev is not None and self._dev.p == p) else self._make_device(p, self.device)
+        return dev.predict_view(float(self.threshold))
 
     def _push_state(self, p: int) -> None:
         c_zero = isinstance(self.C, int) and self.C == 0

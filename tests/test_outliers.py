@@ -245,3 +245,123 @@ def test_seq2seq_gpu_kernel_matches_cpu():
     np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-7)
     np.testing.assert_array_equal(b, c)
     gpu.net.close()
+
+
+# ------------------------------------------------- native Mahalanobis model
+def _maha_stream(rng, p, sizes, scale=None):
+    scale = np.linspace(0.5, 3.0, p) if scale is None else scale
+    return [rng.normal(size=(nb, p)) * scale + (4.0 if i % 7 == 3 else 0.0) for i, nb in enumerate(sizes)]
+
+
+@pytest.mark.parametrize("p,k,start_clip,max_n", [(9, 3, 50, -1), (6, 6, 10, 40), (1, 1, 5, -1)])
+def test_mahalanobis_native_host_step_matches_numpy(p, k, start_clip, max_n):
+    """The C++ host step (csrc/gpu/maha_device.cc: maha_step_host, the device
+    -1 path of the segmented model) against the numpy oracle: scores and the
+    final state over requests of 1-200 rows, through clipping and max_n."""
+    from seldon_core_amd._native import native
+
+    C = native()
+    rng = np.random.default_rng(p + k)
+    ref = OutlierMahalanobis(threshold=10, n_components=k, start_clip=start_clip, max_n=max_n, device=-1)
+    rm = C.mahalanobis_model(p, k, 3.0, float(start_clip), float(max_n), 1e-8, out_mode=0)
+    for X in _maha_stream(rng, p, [1, 1, 3, 60, 1, 200, 2, 1, 17]):
+        ref.predict(X.copy(), [])
+        got = rm.run_cpu(X).ravel()
+        np.testing.assert_allclose(got, ref.score, rtol=1e-7, atol=1e-9)
+    st = np.asarray(C.mahalanobis_state(rm))
+    np.testing.assert_allclose(st[:p], ref.mean, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(st[p:p + p * p].reshape(p, p), ref.C, rtol=1e-10, atol=1e-12)
+    assert int(st[-3]) == ref.n
+
+
+def test_mahalanobis_row_model_predictions_share_state():
+    """row_model(): the reference predict() output (score > threshold, 1-D)
+    from the native unit; it shares the component's state, so state_dict()
+    sees the requests the native node served."""
+    rng = np.random.default_rng(3)
+    det = OutlierMahalanobis(threshold=8, n_components=2, n_features=4, device=-1)
+    ref = OutlierMahalanobis(threshold=8, n_components=2, device=-1)
+    rm = det.row_model()
+    assert rm is not None and rm.flat_output
+    for X in _maha_stream(rng, 4, [5, 1, 30, 2]):
+        want = ref.predict(X.copy(), [])
+        np.testing.assert_array_equal(rm.run_cpu(X).ravel(), want)
+    st = det.state_dict()
+    assert st["n"] == ref.n == 38
+    np.testing.assert_allclose(st["C"], ref.C, rtol=1e-10)
+    assert OutlierMahalanobis(n_components=2, device=-1).row_model() is None  # p unknown
+
+
+@pytest.mark.gpu
+def test_mahalanobis_segmented_launch_matches_sequential_steps():
+    """maha_step_segments: one launch over 6 requests = 6 sequential steps
+    (host oracle), for scores and predictions."""
+    import torch
+
+    from seldon_core_amd._native import native
+
+    C = native()
+    p, k = 9, 3
+    rng = np.random.default_rng(11)
+    reqs = _maha_stream(rng, p, [1, 4, 1, 57, 2, 1] * 12)
+    host = C.mahalanobis_model(p, k, 3.0, 50.0, -1.0, 1e-8, out_mode=0)
+    want = np.concatenate([host.run_cpu(X).ravel() for X in reqs])
+    X = torch.tensor(np.concatenate(reqs), dtype=torch.float64, device="cuda")
+    seg = torch.tensor(np.concatenate([[0], np.cumsum([len(r) for r in reqs])]), dtype=torch.int32, device="cuda")
+    for mode, thr in ((0, 0.0), (1, 10.0)):
+        state = torch.zeros(p * (p + 3) + 3, dtype=torch.float64, device="cuda")
+        state[-2] = 1.0  # c_zero
+        ws = torch.zeros(60 * (3 * p + 2 * k), dtype=torch.float64, device="cuda")
+        out = torch.full((X.shape[0],), -1.0, dtype=torch.float64, device="cuda")
+        C.kernels.maha_step_segments(X.data_ptr(), seg.data_ptr(), len(reqs), p, k, 3.0, 50.0, -1.0, 1e-8, mode, thr,
+                                     state.data_ptr(), ws.data_ptr(), out.data_ptr(), 0)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        if mode == 0:
+            np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-9)
+            st = state.cpu().numpy()
+            np.testing.assert_allclose(st, np.asarray(C.mahalanobis_state(host)), rtol=1e-9, atol=1e-12)
+        else:
+            close = np.abs(want - thr) < 1e-6 * max(1.0, thr)
+            np.testing.assert_array_equal(got[~close], (want[~close] > thr).astype(float))
+
+
+@pytest.mark.gpu
+def test_mahalanobis_device_concurrent_callers_share_launches():
+    """Concurrent step() callers go through the batcher: every request is
+    stepped exactly once (n = total rows) in fewer launches than requests, and
+    the order-independent state (running mean / covariance before clipping)
+    matches the numpy path on all rows."""
+    import threading
+
+    from seldon_core_amd._native import native
+
+    p, k = 12, 3
+    dev = native().MahalanobisDevice(p, k, 3.0, 1e12, -1.0, 1e-8, 0)
+    rng = np.random.default_rng(5)
+    data = [rng.normal(size=(1, p)) * np.linspace(1, 2, p) for _ in range(1600)]
+    errs = []
+
+    def worker(t):
+        try:
+            for X in data[t::16]:
+                assert dev.step(X).shape == (1,)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errs and not any(t.is_alive() for t in th)
+    st = np.asarray(dev.state())
+    assert int(st[-3]) == 1600
+    b = dev.batches()
+    assert b["requests"] == 1600 and b["batches"] < 1600
+    allX = np.concatenate(data)
+    np.testing.assert_allclose(st[:p], allX.mean(0), rtol=1e-9, atol=1e-12)
+    ref = OutlierMahalanobis(n_components=k, start_clip=10 ** 12, device=-1)
+    for X in data:
+        ref.predict(X.copy(), [])
+    np.testing.assert_allclose(st[p:p + p * p].reshape(p, p), ref.C, rtol=1e-8, atol=1e-11)
