@@ -318,8 +318,19 @@ PYBIND11_MODULE(_C, m) {
     d["w_lds"] = g.w_lds;
     d["lds_bytes"] = g.lds_floats * 4;
     d["workspace_floats_per_wg"] = g.seq_ws_floats;
+    const auto& v = p->valu_program(1);
+    d["valu_ok"] = v.ok;
+    d["valu_kpl"] = v.KPL;
+    d["valu_threads"] = v.threads;
+    d["valu_lds_bytes_r1"] = v.lds_floats * 4;
+    d["valu_lds_bytes_r4"] = p->valu_program(4).lds_floats * 4;
     return d;
   });
+  m.def("lstm_path", [](std::shared_ptr<gpu::RowModel> m, int rows) {
+    auto p = std::dynamic_pointer_cast<gpu::LstmSeqModel>(m);
+    if (!p) throw std::runtime_error("not an LSTM model");
+    return p->path_for(rows);
+  }, "Kernel a batch of `rows` sequences runs: 'valu' (small batches) or 'mfma'");
   py::class_<gpu::MahalanobisDevice, std::shared_ptr<gpu::MahalanobisDevice>>(m, "MahalanobisDevice")
       .def(py::init<int, int, double, double, double, double, int>(), py::arg("p"), py::arg("k"),
            py::arg("n_stdev") = 3.0, py::arg("start_clip") = 50.0, py::arg("max_n") = -1.0, py::arg("eps") = 1e-8,
@@ -858,7 +869,7 @@ PYBIND11_MODULE(_C, m) {
   });
   k.def("maha_step_segments", [](uintptr_t X, uintptr_t seg, int nseg, int p, int k_, double n_stdev, double start_clip,
                                   double max_n, double eps, int out_mode, double threshold, uintptr_t state,
-                                  uintptr_t ws, uintptr_t out, uintptr_t s) {
+                                  uintptr_t eig, uintptr_t ws, uintptr_t out, uintptr_t s) {
     if (p < 1 || p > kern::kMahaMaxP || k_ < 1 || k_ > std::min(p, kern::kMahaMaxK))
       throw std::runtime_error("maha_step_segments: 1 <= k <= min(p, 16), p <= 64");
     kern::MahaParams prm;
@@ -870,8 +881,8 @@ PYBIND11_MODULE(_C, m) {
     prm.eps = eps;
     prm.out_mode = out_mode;
     prm.threshold = threshold;
-    kern::maha_step_segments(P<const double>(X), P<const int32_t>(seg), nseg, prm, P<double>(state), P<double>(ws),
-                             P<double>(out), as_stream(s));
+    kern::maha_step_segments(P<const double>(X), P<const int32_t>(seg), nseg, prm, P<double>(state), P<double>(eig),
+                             P<double>(ws), P<double>(out), as_stream(s));
   });
   k.def("mean_sigmoid_rows_f64", [](uintptr_t in, int rows, int F, double thr, uintptr_t out, uintptr_t s) {
     kern::mean_sigmoid_rows_f64(P<const double>(in), rows, F, thr, P<double>(out), as_stream(s));

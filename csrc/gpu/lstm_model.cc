@@ -2,6 +2,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 namespace sca::gpu {
@@ -168,11 +170,161 @@ void LstmSeqModel::build() {
   for (auto& e : enc_) hmax = std::max(hmax, e.first.H);
   p.Hmax2 = 2 * hmax;
   p.seq_ws_floats = p.n_enc > 1 ? 2LL * R * T_ * p.Hmax2 : 0;
+  build_valu();
+}
+
+// Small-batch VALU programs (csrc/kernels/lstm_valu.hip), appended to the
+// same parameter blob: per cell [H][Q][4][KPL] (k < H: W_hh, then W_ih, zero
+// pad), bias [4][H]; Dense [F][Qy][KPL].  KPL is the smallest of 8/16/32 whose
+// lane layout fits 1024 threads; R = 1, 2, 4 rows per workgroup.
+void LstmSeqModel::build_valu() {
+  for (auto& v : vprog_) v = kern::LstmvProgram();
+  auto pow2 = [](int x) {
+    int q = 1;
+    while (q < x) q <<= 1;
+    return q;
+  };
+  int kpl = 0;
+  int threads = 0;
+  for (int cand : {8, 16, 32}) {
+    auto q_of = [&](int K) { return pow2((K + cand - 1) / cand); };
+    int enc_t = 0;
+    for (auto& e : enc_) enc_t = std::max(enc_t, 2 * round_up(e.first.H * q_of(e.first.H + e.first.in), 64));
+    int dec_t = 0;
+    for (auto& d : dec_) dec_t += round_up(d.H * q_of(d.H + d.in), 64);
+    const int Qy = q_of(dec_.back().H);
+    dec_t += round_up(F_ * Qy, 64);
+    bool qok = Qy <= 64;
+    for (auto& e : enc_) qok = qok && q_of(e.first.H + e.first.in) <= 64;
+    for (auto& d : dec_) qok = qok && q_of(d.H + d.in) <= 64;
+    if (qok && std::max(enc_t, dec_t) <= 1024) {
+      kpl = cand;
+      threads = std::max(enc_t, dec_t);
+      break;
+    }
+  }
+  if (!kpl) return;
+  auto pad4 = [&] { params_.resize(size_t(round_up(int(params_.size()), 4)), 0.f); };
+  auto q_of = [&](int K) { return pow2((K + kpl - 1) / kpl); };
+  struct Packed {
+    long long w_off, b_off;
+    int Q;
+  };
+  auto pack = [&](const LstmWeights& w) {
+    Packed r;
+    const int K = w.H + w.in;
+    r.Q = q_of(K);
+    pad4();
+    r.w_off = (long long)params_.size();
+    for (int u = 0; u < w.H; ++u)
+      for (int q = 0; q < r.Q; ++q)
+        for (int g = 0; g < 4; ++g)
+          for (int j = 0; j < kpl; ++j) {
+            const int k = q * kpl + j, row = g * w.H + u;
+            float v = 0.f;
+            if (k < w.H) v = w.W_hh[size_t(row) * w.H + k];
+            else if (k < K) v = w.W_ih[size_t(row) * w.in + (k - w.H)];
+            params_.push_back(v);
+          }
+    pad4();
+    r.b_off = (long long)params_.size();
+    params_.insert(params_.end(), w.b.begin(), w.b.end());
+    return r;
+  };
+  std::vector<std::pair<Packed, Packed>> penc;
+  for (auto& e : enc_) penc.emplace_back(pack(e.first), pack(e.second));
+  std::vector<Packed> pdec;
+  for (auto& d : dec_) pdec.push_back(pack(d));
+  const int D = dec_.back().H, Qy = q_of(D);
+  pad4();
+  const long long yw = (long long)params_.size();
+  for (int f = 0; f < F_; ++f)
+    for (int q = 0; q < Qy; ++q)
+      for (int j = 0; j < kpl; ++j) {
+        const int k = q * kpl + j;
+        params_.push_back(k < D ? dW_[size_t(f) * D + k] : 0.f);
+      }
+  pad4();
+  const long long yb = (long long)params_.size();
+  params_.insert(params_.end(), db_.begin(), db_.end());
+  pad4();
+
+  const int Rs[3] = {1, 2, 4};
+  for (int ri = 0; ri < 3; ++ri) {
+    const int R = Rs[ri];
+    kern::LstmvProgram& p = vprog_[ri];
+    p.T = T_;
+    p.F = F_;
+    p.n_enc = int(enc_.size());
+    p.n_dec = int(dec_.size());
+    p.R = R;
+    p.KPL = kpl;
+    p.threads = threads;
+    p.D = D;
+    p.Qy = Qy;
+    p.out_act = out_act_;
+    p.yw_off = yw;
+    p.yb_off = yb;
+    int off = 0;
+    p.x_off = off;
+    off += round_up(R * T_ * F_, 4);
+    auto set_cell = [&](kern::LstmvCell& c, const LstmWeights& w, const Packed& pk, int lane0) {
+      c.in = w.in;
+      c.H = w.H;
+      c.Q = pk.Q;
+      c.Kv = pk.Q * kpl;
+      c.lane0 = lane0;
+      c.w_off = pk.w_off;
+      c.b_off = pk.b_off;
+      c.v_off = off;
+      off += 2 * R * c.Kv;
+    };
+    for (size_t l = 0; l < enc_.size(); ++l) {
+      set_cell(p.enc[l][0], enc_[l].first, penc[l].first, 0);
+      set_cell(p.enc[l][1], enc_[l].second, penc[l].second, round_up(enc_[l].first.H * penc[l].first.Q, 64));
+    }
+    int lane = 0;
+    for (size_t l = 0; l < dec_.size(); ++l) {
+      set_cell(p.dec[l], dec_[l], pdec[l], lane);
+      lane += round_up(dec_[l].H * pdec[l].Q, 64);
+    }
+    p.y_lane0 = lane;
+    int hmax = 0;
+    for (auto& e : enc_) hmax = std::max(hmax, e.first.H);
+    p.seq_ld = round_up(2 * hmax, 4);
+    if (enc_.size() > 1) {
+      p.seq_off[0] = off;
+      off += R * T_ * p.seq_ld;
+      p.seq_off[1] = off;
+      off += R * T_ * p.seq_ld;
+    }
+    const int He2 = 2 * enc_.back().first.H;
+    p.hfin_off = off;
+    off += round_up(R * He2, 4);
+    p.cfin_off = off;
+    off += round_up(R * He2, 4);
+    p.mse_off = off;
+    off += round_up(R, 4);
+    p.lds_floats = off;
+    p.ok = off <= kMaxLdsFloats ? 1 : 0;
+  }
+}
+
+std::string LstmSeqModel::path_for(int rows) const {
+  if (const char* e = std::getenv("SCA_LSTM_PATH")) {
+    if (!std::strcmp(e, "mfma")) return "mfma";
+    if (!std::strcmp(e, "valu") && valu_program(4).ok) return "valu";
+  }
+  const int R = (rows + n_cu_ - 1) / n_cu_;
+  return R <= kern::kLstmvMaxRows && valu_program(R).ok ? "valu" : "mfma";
 }
 
 void LstmSeqModel::to_device(int device) {
   d_params_.alloc(params_.size() * sizeof(float), device);
   d_params_.upload(params_.data(), params_.size() * sizeof(float));
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    n_cu_ = prop.multiProcessorCount;
 }
 
 size_t LstmSeqModel::workspace_bytes(int max_rows, int) const {
@@ -181,6 +333,13 @@ size_t LstmSeqModel::workspace_bytes(int max_rows, int) const {
 }
 
 void LstmSeqModel::launch(const double* X, int rows, int, double* out, void* ws, hipStream_t s) {
+  if (path_for(rows) == "valu") {
+    // rows per workgroup: spread the batch over the CUs first (R = 1 up to one sequence per CU)
+    int R = (rows + n_cu_ - 1) / n_cu_;
+    R = R <= 1 ? 1 : R <= 2 ? 2 : 4;
+    kern::lstm_valu_mse(X, rows, valu_program(R), d_params_.as<float>(), out, s);
+    return;
+  }
   kern::lstm_seq2seq_mse(X, rows, prog_, d_params_.as<float>(), static_cast<float*>(ws), out, s);
 }
 

@@ -38,14 +38,22 @@ class LstmSeqModel : public RowModel {
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
   std::shared_ptr<RowModel> clone() const override;
   const kern::LstmProgram& program() const { return prog_; }
+  // Small-batch VALU program for R rows per workgroup (R = 1, 2, 4); ok == 0
+  // when the model does not fit it (the MFMA kernel then serves every batch).
+  const kern::LstmvProgram& valu_program(int R) const { return vprog_[R <= 1 ? 0 : R <= 2 ? 1 : 2]; }
+  // Which kernel a batch of `rows` runs: "valu" or "mfma" (SCA_LSTM_PATH forces one).
+  std::string path_for(int rows) const;
 
  private:
   void build();
+  void build_valu();
   int T_, F_, out_act_;
   std::vector<std::pair<LstmWeights, LstmWeights>> enc_;
   std::vector<LstmWeights> dec_;
   std::vector<float> dW_, db_;
   kern::LstmProgram prog_;
+  kern::LstmvProgram vprog_[3];
+  int n_cu_ = 256;
   std::vector<float> params_;
   DeviceBuffer d_params_;
 };

@@ -259,6 +259,7 @@ void MahalanobisModel::to_device(int device) {
   DeviceGuard dg(device);
   st_->d_state.alloc(st_->h_state.size() * sizeof(double), device);
   st_->d_state.upload(st_->h_state.data(), st_->h_state.size() * sizeof(double));
+  st_->d_eig.alloc(kern::kMahaEigDoubles * sizeof(double), device);  // zeroed: cold start
   st_->chain.create(device);
   st_->device = device;
 }
@@ -278,8 +279,11 @@ void MahalanobisModel::launch_segments(const double* X, int rows, int cols, doub
   std::lock_guard<std::mutex> g(st_->mu);
   // after the previous step on whatever stream it ran
   if (st_->chained) SCA_HIP_CHECK(hipStreamWaitEvent(s, st_->chain.get(), 0));
-  if (seg) kern::maha_step_segments(X, seg, nseg, view_, st_->d_state.as<double>(), static_cast<double*>(ws), out, s);
-  else kern::maha_step(X, rows, view_, st_->d_state.as<double>(), static_cast<double*>(ws), out, s);
+  double* eig = st_->d_eig.as<double>();
+  if (seg)
+    kern::maha_step_segments(X, seg, nseg, view_, st_->d_state.as<double>(), eig, static_cast<double*>(ws), out, s);
+  else
+    kern::maha_step(X, rows, view_, st_->d_state.as<double>(), eig, static_cast<double*>(ws), out, s);
   SCA_HIP_CHECK(hipGetLastError());
   SCA_HIP_CHECK(hipEventRecord(st_->chain.get(), s));
   st_->chained = true;

@@ -31,6 +31,7 @@ struct MahaState {
   kern::MahaParams prm;
   int device = -1;                 // -1: host state (CPU reference path)
   DeviceBuffer d_state;
+  DeviceBuffer d_eig;              // previous eigenvectors (Jacobi warm start; a hint, not state)
   std::vector<double> h_state;     // device -1
   Event chain;                     // completes after the last launched step
   bool chained = false;

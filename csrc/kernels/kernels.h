@@ -236,13 +236,16 @@ struct MahaParams {
 inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
 // workspace doubles for a batch of nb rows
 inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (3 * size_t(p) + 2 * size_t(k)); }
-void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* ws, double* scores,
+// eig: kMahaMaxP * kMahaMaxP + 2 doubles, zero-initialised: the previous
+// step's eigenvectors (warm start of the Jacobi solve; not part of the state).
+constexpr int kMahaEigDoubles = kMahaMaxP * kMahaMaxP + 2;
+void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* eig, double* ws, double* scores,
                hipStream_t stream);
 // Several request batches in order (seg: nseg + 1 row offsets, device-visible):
 // one launch steps the state through each request exactly as nseg maha_step
 // calls would; ws is sized for the largest segment.
 void maha_step_segments(const double* X, const int32_t* seg, int nseg, const MahaParams& prm, double* state,
-                        double* ws, double* out, hipStream_t stream);
+                        double* eig, double* ws, double* out, hipStream_t stream);
 bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd, int nb, int k, double n, double* out,
                            hipStream_t stream);
 
@@ -301,5 +304,36 @@ struct LstmProgram {
 };
 void lstm_seq2seq_mse(const double* X, int rows, const LstmProgram& prog, const float* params, float* ws,
                       double* out, hipStream_t stream);
+
+// Small-batch form of the same model (csrc/kernels/lstm_valu.hip): one
+// workgroup per 1..4 sequences, every gate row's weights resident in VGPRs
+// (4 gates x KPL per lane, Q lanes per unit, DPP group sums), the step's
+// [x | h] vector double-buffered in LDS -- one barrier per encoder step, one
+// per decoder layer + one for the Dense feedback per decoder step.  Used when
+// rows / CUs <= 4 (a 1-sequence request no longer pays the 16-row MFMA tile's
+// dependent MFMA chains).
+constexpr int kLstmvMaxRows = 4;
+struct LstmvCell {
+  int in = 0, H = 0, Q = 0, Kv = 0;  // Kv = Q * KPL (the v row, zero padded past in + H)
+  int lane0 = 0;                     // first thread of the cell (multiple of 64)
+  long long w_off = 0;               // global floats: [H][Q][4][KPL]
+  long long b_off = 0;               // global floats: [4][H] (i, f, g, o)
+  int v_off = 0;                     // LDS floats: v[2][R][Kv]
+};
+struct LstmvProgram {
+  int ok = 0;
+  int T = 0, F = 0, n_enc = 0, n_dec = 0, R = 0, KPL = 0, threads = 0;
+  LstmvCell enc[kLstmMaxLayers][2];
+  LstmvCell dec[kLstmMaxLayers];
+  int D = 0, Qy = 0, y_lane0 = 0, out_act = 0;  // Dense: F outputs x Qy lanes, KPL weights each
+  long long yw_off = 0, yb_off = 0;            // global floats: [F][Qy][KPL], [F]
+  int x_off = 0;                               // LDS: input rows [R][T][F] fp32
+  int seq_off[2] = {0, 0}, seq_ld = 0;         // LDS: encoder output sequences [R][T][seq_ld] (n_enc > 1)
+  int hfin_off = 0, cfin_off = 0;              // LDS: final encoder h / c [R][2 He]
+  int mse_off = 0;                             // LDS: [R]
+  int lds_floats = 0;
+};
+void lstm_valu_mse(const double* X, int rows, const LstmvProgram& prog, const float* params, double* out,
+                   hipStream_t stream);
 
 }  // namespace sca::kern

@@ -130,20 +130,69 @@ __global__ __launch_bounds__(64) void maha_sm_kernel(const double* __restrict__ 
 
 
 // ------------------------------------------------------------ full detector step
-// One 256-thread workgroup runs CoreMahalanobis._get_preds (:68-151) for one
-// request batch against the device-resident state.  p <= 64 features, k <= 16
-// components; p x p matrices live in LDS (row stride kLd = 65 doubles).
-constexpr int kT = 256;
+// One workgroup runs CoreMahalanobis._get_preds (:68-151) for one request
+// batch against the device-resident state: NT = 64 threads (one wave: every
+// barrier is nearly free) for p <= 16, 256 otherwise.  p <= 64 features,
+// k <= 16 components; p x p matrices live in LDS (row stride kLd = 65).
+//
+// Eigenvectors: parallel cyclic Jacobi, warm-started from the previous step's
+// eigenvectors (kept in `eig`, a hint outside the checkpointed state): V is
+// re-orthonormalised by one Newton-Schulz step (V <- 1.5 V - 0.5 V V^T V), A =
+// V^T C V is then nearly diagonal and converges in 1-3 sweeps instead of
+// ~8-10 from the identity.  A round applies every pair's rotation to both
+// sides at once (2 x 2 block B_ij <- J_i^T B_ij J_j), two barriers per round.
+// Converged to the same 1e-15 relative off-diagonal norm as a cold start, so
+// the scores do not depend on the hint (eigenvector signs / order cancel).
 constexpr int kLd = kMahaMaxP + 1;
 constexpr int kMaxSweeps = 40;
 
-__device__ double block_sum(double v, double* red) {
+template <int NT> __device__ double block_sum(double v, double* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  return red[0] + red[1] + red[2] + red[3];
+  if constexpr (NT == 64) {
+    return v;
+  } else {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) t += red[w];
+    return t;
+  }
+}
+
+// C = op(A) . B for m x m LDS matrices (stride kLd), 4 x 4 register tiles;
+// op = transpose when TA.  Rows / columns past m read whatever the 64 x 65
+// buffers hold but only feed outputs that are not written.
+template <int NT, bool TA>
+__device__ void mm(const double* A, const double* B, double* C, int m) {
+  const int tm = (m + 3) >> 2;
+  for (int t = threadIdx.x; t < tm * tm; t += NT) {
+    const int ti = t / tm;
+    const int i0 = ti * 4, j0 = (t - ti * tm) * 4;
+    double acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
+    for (int kx = 0; kx < m; ++kx) {
+      double a[4], b[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = TA ? A[kx * kLd + i0 + r] : A[(i0 + r) * kLd + kx];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) b[c] = B[kx * kLd + j0 + c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] += a[r] * b[c];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (i0 + r < m && j0 + c < m) C[(i0 + r) * kLd + j0 + c] = acc[r][c];
+  }
 }
 
 // Gauss-Jordan with partial pivoting; M and inv are caller-provided (LDS)
@@ -184,13 +233,14 @@ __device__ double invert_into(const double* A, double* M, double* inv, int k) {
 // state in HBM; called once per segment by maha_step_kernel.  Callers
 // __syncthreads() between calls: the next segment reads the state this one
 // wrote (same workgroup, same CU: its L1 is coherent at workgroup scope).
+template <int NT>
 __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams& prm, double* __restrict__ state,
-                         double* __restrict__ ws, double* __restrict__ scores) {
-  __shared__ double Cold[kMahaMaxP * kLd], A[kMahaMaxP * kLd], V[kMahaMaxP * kLd];
+                         double* __restrict__ eig, double* __restrict__ ws, double* __restrict__ scores) {
+  __shared__ double A[kMahaMaxP * kLd], V[kMahaMaxP * kLd], W[kMahaMaxP * kLd], Tm[kMahaMaxP * kLd];
   __shared__ double mean0[kMahaMaxP];
   __shared__ double rc[kMahaMaxP / 2], rs[kMahaMaxP / 2];
   __shared__ int rp[kMahaMaxP / 2], rq[kMahaMaxP / 2];
-  __shared__ double red[4];
+  __shared__ double red[NT / 64];
   __shared__ int sel[kMahaMaxK];
   __shared__ double P[kMahaMaxK * kMahaMaxK], Cp[kMahaMaxK * kMahaMaxK], T1[kMahaMaxK * kMahaMaxK],
       T2[kMahaMaxK * kMahaMaxK];
@@ -213,12 +263,11 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   double* DPC = D + size_t(nb) * p;         // [nb][k] projected (Xc - m)
   double* XD = DPC + size_t(nb) * k;        // [nb][k] projected (X - m)
 
-  for (int e = tid; e < p * p; e += kT) Cold[(e / p) * kLd + e % p] = c_zero ? 0.0 : s_C[e];
-  for (int j = tid; j < p; j += kT) mean0[j] = s_mean[j];
+  for (int j = tid; j < p; j += NT) mean0[j] = s_mean[j];
   __syncthreads();
 
   // ---- clip + running means (sequential in rows, parallel in features)
-  for (int j = tid; j < p; j += kT) {
+  for (int j = tid; j < p; j += NT) {
     const double m0 = mean0[j];
     double cum = 0.0, prev = m0;
     for (int i = 0; i < nb; ++i) {
@@ -237,38 +286,58 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   __syncthreads();
 
   // ---- covariance update: cov = (n-1)/(n+max(1,nb-1)) C + 1/(n+max(1,nb-1)) sum_i coef_i d_i d_i^T
+  // (the old C is read from the state in HBM; the new one is written back
+  // after the projections, which still need the old one)
   const double den = n + fmax(1.0, double(nb) - 1.0);
-  for (int e = tid; e < p * p; e += kT) {
-    const int a = e / p, b = e - a * p;
-    double acc = 0.0;
-    for (int i = 0; i < nb; ++i)
-      acc += ((n + i) / (n + i + 1.0)) * (D[size_t(i) * p + a] * D[size_t(i) * p + b]);
-    const double cov = (n - 1.0) / den * Cold[a * kLd + b] + 1.0 / den * acc;
-    A[a * kLd + b] = cov;
-    s_C[e] = cov;
-  }
-  // ---- eigenvectors: parallel cyclic Jacobi (round-robin pairs, m = p rounded up to even)
   const int m = p + (p & 1);
-  for (int e = tid; e < m * m; e += kT) {
+  for (int e = tid; e < m * m; e += NT) {
     const int a = e / m, b = e - a * m;
-    V[a * kLd + b] = a == b ? 1.0 : 0.0;
-    if (a >= p || b >= p) A[a * kLd + b] = 0.0;  // dummy index of an odd p
+    double cov = 0.0;
+    if (a < p && b < p) {  // dummy index of an odd p stays 0
+      double acc = 0.0;
+      for (int i = 0; i < nb; ++i)
+        acc += ((n + i) / (n + i + 1.0)) * (D[size_t(i) * p + a] * D[size_t(i) * p + b]);
+      cov = (n - 1.0) / den * (c_zero ? 0.0 : s_C[a * p + b]) + 1.0 / den * acc;
+    }
+    A[a * kLd + b] = cov;
+    Tm[a * kLd + b] = cov;  // kept: written to the state after the projections
+  }
+  // ---- eigenvectors: warm-started parallel cyclic Jacobi (m = p rounded up to even)
+  const bool warm = eig[kMahaMaxP * kMahaMaxP] != 0.0 && int(eig[kMahaMaxP * kMahaMaxP + 1]) == m;
+  for (int e = tid; e < m * m; e += NT) {
+    const int a = e / m, b = e - a * m;
+    V[a * kLd + b] = warm ? eig[e] : (a == b ? 1.0 : 0.0);
   }
   __syncthreads();
+  if (warm) {
+    mm<NT, true>(V, V, W, m);  // G = V^T V
+    __syncthreads();
+    mm<NT, false>(V, W, A, m);  // V G (A's copy of C is rebuilt below from Tm)
+    __syncthreads();
+    for (int e = tid; e < m * m; e += NT) {
+      const int a = e / m, b = e - a * m;
+      V[a * kLd + b] = 1.5 * V[a * kLd + b] - 0.5 * A[a * kLd + b];
+    }
+    __syncthreads();
+    mm<NT, false>(Tm, V, W, m);  // C V
+    __syncthreads();
+    mm<NT, true>(V, W, A, m);    // V^T C V
+    __syncthreads();
+  }
   const int half = m / 2;
   for (int sweep = 0; sweep < kMaxSweeps && m > 1; ++sweep) {
     double off = 0.0, all = 0.0;
-    for (int e = tid; e < m * m; e += kT) {
+    for (int e = tid; e < m * m; e += NT) {
       const int a = e / m, b = e - a * m;
       const double v = A[a * kLd + b];
       all += v * v;
       if (a != b) off += v * v;
     }
-    off = block_sum(off, red);
-    all = block_sum(all, red);
+    off = block_sum<NT>(off, red);
+    all = block_sum<NT>(all, red);
     if (off <= 1e-30 * all || off == 0.0) break;
     for (int r = 0; r < m - 1; ++r) {
-      for (int i = tid; i < half; i += kT) {
+      for (int i = tid; i < half; i += NT) {
         const int a = i == 0 ? 0 : 1 + (i + r) % (m - 1);
         const int b = 1 + ((i == 0 ? 0 : m - 1 - i) + r) % (m - 1);
         const int pp = min(a, b), qq = max(a, b);
@@ -286,28 +355,41 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
         rq[i] = qq;
       }
       __syncthreads();
-      for (int e = tid; e < m * half; e += kT) {  // columns: A <- A J, V <- V J
-        const int row = e / half, i = e - row * half;
-        const int pp = rp[i], qq = rq[i];
-        const double c = rc[i], sn = rs[i];
-        const double ap = A[row * kLd + pp], aq = A[row * kLd + qq];
-        A[row * kLd + pp] = c * ap - sn * aq;
-        A[row * kLd + qq] = sn * ap + c * aq;
-        const double vp = V[row * kLd + pp], vq = V[row * kLd + qq];
-        V[row * kLd + pp] = c * vp - sn * vq;
-        V[row * kLd + qq] = sn * vp + c * vq;
-      }
-      __syncthreads();
-      for (int e = tid; e < m * half; e += kT) {  // rows: A <- J^T A
-        const int col = e / half, i = e - col * half;
-        const int pp = rp[i], qq = rq[i];
-        const double c = rc[i], sn = rs[i];
-        const double ap = A[pp * kLd + col], aq = A[qq * kLd + col];
-        A[pp * kLd + col] = c * ap - sn * aq;
-        A[qq * kLd + col] = sn * ap + c * aq;
+      // A <- J^T A J as 2 x 2 blocks of pair rows x pair columns; V <- V J
+      const int nblk = half * half;
+      for (int e = tid; e < nblk + m * half; e += NT) {
+        if (e < nblk) {
+          const int bi = e / half, bj = e - bi * half;
+          const int pi = rp[bi], qi = rq[bi], pj = rp[bj], qj = rq[bj];
+          const double ci = rc[bi], si = rs[bi], cj = rc[bj], sj = rs[bj];
+          const double x00 = A[pi * kLd + pj], x01 = A[pi * kLd + qj], x10 = A[qi * kLd + pj], x11 = A[qi * kLd + qj];
+          const double y00 = cj * x00 - sj * x01, y01 = sj * x00 + cj * x01;
+          const double y10 = cj * x10 - sj * x11, y11 = sj * x10 + cj * x11;
+          A[pi * kLd + pj] = ci * y00 - si * y10;
+          A[pi * kLd + qj] = ci * y01 - si * y11;
+          A[qi * kLd + pj] = si * y00 + ci * y10;
+          A[qi * kLd + qj] = si * y01 + ci * y11;
+        } else {
+          const int f = e - nblk;
+          const int row = f / half, i = f - row * half;
+          const int pp = rp[i], qq = rq[i];
+          const double c = rc[i], sn = rs[i];
+          const double vp = V[row * kLd + pp], vq = V[row * kLd + qq];
+          V[row * kLd + pp] = c * vp - sn * vq;
+          V[row * kLd + qq] = sn * vp + c * vq;
+        }
       }
       __syncthreads();
     }
+  }
+  // the eigenvectors seed the next step
+  for (int e = tid; e < m * m; e += NT) {
+    const int a = e / m, b = e - a * m;
+    eig[e] = V[a * kLd + b];
+  }
+  if (tid == 0) {
+    eig[kMahaMaxP * kMahaMaxP] = 1.0;
+    eig[kMahaMaxP * kMahaMaxP + 1] = double(m);
   }
   // ---- top-k eigenpairs (any order: the scores are invariant to it)
   if (tid == 0) {
@@ -322,19 +404,19 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     }
   }
   __syncthreads();
-  // ---- projections; proj_cov = V^T C_old V
-  for (int e = tid; e < kk; e += kT) {
+  // ---- projections; proj_cov = V^T C_old V over the selected columns (C_old from HBM)
+  for (int e = tid; e < kk; e += NT) {
     const int a = e / k, b = e - a * k;
     double acc = 0.0;
     if (!c_zero)
       for (int r = 0; r < p; ++r) {
         double t = 0.0;
-        for (int c = 0; c < p; ++c) t += Cold[r * kLd + c] * V[c * kLd + sel[b]];
+        for (int c = 0; c < p; ++c) t += s_C[r * p + c] * V[c * kLd + sel[b]];
         acc += V[r * kLd + sel[a]] * t;
       }
     P[e] = acc;
   }
-  for (int e = tid; e < nb * k; e += kT) {
+  for (int e = tid; e < nb * k; e += NT) {
     const int i = e / k, a = e - i * k;
     const double* v = V + sel[a];
     double px = 0.0, pxc = 0.0, pm = 0.0;
@@ -349,6 +431,8 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   }
   if (tid == 0) valid = 0;
   __syncthreads();
+  // new covariance into the state (the projections above read the old one)
+  for (int e = tid; e < p * p; e += NT) s_C[e] = Tm[(e / p) * kLd + e % p];
   // ---- Sherman-Morrison scores (sequential in rows)
   for (int i = 0; i < nb; ++i) {
     const double* d = XD + size_t(i) * k;
@@ -367,7 +451,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
         if (n + i != 0.0) {
           const double a = (n + i - 1.0) / (n + i), cb = 1.0 / (n + i + 1.0);
           const double* dp = DPC + size_t(i) * k;
-          for (int e = tid; e < kk; e += kT) P[e] = a * P[e] + cb * dp[e / k] * dp[e % k];
+          for (int e = tid; e < kk; e += NT) P[e] = a * P[e] + cb * dp[e / k] * dp[e % k];
         }
         if (tid == 0) scores[i] = prm.out_mode == 1 ? (0.0 > prm.threshold ? 1.0 : 0.0) : 0.0;
         __syncthreads();
@@ -376,9 +460,9 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     } else {
       const double a = (n + i - 1.0) / (n + i - 2.0), cb = 1.0 / (n + i);  // B_{i-1} = dpc dpc^T / (n + i)
       const double* dp = DPC + size_t(i - 1) * k;
-      for (int e = tid; e < kk; e += kT) T1[e] = a * Cp[e];
+      for (int e = tid; e < kk; e += NT) T1[e] = a * Cp[e];
       __syncthreads();
-      for (int e = tid; e < kk; e += kT) {  // BC1 = B_{i-1} c_inv
+      for (int e = tid; e < kk; e += NT) {  // BC1 = B_{i-1} c_inv
         const int r = e / k, c = e - r * k;
         double sacc = 0.0;
         for (int j = 0; j < k; ++j) sacc += (cb * dp[r] * dp[j]) * T1[j * k + c];
@@ -391,7 +475,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
         scal = 1.0 / (1.0 + tr);
       }
       __syncthreads();
-      for (int e = tid; e < kk; e += kT) {
+      for (int e = tid; e < kk; e += NT) {
         const int r = e / k, c = e - r * k;
         double sacc = 0.0;
         for (int j = 0; j < k; ++j) sacc += T1[r * k + j] * T2[j * k + c];
@@ -400,16 +484,16 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
       __syncthreads();
     }
     double part = 0.0;
-    for (int e = tid; e < kk; e += kT) part += d[e / k] * Cp[e] * d[e % k];
-    part = block_sum(part, red);
+    for (int e = tid; e < kk; e += NT) part += d[e / k] * Cp[e] * d[e % k];
+    part = block_sum<NT>(part, red);
     if (tid == 0) scores[i] = prm.out_mode == 1 ? (part > prm.threshold ? 1.0 : 0.0) : part;
     __syncthreads();
   }
   // ---- state update: n, clip bounds from the new covariance diagonal
   const double n_new = n_state + nb;
-  for (int j = tid; j < p; j += kT) {
+  for (int j = tid; j < p; j += NT) {
     if (n_new > prm.start_clip) {
-      const double sd = sqrt(s_C[j * p + j]);
+      const double sd = sqrt(Tm[j * kLd + j]);
       s_lo[j] = s_mean[j] - prm.n_stdev * sd;
       s_hi[j] = s_mean[j] + prm.n_stdev * sd;
     }
@@ -421,18 +505,28 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   }
 }
 
-__global__ __launch_bounds__(kT) void maha_step_kernel(const double* __restrict__ X, const int32_t* __restrict__ seg,
+template <int NT>
+__global__ __launch_bounds__(NT) void maha_step_kernel(const double* __restrict__ X, const int32_t* __restrict__ seg,
                                                        int nseg, int nb, MahaParams prm, double* __restrict__ state,
-                                                       double* __restrict__ ws, double* __restrict__ out) {
+                                                       double* __restrict__ eig, double* __restrict__ ws,
+                                                       double* __restrict__ out) {
   if (seg == nullptr) {
-    maha_one(X, nb, prm, state, ws, out);
+    maha_one<NT>(X, nb, prm, state, eig, ws, out);
     return;
   }
   for (int r = 0; r < nseg; ++r) {
     const int b = seg[r], e = seg[r + 1];
-    if (e > b) maha_one(X + size_t(b) * prm.p, e - b, prm, state, ws, out + b);
+    if (e > b) maha_one<NT>(X + size_t(b) * prm.p, e - b, prm, state, eig, ws, out + b);
     __syncthreads();
   }
+}
+
+void launch_step(const double* X, const int32_t* seg, int nseg, int nb, const MahaParams& prm, double* state,
+                 double* eig, double* ws, double* out, hipStream_t s) {
+  if (prm.p <= 16)
+    hipLaunchKernelGGL(maha_step_kernel<64>, dim3(1), dim3(64), 0, s, X, seg, nseg, nb, prm, state, eig, ws, out);
+  else
+    hipLaunchKernelGGL(maha_step_kernel<256>, dim3(1), dim3(256), 0, s, X, seg, nseg, nb, prm, state, eig, ws, out);
 }
 
 }  // namespace
@@ -445,17 +539,16 @@ bool mahalanobis_sm_scores(const double* B, const double* cov0, const double* xd
   return true;
 }
 
-void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* ws, double* scores,
-               hipStream_t s) {
+void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* eig, double* ws,
+               double* scores, hipStream_t s) {
   if (nb <= 0) return;
-  hipLaunchKernelGGL(maha_step_kernel, dim3(1), dim3(kT), 0, s, X, static_cast<const int32_t*>(nullptr), 0, nb, prm,
-                     state, ws, scores);
+  launch_step(X, nullptr, 0, nb, prm, state, eig, ws, scores, s);
 }
 
 void maha_step_segments(const double* X, const int32_t* seg, int nseg, const MahaParams& prm, double* state,
-                        double* ws, double* out, hipStream_t s) {
+                        double* eig, double* ws, double* out, hipStream_t s) {
   if (nseg <= 0) return;
-  hipLaunchKernelGGL(maha_step_kernel, dim3(1), dim3(kT), 0, s, X, seg, nseg, 0, prm, state, ws, out);
+  launch_step(X, seg, nseg, 0, prm, state, eig, ws, out, s);
 }
 
 }  // namespace sca::kern

@@ -37,6 +37,22 @@ def test_program_layout():
     assert pb["w_lds"] == 0 and pb["workspace_floats_per_wg"] == 2 * 16 * 8 * 128
 
 
+def test_valu_program_layout():
+    """Small-batch VALU kernel (csrc/kernels/lstm_valu.hip): the reference ECG
+    shape fits with KPL = 8 (encoder 2 x 128 threads, decoder 320 + 64 for the
+    Dense lanes); a model too wide for 1024 lanes falls back to MFMA."""
+    C = sca.native()
+    net = Seq2SeqLSTMNet(1, (20,), (40,), "sigmoid", -1)
+    m = net.native_model(140)
+    p = C.lstm_program(m)
+    assert p["valu_ok"] == 1 and p["valu_kpl"] == 8 and p["valu_threads"] == 384
+    assert p["valu_lds_bytes_r4"] <= 160 * 1024
+    assert C.lstm_path(m, 1) == "valu" and C.lstm_path(m, 4 * 256) == "valu" and C.lstm_path(m, 4 * 256 + 1) == "mfma"
+    big = Seq2SeqLSTMNet(32, (64, 64), (128,), "sigmoid", -1)
+    assert C.lstm_program(big.native_model(8))["valu_ok"] == 0
+    assert C.lstm_path(big.native_model(8), 1) == "mfma"
+
+
 def test_rejects_incompatible_decoder():
     with pytest.raises(ValueError):
         Seq2SeqLSTMNet(1, (20,), (20,), "sigmoid", -1)
@@ -45,7 +61,10 @@ def test_rejects_incompatible_decoder():
 @pytest.mark.gpu
 @pytest.mark.parametrize("F,T,enc,dec,act", SHAPES + [(32, 8, (64, 64), (128,), "sigmoid")])
 @pytest.mark.parametrize("rows", [1, 16, 37])
-def test_gpu_kernel_matches_torch_fp32(F, T, enc, dec, act, rows):
+@pytest.mark.parametrize("path", ["auto", "mfma", "valu"])
+def test_gpu_kernel_matches_torch_fp32(F, T, enc, dec, act, rows, path, monkeypatch):
+    if path != "auto":
+        monkeypatch.setenv("SCA_LSTM_PATH", path)
     C = sca.native()
     net = Seq2SeqLSTMNet(F, enc, dec, act, -1, seed=rows)
     X = np.random.default_rng(rows).random((rows, T, F))
@@ -73,3 +92,21 @@ def test_detector_scores_on_gpu():
         assert det.net._units  # the native kernel ran
     finally:
         det.net.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [300, 700])
+def test_gpu_valu_multi_row_workgroups(rows):
+    """Batches past one sequence per CU: the VALU kernel packs R = 2 / 4
+    sequences per workgroup."""
+    C = sca.native()
+    net = Seq2SeqLSTMNet(2, (10,), (20,), "sigmoid", -1, seed=5)
+    X = np.random.default_rng(rows).random((rows, 30, 2))
+    m = net.native_model(30)
+    assert C.lstm_path(m, rows) == "valu"
+    unit = C.BatchedUnit(m, 0, max_batch=4096)
+    try:
+        got = np.asarray(unit.run(X.reshape(rows, -1)))[:, 0]
+    finally:
+        unit.stop()
+    np.testing.assert_allclose(got, _torch_mse(net, X), rtol=1e-4, atol=1e-7)

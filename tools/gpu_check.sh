@@ -42,6 +42,11 @@ for s in $STEPS; do
       export TMPDIR=/tmp
       run prof_xgb 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_xgb" -o run --output-format csv -- \
         python3 bench.py --model xgb1000 --steps 3 --warmup 1 --step-requests 10000 ;;
+    lstm) run lstm 300 python tools/kernel_microbench.py --only lstm --iters 20 ;;
+    prof_lstm)
+      export TMPDIR=/tmp
+      run prof_lstm 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_lstm" -o run --output-format csv -- \
+        python3 tools/kernel_microbench.py --only lstm --iters 10 ;;
     maha) run maha 300 python tools/maha_bench.py --p 9 64 --requests 2000 --threads 16 --out "$OUT/maha.json" ;;
     prof_maha)
       export TMPDIR=/tmp

@@ -359,7 +359,8 @@ def case_latency(iters):
 
 def case_lstm(iters):
     """seq2seq LSTM detector (ECG-shaped: T=140, F=1, BiLSTM 20 -> LSTM 40 -> Dense),
-    one persistent kernel per batch, vs the torch eager decode loop."""
+    one persistent kernel per batch: the small-batch VALU kernel and the 16-row
+    MFMA kernel at each batch size, vs the torch eager decode loop."""
     import torch
 
     from seldon_core_amd import native
@@ -368,26 +369,31 @@ def case_lstm(iters):
     C = native()
     T, F = 140, 1
     net = Seq2SeqLSTMNet(F, (20,), (40,), "sigmoid", 0, 0)
-    for rows in (16, 1024):
+    for rows in (1, 16, 256, 1024, 4096):
         X = np.random.default_rng(3).random((rows, T, F))
-        unit = C.BatchedUnit(net.native_model(T), 0, max_batch=4096)
-        try:
-            got = np.asarray(unit.run(X.reshape(rows, -1)))[:, 0]
-            if os.environ.get("SCA_PMC"):  # counter passes: only the kernel (torch's eager loop floods the trace)
-                ref, torch_us = got, 0.0
-            else:
-                ref = np.mean((X - net.reconstruct(X)) ** 2, axis=(1, 2))
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                for _ in range(3):
-                    net.reconstruct(X)
-                torch.cuda.synchronize()
-                torch_us = (time.perf_counter() - t0) / 3 * 1e6
-            _time_unit("lstm", unit, X.reshape(rows, -1), iters,
-                       {"T": T, "F": F, "enc": 20, "dec": 40, "torch_eager_us": round(torch_us, 1),
-                        "max_rel_err_vs_torch": float(np.max(np.abs(got - ref) / np.abs(ref)))})
-        finally:
-            unit.stop()
+        ref, torch_us = None, 0.0
+        if rows in (16, 1024) and not os.environ.get("SCA_PMC"):
+            ref = np.mean((X - net.reconstruct(X)) ** 2, axis=(1, 2))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                net.reconstruct(X)
+            torch.cuda.synchronize()
+            torch_us = (time.perf_counter() - t0) / 3 * 1e6
+        for path in ("valu", "mfma"):
+            if path == "valu" and rows > 1024:
+                continue
+            os.environ["SCA_LSTM_PATH"] = path
+            unit = C.BatchedUnit(net.native_model(T), 0, max_batch=4096)
+            try:
+                got = np.asarray(unit.run(X.reshape(rows, -1)))[:, 0]
+                err = float(np.max(np.abs(got - ref) / np.abs(ref))) if ref is not None else None
+                _time_unit("lstm_" + path, unit, X.reshape(rows, -1), iters if rows <= 1024 else max(3, iters // 5),
+                           {"T": T, "F": F, "enc": 20, "dec": 40, "torch_eager_us": round(torch_us, 1),
+                            "max_rel_err_vs_torch": err})
+            finally:
+                unit.stop()
+        os.environ.pop("SCA_LSTM_PATH", None)
 
 
 def main():
