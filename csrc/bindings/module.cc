@@ -349,6 +349,16 @@ PYBIND11_MODULE(_C, m) {
         return py::array_t<double>(py::ssize_t(s.size()), s.data());
       })
       .def("set_state", [](gpu::MahalanobisDevice& d, std::vector<double> s) { d.set_state(s); })
+      .def("jacobi_stats", [](const gpu::MahalanobisDevice& d) {
+        const auto t = d.jacobi_stats();
+        py::dict r;
+        if (t.size() == 3) {
+          r["last_sweeps"] = t[0];
+          r["steps"] = t[1];
+          r["mean_sweeps"] = t[1] > 0 ? t[2] / t[1] : 0.0;
+        }
+        return r;
+      })
       .def("predict_view", [](const gpu::MahalanobisDevice& d, double threshold) {
         return std::static_pointer_cast<gpu::RowModel>(d.predict_view(threshold));
       }, py::arg("threshold"), "RowModel of predictions (score > threshold) over this detector's state")

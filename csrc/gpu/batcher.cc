@@ -67,6 +67,7 @@ FaultSpec fault_from_env(int device) {
 }
 
 BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::move(model)), opts_(opts) {
+  if (const char* e = std::getenv("SCA_IDLE_SPIN_US")) idle_spin_us_ = std::max(0, std::atoi(e));
   if (opts_.max_batch < 1) opts_.max_batch = 1;
   if (opts_.slots < 1) opts_.slots = 1;
   if (opts_.fail_threshold < 1) opts_.fail_threshold = 1;
@@ -453,6 +454,12 @@ void BatchedUnit::handoff_loop() {
       std::unique_lock<std::mutex> lk(ho_mu_);
       for (auto& h : batch) ho_free_.push_back(std::move(h));  // emptied below: capacity goes back
       batch.clear();
+      if (ho_q_.empty() && !ho_stop_ && idle_spin_us_ > 0) {  // brief spin before sleeping (see device_loop)
+        lk.unlock();
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(idle_spin_us_);
+        while (!ho_pending_.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < until) _mm_pause();
+        lk.lock();
+      }
       if (ho_q_.empty()) {
         if (ho_stop_) break;
         ho_sleeping_ = true;
@@ -461,6 +468,7 @@ void BatchedUnit::handoff_loop() {
         if (ho_q_.empty()) break;  // stopping with nothing left
       }
       batch.swap(ho_q_);
+      ho_pending_.store(false, std::memory_order_relaxed);
     }
     for (auto& h : batch) post_responses(h, spare);
   }
@@ -576,6 +584,7 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
         ho_q_.push_back(std::move(h));
         wake = ho_sleeping_;
       }
+      ho_pending_.store(true, std::memory_order_release);
       if (wake) ho_cv_.notify_one();
     }
   }
@@ -600,6 +609,17 @@ void BatchedUnit::device_loop() {
     // ---- take what the front ends queued (O(1) under the lock: producers
     // never wait behind batch formation), then launch everything that fits
     // into the free slots from the device thread's own backlog
+    if (inflight.empty() && pending.empty()) {
+      // Brief idle spin first: a closed-loop caller's next request usually
+      // arrives within tens of microseconds, and a condition-variable wake-up
+      // costs about that much again.
+      if (idle_spin_us_ > 0 && queued_n_.load(std::memory_order_acquire) == 0) {
+        const auto until = clk::now() + std::chrono::microseconds(idle_spin_us_);
+        while (queued_n_.load(std::memory_order_acquire) == 0 && running_.load(std::memory_order_relaxed) &&
+               clk::now() < until)
+          _mm_pause();
+      }
+    }
     if (inflight.empty() && pending.empty()) {
       std::unique_lock<std::mutex> lk(mu_);
       dev_sleeping_.store(true, std::memory_order_seq_cst);

@@ -306,6 +306,17 @@ std::vector<double> MahalanobisModel::state() const {
   return s;
 }
 
+std::vector<double> MahalanobisModel::jacobi_stats() const {
+  std::lock_guard<std::mutex> g(st_->mu);
+  if (st_->device < 0) return {};
+  DeviceGuard dg(st_->device);
+  if (st_->chained) SCA_HIP_CHECK(hipEventSynchronize(st_->chain.get()));
+  std::vector<double> t(3);
+  SCA_HIP_CHECK(hipMemcpy(t.data(), st_->d_eig.as<double>() + kern::kMahaMaxP * kern::kMahaMaxP + 2,
+                          3 * sizeof(double), hipMemcpyDeviceToHost));
+  return t;
+}
+
 void MahalanobisModel::set_state(const std::vector<double>& s) {
   std::lock_guard<std::mutex> g(st_->mu);
   if (s.size() != kern::maha_state_doubles(st_->prm.p)) throw std::runtime_error("Mahalanobis: bad state size");

@@ -61,6 +61,8 @@ class MahalanobisModel : public RowModel {
   std::vector<double> state() const;  // mean[p] | C[p*p] | lo[p] | hi[p] | n | c_zero | has_clip
   void set_state(const std::vector<double>& s);
   std::shared_ptr<MahaState> shared_state() const { return st_; }
+  // Jacobi diagnostics: {sweeps of the last step, steps, total sweeps} (GPU state only).
+  std::vector<double> jacobi_stats() const;
   int p() const { return st_->prm.p; }
   int k() const { return st_->prm.k; }
   int device() const { return st_->device; }
@@ -85,6 +87,7 @@ class MahalanobisDevice {
   // Predictions view over the same state (for a native graph node).
   std::shared_ptr<MahalanobisModel> predict_view(double threshold) const;
   BatcherStats stats() const { return unit_->stats(); }
+  std::vector<double> jacobi_stats() const { return model_->jacobi_stats(); }
   int p() const { return model_->p(); }
   int k() const { return model_->k(); }
   int device() const { return model_->device(); }

@@ -235,10 +235,11 @@ struct MahaParams {
 // state layout (doubles): mean[p] | C[p*p] | clip_lo[p] | clip_hi[p] | n | c_zero | has_clip
 inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
 // workspace doubles for a batch of nb rows
-inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (3 * size_t(p) + 2 * size_t(k)); }
-// eig: kMahaMaxP * kMahaMaxP + 2 doubles, zero-initialised: the previous
+inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (4 * size_t(p) + 2 * size_t(k)); }
+// eig: kMahaEigDoubles doubles, zero-initialised: the previous
 // step's eigenvectors (warm start of the Jacobi solve; not part of the state).
-constexpr int kMahaEigDoubles = kMahaMaxP * kMahaMaxP + 2;
+// Tail: [has_v, m, sweeps of the last step, steps, total sweeps] (diagnostics after the first two).
+constexpr int kMahaEigDoubles = kMahaMaxP * kMahaMaxP + 5;
 void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* eig, double* ws, double* scores,
                hipStream_t stream);
 // Several request batches in order (seg: nseg + 1 row offsets, device-visible):

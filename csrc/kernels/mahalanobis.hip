@@ -260,7 +260,8 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   double* XC = ws;                          // [nb][p] clipped rows
   double* MO = XC + size_t(nb) * p;         // [nb][p] means_offset
   double* D = MO + size_t(nb) * p;          // [nb][p] Xc - means_offset
-  double* DPC = D + size_t(nb) * p;         // [nb][k] projected (Xc - m)
+  double* XR = D + size_t(nb) * p;          // [nb][p] raw rows (X may be host memory: read it once)
+  double* DPC = XR + size_t(nb) * p;        // [nb][k] projected (Xc - m)
   double* XD = DPC + size_t(nb) * k;        // [nb][k] projected (X - m)
 
   for (int j = tid; j < p; j += NT) mean0[j] = s_mean[j];
@@ -270,9 +271,11 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   for (int j = tid; j < p; j += NT) {
     const double m0 = mean0[j];
     double cum = 0.0, prev = m0;
+    const double lo = do_clip ? s_lo[j] : 0.0, hi = do_clip ? s_hi[j] : 0.0;
     for (int i = 0; i < nb; ++i) {
       double x = X[size_t(i) * p + j];
-      if (do_clip) x = fmin(fmax(x, s_lo[j]), s_hi[j]);
+      XR[size_t(i) * p + j] = x;
+      if (do_clip) x = fmin(fmax(x, lo), hi);
       cum += x;
       const double roll = cum / double(i + 1);
       const double nm = m0 + (double(i + 1) / (double(i) + n + 1.0)) * (roll - m0);
@@ -325,7 +328,8 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     __syncthreads();
   }
   const int half = m / 2;
-  for (int sweep = 0; sweep < kMaxSweeps && m > 1; ++sweep) {
+  int sweeps = 0;
+  for (int sweep = 0; sweep < kMaxSweeps && m > 1; ++sweep, ++sweeps) {
     double off = 0.0, all = 0.0;
     for (int e = tid; e < m * m; e += NT) {
       const int a = e / m, b = e - a * m;
@@ -388,8 +392,12 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     eig[e] = V[a * kLd + b];
   }
   if (tid == 0) {
-    eig[kMahaMaxP * kMahaMaxP] = 1.0;
-    eig[kMahaMaxP * kMahaMaxP + 1] = double(m);
+    double* tail = eig + kMahaMaxP * kMahaMaxP;
+    tail[0] = 1.0;
+    tail[1] = double(m);
+    tail[2] = double(sweeps);
+    tail[3] += 1.0;
+    tail[4] += double(sweeps);
   }
   // ---- top-k eigenpairs (any order: the scores are invariant to it)
   if (tid == 0) {
@@ -403,18 +411,17 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
       sel[a] = best;
     }
   }
+  // ---- projections; proj_cov = V^T C_old V over the selected columns:
+  // C_old (still in HBM) -> W, U = C_old V_sel -> A (free after the
+  // selection), P = V_sel^T U
+  for (int e = tid; e < p * p; e += NT) W[(e / p) * kLd + e % p] = c_zero ? 0.0 : s_C[e];
   __syncthreads();
-  // ---- projections; proj_cov = V^T C_old V over the selected columns (C_old from HBM)
-  for (int e = tid; e < kk; e += NT) {
-    const int a = e / k, b = e - a * k;
-    double acc = 0.0;
-    if (!c_zero)
-      for (int r = 0; r < p; ++r) {
-        double t = 0.0;
-        for (int c = 0; c < p; ++c) t += s_C[r * p + c] * V[c * kLd + sel[b]];
-        acc += V[r * kLd + sel[a]] * t;
-      }
-    P[e] = acc;
+  for (int e = tid; e < p * k; e += NT) {
+    const int r = e / k, b = e - r * k;
+    const double* vb = V + sel[b];
+    double t = 0.0;
+    for (int c = 0; c < p; ++c) t += W[r * kLd + c] * vb[c * kLd];
+    A[r * kLd + b] = t;
   }
   for (int e = tid; e < nb * k; e += NT) {
     const int i = e / k, a = e - i * k;
@@ -422,12 +429,20 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     double px = 0.0, pxc = 0.0, pm = 0.0;
     for (int j = 0; j < p; ++j) {
       const double w = v[j * kLd];
-      px += X[size_t(i) * p + j] * w;
+      px += XR[size_t(i) * p + j] * w;
       pxc += XC[size_t(i) * p + j] * w;
       pm += MO[size_t(i) * p + j] * w;
     }
     DPC[e] = pxc - pm;
     XD[e] = px - pm;
+  }
+  __syncthreads();
+  for (int e = tid; e < kk; e += NT) {
+    const int a = e / k, b = e - a * k;
+    const double* va = V + sel[a];
+    double acc = 0.0;
+    for (int r = 0; r < p; ++r) acc += va[r * kLd] * A[r * kLd + b];
+    P[e] = acc;
   }
   if (tid == 0) valid = 0;
   __syncthreads();
