@@ -264,6 +264,14 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   double* DPC = XR + size_t(nb) * p;        // [nb][k] projected (Xc - m)
   double* XD = DPC + size_t(nb) * k;        // [nb][k] projected (X - m)
 
+  uint64_t t_prev = __builtin_amdgcn_s_memrealtime(), ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  auto stamp = [&](int i) {  // phase timer (100 MHz), thread 0; accumulated into eig's tail
+    if (tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      ph[i] += t - t_prev;
+      t_prev = t;
+    }
+  };
   for (int j = tid; j < p; j += NT) mean0[j] = s_mean[j];
   __syncthreads();
 
@@ -287,6 +295,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     s_mean[j] = prev;  // new_means[-1] (mean0 keeps the old value for this step)
   }
   __syncthreads();
+  stamp(0);
 
   // ---- covariance update: cov = (n-1)/(n+max(1,nb-1)) C + 1/(n+max(1,nb-1)) sum_i coef_i d_i d_i^T
   // (the old C is read from the state in HBM; the new one is written back
@@ -312,22 +321,31 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     V[a * kLd + b] = warm ? eig[e] : (a == b ? 1.0 : 0.0);
   }
   __syncthreads();
+  stamp(1);
   if (warm) {
-    mm<NT, true>(V, V, W, m);  // G = V^T V
-    __syncthreads();
-    mm<NT, false>(V, W, A, m);  // V G (A's copy of C is rebuilt below from Tm)
-    __syncthreads();
-    for (int e = tid; e < m * m; e += NT) {
-      const int a = e / m, b = e - a * m;
-      V[a * kLd + b] = 1.5 * V[a * kLd + b] - 0.5 * A[a * kLd + b];
+    // Newton-Schulz re-orthonormalisation every 16 steps: the rotations lose
+    // ~1e-16 of orthogonality per sweep, the step squares the error away
+    if ((int(eig[kMahaMaxP * kMahaMaxP + 3]) & 15) == 0) {
+      mm<NT, true>(V, V, W, m);  // G = V^T V
+      __syncthreads();
+      mm<NT, false>(V, W, A, m);  // V G (A is rebuilt below from Tm)
+      __syncthreads();
+      for (int e = tid; e < m * m; e += NT) {
+        const int a = e / m, b = e - a * m;
+        V[a * kLd + b] = 1.5 * V[a * kLd + b] - 0.5 * A[a * kLd + b];
+      }
+      __syncthreads();
     }
-    __syncthreads();
     mm<NT, false>(Tm, V, W, m);  // C V
     __syncthreads();
     mm<NT, true>(V, W, A, m);    // V^T C V
     __syncthreads();
   }
+  stamp(2);
   const int half = m / 2;
+  // striping: thread -> (pair my_i, first column pair / row my_j0, stride jstep)
+  const int jstep = NT / max(half, 1);
+  const int my_i = tid % max(half, 1), my_j0 = tid / max(half, 1);
   int sweeps = 0;
   for (int sweep = 0; sweep < kMaxSweeps && m > 1; ++sweep, ++sweeps) {
     double off = 0.0, all = 0.0;
@@ -340,10 +358,13 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     off = block_sum<NT>(off, red);
     all = block_sum<NT>(all, red);
     if (off <= 1e-30 * all || off == 0.0) break;
+    // round-robin pairs: lane i < half keeps its two positions mod (m - 1)
+    // (no integer division in the round loop); block / V work is striped so
+    // a thread's pair rows are fixed for the whole sweep
+    int ua = tid == 0 ? -1 : tid % (m - 1), ub = tid == 0 ? 0 : (m - 1 - tid) % (m - 1);
     for (int r = 0; r < m - 1; ++r) {
-      for (int i = tid; i < half; i += NT) {
-        const int a = i == 0 ? 0 : 1 + (i + r) % (m - 1);
-        const int b = 1 + ((i == 0 ? 0 : m - 1 - i) + r) % (m - 1);
+      if (tid < half) {
+        const int a = tid == 0 ? 0 : 1 + ua, b = 1 + ub;
         const int pp = min(a, b), qq = max(a, b);
         const double app = A[pp * kLd + pp], aqq = A[qq * kLd + qq], apq = A[pp * kLd + qq];
         double c = 1.0, sn = 0.0;
@@ -353,19 +374,21 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
           c = 1.0 / sqrt(t * t + 1.0);
           sn = t * c;
         }
-        rc[i] = c;
-        rs[i] = sn;
-        rp[i] = pp;
-        rq[i] = qq;
+        rc[tid] = c;
+        rs[tid] = sn;
+        rp[tid] = pp;
+        rq[tid] = qq;
+        if (tid != 0 && ++ua == m - 1) ua = 0;
+        if (++ub == m - 1) ub = 0;
       }
       __syncthreads();
-      // A <- J^T A J as 2 x 2 blocks of pair rows x pair columns; V <- V J
-      const int nblk = half * half;
-      for (int e = tid; e < nblk + m * half; e += NT) {
-        if (e < nblk) {
-          const int bi = e / half, bj = e - bi * half;
-          const int pi = rp[bi], qi = rq[bi], pj = rp[bj], qj = rq[bj];
-          const double ci = rc[bi], si = rs[bi], cj = rc[bj], sj = rs[bj];
+      // A <- J^T A J as 2 x 2 blocks (pair rows bi x pair columns bj); V <- V J
+      if (my_i < half) {
+        const int pi = rp[my_i], qi = rq[my_i];
+        const double ci = rc[my_i], si = rs[my_i];
+        for (int bj = my_j0; bj < half; bj += jstep) {
+          const int pj = rp[bj], qj = rq[bj];
+          const double cj = rc[bj], sj = rs[bj];
           const double x00 = A[pi * kLd + pj], x01 = A[pi * kLd + qj], x10 = A[qi * kLd + pj], x11 = A[qi * kLd + qj];
           const double y00 = cj * x00 - sj * x01, y01 = sj * x00 + cj * x01;
           const double y10 = cj * x10 - sj * x11, y11 = sj * x10 + cj * x11;
@@ -373,19 +396,17 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
           A[pi * kLd + qj] = ci * y01 - si * y11;
           A[qi * kLd + pj] = si * y00 + ci * y10;
           A[qi * kLd + qj] = si * y01 + ci * y11;
-        } else {
-          const int f = e - nblk;
-          const int row = f / half, i = f - row * half;
-          const int pp = rp[i], qq = rq[i];
-          const double c = rc[i], sn = rs[i];
-          const double vp = V[row * kLd + pp], vq = V[row * kLd + qq];
-          V[row * kLd + pp] = c * vp - sn * vq;
-          V[row * kLd + qq] = sn * vp + c * vq;
+        }
+        for (int row = my_j0; row < m; row += jstep) {
+          const double vp = V[row * kLd + pi], vq = V[row * kLd + qi];
+          V[row * kLd + pi] = ci * vp - si * vq;
+          V[row * kLd + qi] = si * vp + ci * vq;
         }
       }
       __syncthreads();
     }
   }
+  stamp(3);
   // the eigenvectors seed the next step
   for (int e = tid; e < m * m; e += NT) {
     const int a = e / m, b = e - a * m;
@@ -423,18 +444,31 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     for (int c = 0; c < p; ++c) t += W[r * kLd + c] * vb[c * kLd];
     A[r * kLd + b] = t;
   }
-  for (int e = tid; e < nb * k; e += NT) {
-    const int i = e / k, a = e - i * k;
-    const double* v = V + sel[a];
-    double px = 0.0, pxc = 0.0, pm = 0.0;
-    for (int j = 0; j < p; ++j) {
-      const double w = v[j * kLd];
-      px += XR[size_t(i) * p + j] * w;
-      pxc += XC[size_t(i) * p + j] * w;
-      pm += MO[size_t(i) * p + j] * w;
+  // row projections: one wave per (row, component), lanes over the features
+  // (coalesced, independent loads; a 6-step shuffle sum instead of a
+  // p-long dependent chain in one thread)
+  {
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int e = wave; e < nb * k; e += NT / 64) {
+      const int i = e / k, a = e - i * k;
+      double px = 0.0, pxc = 0.0, pm = 0.0;
+      if (lane < p) {
+        const double w = V[lane * kLd + sel[a]];
+        px = XR[size_t(i) * p + lane] * w;
+        pxc = XC[size_t(i) * p + lane] * w;
+        pm = MO[size_t(i) * p + lane] * w;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        px += __shfl_xor(px, o, 64);
+        pxc += __shfl_xor(pxc, o, 64);
+        pm += __shfl_xor(pm, o, 64);
+      }
+      if (lane == 0) {
+        DPC[e] = pxc - pm;
+        XD[e] = px - pm;
+      }
     }
-    DPC[e] = pxc - pm;
-    XD[e] = px - pm;
   }
   __syncthreads();
   for (int e = tid; e < kk; e += NT) {
@@ -446,6 +480,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   }
   if (tid == 0) valid = 0;
   __syncthreads();
+  stamp(4);
   // new covariance into the state (the projections above read the old one)
   for (int e = tid; e < p * p; e += NT) s_C[e] = Tm[(e / p) * kLd + e % p];
   // ---- Sherman-Morrison scores (sequential in rows)
@@ -504,6 +539,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     if (tid == 0) scores[i] = prm.out_mode == 1 ? (part > prm.threshold ? 1.0 : 0.0) : part;
     __syncthreads();
   }
+  stamp(5);
   // ---- state update: n, clip bounds from the new covariance diagonal
   const double n_new = n_state + nb;
   for (int j = tid; j < p; j += NT) {
@@ -517,6 +553,11 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     s_tail[0] = n_new;
     s_tail[1] = 0.0;
     if (n_new > prm.start_clip) s_tail[2] = 1.0;
+  }
+  stamp(6);
+  if (tid == 0) {
+    double* acc = eig + kMahaMaxP * kMahaMaxP + 5;
+    for (int i = 0; i < 7; ++i) acc[i] += double(ph[i]) * 0.01;  // microseconds
   }
 }
 

@@ -87,6 +87,7 @@ def main() -> int:
                                   "requests_per_launch": (b1["requests"] - b0["requests"]) /
                                   max(1, b1["batches"] - b0["batches"])},
             "jacobi_mean_sweeps": jac.get("mean_sweeps"),
+            "kernel_phase_us": jac.get("phase_us_per_step"),
         }
         print(json.dumps({"p": p, **res[p]}), flush=True)
     if a.out:
