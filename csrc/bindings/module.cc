@@ -898,6 +898,33 @@ PYBIND11_MODULE(_C, m) {
     kern::maha_step_segments(P<const double>(X), P<const int32_t>(seg), nseg, prm, P<double>(state), P<double>(eig),
                              P<double>(ws), P<double>(out), as_stream(s));
   });
+  k.def("gemm_bf16", [](uintptr_t A, int lda, int rows, uintptr_t W, int Kp, int Np, int N, uintptr_t bias, int act,
+                        uintptr_t O, int ldo, int o_f32, int path, uintptr_t s) {
+    // O[rows][N] = act(A[rows][Kp] . W[Np][Kp]^T + bias): bf16 operands, fp32 accumulate
+    if (Kp % 64 || Np % 64 || N > Np || lda < Kp || ldo < N || rows <= 0)
+      throw std::runtime_error("gemm_bf16: Kp, Np multiples of 64, N <= Np, lda >= Kp, ldo >= N");
+    kern::DenseGemmArgs a;
+    a.bf16 = 1;
+    a.W = P<const void>(W);
+    a.bias = P<const float>(bias);
+    a.K = Kp;
+    a.Kp = Kp;
+    a.N = N;
+    a.Np = Np;
+    a.act = act;
+    a.A = P<const void>(A);
+    a.lda = lda;
+    a.rows = rows;
+    a.rows_eff = rows;
+    a.O = P<void>(O);
+    a.ldo = ldo;
+    a.o_f32 = o_f32;
+    a.n_store = N;
+    a.path = path;
+    kern::dense_gemm(a, as_stream(s));
+  }, py::arg("A"), py::arg("lda"), py::arg("rows"), py::arg("W"), py::arg("Kp"), py::arg("Np"), py::arg("N"),
+        py::arg("bias"), py::arg("act"), py::arg("O"), py::arg("ldo"), py::arg("o_f32"), py::arg("path"),
+        py::arg("stream") = 0);
   k.def("mean_sigmoid_rows_f64", [](uintptr_t in, int rows, int F, double thr, uintptr_t out, uintptr_t s) {
     kern::mean_sigmoid_rows_f64(P<const double>(in), rows, F, thr, P<double>(out), as_stream(s));
   });

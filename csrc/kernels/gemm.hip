@@ -460,6 +460,127 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   }
 }
 
+// ---- bf16 GEMM with a global_load_lds ring (S stages in flight)
+// For layers whose 128 x 128 tiles fill the chip (e.g. the MLP's 784 -> 512
+// layer at 8192 rows: 256 tiles).  The register-staged kernel above keeps two
+// 64-deep stages in flight per workgroup and is latency bound there (MFMA busy
+// 9%, profiles/r02h_gemm): each CU streams ~400 KB of A and W per tile, so at
+// ~1.5-2 us of L2 / HBM latency it needs >100 KB in flight.  Here the loads are
+// LDS-DMA (global_load_lds_dwordx4: no staging VGPRs, no ds_write pass) into an
+// S-deep ring of 32 KB stages (S = 4: 128 KB, one workgroup per CU), waited
+// with counted `s_waitcnt vmcnt` and raw `s_barrier` so the younger stages stay
+// in flight across the barrier (cdna guide §5 "Pipelining across barriers").
+//
+// The LDS image is lane-linear per glds instruction (base + lane * 16 B), so
+// the row XOR swizzle of the register-staged kernel (chunk ^ ((row >> 1) & 7):
+// conflict-free ds_read_b128 fragment reads) is applied to the per-lane GLOBAL
+// source address instead, and the same involution on the read (guide rule 21).
+// 4 waves (2 x 2), each a 64 x 64 quadrant = 4 x 4 16x16x32 accumulators.
+template <int S>
+__global__ __launch_bounds__(256) void gemm_glds_kernel(const DenseGemmArgs a) {
+  constexpr int BM = 128, BN = 128, BK = 64;
+  constexpr int kStageA = BM * BK, kStage = (BM + BN) * BK;  // elements
+  extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // S x [A 128 x 64 | B 128 x 64], one array
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 1, wc = wave & 1, r16 = lane & 15, kq = lane >> 4;
+  const int nN = (a.Np + BN - 1) / BN;
+  const int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+  const int KS = a.Kp / BK;
+  const __bf16* A = static_cast<const __bf16*>(a.A);
+  const __bf16* W = static_cast<const __bf16*>(a.W);
+  // this thread's 4 + 4 source rows / swizzled chunks (fixed across stages)
+  const __bf16* srcA[4];
+  const __bf16* srcB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int L = (j * 4 + wave) * 64 + lane;  // LDS chunk of instruction j: lane-linear 1 KB per wave
+    const int r = L >> 3, c = (L & 7) ^ ((r >> 1) & 7);
+    srcA[j] = A + size_t(min(m0 + r, a.rows_eff - 1)) * a.lda + c * 8;
+    srcB[j] = W + size_t(min(n0 + r, a.Np - 1)) * a.Kp + c * 8;
+  }
+  auto issue = [&](int ks) {
+    __bf16* st = ring + (ks % S) * kStage;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(srcA[j] + ks * BK),
+          (void __attribute__((address_space(3)))*)(st + (j * 4 + wave) * 512), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(srcB[j] + ks * BK),
+          (void __attribute__((address_space(3)))*)(st + kStageA + (j * 4 + wave) * 512), 16, 0, 0);
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < KS) issue(st);
+  for (int ks = 0; ks < KS; ++ks) {
+    // stage ks complete: the younger issued stages (<= S - 2, 8 glds each) may stay in flight
+    const int younger = min(ks + S - 2, KS - 1) - ks;
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMA of stage ks landed; everyone is done reading ks - 1
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + S - 1 < KS) issue(ks + S - 1);  // into the slot of stage ks - 1
+    const __bf16* As = ring + (ks % S) * kStage;
+    const __bf16* Bs = As + kStageA;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + kq;
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ra = wr * 64 + i * 16 + r16, rb = wc * 64 + i * 16 + r16;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + ra * BK + ((c ^ ((ra >> 1) & 7)) << 3));
+        bfr[i] = *reinterpret_cast<const bf16x8*>(Bs + rb * BK + ((c ^ ((rb >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) {
+    const int col = n0 + wc * 64 + tn * 16 + r16;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 4; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 64 + tm * 16 + kq * 4 + i;
+        if (!a.mse) {
+          if (row < a.rows_eff && col < n_store) {
+            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
+            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+          }
+        } else {
+          const bool ok = live && row < a.rows_eff && col < n_store;
+          const int r = row % a.rows;
+          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
+          d *= d;
+          d += __shfl_xor(d, 1, 64);
+          d += __shfl_xor(d, 2, 64);
+          d += __shfl_xor(d, 4, 64);
+          d += __shfl_xor(d, 8, 64);
+          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int AMODE>
 void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
   // 128 x 64 tiles (two resident workgroups per CU) when they fill the chip,
@@ -477,6 +598,19 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
   if constexpr (AMODE == 2) {
     if (wide >= 256) {
       hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 128, 512>), dim3(wide), dim3(512), 0, s, a);
+      return;
+    }
+  }
+  if constexpr (AMODE == 0 && sizeof(T) == 2) {
+    // glds ring kernel: 128 x 128 tiles that fill the chip, N wide enough not
+    // to waste the tile, no fused N <= 16 head (SCA_GEMM_GLDS=0 disables)
+    static const int glds = [] { const char* v = getenv("SCA_GEMM_GLDS"); return v ? atoi(v) : 1; }();
+    const int tiles128 = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
+    const bool fits = !a.out64 && a.Kp % 64 == 0 && (a.lda & 7) == 0;
+    if (fits && (a.path == 2 || (a.path == 0 && glds && a.Np >= 128 && tiles128 >= 192))) {
+      constexpr int S = 4;
+      const size_t lds = size_t(S) * (128 + 128) * 64 * sizeof(__bf16);
+      hipLaunchKernelGGL((gemm_glds_kernel<S>), dim3(tiles128), dim3(256), lds, s, a);
       return;
     }
   }

@@ -213,6 +213,52 @@ def case_dense_prec(iters):
         os.environ.pop("SCA_MLP_MODE", None)
 
 
+def case_gemm(iters):
+    """bf16 GEMM C = A . W^T (fp32 out) at the MLP layer shapes and square
+    shapes: register-staged LDS kernel (path 1), glds ring kernel (path 2) and
+    torch bf16 (hipBLASLt), interleaved in one process on the same random
+    operands; TFLOP/s from HIP event time per launch."""
+    import torch
+
+    from seldon_core_amd import native
+
+    C = native()
+    for rows, K, N in ((8192, 832, 512), (8192, 512, 256), (4096, 4096, 4096), (8192, 8192, 8192)):
+        A = torch.randn(rows, K, device="cuda").to(torch.bfloat16)
+        W = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+        b = torch.zeros(N, device="cuda")
+        O = torch.empty(rows, N, device="cuda")
+        flops = 2.0 * rows * K * N
+        n = iters if rows * K * N < 1e10 else max(3, iters // 5)
+
+        def run(path):
+            C.kernels.gemm_bf16(A.data_ptr(), K, rows, W.data_ptr(), K, N, N, b.data_ptr(), 0, O.data_ptr(), N, 1, path)
+
+        def lib():
+            torch.matmul(A, W.T, out=None)
+
+        res = {}
+        for _ in range(2):  # interleaved rounds
+            for name, fn in (("reg", lambda: run(1)), ("glds", lambda: run(2)), ("torch", lib)):
+                fn()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(n):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / n
+                res[name] = min(res.get(name, 1e30), us)
+        run(2)
+        ref = (A.float() @ W.float().T)
+        err = float((O - ref).abs().max() / ref.abs().max())
+        print(json.dumps({"case": "gemm_bf16", "M": rows, "K": K, "N": N,
+                          **{f"{k}_us": round(v, 2) for k, v in res.items()},
+                          **{f"{k}_tflops": round(flops / (v * 1e-6) / 1e12, 1) for k, v in res.items()},
+                          "glds_rel_err": err}), flush=True)
+
+
 def case_mlp_torch_bf16(iters, rows_list=(8192,)):
     """The MLP in PyTorch eager bf16 (hipBLASLt bf16 GEMMs)."""
     import torch
@@ -404,7 +450,7 @@ def main():
     cases = {"tree": case_tree, "vae": case_vae, "mlp": case_mlp, "linear": case_linear,
              "mlp_torch": case_mlp_torch,
              "mlp_torch_fp64io": lambda it: case_mlp_torch(it, fp64_io=True), "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes,
-             "lstm": case_lstm, "latency": case_latency, "dense_prec": case_dense_prec, "mlp_torch_bf16": case_mlp_torch_bf16}
+             "lstm": case_lstm, "gemm": case_gemm, "latency": case_latency, "dense_prec": case_dense_prec, "mlp_torch_bf16": case_mlp_torch_bf16}
     for c in a.only.split(","):
         cases[c](a.iters)
 
