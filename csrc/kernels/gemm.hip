@@ -581,6 +581,121 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const DenseGemmArgs a) {
   }
 }
 
+// ---- bf16 GEMM, 256 x 256 tiles, 8 waves, glds double buffer ("2-phase")
+// For GEMMs with enough 256-square tiles to fill the chip (>= 256, e.g.
+// 4096^3): per 64-deep K step a wave owns a 128 x 64 quadrant (8 x 4
+// accumulators, 64 MFMAs) and reads 12 fragments per 32-k half step, so the
+// operand traffic per FLOP is a quarter of the 128 x 128 kernel's (which is
+// L2->CU bound at ~50% MFMA).  Schedule (cdna guide §5.5 T3+T4 minimum form):
+// issue the next K tile's LDS-DMA, read + MFMA the current one, then one
+// vmcnt(0) + barrier per K tile; 2 x 64 KB buffers, one workgroup per CU
+// (two waves per SIMD interleave MFMA and ds_read), XCD-aware tile order,
+// source-side XOR swizzle as in gemm_glds_kernel.
+__global__ __launch_bounds__(512) void gemm_glds256_kernel(const DenseGemmArgs a) {
+  constexpr int BM = 256, BN = 256, BK = 64;
+  constexpr int kStageA = BM * BK, kStage = (BM + BN) * BK;  // elements
+  extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // 2 x [A 256 x 64 | B 256 x 64]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3, r16 = lane & 15, kq = lane >> 4;
+  const int nN = (a.Np + BN - 1) / BN;
+  const int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+  const int KS = a.Kp / BK;
+  const __bf16* A = static_cast<const __bf16*>(a.A);
+  const __bf16* W = static_cast<const __bf16*>(a.W);
+  const __bf16* srcA[4];
+  const __bf16* srcB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int L = (j * 8 + wave) * 64 + lane;  // LDS chunk of instruction j (1 KB per wave-instruction)
+    const int r = L >> 3, c = (L & 7) ^ ((r >> 1) & 7);
+    srcA[j] = A + size_t(min(m0 + r, a.rows_eff - 1)) * a.lda + c * 8;
+    srcB[j] = W + size_t(min(n0 + r, a.Np - 1)) * a.Kp + c * 8;
+  }
+  auto issue = [&](int ks) {
+    __bf16* st = ring + (ks & 1) * kStage;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(srcA[j] + ks * BK),
+          (void __attribute__((address_space(3)))*)(st + (j * 8 + wave) * 512), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(srcB[j] + ks * BK),
+          (void __attribute__((address_space(3)))*)(st + kStageA + (j * 8 + wave) * 512), 16, 0, 0);
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ks = 0; ks < KS; ++ks) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + 1 < KS) issue(ks + 1);  // the other buffer: everyone passed the barrier after reading it
+    const __bf16* As = ring + (ks & 1) * kStage;
+    const __bf16* Bs = As + kStageA;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + kq;
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int ra = wr * 128 + i * 16 + r16;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + ra * BK + ((c ^ ((ra >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rb = wc * 64 + i * 16 + r16;
+        bfr[i] = *reinterpret_cast<const bf16x8*>(Bs + rb * BK + ((c ^ ((rb >> 1) & 7)) << 3));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) {
+    const int col = n0 + wc * 64 + tn * 16 + r16;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 8; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
+        if (!a.mse) {
+          if (row < a.rows_eff && col < n_store) {
+            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
+            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+          }
+        } else {
+          const bool ok = live && row < a.rows_eff && col < n_store;
+          const int r = row % a.rows;
+          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
+          d *= d;
+          d += __shfl_xor(d, 1, 64);
+          d += __shfl_xor(d, 2, 64);
+          d += __shfl_xor(d, 4, 64);
+          d += __shfl_xor(d, 8, 64);
+          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int AMODE>
 void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
   // 128 x 64 tiles (two resident workgroups per CU) when they fill the chip,
@@ -607,7 +722,13 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
     static const int glds = [] { const char* v = getenv("SCA_GEMM_GLDS"); return v ? atoi(v) : 1; }();
     const int tiles128 = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
     const bool fits = !a.out64 && a.Kp % 64 == 0 && (a.lda & 7) == 0;
-    if (fits && (a.path == 2 || (a.path == 0 && glds && a.Np >= 128 && tiles128 >= 192))) {
+    const int tiles256 = ((a.Np + 255) / 256) * ((a.rows_eff + 255) / 256);
+    if (fits && (a.path == 3 || (a.path == 0 && glds && a.Np >= 256 && tiles256 >= 256))) {
+      const size_t lds = size_t(2) * (256 + 256) * 64 * sizeof(__bf16);
+      hipLaunchKernelGGL(gemm_glds256_kernel, dim3(tiles256), dim3(512), lds, s, a);
+      return;
+    }
+    if (fits && (a.path == 2 || (a.path == 0 && glds && a.Np >= 128 && tiles128 >= 192 && false))) {
       constexpr int S = 4;
       const size_t lds = size_t(S) * (128 + 128) * 64 * sizeof(__bf16);
       hipLaunchKernelGGL((gemm_glds_kernel<S>), dim3(tiles128), dim3(256), lds, s, a);

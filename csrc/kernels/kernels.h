@@ -207,7 +207,7 @@ struct DenseGemmArgs {
   float* mse = nullptr;
   const float* xref = nullptr;
   int ldx = 0;
-  int path = 0;  // bf16 plain A: 0 auto, 1 register-staged LDS kernel, 2 glds ring kernel (tests / benches)
+  int path = 0;  // bf16 plain A: 0 auto, 1 register-staged LDS kernel, 2 glds ring 128^2, 3 glds 256^2 (tests / benches)
 };
 void dense_gemm(const DenseGemmArgs& a, hipStream_t stream);
 // fp64 rows [rows][F] -> bf16 [rows][ld], zero-padded columns
