@@ -22,6 +22,7 @@ namespace sca::kern {
 namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
 using f64x2 = __attribute__((ext_vector_type(2))) double;
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 constexpr int kTM = 4;  // row tiles (of 16) per wave
@@ -256,8 +257,16 @@ __device__ __forceinline__ int xcd_tile(int L, int nwg) {
 // fp32 products on v_mfma_f32_16x16x4_f32 (four per 16-B fragment), 32-deep
 // stages.  The LDS image is the same in bytes either way: 128-B rows of eight
 // 16-B chunks, XOR-swizzled per row pair.
-template <typename T, int AMODE, int BM, int BN, int NT, int NS = 2>
+template <typename T, int AMODE, int BM, int BN, int NT, int NS = 2, bool M32 = false>
 __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
+  // M32 (fp32 only): v_mfma_f32_32x32x2_f32 on 32 x 32 tiles -- a wave's
+  // BM/2 x 32 block is BM/64 accumulators of 16 registers; per 32-deep stage
+  // lane (i, h) reads k in [16h, 16h + 16) of its A row / W row (4 x
+  // ds_read_b128, same swizzled image) and the 16 MFMA steps pair k = s with
+  // k = 16 + s.  Half the MFMA instructions of the 16x16x4 form for the same
+  // FLOPs, and its 64-cycle dependent latency equals its issue interval, so
+  // each accumulator chain issues back to back (cdna guide §3).
+  static_assert(!M32 || sizeof(T) == 4, "M32 is the fp32 MFMA form");
   constexpr int kEl = 16 / int(sizeof(T));    // elements per 16-B chunk
   constexpr int kBKe = 8 * kEl;               // K elements per stage (128 B per row)
   constexpr int kLdr = kBKe;                  // LDS row = the 128-B panel row, XOR-swizzled (see sw())
@@ -331,9 +340,32 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int TM32 = M32 ? BM / 64 : 1;
+  f32x16 acc32[TM32];
+#pragma unroll
+  for (int t = 0; t < TM32; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc32[t][i] = 0.f;
   auto compute = [&](int buf) {
     const T* As = smem + buf * kBuf;
     const T* Ws = As + BM * kLdr;
+    if constexpr (M32) {
+      const int i32 = lane & 31, h = lane >> 5;
+      f32x4 bq[4], aq[TM32][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) bq[c] = *reinterpret_cast<const f32x4*>(Ws + sw(wc * 32 + i32, 4 * h + c));
+#pragma unroll
+      for (int t = 0; t < TM32; ++t)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          aq[t][c] = *reinterpret_cast<const f32x4*>(As + sw(wr * (BM / 2) + t * 32 + i32, 4 * h + c));
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int t = 0; t < TM32; ++t)
+          acc32[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[t][s >> 2][s & 3], bq[s >> 2][s & 3], acc32[t], 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {  // two 16-B fragments per row per stage (bytes kk * 64 + kq * 16)
       u32x4 af[TM], bf[TN];
@@ -427,6 +459,30 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
     return;
   }
   const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+  if constexpr (M32) {  // C/D map of 32x32: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+    const int col = n0 + wc * 32 + (lane & 31);
+    if (col >= n_store) return;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int t = 0; t < TM32; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wr * (BM / 2) + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+        if (row >= a.rows_eff) continue;
+        const float v = live ? act_f(acc32[t][i] + bias, a.act) : 0.f;
+        if (!a.mse) {
+          if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+          else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+        } else if (live) {
+          const int r = row % a.rows;
+          const float d = v - a.xref[size_t(r) * a.ldx + col];
+          atomicAdd(&a.mse[r], d * d);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int col = n0 + wc * 32 + tn * 16 + r16;
@@ -732,6 +788,13 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
       constexpr int S = 4;
       const size_t lds = size_t(S) * (128 + 128) * 64 * sizeof(__bf16);
       hipLaunchKernelGGL((gemm_glds_kernel<S>), dim3(tiles128), dim3(256), lds, s, a);
+      return;
+    }
+  }
+  if constexpr (sizeof(T) == 4) {
+    static const int m32 = [] { const char* v = getenv("SCA_GEMM_F32_M32"); return v ? atoi(v) : 1; }();
+    if (m32 && !a.out64 && big >= 256) {
+      hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 64, 256, 2, true>), dim3(big), dim3(256), 0, s, a);
       return;
     }
   }

@@ -223,7 +223,10 @@ def case_gemm(iters):
     from seldon_core_amd import native
 
     C = native()
-    for rows, K, N in ((8192, 832, 512), (8192, 512, 256), (4096, 4096, 4096), (8192, 8192, 8192)):
+    shapes = ((8192, 832, 512), (8192, 512, 256), (4096, 4096, 4096), (8192, 8192, 8192))
+    if os.environ.get("GEMM_SHAPES"):  # e.g. "8192x832x512,4096x4096x4096" (PMC passes)
+        shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["GEMM_SHAPES"].split(",")]
+    for rows, K, N in shapes:
         A = torch.randn(rows, K, device="cuda").to(torch.bfloat16)
         W = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
         b = torch.zeros(N, device="cuda")
@@ -238,7 +241,7 @@ def case_gemm(iters):
             torch.matmul(A, W.T, out=None)
 
         res = {}
-        for _ in range(2):  # interleaved rounds
+        for _ in range(1 if os.environ.get("SCA_PMC") else 2):  # interleaved rounds
             for name, fn in (("reg", lambda: run(1)), ("glds", lambda: run(2)), ("glds256", lambda: run(3)),
                              ("torch", lib)):
                 fn()
