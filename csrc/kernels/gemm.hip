@@ -273,7 +273,7 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   constexpr int WN = NT / 128;                // waves along N (2 along M); each wave owns BM/2 x 32
   constexpr int TM = BM / 32;                 // 16-row tiles per wave
   constexpr int TN = 2;                       // 16-col tiles per wave
-  static_assert(BN == 32 * WN, "BN must be 32 x waves along N");
+  static_assert(M32 ? BN % (32 * WN) == 0 : BN == 32 * WN, "BN must be 32 x waves along N (a multiple for M32)");
   constexpr int CA = BM * 8 / NT;             // A staging chunks per thread (BM rows x 8 chunks)
   constexpr int CW = BN * 8 / NT;             // W staging chunks per thread
   constexpr int kBuf = (BM + BN) * kLdr;      // one LDS buffer: A panel then W panel
@@ -340,20 +340,26 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int TM32 = M32 ? BM / 64 : 1;
-  f32x16 acc32[TM32];
+  constexpr int TM32 = M32 ? BM / 64 : 1, TN32 = M32 ? BN / (32 * WN) : 1;
+  constexpr int WCOLS = BN / WN;  // columns per wave
+  f32x16 acc32[TM32][TN32];
 #pragma unroll
   for (int t = 0; t < TM32; ++t)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc32[t][i] = 0.f;
+    for (int u = 0; u < TN32; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc32[t][u][i] = 0.f;
   auto compute = [&](int buf) {
     const T* As = smem + buf * kBuf;
     const T* Ws = As + BM * kLdr;
     if constexpr (M32) {
       const int i32 = lane & 31, h = lane >> 5;
-      f32x4 bq[4], aq[TM32][4];
+      f32x4 bq[TN32][4], aq[TM32][4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) bq[c] = *reinterpret_cast<const f32x4*>(Ws + sw(wc * 32 + i32, 4 * h + c));
+      for (int u = 0; u < TN32; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          bq[u][c] = *reinterpret_cast<const f32x4*>(Ws + sw(wc * WCOLS + u * 32 + i32, 4 * h + c));
 #pragma unroll
       for (int t = 0; t < TM32; ++t)
 #pragma unroll
@@ -363,7 +369,10 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
       for (int s = 0; s < 16; ++s)
 #pragma unroll
         for (int t = 0; t < TM32; ++t)
-          acc32[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[t][s >> 2][s & 3], bq[s >> 2][s & 3], acc32[t], 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < TN32; ++u)
+            acc32[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[t][s >> 2][s & 3], bq[u][s >> 2][s & 3], acc32[t][u],
+                                                               0, 0, 0);
       return;
     }
 #pragma unroll
@@ -460,24 +469,31 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   }
   const int n_store = a.n_store > 0 ? a.n_store : a.Np;
   if constexpr (M32) {  // C/D map of 32x32: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
-    const int col = n0 + wc * 32 + (lane & 31);
-    if (col >= n_store) return;
-    const bool live = col < a.N;
-    const float bias = live ? a.bias[col] : 0.f;
 #pragma unroll
-    for (int t = 0; t < TM32; ++t) {
+    for (int u = 0; u < TN32; ++u) {
+      const int col = n0 + wc * WCOLS + u * 32 + (lane & 31);
+      const bool live = col < a.N, store = col < n_store;
+      const float bias = live ? a.bias[col] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = m0 + wr * (BM / 2) + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-        if (row >= a.rows_eff) continue;
-        const float v = live ? act_f(acc32[t][i] + bias, a.act) : 0.f;
-        if (!a.mse) {
-          if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
-          else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
-        } else if (live) {
-          const int r = row % a.rows;
-          const float d = v - a.xref[size_t(r) * a.ldx + col];
-          atomicAdd(&a.mse[r], d * d);
+      for (int t = 0; t < TM32; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = m0 + wr * (BM / 2) + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+          const float v = live ? act_f(acc32[t][u][i] + bias, a.act) : 0.f;
+          if (!a.mse) {
+            if (store && row < a.rows_eff) {
+              if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+              else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+            }
+          } else {  // the 32 lanes of a half hold one row's 32 columns: sum them, one atomic per row
+            const bool ok = live && store && row < a.rows_eff;
+            const int r = row % a.rows;
+            float d = ok ? v - a.xref[size_t(r) * a.ldx + col] : 0.f;
+            d *= d;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) d += __shfl_xor(d, o, 64);
+            if ((lane & 31) == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+          }
         }
       }
     }
@@ -793,6 +809,11 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
   }
   if constexpr (sizeof(T) == 4) {
     static const int m32 = [] { const char* v = getenv("SCA_GEMM_F32_M32"); return v ? atoi(v) : 1; }();
+    const int big128 = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
+    if (m32 && !a.out64 && big128 >= 256) {  // 128 x 128: each wave 64 x 64 = 2 x 2 accumulators
+      hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 128, 256, 2, true>), dim3(big128), dim3(256), 0, s, a);
+      return;
+    }
     if (m32 && !a.out64 && big >= 256) {
       hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 64, 256, 2, true>), dim3(big), dim3(256), 0, s, a);
       return;
