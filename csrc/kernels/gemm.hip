@@ -809,11 +809,8 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
   }
   if constexpr (sizeof(T) == 4) {
     static const int m32 = [] { const char* v = getenv("SCA_GEMM_F32_M32"); return v ? atoi(v) : 1; }();
-    const int big128 = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
-    if (m32 && !a.out64 && big128 >= 256) {  // 128 x 128: each wave 64 x 64 = 2 x 2 accumulators
-      hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 128, 256, 2, true>), dim3(big128), dim3(256), 0, s, a);
-      return;
-    }
+    // (128 x 128 tiles with 2 x 2 32x32 accumulators per wave -- one workgroup
+    // per CU -- measured 9-90% slower on every MLP / VAE layer, r03d)
     if (m32 && !a.out64 && big >= 256) {
       hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 64, 256, 2, true>), dim3(big), dim3(256), 0, s, a);
       return;
