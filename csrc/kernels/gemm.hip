@@ -653,6 +653,195 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const DenseGemmArgs a) {
   }
 }
 
+// ---- bf16 GEMM, 256 x 256 tiles, 8-phase ping-pong schedule
+// Same tile and wave layout as gemm_glds256_kernel, but each 64-deep K tile is
+// four phases, one per 64 x 32 quadrant of a wave's 128 x 64 block (16
+// MFMAs), and the two wave groups (wr = 0 / 1) run one barrier apart, so one
+// group's ds_reads overlap the other's MFMAs on every SIMD (cdna guide §5
+// "The 256^2 8-phase template", T3 + T4 + T5).  LDS: 8 half-tile buffers
+// (K-tile parity x A/B x rows 0-127 / 128-255) of 128 x 64 bf16; one half
+// tile (2 glds per thread) is issued per phase:
+//   q0: read B(nh0) + A(mh0); issue A0 of tile t+1          | MFMA (mh0, nh0)
+//   q1: read B(nh1); issue A1 of tile t+1; retire the reads   | MFMA (mh0, nh1)
+//       before the barrier (B0 of this parity is restaged next phase)
+//   q2: read A(mh1); issue B0 of tile t+2                     | MFMA (mh1, nh0)
+//   q3: issue B1 of tile t+2; vmcnt(4) = tile t+1 landed,     | MFMA (mh1, nh1)
+//       placed before the first barrier (the other group reads it one
+//       barrier later: the stagger's extra barrier of margin)
+// so a buffer is restaged >= 2 phases after its last read (B0: 1 phase, with
+// the reads retired first), and read only after a barrier that follows the
+// vmcnt of every issuing wave.  Loads are counted by hand (raw s_barrier,
+// explicit s_waitcnt): __syncthreads() would drain the DMA queue.
+__global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
+  constexpr int BM = 256, BN = 256, BK = 64, HT = 128 * BK;  // half tile (elements)
+  extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // [parity][A/B][half] x HT
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3, r16 = lane & 15, kq = lane >> 4;
+  const int nN = (a.Np + BN - 1) / BN;
+  const int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+  const int KT = a.Kp / BK;
+  const __bf16* A = static_cast<const __bf16*>(a.A);
+  const __bf16* W = static_cast<const __bf16*>(a.W);
+  // this thread's two chunks of any half tile (rows r, swizzled chunk c)
+  const __bf16* srcA[2][2];  // [half][j]
+  const __bf16* srcB[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int L = (j * 8 + wave) * 64 + lane;
+    const int r = L >> 3, c = (L & 7) ^ ((r >> 1) & 7);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      srcA[hf][j] = A + size_t(min(m0 + hf * 128 + r, a.rows_eff - 1)) * a.lda + c * 8;
+      srcB[hf][j] = W + size_t(min(n0 + hf * 128 + r, a.Np - 1)) * a.Kp + c * 8;
+    }
+  }
+  auto buf = [&](int par, int op, int hf) { return ring + ((par * 2 + op) * 2 + hf) * HT; };
+  auto issue = [&](int kt, int op, int hf) {  // half tile (op 0 = A, 1 = B) of K tile kt
+    __bf16* dst = buf(kt & 1, op, hf);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)((op == 0 ? srcA[hf][j] : srcB[hf][j]) + kt * BK),
+          (void __attribute__((address_space(3)))*)(dst + (j * 8 + wave) * 512), 16, 0, 0);
+  };
+  auto frag = [&](const __bf16* b, int row, int kk) {
+    const int c = kk * 4 + kq;
+    return *reinterpret_cast<const bf16x8*>(b + row * BK + ((c ^ ((row >> 1) & 7)) << 3));
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bn0[2][2], bn1[2][2];
+  auto mfma_q = [&](int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af[i][kk], nh == 0 ? bn0[j][kk] : bn1[j][kk], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // prologue: tile 0 whole, B halves of tile 1; tile 0 landed everywhere
+  issue(0, 0, 0);
+  issue(0, 0, 1);
+  issue(0, 1, 0);
+  issue(0, 1, 1);
+  if (KT > 1) {
+    issue(1, 1, 0);
+    issue(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
+  const int bh = wc >> 1, bo = (wc & 1) * 64;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int par = kt & 1;
+    const __bf16* As = buf(par, 0, wr);
+    const __bf16* Bs = buf(par, 1, bh);
+    // ---- q0
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bn0[j][kk] = frag(Bs, bo + j * 16 + r16, kk);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][kk] = frag(As, i * 16 + r16, kk);
+    if (kt + 1 < KT) issue(kt + 1, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q1
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bn1[j][kk] = frag(Bs, bo + 32 + j * 16 + r16, kk);
+    if (kt + 1 < KT) issue(kt + 1, 0, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // B reads retired: B0 of this parity is restaged in q2
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q2
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][kk] = frag(As, 64 + i * 16 + r16, kk);
+    if (kt + 2 < KT) issue(kt + 2, 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q3
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < KT) {
+      issue(kt + 2, 1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile kt + 1 landed (B0 / B1 of kt + 2 may fly)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) {
+    const int col = n0 + wc * 64 + tn * 16 + r16;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 8; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
+        if (!a.mse) {
+          if (row < a.rows_eff && col < n_store) {
+            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
+            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+          }
+        } else {
+          const bool ok = live && row < a.rows_eff && col < n_store;
+          const int r = row % a.rows;
+          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
+          d *= d;
+          d += __shfl_xor(d, 1, 64);
+          d += __shfl_xor(d, 2, 64);
+          d += __shfl_xor(d, 4, 64);
+          d += __shfl_xor(d, 8, 64);
+          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+        }
+      }
+    }
+  }
+}
+
 // ---- bf16 GEMM, 256 x 256 tiles, 8 waves, glds double buffer ("2-phase")
 // For GEMMs with enough 256-square tiles to fill the chip (>= 256, e.g.
 // 4096^3): per 64-deep K step a wave owns a 128 x 64 quadrant (8 x 4
@@ -795,6 +984,11 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
     const int tiles128 = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
     const bool fits = !a.out64 && a.Kp % 64 == 0 && (a.lda & 7) == 0;
     const int tiles256 = ((a.Np + 255) / 256) * ((a.rows_eff + 255) / 256);
+    if (fits && a.path == 4) {
+      const size_t lds = size_t(8) * 128 * 64 * sizeof(__bf16);
+      hipLaunchKernelGGL(gemm_8ph_kernel, dim3(tiles256), dim3(512), lds, s, a);
+      return;
+    }
     if (fits && (a.path == 3 || (a.path == 0 && glds && a.Np >= 256 && tiles256 >= 256))) {
       const size_t lds = size_t(2) * (256 + 256) * 64 * sizeof(__bf16);
       hipLaunchKernelGGL(gemm_glds256_kernel, dim3(tiles256), dim3(512), lds, s, a);

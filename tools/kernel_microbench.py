@@ -243,7 +243,7 @@ def case_gemm(iters):
         res = {}
         for _ in range(1 if os.environ.get("SCA_PMC") else 2):  # interleaved rounds
             for name, fn in (("reg", lambda: run(1)), ("glds", lambda: run(2)), ("glds256", lambda: run(3)),
-                             ("torch", lib)):
+                             ("8ph", lambda: run(4)), ("torch", lib)):
                 fn()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -254,13 +254,15 @@ def case_gemm(iters):
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / n
                 res[name] = min(res.get(name, 1e30), us)
-        run(3)
+        errs = {}
         ref = (A.float() @ W.float().T)
-        err = float((O - ref).abs().max() / ref.abs().max())
+        for pth, nm in ((3, "glds256"), (4, "8ph")):
+            run(pth)
+            errs[nm + "_rel_err"] = float((O - ref).abs().max() / ref.abs().max())
         print(json.dumps({"case": "gemm_bf16", "M": rows, "K": K, "N": N,
                           **{f"{k}_us": round(v, 2) for k, v in res.items()},
                           **{f"{k}_tflops": round(flops / (v * 1e-6) / 1e12, 1) for k, v in res.items()},
-                          "glds256_rel_err": err}), flush=True)
+                          **errs}), flush=True)
 
 
 def case_mlp_torch_bf16(iters, rows_list=(8192,)):
