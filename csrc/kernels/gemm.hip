@@ -661,15 +661,16 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const DenseGemmArgs a) {
 // "The 256^2 8-phase template", T3 + T4 + T5).  LDS: 8 half-tile buffers
 // (K-tile parity x A/B x rows 0-127 / 128-255) of 128 x 64 bf16; one half
 // tile (2 glds per thread) is issued per phase:
-//   q0: read B(nh0) + A(mh0); issue A0 of tile t+1          | MFMA (mh0, nh0)
-//   q1: read B(nh1); issue A1 of tile t+1; retire the reads   | MFMA (mh0, nh1)
-//       before the barrier (B0 of this parity is restaged next phase)
-//   q2: read A(mh1); issue B0 of tile t+2                     | MFMA (mh1, nh0)
-//   q3: issue B1 of tile t+2; vmcnt(4) = tile t+1 landed,     | MFMA (mh1, nh1)
-//       placed before the first barrier (the other group reads it one
-//       barrier later: the stagger's extra barrier of margin)
+//   q0: read all B + A rows 0-63; issue A1 of tile t+1;       | MFMA (mh0, nh0)
+//       retire the B reads before the barrier (B0 is restaged in q1)
+//   q1: read A rows 64-127; issue B0 of tile t+2              | MFMA (mh0, nh1)
+//   q2: issue B1 of tile t+2                                  | MFMA (mh1, nh0)
+//   q3: issue A0 of tile t+2; vmcnt(6) = tile t+1 landed      | MFMA (mh1, nh1)
+//       (3 younger half tiles in flight), placed before the first barrier:
+//       the other group reads it one barrier later (the stagger's margin)
 // so a buffer is restaged >= 2 phases after its last read (B0: 1 phase, with
-// the reads retired first), and read only after a barrier that follows the
+// the reads retired first), the last half tile of a K tile is issued 3 phases
+// before its wait, and data is read only after a barrier that follows the
 // vmcnt of every issuing wave.  Loads are counted by hand (raw s_barrier,
 // explicit s_waitcnt): __syncthreads() would drain the DMA queue.
 __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
@@ -714,8 +715,8 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[4][2], bn0[2][2], bn1[2][2];
-  auto mfma_q = [&](int mh, int nh) {
+  bf16x8 am0[4][2], am1[4][2], bq[4][2];
+  auto mfma_q = [&](bf16x8 (&af)[4][2], int mh, int nh) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -723,19 +724,20 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              af[i][kk], nh == 0 ? bn0[j][kk] : bn1[j][kk], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+          acc[mh * 4 + i][nh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bq[nh * 2 + j][kk], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  // prologue: tile 0 whole, B halves of tile 1; tile 0 landed everywhere
-  issue(0, 0, 0);
-  issue(0, 0, 1);
+  // prologue: tile 0 whole, then B0 / B1 / A0 of tile 1 (3 half tiles may fly)
   issue(0, 1, 0);
   issue(0, 1, 1);
+  issue(0, 0, 0);
+  issue(0, 0, 1);
   if (KT > 1) {
     issue(1, 1, 0);
     issue(1, 1, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    issue(1, 0, 0);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -746,64 +748,60 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
     const int par = kt & 1;
     const __bf16* As = buf(par, 0, wr);
     const __bf16* Bs = buf(par, 1, bh);
-    // ---- q0
+    // ---- q0: all of this wave's B fragments, then A rows 0-63; A1 of tile kt + 1
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bn0[j][kk] = frag(Bs, bo + j * 16 + r16, kk);
+      for (int j = 0; j < 4; ++j) bq[j][kk] = frag(Bs, bo + j * 16 + r16, kk);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i][kk] = frag(As, i * 16 + r16, kk);
-    if (kt + 1 < KT) issue(kt + 1, 0, 0);
+      for (int i = 0; i < 4; ++i) am0[i][kk] = frag(As, i * 16 + r16, kk);
+    if (kt + 1 < KT) issue(kt + 1, 0, 1);
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // the 8 B reads retired: B0 is restaged in q1
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    mfma_q(0, 0);
+    mfma_q(am0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    // ---- q1
+    // ---- q1: A rows 64-127; B0 of tile kt + 2
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bn1[j][kk] = frag(Bs, bo + 32 + j * 16 + r16, kk);
-    if (kt + 1 < KT) issue(kt + 1, 0, 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // B reads retired: B0 of this parity is restaged in q2
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_q(0, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    // ---- q2
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i][kk] = frag(As, 64 + i * 16 + r16, kk);
+      for (int i = 0; i < 4; ++i) am1[i][kk] = frag(As, 64 + i * 16 + r16, kk);
     if (kt + 2 < KT) issue(kt + 2, 1, 0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    mfma_q(1, 0);
+    mfma_q(am0, 0, 1);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    // ---- q3
+    // ---- q2: B1 of tile kt + 2
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < KT) issue(kt + 2, 1, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // am1 (q1's reads)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(am1, 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q3: A0 of tile kt + 2; tile kt + 1 landed (3 younger half tiles may fly)
     __builtin_amdgcn_sched_barrier(0);
     if (kt + 2 < KT) {
-      issue(kt + 2, 1, 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile kt + 1 landed (B0 / B1 of kt + 2 may fly)
+      issue(kt + 2, 0, 0);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    mfma_q(1, 1);
+    mfma_q(am1, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
