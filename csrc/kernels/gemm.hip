@@ -653,6 +653,150 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const DenseGemmArgs a) {
   }
 }
 
+// ---- bf16 GEMM, 256 x 256 tiles, 4 waves of 128 x 128 (one wave per SIMD)
+// The 8-wave kernels read each A / B fragment from LDS 4x / 2x (a wave's
+// 128 x 64 block): 192 KB of ds_read per 64-deep K tile per CU, ~75% of the
+// MFMA time (LDS-bound phases).  Here a wave owns 128 x 128 (8 x 8 16x16
+// accumulators = 256 registers, in AGPRs at one wave per SIMD): 128 KB of
+// ds_read per K tile, 25% of the MFMA time, and the next k-step's 16
+// fragments are read while the current 64 MFMAs issue (two register sets).
+// LDS-DMA double buffer, one vmcnt(0) + barrier per K tile (the next tile
+// had the whole K tile of MFMAs, ~1 us, to land).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
+    const DenseGemmArgs a) {
+  constexpr int BM = 256, BN = 256, BK = 64;
+  constexpr int kStageA = BM * BK, kStage = (BM + BN) * BK;
+  extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // 2 x [A 256 x 64 | B 256 x 64]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 1, wc = wave & 1, r16 = lane & 15, kq = lane >> 4;
+  const int nN = (a.Np + BN - 1) / BN;
+  const int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+  const int KS = a.Kp / BK;
+  const __bf16* A = static_cast<const __bf16*>(a.A);
+  const __bf16* W = static_cast<const __bf16*>(a.W);
+  const __bf16* srcA[8];
+  const __bf16* srcB[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int L = (j * 4 + wave) * 64 + lane;  // LDS chunk of instruction j (1 KB per wave-instruction)
+    const int r = L >> 3, c = (L & 7) ^ ((r >> 1) & 7);
+    srcA[j] = A + size_t(min(m0 + r, a.rows_eff - 1)) * a.lda + c * 8;
+    srcB[j] = W + size_t(min(n0 + r, a.Np - 1)) * a.Kp + c * 8;
+  }
+  auto issue = [&](int ks) {
+    __bf16* st = ring + (ks & 1) * kStage;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(srcA[j] + ks * BK),
+          (void __attribute__((address_space(3)))*)(st + (j * 4 + wave) * 512), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(srcB[j] + ks * BK),
+          (void __attribute__((address_space(3)))*)(st + kStageA + (j * 4 + wave) * 512), 16, 0, 0);
+  };
+  auto frag = [&](const __bf16* b, int row, int kk) {
+    const int c = kk * 4 + kq;
+    return *reinterpret_cast<const bf16x8*>(b + row * BK + ((c ^ ((row >> 1) & 7)) << 3));
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // Per K tile ks (buffer ks & 1):
+  //   reads of k-step 1 fly under k-step 0's 64 MFMAs (k-step 0's fragments
+  //   were read under the previous tile's k-step 1); then lgkmcnt(0) +
+  //   vmcnt(0) (tile ks + 1 landed) + barrier; then tile ks + 2 is issued into
+  //   this tile's buffer (every wave's reads of it retired before the barrier)
+  //   and tile ks + 1's k-step-0 fragments are read under k-step 1's MFMAs.
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  issue(0);
+  if (KS > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 (16 glds per thread per tile)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a0[i] = frag(ring, wr * 128 + i * 16 + r16, 0);
+    b0[i] = frag(ring + kStageA, wc * 128 + i * 16 + r16, 0);
+  }
+  for (int ks = 0; ks < KS; ++ks) {
+    const __bf16* As = ring + (ks & 1) * kStage;
+    const __bf16* Bs = As + kStageA;
+    // k-step 0's fragments (read under the previous MFMAs) retired, as a
+    // builtin so hipcc's wait tracking sees it: the 16 reads below then need
+    // no wait before the MFMAs (lgkmcnt cannot express 16 younger reads)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt untouched
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a1[i] = frag(As, wr * 128 + i * 16 + r16, 1);
+      b1[i] = frag(Bs, wc * 128 + i * 16 + r16, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0), as a builtin (hipcc's tracker sees it)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + 2 < KS) issue(ks + 2);
+    if (ks + 1 < KS) {
+      const __bf16* An = ring + ((ks + 1) & 1) * kStage;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        a0[i] = frag(An, wr * 128 + i * 16 + r16, 0);
+        b0[i] = frag(An + kStageA, wc * 128 + i * 16 + r16, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+  }
+  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+#pragma unroll
+  for (int tn = 0; tn < 8; ++tn) {
+    const int col = n0 + wc * 128 + tn * 16 + r16;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 8; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
+        if (!a.mse) {
+          if (row < a.rows_eff && col < n_store) {
+            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
+            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+          }
+        } else {
+          const bool ok = live && row < a.rows_eff && col < n_store;
+          const int r = row % a.rows;
+          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
+          d *= d;
+          d += __shfl_xor(d, 1, 64);
+          d += __shfl_xor(d, 2, 64);
+          d += __shfl_xor(d, 4, 64);
+          d += __shfl_xor(d, 8, 64);
+          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+        }
+      }
+    }
+  }
+}
+
 // ---- bf16 GEMM, 256 x 256 tiles, 8-phase ping-pong schedule
 // Same tile and wave layout as gemm_glds256_kernel, but each 64-deep K tile is
 // four phases, one per 64 x 32 quadrant of a wave's 128 x 64 block (16
@@ -982,6 +1126,11 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
     const int tiles128 = ((a.Np + 127) / 128) * ((a.rows_eff + 127) / 128);
     const bool fits = !a.out64 && a.Kp % 64 == 0 && (a.lda & 7) == 0;
     const int tiles256 = ((a.Np + 255) / 256) * ((a.rows_eff + 255) / 256);
+    if (fits && a.path == 5) {
+      const size_t lds = size_t(2) * (256 + 256) * 64 * sizeof(__bf16);
+      hipLaunchKernelGGL(gemm_w4_kernel, dim3(tiles256), dim3(256), lds, s, a);
+      return;
+    }
     if (fits && a.path == 4) {
       const size_t lds = size_t(8) * 128 * 64 * sizeof(__bf16);
       hipLaunchKernelGGL(gemm_8ph_kernel, dim3(tiles256), dim3(512), lds, s, a);

@@ -243,7 +243,7 @@ def case_gemm(iters):
         res = {}
         for _ in range(1 if os.environ.get("SCA_PMC") else 2):  # interleaved rounds
             for name, fn in (("reg", lambda: run(1)), ("glds", lambda: run(2)), ("glds256", lambda: run(3)),
-                             ("8ph", lambda: run(4)), ("torch", lib)):
+                             ("8ph", lambda: run(4)), ("w4", lambda: run(5)), ("torch", lib)):
                 fn()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -256,7 +256,7 @@ def case_gemm(iters):
                 res[name] = min(res.get(name, 1e30), us)
         errs = {}
         ref = (A.float() @ W.float().T)
-        for pth, nm in ((3, "glds256"), (4, "8ph")):
+        for pth, nm in ((3, "glds256"), (4, "8ph"), (5, "w4")):
             run(pth)
             errs[nm + "_rel_err"] = float((O - ref).abs().max() / ref.abs().max())
         print(json.dumps({"case": "gemm_bf16", "M": rows, "K": K, "N": N,
