@@ -1131,12 +1131,14 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
       hipLaunchKernelGGL(gemm_w4_kernel, dim3(tiles256), dim3(256), lds, s, a);
       return;
     }
-    if (fits && a.path == 4) {
+    // default for chip-filling 256^2 grids: the 8-phase kernel (984 TF at
+    // 8192^3 vs 905 for path 3 and 774 for path 5, profiles/r03d_gemm)
+    if (fits && (a.path == 4 || (a.path == 0 && glds && a.Np >= 256 && tiles256 >= 256))) {
       const size_t lds = size_t(8) * 128 * 64 * sizeof(__bf16);
       hipLaunchKernelGGL(gemm_8ph_kernel, dim3(tiles256), dim3(512), lds, s, a);
       return;
     }
-    if (fits && (a.path == 3 || (a.path == 0 && glds && a.Np >= 256 && tiles256 >= 256))) {
+    if (fits && a.path == 3) {
       const size_t lds = size_t(2) * (256 + 256) * 64 * sizeof(__bf16);
       hipLaunchKernelGGL(gemm_glds256_kernel, dim3(tiles256), dim3(512), lds, s, a);
       return;
