@@ -352,13 +352,14 @@ PYBIND11_MODULE(_C, m) {
       .def("jacobi_stats", [](const gpu::MahalanobisDevice& d) {
         const auto t = d.jacobi_stats();
         py::dict r;
-        if (t.size() == 10) {
+        if (t.size() == 13) {
           r["last_sweeps"] = t[0];
           r["steps"] = t[1];
           r["mean_sweeps"] = t[1] > 0 ? t[2] / t[1] : 0.0;
-          static const char* names[7] = {"clip", "cov", "warm", "jacobi", "proj", "sm", "update"};
+          static const char* names[10] = {"clip", "cov", "warm", "eigen", "proj", "sm", "update",
+                                          "eigen.tridiag", "eigen.multisection", "eigen.vectors"};
           py::dict ph;
-          for (int i = 0; i < 7; ++i) ph[names[i]] = t[1] > 0 ? t[3 + i] / t[1] : 0.0;
+          for (int i = 0; i < 10; ++i) ph[names[i]] = t[1] > 0 ? t[3 + i] / t[1] : 0.0;
           r["phase_us_per_step"] = ph;
         }
         return r;

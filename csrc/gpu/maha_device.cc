@@ -311,9 +311,9 @@ std::vector<double> MahalanobisModel::jacobi_stats() const {
   if (st_->device < 0) return {};
   DeviceGuard dg(st_->device);
   if (st_->chained) SCA_HIP_CHECK(hipEventSynchronize(st_->chain.get()));
-  std::vector<double> t(10);
+  std::vector<double> t(13);
   SCA_HIP_CHECK(hipMemcpy(t.data(), st_->d_eig.as<double>() + kern::kMahaMaxP * kern::kMahaMaxP + 2,
-                          10 * sizeof(double), hipMemcpyDeviceToHost));
+                          13 * sizeof(double), hipMemcpyDeviceToHost));
   return t;
 }
 

@@ -239,10 +239,11 @@ inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
 inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (4 * size_t(p) + 2 * size_t(k)); }
 // eig: kMahaEigDoubles doubles, zero-initialised: the previous
 // step's eigenvectors (warm start of the Jacobi solve; not part of the state).
-// Tail: [has_v, m, sweeps of the last step, steps, total sweeps, phase us x 7]
-// (diagnostics after the first two: clip, cov, warm start, Jacobi, projections,
-// Sherman-Morrison, state update).
-constexpr int kMahaEigDoubles = kMahaMaxP * kMahaMaxP + 12;
+// Tail: [has_v, m, sweeps of the last step, steps, total sweeps, phase us x 10]
+// (diagnostics after the first two: clip, cov, warm start, eigen, projections,
+// Sherman-Morrison, state update; p > 16 eigen sub-phases: tridiagonalise,
+// multisection, inverse iteration + back-transformation).
+constexpr int kMahaEigDoubles = kMahaMaxP * kMahaMaxP + 15;
 void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* eig, double* ws, double* scores,
                hipStream_t stream);
 // Several request batches in order (seg: nseg + 1 row offsets, device-visible):

@@ -229,10 +229,29 @@ __device__ double invert_into(const double* A, double* M, double* inv, int k) {
   return det;
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// 64-bit DPP move (both halves) and a whole-wave sum: quad_perm / row
+// mirrors inside each 16-lane row (VALU, no LDS crossbar), then the four row
+// sums through v_readlane -- every lane gets the total.
+template <int CTRL> __device__ __forceinline__ double dpp64(double v) {
+  const int2 h = __builtin_bit_cast(int2, v);
+  int2 o;
+  o.x = __builtin_amdgcn_update_dpp(0, h.x, CTRL, 0xF, 0xF, false);
+  o.y = __builtin_amdgcn_update_dpp(0, h.y, CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, o);
+}
+__device__ __forceinline__ double readlane64(double v, int l) {
+  const int2 h = __builtin_bit_cast(int2, v);
+  int2 o;
+  o.x = __builtin_amdgcn_readlane(h.x, l);
+  o.y = __builtin_amdgcn_readlane(h.y, l);
+  return __builtin_bit_cast(double, o);
+}
+__device__ __forceinline__ double wave_sum(double v) {  // requires all 64 lanes active
+  v += dpp64<0xB1>(v);   // lane ^ 1
+  v += dpp64<0x4E>(v);   // lane ^ 2
+  v += dpp64<0x141>(v);  // row_half_mirror: the other quad of the 8
+  v += dpp64<0x140>(v);  // row_mirror: the other 8 of the 16
+  return (readlane64(v, 0) + readlane64(v, 16)) + (readlane64(v, 32) + readlane64(v, 48));
 }
 __device__ __forceinline__ double wave_min(double v) {
 #pragma unroll
@@ -261,9 +280,17 @@ __device__ __forceinline__ double wave_max(double v) {
 // barriers.
 template <int NT>
 __device__ void topk_tridiag(double* A, double* V, const double* W_, double* dg, double* eo, double* e2, double* wv,
-                             double* lam, int* sel, int p, int k) {
+                             double* lam, int* sel, int p, int k, uint64_t* sub) {
   double* W = const_cast<double*>(W_);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint64_t t_prev = __builtin_amdgcn_s_memrealtime();
+  auto mark = [&](int i) {  // sub-phase timer (thread 0)
+    if (tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      sub[i] += t - t_prev;
+      t_prev = t;
+    }
+  };
   constexpr int NW = NT / 64;
   // ---- 1. tridiagonalisation
   for (int j = 0; j + 2 < p; ++j) {
@@ -283,29 +310,31 @@ __device__ void topk_tridiag(double* A, double* V, const double* W_, double* dg,
       if (lane == 0) eo[j] = alpha;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // W row j visible to the wave's other lanes
       double pv = 0.0;
-      if (lane < m) {
-        const double* arow = A + (j + 1 + lane) * kLd + (j + 1);
-        const double* vr = W + j * kLd;
-#pragma unroll 8
-        for (int c = 0; c < m; ++c) pv += arow[c] * vr[c];
+      if (lane < m) {  // 4 independent chains, 16 loads in flight per unrolled block
+        const double* __restrict__ arow = A + (j + 1 + lane) * kLd + (j + 1);
+        const double* __restrict__ vr = W + j * kLd;
+        double s0 = 0.0, s1 = 0.0, s2v = 0.0, s3 = 0.0;
+        int c = 0;
+        for (; c + 8 <= m; c += 8) {
+          s0 += arow[c] * vr[c] + arow[c + 4] * vr[c + 4];
+          s1 += arow[c + 1] * vr[c + 1] + arow[c + 5] * vr[c + 5];
+          s2v += arow[c + 2] * vr[c + 2] + arow[c + 6] * vr[c + 6];
+          s3 += arow[c + 3] * vr[c + 3] + arow[c + 7] * vr[c + 7];
+        }
+        for (; c < m; ++c) s0 += arow[c] * vr[c];
+        pv = (s0 + s1) + (s2v + s3);
       }
       const double K = wave_sum(lane < m ? v * pv : 0.0);
       if (lane < m) wv[lane] = 2.0 * pv - 2.0 * K * v;
     }
     __syncthreads();
-    {  // A22 -= v w^T + w v^T  (row r, column c advanced without divisions)
-      const double* vr = W + j * kLd;
-      const int q = NT / m, rem = NT - q * m;
-      int r = tid / m, c = tid - r * m;
-      for (int e = tid; e < m * m; e += NT) {
-        A[(j + 1 + r) * kLd + (j + 1 + c)] -= vr[r] * wv[c] + wv[r] * vr[c];
-        r += q;
-        c += rem;
-        if (c >= m) {
-          c -= m;
-          ++r;
-        }
-      }
+    if (lane < m) {  // A22 -= v w^T + w v^T: lane = column, wave w = rows w, w + NW, ...
+      const double* __restrict__ vr = W + j * kLd;
+      const double* __restrict__ wr = wv;
+      const double vc = vr[lane], wc = wr[lane];
+      double* __restrict__ acol = A + (j + 1) * kLd + (j + 1) + lane;
+#pragma unroll 4
+      for (int r = wave; r < m; r += NW) acol[r * kLd] -= vr[r] * wc + wr[r] * vc;
     }
     __syncthreads();
   }
@@ -314,6 +343,7 @@ __device__ void topk_tridiag(double* A, double* V, const double* W_, double* dg,
   __syncthreads();
   for (int i = tid; i + 1 < p; i += NT) e2[i] = eo[i] * eo[i];
   __syncthreads();
+  mark(0);
   // ---- 2. k largest eigenvalues: Gershgorin bracket, 64-way multisection per wave
   const double di = lane < p ? dg[lane] : 0.0;
   const double ei = lane + 1 < p ? fabs(eo[lane]) : 0.0, em = lane >= 1 && lane < p ? fabs(eo[lane - 1]) : 0.0;
@@ -326,12 +356,17 @@ __device__ void topk_tridiag(double* A, double* V, const double* W_, double* dg,
     double l = lo, u = hi;
     for (int it = 0; it < 64; ++it) {
       const double x = l + (u - l) * (double(lane + 1) * (1.0 / 65.0));
-      // Sturm count: eigenvalues < x
+      // Sturm count: eigenvalues < x.  Only signs are counted, so 1/q is a
+      // v_rcp_f64 estimate refined by one Newton step instead of an IEEE
+      // division (a ~10-instruction dependent chain per element)
       double qv = dg[0] - x;
       int cnt = qv < 0.0;
+#pragma unroll 4
       for (int i = 1; i < p; ++i) {
         if (fabs(qv) < pivmin) qv = -pivmin;
-        qv = dg[i] - x - e2[i - 1] / qv;
+        double r = __builtin_amdgcn_rcp(qv);
+        r = r * (2.0 - qv * r);
+        qv = (dg[i] - x) - e2[i - 1] * r;
         cnt += qv < 0.0;
       }
       const unsigned long long mask = __ballot(cnt > idx);
@@ -351,65 +386,78 @@ __device__ void topk_tridiag(double* A, double* V, const double* W_, double* dg,
     if (lane == 0) lam[a] = 0.5 * (l + u);
   }
   __syncthreads();
-  // ---- 3. inverse iteration on T - lam I (lane 0 of the wave; LU scratch in A, now free)
-  for (int a = wave; a < k; a += NW) {
-    if (lane == 0) {
-      double* u0 = A + wave * 5 * kMahaMaxP;
-      double* u1 = u0 + kMahaMaxP;
-      double* u2 = u1 + kMahaMaxP;
-      double* lm = u2 + kMahaMaxP;
-      double* sw = lm + kMahaMaxP;
-      const double L = lam[a];
-      double cd = dg[0] - L, cu1 = p > 1 ? eo[0] : 0.0;
-      for (int i = 0; i + 1 < p; ++i) {
-        const double b = eo[i], an = dg[i + 1] - L, bn = i + 2 < p ? eo[i + 1] : 0.0;
-        if (fabs(b) > fabs(cd)) {  // pivot on row i + 1
-          u0[i] = b;
-          u1[i] = an;
-          u2[i] = bn;
-          const double mult = cd / b;
-          lm[i] = mult;
-          sw[i] = 1.0;
-          cd = cu1 - mult * an;
-          cu1 = -mult * bn;
-        } else {
-          if (fabs(cd) < pivmin) cd = pivmin;
-          u0[i] = cd;
-          u1[i] = cu1;
-          u2[i] = 0.0;
-          const double mult = b / cd;
-          lm[i] = mult;
-          sw[i] = 0.0;
-          cd = an - mult * cu1;
-          cu1 = bn;
-        }
-      }
-      if (fabs(cd) < pivmin) cd = pivmin;
-      u0[p - 1] = cd;
-      double* y = V;  // column a of V, stride kLd
-      for (int i = 0; i < p; ++i) y[i * kLd + a] = 1.0 + 0.1 * sin(1.7 * double(i + 1) + double(a));
-      for (int itr = 0; itr < 3; ++itr) {
-        for (int i = 0; i + 1 < p; ++i) {
-          if (sw[i] != 0.0) {
-            const double t0 = y[i * kLd + a];
-            y[i * kLd + a] = y[(i + 1) * kLd + a];
-            y[(i + 1) * kLd + a] = t0;
-          }
-          y[(i + 1) * kLd + a] -= lm[i] * y[i * kLd + a];
-        }
-        double nrm = 0.0;
-        for (int i = p - 1; i >= 0; --i) {
-          double t0 = y[i * kLd + a];
-          if (i + 1 < p) t0 -= u1[i] * y[(i + 1) * kLd + a];
-          if (i + 2 < p) t0 -= u2[i] * y[(i + 2) * kLd + a];
-          t0 /= u0[i];
-          y[i * kLd + a] = t0;
-          nrm = fmax(nrm, fabs(t0));
-        }
-        const double s = nrm > 0.0 ? 1.0 / nrm : 1.0;
-        for (int i = 0; i < p; ++i) y[i * kLd + a] *= s;
+  mark(1);
+  // ---- 3. inverse iteration on T - lam I: wave 0, lane a for eigenvalue a;
+  // LU factors in LDS (scratch in A, now free), the iterate y in registers
+  // (fully unrolled over kMahaMaxP rows), reciprocal pivots (no division in
+  // the solves); 2 iterations from a fixed start vector
+  if (wave == 0 && lane < k) {
+    const int a = lane;
+    double* u0 = A + a * 4 * kMahaMaxP;  // holds 1 / pivot; 16 x 4 x 64 <= 64 x kLd doubles
+    double* u1 = u0 + kMahaMaxP;
+    double* u2 = u1 + kMahaMaxP;
+    double* lm = u2 + kMahaMaxP;
+    unsigned long long swm = 0;  // row i + 1 was the pivot of step i
+    const double L = lam[a];
+    double cd = dg[0] - L, cu1 = p > 1 ? eo[0] : 0.0;
+    for (int i = 0; i + 1 < p; ++i) {
+      const double b = eo[i], an = dg[i + 1] - L, bn = i + 2 < p ? eo[i + 1] : 0.0;
+      if (fabs(b) > fabs(cd)) {  // pivot on row i + 1
+        u0[i] = 1.0 / b;
+        u1[i] = an;
+        u2[i] = bn;
+        const double mult = cd / b;
+        lm[i] = mult;
+        swm |= 1ull << i;
+        cd = cu1 - mult * an;
+        cu1 = -mult * bn;
+      } else {
+        if (fabs(cd) < pivmin) cd = pivmin;
+        u0[i] = 1.0 / cd;
+        u1[i] = cu1;
+        u2[i] = 0.0;
+        const double mult = b / cd;
+        lm[i] = mult;
+        cd = an - mult * cu1;
+        cu1 = bn;
       }
     }
+    if (fabs(cd) < pivmin) cd = pivmin;
+    u0[p - 1] = 1.0 / cd;
+    double y[kMahaMaxP];
+#pragma unroll
+    for (int i = 0; i < kMahaMaxP; ++i) y[i] = 1.0 + 0.1 * sin(1.7 * double(i + 1) + double(a));
+    for (int itr = 0; itr < 2; ++itr) {
+#pragma unroll
+      for (int i = 0; i + 1 < kMahaMaxP; ++i) {
+        if (i + 1 < p) {
+          if ((swm >> i) & 1ull) {
+            const double t0 = y[i];
+            y[i] = y[i + 1];
+            y[i + 1] = t0;
+          }
+          y[i + 1] -= lm[i] * y[i];
+        }
+      }
+      double nrm = 0.0;
+#pragma unroll
+      for (int i = kMahaMaxP - 1; i >= 0; --i) {
+        if (i < p) {
+          double t0 = y[i];
+          if (i + 1 < p) t0 -= u1[i] * y[i + 1];
+          if (i + 2 < p) t0 -= u2[i] * y[i + 2];
+          t0 *= u0[i];
+          y[i] = t0;
+          nrm = fmax(nrm, fabs(t0));
+        }
+      }
+      const double sc = nrm > 0.0 ? 1.0 / nrm : 1.0;
+#pragma unroll
+      for (int i = 0; i < kMahaMaxP; ++i) y[i] *= sc;
+    }
+#pragma unroll
+    for (int i = 0; i < kMahaMaxP; ++i)
+      if (i < p) V[i * kLd + a] = y[i];
   }
   __syncthreads();
   if (wave == 0) {  // normalise; re-orthogonalise within clusters (|lam_a - lam_b| < 1e-3 ||T||, as dstein)
@@ -438,6 +486,7 @@ __device__ void topk_tridiag(double* A, double* V, const double* W_, double* dg,
     if (lane < p) V[lane * kLd + a] = x;
   }
   __syncthreads();
+  mark(2);
 }
 
 // One request's step (CoreMahalanobis._get_preds for X [nb][p]) against the
@@ -476,7 +525,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   double* DPC = XR + size_t(nb) * p;        // [nb][k] projected (Xc - m)
   double* XD = DPC + size_t(nb) * k;        // [nb][k] projected (X - m)
 
-  uint64_t t_prev = __builtin_amdgcn_s_memrealtime(), ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t t_prev = __builtin_amdgcn_s_memrealtime(), ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   auto stamp = [&](int i) {  // phase timer (100 MHz), thread 0; accumulated into eig's tail
     if (tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
@@ -530,7 +579,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     __syncthreads();
     stamp(1);
     stamp(2);
-    topk_tridiag<NT>(A, V, W, tdg, teo, te2, twv, tlam, sel, p, k);
+    topk_tridiag<NT>(A, V, W, tdg, teo, te2, twv, tlam, sel, p, k, ph + 7);
     stamp(3);
     if (tid == 0) eig[kMahaMaxP * kMahaMaxP + 3] += 1.0;
   } else {
@@ -778,7 +827,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   stamp(6);
   if (tid == 0) {
     double* acc = eig + kMahaMaxP * kMahaMaxP + 5;
-    for (int i = 0; i < 7; ++i) acc[i] += double(ph[i]) * 0.01;  // microseconds
+    for (int i = 0; i < 10; ++i) acc[i] += double(ph[i]) * 0.01;  // microseconds
   }
 }
 

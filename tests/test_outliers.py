@@ -313,7 +313,7 @@ def test_mahalanobis_segmented_launch_matches_sequential_steps():
         state[-2] = 1.0  # c_zero
         ws = torch.zeros(60 * (4 * p + 2 * k), dtype=torch.float64, device="cuda")
         out = torch.full((X.shape[0],), -1.0, dtype=torch.float64, device="cuda")
-        eig = torch.zeros(64 * 64 + 12, dtype=torch.float64, device="cuda")  # cold start, then warm
+        eig = torch.zeros(64 * 64 + 15, dtype=torch.float64, device="cuda")  # cold start, then warm
         C.kernels.maha_step_segments(X.data_ptr(), seg.data_ptr(), len(reqs), p, k, 3.0, 50.0, -1.0, 1e-8, mode, thr,
                                      state.data_ptr(), eig.data_ptr(), ws.data_ptr(), out.data_ptr(), 0)
         torch.cuda.synchronize()
