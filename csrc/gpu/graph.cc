@@ -153,6 +153,17 @@ GraphModel::Aux& GraphModel::aux_for(hipStream_t s, int rows, int cols) {
   }
   Aux& a = *slot;
   if (size_t(rows) > a.cap_rows || cols != a.cap_cols) {
+    // Growth (rare: geometric) frees buffers that earlier batches of this
+    // slot used on every stage device: drain the slot's streams first rather
+    // than rely on hipFree's implicit synchronisation, which covers only the
+    // current device.
+    if (a.cap_rows > 0) {
+      SCA_HIP_CHECK(hipStreamSynchronize(s));
+      for (auto& kv : a.streams) {
+        DeviceGuard dg(kv.first);
+        SCA_HIP_CHECK(hipStreamSynchronize(kv.second.get()));
+      }
+    }
     size_t cap = std::max<size_t>(64, a.cap_rows);
     while (cap < size_t(rows)) cap <<= 1;
     stage_cols(cols, a.cols);
