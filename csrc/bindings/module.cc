@@ -349,15 +349,15 @@ PYBIND11_MODULE(_C, m) {
         return py::array_t<double>(py::ssize_t(s.size()), s.data());
       })
       .def("set_state", [](gpu::MahalanobisDevice& d, std::vector<double> s) { d.set_state(s); })
-      .def("jacobi_stats", [](const gpu::MahalanobisDevice& d) {
-        const auto t = d.jacobi_stats();
+      .def("solver_stats", [](const gpu::MahalanobisDevice& d) {
+        const auto t = d.solver_stats();
         py::dict r;
         if (t.size() == 13) {
-          r["last_sweeps"] = t[0];
           r["steps"] = t[1];
-          r["mean_sweeps"] = t[1] > 0 ? t[2] / t[1] : 0.0;
-          static const char* names[10] = {"clip", "cov", "warm", "eigen", "proj", "sm", "update",
-                                          "eigen.tridiag", "eigen.multisection", "eigen.vectors"};
+          // s_memtime cycles / s_memrealtime (100 MHz) ticks over the eigen phase
+          r["eigen_clock_mhz"] = t[2] > 0 ? t[0] / (t[2] * 0.01) : 0.0;
+          static const char* names[10] = {"clip", "cov", "eigen.inverse_iteration", "eigen", "proj", "sm", "update",
+                                          "eigen.tridiag", "eigen.eigenvalues", "eigen.back_transform"};
           py::dict ph;
           for (int i = 0; i < 10; ++i) ph[names[i]] = t[1] > 0 ? t[3 + i] / t[1] : 0.0;
           r["phase_us_per_step"] = ph;

@@ -306,7 +306,7 @@ std::vector<double> MahalanobisModel::state() const {
   return s;
 }
 
-std::vector<double> MahalanobisModel::jacobi_stats() const {
+std::vector<double> MahalanobisModel::solver_stats() const {
   std::lock_guard<std::mutex> g(st_->mu);
   if (st_->device < 0) return {};
   DeviceGuard dg(st_->device);

@@ -31,7 +31,7 @@ struct MahaState {
   kern::MahaParams prm;
   int device = -1;                 // -1: host state (CPU reference path)
   DeviceBuffer d_state;
-  DeviceBuffer d_eig;              // previous eigenvectors (Jacobi warm start; a hint, not state)
+  DeviceBuffer d_eig;              // device diagnostics (step count, phase timers; not state)
   std::vector<double> h_state;     // device -1
   Event chain;                     // completes after the last launched step
   bool chained = false;
@@ -61,8 +61,8 @@ class MahalanobisModel : public RowModel {
   std::vector<double> state() const;  // mean[p] | C[p*p] | lo[p] | hi[p] | n | c_zero | has_clip
   void set_state(const std::vector<double>& s);
   std::shared_ptr<MahaState> shared_state() const { return st_; }
-  // Jacobi diagnostics: {sweeps of the last step, steps, total sweeps} (GPU state only).
-  std::vector<double> jacobi_stats() const;
+  // Device diagnostics: {0, steps, 0, phase us x 10} (GPU state only).
+  std::vector<double> solver_stats() const;
   int p() const { return st_->prm.p; }
   int k() const { return st_->prm.k; }
   int device() const { return st_->device; }
@@ -87,7 +87,7 @@ class MahalanobisDevice {
   // Predictions view over the same state (for a native graph node).
   std::shared_ptr<MahalanobisModel> predict_view(double threshold) const;
   BatcherStats stats() const { return unit_->stats(); }
-  std::vector<double> jacobi_stats() const { return model_->jacobi_stats(); }
+  std::vector<double> solver_stats() const { return model_->solver_stats(); }
   int p() const { return model_->p(); }
   int k() const { return model_->k(); }
   int device() const { return model_->device(); }

@@ -222,8 +222,9 @@ void mlp_mse_finish(const float* mse, int rows, double scale, double* out, hipSt
 // Mahalanobis detector: Sherman-Morrison recurrence + scores over a batch
 // (B [nb][k][k], cov0 [k][k], xd [nb][k]); false if k > 16.
 // Whole Mahalanobis detector step on the device (CoreMahalanobis.py:68-151):
-// clip, running mean / covariance update, top-k eigenvectors (parallel cyclic
-// Jacobi in LDS), projections, Sherman-Morrison scores, state update -- one
+// clip, running mean / covariance update, top-k eigenvectors (one-wave
+// Householder tridiagonalisation + Sturm multisection + inverse iteration in
+// LDS), projections, Sherman-Morrison scores, state update -- one
 // single-workgroup launch per request batch, state resident in HBM.
 constexpr int kMahaMaxP = 64;
 constexpr int kMahaMaxK = 16;
@@ -237,12 +238,13 @@ struct MahaParams {
 inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
 // workspace doubles for a batch of nb rows
 inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (4 * size_t(p) + 2 * size_t(k)); }
-// eig: kMahaEigDoubles doubles, zero-initialised: the previous
-// step's eigenvectors (warm start of the Jacobi solve; not part of the state).
-// Tail: [has_v, m, sweeps of the last step, steps, total sweeps, phase us x 10]
-// (diagnostics after the first two: clip, cov, warm start, eigen, projections,
-// Sherman-Morrison, state update; p > 16 eigen sub-phases: tridiagonalise,
-// multisection, inverse iteration + back-transformation).
+// eig: kMahaEigDoubles doubles, zero-initialised device diagnostics (not
+// part of the state; the first kMahaMaxP^2 are reserved).
+// Tail: [0, 0, eigen-phase shader cycles, steps, eigen-phase 100 MHz ticks,
+// phase us x 10]: clip, cov, (unused), eigen,
+// projections, Sherman-Morrison, state update, and the eigen sub-phases
+// tridiagonalise, eigenvalues (multisection), eigenvectors (inverse
+// iteration + back-transformation).
 constexpr int kMahaEigDoubles = kMahaMaxP * kMahaMaxP + 15;
 void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* eig, double* ws, double* scores,
                hipStream_t stream);

@@ -20,44 +20,12 @@ namespace {
 
 constexpr int kMaxK = 16;
 
-// Gauss-Jordan with partial pivoting on a k x k copy; returns det.
-__device__ double invert(const double* A, double* inv, int k) {
-  double M[kMaxK * kMaxK];
-  for (int e = 0; e < k * k; ++e) {
-    M[e] = A[e];
-    inv[e] = (e / k == e % k) ? 1.0 : 0.0;
-  }
-  double det = 1.0;
-  for (int c = 0; c < k; ++c) {
-    int piv = c;
-    for (int r = c + 1; r < k; ++r)
-      if (fabs(M[r * k + c]) > fabs(M[piv * k + c])) piv = r;
-    if (M[piv * k + c] == 0.0) return 0.0;
-    if (piv != c) {
-      for (int j = 0; j < k; ++j) {
-        double t = M[c * k + j]; M[c * k + j] = M[piv * k + j]; M[piv * k + j] = t;
-        t = inv[c * k + j]; inv[c * k + j] = inv[piv * k + j]; inv[piv * k + j] = t;
-      }
-      det = -det;
-    }
-    const double d = M[c * k + c];
-    det *= d;
-    const double id = 1.0 / d;
-    for (int j = 0; j < k; ++j) { M[c * k + j] *= id; inv[c * k + j] *= id; }
-    for (int r = 0; r < k; ++r) {
-      if (r == c) continue;
-      const double f = M[r * k + c];
-      if (f == 0.0) continue;
-      for (int j = 0; j < k; ++j) { M[r * k + j] -= f * M[c * k + j]; inv[r * k + j] -= f * inv[c * k + j]; }
-    }
-  }
-  return det;
-}
+__device__ double invert_into(const double* A, double* M, double* inv, int k);
 
 __global__ __launch_bounds__(64) void maha_sm_kernel(const double* __restrict__ B, const double* __restrict__ cov0,
                                                      const double* __restrict__ xd, int nb, int k, double n,
                                                      double eps, double* __restrict__ out) {
-  __shared__ double P[kMaxK * kMaxK], Cp[kMaxK * kMaxK], T1[kMaxK * kMaxK], T2[kMaxK * kMaxK];
+  __shared__ double P[kMaxK * kMaxK], Cp[kMaxK * kMaxK], T1[kMaxK * kMaxK], T2[kMaxK * kMaxK], Mw[kMaxK * kMaxK];
   __shared__ int valid, inverted;
   __shared__ double scal;
   const int lane = threadIdx.x;
@@ -70,10 +38,9 @@ __global__ __launch_bounds__(64) void maha_sm_kernel(const double* __restrict__ 
     if (!valid) {
       if (lane == 0) {
         inverted = 0;
-        double inv[kMaxK * kMaxK];
-        const double det = invert(P, inv, k);
+        const double det = invert_into(P, Mw, T1, k);  // T1 is free here
         if (fabs(det) > eps) {
-          for (int e = 0; e < kk; ++e) Cp[e] = inv[e];
+          for (int e = 0; e < kk; ++e) Cp[e] = T1[e];
           inverted = 1;
           valid = 1;
         }
@@ -131,24 +98,21 @@ __global__ __launch_bounds__(64) void maha_sm_kernel(const double* __restrict__ 
 
 // ------------------------------------------------------------ full detector step
 // One workgroup runs CoreMahalanobis._get_preds (:68-151) for one request
-// batch against the device-resident state: NT = 64 threads (one wave: every
-// barrier is nearly free) for p <= 16, 256 otherwise.  p <= 64 features,
-// k <= 16 components; p x p matrices live in LDS (row stride kLd = 65).
-//
-// Eigenvectors: parallel cyclic Jacobi, warm-started from the previous step's
-// eigenvectors (kept in `eig`, a hint outside the checkpointed state): V is
-// re-orthonormalised by one Newton-Schulz step (V <- 1.5 V - 0.5 V V^T V), A =
-// V^T C V is then nearly diagonal and converges in 1-3 sweeps instead of
-// ~8-10 from the identity.  A round applies every pair's rotation to both
-// sides at once (2 x 2 block B_ij <- J_i^T B_ij J_j), two barriers per round.
-// Converged to the same 1e-15 relative off-diagonal norm as a cold start, so
-// the scores do not depend on the hint (eigenvector signs / order cancel).
+// batch against the device-resident state: NT = 64 threads (one wave) for
+// p <= 16, 256 otherwise.  p <= 64 features, k <= 16 components; p x p
+// matrices live in LDS (row stride kLd = 65, conflict-free row-per-lane
+// access).  The top-k eigenpairs are computed by ONE wave (topk_wave): a
+// latency chain of ~p dependent steps, where extra waves would only add
+// barriers.
 constexpr int kLd = kMahaMaxP + 1;
-constexpr int kMaxSweeps = 40;
+// A (the matrix the eigen-solver streams) has 8 private padding columns per
+// row, so 8-wide blocks may run past p without guards (73: still odd, rows
+// on distinct banks)
+constexpr int kLdA = kMahaMaxP + 9;
 
+__device__ __forceinline__ double wave_sum(double v);
 template <int NT> __device__ double block_sum(double v, double* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v = wave_sum(v);
   if constexpr (NT == 64) {
     return v;
   } else {
@@ -159,39 +123,6 @@ template <int NT> __device__ double block_sum(double v, double* red) {
 #pragma unroll
     for (int w = 0; w < NT / 64; ++w) t += red[w];
     return t;
-  }
-}
-
-// C = op(A) . B for m x m LDS matrices (stride kLd), 4 x 4 register tiles;
-// op = transpose when TA.  Rows / columns past m read whatever the 64 x 65
-// buffers hold but only feed outputs that are not written.
-template <int NT, bool TA>
-__device__ void mm(const double* A, const double* B, double* C, int m) {
-  const int tm = (m + 3) >> 2;
-  for (int t = threadIdx.x; t < tm * tm; t += NT) {
-    const int ti = t / tm;
-    const int i0 = ti * 4, j0 = (t - ti * tm) * 4;
-    double acc[4][4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
-    for (int kx = 0; kx < m; ++kx) {
-      double a[4], b[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] = TA ? A[kx * kLd + i0 + r] : A[(i0 + r) * kLd + kx];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) b[c] = B[kx * kLd + j0 + c];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[r][c] += a[r] * b[c];
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (i0 + r < m && j0 + c < m) C[(i0 + r) * kLd + j0 + c] = acc[r][c];
   }
 }
 
@@ -246,246 +177,415 @@ __device__ __forceinline__ double readlane64(double v, int l) {
   o.y = __builtin_amdgcn_readlane(h.y, l);
   return __builtin_bit_cast(double, o);
 }
-__device__ __forceinline__ double wave_sum(double v) {  // requires all 64 lanes active
-  v += dpp64<0xB1>(v);   // lane ^ 1
-  v += dpp64<0x4E>(v);   // lane ^ 2
-  v += dpp64<0x141>(v);  // row_half_mirror: the other quad of the 8
-  v += dpp64<0x140>(v);  // row_mirror: the other 8 of the 16
-  return (readlane64(v, 0) + readlane64(v, 16)) + (readlane64(v, 32) + readlane64(v, 48));
+template <int CTRL> __device__ __forceinline__ double mdpp64(double v) {  // DPP move, no old-value operand
+  const int2 h = __builtin_bit_cast(int2, v);
+  int2 o;
+  o.x = __builtin_amdgcn_mov_dpp(h.x, CTRL, 0xF, 0xF, true);
+  o.y = __builtin_amdgcn_mov_dpp(h.y, CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, o);
+}
+// v + (v of the partner lane) for v_permlane16_swap (lane ^ 16) or
+// v_permlane32_swap (lane ^ 32): a half exchange of vdst with src, here both v
+template <bool P32> __device__ __forceinline__ double swap_add64(double v) {
+  const int2 h = __builtin_bit_cast(int2, v);
+  const auto a = P32 ? __builtin_amdgcn_permlane32_swap(h.x, h.x, false, false)
+                     : __builtin_amdgcn_permlane16_swap(h.x, h.x, false, false);
+  const auto b = P32 ? __builtin_amdgcn_permlane32_swap(h.y, h.y, false, false)
+                     : __builtin_amdgcn_permlane16_swap(h.y, h.y, false, false);
+  return __builtin_bit_cast(double, make_int2(int(a[0]), int(b[0]))) +
+         __builtin_bit_cast(double, make_int2(int(a[1]), int(b[1])));
+}
+// whole-wave double sum, every lane gets the total: 4 DPP stages inside
+// each 16-lane row, then the two cross-row exchanges (VALU only, no SGPR
+// hop; 172 vs 192 clocks for DPP + v_readlane, 492 for __shfl_xor on
+// MI355X, tools/micro/wave_latency.hip).  Requires all 64 lanes active.
+__device__ __forceinline__ double wave_sum(double v) {
+  v += mdpp64<0xB1>(v);   // lane ^ 1
+  v += mdpp64<0x4E>(v);   // lane ^ 2
+  v += mdpp64<0x141>(v);  // row_half_mirror: the other quad of the 8
+  v += mdpp64<0x140>(v);  // row_mirror: the other 8 of the 16
+  v = swap_add64<false>(v);
+  return swap_add64<true>(v);
+}
+template <bool P32> __device__ __forceinline__ double swap_partner64(double v) {  // v of lane ^ 16 / ^ 32
+  const int2 h = __builtin_bit_cast(int2, v);
+  const auto a = P32 ? __builtin_amdgcn_permlane32_swap(h.x, h.x, false, false)
+                     : __builtin_amdgcn_permlane16_swap(h.x, h.x, false, false);
+  const auto b = P32 ? __builtin_amdgcn_permlane32_swap(h.y, h.y, false, false)
+                     : __builtin_amdgcn_permlane16_swap(h.y, h.y, false, false);
+  return __builtin_bit_cast(double, make_int2(int(a[0]), int(b[0])));  // own or partner value
+}
+template <bool P32> __device__ __forceinline__ double swap_other64(double v) {
+  const int2 h = __builtin_bit_cast(int2, v);
+  const auto a = P32 ? __builtin_amdgcn_permlane32_swap(h.x, h.x, false, false)
+                     : __builtin_amdgcn_permlane16_swap(h.x, h.x, false, false);
+  const auto b = P32 ? __builtin_amdgcn_permlane32_swap(h.y, h.y, false, false)
+                     : __builtin_amdgcn_permlane16_swap(h.y, h.y, false, false);
+  return __builtin_bit_cast(double, make_int2(int(a[1]), int(b[1])));  // the other one
 }
 __device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmin(v, mdpp64<0xB1>(v));
+  v = fmin(v, mdpp64<0x4E>(v));
+  v = fmin(v, mdpp64<0x141>(v));
+  v = fmin(v, mdpp64<0x140>(v));
+  // one of the two swap results is the lane's own value: min over both
+  v = fmin(v, fmin(swap_partner64<false>(v), swap_other64<false>(v)));
+  return fmin(v, fmin(swap_partner64<true>(v), swap_other64<true>(v)));
 }
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmax(v, mdpp64<0xB1>(v));
+  v = fmax(v, mdpp64<0x4E>(v));
+  v = fmax(v, mdpp64<0x141>(v));
+  v = fmax(v, mdpp64<0x140>(v));
+  v = fmax(v, fmax(swap_partner64<false>(v), swap_other64<false>(v)));
+  return fmax(v, fmax(swap_partner64<true>(v), swap_other64<true>(v)));
+}
+// 1 / x from v_rcp_f64 plus two Newton steps (full double precision; no
+// IEEE division sequence in the dependent chains below)
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = r * fma(-x, r, 2.0);
+  return r * fma(-x, r, 2.0);
+}
+// LDS ordering point for one wave: the lanes' stores above are visible to
+// the wave's loads below (LDS executes one wave's accesses in order; this
+// keeps the compiler from moving them across).
+__device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// 1 / sqrt(x) from v_rsq_f64 plus two Newton steps
+__device__ __forceinline__ double rsq_nr(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  r = r * fma(-0.5 * x * r, r, 1.5);
+  return r * fma(-0.5 * x * r, r, 1.5);
 }
 
+// x = H_0 ... H_{p-3} x for the KB vectors in V columns a0..a0+KB-1 (lane =
+// row): per reflector, KB independent wave sums (their latencies overlap)
+template <int KB>
+__device__ void back_transform(double* __restrict__ V, const double* __restrict__ Wr, int p, int a0) {
+  const int lane = threadIdx.x & 63;
+  const bool inp = lane < p;
+  double xa[KB];
+#pragma unroll
+  for (int a = 0; a < KB; ++a) xa[a] = inp ? V[lane * kLd + a0 + a] : 0.0;
+  double vt = p >= 3 && lane > p - 3 && inp ? Wr[(p - 3) * kLd + lane] : 0.0;
+  for (int j = p - 3; j >= 0; --j) {
+    const double vnext = j >= 1 && lane > j - 1 && inp ? Wr[(j - 1) * kLd + lane] : 0.0;  // read ahead
+    double sa[KB];
+#pragma unroll
+    for (int a = 0; a < KB; ++a) sa[a] = wave_sum(vt * xa[a]);
+#pragma unroll
+    for (int a = 0; a < KB; ++a) xa[a] -= 2.0 * sa[a] * vt;
+    vt = vnext;
+  }
+#pragma unroll
+  for (int a = 0; a < KB; ++a)
+    if (inp) V[lane * kLd + a0 + a] = xa[a];
+}
+
+// LDS scratch of the eigen-solver (padded by 8 so blocked loops may read
+// past p without leaving the arrays)
+struct EigScratch {
+  double2 rv[kMahaMaxP + 8];  // (v_c, w_c) of the reflector being applied
+  double rn[kMahaMaxP + 8];   // the next reflector
+  double dg[kMahaMaxP + 8], eo[kMahaMaxP + 8];   // tridiagonal T
+  double sd[kMahaMaxP + 16], se2[kMahaMaxP + 16];  // T / 2^E, squared off-diagonal / 2^2E (Sturm counts; a block read ahead)
+  double lam[kMahaMaxK];
+};
+
 // Top-k eigenpairs of the symmetric p x p matrix in A (LDS, stride kLd;
-// destroyed) for p > 16, the way LAPACK's syevr computes a subset (which is
-// what the reference's scipy eigh(eigvals=(p-k, p-1)) runs):
-//  1. Householder tridiagonalisation: per column one wave forms the
-//     reflector v (kept in W row j) and w = 2 A22 v - 2 (v.A22 v) v, then all
-//     threads apply A22 -= v w^T + w v^T (two barriers per column);
-//  2. the k largest eigenvalues by 64-way multisection on Sturm counts, one
-//     wave per eigenvalue (ballot picks the subinterval, no barriers);
-//  3. their tridiagonal eigenvectors by inverse iteration (LU with partial
-//     pivoting on one lane, 3 iterations), re-orthogonalised within clusters;
-//  4. back-transformation through the reflectors, one wave per vector.
-// Output: eigenvectors in V[:, 0..k-1], sel[a] = a.  Replaces ~3.5 warm
-// Jacobi sweeps (63 two-barrier rounds each at p = 64, ~485 us) with ~2p
-// barriers.
-template <int NT>
-__device__ void topk_tridiag(double* A, double* V, const double* W_, double* dg, double* eo, double* e2, double* wv,
-                             double* lam, int* sel, int p, int k, uint64_t* sub) {
-  double* W = const_cast<double*>(W_);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// destroyed), the way LAPACK's syevr computes a subset (what the reference's
+// scipy eigh(eigvals=(p-k, p-1)) runs), by the 64 lanes of ONE wave -- lane g
+// owns matrix row g, so no step needs a workgroup barrier.  Every loop that
+// streams LDS is blocked by 8 with the block's loads issued before its
+// arithmetic, so one LDS latency covers 8 elements of a dependent chain.
+//  1. Householder tridiagonalisation, one pass over the active rows per
+//     column: the pass applies column j's rank-2 update A -= v w^T + w v^T
+//     and, in the same sweep, the matrix-vector product of column j + 1's
+//     reflector (column j + 1 is updated in registers first -- its entries
+//     were kept from the previous pass -- so the reflector exists before the
+//     pass);
+//  2. the k largest eigenvalues by multisection on Sturm counts, the wave
+//     split into k lane groups (64 / k points per group and round, the
+//     subinterval picked by ballot; every lane recomputes the same section
+//     points, no shuffles).  Counts are sign changes of the leading minors
+//     P_{i+1} = (d_i - x) P_i - e_{i-1}^2 P_{i-1} on T scaled by 2^-E ~
+//     1 / ||T|| (renormalised every 8 steps): 2 dependent flops per element
+//     instead of a reciprocal chain;
+//  3. their tridiagonal eigenvectors by inverse iteration, lane a for
+//     eigenvalue a (LU with partial pivoting, 2 iterations), normalised and
+//     re-orthogonalised within clusters (as dstein);
+//  4. back-transformation through the reflectors, all k vectors per step.
+// Wr: reflectors (row j = reflector j, indexed by global row).  Output:
+// eigenvectors in V[:, 0..k-1], sel[a] = a.
+__device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ Wr, EigScratch& es,
+                          int* sel, int p, int k, uint64_t* sub) {
+  const int lane = threadIdx.x & 63;
+  const bool inp = lane < p;
   uint64_t t_prev = __builtin_amdgcn_s_memrealtime();
-  auto mark = [&](int i) {  // sub-phase timer (thread 0)
-    if (tid == 0) {
+  auto mark = [&](int i) {  // sub-phase timer (lane 0)
+    if (lane == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
       sub[i] += t - t_prev;
       t_prev = t;
     }
   };
-  constexpr int NW = NT / 64;
+  double* __restrict__ arow = A + lane * kLdA;
+  double* __restrict__ dg = es.dg;
+  double* __restrict__ eo = es.eo;
   // ---- 1. tridiagonalisation
-  for (int j = 0; j + 2 < p; ++j) {
-    const int m = p - j - 1;
-    if (wave == 0) {
-      const double x = lane < m ? A[(j + 1 + lane) * kLd + j] : 0.0;
-      const double s2 = wave_sum(x * x);
-      const double x0 = __shfl(x, 0, 64);
-      double alpha = 0.0, v = 0.0;
-      if (s2 > 0.0) {
-        alpha = x0 >= 0.0 ? -sqrt(s2) : sqrt(s2);
-        v = lane == 0 ? x - alpha : x;
-        const double vn2 = s2 - x0 * x0 + (x0 - alpha) * (x0 - alpha);  // > 0: x0 and alpha have opposite signs
-        v *= 1.0 / sqrt(vn2);
-      }
-      if (lane < m) W[j * kLd + lane] = v;
-      if (lane == 0) eo[j] = alpha;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // W row j visible to the wave's other lanes
-      double pv = 0.0;
-      if (lane < m) {  // 4 independent chains, 16 loads in flight per unrolled block
-        const double* __restrict__ arow = A + (j + 1 + lane) * kLd + (j + 1);
-        const double* __restrict__ vr = W + j * kLd;
-        double s0 = 0.0, s1 = 0.0, s2v = 0.0, s3 = 0.0;
-        int c = 0;
-        for (; c + 8 <= m; c += 8) {
-          s0 += arow[c] * vr[c] + arow[c + 4] * vr[c + 4];
-          s1 += arow[c + 1] * vr[c + 1] + arow[c + 5] * vr[c + 5];
-          s2v += arow[c + 2] * vr[c + 2] + arow[c + 6] * vr[c + 6];
-          s3 += arow[c + 3] * vr[c + 3] + arow[c + 7] * vr[c + 7];
+  // reflector j from x (column j, rows j+1..p-1 on their lanes, 0 elsewhere):
+  // v (unit norm) -> Wr row j and rn; alpha -> eo[j]
+  auto reflect = [&](int j, double x) -> double {
+    const double s2 = wave_sum(x * x);
+    const double x0 = readlane64(x, j + 1);
+    double v = 0.0, alpha = 0.0;
+    if (s2 > 0.0) {
+      const double nrm = s2 * rsq_nr(s2);
+      alpha = x0 >= 0.0 ? -nrm : nrm;
+      // |v_raw|^2 = s2 - x0^2 + (x0 - alpha)^2 = 2 (s2 + |x0| nrm)
+      v = (lane == j + 1 ? x - alpha : x) * rsq_nr(2.0 * fma(fabs(x0), nrm, s2));
+    }
+    if (lane == 0) eo[j] = alpha;
+    if (lane > j && inp) {
+      Wr[j * kLd + lane] = v;
+      es.rn[lane] = v;
+    }
+    return v;
+  };
+  // zero padding: columns p..p+7 of every active row, reflector slots past p;
+  // Sturm pads (d = 4 > any scaled shift, e^2 = 0) add no sign change
+  if (inp)
+    for (int c = p; c < kMahaMaxP + 8; ++c) arow[c] = 0.0;
+  for (int c = p + lane; c < kMahaMaxP + 8; c += 64) {
+    es.rv[c] = make_double2(0.0, 0.0);
+    es.rn[c] = 0.0;
+  }
+  for (int c = p + lane; c < kMahaMaxP + 16; c += 64) es.sd[c] = 4.0;
+  for (int c = p - 1 + lane; c < kMahaMaxP + 16; c += 64)
+    if (c >= 0) es.se2[c] = 0.0;
+  if (lane == 0) dg[0] = A[0];
+  if (p == 2 && lane == 0) {
+    dg[1] = A[kLdA + 1];
+    eo[0] = A[kLdA];
+  }
+  if (p >= 3) {
+    double vg = reflect(0, lane >= 1 && inp ? arow[0] : 0.0);
+    double col = lane >= 1 && inp ? arow[1] : 0.0;  // this row's entry of the next column
+    wave_lds_sync();
+    double pv = 0.0;
+    if (lane >= 1 && inp) {
+      double s[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int cb = 1; cb < p; cb += 8) {
+        double av[8], nv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          av[u] = arow[cb + u];
+          nv[u] = es.rn[cb + u];
         }
-        for (; c < m; ++c) s0 += arow[c] * vr[c];
-        pv = (s0 + s1) + (s2v + s3);
-      }
-      const double K = wave_sum(lane < m ? v * pv : 0.0);
-      if (lane < m) wv[lane] = 2.0 * pv - 2.0 * K * v;
-    }
-    __syncthreads();
-    if (lane < m) {  // A22 -= v w^T + w v^T: lane = column, wave w = rows w, w + NW, ...
-      const double* __restrict__ vr = W + j * kLd;
-      const double* __restrict__ wr = wv;
-      const double vc = vr[lane], wc = wr[lane];
-      double* __restrict__ acol = A + (j + 1) * kLd + (j + 1) + lane;
-#pragma unroll 4
-      for (int r = wave; r < m; r += NW) acol[r * kLd] -= vr[r] * wc + wr[r] * vc;
-    }
-    __syncthreads();
-  }
-  for (int i = tid; i < p; i += NT) dg[i] = A[i * kLd + i];
-  if (tid == 0 && p >= 2) eo[p - 2] = A[(p - 1) * kLd + (p - 2)];
-  __syncthreads();
-  for (int i = tid; i + 1 < p; i += NT) e2[i] = eo[i] * eo[i];
-  __syncthreads();
-  mark(0);
-  // ---- 2. k largest eigenvalues: Gershgorin bracket, 64-way multisection per wave
-  const double di = lane < p ? dg[lane] : 0.0;
-  const double ei = lane + 1 < p ? fabs(eo[lane]) : 0.0, em = lane >= 1 && lane < p ? fabs(eo[lane - 1]) : 0.0;
-  const double lo0 = wave_min(lane < p ? di - ei - em : 1e300), hi0 = wave_max(lane < p ? di + ei + em : -1e300);
-  const double tnorm = fmax(fabs(lo0), fabs(hi0));
-  const double pivmin = fmax(tnorm, 1e-300) * 2.3e-16;
-  const double lo = lo0 - 1e-10 * tnorm - 1e-300, hi = hi0 + 1e-10 * tnorm + 1e-300;
-  for (int a = wave; a < k; a += NW) {
-    const int idx = p - 1 - a;  // ascending index of the a-th largest eigenvalue
-    double l = lo, u = hi;
-    for (int it = 0; it < 64; ++it) {
-      const double x = l + (u - l) * (double(lane + 1) * (1.0 / 65.0));
-      // Sturm count: eigenvalues < x.  Only signs are counted, so 1/q is a
-      // v_rcp_f64 estimate refined by one Newton step instead of an IEEE
-      // division (a ~10-instruction dependent chain per element)
-      double qv = dg[0] - x;
-      int cnt = qv < 0.0;
-#pragma unroll 4
-      for (int i = 1; i < p; ++i) {
-        if (fabs(qv) < pivmin) qv = -pivmin;
-        double r = __builtin_amdgcn_rcp(qv);
-        r = r * (2.0 - qv * r);
-        qv = (dg[i] - x) - e2[i - 1] * r;
-        cnt += qv < 0.0;
-      }
-      const unsigned long long mask = __ballot(cnt > idx);
-      double nl, nu;
-      if (mask) {
-        const int f = __ffsll(static_cast<long long>(mask)) - 1;
-        nu = __shfl(x, f, 64);
-        nl = f > 0 ? __shfl(x, f - 1, 64) : l;
-      } else {
-        nl = __shfl(x, 63, 64);
-        nu = u;
-      }
-      l = nl;
-      u = nu;
-      if (u - l <= 2.3e-16 * fmax(fabs(l), fabs(u)) + 1e-18 * tnorm + 1e-300) break;
-    }
-    if (lane == 0) lam[a] = 0.5 * (l + u);
-  }
-  __syncthreads();
-  mark(1);
-  // ---- 3. inverse iteration on T - lam I: wave 0, lane a for eigenvalue a;
-  // LU factors in LDS (scratch in A, now free), the iterate y in registers
-  // (fully unrolled over kMahaMaxP rows), reciprocal pivots (no division in
-  // the solves); 2 iterations from a fixed start vector
-  if (wave == 0 && lane < k) {
-    const int a = lane;
-    double* u0 = A + a * 4 * kMahaMaxP;  // holds 1 / pivot; 16 x 4 x 64 <= 64 x kLd doubles
-    double* u1 = u0 + kMahaMaxP;
-    double* u2 = u1 + kMahaMaxP;
-    double* lm = u2 + kMahaMaxP;
-    unsigned long long swm = 0;  // row i + 1 was the pivot of step i
-    const double L = lam[a];
-    double cd = dg[0] - L, cu1 = p > 1 ? eo[0] : 0.0;
-    for (int i = 0; i + 1 < p; ++i) {
-      const double b = eo[i], an = dg[i + 1] - L, bn = i + 2 < p ? eo[i + 1] : 0.0;
-      if (fabs(b) > fabs(cd)) {  // pivot on row i + 1
-        u0[i] = 1.0 / b;
-        u1[i] = an;
-        u2[i] = bn;
-        const double mult = cd / b;
-        lm[i] = mult;
-        swm |= 1ull << i;
-        cd = cu1 - mult * an;
-        cu1 = -mult * bn;
-      } else {
-        if (fabs(cd) < pivmin) cd = pivmin;
-        u0[i] = 1.0 / cd;
-        u1[i] = cu1;
-        u2[i] = 0.0;
-        const double mult = b / cd;
-        lm[i] = mult;
-        cd = an - mult * cu1;
-        cu1 = bn;
-      }
-    }
-    if (fabs(cd) < pivmin) cd = pivmin;
-    u0[p - 1] = 1.0 / cd;
-    double y[kMahaMaxP];
 #pragma unroll
-    for (int i = 0; i < kMahaMaxP; ++i) y[i] = 1.0 + 0.1 * sin(1.7 * double(i + 1) + double(a));
-    for (int itr = 0; itr < 2; ++itr) {
+        for (int u = 0; u < 8; ++u) s[u & 3] += av[u] * nv[u];
+      }
+      pv = (s[0] + s[1]) + (s[2] + s[3]);
+    }
+    double K = wave_sum(vg * pv);
+    double wg = 2.0 * pv - 2.0 * K * vg;
+    if (inp) es.rv[lane] = make_double2(vg, wg);
+    wave_lds_sync();
+    for (int j = 0; j + 2 < p; ++j) {
+      // column j + 1 after update j (lane j + 1: the new diagonal entry)
+      const double vj1 = readlane64(vg, j + 1), wj1 = readlane64(wg, j + 1);
+      const double x = lane > j && inp ? col - (vg * wj1 + wg * vj1) : 0.0;
+      if (lane == j + 1) dg[j + 1] = x;
+      if (j + 3 < p) {
+        const double vn = reflect(j + 1, lane > j + 1 ? x : 0.0);
+        wave_lds_sync();
+        // fused pass over columns j+2..p-1 of rows j+2..p-1: update j, then
+        // (A v_{j+1}) with the updated entries
+        pv = 0.0;
+        if (lane > j + 1 && inp) {
+          double s[4] = {0.0, 0.0, 0.0, 0.0};
+          const int c0 = j + 2;
+          // (a single wave is VALU-issue bound here, ~3 f64 ops per entry:
+          // reading the next block ahead measured slower, not faster)
+          for (int cb = c0; cb < p; cb += 8) {
+            double av[8], nv[8];
+            double2 rw[8];
 #pragma unroll
-      for (int i = 0; i + 1 < kMahaMaxP; ++i) {
-        if (i + 1 < p) {
-          if ((swm >> i) & 1ull) {
-            const double t0 = y[i];
-            y[i] = y[i + 1];
-            y[i + 1] = t0;
+            for (int u = 0; u < 8; ++u) {
+              av[u] = arow[cb + u];
+              rw[u] = es.rv[cb + u];
+              nv[u] = es.rn[cb + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {  // past p: 0 - 0 written back to the row's own padding
+              const double a = fma(-wg, rw[u].x, fma(-vg, rw[u].y, av[u]));
+              arow[cb + u] = a;
+              s[u & 3] = fma(a, nv[u], s[u & 3]);
+            }
+            if (cb == c0) col = fma(-wg, rw[0].x, fma(-vg, rw[0].y, av[0]));
           }
-          y[i + 1] -= lm[i] * y[i];
+          pv = (s[0] + s[1]) + (s[2] + s[3]);
         }
+        K = wave_sum(vn * pv);
+        vg = vn;
+        wg = 2.0 * pv - 2.0 * K * vn;
+        wave_lds_sync();
+        if (inp) es.rv[lane] = make_double2(vg, wg);
+        wave_lds_sync();
+      } else if (lane == p - 1) {  // j = p - 3: the trailing 2 x 2 block
+        eo[p - 2] = x;
+        dg[p - 1] = arow[p - 1] - 2.0 * vg * wg;
       }
-      double nrm = 0.0;
+    }
+  }
+  wave_lds_sync();
+  // ---- 2. k largest eigenvalues: Gershgorin bracket, multisection in k lane groups
+  const double di = inp ? dg[lane] : 0.0;
+  const double ei = lane + 1 < p ? fabs(eo[lane]) : 0.0, em = lane >= 1 && inp ? fabs(eo[lane - 1]) : 0.0;
+  const double lo0 = wave_min(inp ? di - ei - em : 1e300), hi0 = wave_max(inp ? di + ei + em : -1e300);
+  const double tnorm = fmax(fabs(lo0), fabs(hi0));
+  const double pivmin = fmax(tnorm * 2.3e-16, 1e-280);  // the floor keeps 1 / pivmin finite (all-zero C)
+  // scale T by 2^-E (exact) so |d - x| and e^2 are O(1) in the minors' recurrence
+  const int E = tnorm > 0.0 ? __builtin_amdgcn_frexp_exp(tnorm) : 0;
+  if (inp) {
+    es.sd[lane] = ldexp(di, -E);
+    if (lane + 1 < p) {
+      const double es_ = ldexp(eo[lane], -E);
+      es.se2[lane] = es_ * es_;
+    }
+  }
+  wave_lds_sync();
+  mark(0);
+  {
+    const int s = 64 / k;  // points per group
+    const int grp = min(lane / s, k - 1), gi = lane - grp * s;
+    const bool gact = lane < k * s;
+    const int idx = p - 1 - grp;  // ascending index of the grp-th largest eigenvalue
+    const double inv_s1 = 1.0 / double(s + 1);
+    const unsigned long long gmask = s == 64 ? ~0ull : ((1ull << s) - 1ull);
+    double l = lo0 - 1e-10 * tnorm - 1e-300, u = hi0 + 1e-10 * tnorm + 1e-300;
+    for (int it = 0; it < 128; ++it) {
+      const bool done = u - l <= 2.3e-16 * fmax(fabs(l), fabs(u)) + 1e-18 * tnorm + 1e-300;
+      if (__ballot(gact && !done) == 0) break;
+      const double x = l + (u - l) * (double(gi + 1) * inv_s1);
+      const double xs = ldexp(x, -E);
+      // eigenvalues < x = sign changes of P_0 = 1, P_1, ..., P_p (a zero counts as +)
+      // (sign changes from the sign bits of consecutive minors; padding
+      // steps past p keep the sign)
+      double pm = 1.0, pc = es.sd[0] - xs;
+      unsigned cnt = unsigned(__double2hiint(pc)) >> 31;
+      for (int ib = 1; ib < p; ib += 8) {
+        double dd[8], ee[8];
 #pragma unroll
-      for (int i = kMahaMaxP - 1; i >= 0; --i) {
-        if (i < p) {
-          double t0 = y[i];
-          if (i + 1 < p) t0 -= u1[i] * y[i + 1];
-          if (i + 2 < p) t0 -= u2[i] * y[i + 2];
-          t0 *= u0[i];
-          y[i] = t0;
-          nrm = fmax(nrm, fabs(t0));
+        for (int q = 0; q < 8; ++q) {
+          dd[q] = es.sd[ib + q] - xs;
+          ee[q] = es.se2[ib + q - 1];
         }
-      }
-      const double sc = nrm > 0.0 ? 1.0 / nrm : 1.0;
 #pragma unroll
-      for (int i = 0; i < kMahaMaxP; ++i) y[i] *= sc;
-    }
-#pragma unroll
-    for (int i = 0; i < kMahaMaxP; ++i)
-      if (i < p) V[i * kLd + a] = y[i];
-  }
-  __syncthreads();
-  if (wave == 0) {  // normalise; re-orthogonalise within clusters (|lam_a - lam_b| < 1e-3 ||T||, as dstein)
-    for (int a = 0; a < k; ++a) {
-      double y = lane < p ? V[lane * kLd + a] : 0.0;
-      for (int b = 0; b < a; ++b) {
-        if (fabs(lam[a] - lam[b]) < 1e-3 * tnorm) {
-          const double yb = lane < p ? V[lane * kLd + b] : 0.0;
-          y -= wave_sum(y * yb) * yb;
+        for (int q = 0; q < 8; ++q) {
+          const double pn = fma(-ee[q], pm, dd[q] * pc);
+          cnt += unsigned(__double2hiint(pn) ^ __double2hiint(pc)) >> 31;
+          pm = pc;
+          pc = pn;
         }
+        const int ex = __builtin_amdgcn_frexp_exp(pc);  // renormalise (pc == 0: exponent 0)
+        pc = ldexp(pc, -ex);
+        pm = ldexp(pm, -ex);
       }
-      y *= 1.0 / sqrt(fmax(wave_sum(y * y), 1e-300));
-      if (lane < p) V[lane * kLd + a] = y;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const unsigned long long bal = __ballot(gact && int(cnt) > idx);
+      const unsigned long long gm = (bal >> (grp * s)) & gmask;
+      const int f = gm ? __ffsll(static_cast<long long>(gm)) - 1 : s;  // eigenvalue in (x_{f-1}, x_f]
+      if (!done) {
+        const double nl = f > 0 ? l + (u - l) * (double(f) * inv_s1) : l;
+        const double nu = f < s ? l + (u - l) * (double(f + 1) * inv_s1) : u;
+        l = nl;
+        u = nu;
+      }
     }
-    if (lane < k) sel[lane] = lane;
+    if (gact && gi == 0) es.lam[grp] = 0.5 * (l + u);
   }
-  __syncthreads();
-  // ---- 4. back-transformation x = H_0 ... H_{p-3} y, one wave per vector
-  for (int a = wave; a < k; a += NW) {
-    double x = lane < p ? V[lane * kLd + a] : 0.0;
-    for (int j = p - 3; j >= 0; --j) {
-      const double vt = lane > j && lane < p ? W[j * kLd + (lane - j - 1)] : 0.0;
-      x -= 2.0 * wave_sum(vt * x) * vt;
+  wave_lds_sync();
+  mark(1);
+  // ---- 3. eigenvectors of T by twisted factorisation (the MRRR kernel,
+  // LAPACK dlar1v), lane a for eigenvalue a: T - lam I = L+ D+ L+^T
+  // (top-down) = U- D- U-^T (bottom-up), both stationary qd recurrences run
+  // interleaved; twist index r = argmin |gamma_r|, gamma_r = d+_r + d-_r -
+  // (t_rr - lam); z_r = 1 and z follows by one product recurrence each way.
+  // No iteration, no pivoting; scratch in A (free now) as [row][kMahaMaxK].
+  if (lane < k) {
+    const int a = lane;
+    double* LP = A;                             // l+_i = e_i / d+_i
+    double* UM = LP + kMahaMaxP * kMahaMaxK;    // u-_i = e_i / d-_{i+1}
+    double* DP = UM + kMahaMaxP * kMahaMaxK;    // d+_i
+    double* DM = DP + kMahaMaxP * kMahaMaxK;    // d-_i
+    const double L = es.lam[a];
+    double dp = dg[0] - L, dm = dg[p - 1] - L;
+    DP[a] = dp;
+    DM[(p - 1) * kMahaMaxK + a] = dm;
+#pragma unroll 4
+    for (int t = 0; t + 1 < p; ++t) {
+      const int i = t, ib = p - 2 - t;
+      const double bf = eo[i], bb = eo[ib];
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      if (fabs(dm) < pivmin) dm = -pivmin;
+      const double lp = bf * rcp_nr(dp), um = bb * rcp_nr(dm);
+      LP[i * kMahaMaxK + a] = lp;
+      UM[ib * kMahaMaxK + a] = um;
+      dp = (dg[i + 1] - L) - lp * bf;
+      dm = (dg[ib] - L) - um * bb;
+      DP[(i + 1) * kMahaMaxK + a] = dp;
+      DM[ib * kMahaMaxK + a] = dm;
     }
-    if (lane < p) V[lane * kLd + a] = x;
+    int r = 0;
+    double gbest = 1e308;
+#pragma unroll 4
+    for (int i = 0; i < p; ++i) {
+      const double g = fabs(DP[i * kMahaMaxK + a] + DM[i * kMahaMaxK + a] - (dg[i] - L));
+      if (g < gbest) {
+        gbest = g;
+        r = i;
+      }
+    }
+    double z = 1.0;
+    V[r * kLd + a] = 1.0;
+    for (int i = r - 1; i >= 0; --i) {
+      z = -LP[i * kMahaMaxK + a] * z;
+      V[i * kLd + a] = z;
+    }
+    z = 1.0;
+    for (int i = r; i + 1 < p; ++i) {
+      z = -UM[i * kMahaMaxK + a] * z;
+      V[(i + 1) * kLd + a] = z;
+    }
   }
-  __syncthreads();
+  wave_lds_sync();
+  // normalise; re-orthogonalise within clusters (|lam_a - lam_b| < 1e-3 ||T||, as dstein)
+  for (int a = 0; a < k; ++a) {
+    double y = inp ? V[lane * kLd + a] : 0.0;
+    for (int b = 0; b < a; ++b) {
+      if (fabs(es.lam[a] - es.lam[b]) < 1e-3 * tnorm) {
+        const double yb = inp ? V[lane * kLd + b] : 0.0;
+        y -= wave_sum(y * yb) * yb;
+      }
+    }
+    y *= rsq_nr(fmax(wave_sum(y * y), 1e-300));
+    if (inp) V[lane * kLd + a] = y;
+    wave_lds_sync();
+  }
+  if (lane < k) sel[lane] = lane;
+  mark(-5);  // -> ph[2]
+  // ---- 4. back-transformation x = H_0 ... H_{p-3} y, all k vectors per
+  // reflector (their k wave sums overlap); vectors a0.. in groups of 4
+  for (int a0 = 0; a0 < k; a0 += 4) {
+    switch (min(k - a0, 4)) {
+      case 1: back_transform<1>(V, Wr, p, a0); break;
+      case 2: back_transform<2>(V, Wr, p, a0); break;
+      case 3: back_transform<3>(V, Wr, p, a0); break;
+      default: back_transform<4>(V, Wr, p, a0); break;
+    }
+  }
+  wave_lds_sync();
   mark(2);
 }
 
@@ -496,17 +596,15 @@ __device__ void topk_tridiag(double* A, double* V, const double* W_, double* dg,
 template <int NT>
 __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams& prm, double* __restrict__ state,
                          double* __restrict__ eig, double* __restrict__ ws, double* __restrict__ scores) {
-  __shared__ double A[kMahaMaxP * kLd], V[kMahaMaxP * kLd], W[kMahaMaxP * kLd], Tm[kMahaMaxP * kLd];
+  __shared__ double A[kMahaMaxP * kLdA], V[kMahaMaxP * kLd], W[kMahaMaxP * kLd], Tm[kMahaMaxP * kLd];
   __shared__ double mean0[kMahaMaxP];
-  __shared__ double rc[kMahaMaxP / 2], rs[kMahaMaxP / 2];
-  __shared__ int rp[kMahaMaxP / 2], rq[kMahaMaxP / 2];
+  __shared__ EigScratch es;
   __shared__ double red[NT / 64];
   __shared__ int sel[kMahaMaxK];
   __shared__ double P[kMahaMaxK * kMahaMaxK], Cp[kMahaMaxK * kMahaMaxK], T1[kMahaMaxK * kMahaMaxK],
       T2[kMahaMaxK * kMahaMaxK];
   __shared__ int valid, inverted;
   __shared__ double scal;
-  __shared__ double tdg[kMahaMaxP], teo[kMahaMaxP], te2[kMahaMaxP], twv[kMahaMaxP], tlam[kMahaMaxK];
   const int tid = threadIdx.x;
   const int p = prm.p, k = prm.k, kk = k * k;
   double* s_mean = state;
@@ -572,136 +670,21 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
         acc += ((n + i) / (n + i + 1.0)) * (D[size_t(i) * p + a] * D[size_t(i) * p + b]);
       cov = (n - 1.0) / den * (c_zero ? 0.0 : s_C[a * p + b]) + 1.0 / den * acc;
     }
-    A[a * kLd + b] = cov;
+    A[a * kLdA + b] = cov;
     Tm[a * kLd + b] = cov;  // kept: written to the state after the projections
-  }
-  if constexpr (NT == 256) {  // p > 16: top-k via tridiagonalisation (topk_tridiag)
-    __syncthreads();
-    stamp(1);
-    stamp(2);
-    topk_tridiag<NT>(A, V, W, tdg, teo, te2, twv, tlam, sel, p, k, ph + 7);
-    stamp(3);
-    if (tid == 0) eig[kMahaMaxP * kMahaMaxP + 3] += 1.0;
-  } else {
-  // ---- eigenvectors: warm-started parallel cyclic Jacobi (m = p rounded up to even)
-  const bool warm = eig[kMahaMaxP * kMahaMaxP] != 0.0 && int(eig[kMahaMaxP * kMahaMaxP + 1]) == m;
-  for (int e = tid; e < m * m; e += NT) {
-    const int a = e / m, b = e - a * m;
-    V[a * kLd + b] = warm ? eig[e] : (a == b ? 1.0 : 0.0);
   }
   __syncthreads();
   stamp(1);
-  if (warm) {
-    // Newton-Schulz re-orthonormalisation every 16 steps: the rotations lose
-    // ~1e-16 of orthogonality per sweep, the step squares the error away
-    if ((int(eig[kMahaMaxP * kMahaMaxP + 3]) & 15) == 0) {
-      mm<NT, true>(V, V, W, m);  // G = V^T V
-      __syncthreads();
-      mm<NT, false>(V, W, A, m);  // V G (A is rebuilt below from Tm)
-      __syncthreads();
-      for (int e = tid; e < m * m; e += NT) {
-        const int a = e / m, b = e - a * m;
-        V[a * kLd + b] = 1.5 * V[a * kLd + b] - 0.5 * A[a * kLd + b];
-      }
-      __syncthreads();
-    }
-    mm<NT, false>(Tm, V, W, m);  // C V
-    __syncthreads();
-    mm<NT, true>(V, W, A, m);    // V^T C V
-    __syncthreads();
-  }
-  stamp(2);
-  const int half = m / 2;
-  // striping: thread -> (pair my_i, first column pair / row my_j0, stride jstep)
-  const int jstep = NT / max(half, 1);
-  const int my_i = tid % max(half, 1), my_j0 = tid / max(half, 1);
-  int sweeps = 0;
-  for (int sweep = 0; sweep < kMaxSweeps && m > 1; ++sweep, ++sweeps) {
-    double off = 0.0, all = 0.0;
-    for (int e = tid; e < m * m; e += NT) {
-      const int a = e / m, b = e - a * m;
-      const double v = A[a * kLd + b];
-      all += v * v;
-      if (a != b) off += v * v;
-    }
-    off = block_sum<NT>(off, red);
-    all = block_sum<NT>(all, red);
-    if (off <= 1e-30 * all || off == 0.0) break;
-    // round-robin pairs: lane i < half keeps its two positions mod (m - 1)
-    // (no integer division in the round loop); block / V work is striped so
-    // a thread's pair rows are fixed for the whole sweep
-    int ua = tid == 0 ? -1 : tid % (m - 1), ub = tid == 0 ? 0 : (m - 1 - tid) % (m - 1);
-    for (int r = 0; r < m - 1; ++r) {
-      if (tid < half) {
-        const int a = tid == 0 ? 0 : 1 + ua, b = 1 + ub;
-        const int pp = min(a, b), qq = max(a, b);
-        const double app = A[pp * kLd + pp], aqq = A[qq * kLd + qq], apq = A[pp * kLd + qq];
-        double c = 1.0, sn = 0.0;
-        if (apq != 0.0 && fabs(apq) > 1e-18 * (fabs(app) + fabs(aqq))) {
-          const double th = (aqq - app) / (2.0 * apq);
-          const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
-          c = 1.0 / sqrt(t * t + 1.0);
-          sn = t * c;
-        }
-        rc[tid] = c;
-        rs[tid] = sn;
-        rp[tid] = pp;
-        rq[tid] = qq;
-        if (tid != 0 && ++ua == m - 1) ua = 0;
-        if (++ub == m - 1) ub = 0;
-      }
-      __syncthreads();
-      // A <- J^T A J as 2 x 2 blocks (pair rows bi x pair columns bj); V <- V J
-      if (my_i < half) {
-        const int pi = rp[my_i], qi = rq[my_i];
-        const double ci = rc[my_i], si = rs[my_i];
-        for (int bj = my_j0; bj < half; bj += jstep) {
-          const int pj = rp[bj], qj = rq[bj];
-          const double cj = rc[bj], sj = rs[bj];
-          const double x00 = A[pi * kLd + pj], x01 = A[pi * kLd + qj], x10 = A[qi * kLd + pj], x11 = A[qi * kLd + qj];
-          const double y00 = cj * x00 - sj * x01, y01 = sj * x00 + cj * x01;
-          const double y10 = cj * x10 - sj * x11, y11 = sj * x10 + cj * x11;
-          A[pi * kLd + pj] = ci * y00 - si * y10;
-          A[pi * kLd + qj] = ci * y01 - si * y11;
-          A[qi * kLd + pj] = si * y00 + ci * y10;
-          A[qi * kLd + qj] = si * y01 + ci * y11;
-        }
-        for (int row = my_j0; row < m; row += jstep) {
-          const double vp = V[row * kLd + pi], vq = V[row * kLd + qi];
-          V[row * kLd + pi] = ci * vp - si * vq;
-          V[row * kLd + qi] = si * vp + ci * vq;
-        }
-      }
-      __syncthreads();
-    }
-  }
+  const uint64_t c_eig0 = __builtin_amdgcn_s_memtime(), r_eig0 = __builtin_amdgcn_s_memrealtime();
+  if (tid < 64) topk_wave(A, V, W, es, sel, p, k, ph + 7);
+  __syncthreads();
   stamp(3);
-  // the eigenvectors seed the next step
-  for (int e = tid; e < m * m; e += NT) {
-    const int a = e / m, b = e - a * m;
-    eig[e] = V[a * kLd + b];
-  }
-  if (tid == 0) {
+  if (tid == 0) {  // shader-clock cycles and 100 MHz ticks of the eigen phase (effective clock)
     double* tail = eig + kMahaMaxP * kMahaMaxP;
-    tail[0] = 1.0;
-    tail[1] = double(m);
-    tail[2] = double(sweeps);
+    tail[2] += double(__builtin_amdgcn_s_memtime() - c_eig0);
+    tail[4] += double(__builtin_amdgcn_s_memrealtime() - r_eig0);
     tail[3] += 1.0;
-    tail[4] += double(sweeps);
   }
-  // ---- top-k eigenpairs (any order: the scores are invariant to it)
-  if (tid == 0) {
-    for (int a = 0; a < k; ++a) {
-      int best = -1;
-      for (int j = 0; j < p; ++j) {
-        bool taken = false;
-        for (int b = 0; b < a; ++b) taken |= sel[b] == j;
-        if (!taken && (best < 0 || A[j * kLd + j] > A[best * kLd + best])) best = j;
-      }
-      sel[a] = best;
-    }
-  }
-  }  // Jacobi (p <= 16)
   // ---- projections; proj_cov = V^T C_old V over the selected columns:
   // C_old (still in HBM) -> W, U = C_old V_sel -> A (free after the
   // selection), P = V_sel^T U
@@ -712,7 +695,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     const double* vb = V + sel[b];
     double t = 0.0;
     for (int c = 0; c < p; ++c) t += W[r * kLd + c] * vb[c * kLd];
-    A[r * kLd + b] = t;
+    A[r * kLdA + b] = t;
   }
   // row projections: one wave per (row, component), lanes over the features
   // (coalesced, independent loads; a 6-step shuffle sum instead of a
@@ -745,7 +728,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     const int a = e / k, b = e - a * k;
     const double* va = V + sel[a];
     double acc = 0.0;
-    for (int r = 0; r < p; ++r) acc += va[r * kLd] * A[r * kLd + b];
+    for (int r = 0; r < p; ++r) acc += va[r * kLd] * A[r * kLdA + b];
     P[e] = acc;
   }
   if (tid == 0) valid = 0;

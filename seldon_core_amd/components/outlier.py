@@ -6,9 +6,9 @@ scoring on the MI355X:
   covariance, top-k PCA via ``eigh``, Sherman-Morrison inverse updates,
   Mahalanobis score).  On a GPU the state (mean, covariance, clip bounds, n)
   stays in HBM and each request is one single-workgroup kernel launch that
-  runs the whole step -- clip, running moments, top-k eigenvectors by
-  parallel cyclic Jacobi in LDS, projections, Sherman-Morrison recurrence,
-  state update (``MahalanobisDevice``, csrc/kernels/mahalanobis.hip); on the
+  runs the whole step -- clip, running moments, top-k eigenpairs by one
+  wave in LDS (tridiagonalisation, Sturm multisection, twisted-factorisation
+  eigenvectors), projections, Sherman-Morrison recurrence, state update (``MahalanobisDevice``, csrc/kernels/mahalanobis.hip); on the
   CPU it is fp64 numpy (the parity oracle).
 * ``OutlierIsolationForest`` -- isolation-forest/CoreIsolationForest.py:62-76:
   ``decision_function < threshold``; the forest runs on the tree-ensemble HIP

@@ -78,7 +78,7 @@ def main() -> int:
         wall = time.perf_counter() - t0
         b1 = dev.batches()
         flat = [x for v in lat_c for x in v]
-        jac = dev.jacobi_stats()
+        jac = dev.solver_stats()
         res[p] = {
             "numpy_seq_us": {"p50": pct(lat_np, 50), "p99": pct(lat_np, 99), "req_per_s": len(reqs) / sum(lat_np)},
             "device_seq_us": {"p50": pct(lat_dev, 50), "p99": pct(lat_dev, 99), "req_per_s": len(reqs) / sum(lat_dev)},
@@ -86,8 +86,8 @@ def main() -> int:
                                   "req_per_s": len(reqs) / wall,
                                   "requests_per_launch": (b1["requests"] - b0["requests"]) /
                                   max(1, b1["batches"] - b0["batches"])},
-            "jacobi_mean_sweeps": jac.get("mean_sweeps"),
             "kernel_phase_us": jac.get("phase_us_per_step"),
+            "eigen_clock_mhz": jac.get("eigen_clock_mhz"),
         }
         print(json.dumps({"p": p, **res[p]}), flush=True)
     if a.out:
