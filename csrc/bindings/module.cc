@@ -356,7 +356,7 @@ PYBIND11_MODULE(_C, m) {
           r["steps"] = t[1];
           // s_memtime cycles / s_memrealtime (100 MHz) ticks over the eigen phase
           r["eigen_clock_mhz"] = t[2] > 0 ? t[0] / (t[2] * 0.01) : 0.0;
-          static const char* names[10] = {"clip", "cov", "eigen.inverse_iteration", "eigen", "proj", "sm", "update",
+          static const char* names[10] = {"clip", "cov", "eigen.vectors", "eigen", "proj", "sm", "update",
                                           "eigen.tridiag", "eigen.eigenvalues", "eigen.back_transform"};
           py::dict ph;
           for (int i = 0; i < 10; ++i) ph[names[i]] = t[1] > 0 ? t[3 + i] / t[1] : 0.0;

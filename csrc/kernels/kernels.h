@@ -241,10 +241,10 @@ inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (4 * s
 // eig: kMahaEigDoubles doubles, zero-initialised device diagnostics (not
 // part of the state; the first kMahaMaxP^2 are reserved).
 // Tail: [0, 0, eigen-phase shader cycles, steps, eigen-phase 100 MHz ticks,
-// phase us x 10]: clip, cov, (unused), eigen,
-// projections, Sherman-Morrison, state update, and the eigen sub-phases
-// tridiagonalise, eigenvalues (multisection), eigenvectors (inverse
-// iteration + back-transformation).
+// phase us x 10]: clip, cov, eigen.eigenvectors (twisted factorisation),
+// eigen (total), projections, Sherman-Morrison, state update,
+// eigen.tridiagonalise, eigen.eigenvalues (multisection),
+// eigen.back-transformation.
 constexpr int kMahaEigDoubles = kMahaMaxP * kMahaMaxP + 15;
 void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* eig, double* ws, double* scores,
                hipStream_t stream);

@@ -319,14 +319,14 @@ struct EigScratch {
 // Wr: reflectors (row j = reflector j, indexed by global row).  Output:
 // eigenvectors in V[:, 0..k-1], sel[a] = a.
 __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ Wr, EigScratch& es,
-                          int* sel, int p, int k, uint64_t* sub) {
+                          int* sel, int p, int k, uint64_t* ph) {
   const int lane = threadIdx.x & 63;
   const bool inp = lane < p;
   uint64_t t_prev = __builtin_amdgcn_s_memrealtime();
-  auto mark = [&](int i) {  // sub-phase timer (lane 0)
+  auto mark = [&](int i) {  // sub-phase timer (lane 0): ph[i] of the caller's phase array
     if (lane == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
-      sub[i] += t - t_prev;
+      ph[i] += t - t_prev;
       t_prev = t;
     }
   };
@@ -456,7 +456,7 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
     }
   }
   wave_lds_sync();
-  mark(0);
+  mark(7);  // tridiagonalisation
   {
     const int s = 64 / k;  // points per group
     const int grp = min(lane / s, k - 1), gi = lane - grp * s;
@@ -506,7 +506,7 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
     if (gact && gi == 0) es.lam[grp] = 0.5 * (l + u);
   }
   wave_lds_sync();
-  mark(1);
+  mark(8);  // eigenvalues
   // ---- 3. eigenvectors of T by twisted factorisation (the MRRR kernel,
   // LAPACK dlar1v), lane a for eigenvalue a: T - lam I = L+ D+ L+^T
   // (top-down) = U- D- U-^T (bottom-up), both stationary qd recurrences run
@@ -574,7 +574,7 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
     wave_lds_sync();
   }
   if (lane < k) sel[lane] = lane;
-  mark(-5);  // -> ph[2]
+  mark(2);  // eigenvectors (twisted factorisation, normalisation)
   // ---- 4. back-transformation x = H_0 ... H_{p-3} y, all k vectors per
   // reflector (their k wave sums overlap); vectors a0.. in groups of 4
   for (int a0 = 0; a0 < k; a0 += 4) {
@@ -586,7 +586,7 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
     }
   }
   wave_lds_sync();
-  mark(2);
+  mark(9);  // back-transformation
 }
 
 // One request's step (CoreMahalanobis._get_preds for X [nb][p]) against the
@@ -676,7 +676,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   __syncthreads();
   stamp(1);
   const uint64_t c_eig0 = __builtin_amdgcn_s_memtime(), r_eig0 = __builtin_amdgcn_s_memrealtime();
-  if (tid < 64) topk_wave(A, V, W, es, sel, p, k, ph + 7);
+  if (tid < 64) topk_wave(A, V, W, es, sel, p, k, ph);
   __syncthreads();
   stamp(3);
   if (tid == 0) {  // shader-clock cycles and 100 MHz ticks of the eigen phase (effective clock)
