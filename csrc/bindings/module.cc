@@ -110,6 +110,14 @@ PYBIND11_MODULE(_C, m) {
     message_to_json(msg, out);
     return out;
   });
+  m.def("json_fast_roundtrip", [](const std::string& text) -> py::object {
+    SeldonMessage msg;
+    if (!fast_dense_message(text, msg)) return py::none();
+    std::string js, pb;
+    message_to_json(msg, js);
+    message_to_pb(msg, pb);
+    return py::make_tuple(js, py::bytes(pb));
+  }, "The REST fast path (dense ndarray requests): (json, protobuf) re-encodings, or None when it declines.");
   m.def("json_to_pb", [](const std::string& text) {
     SeldonMessage msg;
     message_from_json(parse_json(text), msg);

@@ -150,23 +150,18 @@ MsgPtr merge_meta(MsgPtr latest, const std::vector<const SeldonMessage*>& prev, 
 
 std::string Engine::new_puid() {
   thread_local Xoshiro rng;
-  uint64_t hi = rng.next() & 3, mid = rng.next(), lo = rng.next();  // 130 bits
+  // 130 random bits in base 32, no leading zeros (the reference's
+  // BigInteger(130, random).toString(32)): 5-bit groups straight from a
+  // 128-bit word plus the top 2 bits
+  const uint64_t hi = rng.next() & 3;
+  const unsigned __int128 x = (static_cast<unsigned __int128>(rng.next()) << 64) | rng.next();
   static const char* digits = "0123456789abcdefghijklmnopqrstuv";
-  char buf[27];
-  int n = 0;
-  for (int g = 25; g >= 0; --g) {
-    int bit = g * 5;  // 5-bit group starting at bit `bit` of the 130-bit integer
-    uint32_t v = 0;
-    for (int b = 4; b >= 0; --b) {
-      int pos = bit + b;
-      uint64_t w = pos >= 128 ? hi : pos >= 64 ? mid : lo;
-      v = (v << 1) | uint32_t((w >> (pos & 63)) & 1);
-    }
-    if (n == 0 && v == 0) continue;
-    buf[n++] = digits[v];
-  }
-  if (n == 0) buf[n++] = '0';
-  return std::string(buf, size_t(n));
+  char buf[26];
+  buf[0] = digits[uint32_t((x >> 125) | (hi << 3)) & 31];  // bits 125..129
+  for (int g = 24; g >= 0; --g) buf[25 - g] = digits[uint32_t(x >> (5 * g)) & 31];
+  int lead = 0;
+  while (lead < 25 && buf[lead] == '0') ++lead;
+  return std::string(buf + lead, size_t(26 - lead));
 }
 
 // ------------------------------------------------------------------ engine

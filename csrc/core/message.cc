@@ -531,6 +531,112 @@ void message_from_json(const Json& j, SeldonMessage& m) {
   if (set > 1) bad("Message type \"seldon.protos.SeldonMessage\" has more than one field set in oneof \"data_oneof\"");
 }
 
+bool fast_dense_message(std::string_view text, SeldonMessage& m) {
+  const char* p = text.data();
+  const char* const e = p + text.size();
+  auto ws = [&] {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  };
+  auto lit = [&](char c) {
+    ws();
+    if (p < e && *p == c) { ++p; return true; }
+    return false;
+  };
+  auto str = [&](std::string_view& out) {  // plain string: no escapes / control characters
+    ws();
+    if (p >= e || *p != '"') return false;
+    const char* b = ++p;
+    while (p < e && *p != '"') {
+      if (*p == '\\' || static_cast<unsigned char>(*p) < 0x20) return false;
+      ++p;
+    }
+    if (p >= e) return false;
+    out = std::string_view(b, size_t(p - b));
+    ++p;
+    return true;
+  };
+  auto number = [&](double& d) {  // the general parser's token rule, then the same conversion
+    ws();
+    const char* b = p;
+    if (p < e && *p == '-') ++p;
+    while (p < e && ((*p >= '0' && *p <= '9') || *p == '.' || *p == 'e' || *p == 'E' || *p == '+' || *p == '-')) ++p;
+    return p != b && parse_double(b, p, d);
+  };
+  std::vector<std::string> names;
+  std::vector<double> vals;
+  int64_t rows = 0, cols = -1;
+  bool have_data = false, have_meta = false, have_names = false, have_nd = false;
+  if (!lit('{')) return false;
+  for (;;) {
+    std::string_view k;
+    if (!str(k) || !lit(':')) return false;
+    if (k == "data" && !have_data) {
+      have_data = true;
+      if (!lit('{')) return false;
+      for (;;) {
+        std::string_view dk;
+        if (!str(dk) || !lit(':')) return false;
+        if (dk == "names" && !have_names) {
+          have_names = true;
+          if (!lit('[')) return false;
+          if (!lit(']')) {
+            for (;;) {
+              std::string_view nm;
+              if (!str(nm)) return false;
+              names.emplace_back(nm);
+              if (lit(',')) continue;
+              if (lit(']')) break;
+              return false;
+            }
+          }
+        } else if (dk == "ndarray" && !have_nd) {
+          have_nd = true;
+          if (!lit('[')) return false;
+          for (;;) {
+            if (!lit('[')) return false;
+            int64_t c = 0;
+            for (;;) {
+              double d;
+              if (!number(d)) return false;
+              vals.push_back(d);
+              ++c;
+              if (lit(',')) continue;
+              if (lit(']')) break;
+              return false;
+            }
+            if (cols < 0) cols = c;
+            else if (c != cols) return false;
+            ++rows;
+            if (lit(',')) continue;
+            if (lit(']')) break;
+            return false;
+          }
+        } else {
+          return false;
+        }
+        if (lit(',')) continue;
+        if (lit('}')) break;
+        return false;
+      }
+    } else if (k == "meta" && !have_meta) {
+      have_meta = true;
+      if (!lit('{') || !lit('}')) return false;
+    } else {
+      return false;
+    }
+    if (lit(',')) continue;
+    if (lit('}')) break;
+    return false;
+  }
+  ws();
+  if (p != e || !have_nd) return false;
+  m.payload = Payload::Data;
+  if (have_meta) m.has_meta = true;
+  m.data.names = std::move(names);
+  m.data.set_dense(DataKind::NdArray, {rows, cols}, std::move(vals));
+  return true;
+}
+
 void feedback_from_json(const Json& j, Feedback& f) {
   check_known(j, {"request", "response", "reward", "truth"}, "seldon.protos.Feedback");
   if (auto* x = field(j, "request")) { f.has_request = true; message_from_json(*x, f.request); }

@@ -133,6 +133,13 @@ struct Feedback {
 
 // ------------------------------------------------------------------ JSON codec
 void message_from_json(const Json& j, SeldonMessage& m);
+// Fast path for the dominant REST request shape, {"data": {["names": [..],]
+// "ndarray": [[numbers], ...]}[, "meta": {}]} in any key order: parses
+// straight into a dense ndarray (no JSON tree) with the same numbers and the
+// same message as message_from_json(parse_json(text)).  Returns false, m
+// untouched, for anything else (other fields, escapes, non-numbers, ragged
+// or 1-D arrays, duplicate keys): the caller then takes the general parser.
+bool fast_dense_message(std::string_view text, SeldonMessage& m);
 void message_to_json(const SeldonMessage& m, std::string& out);
 void feedback_from_json(const Json& j, Feedback& f);
 void feedback_to_json(const Feedback& f, std::string& out);

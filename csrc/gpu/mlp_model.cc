@@ -363,7 +363,8 @@ void MlpModel::launch_layerwise(const double* X, int rows, double* out, float* w
   // the LDS-tiled GEMM reads X (fp64) straight into its first layer's staging
   // (no convert pass; the VAE keeps x32 as its MSE reference) and writes the
   // model output from its last layer's epilogue (no mlp_finish).
-  const bool direct_in = !vae_ && lds_layer(0, rows);
+  static const bool stage64 = [] { const char* v = std::getenv("SCA_MLP_DIRECT_IN"); return !v || atoi(v) != 0; }();
+  const bool direct_in = stage64 && !vae_ && lds_layer(0, rows);
   if (!direct_in) kern::mlp_convert(X, rows, F_, int(K0), x32, s);
   const float* cur = x32;
   int cur_ld = int(K0), flip = 0;

@@ -1154,6 +1154,15 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
     static const int m32 = [] { const char* v = getenv("SCA_GEMM_F32_M32"); return v ? atoi(v) : 1; }();
     // (128 x 128 tiles with 2 x 2 32x32 accumulators per wave -- one workgroup
     // per CU -- measured 9-90% slower on every MLP / VAE layer, r03d)
+    // 64 x 64 tiles when 128 x 64 would leave < 2 workgroups per CU (one
+    // wave per SIMD cannot hide the LDS / MFMA latencies); SCA_GEMM_F32_T64:
+    // 0 never, 1 auto, 2 always (A/B)
+    static const int t64 = [] { const char* v = getenv("SCA_GEMM_F32_T64"); return v ? atoi(v) : 1; }();
+    const int tiles64 = nN * ((a.rows_eff + 63) / 64);
+    if (m32 && !a.out64 && ((t64 == 1 && big >= 256 && big < 512) || (t64 == 2 && tiles64 >= 256))) {
+      hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 64, 64, 256, 2, true>), dim3(tiles64), dim3(256), 0, s, a);
+      return;
+    }
     if (m32 && !a.out64 && big >= 256) {
       hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 128, 64, 256, 2, true>), dim3(big), dim3(256), 0, s, a);
       return;

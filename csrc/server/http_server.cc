@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -58,10 +59,11 @@ bool form_value(std::string_view body, std::string_view key, std::string& out) {
   return false;
 }
 
-static bool iequals(std::string_view a, std::string_view b) {
+static inline char ascii_lower(char c) { return c >= 'A' && c <= 'Z' ? char(c | 0x20) : c; }
+static bool iequals(std::string_view a, std::string_view b) {  // ASCII case folding (header names, tokens)
   if (a.size() != b.size()) return false;
   for (size_t i = 0; i < a.size(); ++i)
-    if (tolower((unsigned char)a[i]) != tolower((unsigned char)b[i])) return false;
+    if (ascii_lower(a[i]) != ascii_lower(b[i])) return false;
   return true;
 }
 
@@ -705,8 +707,12 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
     auto msg = std::make_shared<SeldonMessage>();
     Json j;
     std::string err;
-    bool ok = parse_external_body(rq, j, err);
-    if (ok) {
+    bool ok;
+    static const bool fast = [] { const char* v = getenv("SCA_REST_FAST_JSON"); return !v || atoi(v) != 0; }();
+    if (fast && !rq.body.empty() && rq.content_type.find("form") == std::string_view::npos &&
+        fast_dense_message(rq.body, *msg)) {
+      ok = true;  // dense ndarray request parsed without a JSON tree
+    } else if ((ok = parse_external_body(rq, j, err))) {
       try {
         message_from_json(j, *msg);
       } catch (const std::exception& e) {
