@@ -1154,12 +1154,14 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
     static const int m32 = [] { const char* v = getenv("SCA_GEMM_F32_M32"); return v ? atoi(v) : 1; }();
     // (128 x 128 tiles with 2 x 2 32x32 accumulators per wave -- one workgroup
     // per CU -- measured 9-90% slower on every MLP / VAE layer, r03d)
-    // 64 x 64 tiles when 128 x 64 would leave < 2 workgroups per CU (one
-    // wave per SIMD cannot hide the LDS / MFMA latencies); SCA_GEMM_F32_T64:
-    // 0 never, 1 auto, 2 always (A/B)
+    // 64 x 64 tiles (4x the workgroups of 128 x 64, several resident per CU
+    // to hide the LDS / MFMA latencies) for fp32 A panels: MLP 512->256
+    // 32.7 -> 27.1 us, VAE decoder layers 53.2 -> 34.8 and 49.2 -> 43.8 us;
+    // not for fp64 rows staged by the GEMM (AMODE 3: 88.9 vs 91.8 us) --
+    // profiles/r03h_frontend_fp32.  SCA_GEMM_F32_T64: 0 never, 1 auto, 2 always.
     static const int t64 = [] { const char* v = getenv("SCA_GEMM_F32_T64"); return v ? atoi(v) : 1; }();
     const int tiles64 = nN * ((a.rows_eff + 63) / 64);
-    if (m32 && !a.out64 && ((t64 == 1 && big >= 256 && big < 512) || (t64 == 2 && tiles64 >= 256))) {
+    if (m32 && !a.out64 && tiles64 >= 256 && ((t64 == 1 && AMODE != 3) || t64 == 2)) {
       hipLaunchKernelGGL((gemm_lds_kernel<T, AMODE, 64, 64, 256, 2, true>), dim3(tiles64), dim3(256), 0, s, a);
       return;
     }

@@ -589,6 +589,149 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
   mark(9);  // back-transformation
 }
 
+// Sherman-Morrison scores for k <= 4 on one lane (CoreMahalanobis.py:118-146,
+// the same recurrence as the LDS path below): P, C^-1 and the per-row
+// updates live in registers as padded 4 x 4 matrices (identity block past
+// k, so determinants and inverses of the k x k block are unchanged).  The
+// LDS path costs ~60 dependent LDS round trips (60-90 clocks each) per
+// inversion plus a barrier per step.
+__device__ void sm_scores_small(const double* __restrict__ Pin, const double* __restrict__ XD,
+                                const double* __restrict__ DPC, int nb, int k, double n, const MahaParams& prm,
+                                double* __restrict__ scores) {
+  double P[4][4], C[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      P[r][c] = r < k && c < k ? Pin[r * k + c] : (r == c ? 1.0 : 0.0);
+      C[r][c] = 0.0;
+    }
+  bool valid = false;
+  for (int i = 0; i < nb; ++i) {
+    double d[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[r] = r < k ? XD[size_t(i) * k + r] : 0.0;
+    if (!valid) {
+      // Gauss-Jordan, first maximal pivot per column (as invert_into)
+      double M[4][4], I[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          M[r][c] = P[r][c];
+          I[r][c] = r == c ? 1.0 : 0.0;
+        }
+      double det = 1.0;
+      bool sing = false;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        int piv = c;
+        double best = fabs(M[c][c]);
+#pragma unroll
+        for (int r = c + 1; r < 4; ++r)
+          if (fabs(M[r][c]) > best) {
+            best = fabs(M[r][c]);
+            piv = r;
+          }
+        sing |= best == 0.0;
+#pragma unroll
+        for (int r = c + 1; r < 4; ++r)
+          if (piv == r) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              double t = M[c][j];
+              M[c][j] = M[r][j];
+              M[r][j] = t;
+              t = I[c][j];
+              I[c][j] = I[r][j];
+              I[r][j] = t;
+            }
+            det = -det;
+          }
+        const double dd = M[c][c];
+        det *= dd;
+        const double id = sing ? 0.0 : 1.0 / dd;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          M[c][j] *= id;
+          I[c][j] *= id;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (r == c) continue;
+          const double f = M[r][c];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            M[r][j] -= f * M[c][j];
+            I[r][j] -= f * I[c][j];
+          }
+        }
+      }
+      if (!sing && fabs(det) > prm.eps) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) C[r][c] = I[r][c];
+        valid = true;
+      } else {
+        if (n + i != 0.0) {
+          const double a = (n + i - 1.0) / (n + i), cb = 1.0 / (n + i + 1.0);
+          double dp[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dp[r] = r < k ? DPC[size_t(i) * k + r] : 0.0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (r < k && c < k) P[r][c] = a * P[r][c] + cb * dp[r] * dp[c];
+        }
+        scores[i] = prm.out_mode == 1 ? (0.0 > prm.threshold ? 1.0 : 0.0) : 0.0;
+        continue;
+      }
+    } else {
+      const double a = (n + i - 1.0) / (n + i - 2.0), cb = 1.0 / (n + i);  // B_{i-1} = dpc dpc^T / (n + i)
+      double dp[4], T2[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dp[r] = r < k ? DPC[size_t(i - 1) * k + r] : 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) C[r][c] *= a;  // c_inv = a C (in place)
+      double tr = 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s += (cb * dp[r] * dp[j]) * C[j][c];
+          T2[r][c] = s;
+          if (r == c) tr += s;
+        }
+      const double scal = 1.0 / (1.0 + tr);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // row r of c_inv - scal c_inv BC1 needs only row r of c_inv
+        double row[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s += C[r][j] * T2[j][c];
+          row[c] = C[r][c] - scal * s;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) C[r][c] = row[c];
+      }
+    }
+    double part = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) part += d[r] * C[r][c] * d[c];
+    scores[i] = prm.out_mode == 1 ? (part > prm.threshold ? 1.0 : 0.0) : part;
+  }
+}
+
 // One request's step (CoreMahalanobis._get_preds for X [nb][p]) against the
 // state in HBM; called once per segment by maha_step_kernel.  Callers
 // __syncthreads() between calls: the next segment reads the state this one
@@ -737,7 +880,11 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   // new covariance into the state (the projections above read the old one)
   for (int e = tid; e < p * p; e += NT) s_C[e] = Tm[(e / p) * kLd + e % p];
   // ---- Sherman-Morrison scores (sequential in rows)
-  for (int i = 0; i < nb; ++i) {
+  if (k <= 4) {
+    if (tid == 0) sm_scores_small(P, XD, DPC, nb, k, n, prm, scores);
+    __syncthreads();
+  }
+  for (int i = 0; i < (k <= 4 ? 0 : nb); ++i) {
     const double* d = XD + size_t(i) * k;
     if (!valid) {
       if (tid == 0) {  // Gauss-Jordan in LDS (T1 = working copy of P, T2 = inverse)
