@@ -456,8 +456,13 @@ void BatchedUnit::handoff_loop() {
       batch.clear();
       if (ho_q_.empty() && !ho_stop_ && idle_spin_us_ > 0) {  // brief spin before sleeping (see device_loop)
         lk.unlock();
+        // (the clock is read every 32 pauses: a vDSO clock_gettime per pause
+        // was ~10% of the serving process's CPU with several units spinning)
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(idle_spin_us_);
-        while (!ho_pending_.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < until) _mm_pause();
+        for (unsigned n = 1; !ho_pending_.load(std::memory_order_acquire); ++n) {
+          _mm_pause();
+          if ((n & 31) == 0 && std::chrono::steady_clock::now() >= until) break;
+        }
         lk.lock();
       }
       if (ho_q_.empty()) {
@@ -615,9 +620,11 @@ void BatchedUnit::device_loop() {
       // costs about that much again.
       if (idle_spin_us_ > 0 && queued_n_.load(std::memory_order_acquire) == 0) {
         const auto until = clk::now() + std::chrono::microseconds(idle_spin_us_);
-        while (queued_n_.load(std::memory_order_acquire) == 0 && running_.load(std::memory_order_relaxed) &&
-               clk::now() < until)
+        for (unsigned n = 1; queued_n_.load(std::memory_order_acquire) == 0 && running_.load(std::memory_order_relaxed);
+             ++n) {
           _mm_pause();
+          if ((n & 31) == 0 && clk::now() >= until) break;
+        }
       }
     }
     if (inflight.empty() && pending.empty()) {
@@ -657,16 +664,23 @@ void BatchedUnit::device_loop() {
     if (inflight.empty()) continue;
     // ---- reap finished batches
     bool progress = false;
-    const auto now = clk::now();
     const int hang_ms = hang_ms_.load(std::memory_order_relaxed);
+    // The clock is read only when a check needs it: the injected-hang test
+    // on completion, and the watchdog on every 32nd poll of a busy slot.
+    clk::time_point now{};
+    bool have_now = false;
+    auto now_ = [&] {
+      if (!have_now) { now = clk::now(); have_now = true; }
+      return now;
+    };
+    const bool watch = opts_.hang_timeout_ms > 0 && (spins & 31) == 0;
     for (size_t i = 0; i < inflight.size();) {
       Slot* s = inflight[i];
       hipError_t st = cpu_ ? hipSuccess : hipEventQuery(s->ev.get());
-      if (st == hipSuccess && hang_ms > 0 && now - s->t_launch < std::chrono::milliseconds(hang_ms))
+      if (st == hipSuccess && hang_ms > 0 && now_() - s->t_launch < std::chrono::milliseconds(hang_ms))
         st = hipErrorNotReady;  // injected slow / hung device
       if (st == hipErrorNotReady) {
-        if (opts_.hang_timeout_ms > 0 && !s->abandoned &&
-            now - s->t_launch > std::chrono::milliseconds(opts_.hang_timeout_ms))
+        if (watch && !s->abandoned && now_() - s->t_launch > std::chrono::milliseconds(opts_.hang_timeout_ms))
           abandon(s);
         ++i;
         continue;
