@@ -10,6 +10,8 @@ from .utils.storage import Storage
 
 
 def __getattr__(name):  # the client pulls in protobuf / grpc: import it on first use
+    if name == "_C":  # `from seldon_core_amd import _C`: through the loader, torch's HIP runtime first
+        return native()
     if name in ("SeldonClient", "SeldonChannelCredentials", "SeldonCallCredentials"):
         from . import client
 

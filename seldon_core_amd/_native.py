@@ -33,7 +33,7 @@ def _load():
     except Exception:  # pragma: no cover - torch is always present in this image
         pass
     try:
-        from . import _C as mod  # type: ignore[attr-defined]
+        mod = importlib.import_module(__package__ + "._C")
     except ImportError as exc:
         candidates = glob.glob(os.path.join(_PKG, "_C*.so"))
         if candidates:

@@ -9,6 +9,11 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    # torch (and its HIP runtime) before any test module can load the native
+    # extension at collection time: two HIP runtimes in one process leave the
+    # second one with 0 visible devices
+    import torch  # noqa: F401
+
     config.addinivalue_line("markers", "gpu: needs an MI355X (run via gpurun)")
     config.addinivalue_line("markers", "slow: long-running test")
 

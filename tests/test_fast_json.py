@@ -4,7 +4,12 @@ parser + message_from_json produce, and decline everything else."""
 
 import pytest
 
-from seldon_core_amd import _C
+import seldon_core_amd as sca
+
+# through the loader (torch first: one HIP runtime in the process); a bare
+# `import seldon_core_amd._C` here, at collection time, made every later GPU
+# test in the session see 0 devices
+_C = sca.native()
 
 ACCEPT = [
     '{"data":{"names":["a","b","c","d"],"ndarray":[[5.1,3.5,1.4,0.2]]}}',
