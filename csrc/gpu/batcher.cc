@@ -24,6 +24,30 @@ bool available() { return device_count() > 0; }
 
 namespace {
 
+// Idle-spin permits shared by every unit of the process: a graph with
+// several units (A/B, MAB replicas) otherwise keeps a device and a hand-off
+// thread per unit spinning on the CPU share the front end needs (2 CPUs of
+// 12 in the MAB profile).  SCA_MAX_SPINNERS, default 4: at 2 the MAB graph
+// served the same 0.78-0.80M pred/s on 11.0-11.4 instead of 12.3-12.5 server
+// CPUs, single / A/B graphs within noise (profiles/r03h_frontend_fp32).
+std::atomic<int> g_spinners{0};
+int max_spinners() {
+  static const int m = [] {
+    const char* e = std::getenv("SCA_MAX_SPINNERS");
+    return e ? std::max(0, std::atoi(e)) : 4;
+  }();
+  return m;
+}
+struct SpinPermit {
+  bool ok;
+  SpinPermit() : ok(g_spinners.fetch_add(1, std::memory_order_relaxed) < max_spinners()) {
+    if (!ok) g_spinners.fetch_sub(1, std::memory_order_relaxed);
+  }
+  ~SpinPermit() {
+    if (ok) g_spinners.fetch_sub(1, std::memory_order_relaxed);
+  }
+};
+
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -456,10 +480,11 @@ void BatchedUnit::handoff_loop() {
       batch.clear();
       if (ho_q_.empty() && !ho_stop_ && idle_spin_us_ > 0) {  // brief spin before sleeping (see device_loop)
         lk.unlock();
+        SpinPermit permit;
         // (the clock is read every 32 pauses: a vDSO clock_gettime per pause
         // was ~10% of the serving process's CPU with several units spinning)
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(idle_spin_us_);
-        for (unsigned n = 1; !ho_pending_.load(std::memory_order_acquire); ++n) {
+        for (unsigned n = 1; permit.ok && !ho_pending_.load(std::memory_order_acquire); ++n) {
           _mm_pause();
           if ((n & 31) == 0 && std::chrono::steady_clock::now() >= until) break;
         }
@@ -619,8 +644,10 @@ void BatchedUnit::device_loop() {
       // arrives within tens of microseconds, and a condition-variable wake-up
       // costs about that much again.
       if (idle_spin_us_ > 0 && queued_n_.load(std::memory_order_acquire) == 0) {
+        SpinPermit permit;
         const auto until = clk::now() + std::chrono::microseconds(idle_spin_us_);
-        for (unsigned n = 1; queued_n_.load(std::memory_order_acquire) == 0 && running_.load(std::memory_order_relaxed);
+        for (unsigned n = 1; permit.ok && queued_n_.load(std::memory_order_acquire) == 0 &&
+                             running_.load(std::memory_order_relaxed);
              ++n) {
           _mm_pause();
           if ((n & 31) == 0 && clk::now() >= until) break;
