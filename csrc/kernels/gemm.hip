@@ -253,6 +253,23 @@ __device__ __forceinline__ int xcd_tile(int L, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
 }
 
+// Tile t (XCD-contiguous, from xcd_tile) -> (tile row, tile column) in
+// groups of gm tile rows, column-major inside a group: the ~32 tiles an XCD
+// runs at once cover gm A panels x 32/gm B panels instead of 1 x 32, so the
+// XCD's 4 MB L2 serves each K slice to gm (A) and 32/gm (B) tiles.  At
+// 8192^3 (256^2 tiles, row-major) the L2 hit rate was 44% and the fetch 2.3 GB
+// per GEMM against hipBLASLt's 80% / 0.8 GB (profiles/r03i_gemm_l2).
+__device__ __forceinline__ void grouped_tile(int t, int nM, int nN, int gm, int& mi, int& ni) {
+  if (gm <= 1) {
+    mi = t / nN;
+    ni = t - mi * nN;
+    return;
+  }
+  const int per = gm * nN, g = t / per, first = g * gm, gs = min(nM - first, gm), r = t - g * per;
+  mi = first + r % gs;
+  ni = r / gs;
+}
+
 // T = __bf16: v_mfma_f32_16x16x32_bf16, 64-deep K stages; T = float: exact
 // fp32 products on v_mfma_f32_16x16x4_f32 (four per 16-B fragment), 32-deep
 // stages.  The LDS image is the same in bytes either way: 128-B rows of eight
@@ -556,8 +573,9 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const DenseGemmArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 1, wc = wave & 1, r16 = lane & 15, kq = lane >> 4;
   const int nN = (a.Np + BN - 1) / BN;
-  const int t = xcd_tile(blockIdx.x, gridDim.x);
-  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+  int mi, ni;
+  grouped_tile(xcd_tile(blockIdx.x, gridDim.x), (a.rows_eff + BM - 1) / BM, nN, a.group_m, mi, ni);
+  const int m0 = mi * BM, n0 = ni * BN;
   const int KS = a.Kp / BK;
   const __bf16* A = static_cast<const __bf16*>(a.A);
   const __bf16* W = static_cast<const __bf16*>(a.W);
@@ -670,8 +688,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 1, wc = wave & 1, r16 = lane & 15, kq = lane >> 4;
   const int nN = (a.Np + BN - 1) / BN;
-  const int t = xcd_tile(blockIdx.x, gridDim.x);
-  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+  int mi, ni;
+  grouped_tile(xcd_tile(blockIdx.x, gridDim.x), (a.rows_eff + BM - 1) / BM, nN, a.group_m, mi, ni);
+  const int m0 = mi * BM, n0 = ni * BN;
   const int KS = a.Kp / BK;
   const __bf16* A = static_cast<const __bf16*>(a.A);
   const __bf16* W = static_cast<const __bf16*>(a.W);
@@ -817,14 +836,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // before its wait, and data is read only after a barrier that follows the
 // vmcnt of every issuing wave.  Loads are counted by hand (raw s_barrier,
 // explicit s_waitcnt): __syncthreads() would drain the DMA queue.
+//
+// SPREAD (path 6): the fragment reads spread over the phases as 12 / 4 / 8 /
+// 0 (q0: B cols 0-31 + A rows 0-63, q1: B cols 32-63, q2: A rows 64-127)
+// instead of 16 / 8 / 0 / 0, so no phase asks the LDS for more than ~75% of
+// the other group's MFMA time (16 ds_read_b128 per wave x 4 waves is 256
+// LDS clocks = 16 MFMAs).  Restaging moves with the reads: B0 / B1 of tile
+// t + 2 in q2 / q3 (the q1 B reads retired before q1's barrier), A0 of tile
+// t + 2 in q3 (the q2 A reads retired before q2's barrier), A1 of tile t + 1
+// in q0 as before; vmcnt(6) in q3 as before.
+template <bool SPREAD>
 __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
   constexpr int BM = 256, BN = 256, BK = 64, HT = 128 * BK;  // half tile (elements)
   extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // [parity][A/B][half] x HT
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 2, wc = wave & 3, r16 = lane & 15, kq = lane >> 4;
   const int nN = (a.Np + BN - 1) / BN;
-  const int t = xcd_tile(blockIdx.x, gridDim.x);
-  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+  int mi, ni;
+  grouped_tile(xcd_tile(blockIdx.x, gridDim.x), (a.rows_eff + BM - 1) / BM, nN, a.group_m, mi, ni);
+  const int m0 = mi * BM, n0 = ni * BN;
   const int KT = a.Kp / BK;
   const __bf16* A = static_cast<const __bf16*>(a.A);
   const __bf16* W = static_cast<const __bf16*>(a.W);
@@ -888,7 +918,73 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
   const int bh = wc >> 1, bo = (wc & 1) * 64;
-  for (int kt = 0; kt < KT; ++kt) {
+  for (int kt = 0; kt < KT && SPREAD; ++kt) {
+    const int par = kt & 1;
+    const __bf16* As = buf(par, 0, wr);
+    const __bf16* Bs = buf(par, 1, bh);
+    // ---- q0: B cols 0-31, then A rows 0-63; A1 of tile kt + 1
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bq[j][kk] = frag(Bs, bo + j * 16 + r16, kk);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) am0[i][kk] = frag(As, i * 16 + r16, kk);
+    if (kt + 1 < KT) issue(kt + 1, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(am0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q1: B cols 32-63 (retired before the barrier: B is restaged from q2)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 2; j < 4; ++j) bq[j][kk] = frag(Bs, bo + j * 16 + r16, kk);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(am0, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q2: A rows 64-127 (retired before the barrier: A0 is restaged in q3); B0 of tile kt + 2
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) am1[i][kk] = frag(As, 64 + i * 16 + r16, kk);
+    if (kt + 2 < KT) issue(kt + 2, 1, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(am1, 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q3: B1 and A0 of tile kt + 2; tile kt + 1 landed (3 younger half tiles may fly)
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < KT) {
+      issue(kt + 2, 1, 1);
+      issue(kt + 2, 0, 0);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_q(am1, 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  for (int kt = 0; kt < KT && !SPREAD; ++kt) {
     const int par = kt & 1;
     const __bf16* As = buf(par, 0, wr);
     const __bf16* Bs = buf(par, 1, bh);
@@ -1001,8 +1097,9 @@ __global__ __launch_bounds__(512) void gemm_glds256_kernel(const DenseGemmArgs a
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 2, wc = wave & 3, r16 = lane & 15, kq = lane >> 4;
   const int nN = (a.Np + BN - 1) / BN;
-  const int t = xcd_tile(blockIdx.x, gridDim.x);
-  const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+  int mi, ni;
+  grouped_tile(xcd_tile(blockIdx.x, gridDim.x), (a.rows_eff + BM - 1) / BM, nN, a.group_m, mi, ni);
+  const int m0 = mi * BM, n0 = ni * BN;
   const int KS = a.Kp / BK;
   const __bf16* A = static_cast<const __bf16*>(a.A);
   const __bf16* W = static_cast<const __bf16*>(a.W);
@@ -1100,7 +1197,7 @@ __global__ __launch_bounds__(512) void gemm_glds256_kernel(const DenseGemmArgs a
 }
 
 template <typename T, int AMODE>
-void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
+void launch_lds(DenseGemmArgs a, hipStream_t s) {  // by value: the dispatch fills defaults in
   // 128 x 64 tiles (two resident workgroups per CU) when they fill the chip,
   // 32 x 64 otherwise (narrow layers such as a 10-class head: 4x the
   // workgroups, so the A stream is spread over every CU).  The VAE decoder's
@@ -1120,6 +1217,8 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
     }
   }
   if constexpr (AMODE == 0 && sizeof(T) == 2) {
+    static const int gm_env = [] { const char* v = getenv("SCA_GEMM_GROUP_M"); return v ? atoi(v) : 4; }();
+    if (a.group_m <= 0) a.group_m = gm_env;
     // glds ring kernel: 128 x 128 tiles that fill the chip, N wide enough not
     // to waste the tile, no fused N <= 16 head (SCA_GEMM_GLDS=0 disables)
     static const int glds = [] { const char* v = getenv("SCA_GEMM_GLDS"); return v ? atoi(v) : 1; }();
@@ -1131,11 +1230,17 @@ void launch_lds(const DenseGemmArgs& a, hipStream_t s) {
       hipLaunchKernelGGL(gemm_w4_kernel, dim3(tiles256), dim3(256), lds, s, a);
       return;
     }
-    // default for chip-filling 256^2 grids: the 8-phase kernel (984 TF at
-    // 8192^3 vs 905 for path 3 and 774 for path 5, profiles/r03d_gemm)
-    if (fits && (a.path == 4 || (a.path == 0 && glds && a.Np >= 256 && tiles256 >= 256))) {
+    // default for chip-filling 256^2 grids: the 8-phase kernel with the reads
+    // spread 12 / 4 / 8 / 0 over the phases (no scratch; the 16 / 8 / 0 / 0
+    // form spills 528 B per lane) -- 1055 TF at 8192^3 with 4-row tile groups
+    if (fits && (a.path == 6 || (a.path == 0 && glds && a.Np >= 256 && tiles256 >= 256))) {
       const size_t lds = size_t(8) * 128 * 64 * sizeof(__bf16);
-      hipLaunchKernelGGL(gemm_8ph_kernel, dim3(tiles256), dim3(512), lds, s, a);
+      hipLaunchKernelGGL(gemm_8ph_kernel<true>, dim3(tiles256), dim3(512), lds, s, a);
+      return;
+    }
+    if (fits && a.path == 4) {
+      const size_t lds = size_t(8) * 128 * 64 * sizeof(__bf16);
+      hipLaunchKernelGGL(gemm_8ph_kernel<false>, dim3(tiles256), dim3(512), lds, s, a);
       return;
     }
     if (fits && a.path == 3) {

@@ -234,8 +234,13 @@ def case_gemm(iters):
         flops = 2.0 * rows * K * N
         n = iters if rows * K * N < 1e10 else max(3, iters // 5)
 
+        Ob = torch.empty(rows, N, device="cuda", dtype=torch.bfloat16)
+
         def run(path):
             C.kernels.gemm_bf16(A.data_ptr(), K, rows, W.data_ptr(), K, N, N, b.data_ptr(), 0, O.data_ptr(), N, 1, path)
+
+        def run_bf16_out(path):  # bf16 C, as torch.matmul writes it
+            C.kernels.gemm_bf16(A.data_ptr(), K, rows, W.data_ptr(), K, N, N, b.data_ptr(), 0, Ob.data_ptr(), N, 0, path)
 
         def lib():
             torch.matmul(A, W.T, out=None)
@@ -243,7 +248,9 @@ def case_gemm(iters):
         res = {}
         for _ in range(1 if os.environ.get("SCA_PMC") else 2):  # interleaved rounds
             for name, fn in (("reg", lambda: run(1)), ("glds", lambda: run(2)), ("glds256", lambda: run(3)),
-                             ("8ph", lambda: run(4)), ("w4", lambda: run(5)), ("torch", lib)):
+                             ("8ph", lambda: run(4)), ("8ph_spread", lambda: run(6)),
+                             ("8ph_spread_bf16out", lambda: run_bf16_out(6)), ("w4", lambda: run(5)),
+                             ("torch", lib)):
                 fn()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -256,7 +263,7 @@ def case_gemm(iters):
                 res[name] = min(res.get(name, 1e30), us)
         errs = {}
         ref = (A.float() @ W.float().T)
-        for pth, nm in ((3, "glds256"), (4, "8ph"), (5, "w4")):
+        for pth, nm in ((3, "glds256"), (4, "8ph"), (6, "8ph_spread"), (5, "w4")):
             run(pth)
             errs[nm + "_rel_err"] = float((O - ref).abs().max() / ref.abs().max())
         print(json.dumps({"case": "gemm_bf16", "M": rows, "K": K, "N": N,
