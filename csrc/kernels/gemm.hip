@@ -845,7 +845,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // t + 2 in q2 / q3 (the q1 B reads retired before q1's barrier), A0 of tile
 // t + 2 in q3 (the q2 A reads retired before q2's barrier), A1 of tile t + 1
 // in q0 as before; vmcnt(6) in q3 as before.
-template <bool SPREAD>
+// ABL (ablation, paths 7 / 8, timing only -- results are garbage): 1 drops
+// the MFMAs (the fragments are kept live), 2 drops the fragment ds_reads.
+template <bool SPREAD, int ABL = 0>
 __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
   constexpr int BM = 256, BN = 256, BK = 64, HT = 128 * BK;  // half tile (elements)
   extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // [parity][A/B][half] x HT
@@ -891,6 +893,13 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 am0[4][2], am1[4][2], bq[4][2];
   auto mfma_q = [&](bf16x8 (&af)[4][2], int mh, int nh) {
+    if constexpr (ABL == 1) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i][kk]), "v"(bq[nh * 2 + (i & 1)][kk]));
+      return;
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -927,12 +936,12 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bq[j][kk] = frag(Bs, bo + j * 16 + r16, kk);
+      for (int j = 0; j < 2; ++j) bq[j][kk] = ABL == 2 ? bq[j][kk] : frag(Bs, bo + j * 16 + r16, kk);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) am0[i][kk] = frag(As, i * 16 + r16, kk);
+      for (int i = 0; i < 4; ++i) am0[i][kk] = ABL == 2 ? am0[i][kk] : frag(As, i * 16 + r16, kk);
     if (kt + 1 < KT) issue(kt + 1, 0, 1);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -946,7 +955,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 2; j < 4; ++j) bq[j][kk] = frag(Bs, bo + j * 16 + r16, kk);
+      for (int j = 2; j < 4; ++j) bq[j][kk] = ABL == 2 ? bq[j][kk] : frag(Bs, bo + j * 16 + r16, kk);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -959,7 +968,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) am1[i][kk] = frag(As, 64 + i * 16 + r16, kk);
+      for (int i = 0; i < 4; ++i) am1[i][kk] = ABL == 2 ? am0[i][kk] : frag(As, 64 + i * 16 + r16, kk);
     if (kt + 2 < KT) issue(kt + 2, 1, 0);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
@@ -1233,6 +1242,12 @@ void launch_lds(DenseGemmArgs a, hipStream_t s) {  // by value: the dispatch fil
     // default for chip-filling 256^2 grids: the 8-phase kernel with the reads
     // spread 12 / 4 / 8 / 0 over the phases (no scratch; the 16 / 8 / 0 / 0
     // form spills 528 B per lane) -- 1055 TF at 8192^3 with 4-row tile groups
+    if (fits && (a.path == 7 || a.path == 8)) {  // ablations (timing only)
+      const size_t lds = size_t(8) * 128 * 64 * sizeof(__bf16);
+      if (a.path == 7) hipLaunchKernelGGL((gemm_8ph_kernel<true, 1>), dim3(tiles256), dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((gemm_8ph_kernel<true, 2>), dim3(tiles256), dim3(512), lds, s, a);
+      return;
+    }
     if (fits && (a.path == 6 || (a.path == 0 && glds && a.Np >= 256 && tiles256 >= 256))) {
       const size_t lds = size_t(8) * 128 * 64 * sizeof(__bf16);
       hipLaunchKernelGGL(gemm_8ph_kernel<true>, dim3(tiles256), dim3(512), lds, s, a);

@@ -250,7 +250,8 @@ def case_gemm(iters):
             for name, fn in (("reg", lambda: run(1)), ("glds", lambda: run(2)), ("glds256", lambda: run(3)),
                              ("8ph", lambda: run(4)), ("8ph_spread", lambda: run(6)),
                              ("8ph_spread_bf16out", lambda: run_bf16_out(6)), ("w4", lambda: run(5)),
-                             ("torch", lib)):
+                             ("torch", lib)) + ((("abl_no_mfma", lambda: run(7)), ("abl_no_reads", lambda: run(8)))
+                                                if os.environ.get("GEMM_ABLATE") else ()):
                 fn()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
