@@ -989,16 +989,19 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("best_branch", &gpu::BanditModel::best_branch)
       .def_property_readonly("n_branches", &gpu::BanditModel::n_branches)
       .def("snapshot", &gpu::BanditModel::snapshot)
-      .def("restore", &gpu::BanditModel::restore);
+      .def("restore", &gpu::BanditModel::restore)
+      .def("route_host", &gpu::BanditModel::route_host, "epsilon-greedy decision on the host (kernel's Philox stream)");
   py::class_<gpu::BanditRouterUnit, Unit, std::shared_ptr<gpu::BanditRouterUnit>>(m, "BanditRouterUnit")
-      .def(py::init([](std::shared_ptr<gpu::BanditModel> model, int device, int max_batch, int slots) {
+      .def(py::init([](std::shared_ptr<gpu::BanditModel> model, int device, int max_batch, int slots, bool device_route) {
              gpu::BatcherOptions o;
              o.device = device;
              o.max_batch = max_batch;
              o.slots = slots;
-             return std::make_shared<gpu::BanditRouterUnit>(model, o);
+             return std::make_shared<gpu::BanditRouterUnit>(model, o, device_route);
            }),
-           py::arg("model"), py::arg("device") = 0, py::arg("max_batch") = 4096, py::arg("slots") = 2)
+           py::arg("model"), py::arg("device") = 0, py::arg("max_batch") = 4096, py::arg("slots") = 2,
+           py::arg("device_route") = false)
+      .def_property_readonly("batcher", &gpu::BanditRouterUnit::batcher)
       .def_property_readonly("model", &gpu::BanditRouterUnit::model)
       .def("stats", [](const gpu::BanditRouterUnit& u) {
         auto s = u.batcher()->stats();

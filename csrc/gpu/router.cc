@@ -2,6 +2,8 @@
 
 #include <sstream>
 
+#include "../kernels/philox.h"
+
 namespace sca::gpu {
 
 BanditModel::BanditModel(Kind kind, int n_branches, float epsilon, int64_t seed, int best_branch)
@@ -23,6 +25,7 @@ BanditModel::BanditModel(Kind kind, int n_branches, float epsilon, int64_t seed,
 
 void BanditModel::publish() {
   host_state_.best = best_;
+  best_pub_.store(best_, std::memory_order_release);
   for (int i = 0; i < nb_; ++i) {
     host_state_.alpha[i] = float(a_[size_t(i)]);
     host_state_.beta[i] = float(b_[size_t(i)]);
@@ -43,6 +46,19 @@ void BanditModel::launch(const double*, int rows, int, double* out, void*, hipSt
     kern::eg_route(&st->best, nb_, eps_, seed_, off, rows, out, s);
   else
     kern::ts_route(st->alpha, st->beta, nb_, seed_, off, rows, out, s);
+}
+
+int BanditModel::route_host() {
+  const uint64_t off = offset_.fetch_add(1, std::memory_order_relaxed);
+  kern::Philox rng(seed_, off);
+  const int b = best_pub_.load(std::memory_order_acquire);
+  int pick = b;
+  if (nb_ > 1 && rng.uniform() <= eps_) {
+    int other = int(rng.next() % uint32_t(nb_ - 1));
+    if (other >= b) ++other;
+    pick = other;
+  }
+  return pick;
 }
 
 void BanditModel::run_cpu(const double*, int rows, int, double* out) const {
@@ -140,12 +156,22 @@ void BanditModel::restore(const std::string& s) {
 }
 
 // ------------------------------------------------------------------ unit
-BanditRouterUnit::BanditRouterUnit(std::shared_ptr<BanditModel> model, BatcherOptions opts)
+BanditRouterUnit::BanditRouterUnit(std::shared_ptr<BanditModel> model, BatcherOptions opts, bool device_route)
     : model_(std::move(model)), opts_(opts) {
   batched_ = std::make_shared<BatchedUnit>(model_, opts_);
+  host_route_ = opts_.device >= 0 && !device_route && model_->host_routable();
 }
 
 void BanditRouterUnit::route(const CallCtx& c, MsgPtr, Done k) {
+  if (host_route_) {
+    auto m = std::make_shared<SeldonMessage>();
+    m->payload = Payload::Data;
+    m->data.kind = DataKind::Tensor;
+    m->data.shape = {1, 1};
+    m->data.values = {double(model_->route_host())};
+    k(Outcome::ok(std::move(m)));
+    return;
+  }
   static thread_local MsgPtr probe = [] {
     auto m = std::make_shared<SeldonMessage>();
     m->payload = Payload::Data;

@@ -37,6 +37,11 @@ class BanditModel : public RowModel {
   void restore(const std::string& s);
   std::vector<double> values() const;
   int best_branch() const;
+  // Epsilon-greedy decision for the next request on the host: the same
+  // Philox stream (seed, request counter) and rule as eg_route_kernel, so
+  // the decision sequence is identical to the batched device path's.
+  bool host_routable() const { return kind_ == kEpsilonGreedy; }
+  int route_host();
 
  private:
   struct State {
@@ -58,13 +63,22 @@ class BanditModel : public RowModel {
   std::vector<double> a_, b_;
   PinnedBuffer state_;
   State host_state_{};
+  std::atomic<int> best_pub_{0};  // published best branch (host route)
   std::atomic<uint64_t> offset_{0};
 };
 
 class BanditRouterUnit : public Unit {
  public:
-  BanditRouterUnit(std::shared_ptr<BanditModel> model, BatcherOptions opts);
-  std::string kind() const override { return (opts_.device >= 0 ? "gpu:" : "cpu:") + model_->name(); }
+  // device_route: decide through the micro-batched bandit kernel (one GPU
+  // round trip per routed request).  Otherwise an epsilon-greedy router
+  // decides on the caller's thread with the kernel's Philox stream: a
+  // routed request then costs one GPU round trip (its branch) instead of two
+  // (profiles/r03j_router).  Thompson sampling always uses the kernel.
+  BanditRouterUnit(std::shared_ptr<BanditModel> model, BatcherOptions opts, bool device_route = false);
+  std::string kind() const override {
+    if (host_route_) return "host:" + model_->name();
+    return (opts_.device >= 0 ? "gpu:" : "cpu:") + model_->name();
+  }
   void route(const CallCtx& c, MsgPtr in, Done k) override;
   void send_feedback(const CallCtx& c, std::shared_ptr<const Feedback> fb, FbDone k) override;
   std::string snapshot() const override { return model_->snapshot(); }
@@ -76,6 +90,7 @@ class BanditRouterUnit : public Unit {
   std::shared_ptr<BanditModel> model_;
   BatcherOptions opts_;
   std::shared_ptr<BatchedUnit> batched_;
+  bool host_route_ = false;
 };
 
 }  // namespace sca::gpu

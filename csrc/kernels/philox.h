@@ -1,6 +1,9 @@
 // Counter-based Philox4x32-10 generator shared by the device-side samplers
 // (bandit routers, VAE reparameterisation): stream = (seed, subsequence), so
 // draws are reproducible and independent of launch geometry / batching.
+// The integer stream and uniform() also compile for the host (bit-identical:
+// integer arithmetic and one exact int->float conversion), so the host
+// epsilon-greedy path (csrc/gpu/router.cc) makes the same decisions.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -15,7 +18,7 @@ struct Philox {
   uint32_t out[4];
   int used = 4;
 
-  __device__ Philox(uint64_t seed, uint64_t subseq) {
+  __host__ __device__ Philox(uint64_t seed, uint64_t subseq) {
     k[0] = uint32_t(seed);
     k[1] = uint32_t(seed >> 32);
     c[0] = uint32_t(subseq);
@@ -23,11 +26,10 @@ struct Philox {
     c[2] = 0;
     c[3] = 0;
   }
-  __device__ void round() {
+  __host__ __device__ void round() {
     uint32_t kk0 = k[0], kk1 = k[1];
     uint32_t x0 = c[0], x1 = c[1], x2 = c[2], x3 = c[3];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < 10; ++i) {  // (fully unrolled by the compiler: constant trip count)
       const uint64_t p0 = uint64_t(0xD2511F53u) * x0;
       const uint64_t p1 = uint64_t(0xCD9E8D57u) * x2;
       const uint32_t y0 = uint32_t(p1 >> 32) ^ x1 ^ kk0;
@@ -42,12 +44,13 @@ struct Philox {
     if (++c[2] == 0) ++c[3];
     used = 0;
   }
-  __device__ uint32_t next() {
+  __host__ __device__ uint32_t next() {
     if (used == 4) round();
     return out[used++];
   }
   // (0, 1]
-  __device__ float uniform() { return (float(next() >> 8) + 1.0f) * (1.0f / 16777216.0f); }
+  __host__ __device__ float uniform() { return (float(next() >> 8) + 1.0f) * (1.0f / 16777216.0f); }
+#ifdef __HIPCC__  // device-only samplers (host translation units, e.g. router.cc, use the integer stream)
   __device__ float normal() {
     const float u1 = uniform(), u2 = uniform();
     return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
@@ -74,6 +77,7 @@ struct Philox {
     }
     return d * boost;
   }
+#endif
 };
 
 }  // namespace sca::kern

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 from typing import Optional
 
 import numpy as np
@@ -34,7 +35,8 @@ class _BanditRouter:
 
     def __init__(self, n_branches=None, epsilon: float = 0.1, best_branch: Optional[int] = None,
                  verbose: bool = False, seed: Optional[int] = None, history: bool = False,
-                 branch_names: Optional[str] = None, device: Optional[int] = None, max_batch: int = 4096):
+                 branch_names: Optional[str] = None, device: Optional[int] = None, max_batch: int = 4096,
+                 route_on: str = "auto"):
         from .._native import native
 
         try:
@@ -50,6 +52,14 @@ class _BanditRouter:
         self.branch_names = branch_names.split(":") if branch_names else None
         self.device = device
         self.max_batch = max_batch
+        # "auto": on a GPU deployment an epsilon-greedy decision is made on the
+        # caller's thread from the bandit kernel's Philox stream (identical
+        # decisions, one GPU round trip less per routed request); "device":
+        # every decision through the micro-batched bandit kernel
+        # (SCA_ROUTER_ON_DEVICE=1 makes that the default)
+        if route_on not in ("auto", "device"):
+            raise ValueError("route_on must be 'auto' or 'device'")
+        self.route_on = "device" if os.environ.get("SCA_ROUTER_ON_DEVICE") == "1" else route_on
         self._C = native()
         self.model = self._C.BanditModel(self.kind, n_branches, float(epsilon),
                                          -1 if seed is None else int(seed),
@@ -59,7 +69,8 @@ class _BanditRouter:
     # -- native binding (Deployment) ---------------------------------------
     def native_unit(self, device: int):
         dev = device if self.device is None else int(self.device)
-        self._unit = self._C.BanditRouterUnit(self.model, dev, self.max_batch)
+        self._unit = self._C.BanditRouterUnit(self.model, dev, self.max_batch,
+                                              device_route=self.route_on == "device")
         return self._unit
 
     # -- reference component API --------------------------------------------
@@ -95,5 +106,6 @@ class ThompsonSampling(_BanditRouter):
     kind = THOMPSON
 
     def __init__(self, n_branches=None, verbose: bool = False, seed: Optional[int] = None, history: bool = False,
-                 branch_names: Optional[str] = None, device: Optional[int] = None, max_batch: int = 4096):
-        super().__init__(n_branches, 0.0, None, verbose, seed, history, branch_names, device, max_batch)
+                 branch_names: Optional[str] = None, device: Optional[int] = None, max_batch: int = 4096,
+                 route_on: str = "auto"):
+        super().__init__(n_branches, 0.0, None, verbose, seed, history, branch_names, device, max_batch, route_on)

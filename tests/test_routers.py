@@ -48,7 +48,7 @@ def test_router_snapshot_restore():
     assert r2.best_branch == 3 and r2.state()["success"] == r.state()["success"]
 
 
-def _mab_deployment(device, n=4, kind="EPSILON_GREEDY"):
+def _mab_deployment(device, n=4, kind="EPSILON_GREEDY", route_on=None):
     class Const:
         def __init__(self, v):
             self.v = v
@@ -62,6 +62,8 @@ def _mab_deployment(device, n=4, kind="EPSILON_GREEDY"):
     if kind == "EPSILON_GREEDY":
         params += [{"name": "epsilon", "value": "0.2", "type": "FLOAT"},
                    {"name": "best_branch", "value": "0", "type": "INT"}]
+    if route_on:
+        params += [{"name": "route_on", "value": route_on, "type": "STRING"}]
     spec = {"name": "mab", "graph": {"name": "router", "type": "ROUTER", "implementation": kind,
                                      "parameters": params, "children": children}}
     return sca.Deployment(spec, components={f"m{i}": Const(i) for i in range(n)}, device=device)
@@ -84,10 +86,11 @@ def test_mab_graph_with_feedback_cpu(kind):
 
 
 @pytest.mark.gpu
-def test_mab_graph_gpu_router():
-    d = _mab_deployment(0)
+@pytest.mark.parametrize("route_on,kind_name", [("auto", "host:epsilon_greedy"), ("device", "gpu:epsilon_greedy")])
+def test_mab_graph_gpu_router(route_on, kind_name):
+    d = _mab_deployment(0, route_on=route_on)
     try:
-        assert d.engine.unit_kind("router") == "gpu:epsilon_greedy"
+        assert d.engine.unit_kind("router") == kind_name
         counts = np.zeros(4)
         for _ in range(2000):
             out = d.predict({"data": {"ndarray": [[1.0]]}})
@@ -95,3 +98,20 @@ def test_mab_graph_gpu_router():
         assert abs(counts[0] / 2000 - 0.8) < 0.04
     finally:
         d.close()
+
+
+@pytest.mark.gpu
+def test_eg_host_route_matches_bandit_kernel():
+    """The host epsilon-greedy path draws from the kernel's Philox stream
+    (seed, request counter): the same decision sequence as eg_route_kernel."""
+    C = sca.native()
+    dev = C.BanditModel(0, 5, 0.35, 11, 2)
+    host = C.BanditModel(0, 5, 0.35, 11, 2)
+    unit = C.BanditRouterUnit(dev, 0, device_route=True)
+    try:
+        picks_dev = unit.batcher.run(np.zeros((3000, 1))).ravel().astype(int)
+    finally:
+        unit.stop()
+    picks_host = np.array([host.route_host() for _ in range(3000)])
+    assert (picks_dev == picks_host).all()
+    assert abs(np.mean(picks_host == 2) - 0.65) < 0.03
