@@ -843,7 +843,7 @@ PYBIND11_MODULE(_C, m) {
                                    int cmp_le, uintptr_t chunk_begin, int n_chunks, int rb, uintptr_t partial,
                                    uintptr_t s, int lds_trees) {
     kern::tree_perfect_partial(P<const double>(X), rows, F, P<const kern::TreeNode>(nodes), P<const float>(leaves),
-                               depth, cmp_le, P<const int>(chunk_begin), n_chunks, rb, P<float>(partial),
+                               depth, cmp_le, P<const int>(chunk_begin), n_chunks, rb, P<double>(partial),
                                as_stream(s), lds_trees);
   }, py::arg("X"), py::arg("rows"), py::arg("F"), py::arg("nodes"), py::arg("leaves"), py::arg("depth"),
      py::arg("cmp_le"), py::arg("chunk_begin"), py::arg("n_chunks"), py::arg("rb"), py::arg("partial"), py::arg("s"),
@@ -855,13 +855,13 @@ PYBIND11_MODULE(_C, m) {
     const kern::TreeReduceArgs red{P<int>(counter), P<const int>(chunk_group), groups, P<const float>(base), scale,
                                    transform, P<double>(out), out_cols};
     kern::tree_perfect_fused(P<const double>(X), rows, F, P<const kern::TreeNode>(nodes), P<const float>(leaves),
-                             depth, cmp_le, P<const int>(chunk_begin), n_chunks, rb, P<float>(partial), red,
+                             depth, cmp_le, P<const int>(chunk_begin), n_chunks, rb, P<double>(partial), red,
                              as_stream(s), lds_trees);
   });
   k.def("tree_lds_max_trees", &kern::tree_lds_max_trees);
   k.def("tree_reduce", [](uintptr_t partial, int rows, int n_chunks, uintptr_t chunk_group, int groups,
                           uintptr_t base, float scale, int transform, uintptr_t out, int out_cols, uintptr_t s) {
-    kern::tree_reduce(P<const float>(partial), rows, n_chunks, P<const int>(chunk_group), groups, P<const float>(base),
+    kern::tree_reduce(P<const double>(partial), rows, n_chunks, P<const int>(chunk_group), groups, P<const float>(base),
                       scale, transform, P<double>(out), out_cols, as_stream(s));
   });
   k.def("combine_mean_f64", [](uintptr_t inputs, int n_in, int64_t n, uintptr_t out, uintptr_t s) {

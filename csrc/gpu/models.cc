@@ -153,7 +153,7 @@ size_t TreeEnsembleModel::workspace_bytes(int max_rows, int) const {
     plan_for(r, &rb, &pi);
     slab = std::max(slab, size_t(plans_[size_t(pi)]->n_chunks) * size_t(r));
   }
-  return kTreeWsHeader + slab * sizeof(float);
+  return kTreeWsHeader + slab * sizeof(double);
 }
 
 void TreeEnsembleModel::plan_for(int rows, int* rows_per_block, int* plan_index, int* lds_trees) const {
@@ -220,7 +220,7 @@ bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double*
   plan_for(rows, &rb, &pi, &lt);
   const Plan& p = *plans_[size_t(pi)];
   int* counter = static_cast<int*>(ws);
-  float* partial = reinterpret_cast<float*>(static_cast<char*>(ws) + kTreeWsHeader);
+  double* partial = reinterpret_cast<double*>(static_cast<char*>(ws) + kTreeWsHeader);
   // Small slabs may fold in the partial kernel's last workgroup (one launch
   // per batch; the tail does <= 16 slab loads per thread) -- off by default,
   // see plan_for.

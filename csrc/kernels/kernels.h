@@ -46,7 +46,7 @@ struct TreeNode {
 // (perfect trees of depth <= 10; see tree_lds_max_trees).
 void tree_perfect_partial(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves,
                           int depth, int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block,
-                          float* partial, hipStream_t stream, int lds_trees = 0);
+                          double* partial, hipStream_t stream, int lds_trees = 0);
 // Largest chunk (in trees) whose nodes + leaves fit in LDS next to the
 // feature tile for this geometry (0: depth too large for LDS staging).
 int tree_lds_max_trees(int depth, int rows_per_block, int F);
@@ -59,7 +59,7 @@ struct SparseNode {
 };
 // feat bit 31 = default-left; left < 0 marks a leaf (value in thr).
 void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root,
-                         int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
+                         int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block, double* partial,
                          hipStream_t stream);
 // Reduce chunk partials to per-group margins and apply the objective transform.
 // chunk_group[c] = output column of chunk c; out [rows, out_cols] fp64.
@@ -71,7 +71,7 @@ enum TreeTransform : int {
   kTreeMean = 4,          // random forest regression average
   kTreeIsolation = 5,     // isolation forest: 2^(-mean_path / c(n)) score
 };
-void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,
+void tree_reduce(const double* partial, int rows, int n_chunks, const int* chunk_group, int groups,
                  const float* base_margin, float scale, int transform, double* out, int out_cols,
                  hipStream_t stream, hipEvent_t stop = nullptr);
 // Fused variant: the partial kernel's last workgroup to finish (device-scope
@@ -91,11 +91,11 @@ struct TreeReduceArgs {
   int out_cols;
 };
 void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
-                        int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
+                        int cmp_le, const int* chunk_begin, int n_chunks, int rows_per_block, double* partial,
                         const TreeReduceArgs& red, hipStream_t stream, int lds_trees = 0,
                         hipEvent_t stop = nullptr);
 void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
-                       const int* chunk_begin, int n_chunks, int rows_per_block, float* partial,
+                       const int* chunk_begin, int n_chunks, int rows_per_block, double* partial,
                        const TreeReduceArgs& red, hipStream_t stream, hipEvent_t stop = nullptr);
 
 // ------------------------------------------------------------ combiners

@@ -77,7 +77,7 @@ __device__ __forceinline__ void stage_tile(float* tile, const double* __restrict
 // 85% of its cycles waiting on that chain (profiles/r02a_tree).  Invalid
 // slots (past the chunk end) walk tree t0 and contribute 0.
 template <int D, int U, bool STAGED>
-__device__ __forceinline__ float descend_perfect(const TreeNode* __restrict__ nodes, const float* __restrict__ leaves,
+__device__ __forceinline__ double descend_perfect(const TreeNode* __restrict__ nodes, const float* __restrict__ leaves,
                                                  int n_internal, int depth, int t, int t1, int tstride, int tfirst,
                                                  const float* xs, int lrb, const double* __restrict__ xg, int cmp_le) {
   const TreeNode* tn[U];
@@ -109,11 +109,11 @@ __device__ __forceinline__ float descend_perfect(const TreeNode* __restrict__ no
   } else {
     for (int d = 0; d < depth; ++d) level();
   }
-  float acc = 0.f;
+  double acc = 0.0;  // fp64 sums of fp32 leaves: exact in practice, so order-free (see reduce_write)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const float v = lf[u][idx[u] - n_internal];
-    acc += ok[u] ? v : 0.f;
+    acc += ok[u] ? double(v) : 0.0;
   }
   return acc;
 }
@@ -151,15 +151,19 @@ __device__ __forceinline__ void copy_to_lds(void* lds_dst, const void* gsrc, int
 // COHERENT: the slab is read back inside the same launch by the fused tail on
 // another XCD, so rows are written with agent-scope (sc1, write-through past
 // this XCD's L2) stores -- no whole-L2 writeback/invalidate fences needed.
+// Accumulators and the slab are fp64: the fp32 leaves of a model span few
+// binades, so their fp64 partial sums carry no rounding and the result does
+// not depend on how trees were chunked or rows grouped -- a row scores the
+// same in a batch of 1 or 4096 (the chunk plan follows the batch size).
 template <bool COHERENT>
-__device__ __forceinline__ void reduce_write(float* red, float acc, int RB, int row0, int rows, int chunk,
-                                             float* __restrict__ partial) {
+__device__ __forceinline__ void reduce_write(double* red, double acc, int RB, int row0, int rows, int chunk,
+                                             double* __restrict__ partial) {
   for (int off = 32; off >= RB; off >>= 1) acc += __shfl_xor(acc, off, 64);
   const int lane = int(threadIdx.x) & 63, wave = int(threadIdx.x) >> 6;
   if (lane < RB) red[wave * RB + lane] = acc;
   __syncthreads();
   if (int(threadIdx.x) < RB) {
-    float s = 0.f;
+    double s = 0.0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) s += red[w * RB + threadIdx.x];
     const int r = row0 + threadIdx.x;
@@ -218,11 +222,11 @@ __device__ __forceinline__ void apply_transform(double* m, int groups, int trans
 // flushes each XCD's L2 and evicts the resident tree model (measured 15 us vs
 // ~6 us per launch).  The fold uses the whole workgroup: RB rows x (256 / RB)
 // chunk lanes, lanes combined through LDS per group.
-__device__ __forceinline__ float coherent_load(const float* p) {
+__device__ __forceinline__ double coherent_load(const double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ void fused_tail(const float* partial, int rows, int n_chunks, const TreeReduceArgs& red) {
+__device__ void fused_tail(const double* partial, int rows, int n_chunks, const TreeReduceArgs& red) {
   __shared__ int s_last;
   __shared__ double s_fold[kBlock];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slab stores acknowledged at the coherence point
@@ -276,14 +280,14 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
                                                           const TreeNode* __restrict__ nodes,
                                                           const float* __restrict__ leaves, int depth, int cmp_le,
                                                           const int* __restrict__ chunk_begin, int RB,
-                                                          int stage_lds, float* __restrict__ partial, int n_chunks,
+                                                          int stage_lds, double* __restrict__ partial, int n_chunks,
                                                           int lds_trees, TreeReduceArgs red) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* red_lds = lds;        // [kBlock]
-  float* tile = lds + kBlock;  // [F][RB] when staged
+  double* red_lds = reinterpret_cast<double*>(lds);  // [kBlock] doubles
+  float* tile = lds + 2 * kBlock;                     // [F][RB] when staged
   const int tile_floats = stage_lds ? ((RB * F + 3) & ~3) : 0;
   const int n_internal = (1 << depth) - 1;
-  TreeNode* s_nodes = reinterpret_cast<TreeNode*>(lds + kBlock + tile_floats);  // [lds_trees][n_internal]
+  TreeNode* s_nodes = reinterpret_cast<TreeNode*>(lds + 2 * kBlock + tile_floats);  // [lds_trees][n_internal]
   float* s_leaves = reinterpret_cast<float*>(reinterpret_cast<char*>(s_nodes) +
                                             ((size_t(lds_trees) * n_internal * sizeof(TreeNode) + 15) & ~size_t(15)));
   const int lrb = __builtin_ctz(unsigned(RB));
@@ -306,7 +310,7 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
   const TreeNode* nbase = TREES_LDS ? s_nodes - size_t(t0) * n_internal : nodes;
   const float* lbase = TREES_LDS ? s_leaves - size_t(t0) * (n_internal + 1) : leaves;
   constexpr int U = 4;
-  float acc = 0.f;
+  double acc = 0.0;
   if (stage_lds) {
     for (int t = t0 + slot; t < t1; t += tpr * U)
       acc += descend_perfect<D, U, true>(nbase, lbase, n_internal, depth, t, t1, tpr, t0, xs, lrb, xg, cmp_le);
@@ -314,7 +318,7 @@ __global__ __launch_bounds__(kBlock) void perfect_partial(const double* __restri
     for (int t = t0 + slot; t < t1; t += tpr * U)
       acc += descend_perfect<D, U, false>(nbase, lbase, n_internal, depth, t, t1, tpr, t0, xs, lrb, xg, cmp_le);
   }
-  if (!row_ok) acc = 0.f;
+  if (!row_ok) acc = 0.0;
   if (stage_lds) __syncthreads();  // tile no longer needed; `red` is disjoint anyway
   reduce_write<FUSED>(red_lds, acc, RB, row0, rows, chunk, partial);
   if constexpr (FUSED) fused_tail(partial, rows, n_chunks, red);
@@ -327,11 +331,11 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
                                                          const SparseNode* __restrict__ nodes,
                                                          const int* __restrict__ tree_root, int cmp_le,
                                                          const int* __restrict__ chunk_begin, int RB, int stage_lds,
-                                                         float* __restrict__ partial, int n_chunks,
+                                                         double* __restrict__ partial, int n_chunks,
                                                          TreeReduceArgs red) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* red_lds = lds;
-  float* tile = lds + kBlock;
+  double* red_lds = reinterpret_cast<double*>(lds);
+  float* tile = lds + 2 * kBlock;
   const int lrb = __builtin_ctz(unsigned(RB));
   const int row0 = blockIdx.x * RB;
   const int chunk = blockIdx.y;
@@ -345,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
   const bool row_ok = row0 + r_local < rows;
   const int t0 = chunk_begin[chunk], t1 = chunk_begin[chunk + 1];
   constexpr int U = 4;
-  float acc = 0.f;
+  double acc = 0.0;
   if (row_ok) {
     const float* xs = tile + r_local;
     const double* xg = X + size_t(row0 + r_local) * F;
@@ -373,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
           if (nxt[u] >= 0) nd[u] = nodes[nxt[u]];
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc += ok[u] ? nd[u].thr : 0.f;
+      for (int u = 0; u < U; ++u) acc += ok[u] ? double(nd[u].thr) : 0.0;
     }
   }
   if (stage_lds) __syncthreads();
@@ -386,7 +390,7 @@ constexpr int kMaxGroups = 64;
 // Block = RB rows x (blockDim / RB) chunk-lanes: the lanes of a row sum a
 // strided subset of the tree chunks (independent, coalesced slab loads), fold
 // through LDS, and lane 0 applies the objective transform.
-__global__ __launch_bounds__(kBlock) void reduce_transform(const float* __restrict__ partial, int rows, int n_chunks,
+__global__ __launch_bounds__(kBlock) void reduce_transform(const double* __restrict__ partial, int rows, int n_chunks,
                                                            const int* __restrict__ chunk_group, int groups,
                                                            const float* __restrict__ base_margin, float scale,
                                                            int transform, double* __restrict__ out, int out_cols,
@@ -411,7 +415,7 @@ __global__ __launch_bounds__(kBlock) void reduce_transform(const float* __restri
 
 int lds_bytes_for(int RB, int F, bool* stage) {
   *stage = RB * F <= kMaxLdsFloats;
-  return int((kBlock + (*stage ? RB * F : 0)) * sizeof(float));
+  return int((2 * kBlock + (*stage ? RB * F : 0)) * sizeof(float));  // fp64 reduce area + fp32 tile
 }
 
 constexpr int kMaxTreeLdsDepth = 10;
@@ -422,11 +426,11 @@ constexpr int kTreeLdsPad = 16;  // leaves slab rounded up to 16 B
 
 template <bool FUSED>
 void launch_perfect(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
-                    int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
+                    int cmp_le, const int* chunk_begin, int n_chunks, int RB, double* partial, const TreeReduceArgs& red,
                     int lds_trees, hipStream_t s, hipEvent_t stop = nullptr) {
   bool stage;
   int lds = lds_bytes_for(RB, F, &stage);
-  if (stage) lds = int((kBlock + ((RB * F + 3) & ~3)) * sizeof(float));
+  if (stage) lds = int((2 * kBlock + ((RB * F + 3) & ~3)) * sizeof(float));
   if (depth > kMaxTreeLdsDepth || lds + lds_trees * tree_bytes(depth) + kTreeLdsPad > kMaxLdsBytes) lds_trees = 0;
   if (lds_trees) lds += lds_trees * tree_bytes(depth) + kTreeLdsPad;
   dim3 grid((rows + RB - 1) / RB, n_chunks);
@@ -458,7 +462,7 @@ void launch_perfect(const double* X, int rows, int F, const TreeNode* nodes, con
 
 template <bool FUSED>
 void launch_sparse(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
-                   const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
+                   const int* chunk_begin, int n_chunks, int RB, double* partial, const TreeReduceArgs& red,
                    hipStream_t s, hipEvent_t stop = nullptr) {
   bool stage;
   const int lds = lds_bytes_for(RB, F, &stage);
@@ -474,7 +478,7 @@ void launch_sparse(const double* X, int rows, int F, const SparseNode* nodes, co
 }  // namespace
 
 void tree_perfect_partial(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
-                          int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial,
+                          int cmp_le, const int* chunk_begin, int n_chunks, int RB, double* partial,
                           hipStream_t s, int lds_trees) {
   if (rows <= 0 || n_chunks <= 0) return;
   launch_perfect<false>(X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, n_chunks, RB, partial,
@@ -485,18 +489,18 @@ int tree_lds_max_trees(int depth, int rows_per_block, int F) {
   if (depth <= 0 || depth > kMaxTreeLdsDepth) return 0;
   bool stage;
   int lds = lds_bytes_for(rows_per_block, F, &stage);
-  if (stage) lds = int((kBlock + ((rows_per_block * F + 3) & ~3)) * sizeof(float));
+  if (stage) lds = int((2 * kBlock + ((rows_per_block * F + 3) & ~3)) * sizeof(float));
   return std::max(0, (kMaxLdsBytes - lds - kTreeLdsPad) / tree_bytes(depth));
 }
 
 void tree_sparse_partial(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
-                         const int* chunk_begin, int n_chunks, int RB, float* partial, hipStream_t s) {
+                         const int* chunk_begin, int n_chunks, int RB, double* partial, hipStream_t s) {
   if (rows <= 0 || n_chunks <= 0) return;
   launch_sparse<false>(X, rows, F, nodes, tree_root, cmp_le, chunk_begin, n_chunks, RB, partial, TreeReduceArgs{}, s);
 }
 
 void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
-                        int cmp_le, const int* chunk_begin, int n_chunks, int RB, float* partial,
+                        int cmp_le, const int* chunk_begin, int n_chunks, int RB, double* partial,
                         const TreeReduceArgs& red, hipStream_t s, int lds_trees, hipEvent_t stop) {
   if (rows <= 0 || n_chunks <= 0) return;
   launch_perfect<true>(X, rows, F, nodes, leaves, depth, cmp_le, chunk_begin, n_chunks, RB, partial, red, lds_trees,
@@ -504,13 +508,13 @@ void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes,
 }
 
 void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
-                       const int* chunk_begin, int n_chunks, int RB, float* partial, const TreeReduceArgs& red,
+                       const int* chunk_begin, int n_chunks, int RB, double* partial, const TreeReduceArgs& red,
                        hipStream_t s, hipEvent_t stop) {
   if (rows <= 0 || n_chunks <= 0) return;
   launch_sparse<true>(X, rows, F, nodes, tree_root, cmp_le, chunk_begin, n_chunks, RB, partial, red, s, stop);
 }
 
-void tree_reduce(const float* partial, int rows, int n_chunks, const int* chunk_group, int groups,
+void tree_reduce(const double* partial, int rows, int n_chunks, const int* chunk_group, int groups,
                  const float* base_margin, float scale, int transform, double* out, int out_cols, hipStream_t s,
                  hipEvent_t stop) {
   if (rows <= 0) return;

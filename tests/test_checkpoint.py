@@ -139,7 +139,8 @@ def test_gpu_bandit_router_checkpoint_roundtrip(tmp_path):
     def gpu_mab():
         params = [{"name": "n_branches", "value": "3", "type": "INT"}, {"name": "seed", "value": "7", "type": "INT"},
                   {"name": "epsilon", "value": "0.1", "type": "FLOAT"},
-                  {"name": "best_branch", "value": "0", "type": "INT"}]
+                  {"name": "best_branch", "value": "0", "type": "INT"},
+                  {"name": "route_on", "value": "device", "type": "STRING"}]  # the batched bandit kernel
         spec = {"name": "mab", "graph": {"name": "router", "type": "ROUTER", "implementation": "EPSILON_GREEDY",
                                          "parameters": params,
                                          "children": [{"name": f"m{i}", "type": "MODEL"} for i in range(3)]}}

@@ -125,13 +125,36 @@ def test_tree_lds_staging_matches_global(C_):
                            ([0, 7, 23, 40, 41, 64, 90], 0)):
             b = torch.tensor(begin, dtype=torch.int32, device=dev)
             nc = len(begin) - 1
-            part = torch.empty(nc * rows, dtype=torch.float32, device=dev)
+            part = torch.empty(nc * rows, dtype=torch.float64, device=dev)  # fp64 slab
             C_.kernels.tree_perfect_partial(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0,
                                             b.data_ptr(), nc, rb, part.data_ptr(), _stream(), lds)
             torch.cuda.synchronize()
             outs.append(part.view(nc, rows).double().sum(0))
         torch.testing.assert_close(outs[0], outs[2], rtol=0, atol=0)
         torch.testing.assert_close(outs[1], outs[2], rtol=1e-6, atol=1e-5)
+
+
+def test_tree_scores_do_not_depend_on_the_batch(C_):
+    """The chunk plan follows the batch size; fp64 partial sums of the fp32
+    leaves make every plan add up to the same bits, so a row scores the same
+    alone or inside a 4096-row batch (the bench's sampled reply check relies
+    on it)."""
+    from seldon_core_amd.models import to_row_model
+    from seldon_core_amd.models.trees import synthetic_xgboost
+
+    ens = synthetic_xgboost(1000, 8, 32, seed=4)
+    unit = C_.BatchedUnit(to_row_model(ens), 0, max_batch=4096)
+    try:
+        rng = np.random.default_rng(9)
+        X = rng.normal(size=(4096, 32))
+        big = np.asarray(unit.run(X)).ravel()
+        for i in (0, 1, 777, 4095):
+            alone = np.asarray(unit.run(X[i:i + 1])).ravel()
+            assert alone[0] == big[i]
+        mid = np.asarray(unit.run(X[100:164])).ravel()
+        assert (mid == big[100:164]).all()
+    finally:
+        unit.stop()
 
 
 def test_tree_softmax_groups(C_):

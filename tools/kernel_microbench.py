@@ -61,7 +61,7 @@ def case_tree(iters):
     begin = torch.unique_consecutive(torch.arange(0, T + chunk, chunk, dtype=torch.int32).clamp_(max=T)).cuda()
     nc = begin.numel() - 1
     group = torch.zeros(nc, dtype=torch.int32, device="cuda")
-    partial = torch.empty(nc * rows, dtype=torch.float32, device="cuda")
+    partial = torch.empty(nc * rows, dtype=torch.float64, device="cuda")  # fp64 slab
     out = torch.empty(rows, dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
 

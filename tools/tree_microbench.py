@@ -76,7 +76,7 @@ def main():
             if fused and rows * nc > 4096:
                 continue
             group = torch.zeros(nc, dtype=torch.int32, device=dev)
-            partial = torch.empty(nc * rows, dtype=torch.float32, device=dev)
+            partial = torch.empty(nc * rows, dtype=torch.float64, device=dev)  # fp64 slab
             counter = torch.zeros(64, dtype=torch.int32, device=dev)
             out = torch.empty(rows, dtype=torch.float64, device=dev)
 
