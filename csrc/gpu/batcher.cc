@@ -92,6 +92,8 @@ FaultSpec fault_from_env(int device) {
 
 BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::move(model)), opts_(opts) {
   if (const char* e = std::getenv("SCA_IDLE_SPIN_US")) idle_spin_us_ = std::max(0, std::atoi(e));
+  ho_spin_us_ = idle_spin_us_;
+  if (const char* e = std::getenv("SCA_HANDOFF_SPIN_US")) ho_spin_us_ = std::max(0, std::atoi(e));
   if (opts_.max_batch < 1) opts_.max_batch = 1;
   if (opts_.slots < 1) opts_.slots = 1;
   if (opts_.fail_threshold < 1) opts_.fail_threshold = 1;
@@ -478,12 +480,12 @@ void BatchedUnit::handoff_loop() {
       std::unique_lock<std::mutex> lk(ho_mu_);
       for (auto& h : batch) ho_free_.push_back(std::move(h));  // emptied below: capacity goes back
       batch.clear();
-      if (ho_q_.empty() && !ho_stop_ && idle_spin_us_ > 0) {  // brief spin before sleeping (see device_loop)
+      if (ho_q_.empty() && !ho_stop_ && ho_spin_us_ > 0) {  // brief spin before sleeping (see device_loop)
         lk.unlock();
         SpinPermit permit;
         // (the clock is read every 32 pauses: a vDSO clock_gettime per pause
         // was ~10% of the serving process's CPU with several units spinning)
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(idle_spin_us_);
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(ho_spin_us_);
         for (unsigned n = 1; permit.ok && !ho_pending_.load(std::memory_order_acquire); ++n) {
           _mm_pause();
           if ((n & 31) == 0 && std::chrono::steady_clock::now() >= until) break;

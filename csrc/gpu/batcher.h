@@ -253,6 +253,7 @@ class BatchedUnit : public Unit {
   bool ho_stop_ = false;        // guarded by ho_mu_
   std::atomic<bool> ho_pending_{false};  // ho_q_ non-empty (the hand-off thread's idle spin reads it)
   int idle_spin_us_ = 50;       // spin this long before sleeping when idle (SCA_IDLE_SPIN_US)
+  int ho_spin_us_ = 50;         // the hand-off thread's idle spin (SCA_HANDOFF_SPIN_US, default the same)
   mutable std::mutex stats_mu_;
   BatcherStats stats_;
   // device-thread CPU time (single writer: the device thread; relaxed reads)
