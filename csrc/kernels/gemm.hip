@@ -816,6 +816,77 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// Epilogue of the 256 x 256 kernels: a wave's 128 x 64 block of fp32
+// accumulators (acc[tm][tn], C/D map col = lane & 15, row = (lane >> 4) * 4 +
+// i) plus bias and a compile-time activation, stored as fp32 or bf16.
+template <int ACT, bool OF32>
+__device__ __forceinline__ void epi_256(const DenseGemmArgs& a, const f32x4 (&acc)[8][4], int m0, int n0, int wr,
+                                        int wc, int r16, int kq) {
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) {
+    const int col = n0 + wc * 64 + tn * 16 + r16;
+    const bool live = col < a.N;
+    const bool keep = col < n_store;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 8; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
+        const float v = live ? act_f(acc[tm][tn][i] + bias, ACT) : 0.f;
+        if (keep && row < a.rows_eff) {
+          if constexpr (OF32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+          else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+        }
+      }
+    }
+  }
+}
+// reconstruction-error form: per-row sum of squared differences against xref
+__device__ __forceinline__ void epi_256_mse(const DenseGemmArgs& a, const f32x4 (&acc)[8][4], int m0, int n0, int wr,
+                                         int wc, int r16, int kq) {
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) {
+    const int col = n0 + wc * 64 + tn * 16 + r16;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 8; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
+        const bool ok = live && row < a.rows_eff && col < n_store;
+        const int r = row % a.rows;
+        float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
+        d *= d;
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        d += __shfl_xor(d, 4, 64);
+        d += __shfl_xor(d, 8, 64);
+        if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+      }
+    }
+  }
+}
+
+// one uniform dispatch on (mse, act, output type), outside the element loops
+__device__ __forceinline__ void epi_256_store(const DenseGemmArgs& a, const f32x4 (&acc)[8][4], int m0, int n0,
+                                              int wr, int wc, int r16, int kq) {
+  switch (a.mse ? -1 : a.act * 2 + (a.o_f32 ? 1 : 0)) {
+    case kMlpIdentity * 2 + 1: epi_256<kMlpIdentity, true>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpIdentity * 2: epi_256<kMlpIdentity, false>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpRelu * 2 + 1: epi_256<kMlpRelu, true>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpRelu * 2: epi_256<kMlpRelu, false>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpSigmoid * 2 + 1: epi_256<kMlpSigmoid, true>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpSigmoid * 2: epi_256<kMlpSigmoid, false>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpTanh * 2 + 1: epi_256<kMlpTanh, true>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpTanh * 2: epi_256<kMlpTanh, false>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    default: epi_256_mse(a, acc, m0, n0, wr, wc, r16, kq); break;
+  }
+}
+
 // ---- bf16 GEMM, 256 x 256 tiles, 8-phase ping-pong schedule
 // Same tile and wave layout as gemm_glds256_kernel, but each 64-deep K tile is
 // four phases, one per 64 x 32 quadrant of a wave's 128 x 64 block (16
@@ -847,7 +918,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // in q0 as before; vmcnt(6) in q3 as before.
 // ABL (ablation, paths 7 / 8, timing only -- results are garbage): 1 drops
 // the MFMAs (the fragments are kept live), 2 drops the fragment ds_reads.
-template <bool SPREAD, int ABL = 0>
+// RING (path 9, SPREAD only): the 8 parity buffers become a ring of 10 half
+// tiles (160 KB, all of the CU's LDS), so every half tile is issued >= 5
+// phases before its wait instead of 3 (the no-MFMA ablation showed the
+// loads latency bound, profiles/r03i_gemm_l2).  Half tile p = 4 t + {B0, B1,
+// A0, A1} lives in slot p mod 10, so A of tile t + 2 reuses the B slots of
+// tile t (free after q1) and is issued in q2, B of tile t + 3 reuses A's
+// (free after q2) in q3; the q3 wait leaves the 6 younger half tiles in
+// flight (vmcnt(12)).
+template <bool SPREAD, int ABL = 0, bool RING = false>
 __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
   constexpr int BM = 256, BN = 256, BK = 64, HT = 128 * BK;  // half tile (elements)
   extern __shared__ __attribute__((aligned(16))) __bf16 ring[];  // [parity][A/B][half] x HT
@@ -873,9 +952,16 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
       srcB[hf][j] = W + size_t(min(n0 + hf * 128 + r, a.Np - 1)) * a.Kp + c * 8;
     }
   }
-  auto buf = [&](int par, int op, int hf) { return ring + ((par * 2 + op) * 2 + hf) * HT; };
+  auto buf = [&](int kt, int op, int hf) -> __bf16* {
+    if constexpr (RING) {
+      const int s0 = (4 * (kt % 5)) % 10;  // slot of B0; B1 follows, A0 / A1 after that mod 10
+      return ring + ((op == 1 ? s0 : (s0 + 2) % 10) + hf) * HT;
+    } else {
+      return ring + (((kt & 1) * 2 + op) * 2 + hf) * HT;
+    }
+  };
   auto issue = [&](int kt, int op, int hf) {  // half tile (op 0 = A, 1 = B) of K tile kt
-    __bf16* dst = buf(kt & 1, op, hf);
+    __bf16* dst = buf(kt, op, hf);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds(
@@ -911,12 +997,29 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bq[nh * 2 + j][kk], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  // prologue: tile 0 whole, then B0 / B1 / A0 of tile 1 (3 half tiles may fly)
+  // prologue: tile 0 whole, then B0 / B1 / A0 of tile 1 (3 half tiles may fly);
+  // RING: tiles 0 and 1 whole and B of tile 2 (6 may fly)
   issue(0, 1, 0);
   issue(0, 1, 1);
   issue(0, 0, 0);
   issue(0, 0, 1);
-  if (KT > 1) {
+  if constexpr (RING) {
+    if (KT > 1) {
+      issue(1, 1, 0);
+      issue(1, 1, 1);
+      issue(1, 0, 0);
+      issue(1, 0, 1);
+    }
+    if (KT > 2) {
+      issue(2, 1, 0);
+      issue(2, 1, 1);
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else if (KT > 1) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else if (KT > 1) {
     issue(1, 1, 0);
     issue(1, 1, 1);
     issue(1, 0, 0);
@@ -928,10 +1031,9 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
   const int bh = wc >> 1, bo = (wc & 1) * 64;
   for (int kt = 0; kt < KT && SPREAD; ++kt) {
-    const int par = kt & 1;
-    const __bf16* As = buf(par, 0, wr);
-    const __bf16* Bs = buf(par, 1, bh);
-    // ---- q0: B cols 0-31, then A rows 0-63; A1 of tile kt + 1
+    const __bf16* As = buf(kt, 0, wr);
+    const __bf16* Bs = buf(kt, 1, bh);
+    // ---- q0: B cols 0-31, then A rows 0-63; A1 of tile kt + 1 (RING: nothing)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -942,7 +1044,7 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i) am0[i][kk] = ABL == 2 ? am0[i][kk] : frag(As, i * 16 + r16, kk);
-    if (kt + 1 < KT) issue(kt + 1, 0, 1);
+    if (!RING && kt + 1 < KT) issue(kt + 1, 0, 1);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -964,12 +1066,18 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     // ---- q2: A rows 64-127 (retired before the barrier: A0 is restaged in q3); B0 of tile kt + 2
+    //      (RING: A0 / A1 of tile kt + 2 into this tile's B slots)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i) am1[i][kk] = ABL == 2 ? am0[i][kk] : frag(As, 64 + i * 16 + r16, kk);
-    if (kt + 2 < KT) issue(kt + 2, 1, 0);
+    if (RING && kt + 2 < KT) {
+      issue(kt + 2, 0, 0);
+      issue(kt + 2, 0, 1);
+    } else if (!RING && kt + 2 < KT) {
+      issue(kt + 2, 1, 0);
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -978,8 +1086,19 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     // ---- q3: B1 and A0 of tile kt + 2; tile kt + 1 landed (3 younger half tiles may fly)
+    //      (RING: B0 / B1 of tile kt + 3 into this tile's A slots; 6 younger may fly)
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < KT) {
+    if constexpr (RING) {
+      if (kt + 3 < KT) {
+        issue(kt + 3, 1, 0);
+        issue(kt + 3, 1, 1);
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      } else if (kt + 2 < KT) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else if (kt + 2 < KT) {
       issue(kt + 2, 1, 1);
       issue(kt + 2, 0, 0);
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -994,9 +1113,8 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
     __builtin_amdgcn_s_barrier();
   }
   for (int kt = 0; kt < KT && !SPREAD; ++kt) {
-    const int par = kt & 1;
-    const __bf16* As = buf(par, 0, wr);
-    const __bf16* Bs = buf(par, 1, bh);
+    const __bf16* As = buf(kt, 0, wr);
+    const __bf16* Bs = buf(kt, 1, bh);
     // ---- q0: all of this wave's B fragments, then A rows 0-63; A1 of tile kt + 1
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1055,38 +1173,12 @@ __global__ __launch_bounds__(512) void gemm_8ph_kernel(const DenseGemmArgs a) {
     __builtin_amdgcn_s_barrier();
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
-  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
-  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
-#pragma unroll
-  for (int tn = 0; tn < 4; ++tn) {
-    const int col = n0 + wc * 64 + tn * 16 + r16;
-    const bool live = col < a.N;
-    const float bias = live ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int tm = 0; tm < 8; ++tm) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
-        if (!a.mse) {
-          if (row < a.rows_eff && col < n_store) {
-            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
-            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
-            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
-          }
-        } else {
-          const bool ok = live && row < a.rows_eff && col < n_store;
-          const int r = row % a.rows;
-          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
-          d *= d;
-          d += __shfl_xor(d, 1, 64);
-          d += __shfl_xor(d, 2, 64);
-          d += __shfl_xor(d, 4, 64);
-          d += __shfl_xor(d, 8, 64);
-          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
-        }
-      }
-    }
-  }
+  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i).  The
+  // activation and output type are dispatched once, outside the element
+  // loops: with a per-element switch the tanh / sigmoid code raised register
+  // pressure past the 128 live accumulators and the whole tile went through
+  // 528 B per lane of scratch (2x the output's bytes written per GEMM).
+  epi_256_store(a, acc, m0, n0, wr, wc, r16, kq);
 }
 
 // ---- bf16 GEMM, 256 x 256 tiles, 8 waves, glds double buffer ("2-phase")
@@ -1171,38 +1263,7 @@ __global__ __launch_bounds__(512) void gemm_glds256_kernel(const DenseGemmArgs a
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
-  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
-  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
-#pragma unroll
-  for (int tn = 0; tn < 4; ++tn) {
-    const int col = n0 + wc * 64 + tn * 16 + r16;
-    const bool live = col < a.N;
-    const float bias = live ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int tm = 0; tm < 8; ++tm) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
-        if (!a.mse) {
-          if (row < a.rows_eff && col < n_store) {
-            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
-            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
-            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
-          }
-        } else {
-          const bool ok = live && row < a.rows_eff && col < n_store;
-          const int r = row % a.rows;
-          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
-          d *= d;
-          d += __shfl_xor(d, 1, 64);
-          d += __shfl_xor(d, 2, 64);
-          d += __shfl_xor(d, 4, 64);
-          d += __shfl_xor(d, 8, 64);
-          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
-        }
-      }
-    }
-  }
+  epi_256_store(a, acc, m0, n0, wr, wc, r16, kq);  // (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
 }
 
 template <typename T, int AMODE>
@@ -1251,6 +1312,11 @@ void launch_lds(DenseGemmArgs a, hipStream_t s) {  // by value: the dispatch fil
     if (fits && (a.path == 6 || (a.path == 0 && glds && a.Np >= 256 && tiles256 >= 256))) {
       const size_t lds = size_t(8) * 128 * 64 * sizeof(__bf16);
       hipLaunchKernelGGL(gemm_8ph_kernel<true>, dim3(tiles256), dim3(512), lds, s, a);
+      return;
+    }
+    if (fits && a.path == 9) {  // 10-half-tile ring (160 KB)
+      const size_t lds = size_t(10) * 128 * 64 * sizeof(__bf16);
+      hipLaunchKernelGGL((gemm_8ph_kernel<true, 0, true>), dim3(tiles256), dim3(512), lds, s, a);
       return;
     }
     if (fits && a.path == 4) {

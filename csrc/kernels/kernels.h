@@ -208,7 +208,7 @@ struct DenseGemmArgs {
   const float* xref = nullptr;
   int ldx = 0;
   int group_m = 0;  // glds-family bf16 GEMMs: tile rows per L2 group (0: SCA_GEMM_GROUP_M, default 4; 1 = row-major)
-  int path = 0;  // bf16 plain A: 0 auto, 1 register-staged LDS kernel, 2 glds ring 128^2, 3 glds 256^2, 4 8-phase, 5 4-wave, 6 8-phase spread reads (tests / benches)
+  int path = 0;  // bf16 plain A: 0 auto, 1 register-staged LDS kernel, 2 glds ring 128^2, 3 glds 256^2, 4 8-phase, 5 4-wave, 6 8-phase spread reads, 7 / 8 ablations, 9 8-phase spread + 10-half-tile ring (tests / benches)
 };
 void dense_gemm(const DenseGemmArgs& a, hipStream_t stream);
 // fp64 rows [rows][F] -> bf16 [rows][ld], zero-padded columns

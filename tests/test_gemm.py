@@ -23,7 +23,7 @@ def _pad(x, m):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("rows,K,N", SHAPES)
-@pytest.mark.parametrize("path", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("path", [1, 2, 3, 4, 5, 6, 9])
 @pytest.mark.parametrize("act", [0, 1])
 def test_gemm_bf16_matches_torch(rows, K, N, path, act):
     import torch

@@ -249,7 +249,7 @@ def case_gemm(iters):
         for _ in range(1 if os.environ.get("SCA_PMC") else 2):  # interleaved rounds
             for name, fn in (("reg", lambda: run(1)), ("glds", lambda: run(2)), ("glds256", lambda: run(3)),
                              ("8ph", lambda: run(4)), ("8ph_spread", lambda: run(6)),
-                             ("8ph_spread_bf16out", lambda: run_bf16_out(6)), ("w4", lambda: run(5)),
+                             ("8ph_ring", lambda: run(9)), ("8ph_spread_bf16out", lambda: run_bf16_out(6)), ("w4", lambda: run(5)),
                              ("torch", lib)) + ((("abl_no_mfma", lambda: run(7)), ("abl_no_reads", lambda: run(8)))
                                                 if os.environ.get("GEMM_ABLATE") else ()):
                 fn()
@@ -264,7 +264,7 @@ def case_gemm(iters):
                 res[name] = min(res.get(name, 1e30), us)
         errs = {}
         ref = (A.float() @ W.float().T)
-        for pth, nm in ((3, "glds256"), (4, "8ph"), (6, "8ph_spread"), (5, "w4")):
+        for pth, nm in ((3, "glds256"), (4, "8ph"), (6, "8ph_spread"), (9, "8ph_ring"), (5, "w4")):
             run(pth)
             errs[nm + "_rel_err"] = float((O - ref).abs().max() / ref.abs().max())
         print(json.dumps({"case": "gemm_bf16", "M": rows, "K": K, "N": N,
