@@ -671,6 +671,79 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(const DenseGemmArgs a) {
   }
 }
 
+// Epilogue of the 256 x 256 kernels: a wave's 128 x (16 TN) block of fp32
+// accumulators (acc[tm][tn], C/D map col = lane & 15, row = (lane >> 4) * 4 +
+// i) plus bias and a compile-time activation, stored as fp32 or bf16.
+template <int ACT, bool OF32, int TN>
+__device__ __forceinline__ void epi_256(const DenseGemmArgs& a, const f32x4 (&acc)[8][TN], int m0, int n0, int wr,
+                                        int wc, int r16, int kq) {
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int col = n0 + wc * (16 * TN) + tn * 16 + r16;
+    const bool live = col < a.N;
+    const bool keep = col < n_store;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 8; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
+        const float v = live ? act_f(acc[tm][tn][i] + bias, ACT) : 0.f;
+        if (keep && row < a.rows_eff) {
+          if constexpr (OF32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+          else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+        }
+      }
+    }
+  }
+}
+// reconstruction-error form: per-row sum of squared differences against xref
+template <int TN>
+__device__ __forceinline__ void epi_256_mse(const DenseGemmArgs& a, const f32x4 (&acc)[8][TN], int m0, int n0,
+                                            int wr, int wc, int r16, int kq) {
+  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int col = n0 + wc * (16 * TN) + tn * 16 + r16;
+    const bool live = col < a.N;
+    const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 8; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
+        const bool ok = live && row < a.rows_eff && col < n_store;
+        const int r = row % a.rows;
+        float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
+        d *= d;
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        d += __shfl_xor(d, 4, 64);
+        d += __shfl_xor(d, 8, 64);
+        if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
+      }
+    }
+  }
+}
+
+// one uniform dispatch on (mse, act, output type), outside the element loops
+template <int TN>
+__device__ __forceinline__ void epi_256_store(const DenseGemmArgs& a, const f32x4 (&acc)[8][TN], int m0, int n0,
+                                              int wr, int wc, int r16, int kq) {
+  switch (a.mse ? -1 : a.act * 2 + (a.o_f32 ? 1 : 0)) {
+    case kMlpIdentity * 2 + 1: epi_256<kMlpIdentity, true, TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpIdentity * 2: epi_256<kMlpIdentity, false, TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpRelu * 2 + 1: epi_256<kMlpRelu, true, TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpRelu * 2: epi_256<kMlpRelu, false, TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpSigmoid * 2 + 1: epi_256<kMlpSigmoid, true, TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpSigmoid * 2: epi_256<kMlpSigmoid, false, TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpTanh * 2 + 1: epi_256<kMlpTanh, true, TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    case kMlpTanh * 2: epi_256<kMlpTanh, false, TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+    default: epi_256_mse<TN>(a, acc, m0, n0, wr, wc, r16, kq); break;
+  }
+}
+
 // ---- bf16 GEMM, 256 x 256 tiles, 4 waves of 128 x 128 (one wave per SIMD)
 // The 8-wave kernels read each A / B fragment from LDS 4x / 2x (a wave's
 // 128 x 64 block): 192 KB of ds_read per 64-deep K tile per CU, ~75% of the
@@ -782,109 +855,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
   }
-  // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
-  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
-#pragma unroll
-  for (int tn = 0; tn < 8; ++tn) {
-    const int col = n0 + wc * 128 + tn * 16 + r16;
-    const bool live = col < a.N;
-    const float bias = live ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int tm = 0; tm < 8; ++tm) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
-        if (!a.mse) {
-          if (row < a.rows_eff && col < n_store) {
-            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
-            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
-            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
-          }
-        } else {
-          const bool ok = live && row < a.rows_eff && col < n_store;
-          const int r = row % a.rows;
-          float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
-          d *= d;
-          d += __shfl_xor(d, 1, 64);
-          d += __shfl_xor(d, 2, 64);
-          d += __shfl_xor(d, 4, 64);
-          d += __shfl_xor(d, 8, 64);
-          if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
-        }
-      }
-    }
-  }
-}
-
-// Epilogue of the 256 x 256 kernels: a wave's 128 x 64 block of fp32
-// accumulators (acc[tm][tn], C/D map col = lane & 15, row = (lane >> 4) * 4 +
-// i) plus bias and a compile-time activation, stored as fp32 or bf16.
-template <int ACT, bool OF32>
-__device__ __forceinline__ void epi_256(const DenseGemmArgs& a, const f32x4 (&acc)[8][4], int m0, int n0, int wr,
-                                        int wc, int r16, int kq) {
-  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
-#pragma unroll
-  for (int tn = 0; tn < 4; ++tn) {
-    const int col = n0 + wc * 64 + tn * 16 + r16;
-    const bool live = col < a.N;
-    const bool keep = col < n_store;
-    const float bias = live ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int tm = 0; tm < 8; ++tm) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
-        const float v = live ? act_f(acc[tm][tn][i] + bias, ACT) : 0.f;
-        if (keep && row < a.rows_eff) {
-          if constexpr (OF32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
-          else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
-        }
-      }
-    }
-  }
-}
-// reconstruction-error form: per-row sum of squared differences against xref
-__device__ __forceinline__ void epi_256_mse(const DenseGemmArgs& a, const f32x4 (&acc)[8][4], int m0, int n0, int wr,
-                                         int wc, int r16, int kq) {
-  const int n_store = a.n_store > 0 ? a.n_store : a.Np;
-#pragma unroll
-  for (int tn = 0; tn < 4; ++tn) {
-    const int col = n0 + wc * 64 + tn * 16 + r16;
-    const bool live = col < a.N;
-    const float bias = live ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int tm = 0; tm < 8; ++tm) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wr * 128 + tm * 16 + kq * 4 + i;
-        const bool ok = live && row < a.rows_eff && col < n_store;
-        const int r = row % a.rows;
-        float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
-        d *= d;
-        d += __shfl_xor(d, 1, 64);
-        d += __shfl_xor(d, 2, 64);
-        d += __shfl_xor(d, 4, 64);
-        d += __shfl_xor(d, 8, 64);
-        if (r16 == 0 && row < a.rows_eff) atomicAdd(&a.mse[r], d);
-      }
-    }
-  }
-}
-
-// one uniform dispatch on (mse, act, output type), outside the element loops
-__device__ __forceinline__ void epi_256_store(const DenseGemmArgs& a, const f32x4 (&acc)[8][4], int m0, int n0,
-                                              int wr, int wc, int r16, int kq) {
-  switch (a.mse ? -1 : a.act * 2 + (a.o_f32 ? 1 : 0)) {
-    case kMlpIdentity * 2 + 1: epi_256<kMlpIdentity, true>(a, acc, m0, n0, wr, wc, r16, kq); break;
-    case kMlpIdentity * 2: epi_256<kMlpIdentity, false>(a, acc, m0, n0, wr, wc, r16, kq); break;
-    case kMlpRelu * 2 + 1: epi_256<kMlpRelu, true>(a, acc, m0, n0, wr, wc, r16, kq); break;
-    case kMlpRelu * 2: epi_256<kMlpRelu, false>(a, acc, m0, n0, wr, wc, r16, kq); break;
-    case kMlpSigmoid * 2 + 1: epi_256<kMlpSigmoid, true>(a, acc, m0, n0, wr, wc, r16, kq); break;
-    case kMlpSigmoid * 2: epi_256<kMlpSigmoid, false>(a, acc, m0, n0, wr, wc, r16, kq); break;
-    case kMlpTanh * 2 + 1: epi_256<kMlpTanh, true>(a, acc, m0, n0, wr, wc, r16, kq); break;
-    case kMlpTanh * 2: epi_256<kMlpTanh, false>(a, acc, m0, n0, wr, wc, r16, kq); break;
-    default: epi_256_mse(a, acc, m0, n0, wr, wc, r16, kq); break;
-  }
+  epi_256_store(a, acc, m0, n0, wr, wc, r16, kq);  // (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
 }
 
 // ---- bf16 GEMM, 256 x 256 tiles, 8-phase ping-pong schedule
