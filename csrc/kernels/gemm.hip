@@ -678,6 +678,28 @@ template <int ACT, bool OF32, int TN>
 __device__ __forceinline__ void epi_256(const DenseGemmArgs& a, const f32x4 (&acc)[8][TN], int m0, int n0, int wr,
                                         int wc, int r16, int kq) {
   const int n_store = a.n_store > 0 ? a.n_store : a.Np;
+  if (m0 + 256 <= a.rows_eff && n0 + 256 <= min(n_store, a.N)) {
+    // interior tile (every tile of a large GEMM): no per-element predicates,
+    // one row pointer per (tm, i) and the column tiles as immediate offsets
+    const int col0 = n0 + wc * (16 * TN) + r16;
+    float bias[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) bias[tn] = a.bias[col0 + tn * 16];
+#pragma unroll
+    for (int tm = 0; tm < 8; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const size_t off = size_t(m0 + wr * 128 + tm * 16 + kq * 4 + i) * a.ldo + col0;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const float v = act_f(acc[tm][tn][i] + bias[tn], ACT);
+          if constexpr (OF32) static_cast<float*>(a.O)[off + tn * 16] = v;
+          else static_cast<__bf16*>(a.O)[off + tn * 16] = __bf16(v);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int col = n0 + wc * (16 * TN) + tn * 16 + r16;
