@@ -36,6 +36,23 @@ __device__ __forceinline__ float act_f(float v, int a) {
   }
 }
 
+// Calls f(integral_constant<int, ACT>, integral_constant<bool, OF32>) for the
+// runtime activation / output type: epilogues branch once, not per element.
+template <class F>
+__device__ __forceinline__ void act_dispatch(int act, bool of32, F&& f) {
+  using std::integral_constant;
+  switch (act * 2 + (of32 ? 1 : 0)) {
+    case kMlpRelu * 2 + 1: f(integral_constant<int, kMlpRelu>{}, integral_constant<bool, true>{}); break;
+    case kMlpRelu * 2: f(integral_constant<int, kMlpRelu>{}, integral_constant<bool, false>{}); break;
+    case kMlpSigmoid * 2 + 1: f(integral_constant<int, kMlpSigmoid>{}, integral_constant<bool, true>{}); break;
+    case kMlpSigmoid * 2: f(integral_constant<int, kMlpSigmoid>{}, integral_constant<bool, false>{}); break;
+    case kMlpTanh * 2 + 1: f(integral_constant<int, kMlpTanh>{}, integral_constant<bool, true>{}); break;
+    case kMlpTanh * 2: f(integral_constant<int, kMlpTanh>{}, integral_constant<bool, false>{}); break;
+    case kMlpIdentity * 2 + 1: f(integral_constant<int, kMlpIdentity>{}, integral_constant<bool, true>{}); break;
+    default: f(integral_constant<int, kMlpIdentity>{}, integral_constant<bool, false>{}); break;
+  }
+}
+
 // VAE reparameterised input value z[row][k] (same Philox streams as the fused
 // kernel's reparam() and mlp_layer's AMODE 2)
 __device__ __forceinline__ float reparam_z(const DenseGemmArgs& a, int row, int k) {
@@ -486,6 +503,31 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
   }
   const int n_store = a.n_store > 0 ? a.n_store : a.Np;
   if constexpr (M32) {  // C/D map of 32x32: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+    if (!a.mse) {
+      act_dispatch(a.act, a.o_f32, [&](auto actc, auto of32c) {
+        constexpr int ACT = decltype(actc)::value;
+        constexpr bool OF32 = decltype(of32c)::value;
+#pragma unroll
+        for (int u = 0; u < TN32; ++u) {
+          const int col = n0 + wc * WCOLS + u * 32 + (lane & 31);
+          const bool live = col < a.N, store = col < n_store;
+          const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+          for (int t = 0; t < TM32; ++t) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int row = m0 + wr * (BM / 2) + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+              const float v = live ? act_f(acc32[t][u][i] + bias, ACT) : 0.f;
+              if (store && row < a.rows_eff) {
+                if constexpr (OF32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+                else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+              }
+            }
+          }
+        }
+      });
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < TN32; ++u) {
       const int col = n0 + wc * WCOLS + u * 32 + (lane & 31);
@@ -497,12 +539,7 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
         for (int i = 0; i < 16; ++i) {
           const int row = m0 + wr * (BM / 2) + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
           const float v = live ? act_f(acc32[t][u][i] + bias, a.act) : 0.f;
-          if (!a.mse) {
-            if (store && row < a.rows_eff) {
-              if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
-              else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
-            }
-          } else {  // the 32 lanes of a half hold one row's 32 columns: sum them, one atomic per row
+          {  // the 32 lanes of a half hold one row's 32 columns: sum them, one atomic per row
             const bool ok = live && store && row < a.rows_eff;
             const int r = row % a.rows;
             float d = ok ? v - a.xref[size_t(r) * a.ldx + col] : 0.f;
@@ -516,6 +553,32 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
     }
     return;
   }
+  if (!a.mse) {
+    act_dispatch(a.act, a.o_f32, [&](auto actc, auto of32c) {
+      constexpr int ACT = decltype(actc)::value;
+      constexpr bool OF32 = decltype(of32c)::value;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int col = n0 + wc * 32 + tn * 16 + r16;
+        if (col >= n_store) continue;
+        const bool live = col < a.N;
+        const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = m0 + wr * (BM / 2) + tm * 16 + kq * 4 + i;
+            if (row < a.rows_eff) {
+              const float v = live ? act_f(acc[tm][tn][i] + bias, ACT) : 0.f;
+              if constexpr (OF32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+              else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+            }
+          }
+        }
+      }
+    });
+    return;
+  }
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int col = n0 + wc * 32 + tn * 16 + r16;
@@ -527,13 +590,7 @@ __global__ __launch_bounds__(NT) void gemm_lds_kernel(const DenseGemmArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + wr * (BM / 2) + tm * 16 + kq * 4 + i;
-        if (!a.mse) {
-          if (row < a.rows_eff) {
-            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
-            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
-            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
-          }
-        } else {
+        {
           const bool ok = live && row < a.rows_eff;
           const int r = row % a.rows;
           float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
