@@ -151,6 +151,33 @@ __global__ __launch_bounds__(64) void dense_gemm_kernel(const DenseGemmArgs a) {
     for (int tn = 0; tn < TN; ++tn) bv[tn] = bn[tn];
   }
   // ---- epilogue (C/D map: col = lane & 15, row = (lane >> 4) * 4 + i)
+  if (!a.mse) {
+    act_dispatch(a.act, a.o_f32, [&](auto actc, auto of32c) {
+      constexpr int ACT = decltype(actc)::value;
+      constexpr bool OF32 = decltype(of32c)::value;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int t = t0 + tn;
+        if (t >= ntiles) break;
+        const int col = t * 16 + r16;
+        const bool live = col < a.N;
+        const float bias = live ? a.bias[col] : 0.f;
+#pragma unroll
+        for (int tm = 0; tm < kTM; ++tm) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = m0 + 16 * tm + kq * 4 + i;
+            if (row < a.rows_eff) {
+              const float v = live ? act_f(acc[tm][tn][i] + bias, ACT) : 0.f;
+              if constexpr (OF32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
+              else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
+            }
+          }
+        }
+      }
+    });
+    return;
+  }
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int t = t0 + tn;
@@ -163,13 +190,7 @@ __global__ __launch_bounds__(64) void dense_gemm_kernel(const DenseGemmArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * tm + kq * 4 + i;
-        if (!a.mse) {
-          if (row < a.rows_eff) {
-            const float v = live ? act_f(acc[tm][tn][i] + bias, a.act) : 0.f;
-            if (a.o_f32) static_cast<float*>(a.O)[size_t(row) * a.ldo + col] = v;
-            else static_cast<__bf16*>(a.O)[size_t(row) * a.ldo + col] = __bf16(v);
-          }
-        } else {
+        {
           const bool ok = live && row < a.rows_eff;
           const int r = row % a.rows;
           float d = ok ? act_f(acc[tm][tn][i] + bias, a.act) - a.xref[size_t(r) * a.ldx + col] : 0.f;
