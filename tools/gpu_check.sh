@@ -36,10 +36,12 @@ for s in $STEPS; do
     bench_mab) run bench_mab 300 python bench.py --graph mab --steps 5 ;;
     prof)
       export TMPDIR=/tmp
+      export SCA_BENCH_CLEAN_EXIT=1  # bench.py ends with os._exit otherwise: rocprofv3 would write nothing
       run prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
         python3 bench.py --steps 3 --warmup 1 --step-requests 20000 ;;
     prof_xgb)
       export TMPDIR=/tmp
+      export SCA_BENCH_CLEAN_EXIT=1
       run prof_xgb 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_xgb" -o run --output-format csv -- \
         python3 bench.py --model xgb1000 --steps 3 --warmup 1 --step-requests 10000 ;;
     lstm) run lstm 300 python tools/kernel_microbench.py --only lstm --iters 20 ;;
