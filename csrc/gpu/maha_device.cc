@@ -1,3 +1,4 @@
+#include <cstdlib>
 #include "maha_device.h"
 
 #include <algorithm>
@@ -19,6 +20,7 @@ kern::MahaParams make_params(int p, int k, double n_stdev, double start_clip, do
   prm.start_clip = start_clip;
   prm.max_n = max_n;
   prm.eps = eps;
+  if (const char* v = std::getenv("SCA_MAHA_MW_MIN_P")) prm.mw_min_p = std::atoi(v);
   return prm;
 }
 

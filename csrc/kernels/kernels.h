@@ -234,6 +234,11 @@ struct MahaParams {
   double n_stdev = 3.0, start_clip = 50.0, max_n = -1.0, eps = 1e-8;
   int out_mode = 0;        // 0: scores, 1: predictions (score > threshold ? 1 : 0)
   double threshold = 25.0;
+  // the 256-thread kernel splits the tridiagonalisation's per-column sweep
+  // over its 4 waves from this p on (SCA_MAHA_MW_MIN_P; > 64 = never).
+  // Measured: p = 64 87.0 -> 74.9 us, p = 32 30.5 -> 32.3 us, p = 20 16.1 ->
+  // 19.8 us (the two barriers per column cost more than a short sweep saves)
+  int mw_min_p = 48;
 };
 // state layout (doubles): mean[p] | C[p*p] | clip_lo[p] | clip_hi[p] | n | c_zero | has_clip
 inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }

@@ -291,6 +291,7 @@ struct EigScratch {
   double dg[kMahaMaxP + 8], eo[kMahaMaxP + 8];   // tridiagonal T
   double sd[kMahaMaxP + 16], se2[kMahaMaxP + 16];  // T / 2^E, squared off-diagonal / 2^2E (Sturm counts; a block read ahead)
   double lam[kMahaMaxK];
+  double part[3][64];  // multi-wave tridiagonalisation: waves 1-3's partial (A v)_g
 };
 
 // Top-k eigenpairs of the symmetric p x p matrix in A (LDS, stride kLd;
@@ -318,13 +319,22 @@ struct EigScratch {
 //  4. back-transformation through the reflectors, all k vectors per step.
 // Wr: reflectors (row j = reflector j, indexed by global row).  Output:
 // eigenvectors in V[:, 0..k-1], sel[a] = a.
+//
+// nw = 4 (the 256-thread kernel, p >= MahaParams::mw_min_p): every thread
+// calls this; waves 1-3 take part only in step 1's per-column sweep (a share
+// of the 8-column blocks of every row, partial products through LDS, two
+// workgroup barriers per column) and return before step 2.
 __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ Wr, EigScratch& es,
-                          int* sel, int p, int k, uint64_t* ph) {
-  const int lane = threadIdx.x & 63;
+                          int* sel, int p, int k, uint64_t* ph, int nw) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool inp = lane < p;
   uint64_t t_prev = __builtin_amdgcn_s_memrealtime();
-  auto mark = [&](int i) {  // sub-phase timer (lane 0): ph[i] of the caller's phase array
-    if (lane == 0) {
+  auto col_sync = [&] {  // the sweep's data (rn, rv, other waves' columns) visible to every participating wave
+    if (nw > 1) __syncthreads();
+    else wave_lds_sync();
+  };
+  auto mark = [&](int i) {  // sub-phase timer (thread 0): ph[i] of the caller's phase array
+    if (threadIdx.x == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
       ph[i] += t - t_prev;
       t_prev = t;
@@ -355,6 +365,7 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
   };
   // zero padding: columns p..p+7 of every active row, reflector slots past p;
   // Sturm pads (d = 4 > any scaled shift, e^2 = 0) add no sign change
+  if (wv == 0) {
   if (inp)
     for (int c = p; c < kMahaMaxP + 8; ++c) arow[c] = 0.0;
   for (int c = p + lane; c < kMahaMaxP + 8; c += 64) {
@@ -369,11 +380,13 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
     dg[1] = A[kLdA + 1];
     eo[0] = A[kLdA];
   }
+  }  // wv == 0
   if (p >= 3) {
-    double vg = reflect(0, lane >= 1 && inp ? arow[0] : 0.0);
-    double col = lane >= 1 && inp ? arow[1] : 0.0;  // this row's entry of the next column
+    double vg = 0.0, col = 0.0, pv = 0.0, K = 0.0, wg = 0.0;
+    if (wv == 0) {
+    vg = reflect(0, lane >= 1 && inp ? arow[0] : 0.0);
+    col = lane >= 1 && inp ? arow[1] : 0.0;  // this row's entry of the next column
     wave_lds_sync();
-    double pv = 0.0;
     if (lane >= 1 && inp) {
       double s[4] = {0.0, 0.0, 0.0, 0.0};
       for (int cb = 1; cb < p; cb += 8) {
@@ -388,27 +401,40 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
       }
       pv = (s[0] + s[1]) + (s[2] + s[3]);
     }
-    double K = wave_sum(vg * pv);
-    double wg = 2.0 * pv - 2.0 * K * vg;
+    K = wave_sum(vg * pv);
+    wg = 2.0 * pv - 2.0 * K * vg;
     if (inp) es.rv[lane] = make_double2(vg, wg);
     wave_lds_sync();
+    }  // wv == 0
     for (int j = 0; j + 2 < p; ++j) {
       // column j + 1 after update j (lane j + 1: the new diagonal entry)
-      const double vj1 = readlane64(vg, j + 1), wj1 = readlane64(wg, j + 1);
-      const double x = lane > j && inp ? col - (vg * wj1 + wg * vj1) : 0.0;
-      if (lane == j + 1) dg[j + 1] = x;
+      double x = 0.0, vn = 0.0;
+      if (wv == 0) {
+        const double vj1 = readlane64(vg, j + 1), wj1 = readlane64(wg, j + 1);
+        x = lane > j && inp ? col - (vg * wj1 + wg * vj1) : 0.0;
+        if (lane == j + 1) dg[j + 1] = x;
+        if (j + 3 < p) vn = reflect(j + 1, lane > j + 1 ? x : 0.0);
+      }
       if (j + 3 < p) {
-        const double vn = reflect(j + 1, lane > j + 1 ? x : 0.0);
-        wave_lds_sync();
+        col_sync();
         // fused pass over columns j+2..p-1 of rows j+2..p-1: update j, then
-        // (A v_{j+1}) with the updated entries
+        // (A v_{j+1}) with the updated entries; wave wv takes 8-column blocks
+        // [ceil(wv nb / nw), ceil((wv + 1) nb / nw)), so wave 0 always owns
+        // column j + 2 (the next x)
+        const int c0 = j + 2, nb = (p - c0 + 7) >> 3;
+        const int cb0 = c0 + 8 * ((wv * nb + nw - 1) / nw), cb1 = c0 + 8 * (((wv + 1) * nb + nw - 1) / nw);
+        double rvg = vg, rwg = wg;
+        if (wv != 0) {
+          const double2 r = es.rv[lane];
+          rvg = r.x;
+          rwg = r.y;
+        }
         pv = 0.0;
         if (lane > j + 1 && inp) {
           double s[4] = {0.0, 0.0, 0.0, 0.0};
-          const int c0 = j + 2;
           // (a single wave is VALU-issue bound here, ~3 f64 ops per entry:
           // reading the next block ahead measured slower, not faster)
-          for (int cb = c0; cb < p; cb += 8) {
+          for (int cb = cb0; cb < cb1; cb += 8) {
             double av[8], nv[8];
             double2 rw[8];
 #pragma unroll
@@ -419,26 +445,34 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {  // past p: 0 - 0 written back to the row's own padding
-              const double a = fma(-wg, rw[u].x, fma(-vg, rw[u].y, av[u]));
+              const double a = fma(-rwg, rw[u].x, fma(-rvg, rw[u].y, av[u]));
               arow[cb + u] = a;
               s[u & 3] = fma(a, nv[u], s[u & 3]);
             }
-            if (cb == c0) col = fma(-wg, rw[0].x, fma(-vg, rw[0].y, av[0]));
+            if (cb == c0) col = fma(-rwg, rw[0].x, fma(-rvg, rw[0].y, av[0]));
           }
           pv = (s[0] + s[1]) + (s[2] + s[3]);
         }
-        K = wave_sum(vn * pv);
-        vg = vn;
-        wg = 2.0 * pv - 2.0 * K * vn;
-        wave_lds_sync();
-        if (inp) es.rv[lane] = make_double2(vg, wg);
-        wave_lds_sync();
-      } else if (lane == p - 1) {  // j = p - 3: the trailing 2 x 2 block
+        if (nw > 1) {
+          if (wv != 0) es.part[wv - 1][lane] = pv;
+          __syncthreads();
+          if (wv == 0) pv += (es.part[0][lane] + es.part[1][lane]) + es.part[2][lane];
+        }
+        if (wv == 0) {
+          K = wave_sum(vn * pv);
+          vg = vn;
+          wg = 2.0 * pv - 2.0 * K * vn;
+          wave_lds_sync();
+          if (inp) es.rv[lane] = make_double2(vg, wg);
+          wave_lds_sync();
+        }
+      } else if (wv == 0 && lane == p - 1) {  // j = p - 3: the trailing 2 x 2 block
         eo[p - 2] = x;
         dg[p - 1] = arow[p - 1] - 2.0 * vg * wg;
       }
     }
   }
+  if (wv != 0) return;  // steps 2-4 are wave 0's
   wave_lds_sync();
   // ---- 2. k largest eigenvalues: Gershgorin bracket, multisection in k lane groups
   const double di = inp ? dg[lane] : 0.0;
@@ -819,7 +853,8 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   __syncthreads();
   stamp(1);
   const uint64_t c_eig0 = __builtin_amdgcn_s_memtime(), r_eig0 = __builtin_amdgcn_s_memrealtime();
-  if (tid < 64) topk_wave(A, V, W, es, sel, p, k, ph);
+  if (NT >= 256 && p >= prm.mw_min_p) topk_wave(A, V, W, es, sel, p, k, ph, 4);
+  else if (tid < 64) topk_wave(A, V, W, es, sel, p, k, ph, 1);
   __syncthreads();
   stamp(3);
   if (tid == 0) {  // shader-clock cycles and 100 MHz ticks of the eigen phase (effective clock)
