@@ -56,9 +56,11 @@ def _private_include() -> Path:
     inc = BUILD / "include"
     inc.mkdir(parents=True, exist_ok=True)
     link = inc / "nghttp2"
-    if not link.exists():
-        if NGHTTP2_INC.exists():
+    if not link.exists() and NGHTTP2_INC.exists():
+        try:  # the compile pool's threads race here on a fresh tree
             link.symlink_to(NGHTTP2_INC)
+        except FileExistsError:
+            pass
     return inc
 
 
