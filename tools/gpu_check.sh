@@ -30,10 +30,11 @@ for s in $STEPS; do
     smoke) run smoke 180 python __graft_entry__.py smoke ;;
     bench) run bench 400 python bench.py --extra-grpc ;;
     bench_grpc) run bench_grpc 400 python bench.py --api grpc ;;
-    bench_xgb) run bench_xgb 400 python bench.py --model xgb1000 --step-requests 20000 ;;
+    bench_xgb) run bench_xgb 400 python bench.py --model xgb1000 ;;  # calibrated step size (>= 4 s window)
     bench_abtest) run bench_abtest 300 python bench.py --graph abtest --steps 5 ;;
     bench_pipeline) run bench_pipeline 300 python bench.py --graph pipeline --steps 5 ;;
     bench_mab) run bench_mab 300 python bench.py --graph mab --steps 5 ;;
+    bench_replicas) run bench_replicas 300 python bench.py --graph replicas --steps 5 ;;
     prof)
       export TMPDIR=/tmp
       export SCA_BENCH_CLEAN_EXIT=1  # bench.py ends with os._exit otherwise: rocprofv3 would write nothing
