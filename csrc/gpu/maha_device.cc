@@ -1,8 +1,8 @@
-#include <cstdlib>
 #include "maha_device.h"
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace sca::gpu {
