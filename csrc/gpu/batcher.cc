@@ -27,14 +27,16 @@ namespace {
 // Idle-spin permits shared by every unit of the process: a graph with
 // several units (A/B, MAB replicas) otherwise keeps a device and a hand-off
 // thread per unit spinning on the CPU share the front end needs (2 CPUs of
-// 12 in the MAB profile).  SCA_MAX_SPINNERS, default 4: at 2 the MAB graph
+// 12 in the MAB profile).  SCA_MAX_SPINNERS, default 16: at 2 the MAB graph
 // served the same 0.78-0.80M pred/s on 11.0-11.4 instead of 12.3-12.5 server
-// CPUs, single / A/B graphs within noise (profiles/r03h_frontend_fp32).
+// CPUs (profiles/r03h_frontend_fp32); at HEAD, 16 over 4 permits serves
+// +3-10% on A/B (p99 1.62 vs 1.76-1.84 ms) and +2-4% on MAB, two interleaved
+// repetitions each (profiles/r03r_head/spin_ab).
 std::atomic<int> g_spinners{0};
 int max_spinners() {
   static const int m = [] {
     const char* e = std::getenv("SCA_MAX_SPINNERS");
-    return e ? std::max(0, std::atoi(e)) : 4;
+    return e ? std::max(0, std::atoi(e)) : 16;
   }();
   return m;
 }
