@@ -483,6 +483,25 @@ def run_loadgen(port: int, steps: int, warmup: int, api: str, body, users: int, 
     return out
 
 
+def probe_rate(port: int, api: str, body, users: int, threads: int, timeout_fn, min_s: float = 0.5,
+               expect=None) -> float:
+    """Steady-state request rate of a server: a short warm probe, then one
+    step sized to last about `min_s` at the short probe's rate (a one-step
+    probe of a few thousand requests reads about half the steady rate).
+    `timeout_fn()` gives each loadgen call's timeout."""
+    first = run_loadgen(port, 1, 1, api, body, users, threads, max(2000, users * 16), timeout_fn(), expect=expect)
+    r1 = float(first["rps"])
+    second = run_loadgen(port, 1, 0, api, body, users, threads, int(max(2000, r1 * min_s)), timeout_fn(),
+                         expect=expect)
+    return max(r1, float(second["rps"]))
+
+
+def window_requests(rate: float, window_s: float, steps: int = 2) -> int:
+    """Requests per step so `steps` steps at `rate` fill `window_s` (10%
+    headroom: the rate is a probe's, the window a floor)."""
+    return int(max(2000, 1.1 * rate * window_s / max(1, steps)))
+
+
 def step_spread(step_ms: List[float]) -> Dict[str, float]:
     if not step_ms:
         return {}
