@@ -221,7 +221,7 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("W"), py::arg("b"), py::arg("act"));
   // stages: list of dicts {kind: "model"|"mean", model?, device, inputs: [int], node}
-  m.def("graph_model", [](py::list stages, int in_cols) {
+  m.def("graph_model", [](py::list stages, int in_cols, bool split_streams) {
     std::vector<gpu::GraphStage> st;
     for (auto h : stages) {
       py::dict d = h.cast<py::dict>();
@@ -234,12 +234,24 @@ PYBIND11_MODULE(_C, m) {
       s.node = d.contains("node") ? d["node"].cast<std::string>() : std::string();
       st.push_back(std::move(s));
     }
-    return std::static_pointer_cast<gpu::RowModel>(std::make_shared<gpu::GraphModel>(std::move(st), in_cols));
-  }, py::arg("stages"), py::arg("in_cols") = 0);
+    auto g = std::make_shared<gpu::GraphModel>(std::move(st), in_cols);
+    if (split_streams) g->set_split(true);
+    return std::static_pointer_cast<gpu::RowModel>(g);
+  }, py::arg("stages"), py::arg("in_cols") = 0, py::arg("split_streams") = false);
   m.def("graph_devices", [](std::shared_ptr<gpu::RowModel> m) {
     auto g = std::dynamic_pointer_cast<gpu::GraphModel>(m);
     if (!g) throw std::runtime_error("not a graph model");
     return g->devices();
+  });
+  m.def("graph_info", [](std::shared_ptr<gpu::RowModel> m) {
+    auto g = std::dynamic_pointer_cast<gpu::GraphModel>(m);
+    if (!g) throw std::runtime_error("not a graph model");
+    py::dict d;
+    d["devices"] = g->devices();
+    d["split"] = g->split();
+    d["peer_direct"] = g->peer_direct();
+    d["stages"] = int(g->stages().size());
+    return d;
   });
   auto to_layers = [](py::list ls) {
     std::vector<gpu::DenseLayer> out;
@@ -488,6 +500,7 @@ PYBIND11_MODULE(_C, m) {
            },
            py::arg("fail_after") = -1, py::arg("fail_count") = -1, py::arg("hang_ms") = 0)
       .def_property_readonly("ready", &gpu::BatchedUnit::ready)
+      .def_property_readonly("model", &gpu::BatchedUnit::model)
       .def("run", [](gpu::BatchedUnit& u, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
         if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
         const int rows = int(X.shape(0)), cols = int(X.shape(1));
@@ -565,15 +578,24 @@ PYBIND11_MODULE(_C, m) {
       });
 
   // ------------------------------------------------------- RCCL fabric
-  m.def("rccl_unique_id", [] { return py::bytes(par::rccl_unique_id()); });
+  m.def("rccl_unique_ids", [](int world) { return py::bytes(par::rccl_unique_ids(world)); }, py::arg("world"));
+  py::class_<par::LoopbackHub, std::shared_ptr<par::LoopbackHub>>(m, "LoopbackHub")
+      .def(py::init<int>(), py::arg("device"))
+      .def_property_readonly("device", &par::LoopbackHub::device)
+      .def_property_readonly("messages", &par::LoopbackHub::messages)
+      .def_property_readonly("staging_buffers", &par::LoopbackHub::staging_buffers)
+      .def_property_readonly("matched_immediately", &par::LoopbackHub::matched_immediately);
   py::class_<par::Fabric, std::shared_ptr<par::Fabric>>(m, "Fabric")
-      .def(py::init([](int rank, int world, const py::bytes& uid, int device, std::vector<int> ctrl_fds) {
+      .def(py::init([](int rank, int world, const py::bytes& uid, int device, std::vector<int> ctrl_fds,
+                       std::shared_ptr<par::LoopbackHub> hub) {
              std::string id(uid);
              py::gil_scoped_release nogil;  // collective: blocks until every rank joins
-             return std::make_shared<par::Fabric>(rank, world, id, device, std::move(ctrl_fds));
+             return std::make_shared<par::Fabric>(rank, world, id, device, std::move(ctrl_fds), std::move(hub));
            }),
-           py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"), py::arg("ctrl_fds"))
+           py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"), py::arg("ctrl_fds"),
+           py::arg("hub") = nullptr)
       .def_property_readonly("gpu", &par::Fabric::gpu)
+      .def_property_readonly("transport", &par::Fabric::transport)
       .def_property_readonly("rank", &par::Fabric::rank)
       .def_property_readonly("world", &par::Fabric::world)
       .def_property_readonly("device", &par::Fabric::device)

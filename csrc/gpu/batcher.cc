@@ -352,6 +352,23 @@ bool BatchedUnit::launch(Slot* s) {
     s->t_launch = std::chrono::steady_clock::now();
     try {
       s->cpu_out.assign(size_t(rows) * s->out_cols, 0.0);
+      if (!segmented_) {
+        // Models that compute elsewhere (a peer rank) take the whole batch as
+        // one asynchronous call: up to `slots` batches stay outstanding and the
+        // reap loop below polls them like GPU events.
+        const double* x = s->items.front().xp;
+        if (s->items.size() > 1) {
+          s->cpu_in.resize(size_t(rows) * cols);
+          size_t off = 0;
+          for (const auto& it : s->items) {
+            std::memcpy(s->cpu_in.data() + off, it.xp, size_t(it.rows) * cols * sizeof(double));
+            off += size_t(it.rows) * cols;
+          }
+          x = s->cpu_in.data();
+        }
+        s->call = model_->start_cpu(x, rows, cols, s->cpu_out.data());
+        if (s->call) return true;
+      }
       size_t row = 0;
       for (const auto& it : s->items) {
         model_->run_cpu(it.xp, it.rows, cols, s->cpu_out.data() + row * s->out_cols);
@@ -564,6 +581,12 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
   }
   batch_hist_.observe(busy);
   rows_hist_.observe(double(s->rows) * 1e-6);
+  std::string call_err;
+  if (s->call) {
+    call_err = s->call->error();
+    s->call.reset();
+    if (!call_err.empty() && st == hipSuccess) st = hipErrorUnknown;
+  }
   if (s->abandoned) {  // the watchdog already answered these requests
     s->abandoned = false;
     abandoned_slots_.fetch_sub(1, std::memory_order_relaxed);
@@ -579,7 +602,9 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
   std::vector<Item>& items = s->items;  // cleared below; the slot keeps the capacity
   const size_t n_items = items.size();
   if (st != hipSuccess) {
-    auto e = device_error(ApiError::EXECUTION_FAILURE, std::string("GPU execution failed: ") + hipGetErrorString(st));
+    auto e = call_err.empty()
+                 ? device_error(ApiError::EXECUTION_FAILURE, std::string("GPU execution failed: ") + hipGetErrorString(st))
+                 : make_error(ApiError::EXECUTION_FAILURE, "CPU model failed: " + call_err);
     note_failure();
     for (auto& it : items) it.k(Outcome::fail(e));
   } else {
@@ -708,7 +733,7 @@ void BatchedUnit::device_loop() {
     const bool watch = opts_.hang_timeout_ms > 0 && (spins >= 512 || (spins & 31) == 0);  // every poll once yielding
     for (size_t i = 0; i < inflight.size();) {
       Slot* s = inflight[i];
-      hipError_t st = cpu_ ? hipSuccess : hipEventQuery(s->ev.get());
+      hipError_t st = cpu_ ? (!s->call || s->call->done() ? hipSuccess : hipErrorNotReady) : hipEventQuery(s->ev.get());
       if (st == hipSuccess && hang_ms > 0 && now_() - s->t_launch < std::chrono::milliseconds(hang_ms))
         st = hipErrorNotReady;  // injected slow / hung device
       if (st == hipErrorNotReady) {
@@ -766,8 +791,23 @@ void BatchedUnit::device_loop() {
       std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
-  // Shutdown: finish (and answer) everything already launched.
-  for (Slot* s : inflight) complete(s, cpu_ ? hipSuccess : hipEventSynchronize(s->ev.get()));
+  // Shutdown: finish (and answer) everything already launched.  An
+  // asynchronous CPU call gets a bounded wait (it owns its buffers, so one
+  // that never finishes is dropped safely and its requests fail).
+  for (Slot* s : inflight) {
+    hipError_t st = hipSuccess;
+    if (!cpu_) {
+      st = hipEventSynchronize(s->ev.get());
+    } else if (s->call) {
+      const auto until = clk::now() + std::chrono::seconds(10);
+      while (!s->call->done() && clk::now() < until) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      if (!s->call->done()) {
+        s->call.reset();
+        st = hipErrorNotReady;
+      }
+    }
+    complete(s, st);
+  }
 }
 
 ErrPtr BatchedUnit::device_error(ApiError kind, std::string info) {

@@ -143,6 +143,8 @@ class BatchedUnit : public Unit {
   struct Slot {
     PinnedBuffer h_in, h_out, h_seg;
     std::vector<double> cpu_out;  // device -1 (cpu_batching)
+    std::vector<double> cpu_in;   // device -1, asynchronous models: the batch's rows back to back
+    CpuCallPtr call;              // device -1: the batch's outstanding start_cpu() call
     DeviceBuffer d_in, d_out, ws;
     Stream stream;
     Event ev;

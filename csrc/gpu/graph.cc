@@ -1,6 +1,7 @@
 #include "graph.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <set>
 #include <stdexcept>
 
@@ -14,7 +15,7 @@ struct GraphModel::Aux {
   std::vector<DeviceBuffer> ws;                   // per stage model workspace
   std::vector<std::vector<DeviceBuffer>> staged;  // non-peer mode: consumer-local copies of inputs
   std::vector<PinnedBuffer> ptrs;                 // mean stages: device-visible input pointer arrays
-  std::map<int, Stream> streams;                  // per non-root GPU
+  std::map<int, Stream> streams;                  // per non-root lane (GPU, or stage in split mode)
   std::vector<Event> ev;                          // per stage, recorded on the stage's stream
   Event ev_start;                                 // root stream: inputs staged
 };
@@ -23,6 +24,7 @@ GraphModel::~GraphModel() = default;
 
 GraphModel::GraphModel(std::vector<GraphStage> stages, int in_cols) : st_(std::move(stages)), in_cols_(in_cols) {
   if (st_.empty()) throw std::runtime_error("GraphModel: no stages");
+  if (const char* e = std::getenv("SCA_GRAPH_SPLIT")) split_ = std::atoi(e) != 0;
   std::map<const RowModel*, int> placed;
   for (size_t i = 0; i < st_.size(); ++i) {
     const auto& s = st_[i];
@@ -81,6 +83,7 @@ std::shared_ptr<RowModel> GraphModel::clone_on(int device) const {
     s.model = c;
   }
   auto g = std::make_shared<GraphModel>(std::move(st), in_cols_);
+  g->set_split(split_);
   return with_meta(g);
 }
 
@@ -130,6 +133,20 @@ void GraphModel::to_device(int device) {
       if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
       else if (e != hipSuccess) { (void)hipGetLastError(); peer_direct_ = false; }
     }
+  if (split_) peer_direct_ = false;
+}
+
+int GraphModel::lane_of(int stage) const {
+  if (stage < 0) return kRootLane;
+  if (split_) return 1 << 20 | stage;
+  const int d = st_[size_t(stage)].device;
+  return d == root_device_ ? kRootLane : d;
+}
+
+bool GraphModel::multi_lane() const {
+  for (size_t i = 0; i < st_.size(); ++i)
+    if (lane_of(int(i)) != kRootLane) return true;
+  return false;
 }
 
 GraphModel::Aux& GraphModel::aux_for(hipStream_t s, int rows, int cols) {
@@ -143,9 +160,10 @@ GraphModel::Aux& GraphModel::aux_for(hipStream_t s, int rows, int cols) {
     a.staged.resize(st_.size());
     a.ptrs = std::vector<PinnedBuffer>(st_.size());
     a.ev = std::vector<Event>(st_.size());
-    const bool multi = devices().size() > 1 || st_.front().device != root_device_;
+    const bool multi = multi_lane();
     for (size_t i = 0; i < st_.size(); ++i) {
-      if (st_[i].device != root_device_ && !a.streams.count(st_[i].device)) a.streams[st_[i].device].create(st_[i].device);
+      const int lane = lane_of(int(i));
+      if (lane != kRootLane && !a.streams.count(lane)) a.streams[lane].create(st_[i].device);
       if (multi) a.ev[i].create(st_[i].device);
       if (st_[i].kind == GraphStage::kMean) a.ptrs[i].alloc(st_[i].inputs.size() * sizeof(double*));
     }
@@ -159,10 +177,7 @@ GraphModel::Aux& GraphModel::aux_for(hipStream_t s, int rows, int cols) {
     // current device.
     if (a.cap_rows > 0) {
       SCA_HIP_CHECK(hipStreamSynchronize(s));
-      for (auto& kv : a.streams) {
-        DeviceGuard dg(kv.first);
-        SCA_HIP_CHECK(hipStreamSynchronize(kv.second.get()));
-      }
+      for (auto& kv : a.streams) SCA_HIP_CHECK(hipStreamSynchronize(kv.second.get()));
     }
     size_t cap = std::max<size_t>(64, a.cap_rows);
     while (cap < size_t(rows)) cap <<= 1;
@@ -179,8 +194,7 @@ GraphModel::Aux& GraphModel::aux_for(hipStream_t s, int rows, int cols) {
         a.staged[i].resize(st.inputs.size());
         for (size_t k = 0; k < st.inputs.size(); ++k) {
           const int j = st.inputs[k];
-          const int src_dev = j < 0 ? root_device_ : st_[size_t(j)].device;
-          if (src_dev != st.device) {
+          if (lane_of(j) != lane_of(int(i))) {
             const int c = j < 0 ? cols : a.cols[size_t(j)];
             a.staged[i][k].alloc(cap * size_t(c) * sizeof(double), st.device);
           }
@@ -199,21 +213,21 @@ void GraphModel::launch_segments(const double* X, int rows, int cols, double* ou
   Aux& a = aux_for(s, rows, cols);
   const bool multi = a.ev_start.get() != nullptr;
   const size_t last = st_.size() - 1;
-  auto stream_of = [&](int dev) { return dev == root_device_ ? s : a.streams[dev].get(); };
+  auto stream_of = [&](int lane) { return lane == kRootLane ? s : a.streams[lane].get(); };
   if (multi) SCA_HIP_CHECK(hipEventRecord(a.ev_start.get(), s));
   for (size_t i = 0; i < st_.size(); ++i) {
     const auto& st = st_[i];
     DeviceGuard g(st.device);
-    hipStream_t ss = stream_of(st.device);
+    const int lane = lane_of(int(i));
+    hipStream_t ss = stream_of(lane);
     const double* in_ptr[64];
     const size_t n_in = std::min<size_t>(st.inputs.size(), 64);
     for (size_t k = 0; k < n_in; ++k) {
       const int j = st.inputs[k];
-      const int src_dev = j < 0 ? root_device_ : st_[size_t(j)].device;
       const double* p = j < 0 ? X : a.out[size_t(j)].as<double>();
-      if (multi && stream_of(src_dev) != ss)
+      if (multi && lane_of(j) != lane)
         SCA_HIP_CHECK(hipStreamWaitEvent(ss, j < 0 ? a.ev_start.get() : a.ev[size_t(j)].get(), 0));
-      if (!peer_direct_ && src_dev != st.device) {
+      if (!peer_direct_ && lane_of(j) != lane) {
         const int c = j < 0 ? cols : a.cols[size_t(j)];
         double* dst = a.staged[i][k].as<double>();
         SCA_HIP_CHECK(hipMemcpyAsync(dst, p, size_t(rows) * c * sizeof(double), hipMemcpyDefault, ss));
@@ -223,7 +237,7 @@ void GraphModel::launch_segments(const double* X, int rows, int cols, double* ou
     }
     // The output stage writes straight into the caller's buffer when it can
     // address it (same GPU, pinned host, or xGMI peer).
-    const bool direct_out = i == last && (st.device == root_device_ || peer_direct_);
+    const bool direct_out = i == last && (lane == kRootLane || peer_direct_);
     double* o = direct_out ? out : a.out[i].as<double>();
     if (st.kind == GraphStage::kModel) {
       const int ic = st.inputs[0] < 0 ? cols : a.cols[size_t(st.inputs[0])];
@@ -238,7 +252,7 @@ void GraphModel::launch_segments(const double* X, int rows, int cols, double* ou
       SCA_HIP_CHECK(hipMemcpyAsync(out, o, size_t(rows) * a.cols[i] * sizeof(double), hipMemcpyDefault, ss));
     if (multi) SCA_HIP_CHECK(hipEventRecord(a.ev[i].get(), ss));
   }
-  if (multi && st_[last].device != root_device_) SCA_HIP_CHECK(hipStreamWaitEvent(s, a.ev[last].get(), 0));
+  if (multi && lane_of(int(last)) != kRootLane) SCA_HIP_CHECK(hipStreamWaitEvent(s, a.ev[last].get(), 0));
 }
 
 void GraphModel::run_cpu(const double* X, int rows, int cols, double* out) const {

@@ -79,17 +79,30 @@ class GraphModel : public RowModel {
   const std::vector<GraphStage>& stages() const { return st_; }
   std::vector<int> devices() const;
   bool peer_direct() const { return peer_direct_; }
+  // Split mode (tests / rehearsal on one GPU): every stage gets its own
+  // stream and event chain even when stages share a GPU, and cross-stage
+  // inputs go through the staged-copy branch (peer_direct_ = false) -- the
+  // exact code a graph spread over several GPUs without peer access runs.
+  // Set before to_device(); clone_on() keeps it.  Env: SCA_GRAPH_SPLIT=1.
+  void set_split(bool on) { split_ = on; }
+  bool split() const { return split_; }
 
  private:
   struct Aux;  // per-caller-stream resources (one per batcher slot)
   void stage_cols(int in_cols, std::vector<int>& cols) const;
   std::vector<std::string> names_of(int stage) const;
   Aux& aux_for(hipStream_t s, int rows, int cols);
+  // Stream lane of a stage (-1 = graph input): stages on one lane share a
+  // stream; kRootLane is the caller's stream.
+  static constexpr int kRootLane = -1;
+  int lane_of(int stage) const;
+  bool multi_lane() const;
 
   std::vector<GraphStage> st_;
   int in_cols_ = 0;
   int root_device_ = -1;
   bool peer_direct_ = true;
+  bool split_ = false;
   std::mutex mu_;
   std::unordered_map<hipStream_t, std::unique_ptr<Aux>> aux_;
 };

@@ -18,6 +18,16 @@
 
 namespace sca::gpu {
 
+// A CPU-path call still in flight (models whose work happens elsewhere, e.g.
+// on another rank): the batcher polls done() and keeps up to `slots` of them
+// outstanding instead of blocking its device thread on each.
+struct CpuCall {
+  virtual ~CpuCall() = default;
+  virtual bool done() = 0;            // non-blocking; true once `out` holds the result (or it failed)
+  virtual std::string error() const = 0;
+};
+using CpuCallPtr = std::shared_ptr<CpuCall>;
+
 class RowModel {
  public:
   virtual ~RowModel() = default;
@@ -60,6 +70,12 @@ class RowModel {
     return false;
   }
   virtual void run_cpu(const double* X, int rows, int cols, double* out) const = 0;
+  // Asynchronous run_cpu: returns a call to poll, or nullptr if the model has
+  // none (X must stay valid and `out` untouched until done()).
+  virtual CpuCallPtr start_cpu(const double* X, int rows, int cols, double* out) {
+    (void)X; (void)rows; (void)cols; (void)out;
+    return nullptr;
+  }
   // Independent copy (host parameters only; call to_device on it) -- one per
   // GPU replica.
   virtual std::shared_ptr<RowModel> clone() const { throw std::runtime_error(name() + " cannot be replicated"); }

@@ -200,6 +200,13 @@ __global__ __launch_bounds__(kBlock) void segment_minmax(const double* __restric
   for (int64_t i = b0 + threadIdx.x; i < b1; i += kBlock) out[i] = range == 0.0 ? 0.0 : (in[i] - lo) / range;
 }
 
+// One wave that idles for `ticks` of the 100 MHz constant clock (test knob:
+// a slow model whose duration does not depend on the data); always exits.
+__global__ void __launch_bounds__(64) delay_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 int grid_for(int64_t n) {
   int64_t g = (n + kBlock - 1) / kBlock;
   if (g > 2048) g = 2048;
@@ -217,6 +224,12 @@ void combine_mean_f64(const double* const* inputs, int n_inputs, int64_t n, doub
 void combine_mean_strided_f64(const double* base, int k, int64_t n, double* out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(mean_strided_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, base, k, n, out);
+}
+
+void device_delay_us(int us, hipStream_t s) {
+  if (us <= 0) return;
+  const uint64_t ticks = uint64_t(us < 100000 ? us : 100000) * 100;  // wall clock: 100 MHz on CDNA
+  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, ticks);
 }
 
 void segment_minmax_f64(const double* in, const int32_t* seg, int nseg, int cols, double* out, hipStream_t s) {

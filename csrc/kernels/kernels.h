@@ -103,6 +103,8 @@ void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes
 void combine_mean_f64(const double* const* inputs, int n_inputs, int64_t n, double* out, hipStream_t stream);
 // out = mean over k slabs base[j*n : (j+1)*n] (gathered replica outputs).
 void combine_mean_strided_f64(const double* base, int k, int64_t n, double* out, hipStream_t stream);
+// One wave idling `us` microseconds (capped at 100 ms) on `stream`: test knob for a slow model.
+void device_delay_us(int us, hipStream_t stream);
 // Per-segment (request) global min-max normalisation; seg = nseg+1 row offsets.
 void segment_minmax_f64(const double* in, const int32_t* seg, int nseg, int cols, double* out, hipStream_t stream);
 // Decoded HWC uint8 image -> centre crop (bilinear up-size of short axes) -> CHW fp32.

@@ -75,30 +75,128 @@ void backoff_until(Ready ready, Slow slow) {
     }
   }
 }
+
+constexpr int kChanX = 0, kChanY = 1;
 }  // namespace
 
-std::string rccl_unique_id() {
-  ncclUniqueId ids[2];
-  SCA_NCCL_CHECK(ncclGetUniqueId(&ids[0]));
-  SCA_NCCL_CHECK(ncclGetUniqueId(&ids[1]));
-  return std::string(reinterpret_cast<const char*>(ids), sizeof ids);
+std::string rccl_unique_ids(int world) {
+  if (world < 2) return std::string();
+  std::vector<ncclUniqueId> ids(size_t(2 * (world - 1)));
+  for (auto& id : ids) SCA_NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(ids.data()), ids.size() * sizeof(ncclUniqueId));
+}
+
+// ------------------------------------------------------------ loopback hub
+LoopbackHub::LoopbackHub(int device) : device_(device) {
+  if (device < 0) throw std::runtime_error("LoopbackHub: needs a GPU");
+  if (const char* e = std::getenv("SCA_LOOPBACK_TIMEOUT_MS")) recv_timeout_ms_ = std::max(100, std::atoi(e));
+}
+
+LoopbackHub::~LoopbackHub() {
+  // Stages may still be read by copies in flight on streams that are gone by
+  // now; the device drains before the buffers go.
+  gpu::DeviceGuard g(device_);
+  (void)hipDeviceSynchronize();
+}
+
+LoopbackHub::Stage* LoopbackHub::acquire(size_t bytes) {
+  // caller holds mu_
+  for (auto& st : pool_)
+    if (!st->busy && st->buf.bytes() >= bytes && hipEventQuery(st->freed.get()) == hipSuccess) {
+      st->busy = true;
+      return st.get();
+    }
+  auto st = std::make_unique<Stage>();
+  st->buf.alloc(std::max<size_t>(bytes, 4096), device_);
+  st->ready.create(device_);
+  st->freed.create(device_);
+  st->busy = true;
+  pool_.push_back(std::move(st));
+  return pool_.back().get();
+}
+
+uint64_t LoopbackHub::staging_buffers() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return pool_.size();
+}
+
+void LoopbackHub::send(int src, int dst, int chan, const void* p, size_t bytes, hipStream_t s) {
+  gpu::DeviceGuard g(device_);
+  std::lock_guard<std::mutex> lk(mu_);
+  if (std::find(closed_.begin(), closed_.end(), src) != closed_.end())
+    throw std::runtime_error("loopback fabric closed");
+  Stage* st = acquire(bytes);
+  SCA_HIP_CHECK(hipMemcpyAsync(st->buf.get(), p, bytes, hipMemcpyDeviceToDevice, s));
+  SCA_HIP_CHECK(hipEventRecord(st->ready.get(), s));
+  chans_[std::make_tuple(src, dst, chan)].q.push_back({st, bytes});
+  messages_++;
+  cv_.notify_all();
+}
+
+void LoopbackHub::recv(int src, int dst, int chan, void* p, size_t bytes, hipStream_t s) {
+  gpu::DeviceGuard g(device_);
+  std::unique_lock<std::mutex> lk(mu_);
+  Chan& c = chans_[std::make_tuple(src, dst, chan)];
+  auto closed = [&] { return std::find(closed_.begin(), closed_.end(), dst) != closed_.end(); };
+  if (!c.q.empty()) immediate_++;
+  if (!cv_.wait_for(lk, std::chrono::milliseconds(recv_timeout_ms_), [&] { return !c.q.empty() || closed(); }))
+    throw std::runtime_error("loopback fabric: no send from rank " + std::to_string(src) + " within " +
+                             std::to_string(recv_timeout_ms_) + " ms");
+  if (c.q.empty()) throw std::runtime_error("loopback fabric closed");
+  const Msg m = c.q.front();
+  c.q.pop_front();
+  if (m.bytes != bytes) {
+    m.st->busy = false;
+    throw std::runtime_error("loopback fabric: rank " + std::to_string(src) + " sent " + std::to_string(m.bytes) +
+                             " bytes, rank " + std::to_string(dst) + " expects " + std::to_string(bytes));
+  }
+  SCA_HIP_CHECK(hipStreamWaitEvent(s, m.st->ready.get(), 0));
+  SCA_HIP_CHECK(hipMemcpyAsync(p, m.st->buf.get(), bytes, hipMemcpyDeviceToDevice, s));
+  SCA_HIP_CHECK(hipEventRecord(m.st->freed.get(), s));
+  m.st->busy = false;  // reusable once `freed` has fired
+}
+
+void LoopbackHub::close_rank(int rank) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (std::find(closed_.begin(), closed_.end(), rank) == closed_.end()) closed_.push_back(rank);
+  cv_.notify_all();
 }
 
 // ------------------------------------------------------------------ fabric
-Fabric::Fabric(int rank, int world, const std::string& unique_id, int device, std::vector<int> ctrl_fds)
-    : rank_(rank), world_(world), device_(device), fds_(std::move(ctrl_fds)) {
+Fabric::Fabric(int rank, int world, const std::string& unique_ids, int device, std::vector<int> ctrl_fds,
+               LoopbackHubPtr hub)
+    : rank_(rank), world_(world), device_(device), hub_(std::move(hub)), fds_(std::move(ctrl_fds)) {
   if (rank < 0 || rank >= world) throw std::runtime_error("Fabric: rank out of range");
   if (int(fds_.size()) != world) throw std::runtime_error("Fabric: need one control socket slot per rank");
+  if (hub_ && hub_->device() != device) throw std::runtime_error("Fabric: loopback hub lives on another GPU");
+  links_.resize(size_t(world));
+  for (int r = 0; r < world; ++r)
+    if ((rank == 0) != (r == 0)) links_[size_t(r)] = std::make_unique<Link>();
   map_rings();
   if (device_ < 0) return;
-  if (unique_id.size() != 2 * sizeof(ncclUniqueId)) throw std::runtime_error("Fabric: bad RCCL unique id size");
-  ncclUniqueId ids[2];
-  std::memcpy(ids, unique_id.data(), sizeof ids);
   gpu::DeviceGuard g(device);
-  sx_.create(device);
-  sy_.create(device);
-  SCA_NCCL_CHECK(ncclCommInitRank(&comm_x_, world, ids[0], rank));
-  SCA_NCCL_CHECK(ncclCommInitRank(&comm_y_, world, ids[1], rank));
+  for (auto& l : links_)
+    if (l) {
+      l->sx.create(device);
+      l->sy.create(device);
+    }
+  if (hub_) return;
+  if (unique_ids.size() != size_t(2 * (world - 1)) * sizeof(ncclUniqueId))
+    throw std::runtime_error("Fabric: bad RCCL unique id blob size");
+  auto id_of = [&](int link, int chan) {
+    ncclUniqueId id;
+    std::memcpy(&id, unique_ids.data() + size_t(2 * (link - 1) + chan) * sizeof(ncclUniqueId), sizeof id);
+    return id;
+  };
+  // One 2-rank communicator pair per rank-0 <-> worker link: rank 0 is rank 0
+  // of each, the worker rank 1.  Rank 0 joins its links in worker order; a
+  // worker waits in its init until rank 0 reaches its link.
+  for (int r = 1; r < world; ++r) {
+    if (rank != 0 && rank != r) continue;
+    Link& l = *links_[size_t(rank == 0 ? r : 0)];
+    SCA_NCCL_CHECK(ncclCommInitRank(&l.cx, 2, id_of(r, kChanX), rank == 0 ? 0 : 1));
+    SCA_NCCL_CHECK(ncclCommInitRank(&l.cy, 2, id_of(r, kChanY), rank == 0 ? 0 : 1));
+  }
 }
 
 Fabric::~Fabric() {
@@ -108,6 +206,12 @@ Fabric::~Fabric() {
       munmap(r, sizeof(HeaderRing));
       r = nullptr;
     }
+}
+
+Fabric::Link& Fabric::link(int peer) const {
+  if (peer < 0 || peer >= world_ || !links_[size_t(peer)])
+    throw std::runtime_error("Fabric: no link from rank " + std::to_string(rank_) + " to rank " + std::to_string(peer));
+  return *links_[size_t(peer)];
 }
 
 // Rank 0 creates one shared header ring per worker and sends its name over
@@ -164,31 +268,39 @@ void Fabric::map_rings() {
 }
 
 void Fabric::close() {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<std::mutex> g(close_mu_);
   if (!open_.exchange(false)) return;
-  if (comm_x_ || comm_y_) {
+  if (hub_) hub_->close_rank(rank_);
+  if (gpu()) {
     gpu::DeviceGuard d(device_);
     // A peer that died leaves posted operations that never finish: wait a
     // bounded time, then abort the communicators instead of hanging.
     const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(5);
     bool idle = false;
     while (std::chrono::steady_clock::now() < until) {
-      if (hipStreamQuery(sx_.get()) == hipSuccess && hipStreamQuery(sy_.get()) == hipSuccess) {
-        idle = true;
-        break;
-      }
+      idle = true;
+      for (auto& l : links_)
+        if (l && (hipStreamQuery(l->sx.get()) != hipSuccess || hipStreamQuery(l->sy.get()) != hipSuccess))
+          idle = false;
+      if (idle) break;
       std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
-    for (ncclComm_t* c : {&comm_x_, &comm_y_}) {
-      if (*c) (void)(idle ? ncclCommDestroy(*c) : ncclCommAbort(*c));
-      *c = nullptr;
+    for (auto& l : links_) {
+      if (!l) continue;
+      for (ncclComm_t* c : {&l->cx, &l->cy}) {
+        if (*c) (void)(idle ? ncclCommDestroy(*c) : ncclCommAbort(*c));
+        *c = nullptr;
+      }
     }
   }
-  for (auto& q : rq_)
-    if (q) {
-      std::lock_guard<std::mutex> qg(q->mu);
-      q->cv.notify_all();
-    }
+  {
+    std::lock_guard<std::mutex> rg(rq_mu_);
+    for (auto& q : rq_)
+      if (q) {
+        std::lock_guard<std::mutex> qg(q->mu);
+        q->cv.notify_all();
+      }
+  }
   for (int& fd : fds_)
     if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
   for (auto& q : rq_)
@@ -216,6 +328,7 @@ bool Fabric::peer_gone(int peer) const {
   return r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR);
 }
 
+// Callers hold the link's mutex (one publisher per ring).
 void Fabric::publish(int peer, const PeerHeader& h) {
   if (rank_ != 0) throw std::runtime_error("Fabric::publish: only rank 0 issues batches");
   HeaderRing* R = rings_.at(size_t(peer));
@@ -249,35 +362,41 @@ PeerHeader Fabric::take() {
   return h;
 }
 
-void Fabric::send_x(const void* p, size_t bytes, int peer) {
-  if (gpu()) SCA_NCCL_CHECK(ncclSend(p, bytes, ncclChar, peer, comm_x_, sx_.get()));
-  else write_all(fd(peer), p, bytes);
-}
-void Fabric::recv_x(void* p, size_t bytes, int peer) {
-  if (gpu()) SCA_NCCL_CHECK(ncclRecv(p, bytes, ncclChar, peer, comm_x_, sx_.get()));
-  else read_all(fd(peer), p, bytes);
-}
-void Fabric::send_y(const void* p, size_t bytes, int peer) {
-  if (gpu()) SCA_NCCL_CHECK(ncclSend(p, bytes, ncclChar, peer, comm_y_, sy_.get()));
-  else write_all(fd(peer), p, bytes);
-}
-void Fabric::recv_y(void* p, size_t bytes, int peer) {
-  if (gpu()) SCA_NCCL_CHECK(ncclRecv(p, bytes, ncclChar, peer, comm_y_, sy_.get()));
-  else read_all(fd(peer), p, bytes);
-}
-void Fabric::group_start() {
-  if (gpu()) SCA_NCCL_CHECK(ncclGroupStart());
-}
-void Fabric::group_end() {
-  if (gpu()) SCA_NCCL_CHECK(ncclGroupEnd());
+void Fabric::xfer(bool send, int chan, void* p, size_t bytes, int peer) {
+  if (!gpu()) {
+    if (send) write_all(fd(peer), p, bytes);
+    else read_all(fd(peer), p, bytes);
+    return;
+  }
+  Link& l = link(peer);
+  hipStream_t s = chan == kChanX ? l.sx.get() : l.sy.get();
+  if (hub_) {
+    if (send) hub_->send(rank_, peer, chan, p, bytes, s);
+    else hub_->recv(peer, rank_, chan, p, bytes, s);
+    return;
+  }
+  ncclComm_t c = chan == kChanX ? l.cx : l.cy;
+  const int to = rank_ == 0 ? 1 : 0;  // the other end, as a rank of the link's 2-rank communicator
+  if (send) SCA_NCCL_CHECK(ncclSend(p, bytes, ncclChar, to, c, s));
+  else SCA_NCCL_CHECK(ncclRecv(p, bytes, ncclChar, to, c, s));
 }
 
+void Fabric::send_x(const void* p, size_t bytes, int peer) { xfer(true, kChanX, const_cast<void*>(p), bytes, peer); }
+void Fabric::recv_x(void* p, size_t bytes, int peer) { xfer(false, kChanX, p, bytes, peer); }
+void Fabric::send_y(const void* p, size_t bytes, int peer) { xfer(true, kChanY, const_cast<void*>(p), bytes, peer); }
+void Fabric::recv_y(void* p, size_t bytes, int peer) { xfer(false, kChanY, p, bytes, peer); }
+
 void Fabric::expect_reply(int peer, void* dst, size_t bytes, std::shared_ptr<Waiter> w) {
-  if (rq_.empty()) rq_.resize(size_t(world_));
-  auto& q = rq_[size_t(peer)];
-  if (!q) {
-    q = std::make_unique<RecvQ>();
-    q->th = std::thread([this, peer] { receiver(peer); });
+  RecvQ* q;
+  {
+    std::lock_guard<std::mutex> g(rq_mu_);
+    if (rq_.empty()) rq_.resize(size_t(world_));
+    auto& slot = rq_[size_t(peer)];
+    if (!slot) {
+      slot = std::make_unique<RecvQ>();
+      slot->th = std::thread([this, peer] { receiver(peer); });
+    }
+    q = slot.get();
   }
   std::lock_guard<std::mutex> g(q->mu);
   q->q.push_back({dst, bytes, std::move(w)});
@@ -287,7 +406,12 @@ void Fabric::expect_reply(int peer, void* dst, size_t bytes, std::shared_ptr<Wai
 // Rank 0, CPU fabrics: replies of one worker arrive in issue order; hand each
 // to the caller that queued it.
 void Fabric::receiver(int peer) {
-  RecvQ& q = *rq_[size_t(peer)];
+  RecvQ* qp;
+  {
+    std::lock_guard<std::mutex> g(rq_mu_);
+    qp = rq_[size_t(peer)].get();
+  }
+  RecvQ& q = *qp;
   auto finish = [](Pending& p, const std::string& err) {
     std::lock_guard<std::mutex> g(p.w->mu);
     if (!err.empty() && p.w->error.empty()) p.w->error = err;
@@ -316,16 +440,19 @@ void Fabric::receiver(int peer) {
 }
 
 void stop_peers(Fabric& f) {
-  std::lock_guard<std::mutex> g(f.issue_mutex());
   if (!f.open()) return;
   PeerHeader h;
   h.op = kPeerStop;
-  for (int r = 0; r < f.world(); ++r)
-    if (r != f.rank()) f.publish(r, h);
-  if (f.gpu()) {
-    SCA_HIP_CHECK(hipStreamSynchronize(f.stream_x()));
-    SCA_HIP_CHECK(hipStreamSynchronize(f.stream_y()));
+  for (int r = 0; r < f.world(); ++r) {
+    if (r == f.rank()) continue;
+    std::lock_guard<std::mutex> g(f.link_mutex(r));
+    f.publish(r, h);
   }
+  if (f.gpu())
+    for (int r = 1; r < f.world(); ++r) {
+      SCA_HIP_CHECK(hipStreamSynchronize(f.stream_x(r)));
+      SCA_HIP_CHECK(hipStreamSynchronize(f.stream_y(r)));
+    }
 }
 
 // ----------------------------------------------------------- front end side
@@ -342,7 +469,8 @@ PeerRowModel::~PeerRowModel() = default;
 void PeerRowModel::to_device(int device) {
   if (device != f_->device()) throw std::runtime_error("PeerRowModel: must run on the fabric's GPU");
   ev_in_.create(device);
-  ev_done_.create(device);
+  ev_y_ = std::vector<gpu::Event>(peers_.size());
+  for (auto& e : ev_y_) e.create(device);
 }
 
 size_t PeerRowModel::workspace_bytes(int max_rows, int) const {
@@ -350,82 +478,120 @@ size_t PeerRowModel::workspace_bytes(int max_rows, int) const {
   return peers_.size() > 1 ? peers_.size() * size_t(max_rows) * out_cols_ * sizeof(double) : 0;
 }
 
-void PeerRowModel::headers(int rows, int cols) const {
+void PeerRowModel::header(int peer, int rows, int cols) const {
   PeerHeader h;
   h.op = kPeerRun;
   h.model = model_id_;
   h.rows = rows;
   h.cols = cols;
-  for (int p : peers_) f_->publish(p, h);
+  f_->publish(peer, h);
 }
 
-// GPU: everything is stream-ordered and returns at once.  X leaves on the
-// fabric's X stream once the batcher has staged it; the reply lands on the Y
-// stream (gather + combine for fan-outs), and the batcher's stream waits for
-// that -- so the next batch's send is never queued behind this reply.
+// GPU: everything is stream-ordered and returns at once.  Each peer's link
+// waits for the batcher's staged X, sends it on the link's X stream and
+// receives the reply on the link's Y stream; only that link's mutex is held,
+// so batches for other peers (other units' device threads) go out in
+// parallel.  The batcher's stream waits for every link's reply, then (fan-out)
+// averages the gathered slabs.
 void PeerRowModel::launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) {
-  std::lock_guard<std::mutex> g(f_->issue_mutex());
+  std::lock_guard<std::mutex> g(mu_);
   if (!f_->open()) throw std::runtime_error("RCCL fabric closed");
-  hipStream_t sx = f_->stream_x(), sy = f_->stream_y();
   SCA_HIP_CHECK(hipEventRecord(ev_in_.get(), s));  // X staged on the batcher's stream
-  SCA_HIP_CHECK(hipStreamWaitEvent(sx, ev_in_.get(), 0));
-  headers(rows, cols);  // doorbells: the workers post their receives now
   const size_t bx = size_t(rows) * cols * sizeof(double), by = size_t(rows) * out_cols_ * sizeof(double);
-  if (peers_.size() == 1) {
-    f_->send_x(X, bx, peers_[0]);
-    f_->recv_y(out, by, peers_[0]);
-  } else {
-    // broadcast the batch, gather every replica's output, average on this GPU
-    auto* slabs = static_cast<double*>(ws);
-    f_->group_start();
-    for (int p : peers_) f_->send_x(X, bx, p);
-    f_->group_end();
-    f_->group_start();
-    for (size_t i = 0; i < peers_.size(); ++i) f_->recv_y(slabs + i * size_t(rows) * out_cols_, by, peers_[i]);
-    f_->group_end();
-    kern::combine_mean_strided_f64(slabs, int(peers_.size()), int64_t(rows) * out_cols_, out, sy);
+  const bool fan = peers_.size() > 1;
+  auto* slabs = static_cast<double*>(ws);
+  for (size_t i = 0; i < peers_.size(); ++i) {
+    const int p = peers_[i];
+    std::lock_guard<std::mutex> lg(f_->link_mutex(p));
+    SCA_HIP_CHECK(hipStreamWaitEvent(f_->stream_x(p), ev_in_.get(), 0));
+    header(p, rows, cols);  // doorbell: the worker posts its receive now
+    f_->send_x(X, bx, p);
+    f_->recv_y(fan ? slabs + i * size_t(rows) * out_cols_ : out, by, p);
+    SCA_HIP_CHECK(hipEventRecord(ev_y_[i].get(), f_->stream_y(p)));
   }
-  SCA_HIP_CHECK(hipEventRecord(ev_done_.get(), sy));
-  SCA_HIP_CHECK(hipStreamWaitEvent(s, ev_done_.get(), 0));
+  for (auto& e : ev_y_) SCA_HIP_CHECK(hipStreamWaitEvent(s, e.get(), 0));
+  if (fan) kern::combine_mean_strided_f64(slabs, int(peers_.size()), int64_t(rows) * out_cols_, out, s);
   batches_++;
 }
 
-// CPU fabric: issue under the fabric's mutex (header + payload), then wait
-// for the reply outside it, so concurrent callers keep several batches in
-// flight per worker.
-void PeerRowModel::run_cpu(const double* X, int rows, int cols, double* out) const {
+// CPU fabric: header + payload go out under each link's mutex; the replies
+// land in call-owned buffers through the per-peer receiver threads.
+std::shared_ptr<Fabric::Waiter> PeerRowModel::issue_cpu(const double* X, int rows, int cols) const {
   if (f_->gpu()) throw std::runtime_error("rccl_peer: GPU fabric models run on their GPU");
+  if (!f_->open()) throw std::runtime_error("fabric closed");
   const size_t bx = size_t(rows) * cols * sizeof(double), ny = size_t(rows) * out_cols_;
-  std::vector<std::vector<double>> slabs(peers_.size() > 1 ? peers_.size() : 0, std::vector<double>(ny));
   auto w = std::make_shared<Fabric::Waiter>();
   w->pending = int(peers_.size());
-  {
-    std::lock_guard<std::mutex> g(f_->issue_mutex());
-    if (!f_->open()) throw std::runtime_error("fabric closed");
-    headers(rows, cols);
-    for (size_t i = 0; i < peers_.size(); ++i) {
-      f_->send_x(X, bx, peers_[i]);
-      f_->expect_reply(peers_[i], peers_.size() == 1 ? static_cast<void*>(out) : slabs[i].data(),
-                       ny * sizeof(double), w);
-    }
-  }
-  {
-    std::unique_lock<std::mutex> lk(w->mu);
-    w->cv.wait(lk, [&] { return w->pending == 0; });
-    if (!w->error.empty()) throw std::runtime_error(w->error);
-  }
-  if (peers_.size() > 1) {
-    std::fill(out, out + ny, 0.0);
-    for (const auto& sl : slabs)
-      for (size_t i = 0; i < ny; ++i) out[i] += sl[i];
-    for (size_t i = 0; i < ny; ++i) out[i] /= double(peers_.size());
+  w->bufs.assign(peers_.size(), std::vector<double>(ny));
+  for (size_t i = 0; i < peers_.size(); ++i) {
+    const int p = peers_[i];
+    std::lock_guard<std::mutex> g(f_->link_mutex(p));
+    header(p, rows, cols);
+    f_->send_x(X, bx, p);
+    f_->expect_reply(p, w->bufs[i].data(), ny * sizeof(double), w);
   }
   batches_++;
+  return w;
+}
+
+namespace {
+// The reply (mean of the gathered replies for a fan-out) goes into `out` once.
+struct PeerCall : gpu::CpuCall {
+  std::shared_ptr<Fabric::Waiter> w;
+  double* out;
+  bool finished = false;
+  std::string err;
+  bool done() override {
+    if (finished) return true;
+    {
+      std::lock_guard<std::mutex> g(w->mu);
+      if (w->pending > 0) return false;
+      err = w->error;
+    }
+    if (err.empty()) {
+      const auto& b = w->bufs;
+      const size_t n = b[0].size();
+      if (b.size() == 1) {
+        std::copy(b[0].begin(), b[0].end(), out);
+      } else {
+        for (size_t i = 0; i < n; ++i) {
+          double acc = 0.0;
+          for (const auto& sl : b) acc += sl[i];
+          out[i] = acc / double(b.size());
+        }
+      }
+    }
+    finished = true;
+    return true;
+  }
+  std::string error() const override { return err; }
+};
+}  // namespace
+
+gpu::CpuCallPtr PeerRowModel::start_cpu(const double* X, int rows, int cols, double* out) {
+  auto c = std::make_shared<PeerCall>();
+  c->w = issue_cpu(X, rows, cols);
+  c->out = out;
+  return c;
+}
+
+void PeerRowModel::run_cpu(const double* X, int rows, int cols, double* out) const {
+  PeerCall c;
+  c.w = issue_cpu(X, rows, cols);
+  c.out = out;
+  {
+    std::unique_lock<std::mutex> lk(c.w->mu);
+    c.w->cv.wait(lk, [&] { return c.w->pending == 0; });
+  }
+  c.done();
+  if (!c.err.empty()) throw std::runtime_error(c.err);
 }
 
 // ---------------------------------------------------------------- worker side
 PeerServer::PeerServer(FabricPtr fabric) : f_(std::move(fabric)) {
   if (const char* e = std::getenv("SCA_FABRIC_SLOTS")) slots_ = std::max(1, std::min(64, std::atoi(e)));
+  if (const char* e = std::getenv("SCA_FABRIC_WORKER_DELAY_US")) delay_us_ = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("SCA_FABRIC_WORKER_HOST_DELAY_US")) host_delay_us_ = std::max(0, std::atoi(e));
 }
 
 PeerServer::~PeerServer() { join(); }
@@ -472,7 +638,7 @@ void PeerServer::note_inflight(uint64_t n) {
 void PeerServer::loop() {
   gpu::DeviceGuard g(f_->device());
   const int dev = f_->device();
-  hipStream_t sx = f_->stream_x(), sy = f_->stream_y();
+  hipStream_t sx = f_->stream_x(0), sy = f_->stream_y(0);
   gpu::Stream sc(dev);
   struct Slot {
     gpu::DeviceBuffer x, y;
@@ -515,9 +681,11 @@ void PeerServer::loop() {
     SCA_HIP_CHECK(hipEventRecord(s.ev_recv.get(), sx));
     SCA_HIP_CHECK(hipStreamWaitEvent(sc.get(), s.ev_recv.get(), 0));
     if (s.used) SCA_HIP_CHECK(hipStreamWaitEvent(sc.get(), s.ev_sent.get(), 0));  // previous y has left
+    if (delay_us_) kern::device_delay_us(delay_us_, sc.get());
     m->launch(s.x.as<double>(), h.rows, h.cols, s.y.as<double>(), ws.get(), sc.get());
     SCA_HIP_CHECK(hipEventRecord(s.ev_done.get(), sc.get()));
     SCA_HIP_CHECK(hipStreamWaitEvent(sy, s.ev_done.get(), 0));
+    if (host_delay_us_) std::this_thread::sleep_for(std::chrono::microseconds(host_delay_us_));
     f_->send_y(s.y.get(), by, 0);
     SCA_HIP_CHECK(hipEventRecord(s.ev_sent.get(), sy));
     s.used = true;
@@ -547,8 +715,6 @@ void PeerServer::loop_cpu() {
   std::deque<Batch> q;
   bool done = false, computing = false;
   std::string rerr;
-  int delay_us = 0;  // test knob: slow model
-  if (const char* e = std::getenv("SCA_FABRIC_WORKER_DELAY_US")) delay_us = std::max(0, std::atoi(e));
   std::thread reader([&] {
     try {
       while (true) {
@@ -593,7 +759,7 @@ void PeerServer::loop_cpu() {
     try {
       auto& m = models_[size_t(b.h.model)];
       y.resize(size_t(b.h.rows) * m->out_cols(b.h.cols));
-      if (delay_us) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
+      if (delay_us_) std::this_thread::sleep_for(std::chrono::microseconds(delay_us_));
       m->run_cpu(b.x.data(), b.h.rows, b.h.cols, y.data());
       f_->send_y(y.data(), y.size() * sizeof(double), 0);
     } catch (const std::exception& e) {

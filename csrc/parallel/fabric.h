@@ -11,33 +11,51 @@
 //   header {seq, op, model, rows, cols} ------> header ring (shared memory,
 //     into the worker's header ring,             sequence-number doorbell)
 //     no syscall                                 polled by the worker thread
-//   X [rows, cols] fp64 --- comm_x / stream_x -> recv into slot k = seq % K
+//   X [rows, cols] fp64 --- link r, X chan ---> recv into slot k = seq % K
 //                                                model.launch(slot k) on the
 //                                                compute stream
-//   Y [rows, out_cols] <--- comm_y / stream_y -- send from slot k
+//   Y [rows, out_cols] <--- link r, Y chan ---- send from slot k
+//
+// Links: rank 0 holds one link per worker, each with its own X and Y streams,
+// its own pair of 2-rank RCCL communicators and its own issue mutex, so
+// batches bound for different workers (the two arms of an A/B test, the
+// branches of a bandit, the replicas of a combiner) are issued and move over
+// xGMI concurrently; only batches on the same link are ordered.  xGMI is
+// point-to-point (one link per GPU pair), so per-pair communicators map 1:1
+// onto the hardware instead of funnelling every peer through one ring.
 //
 // Pipelining: the worker owns K batch slots; slot k's receive, kernel and
 // reply are chained with events across three streams, and a slot is reused
 // only once its previous reply has left (device-side waits -- the worker
-// thread never blocks on the GPU).  X travels on one RCCL communicator and Y
-// on a second one, each on its own stream, so the receive of batch k+1
-// overlaps the kernel and reply of batch k, and the front end's send of the
-// next batch is not queued behind the receive of the previous reply.
+// thread never blocks on the GPU).  X travels on one communicator and Y on a
+// second one, each on its own stream, so the receive of batch k+1 overlaps
+// the kernel and reply of batch k.
 //
-// Two planes:
+// Planes:
 //  * control: a shared-memory ring per (rank 0, worker) pair carries the
 //    headers (the ranks share one host); the socket pair made at rendezvous
 //    carries only the ring's name and serves as a liveness check;
-//  * data: RCCL point-to-point (GPU memory to GPU memory over xGMI) for GPU
-//    fabrics, or the sockets for CPU fabrics (device -1: multi-process tests
-//    and CPU serving run the same header ring; a receiver thread per peer
-//    hands replies to concurrent callers in order, and the worker reads
-//    batches ahead of its compute thread, so K batches are in flight too).
+//  * data, one of three transports behind send/recv:
+//    - RCCL point-to-point (GPU memory to GPU memory over xGMI), GPU fabrics;
+//    - loopback: every rank of the fabric lives in ONE process on ONE GPU
+//      (LoopbackHub).  This runs the GPU code paths of both sides -- the
+//      worker's slot pipeline, the front end's per-link streams, the fan-out
+//      gather + combine kernel -- on a single device, so they are tested on
+//      a 1-GPU box.  Eager protocol: a send copies into a hub-owned staging
+//      buffer on the sender's stream (the sender's buffer is reusable in
+//      stream order, as after ncclSend); a receive waits on the host until
+//      the matching send is posted, then copies out on the receiver's stream
+//      after the send's event.  No GPU-side wait on work not yet enqueued, so
+//      the transport cannot wedge a hardware queue;
+//    - sockets, CPU fabrics (device -1: multi-process tests and CPU serving
+//      run the same header ring; a receiver thread per peer hands replies to
+//      concurrent callers in order, the worker reads batches ahead of its
+//      compute thread, and the front end's batcher keeps K calls outstanding
+//      through RowModel::start_cpu).
 //
-// A fan-out to K ranks (COMBINER over replicas on K GPUs) is one RCCL group
-// per direction: the sends are the broadcast, the receives the gather, and the
-// combine kernel runs on rank 0's GPU.  All issues of a rank happen under one
-// mutex, so every worker sees headers and payloads in one order.
+// A fan-out to K ranks (COMBINER over replicas on K GPUs) sends the batch on
+// every link (the broadcast), receives every reply into its own slab (the
+// gather) and averages them on rank 0's GPU once every link's Y event fired.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -46,10 +64,12 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../gpu/hip_util.h"
@@ -57,9 +77,10 @@
 
 namespace sca::par {
 
-// Two 128-byte RCCL ids (X and Y communicators); rank 0 creates, everyone
-// receives them out of band.
-std::string rccl_unique_id();
+// 2 * (world - 1) 128-byte RCCL ids (X and Y communicators of every
+// rank-0 <-> worker link, link r at [2(r-1), 2(r-1)+1]); rank 0 creates them,
+// everyone receives them out of band.
+std::string rccl_unique_ids(int world);
 
 struct PeerHeader {
   int32_t op = 0, model = 0, rows = 0, cols = 0;
@@ -78,21 +99,69 @@ struct HeaderRing {
   Slot slots[kSlots];
 };
 
+// In-process transport between the Fabric objects of one process (see the
+// file comment).  Channels are keyed (src rank, dst rank, chan); messages on a
+// channel match in posting order, like RCCL p2p on one communicator.
+class LoopbackHub {
+ public:
+  explicit LoopbackHub(int device);
+  ~LoopbackHub();
+  int device() const { return device_; }
+  void send(int src, int dst, int chan, const void* p, size_t bytes, hipStream_t s);
+  void recv(int src, int dst, int chan, void* p, size_t bytes, hipStream_t s);
+  void close_rank(int rank);  // wakes that rank's blocked receives (they throw)
+  uint64_t messages() const { return messages_.load(); }
+  uint64_t staging_buffers() const;
+  // Receives that found their send already posted (the other case waited on
+  // the host): the split shows whether the two sides ran concurrently.
+  uint64_t matched_immediately() const { return immediate_.load(); }
+
+ private:
+  struct Stage {
+    gpu::DeviceBuffer buf;
+    gpu::Event ready, freed;
+    bool busy = false;
+  };
+  struct Msg {
+    Stage* st;
+    size_t bytes;
+  };
+  struct Chan {
+    std::deque<Msg> q;
+  };
+  Stage* acquire(size_t bytes);
+  int device_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<std::tuple<int, int, int>, Chan> chans_;
+  std::vector<std::unique_ptr<Stage>> pool_;
+  std::vector<int> closed_;
+  std::atomic<uint64_t> messages_{0}, immediate_{0};
+  int recv_timeout_ms_ = 30000;
+};
+using LoopbackHubPtr = std::shared_ptr<LoopbackHub>;
+
 class Fabric {
  public:
   // ctrl_fds[r] = connected socket to rank r (-1 for self / no link): rank 0
   // holds one per worker, a worker one to rank 0.  The fabric owns them.
-  // device >= 0: RCCL data plane (unique_id from rccl_unique_id on rank 0);
-  // device < 0: the sockets carry the data too (unique_id ignored).
-  Fabric(int rank, int world, const std::string& unique_id, int device, std::vector<int> ctrl_fds);
+  // device >= 0: GPU data plane -- RCCL (unique_ids from rccl_unique_ids on
+  // rank 0) or, with `hub`, the in-process loopback transport;
+  // device < 0: the sockets carry the data too (unique_ids ignored).
+  Fabric(int rank, int world, const std::string& unique_ids, int device, std::vector<int> ctrl_fds,
+         LoopbackHubPtr hub = nullptr);
   ~Fabric();
   int rank() const { return rank_; }
   int world() const { return world_; }
   int device() const { return device_; }
   bool gpu() const { return device_ >= 0; }
-  hipStream_t stream_x() const { return sx_.get(); }
-  hipStream_t stream_y() const { return sy_.get(); }
-  std::mutex& issue_mutex() { return mu_; }
+  bool loopback() const { return hub_ != nullptr; }
+  std::string transport() const { return !gpu() ? "sockets" : (hub_ ? "loopback" : "rccl"); }
+  // Per-link resources (peer = the other end: a worker rank on rank 0, 0 on
+  // a worker).
+  hipStream_t stream_x(int peer) const { return link(peer).sx.get(); }
+  hipStream_t stream_y(int peer) const { return link(peer).sy.get(); }
+  std::mutex& link_mutex(int peer) { return link(peer).mu; }
   bool open() const { return open_.load(); }
   void close();
 
@@ -100,14 +169,12 @@ class Fabric {
   // throws once the peer's socket is gone)
   void publish(int peer, const PeerHeader& h);
   PeerHeader take();
-  // data plane: GPU fabrics enqueue on stream_x (X) / stream_y (Y); CPU
-  // fabrics write / read the sockets
+  // data plane: GPU fabrics enqueue on the link's X / Y stream; CPU fabrics
+  // write / read the link's socket
   void send_x(const void* p, size_t bytes, int peer);
   void recv_x(void* p, size_t bytes, int peer);
   void send_y(const void* p, size_t bytes, int peer);
   void recv_y(void* p, size_t bytes, int peer);
-  void group_start();
-  void group_end();
 
   // CPU fabrics, rank 0: queue a reply read (bytes into `dst`) on the peer's
   // receiver thread; replies arrive in issue order.
@@ -116,21 +183,29 @@ class Fabric {
     std::condition_variable cv;
     int pending = 0;
     std::string error;
+    std::vector<std::vector<double>> bufs;  // reply buffers owned by the call (outlive an abandoned caller)
   };
   void expect_reply(int peer, void* dst, size_t bytes, std::shared_ptr<Waiter> w);
 
  private:
+  struct Link {
+    gpu::Stream sx, sy;
+    ncclComm_t cx = nullptr, cy = nullptr;
+    std::mutex mu;
+  };
+  Link& link(int peer) const;
   int fd(int peer) const;
   void map_rings();
   bool peer_gone(int peer) const;
   void receiver(int peer);
+  void xfer(bool send, int chan, void* p, size_t bytes, int peer);
   int rank_, world_, device_;
-  ncclComm_t comm_x_ = nullptr, comm_y_ = nullptr;
-  gpu::Stream sx_, sy_;
+  LoopbackHubPtr hub_;
+  std::vector<std::unique_ptr<Link>> links_;  // indexed by peer rank (null where there is no link)
   std::vector<int> fds_;
   std::vector<HeaderRing*> rings_;  // rank 0: one per worker; worker: rings_[0]
   std::vector<uint64_t> next_;      // rank 0: next seq per worker; worker: next_[0] to take
-  std::mutex mu_;
+  std::mutex close_mu_;
   std::atomic<bool> open_{true};
   // CPU reply receivers (rank 0)
   struct Pending {
@@ -144,6 +219,7 @@ class Fabric {
     std::deque<Pending> q;
     std::thread th;
   };
+  std::mutex rq_mu_;
   std::vector<std::unique_ptr<RecvQ>> rq_;
 };
 using FabricPtr = std::shared_ptr<Fabric>;
@@ -165,14 +241,18 @@ class PeerRowModel : public gpu::RowModel {
   size_t workspace_bytes(int max_rows, int cols) const override;
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
+  gpu::CpuCallPtr start_cpu(const double* X, int rows, int cols, double* out) override;
   uint64_t batches() const { return batches_.load(); }
 
  private:
-  void headers(int rows, int cols) const;
+  std::shared_ptr<Fabric::Waiter> issue_cpu(const double* X, int rows, int cols) const;
+  void header(int peer, int rows, int cols) const;
   FabricPtr f_;
   std::vector<int> peers_;
   int model_id_, in_cols_, out_cols_;
-  gpu::Event ev_in_, ev_done_;
+  std::mutex mu_;  // launch() state (the events) -- one batcher device thread in practice
+  gpu::Event ev_in_;
+  std::vector<gpu::Event> ev_y_;  // per peer: reply landed
   mutable std::atomic<uint64_t> batches_{0};
 };
 
@@ -200,6 +280,8 @@ class PeerServer {
   std::vector<gpu::RowModelPtr> models_;
   std::thread th_;
   int slots_ = 4;
+  int delay_us_ = 0;       // test knob (SCA_FABRIC_WORKER_DELAY_US): a slow model (GPU: a delay kernel)
+  int host_delay_us_ = 0;  // test knob (SCA_FABRIC_WORKER_HOST_DELAY_US, GPU loop): a slow worker thread
   std::atomic<uint64_t> batches_{0}, rows_{0}, host_syncs_{0}, max_inflight_{0};
   mutable std::mutex err_mu_;
   std::string err_;

@@ -123,9 +123,11 @@ def plan(graph: Dict, row_models: Dict[str, Any], bound: Dict[str, Any],
     return found
 
 
-def build(C, fg: FusedGraph, in_cols: int = 0):
-    """Native GraphModel for a plan entry (raises if the stage widths disagree)."""
-    return C.graph_model(fg.stages, in_cols)
+def build(C, fg: FusedGraph, in_cols: int = 0, split: bool = False):
+    """Native GraphModel for a plan entry (raises if the stage widths disagree).
+    ``split``: one stream per stage and staged copies between stages even on
+    one GPU -- the multi-GPU code path, rehearsed on a single device."""
+    return C.graph_model(fg.stages, in_cols, split)
 
 
 def describe(fg: FusedGraph) -> str:
@@ -134,6 +136,13 @@ def describe(fg: FusedGraph) -> str:
         src = ",".join("in" if j < 0 else f"s{j}" for j in s["inputs"])
         parts.append(f"s{i}={s['kind']}:{s['node']}@gpu{s['device']}({src})")
     return " ".join(parts)
+
+
+def split_enabled(annotations: Optional[Dict[str, str]]) -> bool:
+    """``seldon.io/device-graph-split: true`` (or SCA_GRAPH_SPLIT=1): build
+    fused graphs in split mode (see ``build``)."""
+    v = (annotations or {}).get("seldon.io/device-graph-split")
+    return v is not None and str(v).lower() in ("1", "true", "yes", "on")
 
 
 def fusion_enabled(annotations: Optional[Dict[str, str]], default: bool = True) -> bool:

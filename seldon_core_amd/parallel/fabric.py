@@ -77,10 +77,49 @@ def init_fabric(device: Optional[int] = None):
     fds = _control_links(rank, world)
     uid = b""
     if device >= 0:
-        box = [C.rccl_unique_id() if rank == 0 else None]
+        box = [C.rccl_unique_ids(world) if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
     return C.Fabric(rank, world, uid, int(device), fds)
+
+
+def loopback_fabrics(world: int, device: int = 0) -> List[Any]:
+    """Every rank of a ``world``-rank fabric in THIS process on ONE GPU (the
+    loopback transport, csrc/parallel/fabric.h): the front end's and the
+    workers' GPU code paths -- per-link streams, the worker's slot pipeline,
+    the fan-out gather + combine -- run on a 1-GPU box.  The control plane is
+    the real one (shared-memory header rings, socket pairs).  Returns the
+    fabrics by rank; worker fabrics go to ``serve_peer`` like any other."""
+    import socket
+    import threading
+
+    if world < 2:
+        raise ValueError("loopback fabric needs world >= 2")
+    C = native()
+    hub = C.LoopbackHub(int(device))
+    fds = [[-1] * world for _ in range(world)]
+    for r in range(1, world):
+        a, b = socket.socketpair()
+        fds[0][r], fds[r][0] = a.detach(), b.detach()
+    out: List[Any] = [None] * world
+    errs: List[BaseException] = []
+
+    def make(r: int) -> None:
+        try:
+            out[r] = C.Fabric(r, world, b"", int(device), fds[r], hub)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            errs.append(e)
+
+    # rank 0 hands each worker its header ring over the socket pair: the
+    # constructors rendezvous, so they run concurrently (they drop the GIL)
+    th = [threading.Thread(target=make, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return out
 
 
 def node_rank(node: Dict) -> Optional[int]:

@@ -192,6 +192,11 @@ class Deployment:
         devs = self.replica_devices(node)
         opts = self._batcher_opts(node)
         retries = int(opts.pop("max_retries", 1))
+        if self.fabric is not None and node.get("rank") is not None and devs == [-1]:
+            # CPU fabric: the peer call is asynchronous (RowModel.start_cpu),
+            # so the batcher's device thread keeps `slots` batches outstanding
+            # at the worker instead of one per blocked front-end thread.
+            opts.setdefault("cpu_batching", True)
         if len(devs) == 1:
             return self.C.BatchedUnit(row_model, devs[0], **opts)
         reps = []
@@ -229,7 +234,7 @@ class Deployment:
         if self.fuse and self._row_models:
             for fg in device_graph.plan(self.predictor["graph"], self._row_models, self.units, self._node_device):
                 try:
-                    gm = device_graph.build(self.C, fg)
+                    gm = device_graph.build(self.C, fg, split=device_graph.split_enabled(self.annotations()))
                 except Exception as e:  # stage widths disagree: the engine reports it per request
                     logger.info("device graph at %s not fused: %s", fg.root, e)
                     continue

@@ -103,7 +103,7 @@ def test_combiner_gathers_from_every_rank_cpu_fabric():
 
 def test_native_fabric_api_present():
     C = sca.native()
-    for name in ("rccl_unique_id", "Fabric", "PeerServer", "peer_row_model"):
+    for name in ("rccl_unique_ids", "Fabric", "LoopbackHub", "PeerServer", "peer_row_model"):
         assert hasattr(C, name)
 
 
