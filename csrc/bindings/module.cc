@@ -1012,7 +1012,10 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("n_branches", &gpu::BanditModel::n_branches)
       .def("snapshot", &gpu::BanditModel::snapshot)
       .def("restore", &gpu::BanditModel::restore)
-      .def("route_host", &gpu::BanditModel::route_host, "epsilon-greedy decision on the host (kernel's Philox stream)");
+      .def("route_host", &gpu::BanditModel::route_host, "epsilon-greedy decision on the host (kernel's Philox stream)")
+      .def("attach_shared", &gpu::BanditModel::attach_shared, py::arg("name"), py::arg("worker") = 0,
+           "keep the counters in the host-wide shared mapping `name` (one router state across engine processes)")
+      .def_property_readonly("shared", &gpu::BanditModel::shared);
   py::class_<gpu::BanditRouterUnit, Unit, std::shared_ptr<gpu::BanditRouterUnit>>(m, "BanditRouterUnit")
       .def(py::init([](std::shared_ptr<gpu::BanditModel> model, int device, int max_batch, int slots, bool device_route) {
              gpu::BatcherOptions o;

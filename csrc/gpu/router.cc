@@ -1,10 +1,127 @@
 #include "router.h"
 
+#include <fcntl.h>
+#include <immintrin.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
 #include <sstream>
+#include <thread>
 
 #include "../kernels/philox.h"
 
 namespace sca::gpu {
+
+// One bandit's state shared by the engine processes of a host.  Updates take
+// a spinlock in the mapping (feedback is rare next to routing, and the
+// critical section is a few hundred nanoseconds); readers compare `version`
+// with the last one they pulled.  A lock held for over a second belongs to a
+// process that died inside the critical section and is taken over.
+struct BanditModel::Shared {
+  std::atomic<uint32_t> init;  // 0 fresh, 1 being seeded, 2 ready
+  std::atomic<uint32_t> lock;
+  std::atomic<uint64_t> version;
+  std::atomic<int32_t> best;
+  int32_t kind, nb;
+  int64_t success[kMaxBranches], tries[kMaxBranches];
+  double values[kMaxBranches], alpha[kMaxBranches], beta[kMaxBranches];
+};
+
+namespace {
+struct ShmLock {
+  std::atomic<uint32_t>& l;
+  explicit ShmLock(std::atomic<uint32_t>& lk) : l(lk) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned n = 0;; ++n) {
+      uint32_t z = 0;
+      if (l.compare_exchange_weak(z, 1, std::memory_order_acquire)) return;
+      if (n < 4096) {
+        _mm_pause();
+      } else {
+        std::this_thread::yield();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+          l.store(1, std::memory_order_acquire);  // owner died mid-update: take it over
+          return;
+        }
+      }
+    }
+  }
+  ~ShmLock() { l.store(0, std::memory_order_release); }
+};
+}  // namespace
+
+BanditModel::~BanditModel() {
+  if (shm_) munmap(shm_, sizeof(Shared));
+}
+
+void BanditModel::attach_shared(const std::string& name, int worker) {
+  if (shm_) return;
+  const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+  if (fd < 0) throw std::runtime_error("bandit: shm_open(" + name + ") failed: " + std::strerror(errno));
+  if (ftruncate(fd, off_t(sizeof(Shared))) != 0) {
+    ::close(fd);
+    throw std::runtime_error(std::string("bandit: ftruncate failed: ") + std::strerror(errno));
+  }
+  void* p = mmap(nullptr, sizeof(Shared), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  ::close(fd);
+  if (p == MAP_FAILED) throw std::runtime_error(std::string("bandit: mmap failed: ") + std::strerror(errno));
+  auto* sh = static_cast<Shared*>(p);
+  uint32_t fresh = 0;
+  std::lock_guard<std::mutex> g(mu_);
+  if (sh->init.compare_exchange_strong(fresh, 1)) {  // first worker seeds the shared state with its own
+    sh->kind = int32_t(kind_);
+    sh->nb = nb_;
+    for (int i = 0; i < nb_; ++i) {
+      sh->success[i] = success_[size_t(i)];
+      sh->tries[i] = tries_[size_t(i)];
+      sh->values[i] = values_[size_t(i)];
+      sh->alpha[i] = a_[size_t(i)];
+      sh->beta[i] = b_[size_t(i)];
+    }
+    sh->best.store(best_);
+    sh->version.store(1);
+    sh->init.store(2, std::memory_order_release);
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (sh->init.load(std::memory_order_acquire) != 2) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        munmap(p, sizeof(Shared));
+        throw std::runtime_error("bandit: shared state " + name + " never became ready");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    if (sh->kind != int32_t(kind_) || sh->nb != nb_) {
+      munmap(p, sizeof(Shared));
+      throw std::runtime_error("bandit: shared state " + name + " belongs to a different router");
+    }
+  }
+  shm_ = sh;
+  seed_ ^= 0x9E3779B97F4A7C15ull * uint64_t(worker + 1);
+  rng_.seed(seed_);
+  pull_shared();
+}
+
+void BanditModel::pull_shared() {
+  ShmLock l(shm_->lock);
+  for (int i = 0; i < nb_; ++i) {
+    success_[size_t(i)] = shm_->success[i];
+    tries_[size_t(i)] = shm_->tries[i];
+    values_[size_t(i)] = shm_->values[i];
+    a_[size_t(i)] = shm_->alpha[i];
+    b_[size_t(i)] = shm_->beta[i];
+  }
+  best_ = shm_->best.load(std::memory_order_relaxed);
+  seen_version_.store(shm_->version.load(std::memory_order_relaxed), std::memory_order_relaxed);
+  publish();
+}
+
+void BanditModel::maybe_pull() const {
+  if (!shm_ || shm_->version.load(std::memory_order_acquire) == seen_version_.load(std::memory_order_relaxed)) return;
+  std::lock_guard<std::mutex> g(mu_);
+  const_cast<BanditModel*>(this)->pull_shared();
+}
 
 BanditModel::BanditModel(Kind kind, int n_branches, float epsilon, int64_t seed, int best_branch)
     : kind_(kind), nb_(n_branches), eps_(epsilon) {
@@ -40,6 +157,7 @@ void BanditModel::to_device(int) {
 }
 
 void BanditModel::launch(const double*, int rows, int, double* out, void*, hipStream_t s) {
+  maybe_pull();
   const uint64_t off = offset_.fetch_add(uint64_t(rows));
   State* st = state_.dev<State>();
   if (kind_ == kEpsilonGreedy)
@@ -51,7 +169,7 @@ void BanditModel::launch(const double*, int rows, int, double* out, void*, hipSt
 int BanditModel::route_host() {
   const uint64_t off = offset_.fetch_add(1, std::memory_order_relaxed);
   kern::Philox rng(seed_, off);
-  const int b = best_pub_.load(std::memory_order_acquire);
+  const int b = shm_ ? shm_->best.load(std::memory_order_acquire) : best_pub_.load(std::memory_order_acquire);
   int pick = b;
   if (nb_ > 1 && rng.uniform() <= eps_) {
     int other = int(rng.next() % uint32_t(nb_ - 1));
@@ -62,6 +180,7 @@ int BanditModel::route_host() {
 }
 
 void BanditModel::run_cpu(const double*, int rows, int, double* out) const {
+  maybe_pull();
   std::lock_guard<std::mutex> g(mu_);
   std::uniform_real_distribution<double> U(0.0, 1.0);
   for (int r = 0; r < rows; ++r) {
@@ -90,6 +209,30 @@ void BanditModel::run_cpu(const double*, int rows, int, double* out) const {
 void BanditModel::feedback(int routing, int n_success, int n_failures) {
   if (routing < 0 || routing >= nb_) throw std::runtime_error("bandit feedback: invalid routing " + std::to_string(routing));
   std::lock_guard<std::mutex> g(mu_);
+  if (shm_) {  // the update happens on the shared counters, under their lock
+    ShmLock l(shm_->lock);
+    for (int i = 0; i < nb_; ++i) {
+      success_[size_t(i)] = shm_->success[i];
+      tries_[size_t(i)] = shm_->tries[i];
+      a_[size_t(i)] = shm_->alpha[i];
+      b_[size_t(i)] = shm_->beta[i];
+      values_[size_t(i)] = shm_->values[i];
+    }
+    update_locked(routing, n_success, n_failures);
+    shm_->success[routing] = success_[size_t(routing)];
+    shm_->tries[routing] = tries_[size_t(routing)];
+    shm_->values[routing] = values_[size_t(routing)];
+    shm_->alpha[routing] = a_[size_t(routing)];
+    shm_->beta[routing] = b_[size_t(routing)];
+    shm_->best.store(best_, std::memory_order_release);
+    seen_version_.store(shm_->version.fetch_add(1, std::memory_order_acq_rel) + 1, std::memory_order_relaxed);
+  } else {
+    update_locked(routing, n_success, n_failures);
+  }
+  publish();
+}
+
+void BanditModel::update_locked(int routing, int n_success, int n_failures) {
   success_[size_t(routing)] += n_success;
   tries_[size_t(routing)] += n_success + n_failures;
   if (kind_ == kEpsilonGreedy) {
@@ -105,20 +248,22 @@ void BanditModel::feedback(int routing, int n_success, int n_failures) {
     a_[size_t(routing)] += n_success;
     b_[size_t(routing)] += n_failures;
   }
-  publish();
 }
 
 std::vector<double> BanditModel::values() const {
+  maybe_pull();
   std::lock_guard<std::mutex> g(mu_);
   return values_;
 }
 
 int BanditModel::best_branch() const {
+  maybe_pull();
   std::lock_guard<std::mutex> g(mu_);
   return best_;
 }
 
 std::string BanditModel::snapshot() const {
+  maybe_pull();
   std::lock_guard<std::mutex> g(mu_);
   std::ostringstream o;
   o.precision(17);
@@ -152,6 +297,18 @@ void BanditModel::restore(const std::string& s) {
   arr("beta", b_);
   if (const Json* b = j.find("best")) best_ = int(b->as_number());
   if (const Json* o = j.find("offset")) offset_.store(uint64_t(o->as_number()));
+  if (shm_) {  // every worker restores the same snapshot: the shared state takes it once more
+    ShmLock l(shm_->lock);
+    for (int i = 0; i < nb_; ++i) {
+      shm_->success[i] = success_[size_t(i)];
+      shm_->tries[i] = tries_[size_t(i)];
+      shm_->values[i] = values_[size_t(i)];
+      shm_->alpha[i] = a_[size_t(i)];
+      shm_->beta[i] = b_[size_t(i)];
+    }
+    shm_->best.store(best_, std::memory_order_release);
+    seen_version_.store(shm_->version.fetch_add(1, std::memory_order_acq_rel) + 1, std::memory_order_relaxed);
+  }
   publish();
 }
 

@@ -43,7 +43,22 @@ class BanditModel : public RowModel {
   bool host_routable() const { return kind_ == kEpsilonGreedy; }
   int route_host();
 
+  // Cross-process state (serve --gpus N runs one engine process per GPU and
+  // the reference keeps ONE router object per deployment,
+  // EpsilonGreedy.py:87-130): the counters and the best branch live in the
+  // shared mapping `name` (POSIX shm, created by the first attacher, which
+  // seeds it with its own state), so every worker learns from every
+  // worker's feedback and routes by the same best branch.  `worker` mixes
+  // into the Philox seed so workers draw different random streams.
+  void attach_shared(const std::string& name, int worker);
+  bool shared() const { return shm_ != nullptr; }
+  ~BanditModel() override;
+
  private:
+  struct Shared;
+  void pull_shared();         // shared -> local + pinned (mu_ held)
+  void maybe_pull() const;    // pull if another worker updated the shared state
+  void update_locked(int routing, int n_success, int n_failures);  // the reference's update rule (mu_ held)
   struct State {
     int32_t best;
     int32_t pad[3];
@@ -65,6 +80,8 @@ class BanditModel : public RowModel {
   State host_state_{};
   std::atomic<int> best_pub_{0};  // published best branch (host route)
   std::atomic<uint64_t> offset_{0};
+  Shared* shm_ = nullptr;
+  mutable std::atomic<uint64_t> seen_version_{0};
 };
 
 class BanditRouterUnit : public Unit {

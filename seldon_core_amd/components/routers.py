@@ -67,6 +67,14 @@ class _BanditRouter:
         self._unit = None
 
     # -- native binding (Deployment) ---------------------------------------
+    def share_state(self, name: str, worker: int = 0) -> None:
+        """One router state across the engine processes of a host (``serve
+        --gpus N``): counters in the shared mapping ``name``, so feedback sent
+        to any worker trains the bandit every worker routes with (the
+        reference has one router object per deployment,
+        EpsilonGreedy.py:87-130)."""
+        self.model.attach_shared(name, int(worker))
+
     def native_unit(self, device: int):
         dev = device if self.device is None else int(self.device)
         self._unit = self._C.BanditRouterUnit(self.model, dev, self.max_batch,

@@ -26,6 +26,22 @@ same ports through ``SO_REUSEPORT``), and only once it reports ready is the
 old one drained -- one extra worker at a time, never fewer than N serving.
 A new worker that fails to come up stops the rollout and the old one stays.
 
+Rank-placed graphs: a spec whose nodes carry ``rank: r`` (the GPU / process
+hosting that node, see ``seldon_core_amd.parallel.fabric``) runs as ONE graph
+over ``--gpus N`` processes instead of N copies: the supervisor starts the N
+rank processes as a gang (RANK / WORLD_SIZE / MASTER_* like torchrun, every
+GPU visible), rank 0 serves the REST/gRPC front end and the graph, and ranks
+1..N-1 run ``serve_peer`` -- batches cross to them over RCCL (xGMI) or, on
+CPU, sockets.  A rank that dies takes the gang down and the supervisor
+restarts all of it (the communicators cannot be re-joined); SIGHUP restarts
+the gang from the current spec.
+
+Shared router state: with N replica workers, stateful routers (epsilon-greedy,
+Thompson) keep their counters in one host-wide shared mapping
+(``SCA_SHARED_STATE``), so feedback that SO_REUSEPORT hands to any worker
+trains the one bandit every worker routes with -- the reference's single
+router object per deployment (``EpsilonGreedy.py:87-130``).
+
 Configuration precedence: defaults < ``/etc/podinfo/annotations`` < spec
 annotations < environment (``ENGINE_SERVER_PORT``, ``SELDON_LOG_*``, ...) < flags.
 """
@@ -90,8 +106,69 @@ def _n_workers(arg: str) -> int:
     return max(1, int(arg))
 
 
+def _placed_world(spec_path: Optional[str], predictor: Optional[str]) -> int:
+    """1 + the highest ``rank:`` of the served predictor's graph (0 = no
+    rank placement)."""
+    from .parallel.fabric import rank_assignments
+    from .serving.spec import load_spec, select_predictor
+
+    try:
+        pred = select_predictor(load_spec(spec_path), predictor)
+    except Exception:  # the worker reports spec errors
+        return 0
+    ranks = rank_assignments(pred.get("graph") or {})
+    return (max(ranks) + 1) if ranks and max(ranks) > 0 else 0
+
+
+def run_fabric_worker(args: argparse.Namespace) -> int:
+    """One rank of a rank-placed graph (see the module doc)."""
+    import datetime
+
+    import torch.distributed as dist
+
+    from .parallel.fabric import init_fabric, serve_peer
+    from .serving.spec import load_spec
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=120))
+    device = args.device
+    if device is None:
+        from ._native import gpu_count
+
+        device = rank if gpu_count() > rank else -1
+    fabric = init_fabric(device=device)
+    if rank == 0:
+        return run_worker(args, fabric=fabric)
+    comps = {}
+    for c in args.component:
+        node, _, cls = c.partition("=")
+        comps[node] = cls
+    stop_requested = threading.Event()
+    # SIGTERM: rank 0 drains first and then stops this loop; leave on our own
+    # only if it never does.
+    signal.signal(signal.SIGTERM, lambda *_: stop_requested.set())
+    signal.signal(signal.SIGINT, lambda *_: stop_requested.set())
+    srv = serve_peer(load_spec(args.spec), fabric, comps, predictor=args.predictor)
+    logger.info("rank %d/%d serving its placed nodes on device %s (%s)", rank, world, device, fabric.transport)
+    joiner = threading.Thread(target=srv.join, daemon=True)
+    joiner.start()
+    while joiner.is_alive():
+        joiner.join(0.2)
+        if stop_requested.is_set():
+            deadline = time.monotonic() + 60.0
+            while joiner.is_alive() and time.monotonic() < deadline:
+                joiner.join(0.2)
+            break
+    err = srv.error()
+    fabric.close()
+    if err:
+        logger.error("rank %d peer loop ended: %s", rank, err)
+    logger.info("rank %d done: %d batches, %d rows", rank, srv.batches, srv.rows)
+    os._exit(0 if not err or stop_requested.is_set() else 1)
+
+
 # ------------------------------------------------------------------ worker
-def run_worker(args: argparse.Namespace) -> int:
+def run_worker(args: argparse.Namespace, fabric=None) -> int:
     if args.pin_cpus > 0 and (args.device is None or args.device >= 0):
         # before the front end and the GPU units start their threads (they inherit it)
         from .utils.topology import pin
@@ -113,8 +190,10 @@ def run_worker(args: argparse.Namespace) -> int:
     for c in args.component:
         node, _, cls = c.partition("=")
         comps[node] = cls
+    device = args.device if fabric is None else int(fabric.device)
     dep = Deployment(sdep, components=comps, predictor=args.predictor, deployment_name=cfg.deployment_name,
-                     device=args.device, fuse=False if args.no_fuse else None, config=cfg)
+                     device=device, fuse=False if (args.no_fuse or fabric is not None) else None, config=cfg,
+                     fabric=fabric)
     if args.persistence:
         dep.restore_checkpoint()
         dep.start_checkpointing(args.push_frequency)
@@ -158,7 +237,9 @@ def run_worker(args: argparse.Namespace) -> int:
         explainer.stop()
     clean = h.drain(cfg.drain_seconds)
     dep.engine.flush_message_log()
-    dep.close()
+    dep.close()  # rank-placed graph: also stops the other ranks' peer loops
+    if fabric is not None:
+        fabric.close()
     logger.info("worker %s drained (%s)", rank, "clean" if clean else "timeout")
     return 0
 
@@ -168,8 +249,11 @@ class Supervisor:
     """Keeps one worker process per GPU alive."""
 
     def __init__(self, n: int, worker_argv: List[str], max_restarts: int = 5, ready_timeout: float = 120.0,
-                 drain_timeout: float = 60.0):
+                 drain_timeout: float = 60.0, gang: bool = False):
         self.n = n
+        self.gang = gang  # rank-placed graph: the N processes are ranks of ONE graph
+        self.master_port = 0
+        self.shared_prefix = f"/sca_state_{os.getpid()}"
         self.argv = worker_argv
         self.max_restarts = max_restarts
         self.ready_timeout = ready_timeout
@@ -184,7 +268,12 @@ class Supervisor:
 
     def _start(self, rank: int, ready_file: Optional[str] = None) -> subprocess.Popen:
         env = dict(os.environ)
-        env["HIP_VISIBLE_DEVICES"] = str(rank)
+        if self.gang:  # torchrun-style rank environment; every GPU visible (peer links between them)
+            env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(self.n), LOCAL_WORLD_SIZE=str(self.n),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(self.master_port), SCA_FABRIC_WORLD=str(self.n))
+        else:
+            env["HIP_VISIBLE_DEVICES"] = str(rank)
+            env["SCA_SHARED_STATE"] = self.shared_prefix
         env["SCA_WORKER_RANK"] = str(rank)
         env["SCA_WORKERS"] = str(self.n)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -199,11 +288,54 @@ class Supervisor:
     def spawn(self, rank: int) -> None:
         self.procs[rank] = self._start(rank)
 
+    def spawn_gang(self) -> None:
+        """(Re)start every rank of a rank-placed graph on a fresh rendezvous port."""
+        import socket
+
+        for p in self.procs.values():
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in self.procs.values():
+            try:
+                p.wait(timeout=self.drain_timeout)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            self.master_port = sk.getsockname()[1]
+        for r in range(self.n):
+            self.spawn(r)
+
+    def cleanup_shared(self) -> None:
+        """Remove the shared router-state mappings the workers created."""
+        base = "/dev/shm"
+        tag = self.shared_prefix.lstrip("/") + "_"
+        try:
+            names = os.listdir(base)
+        except OSError:
+            return
+        for n in names:
+            if n.startswith(tag):
+                try:
+                    os.unlink(os.path.join(base, n))
+                except OSError:
+                    pass
+
     def rolling_update(self) -> bool:
         """Replace every worker, one at a time, surge 1: start the new one,
         wait for its ready marker, then drain the old one.  Returns False (and
-        keeps the old worker) if a new worker does not come up."""
+        keeps the old worker) if a new worker does not come up.  A rank-placed
+        gang cannot run two generations side by side: it restarts whole."""
         import tempfile
+
+        if self.gang:
+            self.generation += 1
+            logger.warning("rollout %d: rank-placed graph restarts as a gang", self.generation)
+            self.spawn_gang()
+            self.rollouts.append({"generation": self.generation, "replaced": list(range(self.n)), "ok": True,
+                                  "gang": True})
+            return True
 
         self.generation += 1
         record = {"generation": self.generation, "replaced": [], "ok": True}
@@ -266,8 +398,17 @@ class Supervisor:
                 p.send_signal(signal.SIGTERM)
 
     def run(self) -> int:
-        for r in range(self.n):
-            self.spawn(r)
+        try:
+            return self._run()
+        finally:
+            self.cleanup_shared()
+
+    def _run(self) -> int:
+        if self.gang:
+            self.spawn_gang()
+        else:
+            for r in range(self.n):
+                self.spawn(r)
         signal.signal(signal.SIGTERM, lambda *_: self.terminate())
         signal.signal(signal.SIGINT, lambda *_: self.terminate())
         signal.signal(signal.SIGHUP, lambda *_: setattr(self, "roll_requested", True))
@@ -293,6 +434,11 @@ class Supervisor:
                     self.terminate()
                     continue
                 self.restarts[r].append(now)
+                if self.gang:
+                    logger.warning("rank %d exited with %s; restarting the gang", r, code)
+                    self.spawn_gang()
+                    alive = self.n
+                    break
                 logger.warning("worker %d exited with %s; restarting", r, code)
                 self.spawn(r)
                 alive += 1
@@ -305,8 +451,14 @@ def main(argv: Optional[List[str]] = None) -> int:
     logging.basicConfig(level=getattr(logging, str(args.log_level).upper(), logging.INFO),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     if args.worker:
+        if os.environ.get("SCA_FABRIC_WORLD"):
+            return run_fabric_worker(args)
         return run_worker(args)
     n = _n_workers(args.gpus)
+    placed = _placed_world(args.spec, args.predictor)
+    if placed > n:
+        logger.error("the graph places nodes on %d ranks but --gpus is %d", placed, n)
+        return 2
     if n == 1 and not args.supervise:
         return run_worker(args)
     raw = list(sys.argv[1:] if argv is None else argv)
@@ -322,7 +474,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         if a.startswith("--gpus="):
             continue
         worker_argv.append(a)
-    return Supervisor(n, worker_argv, args.max_restarts).run()
+    return Supervisor(n, worker_argv, args.max_restarts, gang=placed > 0).run()
 
 
 if __name__ == "__main__":

@@ -316,6 +316,18 @@ class Deployment:
             return rm
         return None
 
+    def shared_state_name(self, node: Dict) -> Optional[str]:
+        """Name of the host-wide shared mapping of a stateful node when the
+        supervisor runs several engine processes (SCA_SHARED_STATE prefix,
+        SCA_WORKERS > 1), else None."""
+        prefix = os.environ.get("SCA_SHARED_STATE")
+        if not prefix or int(os.environ.get("SCA_WORKERS", "1") or 1) <= 1:
+            return None
+        import re
+
+        tag = re.sub(r"[^A-Za-z0-9_.-]", "_", f"{self.deployment_name}_{self.predictor.get('name', '')}_{node['name']}")
+        return f"{prefix}_{tag}"[:250]
+
     def _bind_object(self, node: Dict, obj: Any) -> None:
         obj = self._instantiate(node, obj)
         rm = self._row_model_of(obj)
@@ -328,6 +340,10 @@ class Deployment:
             return
         native_unit = getattr(obj, "native_unit", None)
         if callable(native_unit):
+            share = getattr(obj, "share_state", None)
+            name = self.shared_state_name(node)
+            if callable(share) and name:
+                share(name, int(os.environ.get("SCA_WORKER_RANK", "0") or 0))
             unit = native_unit(self._node_device(node))
             self.engine.bind_unit(node["name"], unit)
             self.units[node["name"]] = unit

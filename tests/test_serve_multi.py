@@ -1,0 +1,144 @@
+"""`serve --gpus N` as a multi-process deployment.
+
+* Shared router state: an epsilon-greedy MAB over N replica workers learns
+  from feedback that SO_REUSEPORT hands to ANY worker, as fast as one process
+  (the reference keeps one router object per deployment,
+  components/routers/epsilon-greedy/EpsilonGreedy.py:87-130).
+* Rank placement from the spec: a graph with ``rank:`` nodes runs as ONE
+  graph over the N processes (rank 0 front end, rank 1.. serve_peer), the
+  operator-built multi-component deployment
+  (operator/controllers/seldondeployment_controller.go:253-392).
+
+Both run on CPU devices (device -1: fabric payloads over sockets)."""
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.request
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _post(port, path, body, timeout=10):
+    req = urllib.request.Request(f"http://127.0.0.1:{port}{path}", data=json.dumps(body).encode(),
+                                 headers={"Content-Type": "application/json", "Connection": "close"})
+    return json.loads(urllib.request.urlopen(req, timeout=timeout).read())
+
+
+def _start(tmp_path, spec, n, extra=(), env_extra=None):
+    sp = tmp_path / "spec.json"
+    sp.write_text(json.dumps(spec))
+    hp, gp = _free_port(), _free_port()
+    log = open(tmp_path / "serve.log", "w")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, str(tmp_path)]), CUDA_VISIBLE_DEVICES="",
+               **(env_extra or {}))
+    p = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--spec", str(sp), "--gpus", str(n),
+                          "--device", "-1", "--http-port", str(hp), "--grpc-port", str(gp), "--admin-port", "0",
+                          "--threads", "2", "--log-level", "INFO", *extra],
+                         env=env, cwd=ROOT, start_new_session=True, stdout=log, stderr=subprocess.STDOUT)
+    return p, hp, tmp_path / "serve.log"
+
+
+def _wait_log(path, needle, count, timeout=120):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        if path.read_text().count(needle) >= count:
+            return True
+        time.sleep(0.2)
+    return False
+
+
+def _stop(p):
+    try:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+            return p.wait(timeout=90)
+        return p.returncode
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+
+
+def test_mab_feedback_to_any_worker_trains_every_worker(tmp_path):
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+            "graph": {"name": "mab", "type": "ROUTER", "implementation": "EPSILON_GREEDY",
+                      "parameters": [{"name": "n_branches", "value": "2", "type": "INT"},
+                                     {"name": "epsilon", "value": "0.1", "type": "FLOAT"},
+                                     {"name": "best_branch", "value": "0", "type": "INT"}],
+                      "children": [{"name": "b0", "type": "MODEL", "implementation": "SIMPLE_MODEL"},
+                                   {"name": "b1", "type": "MODEL", "implementation": "SIMPLE_MODEL"}]}}
+    p, hp, log = _start(tmp_path, spec, 4)
+    try:
+        assert _wait_log(log, "serving p:", 4), log.read_text()[-3000:]
+        req = {"data": {"ndarray": [[1.0, 2.0]]}}
+
+        def share_of_branch1(k):
+            return np.mean([_post(hp, "/api/v0.1/predictions", req)["meta"]["routing"]["mab"] == 1 for _ in range(k)])
+
+        assert share_of_branch1(80) < 0.3  # every worker starts on branch 0
+        # ONE feedback, on one connection: whichever worker takes it
+        _post(hp, "/api/v0.1/feedback", {"request": req, "response": {"meta": {"routing": {"mab": 1}},
+                                                                        "data": {"ndarray": [[0.0]]}},
+                                          "reward": 1.0})
+        # ... and every worker now routes to branch 1 (90% = 1 - epsilon)
+        share = share_of_branch1(200)
+        assert share > 0.8, share
+        assert _stop(p) == 0
+    finally:
+        _stop(p)
+    assert not [n for n in os.listdir("/dev/shm") if n.startswith(f"sca_state_{p.pid}_")]
+
+
+def test_rank_placed_spec_serves_through_the_cli(tmp_path):
+    (tmp_path / "mymodels.py").write_text(
+        "from seldon_core_amd.models import iris_logistic_regression\n"
+        "from seldon_core_amd.servers import SKLearnServer\n\n\n"
+        "class Iris(SKLearnServer):\n"
+        "    def __init__(self):\n"
+        "        super().__init__(model=iris_logistic_regression())\n")
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+            "graph": {"name": "ab", "type": "ROUTER", "implementation": "RANDOM_ABTEST",
+                      "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
+                      "children": [{"name": "a", "type": "MODEL", "rank": 1},
+                                   {"name": "b", "type": "MODEL", "rank": 2}]}}
+    p, hp, log = _start(tmp_path, spec, 3, extra=("--component", "a=mymodels.Iris", "--component", "b=mymodels.Iris"))
+    try:
+        assert _wait_log(log, "serving p:", 1), log.read_text()[-3000:]
+        text = log.read_text()
+        assert "rccl_peer" in text, text[-2000:]  # rank 0 reaches a and b through the fabric
+        from seldon_core_amd.models import iris_logistic_regression
+
+        lr = iris_logistic_regression()
+        rng = np.random.default_rng(0)
+        seen = set()
+        for i in range(40):
+            X = rng.normal(loc=4.0, scale=1.5, size=(1 + i % 4, 4))
+            out = _post(hp, "/api/v0.1/predictions", {"data": {"ndarray": X.tolist()}})
+            np.testing.assert_allclose(np.asarray(out["data"]["ndarray"]), lr.predict_proba(X), rtol=0, atol=1e-12)
+            seen.add(out["meta"]["routing"]["ab"])
+        assert seen == {0, 1}
+        assert _stop(p) == 0
+    finally:
+        _stop(p)
+    text = log.read_text()
+    assert text.count("done:") == 2, text[-3000:]  # both peer ranks left their loops on rank 0's stop
+
+
+def test_rank_placement_needs_enough_gpus(tmp_path):
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+            "graph": {"name": "m", "type": "MODEL", "rank": 3}}
+    p, _, log = _start(tmp_path, spec, 2)
+    assert p.wait(timeout=60) == 2
+    assert "places nodes on 4 ranks" in log.read_text()
