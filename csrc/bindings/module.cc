@@ -194,6 +194,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_class_names", &gpu::RowModel::set_class_names)
       .def("class_names", &gpu::RowModel::class_names)
       .def_property("flat_output", &gpu::RowModel::flat_output, &gpu::RowModel::set_flat_output)
+      .def_property("input_names", &gpu::RowModel::input_names, &gpu::RowModel::set_input_names)
       .def("clone", &gpu::RowModel::clone)
       .def("clone_on", [](const gpu::RowModel& mdl, int device) {
         auto* g = dynamic_cast<const gpu::GraphModel*>(&mdl);

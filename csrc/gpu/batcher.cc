@@ -273,6 +273,29 @@ void BatchedUnit::transform_input(const CallCtx& c, MsgPtr in, Done k) {
     for (size_t i = 1; i < shape.size(); ++i) cc *= shape[i];
     it.cols = int(cc);
   }
+  const auto& cols_want = model_->input_names();
+  if (!cols_want.empty() && !dd.names.empty() && int(dd.names.size()) == it.cols && dd.names != cols_want) {
+    // the request names its columns in another order than the model's
+    // signature: gather them into signature order (MLflow schema enforcement)
+    std::vector<int> src(cols_want.size());
+    std::string missing;
+    for (size_t c = 0; c < cols_want.size(); ++c) {
+      const auto f = std::find(dd.names.begin(), dd.names.end(), cols_want[c]);
+      if (f == dd.names.end()) missing += (missing.empty() ? "'" : ", '") + cols_want[c] + "'";
+      src[c] = int(f - dd.names.begin());
+    }
+    if (!missing.empty()) {
+      k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "request is missing signature column(s) [" + missing + "]")));
+      return;
+    }
+    std::vector<double> perm(size_t(it.rows) * cols_want.size());
+    for (int r = 0; r < it.rows; ++r)
+      for (size_t c = 0; c < cols_want.size(); ++c)
+        perm[size_t(r) * cols_want.size() + c] = it.xp[size_t(r) * it.cols + size_t(src[c])];
+    it.x = std::move(perm);
+    it.xp = it.x.data();
+    it.cols = int(cols_want.size());
+  }
   const int want = model_->in_cols();
   if (it.rows <= 0 || it.cols <= 0) {
     k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, model_->name() + " expects a non-empty 2-D numeric payload")));

@@ -40,6 +40,11 @@ class RowModel {
   // (e.g. xgboost Booster.predict): response shape [rows], no class names.
   bool flat_output() const { return flat_; }
   void set_flat_output(bool f) { flat_ = f; }
+  // Named input columns (an MLflow signature): a request whose
+  // `data.names` lists the same columns in another order is permuted into
+  // this order before batching; one missing a column is rejected.
+  const std::vector<std::string>& input_names() const { return in_names_; }
+  void set_input_names(std::vector<std::string> n) { in_names_ = std::move(n); }
   virtual void to_device(int device) = 0;
   // True if launch() needs X/out in device memory (no zero-copy host I/O).
   virtual bool device_io_only() const { return false; }
@@ -84,9 +89,11 @@ class RowModel {
   template <class T> std::shared_ptr<RowModel> with_meta(std::shared_ptr<T> m) const {
     m->names_ = names_;
     m->flat_ = flat_;
+    m->in_names_ = in_names_;
     return m;
   }
   std::vector<std::string> names_;
+  std::vector<std::string> in_names_;
   bool flat_ = false;
 };
 using RowModelPtr = std::shared_ptr<RowModel>;

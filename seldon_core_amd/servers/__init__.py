@@ -143,7 +143,17 @@ class MLFlowServer:
             return None
         from ..models import to_row_model
 
-        return to_row_model(m, "predict") if self.flavour == "sklearn" else to_row_model(m)
+        sig = self.signature
+        if sig is not None and sig.columns:
+            types = {c.get("type", "double") for c in sig.columns}
+            if not types <= {"double", "float"}:
+                return None  # integer / string columns: the Python path casts them
+        rm = to_row_model(m, "predict") if self.flavour == "sklearn" else to_row_model(m)
+        if rm is not None and sig is not None and sig.columns and all(sig.names):
+            # named signature: the native unit permutes requests that name the
+            # columns in another order (and rejects ones missing a column)
+            rm.input_names = list(sig.names)
+        return rm
 
 
 class TFServingProxy:

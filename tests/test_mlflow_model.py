@@ -68,6 +68,34 @@ def test_signature_reorders_named_columns(wine_dir):
         s.predict(X[:1, :5], [])
 
 
+def test_native_node_permutes_named_columns(wine_dir):
+    """The MLflow node served natively (linear kernel behind the batcher)
+    honours the signature too: permuted names are gathered back into
+    signature order, a missing column is rejected."""
+    import seldon_core_amd as sca
+
+    root, m, X = wine_dir
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+            "graph": {"name": "wine", "type": "MODEL", "implementation": "MLFLOW_SERVER", "modelUri": str(root)}}
+    dep = sca.Deployment(spec, device=-1)
+    try:
+        assert dep.engine.unit_kind("wine") == "gpu:linear"
+        perm = np.random.default_rng(1).permutation(len(WINE))
+        names = [WINE[i] for i in perm]
+        for payload in ({"ndarray": X[:4][:, perm].tolist()},
+                        {"tensor": {"shape": [4, len(WINE)], "values": X[:4][:, perm].ravel().tolist()}}):
+            out = dep.predict({"data": {"names": names, **payload}})
+            got = np.asarray(out["data"]["ndarray"] if "ndarray" in out["data"] else out["data"]["tensor"]["values"])
+            np.testing.assert_allclose(got.ravel(), m.predict(X[:4]), rtol=1e-12)
+        status, body = dep.predict_raw({"data": {"names": ["bogus"] + WINE[1:], "ndarray": X[:1].tolist()}})
+        assert status != 200 and "missing signature column" in json.dumps(body), body
+        # unnamed requests are taken in signature order
+        out = dep.predict({"data": {"ndarray": X[:2].tolist()}})
+        np.testing.assert_allclose(np.asarray(out["data"]["ndarray"]).ravel(), m.predict(X[:2]), rtol=1e-12)
+    finally:
+        dep.close()
+
+
 def test_python_function_only_maps_loader_module(tmp_path):
     from sklearn.linear_model import LinearRegression
 
