@@ -445,6 +445,7 @@ PYBIND11_MODULE(_C, m) {
           }
           auto tm = std::make_shared<gpu::TreeEnsembleModel>(std::move(s));
           if (d.contains("fused_reduce")) tm->set_fused_reduce(d["fused_reduce"].cast<bool>());
+          if (d.contains("whole_max_rows")) tm->set_whole_max_rows(d["whole_max_rows"].cast<int>());
           return std::static_pointer_cast<gpu::RowModel>(tm);
         });
 

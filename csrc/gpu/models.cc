@@ -74,6 +74,9 @@ static const int kPlanSizes[] = {4, 8, 16, 32, 64, 128, 256, 512};
 TreeEnsembleModel::TreeEnsembleModel(TreeEnsembleSpec spec) : spec_(std::move(spec)) {
   // SCA_TREE_FUSED=0/1 forces the single-launch fused-fold plan off / on (A/B runs)
   if (const char* f = std::getenv("SCA_TREE_FUSED")) fused_reduce_ = f[0] == '1';
+  // SCA_TREE_WHOLE_ROWS: largest batch served by the single-launch
+  // whole-ensemble kernel (0 = off)
+  if (const char* f = std::getenv("SCA_TREE_WHOLE_ROWS")) whole_max_rows_ = std::max(0, std::atoi(f));
   const int T = spec_.n_trees;
   if (T <= 0) throw std::runtime_error("TreeEnsembleModel: no trees");
   if (int(spec_.tree_group.size()) != T) spec_.tree_group.assign(size_t(T), 0);
@@ -186,7 +189,13 @@ void TreeEnsembleModel::plan_for(int rows, int* rows_per_block, int* plan_index,
   *plan_index = idx;
 }
 
+bool TreeEnsembleModel::uses_whole(int rows) const {
+  return spec_.depth > 0 && spec_.groups == 1 && rows <= whole_max_rows_;
+}
+
 bool TreeEnsembleModel::zero_copy_input_for(int rows, int cols) const {
+  // whole-ensemble kernel: each workgroup reads its rows once
+  if (uses_whole(rows)) return size_t(rows) * size_t(cols) * sizeof(double) <= (256u << 10);
   int rb, pi;
   plan_for(rows, &rb, &pi);
   // Every chunk's workgroups re-read their rows' tile: keep the host traffic of
@@ -216,6 +225,13 @@ bool TreeEnsembleModel::uses_fused(int rows) const {
 bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
                                     hipEvent_t done) {
   (void)cols;
+  if (uses_whole(rows)) {
+    kern::tree_perfect_whole(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
+                             spec_.depth, spec_.cmp_le, spec_.n_trees,
+                             kern::tree_whole_rows_per_block(spec_.n_trees, rows), d_base_.as<float>(), spec_.scale,
+                             spec_.transform, out, spec_.out_cols, s, done);
+    return done != nullptr;
+  }
   int rb, pi, lt;
   plan_for(rows, &rb, &pi, &lt);
   const Plan& p = *plans_[size_t(pi)];

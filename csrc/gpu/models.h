@@ -158,12 +158,21 @@ class TreeEnsembleModel : public RowModel {
   bool zero_copy_input() const override { return false; }  // every tree-chunk block stages the X tile
   // Host reads = rows x cols x 8 B x chunks: zero-copy while that stays small.
   bool zero_copy_input_for(int rows, int cols) const override;
-  std::shared_ptr<RowModel> clone() const override { return with_meta(std::make_shared<TreeEnsembleModel>(spec_)); }
+  std::shared_ptr<RowModel> clone() const override {
+    auto m = std::make_shared<TreeEnsembleModel>(spec_);
+    m->fused_reduce_ = fused_reduce_;
+    m->whole_max_rows_ = whole_max_rows_;
+    return with_meta(m);
+  }
   // Launch geometry chosen for a batch (exposed for tests/benchmarks).
   void plan_for(int rows, int* rows_per_block, int* plan_index, int* lds_trees = nullptr) const;
   // In-kernel last-workgroup slab fold for small batches (default off: slower
   // than the two-pass reduce on MI355X, see plan_for).
   void set_fused_reduce(bool on) { fused_reduce_ = on; }
+  // Batches up to this many rows of a single-output perfect ensemble run as
+  // one whole-ensemble launch (kern::tree_perfect_whole); 0 = never.
+  void set_whole_max_rows(int n) { whole_max_rows_ = n; }
+  bool uses_whole(int rows) const;
 
  private:
   bool launch_impl(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s, hipEvent_t done);
@@ -181,6 +190,7 @@ class TreeEnsembleModel : public RowModel {
   int max_chunks_ = 1;
   int device_ = -1;
   bool fused_reduce_ = false;
+  int whole_max_rows_ = 256;
 };
 
 // ------------------------------------------------------------- elementwise

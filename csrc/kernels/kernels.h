@@ -97,6 +97,14 @@ void tree_perfect_fused(const double* X, int rows, int F, const TreeNode* nodes,
 void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes, const int* tree_root, int cmp_le,
                        const int* chunk_begin, int n_chunks, int rows_per_block, double* partial,
                        const TreeReduceArgs& red, hipStream_t stream, hipEvent_t stop = nullptr);
+// Single-output perfect-tree ensembles, small batches: one 1024-thread
+// workgroup per tile of rows_per_block rows walks every tree, folds in LDS and
+// writes the transformed output -- one launch, no slab.  rows_per_block from
+// tree_whole_rows_per_block (power of two <= 16, <= 4 trees per thread).
+int tree_whole_rows_per_block(int n_trees, int rows);
+void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                        int cmp_le, int n_trees, int rows_per_block, const float* base_margin, float scale,
+                        int transform, double* out, int out_cols, hipStream_t stream, hipEvent_t stop = nullptr);
 
 // ------------------------------------------------------------ combiners
 // out = mean over N inputs (each [n] fp64). inputs: device array of pointers.

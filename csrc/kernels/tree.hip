@@ -49,22 +49,23 @@ __device__ __forceinline__ float tile_x(const float* xs, int32_t feat, int lrb) 
 // writes are consecutive addresses (conflict-free); rows past `rows` are
 // zero-filled so every thread can traverse unconditionally.  Loads are issued
 // kU at a time into registers before any LDS write (one round trip).
+template <int BS = kBlock>
 __device__ __forceinline__ void stage_tile(float* tile, const double* __restrict__ X, int row0, int rows, int RB,
                                            int lrb, int F) {
   constexpr int kU = 8;
   const int n = RB * F, nrow = min(RB, rows - row0);
-  for (int i0 = threadIdx.x; i0 < n; i0 += kBlock * kU) {
+  for (int i0 = threadIdx.x; i0 < n; i0 += BS * kU) {
     double v[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {  // branch-free: clamped address, select after the load
-      const int i = min(i0 + u * kBlock, n - 1);
+      const int i = min(i0 + u * BS, n - 1);
       const int r = i & (RB - 1), f = i >> lrb;
       const double x = X[size_t(row0 + min(r, nrow - 1)) * F + f];
       v[u] = r < nrow ? x : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const int i = i0 + u * kBlock;
+      const int i = i0 + u * BS;
       if (i < n) tile[i] = float(v[u]);
     }
   }
@@ -109,7 +110,7 @@ __device__ __forceinline__ double descend_perfect(const TreeNode* __restrict__ n
   } else {
     for (int d = 0; d < depth; ++d) level();
   }
-  double acc = 0.0;  // fp64 sums of fp32 leaves: exact in practice, so order-free (see reduce_write)
+  double acc = 0.0;  // fp64 sums of fp32 leaves: nearly order-free (see reduce_write)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const float v = lf[u][idx[u] - n_internal];
@@ -151,10 +152,13 @@ __device__ __forceinline__ void copy_to_lds(void* lds_dst, const void* gsrc, int
 // COHERENT: the slab is read back inside the same launch by the fused tail on
 // another XCD, so rows are written with agent-scope (sc1, write-through past
 // this XCD's L2) stores -- no whole-L2 writeback/invalidate fences needed.
-// Accumulators and the slab are fp64: the fp32 leaves of a model span few
-// binades, so their fp64 partial sums carry no rounding and the result does
-// not depend on how trees were chunked or rows grouped -- a row scores the
-// same in a batch of 1 or 4096 (the chunk plan follows the batch size).
+// Accumulators and the slab are fp64: while the fp32 leaves of a row's trees
+// span at most ~29 binades (53 - 24 bits, less log2(trees) of headroom) their
+// fp64 sums carry no rounding, so the result does not depend on how trees
+// were chunked or rows grouped and a row scores the same in a batch of 1 or
+// 4096.  Models whose late trees have leaves far below the early ones can
+// exceed that span; their scores are then nearly, not exactly, order-free
+// across batch sizes (the chunk plan follows the batch size).
 template <bool COHERENT>
 __device__ __forceinline__ void reduce_write(double* red, double acc, int RB, int row0, int rows, int chunk,
                                              double* __restrict__ partial) {
@@ -385,6 +389,64 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
   if constexpr (FUSED) fused_tail(partial, rows, n_chunks, red);
 }
 
+// Small batches, single-output models: ONE workgroup of 1024 threads owns a
+// tile of RB rows and the WHOLE ensemble (thread i -> row i % RB, trees
+// i / RB, i / RB + 1024 / RB, ...; RB is sized so a thread walks <= 4 trees,
+// one interleaved U = 4 round), folds its rows' sums in-workgroup (butterfly
+// + LDS across the 16 waves) and applies the objective transform -- one
+// launch per batch, no slab, no second kernel, no cross-workgroup
+// signalling.  The batch rows are read once per workgroup, so they come
+// straight from the batcher's pinned buffer (no H2D copy).
+constexpr int kWholeBlock = 1024;
+
+template <int D>
+__global__ __launch_bounds__(kWholeBlock) void perfect_whole(const double* __restrict__ X, int rows, int F,
+                                                             const TreeNode* __restrict__ nodes,
+                                                             const float* __restrict__ leaves, int depth, int cmp_le,
+                                                             int n_trees, int RB, int stage_lds,
+                                                             const float* __restrict__ base_margin, float scale,
+                                                             int transform, double* __restrict__ out, int out_cols) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  double* red = reinterpret_cast<double*>(lds);  // [16 waves][RB <= 16]
+  float* tile = lds + 2 * 256;                   // [F][RB] when staged
+  const int n_internal = (1 << depth) - 1;
+  const int lrb = __builtin_ctz(unsigned(RB));
+  const int row0 = int(blockIdx.x) * RB;
+  const int r_local = int(threadIdx.x) & (RB - 1);
+  const int slot = int(threadIdx.x) >> lrb;
+  const int tpr = kWholeBlock >> lrb;
+  if (stage_lds) {
+    stage_tile<kWholeBlock>(tile, X, row0, rows, RB, lrb, F);
+    __syncthreads();
+  }
+  const float* xs = tile + r_local;
+  const bool row_ok = row0 + r_local < rows;
+  const double* xg = X + size_t(min(row0 + r_local, rows - 1)) * F;
+  constexpr int U = 4;
+  double acc = 0.0;
+  if (stage_lds) {
+    for (int t = slot; t < n_trees; t += tpr * U)
+      acc += descend_perfect<D, U, true>(nodes, leaves, n_internal, depth, t, n_trees, tpr, 0, xs, lrb, xg, cmp_le);
+  } else if (row_ok) {
+    for (int t = slot; t < n_trees; t += tpr * U)
+      acc += descend_perfect<D, U, false>(nodes, leaves, n_internal, depth, t, n_trees, tpr, 0, xs, lrb, xg, cmp_le);
+  }
+  if (!row_ok) acc = 0.0;
+  for (int off = 32; off >= RB; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  const int lane = int(threadIdx.x) & 63, wave = int(threadIdx.x) >> 6;
+  if (lane < RB) red[wave * RB + lane] = acc;
+  __syncthreads();
+  if (int(threadIdx.x) < RB) {
+    const int r = row0 + int(threadIdx.x);
+    if (r < rows) {
+      double m[1] = {0.0};
+#pragma unroll
+      for (int w = 0; w < kWholeBlock / 64; ++w) m[0] += red[w * RB + threadIdx.x];
+      apply_transform<1>(m, 1, transform, scale, base_margin, out + size_t(r) * out_cols);
+    }
+  }
+}
+
 constexpr int kMaxGroups = 64;
 
 // Block = RB rows x (blockDim / RB) chunk-lanes: the lanes of a row sum a
@@ -512,6 +574,42 @@ void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes
                        hipStream_t s, hipEvent_t stop) {
   if (rows <= 0 || n_chunks <= 0) return;
   launch_sparse<true>(X, rows, F, nodes, tree_root, cmp_le, chunk_begin, n_chunks, RB, partial, red, s, stop);
+}
+
+int tree_whole_rows_per_block(int n_trees, int rows) {
+  int rb = 1;
+  while (rb < 16 && rb < rows && (long long)n_trees * (rb * 2) <= 4LL * kWholeBlock) rb <<= 1;
+  return rb;
+}
+
+void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                        int cmp_le, int n_trees, int RB, const float* base_margin, float scale, int transform,
+                        double* out, int out_cols, hipStream_t s, hipEvent_t stop) {
+  if (rows <= 0 || n_trees <= 0) return;
+  const bool stage = RB * F <= kMaxLdsFloats;
+  const uint32_t lds = uint32_t((2 * 256 + (stage ? ((RB * F + 3) & ~3) : 0)) * sizeof(float));
+  const dim3 grid((rows + RB - 1) / RB);
+#define SCA_WHOLE_LAUNCH(DD)                                                                                       \
+  do {                                                                                                            \
+    if (stop)                                                                                                     \
+      hipExtLaunchKernelGGL((perfect_whole<DD>), grid, dim3(kWholeBlock), lds, s, nullptr, stop, 0, X, rows, F,     \
+                            nodes, leaves, depth, cmp_le, n_trees, RB, int(stage), base_margin, scale, transform,  \
+                            out, out_cols);                                                                       \
+    else                                                                                                          \
+      hipLaunchKernelGGL((perfect_whole<DD>), grid, dim3(kWholeBlock), lds, s, X, rows, F, nodes, leaves, depth,   \
+                         cmp_le, n_trees, RB, int(stage), base_margin, scale, transform, out, out_cols);          \
+  } while (0)
+  switch (depth) {
+    case 4: SCA_WHOLE_LAUNCH(4); break;
+    case 5: SCA_WHOLE_LAUNCH(5); break;
+    case 6: SCA_WHOLE_LAUNCH(6); break;
+    case 7: SCA_WHOLE_LAUNCH(7); break;
+    case 8: SCA_WHOLE_LAUNCH(8); break;
+    case 9: SCA_WHOLE_LAUNCH(9); break;
+    case 10: SCA_WHOLE_LAUNCH(10); break;
+    default: SCA_WHOLE_LAUNCH(0);
+  }
+#undef SCA_WHOLE_LAUNCH
 }
 
 void tree_reduce(const double* partial, int rows, int n_chunks, const int* chunk_group, int groups,

@@ -157,6 +157,57 @@ def test_tree_scores_do_not_depend_on_the_batch(C_):
         unit.stop()
 
 
+@pytest.mark.parametrize("depth", [4, 8, 10, 12])
+@pytest.mark.parametrize("transform", [0, 3])
+def test_tree_whole_kernel_matches_chunked_and_cpu(C_, depth, transform):
+    """Single-launch whole-ensemble kernel (batches <= whole_max_rows) vs the
+    chunked two-kernel plan vs the host walker, over batch sizes that cross
+    every rows-per-block choice; NaNs take the default direction."""
+    from seldon_core_amd.models import synthetic_xgboost
+
+    ens = synthetic_xgboost(700 if depth < 12 else 60, depth, 24, seed=depth + 10 * transform)
+    d = ens.device_spec()
+    d["transform"] = transform
+    d["out_cols"] = 2 if transform == 3 else 1
+    whole = C_.tree_model(dict(d, whole_max_rows=256))
+    chunked = C_.tree_model(dict(d, whole_max_rows=0))
+    uw, uc = C_.BatchedUnit(whole, 0, max_batch=512), C_.BatchedUnit(chunked, 0, max_batch=512)
+    try:
+        rng = np.random.default_rng(depth)
+        for n in (1, 2, 3, 5, 16, 17, 64, 65, 200, 256):
+            X = rng.standard_normal((n, 24))
+            X[::5, 2] = np.nan
+            a, b = np.asarray(uw.run(X)), np.asarray(uc.run(X))
+            np.testing.assert_allclose(a, b, rtol=1e-13, atol=1e-13)
+            np.testing.assert_allclose(a.reshape(-1), whole.run_cpu(X).reshape(-1), rtol=2e-5, atol=2e-5)
+    finally:
+        uw.stop()
+        uc.stop()
+
+
+def test_tree_wide_leaf_range_is_nearly_order_free(C_):
+    """Leaves spanning ~40 binades (late trees' leaves scaled by 2^-40): the
+    fp64 sums may now round differently under another chunk plan, so a row's
+    score alone and inside a 4096-row batch agree to fp64 rounding rather than
+    bit for bit (the claim is 'nearly order-free')."""
+    from seldon_core_amd.models import synthetic_xgboost
+
+    ens = synthetic_xgboost(1000, 8, 32, seed=21)
+    d = ens.device_spec()
+    leaves = np.asarray(d["leaves"], dtype=np.float32).reshape(1000, -1).copy()
+    leaves[500:] *= np.float32(2.0 ** -40)
+    d["leaves"] = leaves.ravel()
+    unit = C_.BatchedUnit(C_.tree_model(d), 0, max_batch=4096)
+    try:
+        X = np.random.default_rng(2).normal(size=(4096, 32))
+        big = np.asarray(unit.run(X)).ravel()
+        for i in (0, 9, 4095):
+            alone = np.asarray(unit.run(X[i:i + 1])).ravel()[0]
+            assert abs(alone - big[i]) <= 1e-14 * max(1.0, abs(big[i])), (alone, big[i])
+    finally:
+        unit.stop()
+
+
 def test_tree_softmax_groups(C_):
     """multi:softprob-style: 3 groups, softmax transform."""
     from seldon_core_amd.models import to_row_model
