@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -52,7 +53,13 @@ class DeviceBuffer {
     if (!bytes) return;
     DeviceGuard g(device);
     SCA_HIP_CHECK(hipMalloc(&ptr_, bytes));
-    SCA_HIP_CHECK(hipMemset(ptr_, 0, bytes));  // workspaces may hold counters that must start at 0
+    // Zero it (workspaces may hold counters that must start at 0) and WAIT:
+    // hipMemset is queued on the null stream, which our non-blocking streams
+    // do not order against, so a buffer grown mid-stream could be zeroed
+    // after the copy that fills it -- tests/test_fabric_loopback.py caught a
+    // worker slot's fresh input buffer read back as zeros.
+    SCA_HIP_CHECK(hipMemsetAsync(ptr_, 0, bytes, nullptr));
+    SCA_HIP_CHECK(hipStreamSynchronize(nullptr));
   }
   void reset() {
     if (ptr_) {

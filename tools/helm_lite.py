@@ -7,7 +7,8 @@ to it, so ``helm template`` and this renderer produce the same documents:
 
 * ``{{ .Values.a.b }}``, ``{{ .Release.Name }}``, ``{{ .Release.Namespace }}``,
   ``{{ .Chart.Name }}``, ``{{ .Chart.Version }}``, ``{{ $var }}`` / ``{{ $var.field }}``
-* pipelines ``| toJson``, ``| quote``, ``| default <literal>``
+* ``{{ .Files.Get "files/x" }}`` (a file of the chart), pipelines ``| toJson``,
+  ``| quote``, ``| default <literal>``, ``| indent N``, ``| nindent N``
 * ``{{ if X }} ... {{ else }} ... {{ end }}`` (X: a path, ``not`` path, or
   ``eq`` path "literal"), ``{{ range $k, $v := X }}``, ``{{ range $v := X }}``
 * ``{{-`` / ``-}}`` whitespace trimming and ``{{/* comments */}}``.
@@ -100,7 +101,10 @@ def _literal(tok: str) -> Any:
 def _value(expr: str, ctx: Dict[str, Any]) -> Any:
     stages = [s.strip() for s in expr.split("|")]
     head = stages[0].split()
-    if head[0] == "not":
+    if head[0] == ".Files.Get":
+        with open(os.path.join(ctx["root"]["_chart_dir"], _literal(head[1]))) as f:
+            v = f.read()
+    elif head[0] == "not":
         v = not _truthy(_lookup(head[1], ctx))
     elif head[0] == "eq":
         a = _lookup(head[1], ctx) if head[1].startswith((".", "$")) else _literal(head[1])
@@ -118,6 +122,11 @@ def _value(expr: str, ctx: Dict[str, Any]) -> Any:
         elif fn == "default":
             if not _truthy(v):
                 v = _literal(args[0])
+        elif fn in ("indent", "nindent"):
+            pad = " " * int(args[0])
+            v = "\n".join(pad + ln if ln else ln for ln in _str(v).split("\n"))
+            if fn == "nindent":
+                v = "\n" + v
         else:
             raise ValueError(f"helm_lite: unsupported function {fn!r}")
     return v
@@ -185,7 +194,7 @@ def render_chart(chart_dir: str, name: str, namespace: str = "default", values: 
         k, _, v = s.partition("=")
         _set(vals, k, v)
     root = {"Values": vals, "Release": {"Name": name, "Namespace": namespace},
-            "Chart": {"Name": chart.get("name"), "Version": chart.get("version")}}
+            "Chart": {"Name": chart.get("name"), "Version": chart.get("version")}, "_chart_dir": chart_dir}
     docs: List[Dict] = []
     tdir = os.path.join(chart_dir, "templates")
     for fn in sorted(os.listdir(tdir)):
