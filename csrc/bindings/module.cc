@@ -883,6 +883,14 @@ PYBIND11_MODULE(_C, m) {
                              as_stream(s), lds_trees);
   });
   k.def("tree_lds_max_trees", &kern::tree_lds_max_trees);
+  k.def("tree_whole_rows_per_block", &kern::tree_whole_rows_per_block);
+  k.def("tree_perfect_whole", [](uintptr_t X, int rows, int F, uintptr_t nodes, uintptr_t leaves, int depth,
+                                 int cmp_le, int n_trees, int rb, uintptr_t base, float scale, int transform,
+                                 uintptr_t out, int out_cols, uintptr_t s) {
+    kern::tree_perfect_whole(P<const double>(X), rows, F, P<const kern::TreeNode>(nodes), P<const float>(leaves),
+                             depth, cmp_le, n_trees, rb, P<const float>(base), scale, transform, P<double>(out),
+                             out_cols, as_stream(s));
+  });
   k.def("tree_reduce", [](uintptr_t partial, int rows, int n_chunks, uintptr_t chunk_group, int groups,
                           uintptr_t base, float scale, int transform, uintptr_t out, int out_cols, uintptr_t s) {
     kern::tree_reduce(P<const double>(partial), rows, n_chunks, P<const int>(chunk_group), groups, P<const float>(base),

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 
 #include "kernels.h"
@@ -577,8 +578,15 @@ void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes
 }
 
 int tree_whole_rows_per_block(int n_trees, int rows) {
+  // trees one thread walks (SCA_TREE_WHOLE_TPT, default 4: one interleaved
+  // U = 4 round); fewer = more workgroups per batch
+  static const int tpt = [] {
+    const char* e = std::getenv("SCA_TREE_WHOLE_TPT");
+    const int v = e ? std::atoi(e) : 4;
+    return v < 1 ? 1 : v;
+  }();
   int rb = 1;
-  while (rb < 16 && rb < rows && (long long)n_trees * (rb * 2) <= 4LL * kWholeBlock) rb <<= 1;
+  while (rb < 16 && rb < rows && (long long)n_trees * (rb * 2) <= (long long)tpt * kWholeBlock) rb <<= 1;
   return rb;
 }
 

@@ -46,6 +46,12 @@ for s in $STEPS; do
       run prof_xgb 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_xgb" -o run --output-format csv -- \
         python3 bench.py --model xgb1000 --steps 3 --warmup 1 --step-requests 10000 ;;
     lstm) run lstm 300 python tools/kernel_microbench.py --only lstm --iters 20 ;;
+    tree_small) run tree_small 300 python tools/kernel_microbench.py --only tree_small --iters 200 ;;
+    prof_abtest)
+      export TMPDIR=/tmp
+      export SCA_BENCH_CLEAN_EXIT=1
+      run prof_abtest 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_abtest" -o run --output-format csv -- \
+        python3 bench.py --graph abtest --steps 3 --warmup 1 --step-requests 20000 ;;
     prof_lstm)
       export TMPDIR=/tmp
       run prof_lstm 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_lstm" -o run --output-format csv -- \

@@ -43,6 +43,71 @@ def _time_unit(name, unit, X, iters, extra):
     return rec
 
 
+def case_tree_small(iters):
+    """Serving-size batches of the xgb1000 model: the two-kernel chunked plan
+    (partial + reduce, the plan TreeEnsembleModel picks) vs the single-launch
+    whole-ensemble kernel at every rows-per-block choice."""
+    import torch
+
+    from seldon_core_amd import native
+
+    K = native().kernels
+    T, D, F = 1000, 8, 32
+    ni = (1 << D) - 1
+    g = torch.Generator().manual_seed(0)
+    thr = torch.randn(T * ni, generator=g)
+    feat = torch.randint(0, F, (T * ni,), generator=g, dtype=torch.int32)
+    nodes = torch.stack([thr.view(torch.int32), feat], 1).contiguous().cuda()
+    leaves = (torch.randn(T * (ni + 1), generator=g) * 0.01).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    out_rec = []
+    for rows in (1, 4, 10, 16, 64, 256):
+        X = torch.randn(rows, F, dtype=torch.float64, generator=g).cuda()
+        out = torch.empty(rows, dtype=torch.float64, device="cuda")
+        rb = 1 if rows == 1 else 2
+        while rb * 2 <= rows // 16 and rb < 64:
+            rb *= 2
+        chunk = max(256 // rb, (T * ((rows + rb - 1) // rb) + 2047) // 2048)
+        chunk = next(c for c in (4, 8, 16, 32, 64, 128, 256, 512) if c >= chunk) if chunk <= 512 else 512
+        begin = torch.unique_consecutive(torch.arange(0, T + chunk, chunk, dtype=torch.int32).clamp_(max=T)).cuda()
+        nc = begin.numel() - 1
+        group = torch.zeros(nc, dtype=torch.int32, device="cuda")
+        partial = torch.empty(nc * rows, dtype=torch.float64, device="cuda")
+
+        def two():
+            K.tree_perfect_partial(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0, begin.data_ptr(),
+                                   nc, rb, partial.data_ptr(), s, 0)
+            K.tree_reduce(partial.data_ptr(), rows, nc, group.data_ptr(), 1, 0, 1.0, 0, out.data_ptr(), 1, s)
+
+        def timed(fn):
+            for _ in range(5):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            return round(e0.elapsed_time(e1) * 1000.0 / iters, 2)
+
+        rec = {"case": "tree_small", "rows": rows, "two_kernel_us": timed(two), "chunks": nc, "chunk_rb": rb}
+        ref = out.clone()
+        for wrb in (1, 2, 4, 8, 16):
+            if wrb > 1 and wrb >= 2 * rows:
+                break
+
+            def whole(wrb=wrb):
+                K.tree_perfect_whole(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0, T, wrb, 0, 1.0,
+                                     0, out.data_ptr(), 1, s)
+
+            rec[f"whole_rb{wrb}_us"] = timed(whole)
+            rec[f"whole_rb{wrb}_maxdiff"] = float((out - ref).abs().max())
+        print(json.dumps(rec), flush=True)
+        out_rec.append(rec)
+    return out_rec
+
+
 def case_tree(iters):
     import torch
 
@@ -461,7 +526,7 @@ def main():
     ap.add_argument("--only", default="tree,vae,mlp,linear")
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
-    cases = {"tree": case_tree, "vae": case_vae, "mlp": case_mlp, "linear": case_linear,
+    cases = {"tree": case_tree, "tree_small": case_tree_small, "vae": case_vae, "mlp": case_mlp, "linear": case_linear,
              "mlp_torch": case_mlp_torch,
              "mlp_torch_fp64io": lambda it: case_mlp_torch(it, fp64_io=True), "vae_torch": case_vae_torch, "mlp_modes": case_mlp_modes,
              "lstm": case_lstm, "gemm": case_gemm, "latency": case_latency, "dense_prec": case_dense_prec, "mlp_torch_bf16": case_mlp_torch_bf16}
