@@ -89,3 +89,83 @@ def test_loadtesting_chart_args_parse():
     job, = _render("seldon-core-amd-loadtesting", sets=["feedback=true"])
     c = job["spec"]["template"]["spec"]["containers"][0]
     assert c["command"][-1] == "seldon_core_amd.loadtester" and "--feedback" in c["args"]
+
+
+@pytest.mark.parametrize("od", ["mahalanobis", "isolationforest", "vae", "seq2seq"])
+def test_od_transformer_chart_valid(od):
+    sdep, = _render("seldon-od-transformer", sets=[f"outlierDetection.type={od}"])
+    g = sdep["spec"]["predictors"][0]["graph"]
+    assert g["type"] == "TRANSFORMER" and g["name"] == "outlier-detector"
+    assert g["implementation"].endswith("_OD") and g["children"][0]["name"] == "classifier"
+    assert validate(apply_defaults(sdep)) == []
+    off, = _render("seldon-od-transformer", sets=["outlierDetection.enabled=false"])
+    assert off["spec"]["predictors"][0]["graph"]["name"] == "classifier"
+
+
+def test_od_transformer_chart_serves():
+    """Mahalanobis detector in front of the iris classifier, in-process: the
+    request is scored and tagged by the detector, then classified."""
+    from seldon_core_amd.models import iris_logistic_regression
+
+    sdep, = _render("seldon-od-transformer")
+    lr = iris_logistic_regression()
+    dep = sca.Deployment(sdep, components={"classifier": lr}, device=-1)
+    try:
+        X = np.random.default_rng(0).normal(loc=4.0, size=(3, 4))
+        out = dep.predict({"data": {"ndarray": X.tolist()}})
+        np.testing.assert_allclose(np.asarray(out["data"]["ndarray"]), lr.predict_proba(X), rtol=1e-12)
+        assert out["meta"]["requestPath"].keys() >= {"outlier-detector", "classifier"}
+    finally:
+        dep.close()
+
+
+def test_openvino_chart():
+    sdep, = _render("seldon-openvino")
+    pred = sdep["spec"]["predictors"][0]
+    g = pred["graph"]
+    assert g["implementation"] == "TENSORFLOW_SERVER"
+    params = {p["name"]: p["value"] for p in g["parameters"]}
+    assert params["rest_endpoint"] == "http://localhost:8001" and params["model_name"] == "squeezenet1.1"
+    c, = pred["componentSpecs"][0]["spec"]["containers"]
+    assert c["image"].startswith("intelaipg/openvino-model-server") and c["ports"][0]["containerPort"] == 8001
+    assert validate(apply_defaults(sdep)) == []
+
+
+def test_kafka_chart():
+    docs = _render("seldon-core-kafka")
+    kinds = sorted(d["kind"] for d in docs)
+    assert kinds == ["Deployment", "Service", "Service", "StatefulSet"]
+    sts = next(d for d in docs if d["kind"] == "StatefulSet")
+    env = {e["name"]: e["value"] for e in sts["spec"]["template"]["spec"]["containers"][0]["env"]}
+    assert env["KAFKA_PROCESS_ROLES"] == "broker,controller"
+    assert env["KAFKA_ADVERTISED_LISTENERS"] == "PLAINTEXT://rel-kafka.seldon.svc.cluster.local:9092"
+    logger = next(d for d in docs if d["kind"] == "Deployment")
+    args = logger["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert args[args.index("--kafka") + 1] == "rel-kafka.seldon.svc.cluster.local:9092"
+    from seldon_core_amd import request_logger
+
+    request_logger.main.__code__  # the module the container runs exists
+    persistent = _render("seldon-core-kafka", sets=["kafka.persistence=true", "requestLogger.enabled=false"])
+    assert [d["kind"] for d in persistent] == ["Service", "StatefulSet"]
+    assert "volumeClaimTemplates" in persistent[1]["spec"]
+
+
+def test_analytics_chart_ships_the_monitoring_dashboards():
+    import json
+
+    import yaml
+
+    docs = _render("seldon-core-analytics")
+    kinds = {d["kind"] for d in docs}
+    assert {"ConfigMap", "Deployment", "Service", "Secret", "ClusterRole", "ServiceAccount"} <= kinds
+    dash = next(d for d in docs if d["metadata"]["name"] == "rel-grafana-dashboards")
+    mon = os.path.join(ROOT, "monitoring", "grafana")
+    assert set(dash["data"]) == set(os.listdir(mon))
+    for name, text in dash["data"].items():
+        with open(os.path.join(mon, name)) as f:
+            assert json.loads(text) == json.load(f), name  # chart copies == monitoring/ sources
+    prom = next(d for d in docs if d["metadata"]["name"] == "rel-prometheus-config")
+    cfg = yaml.safe_load(prom["data"]["prometheus.yml"])
+    assert cfg["scrape_configs"][0]["kubernetes_sd_configs"] == [{"role": "pod"}]
+    with open(os.path.join(ROOT, "monitoring", "prometheus", "rules.yml")) as f:
+        assert yaml.safe_load(prom["data"]["rules.yml"]) == yaml.safe_load(f)
