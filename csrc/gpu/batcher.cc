@@ -1,6 +1,7 @@
 #include "batcher.h"
 
 #include "../core/roctx.h"
+#include "driver.h"
 
 #include <immintrin.h>
 
@@ -23,32 +24,6 @@ int device_count() {
 bool available() { return device_count() > 0; }
 
 namespace {
-
-// Idle-spin permits shared by every unit of the process: a graph with
-// several units (A/B, MAB replicas) otherwise keeps a device and a hand-off
-// thread per unit spinning on the CPU share the front end needs (2 CPUs of
-// 12 in the MAB profile).  SCA_MAX_SPINNERS, default 16: at 2 the MAB graph
-// served the same 0.78-0.80M pred/s on 11.0-11.4 instead of 12.3-12.5 server
-// CPUs (profiles/r03h_frontend_fp32); at HEAD, 16 over 4 permits serves
-// +3-10% on A/B (p99 1.62 vs 1.76-1.84 ms) and +2-4% on MAB, two interleaved
-// repetitions each (profiles/r03r_head/spin_ab).
-std::atomic<int> g_spinners{0};
-int max_spinners() {
-  static const int m = [] {
-    const char* e = std::getenv("SCA_MAX_SPINNERS");
-    return e ? std::max(0, std::atoi(e)) : 16;
-  }();
-  return m;
-}
-struct SpinPermit {
-  bool ok;
-  SpinPermit() : ok(g_spinners.fetch_add(1, std::memory_order_relaxed) < max_spinners()) {
-    if (!ok) g_spinners.fetch_sub(1, std::memory_order_relaxed);
-  }
-  ~SpinPermit() {
-    if (ok) g_spinners.fetch_sub(1, std::memory_order_relaxed);
-  }
-};
 
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -93,9 +68,6 @@ FaultSpec fault_from_env(int device) {
 }
 
 BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::move(model)), opts_(opts) {
-  if (const char* e = std::getenv("SCA_IDLE_SPIN_US")) idle_spin_us_ = std::max(0, std::atoi(e));
-  ho_spin_us_ = idle_spin_us_;
-  if (const char* e = std::getenv("SCA_HANDOFF_SPIN_US")) ho_spin_us_ = std::max(0, std::atoi(e));
   if (opts_.max_batch < 1) opts_.max_batch = 1;
   if (opts_.slots < 1) opts_.slots = 1;
   if (opts_.fail_threshold < 1) opts_.fail_threshold = 1;
@@ -117,8 +89,9 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
     if (opts_.cpu_batching) {
       cpu_ = true;
       for (int i = 0; i < opts_.slots; ++i) slots_.push_back(std::make_unique<Slot>());
-      handoff_th_ = std::thread([this] { handoff_loop(); });
-      device_th_ = std::thread([this] { device_loop(); });
+      for (auto& s : slots_) ps_.free_list.push_back(s.get());
+      driver_ = DeviceDriver::acquire(-1, false);  // launch() may compute inline: a pump of its own
+      driver_->add(this);
     }
     return;
   }
@@ -135,26 +108,20 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
     ensure_capacity(*s, opts_.max_batch, cols);
     slots_.push_back(std::move(s));
   }
+  for (auto& s : slots_) ps_.free_list.push_back(s.get());
   running_.store(true);
-  handoff_th_ = std::thread([this] { handoff_loop(); });
-  device_th_ = std::thread([this] { device_loop(); });
+  driver_ = DeviceDriver::acquire(opts_.device, true);  // one pump + hand-off thread pair per GPU
+  driver_->add(this);
 }
 
 BatchedUnit::~BatchedUnit() { stop(); }
 
 void BatchedUnit::stop() {
   if (!running_.exchange(false)) return;
-  {
-    std::lock_guard<std::mutex> g(mu_);
+  if (driver_) {
+    driver_->remove(this);  // completes everything taken or in flight, posts every response
+    driver_.reset();
   }
-  cv_submit_.notify_all();
-  if (device_th_.joinable()) device_th_.join();  // completes everything in flight
-  {
-    std::lock_guard<std::mutex> g(ho_mu_);
-    ho_stop_ = true;
-  }
-  ho_cv_.notify_all();
-  if (handoff_th_.joinable()) handoff_th_.join();  // posts what the device thread handed over
   std::deque<Item> rest;
   drain_shards(rest);
   for (auto& it : rest) it.k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "GPU unit stopped")));
@@ -352,12 +319,9 @@ void BatchedUnit::submit_item(Item it) {
     sh.n.fetch_add(1, std::memory_order_release);
     queued_n_.fetch_add(1, std::memory_order_seq_cst);
   }
-  // Pairs with the device thread's dev_sleeping_ store + queued_n_ re-check
-  // under mu_: either it sees this item or we see it asleep and wake it.
-  if (dev_sleeping_.load(std::memory_order_seq_cst)) {
-    { std::lock_guard<std::mutex> g(mu_); }
-    cv_submit_.notify_one();
-  }
+  // Pairs with the driver's sleeping_ store + queued re-check under its
+  // mutex: either it sees this item or we see it asleep and wake it.
+  if (driver_) driver_->notify();
 }
 
 bool BatchedUnit::launch(Slot* s) {
@@ -514,41 +478,6 @@ void BatchedUnit::Parcel::run() {
   keep->put(this);
 }
 
-void BatchedUnit::handoff_loop() {
-  std::vector<Handoff> batch;
-  std::vector<Parcel*> spare;
-  while (true) {
-    {
-      std::unique_lock<std::mutex> lk(ho_mu_);
-      for (auto& h : batch) ho_free_.push_back(std::move(h));  // emptied below: capacity goes back
-      batch.clear();
-      if (ho_q_.empty() && !ho_stop_ && ho_spin_us_ > 0) {  // brief spin before sleeping (see device_loop)
-        lk.unlock();
-        SpinPermit permit;
-        // (the clock is read every 32 pauses: a vDSO clock_gettime per pause
-        // was ~10% of the serving process's CPU with several units spinning)
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(ho_spin_us_);
-        for (unsigned n = 1; permit.ok && !ho_pending_.load(std::memory_order_acquire); ++n) {
-          _mm_pause();
-          if ((n & 31) == 0 && std::chrono::steady_clock::now() >= until) break;
-        }
-        lk.lock();
-      }
-      if (ho_q_.empty()) {
-        if (ho_stop_) break;
-        ho_sleeping_ = true;
-        ho_cv_.wait(lk, [&] { return ho_stop_ || !ho_q_.empty(); });
-        ho_sleeping_ = false;
-        if (ho_q_.empty()) break;  // stopping with nothing left
-      }
-      batch.swap(ho_q_);
-      ho_pending_.store(false, std::memory_order_relaxed);
-    }
-    for (auto& h : batch) post_responses(h, spare);
-  }
-  for (Parcel* p : spare) delete p;
-}
-
 // One parcel per front-end executor: its task builds the responses and runs
 // the continuations on that thread.
 void BatchedUnit::post_responses(Handoff& h, std::vector<Parcel*>& spare) {
@@ -637,14 +566,8 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     // answered here, before the slot is reused.
     const int oc = s->out_cols;
     const double* out = cpu_ ? s->cpu_out.data() : s->h_out.host<double>();
-    Handoff h;
-    {
-      std::lock_guard<std::mutex> g(ho_mu_);
-      if (!ho_free_.empty()) {  // reuse a drained hand-off's buffers
-        h = std::move(ho_free_.back());
-        ho_free_.pop_back();
-      }
-    }
+    Handoff h = driver_->take_free_handoff();  // reuse a drained hand-off's buffers
+    h.unit = this;
     h.out_cols = oc;
     size_t row = 0;
     for (auto& it : items) {
@@ -660,14 +583,7 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     }
     if (!h.items.empty()) {
       h.out.assign(out, out + size_t(s->rows) * oc);
-      bool wake;
-      {
-        std::lock_guard<std::mutex> g(ho_mu_);
-        ho_q_.push_back(std::move(h));
-        wake = ho_sleeping_;
-      }
-      ho_pending_.store(true, std::memory_order_release);
-      if (wake) ho_cv_.notify_one();
+      driver_->push_handoff(std::move(h));
     }
   }
   items.clear();
@@ -679,88 +595,75 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
   stats_.gpu_busy_s += busy;
 }
 
-void BatchedUnit::device_loop() {
-  if (!cpu_) (void)hipSetDevice(opts_.device);
-  std::vector<Slot*> free_list, inflight;
-  for (auto& s : slots_) free_list.push_back(s.get());
-  std::deque<Item> pending;  // taken from the shards, not yet in a slot (device thread only)
+// One round for this unit on its driver's pump thread (see driver.h).
+bool BatchedUnit::pump(bool watch, bool& busy) {
   using clk = std::chrono::steady_clock;
-  clk::time_point wait_start{};
-  int spins = 0;
-  while (true) {
-    // ---- take what the front ends queued (O(1) under the lock: producers
-    // never wait behind batch formation), then launch everything that fits
-    // into the free slots from the device thread's own backlog
-    if (inflight.empty() && pending.empty()) {
-      // Brief idle spin first: a closed-loop caller's next request usually
-      // arrives within tens of microseconds, and a condition-variable wake-up
-      // costs about that much again.
-      if (idle_spin_us_ > 0 && queued_n_.load(std::memory_order_acquire) == 0) {
-        SpinPermit permit;
-        const auto until = clk::now() + std::chrono::microseconds(idle_spin_us_);
-        for (unsigned n = 1; permit.ok && queued_n_.load(std::memory_order_acquire) == 0 &&
-                             running_.load(std::memory_order_relaxed);
-             ++n) {
-          _mm_pause();
-          if ((n & 31) == 0 && clk::now() >= until) break;
-        }
+  PumpState& P = ps_;
+  bool progress = false;
+  // ---- take what the front ends queued (O(1) under each shard's lock:
+  // producers never wait behind batch formation), then launch everything
+  // that fits into the free slots
+  if (!P.free_list.empty() && queued_n_.load(std::memory_order_acquire) > 0) drain_shards(P.pending);
+  bool hold = false;
+  if (opts_.max_wait_us > 0 && P.inflight.empty() && !P.pending.empty()) {
+    // idle device: give a lone request up to max_wait_us to gather company
+    int64_t rows = queued_rows_.load(std::memory_order_relaxed);
+    for (const auto& it : P.pending) rows += it.rows;
+    if (rows < opts_.max_batch) {
+      const auto now = clk::now();
+      if (!P.holding) {
+        P.holding = true;
+        P.hold_start = now;
       }
+      hold = now - P.hold_start < std::chrono::microseconds(opts_.max_wait_us) && running_.load();
     }
-    if (inflight.empty() && pending.empty()) {
-      std::unique_lock<std::mutex> lk(mu_);
-      dev_sleeping_.store(true, std::memory_order_seq_cst);
-      cv_submit_.wait(lk, [&] { return !running_.load() || queued_n_.load(std::memory_order_seq_cst) > 0; });
-      if (running_.load() && opts_.max_wait_us > 0 && queued_rows_.load() < opts_.max_batch) {
-        const auto deadline = clk::now() + std::chrono::microseconds(opts_.max_wait_us);
-        cv_submit_.wait_until(lk, deadline,
-                              [&] { return !running_.load() || queued_rows_.load() >= opts_.max_batch; });
-      }
-      dev_sleeping_.store(false, std::memory_order_relaxed);
-      if (!running_.load()) break;
+  }
+  if (!hold) P.holding = false;
+  while (!hold && !P.pending.empty() && !P.free_list.empty()) {
+    Slot* s = P.free_list.back();
+    P.free_list.pop_back();
+    int rows = 0;
+    const int cols = P.pending.front().cols;
+    while (!P.pending.empty()) {
+      Item& it = P.pending.front();
+      if (!s->items.empty() && (it.cols != cols || rows + it.rows > opts_.max_batch)) break;
+      rows += it.rows;
+      s->items.push_back(std::move(it));
+      P.pending.pop_front();
     }
-    if (!free_list.empty() && queued_n_.load(std::memory_order_acquire) > 0) drain_shards(pending);
-    while (!pending.empty() && !free_list.empty()) {
-      Slot* s = free_list.back();
-      free_list.pop_back();
-      int rows = 0;
-      const int cols = pending.front().cols;
-      while (!pending.empty()) {
-        Item& it = pending.front();
-        if (!s->items.empty() && (it.cols != cols || rows + it.rows > opts_.max_batch)) break;
-        rows += it.rows;
-        s->items.push_back(std::move(it));
-        pending.pop_front();
-      }
-      s->rows = rows;
-      s->cols = cols;
-      const auto t0 = clk::now();
-      const bool ok = launch(s);
-      launch_cpu_s_.store(launch_cpu_s_.load(std::memory_order_relaxed) +
-                              std::chrono::duration<double>(clk::now() - t0).count(),
-                          std::memory_order_relaxed);
-      (ok ? inflight : free_list).push_back(s);
-    }
-    if (inflight.empty()) continue;
-    // ---- reap finished batches
-    bool progress = false;
+    s->rows = rows;
+    s->cols = cols;
+    const auto t0 = clk::now();
+    const bool ok = launch(s);
+    launch_cpu_s_.store(launch_cpu_s_.load(std::memory_order_relaxed) +
+                            std::chrono::duration<double>(clk::now() - t0).count(),
+                        std::memory_order_relaxed);
+    (ok ? P.inflight : P.free_list).push_back(s);
+    progress = true;
+  }
+  // ---- reap finished batches
+  if (!P.inflight.empty()) {
     const int hang_ms = hang_ms_.load(std::memory_order_relaxed);
     // The clock is read only when a check needs it: the injected-hang test
-    // on completion, and the watchdog on every 32nd poll of a busy slot while
-    // spinning (every poll once the loop yields / sleeps).
+    // on completion, and the watchdog when the driver asks (`watch`).
     clk::time_point now{};
     bool have_now = false;
     auto now_ = [&] {
-      if (!have_now) { now = clk::now(); have_now = true; }
+      if (!have_now) {
+        now = clk::now();
+        have_now = true;
+      }
       return now;
     };
-    const bool watch = opts_.hang_timeout_ms > 0 && (spins >= 512 || (spins & 31) == 0);  // every poll once yielding
-    for (size_t i = 0; i < inflight.size();) {
-      Slot* s = inflight[i];
-      hipError_t st = cpu_ ? (!s->call || s->call->done() ? hipSuccess : hipErrorNotReady) : hipEventQuery(s->ev.get());
+    const bool wd = opts_.hang_timeout_ms > 0 && watch;
+    for (size_t i = 0; i < P.inflight.size();) {
+      Slot* s = P.inflight[i];
+      hipError_t st =
+          cpu_ ? (!s->call || s->call->done() ? hipSuccess : hipErrorNotReady) : hipEventQuery(s->ev.get());
       if (st == hipSuccess && hang_ms > 0 && now_() - s->t_launch < std::chrono::milliseconds(hang_ms))
         st = hipErrorNotReady;  // injected slow / hung device
       if (st == hipErrorNotReady) {
-        if (watch && !s->abandoned && now_() - s->t_launch > std::chrono::milliseconds(opts_.hang_timeout_ms))
+        if (wd && !s->abandoned && now_() - s->t_launch > std::chrono::milliseconds(opts_.hang_timeout_ms))
           abandon(s);
         // Slots are polled in launch order and the poll stops at the first
         // busy one (an hipEventQuery per slot per spin was ~3% of serving
@@ -775,54 +678,46 @@ void BatchedUnit::device_loop() {
       complete_cpu_s_.store(complete_cpu_s_.load(std::memory_order_relaxed) +
                                 std::chrono::duration<double>(clk::now() - t0).count(),
                             std::memory_order_relaxed);
-      inflight.erase(inflight.begin() + long(i));
-      free_list.push_back(s);
+      P.inflight.erase(P.inflight.begin() + long(i));
+      P.free_list.push_back(s);
       progress = true;
     }
-    if (progress) { spins = 0; continue; }
-    if (abandoned_slots_.load(std::memory_order_relaxed) >= int(slots_.size())) {
-      // Wedged device: answer what is still queued instead of letting it wait.
-      std::deque<Item> rest;
-      drain_shards(rest);
-      for (auto& it : pending) rest.push_back(std::move(it));
-      pending.clear();
-      if (!rest.empty()) {
-        auto e = device_error(ApiError::UNAVAILABLE, "every batch slot of this GPU is wedged");
-        for (auto& it : rest) {
-          inflight_rows_.fetch_sub(it.rows, std::memory_order_relaxed);
-          it.k(Outcome::fail(e));
-        }
+  }
+  if (!progress && abandoned_slots_.load(std::memory_order_relaxed) >= int(slots_.size())) {
+    // Wedged device: answer what is still queued instead of letting it wait.
+    std::deque<Item> rest;
+    drain_shards(rest);
+    for (auto& it : P.pending) rest.push_back(std::move(it));
+    P.pending.clear();
+    if (!rest.empty()) {
+      auto e = device_error(ApiError::UNAVAILABLE, "every batch slot of this GPU is wedged");
+      for (auto& it : rest) {
+        inflight_rows_.fetch_sub(it.rows, std::memory_order_relaxed);
+        it.k(Outcome::fail(e));
       }
     }
-    if (!opts_.spin_wait && !cpu_) {  // low-CPU mode: block on the oldest batch
-      if (opts_.hang_timeout_ms > 0 || hang_ms > 0)
-        std::this_thread::sleep_for(std::chrono::microseconds(20));  // stay able to run the watchdog
-      else
-        (void)hipEventSynchronize(inflight.front()->ev.get());
-      continue;
-    }
-    if (!free_list.empty() && (!pending.empty() || queued_n_.load(std::memory_order_acquire) > 0))
-      continue;  // new work: launch it
-    // Spin through the usual 10-50 us round trip; back off if the GPU is slow
-    // so a long kernel does not burn a core (and CPU quota) for nothing.
-    if (spins++ == 0) wait_start = clk::now();
-    if (spins < 512) {
-      _mm_pause();
-    } else if (clk::now() - wait_start < std::chrono::microseconds(200)) {
-      std::this_thread::yield();
-    } else {
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
   }
-  // Shutdown: finish (and answer) everything already launched.  An
-  // asynchronous CPU call gets a bounded wait (it owns its buffers, so one
-  // that never finishes is dropped safely and its requests fail).
-  for (Slot* s : inflight) {
+  busy = !P.inflight.empty() || !P.pending.empty();
+  return progress;
+}
+
+// Shutdown (pump thread, from DeviceDriver::retire): launch what was taken,
+// then finish and answer everything in flight.  An asynchronous CPU call gets
+// a bounded wait (it owns its buffers, so one that never finishes is dropped
+// safely and its requests fail).
+void BatchedUnit::finish_all() {
+  using clk = std::chrono::steady_clock;
+  PumpState& P = ps_;
+  const auto until = clk::now() + std::chrono::seconds(10);
+  while (!P.pending.empty() && clk::now() < until) {
+    bool busy = false;
+    if (!pump(true, busy)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  for (Slot* s : P.inflight) {
     hipError_t st = hipSuccess;
     if (!cpu_) {
       st = hipEventSynchronize(s->ev.get());
     } else if (s->call) {
-      const auto until = clk::now() + std::chrono::seconds(10);
       while (!s->call->done() && clk::now() < until) std::this_thread::sleep_for(std::chrono::microseconds(50));
       if (!s->call->done()) {
         s->call.reset();
@@ -830,7 +725,24 @@ void BatchedUnit::device_loop() {
       }
     }
     complete(s, st);
+    P.free_list.push_back(s);
   }
+  P.inflight.clear();
+  for (auto& it : P.pending) {
+    inflight_rows_.fetch_sub(it.rows, std::memory_order_relaxed);
+    it.k(Outcome::fail(make_error(ApiError::UNAVAILABLE, "GPU unit stopped")));
+  }
+  P.pending.clear();
+}
+
+// Low-CPU mode (spin_wait off), the only busy unit of its driver: block on
+// its oldest batch -- unless the hang watchdog or an injected hang needs the
+// pump to keep polling.
+bool BatchedUnit::block_on_oldest() {
+  if (cpu_ || ps_.inflight.empty() || opts_.hang_timeout_ms > 0 || hang_ms_.load(std::memory_order_relaxed) > 0)
+    return false;
+  (void)hipEventSynchronize(ps_.inflight.front()->ev.get());
+  return true;
 }
 
 ErrPtr BatchedUnit::device_error(ApiError kind, std::string info) {

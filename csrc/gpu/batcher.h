@@ -10,8 +10,10 @@
 //   request's continuation is posted back to the front-end thread that owns
 //   it (Executor), which builds the response and walks on through the graph.
 //
-// One device thread per unit does all launching and completion polling, so
-// the unit costs one core while busy and none while idle; the per-request
+// One device thread per GPU (DeviceDriver, driver.h) does all launching and
+// completion polling for every unit placed on that GPU, and one hand-off
+// thread per GPU posts their responses, so a GPU costs two cores while busy
+// and none while idle however many graph nodes it serves; the per-request
 // work (response construction, meta merge, serialisation) runs on the
 // front-end threads.  Batching is "greedy continuous": when the device is
 // idle a lone request is launched immediately (latency = one launch); while
@@ -23,6 +25,7 @@
 #pragma once
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <memory>
@@ -34,6 +37,8 @@
 #include "models.h"
 
 namespace sca::gpu {
+
+class DeviceDriver;
 
 struct BatcherOptions {
   int device = 0;            // -1 = run on the CPU (reference path)
@@ -122,6 +127,7 @@ class BatchedUnit : public Unit {
 
   void stop();
 
+  friend class DeviceDriver;
   // Response construction shared with posted continuations (outlives no unit
   // state it does not own).
   struct RespInfo {
@@ -168,6 +174,8 @@ class BatchedUnit : public Unit {
   // One completed batch on its way to the front-end threads: the requests and
   // one copy of the slot's output rows (the slot is reused at once).
   struct Handoff {
+    BatchedUnit* unit = nullptr;
+    bool fence = false;        // marker: every earlier hand-off of `unit` has been posted
     std::vector<Item> items;
     std::vector<size_t> offs;  // each item's first output value in `out`
     std::vector<double> out;
@@ -198,8 +206,15 @@ class BatchedUnit : public Unit {
   };
 
   void ensure_capacity(Slot& s, int rows, int cols);
-  void device_loop();
-  void handoff_loop();
+  // Driven by the DeviceDriver thread of this unit's GPU (one thread per GPU
+  // pumps every unit placed there): one round of take queued requests ->
+  // launch into free slots -> reap finished batches.  Returns whether it made
+  // progress; `busy` = batches in flight or requests taken but not launched.
+  bool pump(bool watch, bool& busy);
+  void finish_all();            // stop(): launch what was taken, complete everything in flight
+  bool block_on_oldest();       // low-CPU mode: wait for the oldest batch (false: cannot here)
+  bool has_queued() const { return queued_n_.load(std::memory_order_acquire) > 0; }
+  bool spin_wait() const { return opts_.spin_wait && !cpu_; }
   void post_responses(Handoff& h, std::vector<Parcel*>& spare);
   bool launch(Slot* s);
   void complete(Slot* s, hipError_t st);
@@ -230,9 +245,6 @@ class BatchedUnit : public Unit {
   static constexpr int kShards = 16;
   Shard shards_[kShards];
   void drain_shards(std::deque<Item>& into);
-  std::mutex mu_;                       // device-thread sleep / wake-up only
-  std::condition_variable cv_submit_;
-  std::atomic<bool> dev_sleeping_{false};
   std::atomic<int64_t> queued_rows_{0};
   std::atomic<int> queued_n_{0};        // items in the shards (the device thread's "work waiting" test)
   std::atomic<bool> running_{false};
@@ -241,21 +253,16 @@ class BatchedUnit : public Unit {
   bool zc_input_ = true;    // model reads X once per element (zero-copy input is cheaper than a DMA)
   bool segmented_ = false;
   bool cpu_ = false;        // device -1 with cpu_batching
-  std::thread device_th_;
-  // Response hand-off thread: groups a completed batch's requests by front-end
-  // executor and posts them (eventfd wake-ups), off the device thread, which
-  // only launches and reaps batches.
-  std::thread handoff_th_;
-  std::mutex ho_mu_;
-  std::condition_variable ho_cv_;
-  std::vector<Handoff> ho_q_;   // guarded by ho_mu_
-  std::vector<Handoff> ho_free_;  // emptied hand-offs, reused by the device thread (guarded by ho_mu_)
+  // Device-thread state (touched only by the driver's pump thread)
+  struct PumpState {
+    std::vector<Slot*> free_list, inflight;
+    std::deque<Item> pending;  // taken from the shards, not yet in a slot
+    std::chrono::steady_clock::time_point hold_start{};
+    bool holding = false;      // max_wait_us: waiting for a fuller first batch
+  };
+  PumpState ps_;
+  std::shared_ptr<DeviceDriver> driver_;  // the thread pair that pumps this unit and posts its responses
   std::shared_ptr<ParcelPool> parcels_ = std::make_shared<ParcelPool>();
-  bool ho_sleeping_ = false;    // guarded by ho_mu_
-  bool ho_stop_ = false;        // guarded by ho_mu_
-  std::atomic<bool> ho_pending_{false};  // ho_q_ non-empty (the hand-off thread's idle spin reads it)
-  int idle_spin_us_ = 50;       // spin this long before sleeping when idle (SCA_IDLE_SPIN_US)
-  int ho_spin_us_ = 50;         // the hand-off thread's idle spin (SCA_HANDOFF_SPIN_US, default the same)
   mutable std::mutex stats_mu_;
   BatcherStats stats_;
   // device-thread CPU time (single writer: the device thread; relaxed reads)

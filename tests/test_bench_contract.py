@@ -119,11 +119,15 @@ def test_bench_calibrated_window_hits_target():
     target = 3.0
     env = _cpu_env(SCA_BENCH_TARGET_S=str(target), SCA_BENCH_EXTRA_S="1.0")
     cmd = [sys.executable, "bench.py", "--steps", "4", "--warmup", "2", "--users", "16"]
-    res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
-    assert res.returncode == 0, res.stderr[-3000:]
-    line = _json_lines(res.stdout)[-1]
-    assert 0.8 * target <= line["timed_region_s"] <= 2.0 * target, line["timed_region_s"]
-    assert 0.8 <= line["grpc"]["window_s"] <= 3.0, line["grpc"]
+    seen = []
+    for _ in range(2):  # a CPU box shared with other test workers changes the rate under the probe: one retry
+        res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+        assert res.returncode == 0, res.stderr[-3000:]
+        line = _json_lines(res.stdout)[-1]
+        seen.append((line["timed_region_s"], line["grpc"].get("window_s")))
+        if 0.8 * target <= line["timed_region_s"] <= 2.0 * target and 0.8 <= line["grpc"]["window_s"] <= 3.0:
+            return
+    raise AssertionError(f"calibrated windows (timed, grpc) {seen} outside 0.8-2x of {target} s / 1 s")
 
 
 def test_step_size():

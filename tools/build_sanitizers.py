@@ -34,6 +34,7 @@ SOURCES = [
     "core/engine.cc", "core/units.cc", "core/msglog.cc", "core/roctx.cc",
     "server/http_server.cc", "server/grpc_server.cc", "server/remote_unit.cc",
     "gpu/batcher.cc",  # host machinery only: the stress driver runs it on its CPU path
+    "gpu/driver.cc",
     "tests/core_stress.cc",
 ]
 FLAGS = {
