@@ -75,7 +75,7 @@ try:
     ORIG_AFFINITY = sorted(os.sched_getaffinity(0))
 except AttributeError:
     ORIG_AFFINITY = []
-VARIANTS = ("abtest", "pipeline", "mab", "replicas")
+VARIANTS = ("abtest", "pipeline", "mab", "replicas", "reuseport")
 RANK_VARIANTS = ("abtest", "pipeline", "mab")
 SPAN = {"abtest": 2, "pipeline": 4}  # GPUs a graph spans (mab / replicas: all of the job's)
 
@@ -580,6 +580,9 @@ def variant_child(args) -> None:
         except OSError:
             pass
     kind = args.variant_child
+    if kind == "reuseport":
+        print(json.dumps(reuseport_child(args, budget)), flush=True)
+        return
     out = {"error": "unfinished"}
     dep = h = None
     try:
@@ -655,6 +658,94 @@ def variant_child(args) -> None:
         except Exception:
             pass
     print(json.dumps(out), flush=True)
+
+
+def reuseport_child(args, budget: bk.Budget) -> dict:
+    """The production multi-worker path: ``serve --gpus
+    N`` -- the Supervisor's N worker processes, one per GPU, all bound to ONE
+    port with SO_REUSEPORT (the reference's replicas behind one Service,
+    seldondeployment_controller.go:296-302) -- driven by one load generator
+    with N x users connections.  Reports the whole-endpoint rate and each
+    worker's share of the requests (the kernel's connection balancing)."""
+    import signal
+
+    n = args.span
+    work = tempfile.mkdtemp(prefix="sca_reuseport_")
+    proc = None
+    try:
+        with open(os.path.join(work, "bench_iris.py"), "w") as f:
+            f.write("from seldon_core_amd.models import iris_logistic_regression\n"
+                    "from seldon_core_amd.servers import SKLearnServer\n\n\n"
+                    "class Iris(SKLearnServer):\n"
+                    "    def __init__(self):\n"
+                    "        super().__init__(model=iris_logistic_regression())\n")
+        spec = {"name": "reuseport", "componentSpecs": [{"spec": {"containers": []}}],
+                "graph": {"name": "classifier", "type": "MODEL", "children": []}}
+        with open(os.path.join(work, "spec.json"), "w") as f:
+            json.dump(spec, f)
+        stats = os.path.join(work, "stats")
+        os.makedirs(stats)
+        port = _free_port()
+        cpus = bk.cpu_budget()
+        threads = max(2, int(cpus * 0.5 / n))
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("TORCHELASTIC_", "RANK", "LOCAL_RANK",
+                                                                       "WORLD_SIZE", "LOCAL_WORLD_SIZE"))}
+        env.update(PYTHONPATH=os.pathsep.join([ROOT, work]), SCA_WORKER_STATS_DIR=stats)
+        cmd = [sys.executable, "-m", "seldon_core_amd.serve", "--spec", os.path.join(work, "spec.json"),
+               "--gpus", str(n), "--http-port", str(port), "--grpc-port", str(_free_port()), "--admin-port", "0",
+               "--threads", str(threads), "--component", "classifier=bench_iris.Iris", "--log-level", "INFO"]
+        import torch
+
+        if torch.cuda.device_count() < n:  # (counting does not initialise the GPU on this stack)
+            cmd += ["--device", "-1"]
+        log = open(os.path.join(work, "serve.log"), "w")
+        proc = subprocess.Popen(cmd, env=env, cwd=work, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+        deadline = time.time() + min(90.0, budget.left(10))
+        while time.time() < deadline:
+            with open(os.path.join(work, "serve.log")) as f:
+                if f.read().count("serving reuseport") >= n:
+                    break
+            if proc.poll() is not None:
+                raise RuntimeError(f"serve --gpus {n} exited rc={proc.returncode}")
+            time.sleep(0.2)
+        else:
+            raise TimeoutError(f"{n} workers not up")
+        wl = bk.Workload("iris")
+        body = wl.rest_body()
+        expect = bk.rest_expect(port, body)
+        users = args.users * n
+        cthreads = max(1, min(32, int(cpus * 0.3)))
+        rate = bk.probe_rate(port, "rest", body, users, cthreads, lambda: budget.timeout(reserve=10), min_s=PROBE_S,
+                             expect=expect)
+        lg = bk.run_loadgen(port, 2, 0, "rest", body, users, cthreads, bk.window_requests(rate, EXTRA_WINDOW_S),
+                            budget.timeout(reserve=10), expect=expect)
+        os.killpg(proc.pid, signal.SIGTERM)  # drain: every worker files its request count
+        proc.wait(timeout=max(5.0, budget.left(5)))
+        per = []
+        for fn in sorted(os.listdir(stats)):
+            with open(os.path.join(stats, fn)) as f:
+                per.append(json.load(f))
+        counts = [w["requests"] for w in per]
+        return {"graph": f"single-model x {n} workers (serve --gpus {n}, SO_REUSEPORT)", "workers": n,
+                "value": round(lg["rps"], 2), "unit": "predictions/s", "vs_rest_baseline": round(lg["rps"] / REST_BASELINE, 3),
+                "p50_ms": lg["p50_ms"], "p99_ms": lg["p99_ms"], "window_s": round(lg["seconds"], 3),
+                "users": users, "sampled_replies_checked": lg.get("checked", 0),
+                "self_check": {"ok": lg.get("bad_body", 0) == 0},
+                "per_worker_requests": {str(w["rank"]): w["requests"] for w in per},
+                "balance_min_over_max": round(min(counts) / max(1, max(counts)), 3) if counts else None,
+                "server_threads_per_worker": threads, "client_threads": cthreads}
+    except Exception as e:
+        return {"error": f"{type(e).__name__}: {e}"[:600]}
+    finally:
+        if proc is not None and proc.poll() is None:
+            import signal as _s
+
+            try:
+                os.killpg(proc.pid, _s.SIGKILL)
+            except OSError:
+                pass
+            proc.wait()
+        shutil.rmtree(work, ignore_errors=True)
 
 
 # ------------------------------------------------------------------ fabric

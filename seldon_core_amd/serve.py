@@ -236,6 +236,16 @@ def run_worker(args: argparse.Namespace, fabric=None) -> int:
     if explainer is not None:
         explainer.stop()
     clean = h.drain(cfg.drain_seconds)
+    stats_dir = os.environ.get("SCA_WORKER_STATS_DIR")
+    if stats_dir:  # per-worker share of the traffic SO_REUSEPORT handed out (bench reuseport variant)
+        served = 0.0
+        for ln in dep.metrics().splitlines():
+            if ln.startswith("seldon_api_engine_server_requests") and "_count" in ln.split(" ")[0]:
+                served += float(ln.rsplit(" ", 1)[-1])
+        with open(os.path.join(stats_dir, f"worker-{rank}.json"), "w") as f:
+            json.dump({"rank": int(rank), "pid": os.getpid(), "requests": int(served),
+                       "units": {k: v.get("requests", 0) for k, v in dep.batcher_stats().items()
+                                 if isinstance(v, dict)}}, f)
     dep.engine.flush_message_log()
     dep.close()  # rank-placed graph: also stops the other ranks' peer loops
     if fabric is not None:

@@ -51,7 +51,10 @@ def test_bench_two_ranks_torchrun_cpu():
     assert line["self_check"]["ok"] and line["self_check"]["sampled_replies_checked"] > 0
     assert set(line["step_ms"]) == {"min", "median", "max"}
     v = line["variants"]
-    assert set(v) == {"abtest", "mab", "replicas", "abtest_rccl", "mab_rccl"}  # pipeline needs 4
+    assert set(v) == {"abtest", "mab", "replicas", "reuseport", "abtest_rccl", "mab_rccl"}  # pipeline needs 4
+    rp = v["reuseport"]  # serve --gpus 2: two workers on one SO_REUSEPORT port
+    assert rp["workers"] == 2 and set(rp["per_worker_requests"]) == {"0", "1"}, rp
+    assert sum(rp["per_worker_requests"].values()) > 0 and rp["balance_min_over_max"] > 0, rp
     for k, r in v.items():
         assert "error" not in r, (k, r)
         assert r["self_check"]["ok"] and r["value"] > 0 and r["sampled_replies_checked"] > 0, (k, r)
