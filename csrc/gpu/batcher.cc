@@ -110,7 +110,8 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
   }
   for (auto& s : slots_) ps_.free_list.push_back(s.get());
   running_.store(true);
-  driver_ = DeviceDriver::acquire(opts_.device, true);  // one pump + hand-off thread pair per GPU
+  // one pump + hand-off thread pair per GPU, unless launch() may block on the host
+  driver_ = DeviceDriver::acquire(opts_.device, !model_->exclusive_driver());
   driver_->add(this);
 }
 

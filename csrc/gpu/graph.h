@@ -63,6 +63,11 @@ class GraphModel : public RowModel {
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override {
     launch_segments(X, rows, cols, out, ws, nullptr, 0, s);
   }
+  bool exclusive_driver() const override {
+    for (const auto& s : st_)
+      if (s.model && s.model->exclusive_driver()) return true;
+    return false;
+  }
   bool segmented() const override {
     for (const auto& s : st_)
       if (s.model && s.model->segmented()) return true;

@@ -75,6 +75,10 @@ class RowModel {
     return false;
   }
   virtual void run_cpu(const double* X, int rows, int cols, double* out) const = 0;
+  // True if launch() can wait on the host (a peer model taking a link lock /
+  // the loopback transport's rendezvous): its unit gets a pump thread of its
+  // own instead of sharing the GPU's, so it never stalls the other units.
+  virtual bool exclusive_driver() const { return false; }
   // Asynchronous run_cpu: returns a call to poll, or nullptr if the model has
   // none (X must stay valid and `out` untouched until done()).
   virtual CpuCallPtr start_cpu(const double* X, int rows, int cols, double* out) {

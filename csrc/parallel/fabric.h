@@ -237,6 +237,7 @@ class PeerRowModel : public gpu::RowModel {
   int in_cols() const override { return in_cols_; }
   int out_cols(int) const override { return out_cols_; }
   bool device_io_only() const override { return true; }
+  bool exclusive_driver() const override { return true; }  // one issuing thread per peer unit
   void to_device(int device) override;
   size_t workspace_bytes(int max_rows, int cols) const override;
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
