@@ -8,7 +8,6 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
-#include <future>
 
 namespace sca::gpu {
 
@@ -377,10 +376,11 @@ bool BatchedUnit::launch(Slot* s) {
     ensure_capacity(*s, rows, cols);
     double* hin = s->h_in.host<double>();
     const size_t bin = size_t(rows) * cols * sizeof(double), bout = size_t(rows) * s->out_cols * sizeof(double);
-    // A lone large request is DMA'd straight from its own memory (the
-    // message's tensor, or the caller's buffer for run_ptr): no host copy
-    // into the pinned slot first (8192 x 784 fp64: 51 MB).
-    const bool direct = s->items.size() == 1 && bin >= kDirectH2DBytes;
+    // A lone large request is DMA'd straight from its message's memory: no
+    // host copy into the pinned slot first (8192 x 784 fp64: 51 MB).  Not a
+    // run_ptr caller's buffer: the watchdog must be able to answer that
+    // caller (who then frees the buffer) while the device may still read.
+    const bool direct = s->items.size() == 1 && bin >= kDirectH2DBytes && !s->items[0].caller_mem;
     s->direct = direct;
     if (!direct) {
       size_t off = 0;
@@ -544,11 +544,8 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     s->abandoned = false;
     abandoned_slots_.fetch_sub(1, std::memory_order_relaxed);
     if (st != hipSuccess) note_failure();
-    // the device is done with the direct-path source: release / answer it now
-    for (auto& it : s->parked)
-      if (it.caller_mem) it.k(Outcome::fail(s->parked_err));
+    // the device is done with the direct-path source: release it now
     s->parked.clear();
-    s->parked_err.reset();
     return;
   }
   inflight_rows_.fetch_sub(s->rows, std::memory_order_relaxed);
@@ -783,12 +780,7 @@ void BatchedUnit::abandon(Slot* s) {
   auto e = device_error(ApiError::DEADLINE_EXCEEDED, "GPU batch exceeded the hang watchdog (" +
                                                          std::to_string(opts_.hang_timeout_ms) + " ms)");
   for (auto& it : items) {
-    if (s->direct && it.caller_mem) {  // its buffer is the DMA source: answer once the device lets go
-      s->parked_err = e;
-      s->parked.push_back(std::move(it));
-      continue;
-    }
-    it.k(Outcome::fail(e));
+    it.k(Outcome::fail(e));  // run_ptr callers too: their buffers are never a DMA source
     if (s->direct) s->parked.push_back(std::move(it));  // keep the request (DMA source) alive
   }
 }
@@ -863,6 +855,42 @@ void BatchedUnit::reset_stats() {
   complete_cpu_s_.store(0.0, std::memory_order_relaxed);
 }
 
+namespace {
+// A synchronous caller's wait for its continuation (run_ptr / run_dense:
+// Python ops, the device Mahalanobis step, tests).  The pump thread answers
+// within tens of microseconds, so the caller spins that long before it
+// sleeps: a futex wake-up of a blocked waiter costs about as much again as
+// the whole GPU round trip (std::promise always took that path).
+struct SyncWait {
+  std::atomic<int> state{0};  // 0 waiting, 1 done
+  std::atomic<bool> sleeping{false};
+  std::mutex mu;
+  std::condition_variable cv;
+  Outcome out;
+  void set(Outcome o) {
+    out = std::move(o);
+    state.store(1, std::memory_order_release);
+    if (sleeping.load(std::memory_order_seq_cst)) {
+      std::lock_guard<std::mutex> g(mu);
+      cv.notify_all();
+    }
+  }
+  Outcome wait() {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(200);
+    for (unsigned n = 1; state.load(std::memory_order_acquire) == 0; ++n) {
+      _mm_pause();
+      if ((n & 63) == 0 && std::chrono::steady_clock::now() >= until) {
+        std::unique_lock<std::mutex> lk(mu);
+        sleeping.store(true, std::memory_order_seq_cst);
+        cv.wait(lk, [&] { return state.load(std::memory_order_acquire) != 0; });
+        break;
+      }
+    }
+    return std::move(out);
+  }
+};
+}  // namespace
+
 std::vector<double> BatchedUnit::run_ptr(const double* X, int rows, int cols) {
   if (rows <= 0 || cols <= 0) throw std::runtime_error("run_ptr: empty input");
   const int want = model_->in_cols();
@@ -873,17 +901,16 @@ std::vector<double> BatchedUnit::run_ptr(const double* X, int rows, int cols) {
   msg->payload = Payload::Data;
   msg->data.kind = DataKind::Tensor;
   msg->data.shape = {rows, cols};
-  std::promise<Outcome> p;
-  auto f = p.get_future();
+  auto w = std::make_shared<SyncWait>();
   Item it;
   it.req = std::move(msg);
   it.xp = X;
   it.caller_mem = true;
   it.rows = rows;
   it.cols = cols;
-  it.k = [&p](Outcome o) { p.set_value(std::move(o)); };
+  it.k = [w](Outcome o) { w->set(std::move(o)); };
   submit_item(std::move(it));
-  Outcome o = f.get();
+  Outcome o = w->wait();
   if (o.err) throw std::runtime_error(o.err->info);
   return std::move(o.msg->data.values);
 }
@@ -894,11 +921,10 @@ std::vector<double> BatchedUnit::run_dense(const std::vector<double>& X, int row
   msg->data.kind = DataKind::Tensor;
   msg->data.shape = {rows, cols};
   msg->data.values = X;
-  std::promise<Outcome> p;
-  auto f = p.get_future();
+  auto w = std::make_shared<SyncWait>();
   CallCtx c{nullptr, nullptr};
-  transform_input(c, msg, [&p](Outcome o) { p.set_value(std::move(o)); });
-  Outcome o = f.get();
+  transform_input(c, msg, [w](Outcome o) { w->set(std::move(o)); });
+  Outcome o = w->wait();
   if (o.err) throw std::runtime_error(o.err->info);
   return std::move(o.msg->data.values);
 }

@@ -160,13 +160,12 @@ class BatchedUnit : public Unit {
     int cols = 0;
     int out_cols = 0;
     bool abandoned = false;  // watchdog answered its requests; waiting for the device to finish
-    // Direct path (one request >= kDirectH2DBytes DMA'd from its own memory):
-    // a watchdog-abandoned batch keeps the request alive here until the slot's
-    // event completes, since that copy may still be reading it; run_ptr callers
-    // are answered only then (their buffer is the DMA source).
+    // Direct path (one message-owned request >= kDirectH2DBytes DMA'd from
+    // its own memory): a watchdog-abandoned batch keeps the request alive
+    // here until the slot's event completes, since that copy may still be
+    // reading it.  (run_ptr callers' buffers never take this path.)
     bool direct = false;
     std::vector<Item> parked;
-    ErrPtr parked_err;
     uint64_t roctx = 0;      // marker range of the batch (SCA_ROCTX=1)
     std::chrono::steady_clock::time_point t_launch;
   };

@@ -159,3 +159,26 @@ def test_gpu_replica_failover():
         assert rep.retries >= 1
     finally:
         dep.close()
+
+
+@pytest.mark.gpu
+def test_hang_watchdog_answers_a_large_run_ptr_caller_at_once():
+    """A >= 1 MiB run_ptr batch (the caller's buffer) held by an injected hang:
+    the watchdog answers the caller at its deadline -- the buffer is copied
+    into the slot's pinned staging, never DMA'd in place, so nothing needs to
+    wait for the device before the caller may free it."""
+    C = sca.native()
+    u = C.BatchedUnit(C.linear_model(np.ones((3, 16)), np.zeros(3), 1), 0, slots=1, hang_timeout_ms=200,
+                      cooldown_ms=100, max_batch=65536)
+    X = np.random.default_rng(0).normal(size=(9000, 16))  # 1.15 MB
+    try:
+        u.run(X[:10])
+        u.inject_fault(hang_ms=3000)
+        t0 = time.perf_counter()
+        with pytest.raises(RuntimeError, match="hang watchdog"):
+            u.run(X)
+        assert time.perf_counter() - t0 < 1.5
+        del X  # the caller frees its buffer while the slot is still parked
+        u.inject_fault()
+    finally:
+        u.stop()
