@@ -258,10 +258,10 @@ class OutlierMahalanobis(_FeedbackMetrics):
         single-workgroup launch that steps the HBM-resident state through them
         in order (csrc/kernels/mahalanobis.hip: maha_step_segments); p <= 64,
         k <= 16."""
+        if self.device < 0 or p > 64 or min(self.n_components, p) > 16:
+            return None  # CPU placement: the numpy / scipy-eigh path (the parity oracle)
         if self._dev is not None and self._dev.p == p:
             return self._dev
-        if self.device < 0 or p > 64 or min(self.n_components, p) > 16:
-            return None
         return self._make_device(p, self.device)
 
     def _make_device(self, p: int, device: int):
@@ -279,7 +279,10 @@ class OutlierMahalanobis(_FeedbackMetrics):
         the micro-batcher with no Python per request.  Needs ``n_features``
         (the reference learns p from the first request; a native unit is bound
         before any arrives).  The node shares this object's detector state, so
-        state_dict()/load_state_dict() checkpoint it."""
+        state_dict()/load_state_dict() checkpoint it.  Served natively, the
+        per-request Python bookkeeping (``n``, ``nb_outliers``, the feedback
+        metrics) is not updated -- no Python runs per request;
+        state_dict() pulls ``n`` and the state from the device."""
         p = self.n_features
         if not p or p > 64 or min(self.n_components, p) > 16:
             return None
@@ -343,7 +346,13 @@ class OutlierMahalanobis(_FeedbackMetrics):
             self.n += X.shape[0]
             self.prediction = (self.score > self.threshold).astype(int)
             return self.prediction
-        return self._get_preds_host(X)
+        shared = self._dev is not None and X.ndim == 2 and self._dev.p == X.shape[1]
+        if shared:  # a native node (row_model) holds the state: one detector, two entry points
+            self._pull_state()
+        out = self._get_preds_host(X)
+        if shared:
+            self._push_state(self._dev.p)
+        return out
 
     def _get_preds_host(self, X):
         """numpy path (CPU placement; the parity oracle of the device kernel)."""
