@@ -21,6 +21,7 @@ kern::MahaParams make_params(int p, int k, double n_stdev, double start_clip, do
   prm.max_n = max_n;
   prm.eps = eps;
   if (const char* v = std::getenv("SCA_MAHA_MW_MIN_P")) prm.mw_min_p = std::atoi(v);
+  if (const char* v = std::getenv("SCA_MAHA_JACOBI_MAX_P")) prm.jacobi_max_p = std::min(32, std::max(0, std::atoi(v)));
   return prm;
 }
 

@@ -249,14 +249,20 @@ struct MahaParams {
   // Measured: p = 64 87.0 -> 74.9 us, p = 32 30.5 -> 32.3 us, p = 20 16.1 ->
   // 19.8 us (the two barriers per column cost more than a short sweep saves)
   int mw_min_p = 48;
+  // p <= jacobi_max_p: warm-started cyclic Jacobi (one wave) instead of the
+  // Householder / Sturm / inverse-iteration path (SCA_MAHA_JACOBI_MAX_P,
+  // capped at 32; 0 = never)
+  int jacobi_max_p = 32;
 };
 // state layout (doubles): mean[p] | C[p*p] | clip_lo[p] | clip_hi[p] | n | c_zero | has_clip
 inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
 // workspace doubles for a batch of nb rows
 inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (4 * size_t(p) + 2 * size_t(k)); }
-// eig: kMahaEigDoubles doubles, zero-initialised device diagnostics (not
-// part of the state; the first kMahaMaxP^2 are reserved).
-// Tail: [0, 0, eigen-phase shader cycles, steps, eigen-phase 100 MHz ticks,
+// eig: kMahaEigDoubles doubles, zero-initialised: the first kMahaMaxP^2 hold
+// the last step's eigenvectors (the Jacobi path's warm start; a cache, not
+// part of the checkpointed state).
+// Tail: [p of the cached eigenvectors, warm steps since the last cold start,
+// eigen-phase shader cycles, steps, eigen-phase 100 MHz ticks,
 // phase us x 10]: clip, cov, eigen.eigenvectors (twisted factorisation),
 // eigen (total), projections, Sherman-Morrison, state update,
 // eigen.tridiagonalise, eigen.eigenvalues (multisection),

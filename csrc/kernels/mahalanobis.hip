@@ -623,6 +623,164 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
   mark(9);  // back-transformation
 }
 
+// Top-k eigenpairs for p <= kJacobiMaxP by cyclic Jacobi, WARM-STARTED from
+// the previous step's eigenvectors (kept in eig[0 .. p*p)).  The covariance
+// changes by a rank-nb update of weight ~1/n per request, so
+// B = V0^T C V0 is diagonal but for O(1/n) off-diagonals and two or three
+// threshold-Jacobi sweeps (quadratic convergence) diagonalise it, where the
+// Householder path pays a full tridiagonalisation every step
+// (profiles/r03r_head: 15.8 us of a 24 us step at p = 9).  Cold starts (no
+// cache, the first step, every kJacobiRefresh-th step to bound the drift of
+// V0's orthogonality) start from V0 = I.  The score depends only on the
+// top-k SUBSPACE (projections, proj_cov and the Sherman-Morrison recurrence
+// all change by the same k x k rotation), so any orthonormal basis of it
+// gives the reference's scores.
+//
+// One wave; lane r owns row r of B and of V.  Parallel ordering: a round
+// rotates m/2 disjoint pairs (round-robin tournament, m = p rounded up to
+// even; pairs with the dummy index p are skipped), B <- R^T B R out of
+// place (rows mixed in registers, then columns through the lane's own LDS
+// row), V <- V R in place.  A pair rotates only while
+// |b_ij| > tol * sqrt(|b_ii b_jj|) (tol = 1e-15, a few ulps): the sweep with no
+// rotation ends the solve.
+constexpr int kJacobiMaxP = 32;
+constexpr int kJacobiRefresh = 256;
+
+__device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W, int* sel, int p,
+                            int k, double* __restrict__ cache, double* __restrict__ tail, double2* __restrict__ coef,
+                            int* __restrict__ partner) {
+  const int lane = threadIdx.x & 63;
+  const int m = p + (p & 1);
+  const bool row = lane < p;
+  const bool warm = tail[0] == double(p) && tail[1] < double(kJacobiRefresh);
+  double reg[kJacobiMaxP];
+  if (warm) {
+    for (int e = lane; e < p * p; e += 64) V[(e / p) * kLd + e % p] = cache[e];
+    wave_lds_sync();
+    // T = C V0 -> W (lane r: row r), then B = V0^T T -> A (lane r: row r = column r of V0)
+    if (row) {
+#pragma unroll
+      for (int j = 0; j < kJacobiMaxP; ++j) reg[j] = j < p ? A[lane * kLdA + j] : 0.0;
+      for (int q = 0; q < p; ++q) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < kJacobiMaxP; ++j)
+          if (j < p) t += reg[j] * V[j * kLd + q];
+        W[lane * kLd + q] = t;
+      }
+    }
+    wave_lds_sync();
+    if (row) {
+#pragma unroll
+      for (int j = 0; j < kJacobiMaxP; ++j) reg[j] = j < p ? V[j * kLd + lane] : 0.0;
+      for (int q = 0; q < p; ++q) {
+        double b = 0.0;
+#pragma unroll
+        for (int j = 0; j < kJacobiMaxP; ++j)
+          if (j < p) b += reg[j] * W[j * kLd + q];
+        A[lane * kLdA + q] = b;
+      }
+    }
+  } else if (row) {
+    for (int q = 0; q < p; ++q) V[lane * kLd + q] = lane == q ? 1.0 : 0.0;
+  }
+  wave_lds_sync();
+  // symmetric working copy: B[r][q] for q < r taken from the upper triangle
+  if (row)
+    for (int q = 0; q < lane; ++q) A[lane * kLdA + q] = A[q * kLdA + lane];
+  wave_lds_sync();
+  double* cur = A;
+  double* nxt = W;
+  int ld_cur = kLdA, ld_nxt = kLd;
+  constexpr double tol = 1e-15;
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    bool rotated = false;
+    for (int rnd = 0; rnd < m - 1; ++rnd) {
+      // tournament position of player `lane`, and its partner
+      int pr = lane;
+      if (lane < m) {
+        const int pos = lane == 0 ? 0 : ((lane - 1 - rnd) % (m - 1) + (m - 1)) % (m - 1) + 1;
+        const int opp = m - 1 - pos;
+        pr = opp == 0 ? 0 : 1 + (opp - 1 + rnd) % (m - 1);
+      }
+      double al = 1.0, be = 0.0;
+      if (row && pr < p) {
+        const int i = min(lane, pr), j = max(lane, pr);
+        const double aii = cur[i * ld_cur + i], ajj = cur[j * ld_cur + j], aij = cur[i * ld_cur + j];
+        if (aij != 0.0 && fabs(aij) > tol * sqrt(fabs(aii * ajj))) {
+          const double th = (aii - ajj) / (2.0 * aij);
+          const double t = -copysign(1.0, th) / (fabs(th) + sqrt(1.0 + th * th));
+          const double c = 1.0 / sqrt(1.0 + t * t), sn = t * c;
+          al = c;
+          be = lane == i ? -sn : sn;
+          rotated = true;
+        }
+      }
+      if (lane < m) {
+        coef[lane] = make_double2(al, be);
+        partner[lane] = (row && pr < p) ? pr : lane;
+      }
+      wave_lds_sync();
+      if (row) {
+        // rows: u = al * B[lane] + be * B[partner]; columns: B'[lane][q] = a_q u[q] + b_q u[pi_q]
+        const int pl = partner[lane];
+#pragma unroll
+        for (int q = 0; q < kJacobiMaxP; ++q)
+          if (q < p) reg[q] = al * cur[lane * ld_cur + q] + be * cur[pl * ld_cur + q];
+#pragma unroll
+        for (int q = 0; q < kJacobiMaxP; ++q)
+          if (q < p) nxt[lane * ld_nxt + q] = reg[q];
+        // (own row: the reads below see this lane's writes in program order)
+#pragma unroll
+        for (int q = 0; q < kJacobiMaxP; ++q)
+          if (q < p) {
+            const double2 cq = coef[q];
+            reg[q] = cq.x * reg[q] + cq.y * nxt[lane * ld_nxt + partner[q]];
+          }
+#pragma unroll
+        for (int q = 0; q < kJacobiMaxP; ++q)
+          if (q < p) nxt[lane * ld_nxt + q] = reg[q];
+        // V <- V R (own row)
+#pragma unroll
+        for (int q = 0; q < kJacobiMaxP; ++q)
+          if (q < p) {
+            const double2 cq = coef[q];
+            reg[q] = cq.x * V[lane * kLd + q] + cq.y * V[lane * kLd + partner[q]];
+          }
+#pragma unroll
+        for (int q = 0; q < kJacobiMaxP; ++q)
+          if (q < p) V[lane * kLd + q] = reg[q];
+      }
+      wave_lds_sync();
+      double* tp = cur;
+      cur = nxt;
+      nxt = tp;
+      const int tl = ld_cur;
+      ld_cur = ld_nxt;
+      ld_nxt = tl;
+    }
+    if (!__any(rotated)) break;
+  }
+  // top-k by the diagonal (eigenvalues), largest first
+  const double ninf = -__builtin_inf();
+  double lam = row ? cur[lane * ld_cur + lane] : ninf;
+  for (int a = 0; a < k; ++a) {
+    const double mx = wave_max(lam);
+    const unsigned long long hit = __ballot(lam == mx && row);
+    const int idx = hit ? int(__builtin_ctzll(hit)) : a;
+    if (lane == 0) sel[a] = idx;
+    if (lane == idx) lam = ninf;
+  }
+  // cache the basis for the next step's warm start
+  wave_lds_sync();
+  for (int e = lane; e < p * p; e += 64) cache[e] = V[(e / p) * kLd + e % p];
+  if (lane == 0) {
+    tail[0] = double(p);
+    tail[1] = warm ? tail[1] + 1.0 : 0.0;
+  }
+  wave_lds_sync();
+}
+
 // Sherman-Morrison scores for k <= 4 on one lane (CoreMahalanobis.py:118-146,
 // the same recurrence as the LDS path below): P, C^-1 and the per-row
 // updates live in registers as padded 4 x 4 matrices (identity block past
@@ -853,8 +1011,15 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   __syncthreads();
   stamp(1);
   const uint64_t c_eig0 = __builtin_amdgcn_s_memtime(), r_eig0 = __builtin_amdgcn_s_memrealtime();
-  if (NT >= 256 && p >= prm.mw_min_p) topk_wave(A, V, W, es, sel, p, k, ph, 4);
-  else if (tid < 64) topk_wave(A, V, W, es, sel, p, k, ph, 1);
+  if (p <= prm.jacobi_max_p) {
+    if (tid < 64)
+      jacobi_wave(A, V, W, sel, p, k, eig, eig + kMahaMaxP * kMahaMaxP, es.rv,
+                  reinterpret_cast<int*>(es.rn));
+  } else if (NT >= 256 && p >= prm.mw_min_p) {
+    topk_wave(A, V, W, es, sel, p, k, ph, 4);
+  } else if (tid < 64) {
+    topk_wave(A, V, W, es, sel, p, k, ph, 1);
+  }
   __syncthreads();
   stamp(3);
   if (tid == 0) {  // shader-clock cycles and 100 MHz ticks of the eigen phase (effective clock)

@@ -178,15 +178,21 @@ def test_mahalanobis_gpu_recurrence_matches_numpy():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("p,k,start_clip,max_n", [(9, 3, 50, -1), (20, 4, 10, 300), (5, 5, 50, -1), (64, 3, 100, -1),
-                                                  (41, 2, 50, -1)])
-def test_mahalanobis_device_state_parity_over_1000_requests(p, k, start_clip, max_n, monkeypatch):
+@pytest.mark.parametrize("p,k,start_clip,max_n,path", [(9, 3, 50, -1, "jacobi"), (20, 4, 10, 300, "jacobi"),
+                                                       (5, 5, 50, -1, "jacobi"), (32, 3, 50, -1, "jacobi"),
+                                                       (9, 3, 50, -1, "householder"), (64, 3, 100, -1, "householder"),
+                                                       (41, 2, 50, -1, "householder")])
+def test_mahalanobis_device_state_parity_over_1000_requests(p, k, start_clip, max_n, path, monkeypatch):
     """Whole _get_preds on the device for 1-row requests: state (mean, C, n,
     clip) within 1e-9 of the numpy path over a 1,000-request stream (VERDICT
-    r1 next-round #6), scores to 1e-6.  p = 64 (default threshold) and p = 41
-    (threshold lowered) run the 4-wave tridiagonalisation sweep."""
+    r1 next-round #6), scores to 1e-6.  p <= 32 runs the warm-started Jacobi
+    eigen path (cold restarts every 256 steps included); "householder" forces
+    the tridiagonalisation path; p = 64 (default threshold) and p = 41
+    (threshold lowered) run its 4-wave sweep."""
     if p == 41:
         monkeypatch.setenv("SCA_MAHA_MW_MIN_P", "32")
+    if path == "householder":
+        monkeypatch.setenv("SCA_MAHA_JACOBI_MAX_P", "0")
     rng = np.random.default_rng(p)
     cpu = OutlierMahalanobis(threshold=10, n_components=k, start_clip=start_clip, max_n=max_n, device=-1)
     gpu = OutlierMahalanobis(threshold=10, n_components=k, start_clip=start_clip, max_n=max_n, device=0)
