@@ -173,7 +173,12 @@ Fabric::Fabric(int rank, int world, const std::string& unique_ids, int device, s
   for (int r = 0; r < world; ++r)
     if ((rank == 0) != (r == 0)) links_[size_t(r)] = std::make_unique<Link>();
   map_rings();
-  if (device_ < 0) return;
+  if (device_ < 0) {
+    rq_.resize(size_t(world_));
+    if (rank_ == 0)
+      for (int r = 1; r < world_; ++r) rq_[size_t(r)] = std::make_unique<RecvQ>();
+    return;
+  }
   gpu::DeviceGuard g(device);
   for (auto& l : links_)
     if (l) {
@@ -293,23 +298,16 @@ void Fabric::close() {
       }
     }
   }
-  {
-    std::lock_guard<std::mutex> rg(rq_mu_);
-    for (auto& q : rq_)
-      if (q) {
-        std::lock_guard<std::mutex> qg(q->mu);
-        q->cv.notify_all();
-      }
-  }
   for (int& fd : fds_)
-    if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
-  for (auto& q : rq_)
-    if (q && q->th.joinable()) q->th.join();
-  for (int& fd : fds_)
-    if (fd >= 0) {
-      ::close(fd);
-      fd = -1;
+    if (fd >= 0) ::shutdown(fd, SHUT_RDWR);  // a reader blocked in recv() returns
+  for (size_t r = 0; r < fds_.size(); ++r) {
+    std::unique_lock<std::mutex> rd;
+    if (r < rq_.size() && rq_[r]) rd = std::unique_lock<std::mutex>(rq_[r]->rd);
+    if (fds_[r] >= 0) {
+      ::close(fds_[r]);
+      fds_[r] = -1;
     }
+  }
   // The rings stay mapped until the destructor: a worker thread may still be
   // polling one (its take() sees open_ == false and leaves).
 }
@@ -362,6 +360,17 @@ PeerHeader Fabric::take() {
   return h;
 }
 
+int Fabric::backlog() const {
+  if (rank_ == 0 || rings_.empty() || !rings_[0]) return 0;
+  const HeaderRing* R = rings_[0];
+  const uint64_t seq = next_[0];
+  int n = 0;
+  while (n < 64 && R->slots[(seq + uint64_t(n)) % HeaderRing::kSlots].seq.load(std::memory_order_acquire) ==
+                       seq + uint64_t(n) + 1)
+    ++n;
+  return n;
+}
+
 void Fabric::xfer(bool send, int chan, void* p, size_t bytes, int peer) {
   if (!gpu()) {
     if (send) write_all(fd(peer), p, bytes);
@@ -387,55 +396,75 @@ void Fabric::send_y(const void* p, size_t bytes, int peer) { xfer(true, kChanY, 
 void Fabric::recv_y(void* p, size_t bytes, int peer) { xfer(false, kChanY, p, bytes, peer); }
 
 void Fabric::expect_reply(int peer, void* dst, size_t bytes, std::shared_ptr<Waiter> w) {
-  RecvQ* q;
-  {
-    std::lock_guard<std::mutex> g(rq_mu_);
-    if (rq_.empty()) rq_.resize(size_t(world_));
-    auto& slot = rq_[size_t(peer)];
-    if (!slot) {
-      slot = std::make_unique<RecvQ>();
-      slot->th = std::thread([this, peer] { receiver(peer); });
-    }
-    q = slot.get();
-  }
-  std::lock_guard<std::mutex> g(q->mu);
-  q->q.push_back({dst, bytes, std::move(w)});
-  q->cv.notify_one();
+  RecvQ& q = recvq(peer);
+  std::lock_guard<std::mutex> g(q.mu);
+  q.q.push_back({dst, bytes, std::move(w)});
 }
 
-// Rank 0, CPU fabrics: replies of one worker arrive in issue order; hand each
-// to the caller that queued it.
-void Fabric::receiver(int peer) {
-  RecvQ* qp;
-  {
-    std::lock_guard<std::mutex> g(rq_mu_);
-    qp = rq_[size_t(peer)].get();
-  }
-  RecvQ& q = *qp;
+Fabric::RecvQ& Fabric::recvq(int peer) {
+  if (gpu() || rank_ != 0 || peer <= 0 || peer >= world_ || !rq_[size_t(peer)])
+    throw std::runtime_error("Fabric: no reply queue for rank " + std::to_string(peer));
+  return *rq_[size_t(peer)];
+}
+
+// Rank 0, CPU fabrics.  Replies of one worker arrive on its socket in issue
+// order; whichever caller polls reads them into the buffers queued by
+// expect_reply and finishes their waiters (no receiver thread: the batcher's
+// pump polls between launches, so a reply costs no extra thread wake-up).
+// One reader per link at a time (q.rd); the queue lock only guards push/pop,
+// and a deque's elements stay put under push_back.
+bool Fabric::poll_replies(int peer, bool block) {
+  RecvQ& q = recvq(peer);
+  std::unique_lock<std::mutex> rd(q.rd, std::defer_lock);
+  if (block) rd.lock();
+  else if (!rd.try_lock()) return false;
   auto finish = [](Pending& p, const std::string& err) {
     std::lock_guard<std::mutex> g(p.w->mu);
     if (!err.empty() && p.w->error.empty()) p.w->error = err;
     if (--p.w->pending == 0) p.w->cv.notify_all();
   };
+  auto fail_all = [&](const std::string& err) {
+    std::lock_guard<std::mutex> g(q.mu);
+    for (auto& r : q.q) finish(r, err);
+    q.q.clear();
+    q.off = 0;
+  };
+  bool progress = false;
   while (true) {
-    Pending p;
+    Pending* p;
     {
-      std::unique_lock<std::mutex> lk(q.mu);
-      q.cv.wait(lk, [&] { return !q.q.empty() || !open_.load(); });
-      if (q.q.empty()) return;
-      p = q.q.front();
+      std::lock_guard<std::mutex> g(q.mu);
+      if (q.q.empty()) return progress;
+      p = &q.q.front();
+    }
+    const int fd = fds_[size_t(peer)];
+    if (fd < 0) {
+      fail_all("fabric closed");
+      return true;
+    }
+    char* dst = static_cast<char*>(p->dst);
+    while (q.off < p->bytes) {
+      const ssize_t r = ::recv(fd, dst + q.off, p->bytes - q.off, block ? 0 : MSG_DONTWAIT);
+      if (r > 0) {
+        q.off += size_t(r);
+        continue;
+      }
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return progress;
+      fail_all(r == 0 ? std::string("fabric peer closed the connection")
+                      : std::string("fabric socket read failed: ") + std::strerror(errno));
+      return true;
+    }
+    Pending done;
+    {
+      std::lock_guard<std::mutex> g(q.mu);
+      done = std::move(q.q.front());
       q.q.pop_front();
+      q.off = 0;
     }
-    try {
-      read_all(fds_[size_t(peer)], p.dst, p.bytes);
-      finish(p, "");
-    } catch (const std::exception& e) {
-      finish(p, e.what());
-      std::lock_guard<std::mutex> lk(q.mu);
-      for (auto& r : q.q) finish(r, e.what());
-      q.q.clear();
-      return;
-    }
+    finish(done, "");
+    progress = true;
+    if (block) return true;  // the caller re-checks its own waiter
   }
 }
 
@@ -515,7 +544,7 @@ void PeerRowModel::launch(const double* X, int rows, int cols, double* out, void
 }
 
 // CPU fabric: header + payload go out under each link's mutex; the replies
-// land in call-owned buffers through the per-peer receiver threads.
+// land in call-owned buffers when a caller polls the link (poll_replies).
 std::shared_ptr<Fabric::Waiter> PeerRowModel::issue_cpu(const double* X, int rows, int cols) const {
   if (f_->gpu()) throw std::runtime_error("rccl_peer: GPU fabric models run on their GPU");
   if (!f_->open()) throw std::runtime_error("fabric closed");
@@ -526,9 +555,11 @@ std::shared_ptr<Fabric::Waiter> PeerRowModel::issue_cpu(const double* X, int row
   for (size_t i = 0; i < peers_.size(); ++i) {
     const int p = peers_[i];
     std::lock_guard<std::mutex> g(f_->link_mutex(p));
-    header(p, rows, cols);
-    f_->send_x(X, bx, p);
+    // payload first: the worker, spinning on its ring, then finds the bytes
+    // already in its socket buffer instead of sleeping in read()
     f_->expect_reply(p, w->bufs[i].data(), ny * sizeof(double), w);
+    f_->send_x(X, bx, p);
+    header(p, rows, cols);
   }
   batches_++;
   return w;
@@ -537,12 +568,20 @@ std::shared_ptr<Fabric::Waiter> PeerRowModel::issue_cpu(const double* X, int row
 namespace {
 // The reply (mean of the gathered replies for a fan-out) goes into `out` once.
 struct PeerCall : gpu::CpuCall {
+  FabricPtr f;             // held: an abandoned call may outlive its model
+  std::vector<int> peers;
   std::shared_ptr<Fabric::Waiter> w;
   double* out;
   bool finished = false;
   std::string err;
+  bool pending() {
+    std::lock_guard<std::mutex> g(w->mu);
+    return w->pending > 0;
+  }
   bool done() override {
     if (finished) return true;
+    if (pending())
+      for (int p : peers) f->poll_replies(p, false);
     {
       std::lock_guard<std::mutex> g(w->mu);
       if (w->pending > 0) return false;
@@ -570,6 +609,8 @@ struct PeerCall : gpu::CpuCall {
 
 gpu::CpuCallPtr PeerRowModel::start_cpu(const double* X, int rows, int cols, double* out) {
   auto c = std::make_shared<PeerCall>();
+  c->f = f_;
+  c->peers = peers_;
   c->w = issue_cpu(X, rows, cols);
   c->out = out;
   return c;
@@ -577,11 +618,29 @@ gpu::CpuCallPtr PeerRowModel::start_cpu(const double* X, int rows, int cols, dou
 
 void PeerRowModel::run_cpu(const double* X, int rows, int cols, double* out) const {
   PeerCall c;
+  c.f = f_;
+  c.peers = peers_;
   c.w = issue_cpu(X, rows, cols);
   c.out = out;
-  {
-    std::unique_lock<std::mutex> lk(c.w->mu);
-    c.w->cv.wait(lk, [&] { return c.w->pending == 0; });
+  // Read replies (ours and older callers') until ours are in: a blocking
+  // read of a peer returns after one reply, so no peer is waited on for
+  // longer than its oldest outstanding batch.
+  // Spin briefly first: a worker's reply usually lands within tens of
+  // microseconds, and waking from a blocking read costs about as much again.
+  const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(100);
+  unsigned polls = 0;
+  while (c.pending()) {
+    bool got = false;
+    for (int p : peers_)
+      if (c.pending()) got |= f_->poll_replies(p, false);
+    if (!got && c.pending() && ((++polls & 7) != 0 || std::chrono::steady_clock::now() < spin_until)) {
+      _mm_pause();
+      continue;
+    }
+    if (!got && c.pending()) {
+      for (int p : peers_)
+        if (c.pending() && f_->poll_replies(p, true)) break;
+    }
   }
   c.done();
   if (!c.err.empty()) throw std::runtime_error(c.err);
@@ -703,88 +762,34 @@ void PeerServer::loop() {
   SCA_HIP_CHECK(hipStreamSynchronize(sy));
 }
 
-// CPU worker (device -1 fabrics): a reader thread takes headers and payloads
-// into up to K buffered batches while this thread computes and replies.
+// CPU worker (device -1 fabrics): one thread takes a header, reads its
+// payload, computes and replies, back to back.  Rank 0 keeps up to K calls
+// outstanding; their headers wait in the ring and their payloads in the
+// socket buffer, so a hand-off to a second thread would only add a wake-up
+// per batch (profiles/r04d_fabric_cpu).
 void PeerServer::loop_cpu() {
-  struct Batch {
-    PeerHeader h;
-    std::vector<double> x;
-  };
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<Batch> q;
-  bool done = false, computing = false;
-  std::string rerr;
-  std::thread reader([&] {
-    try {
-      while (true) {
-        Batch b;
-        b.h = f_->take();
-        if (b.h.op != kPeerStop) {
-          if (b.h.model < 0 || b.h.model >= int(models_.size()) || b.h.rows <= 0 || b.h.cols <= 0)
-            throw std::runtime_error("PeerServer: bad header (model " + std::to_string(b.h.model) + ")");
-          b.x.resize(size_t(b.h.rows) * b.h.cols);
-          f_->recv_x(b.x.data(), b.x.size() * sizeof(double), 0);
-        }
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return q.size() + (computing ? 1 : 0) < size_t(slots_) || done; });  // K slots incl. the one computing
-        if (done) return;  // the compute side failed
-        const bool stop = b.h.op == kPeerStop;
-        q.push_back(std::move(b));
-        note_inflight(q.size() + (computing ? 1 : 0) - (stop ? 1 : 0));
-        cv.notify_all();
-        if (stop) return;
-      }
-    } catch (const std::exception& e) {
-      std::lock_guard<std::mutex> lk(mu);
-      rerr = e.what();
-      done = true;
-      cv.notify_all();
-    }
-  });
-  std::vector<double> y;
-  std::string err;
+  std::vector<double> x, y;
   while (true) {
-    Batch b;
-    {
-      std::unique_lock<std::mutex> lk(mu);
-      cv.wait(lk, [&] { return !q.empty() || done; });
-      if (q.empty()) break;
-      b = std::move(q.front());
-      q.pop_front();
-      computing = b.h.op != kPeerStop;
-      cv.notify_all();
-    }
-    if (b.h.op == kPeerStop) break;
+    const PeerHeader h = f_->take();
+    if (h.op == kPeerStop) break;
+    if (h.model < 0 || h.model >= int(models_.size()) || h.rows <= 0 || h.cols <= 0)
+      throw std::runtime_error("PeerServer: bad header (model " + std::to_string(h.model) + ")");
+    note_inflight(uint64_t(1 + f_->backlog()));
+    x.resize(size_t(h.rows) * h.cols);
+    f_->recv_x(x.data(), x.size() * sizeof(double), 0);
     try {
-      auto& m = models_[size_t(b.h.model)];
-      y.resize(size_t(b.h.rows) * m->out_cols(b.h.cols));
+      auto& m = models_[size_t(h.model)];
+      y.resize(size_t(h.rows) * m->out_cols(h.cols));
       if (delay_us_) std::this_thread::sleep_for(std::chrono::microseconds(delay_us_));
-      m->run_cpu(b.x.data(), b.h.rows, b.h.cols, y.data());
-      f_->send_y(y.data(), y.size() * sizeof(double), 0);
-    } catch (const std::exception& e) {
-      err = e.what();
-      break;
+      m->run_cpu(x.data(), h.rows, h.cols, y.data());
+    } catch (...) {
+      f_->close();  // rank 0's outstanding calls fail instead of waiting for replies
+      throw;
     }
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      computing = false;
-      cv.notify_all();
-    }
+    f_->send_y(y.data(), y.size() * sizeof(double), 0);
     batches_++;
-    rows_ += uint64_t(b.h.rows);
+    rows_ += uint64_t(h.rows);
   }
-  if (!err.empty()) {  // unblock the reader: it cannot make progress without us
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      done = true;
-      cv.notify_all();
-    }
-    f_->close();
-  }
-  reader.join();
-  if (!err.empty()) throw std::runtime_error(err);
-  if (!rerr.empty()) throw std::runtime_error(rerr);
 }
 
 }  // namespace sca::par

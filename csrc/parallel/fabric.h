@@ -48,10 +48,11 @@
 //      after the send's event.  No GPU-side wait on work not yet enqueued, so
 //      the transport cannot wedge a hardware queue;
 //    - sockets, CPU fabrics (device -1: multi-process tests and CPU serving
-//      run the same header ring; a receiver thread per peer hands replies to
-//      concurrent callers in order, the worker reads batches ahead of its
-//      compute thread, and the front end's batcher keeps K calls outstanding
-//      through RowModel::start_cpu).
+//      run the same header ring; replies are read from the link's socket by
+//      whichever caller polls it (the batcher's pump, via CpuCall::done), the
+//      worker serves batches back to back from one thread (the ring and the
+//      socket buffer hold the backlog), and the front end's batcher keeps K
+//      calls outstanding through RowModel::start_cpu).
 //
 // A fan-out to K ranks (COMBINER over replicas on K GPUs) sends the batch on
 // every link (the broadcast), receives every reply into its own slab (the
@@ -176,8 +177,8 @@ class Fabric {
   void send_y(const void* p, size_t bytes, int peer);
   void recv_y(void* p, size_t bytes, int peer);
 
-  // CPU fabrics, rank 0: queue a reply read (bytes into `dst`) on the peer's
-  // receiver thread; replies arrive in issue order.
+  // CPU fabrics, rank 0: queue a reply read (bytes into `dst`); replies
+  // arrive in issue order and are read by poll_replies.
   struct Waiter {
     std::mutex mu;
     std::condition_variable cv;
@@ -186,6 +187,14 @@ class Fabric {
     std::vector<std::vector<double>> bufs;  // reply buffers owned by the call (outlive an abandoned caller)
   };
   void expect_reply(int peer, void* dst, size_t bytes, std::shared_ptr<Waiter> w);
+  // Read the replies of `peer` that have arrived and finish their waiters.
+  // block = false: never waits (another thread reading that link -> returns);
+  // block = true: waits for the oldest outstanding reply.  True if any
+  // waiter was finished.
+  bool poll_replies(int peer, bool block);
+  // Worker: headers published behind the next one to take (the batches
+  // rank 0 has outstanding here beyond the current one).
+  int backlog() const;
 
  private:
   struct Link {
@@ -197,7 +206,6 @@ class Fabric {
   int fd(int peer) const;
   void map_rings();
   bool peer_gone(int peer) const;
-  void receiver(int peer);
   void xfer(bool send, int chan, void* p, size_t bytes, int peer);
   int rank_, world_, device_;
   LoopbackHubPtr hub_;
@@ -207,19 +215,19 @@ class Fabric {
   std::vector<uint64_t> next_;      // rank 0: next seq per worker; worker: next_[0] to take
   std::mutex close_mu_;
   std::atomic<bool> open_{true};
-  // CPU reply receivers (rank 0)
+  // CPU reply queues (rank 0, one per worker, created with the fabric)
   struct Pending {
-    void* dst;
-    size_t bytes;
+    void* dst = nullptr;
+    size_t bytes = 0;
     std::shared_ptr<Waiter> w;
   };
   struct RecvQ {
-    std::mutex mu;
-    std::condition_variable cv;
+    std::mutex mu;  // the queue
+    std::mutex rd;  // the reader of the link's socket (and `off`)
     std::deque<Pending> q;
-    std::thread th;
+    size_t off = 0;  // bytes of the front reply already read
   };
-  std::mutex rq_mu_;
+  RecvQ& recvq(int peer);
   std::vector<std::unique_ptr<RecvQ>> rq_;
 };
 using FabricPtr = std::shared_ptr<Fabric>;
