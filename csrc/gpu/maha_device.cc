@@ -21,7 +21,10 @@ kern::MahaParams make_params(int p, int k, double n_stdev, double start_clip, do
   prm.max_n = max_n;
   prm.eps = eps;
   if (const char* v = std::getenv("SCA_MAHA_MW_MIN_P")) prm.mw_min_p = std::atoi(v);
-  if (const char* v = std::getenv("SCA_MAHA_JACOBI_MAX_P")) prm.jacobi_max_p = std::min(32, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("SCA_MAHA_JACOBI_MAX_P"))
+    prm.jacobi_max_p = std::min(kern::kMahaMaxP, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("SCA_MAHA_RANK1_MAX_P"))
+    prm.rank1_max_p = std::min(kern::kMahaMaxP, std::max(0, std::atoi(v)));
   return prm;
 }
 
@@ -314,9 +317,11 @@ std::vector<double> MahalanobisModel::solver_stats() const {
   if (st_->device < 0) return {};
   DeviceGuard dg(st_->device);
   if (st_->chained) SCA_HIP_CHECK(hipEventSynchronize(st_->chain.get()));
-  std::vector<double> t(13);
-  SCA_HIP_CHECK(hipMemcpy(t.data(), st_->d_eig.as<double>() + kern::kMahaMaxP * kern::kMahaMaxP + 2,
-                          13 * sizeof(double), hipMemcpyDeviceToHost));
+  std::vector<double> t(15);
+  SCA_HIP_CHECK(hipMemcpy(t.data(), st_->d_eig.as<double>() + kern::kMahaEigTail + 2, 13 * sizeof(double),
+                          hipMemcpyDeviceToHost));
+  SCA_HIP_CHECK(hipMemcpy(t.data() + 13, st_->d_eig.as<double>() + kern::kMahaEigMeta + 1, 2 * sizeof(double),
+                          hipMemcpyDeviceToHost));
   return t;
 }
 
@@ -330,6 +335,10 @@ void MahalanobisModel::set_state(const std::vector<double>& s) {
   DeviceGuard dg(st_->device);
   if (st_->chained) SCA_HIP_CHECK(hipEventSynchronize(st_->chain.get()));
   st_->d_state.upload(s.data(), s.size() * sizeof(double));
+  // the cached eigendecomposition describes the old covariance: the next
+  // step re-solves (a NaN never equals the state's n)
+  const double nan = std::nan("");
+  SCA_HIP_CHECK(hipMemcpy(st_->d_eig.as<double>() + kern::kMahaEigMeta, &nan, sizeof nan, hipMemcpyHostToDevice));
 }
 
 // ----------------------------------------------------------- MahalanobisDevice

@@ -251,23 +251,34 @@ struct MahaParams {
   int mw_min_p = 48;
   // p <= jacobi_max_p: warm-started cyclic Jacobi (one wave) instead of the
   // Householder / Sturm / inverse-iteration path (SCA_MAHA_JACOBI_MAX_P,
-  // capped at 32; 0 = never)
+  // 0 = never)
   int jacobi_max_p = 32;
+  // p <= rank1_max_p: eigen-tracking -- a one-row step updates the cached
+  // full eigendecomposition by the rank-1 secular equation (O(p^2) roots +
+  // one p^3 basis product) with a residual check; Jacobi re-seeds it when
+  // the check or the cache fails (SCA_MAHA_RANK1_MAX_P, 0 = never)
+  int rank1_max_p = 64;
 };
 // state layout (doubles): mean[p] | C[p*p] | clip_lo[p] | clip_hi[p] | n | c_zero | has_clip
 inline size_t maha_state_doubles(int p) { return size_t(p) * (p + 3) + 3; }
 // workspace doubles for a batch of nb rows
 inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (4 * size_t(p) + 2 * size_t(k)); }
 // eig: kMahaEigDoubles doubles, zero-initialised: the first kMahaMaxP^2 hold
-// the last step's eigenvectors (the Jacobi path's warm start; a cache, not
-// part of the checkpointed state).
+// the last step's eigenvectors, sorted by descending eigenvalue (the Jacobi
+// path's warm start and the eigen-tracking basis; a cache, not part of the
+// checkpointed state), then the tail, the eigenvalues (kMahaEigLam) and the
+// meta block (kMahaEigMeta: [state n the cache describes, eigen-tracking
+// steps, eigen-tracking fallbacks]).
 // Tail: [p of the cached eigenvectors, warm steps since the last cold start,
 // eigen-phase shader cycles, steps, eigen-phase 100 MHz ticks,
 // phase us x 10]: clip, cov, eigen.eigenvectors (twisted factorisation),
 // eigen (total), projections, Sherman-Morrison, state update,
 // eigen.tridiagonalise, eigen.eigenvalues (multisection),
 // eigen.back-transformation.
-constexpr int kMahaEigDoubles = kMahaMaxP * kMahaMaxP + 15;
+constexpr int kMahaEigTail = kMahaMaxP * kMahaMaxP;
+constexpr int kMahaEigLam = kMahaEigTail + 16;
+constexpr int kMahaEigMeta = kMahaEigLam + kMahaMaxP;
+constexpr int kMahaEigDoubles = kMahaEigMeta + 8;
 void maha_step(const double* X, int nb, const MahaParams& prm, double* state, double* eig, double* ws, double* scores,
                hipStream_t stream);
 // Several request batches in order (seg: nseg + 1 row offsets, device-visible):

@@ -643,12 +643,18 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
 // row), V <- V R in place.  A pair rotates only while
 // |b_ij| > tol * sqrt(|b_ii b_jj|) (tol = 1e-15, a few ulps): the sweep with no
 // rotation ends the solve.
-constexpr int kJacobiMaxP = 32;
+//
+// On exit the eigenpairs are sorted by descending eigenvalue (V's columns
+// permuted in place, sel = 0..k-1) and cached with their eigenvalues for the
+// eigen-tracking path (rank1_eigen).
+// MAXP (32 or 64) sizes the per-lane row registers: the 64 instance (p > 32,
+// only the eigen-tracking path's seed / fallback) spills; the 32 one does not.
 constexpr int kJacobiRefresh = 256;
 
+template <int kJacobiMaxP>
 __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W, int* sel, int p,
                             int k, double* __restrict__ cache, double* __restrict__ tail, double2* __restrict__ coef,
-                            int* __restrict__ partner) {
+                            int* __restrict__ partner, double* __restrict__ lamv, double* __restrict__ lam_cache) {
   const int lane = threadIdx.x & 63;
   const int m = p + (p & 1);
   const bool row = lane < p;
@@ -722,34 +728,24 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
       }
       wave_lds_sync();
       if (row) {
-        // rows: u = al * B[lane] + be * B[partner]; columns: B'[lane][q] = a_q u[q] + b_q u[pi_q]
+        // rows: u = al * B[lane] + be * B[partner] (out of place); then the
+        // columns of the lane's own row, pair by pair in place:
+        // B'[lane][q] = a_q u[q] + b_q u[pi_q]; V <- V R the same way
         const int pl = partner[lane];
-#pragma unroll
-        for (int q = 0; q < kJacobiMaxP; ++q)
-          if (q < p) reg[q] = al * cur[lane * ld_cur + q] + be * cur[pl * ld_cur + q];
-#pragma unroll
-        for (int q = 0; q < kJacobiMaxP; ++q)
-          if (q < p) nxt[lane * ld_nxt + q] = reg[q];
-        // (own row: the reads below see this lane's writes in program order)
-#pragma unroll
-        for (int q = 0; q < kJacobiMaxP; ++q)
-          if (q < p) {
-            const double2 cq = coef[q];
-            reg[q] = cq.x * reg[q] + cq.y * nxt[lane * ld_nxt + partner[q]];
-          }
-#pragma unroll
-        for (int q = 0; q < kJacobiMaxP; ++q)
-          if (q < p) nxt[lane * ld_nxt + q] = reg[q];
-        // V <- V R (own row)
-#pragma unroll
-        for (int q = 0; q < kJacobiMaxP; ++q)
-          if (q < p) {
-            const double2 cq = coef[q];
-            reg[q] = cq.x * V[lane * kLd + q] + cq.y * V[lane * kLd + partner[q]];
-          }
-#pragma unroll
-        for (int q = 0; q < kJacobiMaxP; ++q)
-          if (q < p) V[lane * kLd + q] = reg[q];
+        double* un = nxt + lane * ld_nxt;
+        double* vr = V + lane * kLd;
+        for (int q = 0; q < p; ++q) un[q] = al * cur[lane * ld_cur + q] + be * cur[pl * ld_cur + q];
+        for (int q = 0; q < p; ++q) {
+          const int pq = partner[q];  // uniform over the wave
+          if (pq <= q) continue;      // unpaired (identity) or done with its partner
+          const double2 cq = coef[q], cp = coef[pq];
+          const double a = un[q], b = un[pq];
+          un[q] = cq.x * a + cq.y * b;
+          un[pq] = cp.x * b + cp.y * a;
+          const double va = vr[q], vb = vr[pq];
+          vr[q] = cq.x * va + cq.y * vb;
+          vr[pq] = cp.x * vb + cp.y * va;
+        }
       }
       wave_lds_sync();
       double* tp = cur;
@@ -761,17 +757,32 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
     }
     if (!__any(rotated)) break;
   }
-  // top-k by the diagonal (eigenvalues), largest first
-  const double ninf = -__builtin_inf();
-  double lam = row ? cur[lane * ld_cur + lane] : ninf;
-  for (int a = 0; a < k; ++a) {
-    const double mx = wave_max(lam);
-    const unsigned long long hit = __ballot(lam == mx && row);
-    const int idx = hit ? int(__builtin_ctzll(hit)) : a;
-    if (lane == 0) sel[a] = idx;
-    if (lane == idx) lam = ninf;
+  // eigenvalues (the diagonal) in descending order: lane r's rank, then
+  // every lane permutes its own row of V (held in registers) -- top-k = the
+  // first k columns
+  const double lam = row ? cur[lane * ld_cur + lane] : 0.0;
+  if (row) lamv[lane] = lam;
+  wave_lds_sync();
+  if (row) {
+    int pos = 0;
+    for (int j = 0; j < p; ++j) {
+      const double lj = lamv[j];
+      pos += (lj > lam || (lj == lam && j < lane)) ? 1 : 0;
+    }
+    partner[lane] = pos;
+    lam_cache[pos] = lam;
   }
-  // cache the basis for the next step's warm start
+  if (lane < k) sel[lane] = lane;
+  wave_lds_sync();
+  if (row) {
+#pragma unroll
+    for (int q = 0; q < kJacobiMaxP; ++q)
+      if (q < p) reg[q] = V[lane * kLd + q];
+#pragma unroll
+    for (int q = 0; q < kJacobiMaxP; ++q)
+      if (q < p) V[lane * kLd + partner[q]] = reg[q];
+  }
+  // cache the basis for the next step's warm start / eigen-tracking
   wave_lds_sync();
   for (int e = lane; e < p * p; e += 64) cache[e] = V[(e / p) * kLd + e % p];
   if (lane == 0) {
@@ -779,6 +790,208 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
     tail[1] = warm ? tail[1] + 1.0 : 0.0;
   }
   wave_lds_sync();
+}
+
+// Eigen-tracking step for a one-row request (CoreMahalanobis.py:92-103 with
+// nb = 1): C_new = alpha C_old + rho d d^T, and the cache holds C_old =
+// V diag(lam) V^T (lam descending).  In that basis C_new = V (D + rho z z^T)
+// V^T with D = alpha diag(lam), z = V^T d: a diagonal-plus-rank-1 problem
+// whose eigenvalues are the roots of the secular equation
+//   f(x) = 1 + rho' sum_j zh_j^2 / (D_j - x) = 0,   zh = z / |z|, rho' = rho |z|^2,
+// one root in each interval (D_i, D_{i-1}) (and (D_0, D_0 + rho')).  Lane i
+// finds root i from the pole nearer to it (x = D_K + tau, the differences
+// D_j - x kept as (D_j - D_K) - tau), starting from the one-pole estimate,
+// by a bracketed two-pole rational model (Bunch-Nielsen-Sorensen: 2-3
+// iterations typical, 10 worst in 10^5 roots of the prototype).  The
+// eigenvectors use the Gu-Eisenstat recomputed zt (numerically orthogonal
+// even when roots crowd a pole), and V_new = V Q is one p^3 product in 4x4
+// register blocks (all NT threads).  Returns false -- the caller re-solves by
+// Jacobi -- on deflation (a tiny |zh_j| or a near-double eigenvalue), a root
+// that did not converge, or a residual |C_new v - lam v| above 1e-11 lam_max
+// on any of the top-k pairs (which also catches a stale cache).  A numpy
+// prototype over 1,000 steps stayed within 6e-15 of eigh's eigenvalues and
+// 1e-13 of its top-k subspace at p = 9, 32, 64.
+template <int NT>
+__device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, double rho, int p, int k,
+                            const double* __restrict__ Cn, double* __restrict__ A, double* __restrict__ V,
+                            double* __restrict__ W, EigScratch& es, int* sel, double* __restrict__ cache,
+                            double* __restrict__ tail, double* __restrict__ lam_cache, double* red, int* flag) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  double* dd = es.dg;    // D = alpha lam
+  double* zz = es.eo;    // zh^2
+  double* taus = es.sd;  // root offsets from their pole
+  double* zt = es.se2;   // Gu-Eisenstat z
+  int* Ks = reinterpret_cast<int*>(es.rn);  // root poles
+  double* inv_norm = es.part[0];
+  double* lam_new = es.part[1];
+  for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = cache[e];
+  if (tid == 0) *flag = 1;
+  __syncthreads();
+  if (tid < 64) {
+    const bool own = lane < p;
+    double z = 0.0;
+    if (own)
+      for (int r = 0; r < p; ++r) z += V[r * kLd + lane] * dvec[r];
+    const double nz2 = wave_sum(z * z);
+    const double rho2 = rho * nz2;
+    const double zh = nz2 > 0.0 ? z * rsq_nr(nz2) : 0.0;
+    const double dl = own ? alpha * lam_cache[lane] : 0.0;
+    dd[lane] = dl;
+    zz[lane] = zh * zh;
+    const double tol = 8.0 * __DBL_EPSILON__ * fmax(wave_max(fabs(dl)), rho2);
+    wave_lds_sync();
+    bool bad = own && (!(rho2 > 0.0) || rho2 * fabs(zh) <= tol || (lane > 0 && dd[lane - 1] - dl <= tol));
+    if (!__any(bad)) {
+      int K = 0;
+      double tau = 0.0;
+      bool conv = !own;
+      if (own) {
+        double lo = 0.0, hi = rho2;
+        if (lane > 0) {
+          const double mid = 0.5 * (dl + dd[lane - 1]);
+          double f = 0.0;
+          for (int j = 0; j < p; ++j) f += zz[j] / (dd[j] - mid);
+          if (1.0 + rho2 * f > 0.0) {  // f increases: the root lies below mid, nearer pole D_i
+            K = lane;
+            hi = mid - dl;
+          } else {
+            K = lane - 1;
+            lo = mid - dd[lane - 1];
+            hi = 0.0;
+          }
+        }
+        const double dK = dd[K];
+        double r0 = 0.0;
+        for (int j = 0; j < p; ++j)
+          if (j != K) r0 += zz[j] / (dd[j] - dK);
+        const double t0 = rho2 * zz[K] / (1.0 + rho2 * r0);
+        tau = (t0 > lo && t0 < hi) ? t0 : 0.5 * (lo + hi);
+        const double Dp = lane > 0 ? dd[lane - 1] - dK : 0.0;
+        for (int it = 0; it < 48 && !conv; ++it) {
+          double psi = 0.0, dpsi = 0.0, phi = 0.0, dphi = 0.0;
+          for (int j = 0; j < p; ++j) {
+            const double r = rcp_nr((dd[j] - dK) - tau);
+            const double t = zz[j] * r;
+            if (j >= lane) {
+              psi += t;
+              dpsi += t * r;
+            } else {
+              phi += t;
+              dphi += t * r;
+            }
+          }
+          psi *= rho2;
+          dpsi *= rho2;
+          phi *= rho2;
+          dphi *= rho2;
+          const double f = 1.0 + psi + phi;
+          if (f < 0.0) lo = tau;
+          else hi = tau;
+          if (fabs(f) <= 32.0 * __DBL_EPSILON__ * (1.0 + fabs(psi) + fabs(phi)) ||
+              hi - lo <= 4.0 * __DBL_EPSILON__ * fmax(fabs(lo), fabs(hi))) {
+            conv = true;
+            break;
+          }
+          // psi ~ P / (Q - t) (poles at and below the interval), phi ~ R + S / (Dp - t)
+          const double qm = tau + psi / dpsi, pp = psi * psi / dpsi;
+          double nt = 0.5 * (lo + hi);
+          if (lane == 0) {
+            nt = qm + pp;
+          } else {
+            const double dt = Dp - tau;
+            const double S = dphi * dt * dt, R = phi - S / dt;
+            const double a = 1.0 + R, b = -(a * (qm + Dp) + pp + S), c = a * qm * Dp + pp * Dp + S * qm;
+            const double disc = b * b - 4.0 * a * c;
+            if (a != 0.0 && disc >= 0.0) {
+              const double r1 = (-b - copysign(sqrt(disc), b)) / (2.0 * a);
+              const double r2 = r1 != 0.0 ? c / (a * r1) : r1;
+              if (r1 > lo && r1 < hi) nt = r1;
+              else if (r2 > lo && r2 < hi) nt = r2;
+            }
+          }
+          tau = (nt > lo && nt < hi) ? nt : 0.5 * (lo + hi);
+        }
+        Ks[lane] = K;
+        taus[lane] = tau;
+        lam_new[lane] = dK + tau;
+      }
+      bad = !conv;
+      wave_lds_sync();
+      if (!__any(bad) && own) {
+        // zt_j^2 = prod_k (lam_k - D_j) / prod_{k != j} (D_k - D_j) / rho'
+        double prod = ((dd[Ks[lane]] - dl) + taus[lane]) / rho2;
+        for (int q = 0; q < p; ++q)
+          if (q != lane) prod *= ((dd[Ks[q]] - dl) + taus[q]) / (dd[q] - dl);
+        bad = !(prod > 0.0) || !isfinite(prod);
+        zt[lane] = copysign(sqrt(fmax(prod, 0.0)), zh);
+      }
+    }
+    if (__any(bad) && lane == 0) *flag = 0;
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  // Q (columns unnormalised) -> W: Q[j][i] = zt_j / (D_j - lam_i)
+  for (int e = tid; e < p * p; e += NT) {
+    const int j = e / p, i = e - j * p;
+    W[j * kLd + i] = zt[j] / ((dd[j] - dd[Ks[i]]) - taus[i]);
+  }
+  __syncthreads();
+  if (tid < p) {
+    double sq = 0.0;
+    for (int j = 0; j < p; ++j) {
+      const double q = W[j * kLd + tid];
+      sq += q * q;
+    }
+    inv_norm[tid] = rsq_nr(sq);
+  }
+  __syncthreads();
+  // V_new = V Q diag(inv_norm) -> A (rows / columns past p of the 4x4
+  // blocks read in-bounds LDS garbage and are not stored)
+  const int nb4 = (p + 3) >> 2;
+  for (int e = tid; e < nb4 * nb4; e += NT) {
+    const int r0 = (e / nb4) * 4, c0 = (e - (e / nb4) * nb4) * 4;
+    double acc[4][4] = {};
+    for (int q = 0; q < p; ++q) {
+      double v[4], w[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) v[a] = V[(r0 + a) * kLd + q];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) w[b] = W[q * kLd + c0 + b];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] += v[a] * w[b];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (r0 + a < p && c0 + b < p) A[(r0 + a) * kLdA + c0 + b] = acc[a][b] * inv_norm[c0 + b];
+  }
+  __syncthreads();
+  // residual of the top-k pairs against the new covariance
+  double res = 0.0;
+  for (int e = tid; e < p * k; e += NT) {
+    const int r = e / k, c = e - r * k;
+    double sacc = 0.0;
+    for (int j = 0; j < p; ++j) sacc += Cn[r * kLd + j] * A[j * kLdA + c];
+    const double d = sacc - lam_new[c] * A[r * kLdA + c];
+    res += d * d;
+  }
+  res = block_sum<NT>(res, red);
+  const double lim = 1e-11 * fabs(lam_new[0]);
+  if (!(res <= lim * lim)) return false;  // (uniform: every thread holds the block sum)
+  for (int e = tid; e < p * p; e += NT) {
+    const int r = e / p, c = e - r * p;
+    const double v = A[r * kLdA + c];
+    V[r * kLd + c] = v;
+    cache[e] = v;
+  }
+  if (tid < p) lam_cache[tid] = lam_new[tid];
+  if (tid < k) sel[tid] = tid;
+  if (tid == 0) tail[1] += 1.0;  // steps since the last cold solve (tail[0] = p already)
+  __syncthreads();
+  return true;
 }
 
 // Sherman-Morrison scores for k <= 4 on one lane (CoreMahalanobis.py:118-146,
@@ -938,7 +1151,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   __shared__ int sel[kMahaMaxK];
   __shared__ double P[kMahaMaxK * kMahaMaxK], Cp[kMahaMaxK * kMahaMaxK], T1[kMahaMaxK * kMahaMaxK],
       T2[kMahaMaxK * kMahaMaxK];
-  __shared__ int valid, inverted;
+  __shared__ int valid, inverted, r1flag;
   __shared__ double scal;
   const int tid = threadIdx.x;
   const int p = prm.p, k = prm.k, kk = k * k;
@@ -1011,10 +1224,26 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   __syncthreads();
   stamp(1);
   const uint64_t c_eig0 = __builtin_amdgcn_s_memtime(), r_eig0 = __builtin_amdgcn_s_memrealtime();
-  if (p <= prm.jacobi_max_p) {
-    if (tid < 64)
-      jacobi_wave(A, V, W, sel, p, k, eig, eig + kMahaMaxP * kMahaMaxP, es.rv,
-                  reinterpret_cast<int*>(es.rn));
+  const bool tracked = p <= prm.rank1_max_p || p <= prm.jacobi_max_p;
+  if (tracked) {
+    double* tail = eig + kMahaEigTail;
+    bool done = false;
+    if (p <= prm.rank1_max_p && nb == 1 && !c_zero && tail[0] == double(p) && tail[1] < double(kJacobiRefresh) &&
+        eig[kMahaEigMeta] == n_state) {
+      done = rank1_eigen<NT>(D, (n - 1.0) / den, (n / (n + 1.0)) / den, p, k, Tm, A, V, W, es, sel, eig, tail,
+                             eig + kMahaEigLam, red, &r1flag);
+      if (tid == 0) eig[kMahaEigMeta + (done ? 1 : 2)] += 1.0;
+      if (!done) {  // A held V_new: the new covariance back for the re-solve
+        for (int e = tid; e < m * m; e += NT) A[(e / m) * kLdA + e % m] = Tm[(e / m) * kLd + e % m];
+        __syncthreads();
+      }
+    }
+    if (!done && tid < 64) {
+      if (p <= 32)
+        jacobi_wave<32>(A, V, W, sel, p, k, eig, tail, es.rv, reinterpret_cast<int*>(es.rn), es.dg, eig + kMahaEigLam);
+      else
+        jacobi_wave<64>(A, V, W, sel, p, k, eig, tail, es.rv, reinterpret_cast<int*>(es.rn), es.dg, eig + kMahaEigLam);
+    }
   } else if (NT >= 256 && p >= prm.mw_min_p) {
     topk_wave(A, V, W, es, sel, p, k, ph, 4);
   } else if (tid < 64) {
@@ -1023,7 +1252,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   __syncthreads();
   stamp(3);
   if (tid == 0) {  // shader-clock cycles and 100 MHz ticks of the eigen phase (effective clock)
-    double* tail = eig + kMahaMaxP * kMahaMaxP;
+    double* tail = eig + kMahaEigTail;
     tail[2] += double(__builtin_amdgcn_s_memtime() - c_eig0);
     tail[4] += double(__builtin_amdgcn_s_memrealtime() - r_eig0);
     tail[3] += 1.0;
@@ -1156,7 +1385,9 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   }
   stamp(6);
   if (tid == 0) {
-    double* acc = eig + kMahaMaxP * kMahaMaxP + 5;
+    // the cached eigendecomposition now describes the state's new covariance
+    eig[kMahaEigMeta] = (p <= prm.rank1_max_p || p <= prm.jacobi_max_p) ? n_new : -1.0;
+    double* acc = eig + kMahaEigTail + 5;
     for (int i = 0; i < 10; ++i) acc[i] += double(ph[i]) * 0.01;  // microseconds
   }
 }

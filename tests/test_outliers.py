@@ -178,19 +178,24 @@ def test_mahalanobis_gpu_recurrence_matches_numpy():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("p,k,start_clip,max_n,path", [(9, 3, 50, -1, "jacobi"), (20, 4, 10, 300, "jacobi"),
-                                                       (5, 5, 50, -1, "jacobi"), (32, 3, 50, -1, "jacobi"),
+@pytest.mark.parametrize("p,k,start_clip,max_n,path", [(9, 3, 50, -1, "rank1"), (20, 4, 10, 300, "rank1"),
+                                                       (5, 5, 50, -1, "rank1"), (64, 3, 100, -1, "rank1"),
+                                                       (41, 2, 50, -1, "rank1"),
+                                                       (9, 3, 50, -1, "jacobi"), (32, 3, 50, -1, "jacobi"),
                                                        (9, 3, 50, -1, "householder"), (64, 3, 100, -1, "householder"),
                                                        (41, 2, 50, -1, "householder")])
 def test_mahalanobis_device_state_parity_over_1000_requests(p, k, start_clip, max_n, path, monkeypatch):
     """Whole _get_preds on the device for 1-row requests: state (mean, C, n,
     clip) within 1e-9 of the numpy path over a 1,000-request stream (VERDICT
-    r1 next-round #6), scores to 1e-6.  p <= 32 runs the warm-started Jacobi
-    eigen path (cold restarts every 256 steps included); "householder" forces
-    the tridiagonalisation path; p = 64 (default threshold) and p = 41
-    (threshold lowered) run its 4-wave sweep."""
+    r1 next-round #6), scores to 1e-6.  "rank1" (default) tracks the
+    eigendecomposition by rank-1 secular updates, Jacobi seeding it and
+    re-solving every 256 steps; "jacobi" forces the warm-started Jacobi path;
+    "householder" the tridiagonalisation path (p = 64 and, with the
+    threshold lowered, p = 41 run its 4-wave sweep)."""
     if p == 41:
         monkeypatch.setenv("SCA_MAHA_MW_MIN_P", "32")
+    if path in ("jacobi", "householder"):
+        monkeypatch.setenv("SCA_MAHA_RANK1_MAX_P", "0")
     if path == "householder":
         monkeypatch.setenv("SCA_MAHA_JACOBI_MAX_P", "0")
     rng = np.random.default_rng(p)
@@ -205,6 +210,11 @@ def test_mahalanobis_device_state_parity_over_1000_requests(p, k, start_clip, ma
         scores_c.append(cpu.score[0])
         scores_g.append(gpu.score[0])
     assert gpu._dev is not None
+    ss = gpu._dev.solver_stats()
+    if path == "rank1":  # most steps tracked (rank-deficient early steps and 256-step refreshes re-solve)
+        assert ss["rank1_steps"] > 500, ss
+    else:
+        assert ss["rank1_steps"] == 0, ss
     st = gpu.state_dict()
     np.testing.assert_allclose(st["mean"], cpu.mean, rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(st["C"], cpu.C, rtol=1e-9, atol=1e-12)
