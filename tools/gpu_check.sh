@@ -57,7 +57,8 @@ for s in $STEPS; do
       run prof_lstm 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_lstm" -o run --output-format csv -- \
         python3 tools/kernel_microbench.py --only lstm --iters 10 ;;
     maha) run maha 300 python tools/maha_bench.py --p 9 20 32 64 --requests 2000 --threads 16 --out "$OUT/maha.json" ;;
-    maha_hh) SCA_MAHA_JACOBI_MAX_P=0 run maha_hh 300 python tools/maha_bench.py --p 9 20 32 --requests 2000 --threads 16 --out "$OUT/maha_householder.json" ;;
+    maha_jac) SCA_MAHA_RANK1_MAX_P=0 run maha_jac 300 python tools/maha_bench.py --p 9 20 32 --requests 2000 --threads 16 --out "$OUT/maha_jacobi.json" ;;
+    maha_hh) SCA_MAHA_RANK1_MAX_P=0 SCA_MAHA_JACOBI_MAX_P=0 run maha_hh 300 python tools/maha_bench.py --p 9 32 64 --requests 2000 --threads 16 --out "$OUT/maha_householder.json" ;;
     prof_maha)
       export TMPDIR=/tmp
       run prof_maha 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_maha" -o run --output-format csv -- \

@@ -88,6 +88,9 @@ def main() -> int:
                                   max(1, b1["batches"] - b0["batches"])},
             "kernel_phase_us": jac.get("phase_us_per_step"),
             "eigen_clock_mhz": jac.get("eigen_clock_mhz"),
+            "rank1_steps": jac.get("rank1_steps"),
+            "rank1_fallbacks": jac.get("rank1_fallbacks"),
+            "solver_steps": jac.get("steps"),
         }
         print(json.dumps({"p": p, **res[p]}), flush=True)
     if a.out:
