@@ -638,9 +638,9 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
 //
 // One wave; lane r owns row r of B and of V.  Parallel ordering: a round
 // rotates m/2 disjoint pairs (round-robin tournament, m = p rounded up to
-// even; pairs with the dummy index p are skipped), B <- R^T B R out of
-// place (rows mixed in registers, then columns through the lane's own LDS
-// row), V <- V R in place.  A pair rotates only while
+// even; pairs with the dummy index p are skipped), B <- R^T B R (rows mixed
+// out of place into the other buffer, then the columns of each lane's own
+// row pair by pair in place), V <- V R in place.  A pair rotates only while
 // |b_ij| > tol * sqrt(|b_ii b_jj|) (tol = 1e-15, a few ulps): the sweep with no
 // rotation ends the solve.
 //
