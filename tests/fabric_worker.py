@@ -26,6 +26,8 @@ def main():
         return concurrent(lr, rank, world)
     if mode == "orphan":
         return orphan(lr, rank, world)
+    if mode == "large":
+        return large(lr, rank, world)
     if mode == "combiner":  # K-way gather: one model per rank, averaged on rank 0
         kids = [{"name": f"m{r}", "type": "MODEL", "rank": r} for r in range(world)]
         graph = {"name": "comb", "type": "COMBINER", "implementation": "AVERAGE_COMBINER", "children": kids}
@@ -119,6 +121,62 @@ def concurrent(lr, rank, world):
     fabric.stop_peers()
     fabric.close()
     print(json.dumps({"rank": 0, "worst": worst[0], "rows": rows[0], "errors": errors}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def large(lr, rank, world):
+    """Replies far larger than a socket buffer (60k rows x 3 classes = 1.4 MB)
+    arrive in pieces: the polling reader keeps its place in the reply across
+    EAGAINs, both through the asynchronous path (two callers' replies queued
+    back to back) and the synchronous one."""
+    import threading
+
+    import numpy as np
+    import torch.distributed as dist
+
+    import seldon_core_amd as sca
+    from seldon_core_amd.parallel.fabric import init_fabric, serve_peer
+
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+            "graph": {"name": "m", "type": "MODEL", "rank": 1}}
+    fabric = init_fabric(device=-1)
+    if rank != 0:
+        srv = serve_peer(spec, fabric, {"m": lr})
+        srv.join()
+        print(json.dumps({"rank": rank, "batches": srv.batches, "rows": srv.rows, "error": srv.error()}), flush=True)
+        fabric.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    C = sca.native()
+    m = C.peer_row_model(fabric, [1], 0, 4, 3)
+    rng = np.random.default_rng(3)
+    worst = [0.0]
+    errors = []
+
+    def client(t):
+        try:
+            for _ in range(3):
+                X = rng.normal(loc=4.0, scale=1.5, size=(60000 - 7 * t, 4))
+                got = m.run_cpu(X)
+                worst[0] = max(worst[0], float(np.abs(got - lr.predict_proba(X)).max()))
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=client, args=(t,)) for t in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    # the batcher's asynchronous path (start_cpu + polling)
+    dep = sca.Deployment(spec, components={"m": lr}, device=-1, fabric=fabric)
+    X = rng.normal(loc=4.0, scale=1.5, size=(30000, 4))
+    out = dep.predict({"data": {"ndarray": X.tolist()}})
+    worst[0] = max(worst[0], float(np.abs(np.asarray(out["data"]["ndarray"]) - lr.predict_proba(X)).max()))
+    dep.close()
+    fabric.close()
+    print(json.dumps({"rank": 0, "worst": worst[0], "errors": errors}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

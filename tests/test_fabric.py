@@ -120,6 +120,12 @@ def test_concurrent_senders_keep_k_batches_in_flight_cpu_fabric():
         assert 2 <= w["max_inflight"] <= 4, w
 
 
+def test_large_replies_arrive_in_pieces_cpu_fabric():
+    outs = _run_ranks(2, "large")
+    assert outs[0]["errors"] == [] and outs[0]["worst"] < 1e-12, outs[0]
+    assert outs[1]["error"] == "" and outs[1]["rows"] >= 3 * 60000, outs[1]
+
+
 def test_header_ring_liveness_worker_exits_when_front_end_dies():
     """A worker polling its header ring notices rank 0's death (control
     socket EOF) and leaves with an error instead of spinning forever."""
