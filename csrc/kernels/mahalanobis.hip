@@ -623,70 +623,74 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
   mark(9);  // back-transformation
 }
 
-// Top-k eigenpairs for p <= kJacobiMaxP by cyclic Jacobi, WARM-STARTED from
+// Full eigendecomposition by cyclic Jacobi (one wave), WARM-STARTED from
 // the previous step's eigenvectors (kept in eig[0 .. p*p)).  The covariance
 // changes by a rank-nb update of weight ~1/n per request, so
 // B = V0^T C V0 is diagonal but for O(1/n) off-diagonals and two or three
-// threshold-Jacobi sweeps (quadratic convergence) diagonalise it, where the
-// Householder path pays a full tridiagonalisation every step
-// (profiles/r03r_head: 15.8 us of a 24 us step at p = 9).  Cold starts (no
-// cache, the first step, every kJacobiRefresh-th step to bound the drift of
-// V0's orthogonality) start from V0 = I.  The score depends only on the
-// top-k SUBSPACE (projections, proj_cov and the Sherman-Morrison recurrence
-// all change by the same k x k rotation), so any orthonormal basis of it
-// gives the reference's scores.
+// threshold-Jacobi sweeps (quadratic convergence) diagonalise it.  Cold
+// starts (no cache, the first step, every `refresh`-th step to bound the
+// drift of V0's orthogonality) start from V0 = I.  The score depends only on
+// the top-k SUBSPACE (projections, proj_cov and the Sherman-Morrison
+// recurrence all change by the same k x k rotation), so any orthonormal basis
+// of it gives the reference's scores.
 //
-// One wave; lane r owns row r of B and of V.  Parallel ordering: a round
-// rotates m/2 disjoint pairs (round-robin tournament, m = p rounded up to
-// even; pairs with the dummy index p are skipped), B <- R^T B R (rows mixed
-// out of place into the other buffer, then the columns of each lane's own
-// row pair by pair in place), V <- V R in place.  A pair rotates only while
-// |b_ij| > tol * sqrt(|b_ii b_jj|) (tol = 1e-15, a few ulps): the sweep with no
-// rotation ends the solve.
-//
-// On exit the eigenpairs are sorted by descending eigenvalue (V's columns
-// permuted in place, sel = 0..k-1) and cached with their eigenvalues for the
-// eigen-tracking path (rank1_eigen).
-// MAXP (32 or 64) sizes the per-lane row registers: the 64 instance (p > 32,
-// only the eigen-tracking path's seed / fallback) spills; the 32 one does not.
-constexpr int kJacobiRefresh = 256;
+// Lane r owns row r of B and row r of V^T (the eigenvectors are kept
+// transposed during the sweeps).  A round rotates m/2 disjoint pairs
+// (round-robin tournament, m = p rounded up to even; pairs with the dummy
+// index p are skipped); every lane needs only ITS pair's (c, s) and partner:
+//   U = R^T B      row mix:          U[r][:]  = a_r B[r][:] + b_r B[pi_r][:]
+//   B' = U R       by symmetry:      B'[r][q] = a_r U[q][r] + b_r U[q][pi_r]
+//                  (column reads of U, conflict-free across the wave)
+//   V'^T = R^T V^T row mix in place (a column's loads precede its stores)
+// Every LDS loop runs in blocks of 8 independent loads.  A pair rotates only
+// while |b_ij| > tol * sqrt(|b_ii b_jj|) (tol = 1e-15, a few ulps): the sweep
+// with no rotation ends the solve.  On exit the eigenpairs are sorted by
+// descending eigenvalue into V (columns; sel = 0..k-1) and cached with their
+// eigenvalues for the eigen-tracking path (rank1_eigen).
+constexpr int kJacobiRefresh = 256;   // Jacobi-only mode: cold solve period
+constexpr int kTrackRefresh = 1024;   // eigen-tracking mode: cold solve period
 
-template <int kJacobiMaxP>
 __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W, int* sel, int p,
-                            int k, double* __restrict__ cache, double* __restrict__ tail, double2* __restrict__ coef,
-                            int* __restrict__ partner, double* __restrict__ lamv, double* __restrict__ lam_cache) {
+                            int k, double* __restrict__ cache, double* __restrict__ tail, double* __restrict__ lamv, double* __restrict__ lam_cache, int refresh) {
   const int lane = threadIdx.x & 63;
   const int m = p + (p & 1);
   const bool row = lane < p;
-  const bool warm = tail[0] == double(p) && tail[1] < double(kJacobiRefresh);
-  double reg[kJacobiMaxP];
+  const bool warm = tail[0] == double(p) && tail[1] < double(refresh);
   if (warm) {
     for (int e = lane; e < p * p; e += 64) V[(e / p) * kLd + e % p] = cache[e];
     wave_lds_sync();
-    // T = C V0 -> W (lane r: row r), then B = V0^T T -> A (lane r: row r = column r of V0)
+    // T = C V0 -> W (lane r: row r); then B = V0^T T -> A (lane r: row r)
     if (row) {
+      for (int q0 = 0; q0 < p; q0 += 8) {
+        double acc[8] = {};
+        for (int j = 0; j < p; ++j) {
+          const double a = A[lane * kLdA + j];
 #pragma unroll
-      for (int j = 0; j < kJacobiMaxP; ++j) reg[j] = j < p ? A[lane * kLdA + j] : 0.0;
-      for (int q = 0; q < p; ++q) {
-        double t = 0.0;
+          for (int b = 0; b < 8; ++b) acc[b] += a * V[j * kLd + q0 + b];  // (q0 + b <= 63: in the row)
+        }
 #pragma unroll
-        for (int j = 0; j < kJacobiMaxP; ++j)
-          if (j < p) t += reg[j] * V[j * kLd + q];
-        W[lane * kLd + q] = t;
+        for (int b = 0; b < 8; ++b)
+          if (q0 + b < p) W[lane * kLd + q0 + b] = acc[b];
       }
     }
     wave_lds_sync();
     if (row) {
+      for (int q0 = 0; q0 < p; q0 += 8) {
+        double acc[8] = {};
+        for (int j = 0; j < p; ++j) {
+          const double v = V[j * kLd + lane];
 #pragma unroll
-      for (int j = 0; j < kJacobiMaxP; ++j) reg[j] = j < p ? V[j * kLd + lane] : 0.0;
-      for (int q = 0; q < p; ++q) {
-        double b = 0.0;
+          for (int b = 0; b < 8; ++b) acc[b] += v * W[j * kLd + q0 + b];
+        }
 #pragma unroll
-        for (int j = 0; j < kJacobiMaxP; ++j)
-          if (j < p) b += reg[j] * W[j * kLd + q];
-        A[lane * kLdA + q] = b;
+        for (int b = 0; b < 8; ++b)
+          if (q0 + b < p) A[lane * kLdA + q0 + b] = acc[b];
       }
     }
+    wave_lds_sync();
+    // V^T = V0^T
+    if (row)
+      for (int q = 0; q < p; ++q) V[lane * kLd + q] = cache[q * p + lane];
   } else if (row) {
     for (int q = 0; q < p; ++q) V[lane * kLd + q] = lane == q ? 1.0 : 0.0;
   }
@@ -695,9 +699,6 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
   if (row)
     for (int q = 0; q < lane; ++q) A[lane * kLdA + q] = A[q * kLdA + lane];
   wave_lds_sync();
-  double* cur = A;
-  double* nxt = W;
-  int ld_cur = kLdA, ld_nxt = kLd;
   constexpr double tol = 1e-15;
   for (int sweep = 0; sweep < 40; ++sweep) {
     bool rotated = false;
@@ -710,81 +711,89 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
         pr = opp == 0 ? 0 : 1 + (opp - 1 + rnd) % (m - 1);
       }
       double al = 1.0, be = 0.0;
+      int pl = lane;
       if (row && pr < p) {
         const int i = min(lane, pr), j = max(lane, pr);
-        const double aii = cur[i * ld_cur + i], ajj = cur[j * ld_cur + j], aij = cur[i * ld_cur + j];
+        const double aii = A[i * kLdA + i], ajj = A[j * kLdA + j], aij = A[i * kLdA + j];
         if (aij != 0.0 && fabs(aij) > tol * sqrt(fabs(aii * ajj))) {
           const double th = (aii - ajj) / (2.0 * aij);
           const double t = -copysign(1.0, th) / (fabs(th) + sqrt(1.0 + th * th));
           const double c = 1.0 / sqrt(1.0 + t * t), sn = t * c;
           al = c;
           be = lane == i ? -sn : sn;
+          pl = pr;
           rotated = true;
         }
       }
-      if (lane < m) {
-        coef[lane] = make_double2(al, be);
-        partner[lane] = (row && pr < p) ? pr : lane;
-      }
-      wave_lds_sync();
       if (row) {
-        // rows: u = al * B[lane] + be * B[partner] (out of place); then the
-        // columns of the lane's own row, pair by pair in place:
-        // B'[lane][q] = a_q u[q] + b_q u[pi_q]; V <- V R the same way
-        const int pl = partner[lane];
-        double* un = nxt + lane * ld_nxt;
-        double* vr = V + lane * kLd;
-        for (int q = 0; q < p; ++q) un[q] = al * cur[lane * ld_cur + q] + be * cur[pl * ld_cur + q];
-        for (int q = 0; q < p; ++q) {
-          const int pq = partner[q];  // uniform over the wave
-          if (pq <= q) continue;      // unpaired (identity) or done with its partner
-          const double2 cq = coef[q], cp = coef[pq];
-          const double a = un[q], b = un[pq];
-          un[q] = cq.x * a + cq.y * b;
-          un[pq] = cp.x * b + cp.y * a;
-          const double va = vr[q], vb = vr[pq];
-          vr[q] = cq.x * va + cq.y * vb;
-          vr[pq] = cp.x * vb + cp.y * va;
+        // U = R^T B -> W (rows)
+        for (int q0 = 0; q0 < p; q0 += 8) {
+          double x[8], y[8];
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            x[b] = A[lane * kLdA + q0 + b];  // (A rows carry 8 padding columns)
+            y[b] = A[pl * kLdA + q0 + b];
+          }
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+            if (q0 + b < p) W[lane * kLd + q0 + b] = al * x[b] + be * y[b];
         }
       }
       wave_lds_sync();
-      double* tp = cur;
-      cur = nxt;
-      nxt = tp;
-      const int tl = ld_cur;
-      ld_cur = ld_nxt;
-      ld_nxt = tl;
+      if (row) {
+        // B' = U R -> A, through the symmetry: B'[r][q] = a_r U[q][r] + b_r U[q][pi_r]
+        for (int q0 = 0; q0 < p; q0 += 8) {
+          double x[8], y[8];
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            const int q = min(q0 + b, p - 1);
+            x[b] = W[q * kLd + lane];
+            y[b] = W[q * kLd + pl];
+          }
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+            if (q0 + b < p) A[lane * kLdA + q0 + b] = al * x[b] + be * y[b];
+        }
+        // V^T <- R^T V^T in place: this block's loads (own and partner rows)
+        // are all issued before its stores
+        for (int q0 = 0; q0 < p; q0 += 8) {
+          double x[8], y[8];
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            x[b] = V[lane * kLd + q0 + b];
+            y[b] = V[pl * kLd + q0 + b];
+          }
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+            if (q0 + b < p) V[lane * kLd + q0 + b] = al * x[b] + be * y[b];
+        }
+      }
+      wave_lds_sync();
     }
     if (!__any(rotated)) break;
   }
-  // eigenvalues (the diagonal) in descending order: lane r's rank, then
-  // every lane permutes its own row of V (held in registers) -- top-k = the
-  // first k columns
-  const double lam = row ? cur[lane * ld_cur + lane] : 0.0;
+  // eigenvalues (the diagonal) in descending order: lane r's rank; the
+  // eigenvectors (rows of V^T) land sorted in the COLUMNS of V through W
+  const double lam = row ? A[lane * kLdA + lane] : 0.0;
   if (row) lamv[lane] = lam;
   wave_lds_sync();
+  int pos = 0;
   if (row) {
-    int pos = 0;
     for (int j = 0; j < p; ++j) {
       const double lj = lamv[j];
       pos += (lj > lam || (lj == lam && j < lane)) ? 1 : 0;
     }
-    partner[lane] = pos;
     lam_cache[pos] = lam;
+    for (int r = 0; r < p; ++r) W[r * kLd + pos] = V[lane * kLd + r];
   }
   if (lane < k) sel[lane] = lane;
   wave_lds_sync();
-  if (row) {
-#pragma unroll
-    for (int q = 0; q < kJacobiMaxP; ++q)
-      if (q < p) reg[q] = V[lane * kLd + q];
-#pragma unroll
-    for (int q = 0; q < kJacobiMaxP; ++q)
-      if (q < p) V[lane * kLd + partner[q]] = reg[q];
+  for (int e = lane; e < p * p; e += 64) {
+    const double v = W[(e / p) * kLd + e % p];
+    V[(e / p) * kLd + e % p] = v;
+    cache[e] = v;  // the basis for the next step's warm start / eigen-tracking
   }
-  // cache the basis for the next step's warm start / eigen-tracking
-  wave_lds_sync();
-  for (int e = lane; e < p * p; e += 64) cache[e] = V[(e / p) * kLd + e % p];
   if (lane == 0) {
     tail[0] = double(p);
     tail[1] = warm ? tail[1] + 1.0 : 0.0;
@@ -1228,7 +1237,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   if (tracked) {
     double* tail = eig + kMahaEigTail;
     bool done = false;
-    if (p <= prm.rank1_max_p && nb == 1 && !c_zero && tail[0] == double(p) && tail[1] < double(kJacobiRefresh) &&
+    if (p <= prm.rank1_max_p && nb == 1 && !c_zero && tail[0] == double(p) && tail[1] < double(kTrackRefresh) &&
         eig[kMahaEigMeta] == n_state) {
       done = rank1_eigen<NT>(D, (n - 1.0) / den, (n / (n + 1.0)) / den, p, k, Tm, A, V, W, es, sel, eig, tail,
                              eig + kMahaEigLam, red, &r1flag);
@@ -1238,12 +1247,9 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
         __syncthreads();
       }
     }
-    if (!done && tid < 64) {
-      if (p <= 32)
-        jacobi_wave<32>(A, V, W, sel, p, k, eig, tail, es.rv, reinterpret_cast<int*>(es.rn), es.dg, eig + kMahaEigLam);
-      else
-        jacobi_wave<64>(A, V, W, sel, p, k, eig, tail, es.rv, reinterpret_cast<int*>(es.rn), es.dg, eig + kMahaEigLam);
-    }
+    if (!done && tid < 64)
+      jacobi_wave(A, V, W, sel, p, k, eig, tail, es.dg, eig + kMahaEigLam,
+                  p <= prm.rank1_max_p ? kTrackRefresh : kJacobiRefresh);
   } else if (NT >= 256 && p >= prm.mw_min_p) {
     topk_wave(A, V, W, es, sel, p, k, ph, 4);
   } else if (tid < 64) {
