@@ -373,10 +373,12 @@ PYBIND11_MODULE(_C, m) {
       .def("solver_stats", [](const gpu::MahalanobisDevice& d) {
         const auto t = d.solver_stats();
         py::dict r;
-        if (t.size() == 15) {
+        if (t.size() == 17) {
           r["steps"] = t[1];
           r["rank1_steps"] = t[13];     // eigen-tracking (secular-equation) steps
           r["rank1_fallbacks"] = t[14];  // of which re-solved by Jacobi (cache or residual check failed)
+          r["jacobi_solves"] = t[16];
+          r["jacobi_sweeps_per_solve"] = t[16] > 0 ? t[15] / t[16] : 0.0;
           // s_memtime cycles / s_memrealtime (100 MHz) ticks over the eigen phase
           r["eigen_clock_mhz"] = t[2] > 0 ? t[0] / (t[2] * 0.01) : 0.0;
           static const char* names[10] = {"clip", "cov", "eigen.vectors", "eigen", "proj", "sm", "update",

@@ -317,10 +317,10 @@ std::vector<double> MahalanobisModel::solver_stats() const {
   if (st_->device < 0) return {};
   DeviceGuard dg(st_->device);
   if (st_->chained) SCA_HIP_CHECK(hipEventSynchronize(st_->chain.get()));
-  std::vector<double> t(15);
+  std::vector<double> t(17);
   SCA_HIP_CHECK(hipMemcpy(t.data(), st_->d_eig.as<double>() + kern::kMahaEigTail + 2, 13 * sizeof(double),
                           hipMemcpyDeviceToHost));
-  SCA_HIP_CHECK(hipMemcpy(t.data() + 13, st_->d_eig.as<double>() + kern::kMahaEigMeta + 1, 2 * sizeof(double),
+  SCA_HIP_CHECK(hipMemcpy(t.data() + 13, st_->d_eig.as<double>() + kern::kMahaEigMeta + 1, 4 * sizeof(double),
                           hipMemcpyDeviceToHost));
   return t;
 }

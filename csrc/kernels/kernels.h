@@ -268,7 +268,7 @@ inline size_t maha_ws_doubles(int nb, int p, int k) { return size_t(nb) * (4 * s
 // path's warm start and the eigen-tracking basis; a cache, not part of the
 // checkpointed state), then the tail, the eigenvalues (kMahaEigLam) and the
 // meta block (kMahaEigMeta: [state n the cache describes, eigen-tracking
-// steps, eigen-tracking fallbacks]).
+// steps, eigen-tracking fallbacks, Jacobi sweeps, Jacobi solves]).
 // Tail: [p of the cached eigenvectors, warm steps since the last cold start,
 // eigen-phase shader cycles, steps, eigen-phase 100 MHz ticks,
 // phase us x 10]: clip, cov, eigen.eigenvectors (twisted factorisation),

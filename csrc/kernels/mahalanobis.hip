@@ -643,15 +643,16 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
 //                  (column reads of U, conflict-free across the wave)
 //   V'^T = R^T V^T row mix in place (a column's loads precede its stores)
 // Every LDS loop runs in blocks of 8 independent loads.  A pair rotates only
-// while |b_ij| > tol * sqrt(|b_ii b_jj|) (tol = 1e-15, a few ulps): the sweep
-// with no rotation ends the solve.  On exit the eigenpairs are sorted by
+// while |b_ij| > tol * sqrt(|b_ii b_jj|) (tol = 1e-14; the rotated element is
+// set to exactly 0): the sweep with no rotation ends the solve.  On exit the eigenpairs are sorted by
 // descending eigenvalue into V (columns; sel = 0..k-1) and cached with their
 // eigenvalues for the eigen-tracking path (rank1_eigen).
 constexpr int kJacobiRefresh = 256;   // Jacobi-only mode: cold solve period
 constexpr int kTrackRefresh = 1024;   // eigen-tracking mode: cold solve period
 
 __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W, int* sel, int p,
-                            int k, double* __restrict__ cache, double* __restrict__ tail, double* __restrict__ lamv, double* __restrict__ lam_cache, int refresh) {
+                            int k, double* __restrict__ cache, double* __restrict__ tail, double* __restrict__ lamv,
+                            double* __restrict__ lam_cache, int refresh, double* __restrict__ stats) {
   const int lane = threadIdx.x & 63;
   const int m = p + (p & 1);
   const bool row = lane < p;
@@ -699,7 +700,7 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
   if (row)
     for (int q = 0; q < lane; ++q) A[lane * kLdA + q] = A[q * kLdA + lane];
   wave_lds_sync();
-  constexpr double tol = 1e-15;
+  constexpr double tol = 1e-14;
   for (int sweep = 0; sweep < 40; ++sweep) {
     bool rotated = false;
     for (int rnd = 0; rnd < m - 1; ++rnd) {
@@ -754,6 +755,7 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
           for (int b = 0; b < 8; ++b)
             if (q0 + b < p) A[lane * kLdA + q0 + b] = al * x[b] + be * y[b];
         }
+        if (pl != lane) A[lane * kLdA + pl] = 0.0;  // the annihilated pair: exactly, not its rounding residue
         // V^T <- R^T V^T in place: this block's loads (own and partner rows)
         // are all issued before its stores
         for (int q0 = 0; q0 < p; q0 += 8) {
@@ -771,7 +773,17 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
       }
       wave_lds_sync();
     }
-    if (!__any(rotated)) break;
+    if (!__any(rotated)) {
+      if (lane == 0) {  // solver statistics (kMahaEigMeta + 3 / + 4)
+        stats[0] += double(sweep + 1);
+        stats[1] += 1.0;
+      }
+      break;
+    }
+    if (sweep == 39 && lane == 0) {
+      stats[0] += 40.0;
+      stats[1] += 1.0;
+    }
   }
   // eigenvalues (the diagonal) in descending order: lane r's rank; the
   // eigenvectors (rows of V^T) land sorted in the COLUMNS of V through W
@@ -1249,7 +1261,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     }
     if (!done && tid < 64)
       jacobi_wave(A, V, W, sel, p, k, eig, tail, es.dg, eig + kMahaEigLam,
-                  p <= prm.rank1_max_p ? kTrackRefresh : kJacobiRefresh);
+                  p <= prm.rank1_max_p ? kTrackRefresh : kJacobiRefresh, eig + kMahaEigMeta + 3);
   } else if (NT >= 256 && p >= prm.mw_min_p) {
     topk_wave(A, V, W, es, sel, p, k, ph, 4);
   } else if (tid < 64) {

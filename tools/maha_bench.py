@@ -91,6 +91,8 @@ def main() -> int:
             "rank1_steps": jac.get("rank1_steps"),
             "rank1_fallbacks": jac.get("rank1_fallbacks"),
             "solver_steps": jac.get("steps"),
+            "jacobi_solves": jac.get("jacobi_solves"),
+            "jacobi_sweeps_per_solve": jac.get("jacobi_sweeps_per_solve"),
         }
         print(json.dumps({"p": p, **res[p]}), flush=True)
     if a.out:
