@@ -649,6 +649,7 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
 // eigenvalues for the eigen-tracking path (rank1_eigen).
 constexpr int kJacobiRefresh = 256;   // Jacobi-only mode: cold solve period
 constexpr int kTrackRefresh = 1024;   // eigen-tracking mode: cold solve period
+constexpr int kTrackMaxRows = 16;     // requests with more rows re-solve by Jacobi
 
 __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W, int* sel, int p,
                             int k, double* __restrict__ cache, double* __restrict__ tail, double* __restrict__ lamv,
@@ -813,8 +814,9 @@ __device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, doub
   wave_lds_sync();
 }
 
-// Eigen-tracking step for a one-row request (CoreMahalanobis.py:92-103 with
-// nb = 1): C_new = alpha C_old + rho d d^T, and the cache holds C_old =
+// Eigen-tracking update for one row of a request (CoreMahalanobis.py:92-103;
+// a request of nb <= kTrackMaxRows rows is nb of these in turn, the residual
+// checked after the last): C_new = alpha C_old + rho d d^T, and the cache holds C_old =
 // V diag(lam) V^T (lam descending).  In that basis C_new = V (D + rho z z^T)
 // V^T with D = alpha diag(lam), z = V^T d: a diagonal-plus-rank-1 problem
 // whose eigenvalues are the roots of the secular equation
@@ -836,7 +838,11 @@ template <int NT>
 __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, double rho, int p, int k,
                             const double* __restrict__ Cn, double* __restrict__ A, double* __restrict__ V,
                             double* __restrict__ W, EigScratch& es, int* sel, double* __restrict__ cache,
-                            double* __restrict__ tail, double* __restrict__ lam_cache, double* red, int* flag) {
+                            double* __restrict__ tail, double* __restrict__ lam_cache, double* red, int* flag,
+                            bool first, bool last) {
+  // first: the basis / eigenvalues come from the cache (else from the
+  // previous update of this request: V and lam_new in LDS); last: check the
+  // residual against C_new and write the cache
   const int tid = threadIdx.x, lane = tid & 63;
   double* dd = es.dg;    // D = alpha lam
   double* zz = es.eo;    // zh^2
@@ -845,7 +851,9 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   int* Ks = reinterpret_cast<int*>(es.rn);  // root poles
   double* inv_norm = es.part[0];
   double* lam_new = es.part[1];
-  for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = cache[e];
+  const double* lam_src = first ? lam_cache : lam_new;
+  if (first)
+    for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = cache[e];
   if (tid == 0) *flag = 1;
   __syncthreads();
   if (tid < 64) {
@@ -856,7 +864,8 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     const double nz2 = wave_sum(z * z);
     const double rho2 = rho * nz2;
     const double zh = nz2 > 0.0 ? z * rsq_nr(nz2) : 0.0;
-    const double dl = own ? alpha * lam_cache[lane] : 0.0;
+    const double dl = own ? alpha * lam_src[lane] : 0.0;
+    wave_lds_sync();  // (lam_src may be lam_new, rewritten below)
     dd[lane] = dl;
     zz[lane] = zh * zh;
     const double tol = 8.0 * __DBL_EPSILON__ * fmax(wave_max(fabs(dl)), rho2);
@@ -990,6 +999,11 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
         if (r0 + a < p && c0 + b < p) A[(r0 + a) * kLdA + c0 + b] = acc[a][b] * inv_norm[c0 + b];
   }
   __syncthreads();
+  if (!last) {  // the next row's update starts from this basis
+    for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = A[(e / p) * kLdA + e % p];
+    __syncthreads();
+    return true;
+  }
   // residual of the top-k pairs against the new covariance
   double res = 0.0;
   for (int e = tid; e < p * k; e += NT) {
@@ -1249,10 +1263,14 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   if (tracked) {
     double* tail = eig + kMahaEigTail;
     bool done = false;
-    if (p <= prm.rank1_max_p && nb == 1 && !c_zero && tail[0] == double(p) && tail[1] < double(kTrackRefresh) &&
-        eig[kMahaEigMeta] == n_state) {
-      done = rank1_eigen<NT>(D, (n - 1.0) / den, (n / (n + 1.0)) / den, p, k, Tm, A, V, W, es, sel, eig, tail,
-                             eig + kMahaEigLam, red, &r1flag);
+    if (p <= prm.rank1_max_p && nb <= kTrackMaxRows && !c_zero && tail[0] == double(p) &&
+        tail[1] < double(kTrackRefresh) && eig[kMahaEigMeta] == n_state) {
+      // C_new = alpha C_old + sum_i c_i / den d_i d_i^T: one rank-1 update per row
+      done = true;
+      for (int i = 0; i < nb && done; ++i)
+        done = rank1_eigen<NT>(D + size_t(i) * p, i == 0 ? (n - 1.0) / den : 1.0, ((n + i) / (n + i + 1.0)) / den, p,
+                               k, Tm, A, V, W, es, sel, eig, tail, eig + kMahaEigLam, red, &r1flag, i == 0,
+                               i == nb - 1);
       if (tid == 0) eig[kMahaEigMeta + (done ? 1 : 2)] += 1.0;
       if (!done) {  // A held V_new: the new covariance back for the re-solve
         for (int e = tid; e < m * m; e += NT) A[(e / m) * kLdA + e % m] = Tm[(e / m) * kLd + e % m];

@@ -178,6 +178,29 @@ def test_mahalanobis_gpu_recurrence_matches_numpy():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("p", [7, 40])
+def test_mahalanobis_device_multirow_tracking_parity(p):
+    """Requests of 1-16 rows: each row one rank-1 update of the tracked
+    eigendecomposition, the residual checked after the last; requests of more
+    rows (20) re-solve by Jacobi.  Scores and state match numpy over 300
+    requests."""
+    rng = np.random.default_rng(11)
+    cpu = OutlierMahalanobis(n_components=3, device=-1)
+    gpu = OutlierMahalanobis(n_components=3, device=0)
+    scale = np.linspace(0.5, 2.0, p)
+    for i in range(300):
+        nb = [1, 2, 5, 16, 20][i % 5]
+        X = rng.normal(size=(nb, p)) * scale
+        cpu.predict(X.copy(), [])
+        gpu.predict(X.copy(), [])
+        np.testing.assert_allclose(gpu.score, cpu.score, rtol=1e-6, atol=1e-9)
+    ss = gpu._dev.solver_stats()
+    assert ss["rank1_steps"] > 150, ss
+    st = gpu.state_dict()
+    np.testing.assert_allclose(st["C"], cpu.C, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("p,k,start_clip,max_n,path", [(9, 3, 50, -1, "rank1"), (20, 4, 10, 300, "rank1"),
                                                        (5, 5, 50, -1, "rank1"), (64, 3, 100, -1, "rank1"),
                                                        (41, 2, 50, -1, "rank1"),
