@@ -651,7 +651,7 @@ constexpr int kJacobiRefresh = 256;   // Jacobi-only mode: cold solve period
 constexpr int kTrackRefresh = 1024;   // eigen-tracking mode: cold solve period
 constexpr int kTrackMaxRows = 16;     // requests with more rows re-solve by Jacobi
 
-__device__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W, int* sel, int p,
+__device__ __forceinline__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W, int* sel, int p,
                             int k, double* __restrict__ cache, double* __restrict__ tail, double* __restrict__ lamv,
                             double* __restrict__ lam_cache, int refresh, double* __restrict__ stats) {
   const int lane = threadIdx.x & 63;
