@@ -1186,7 +1186,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   __shared__ int sel[kMahaMaxK];
   __shared__ double P[kMahaMaxK * kMahaMaxK], Cp[kMahaMaxK * kMahaMaxK], T1[kMahaMaxK * kMahaMaxK],
       T2[kMahaMaxK * kMahaMaxK];
-  __shared__ int valid, inverted, r1flag;
+  __shared__ int valid, inverted, r1flag, track;
   __shared__ double scal;
   const int tid = threadIdx.x;
   const int p = prm.p, k = prm.k, kk = k * k;
@@ -1263,8 +1263,13 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   if (tracked) {
     double* tail = eig + kMahaEigTail;
     bool done = false;
-    if (p <= prm.rank1_max_p && nb <= kTrackMaxRows && !c_zero && tail[0] == double(p) &&
-        tail[1] < double(kTrackRefresh) && eig[kMahaEigMeta] == n_state) {
+    // The branch below has barriers: decided by ONE thread from the cache
+    // words (global memory) and broadcast, so every wave takes it or none.
+    if (tid == 0)
+      track = p <= prm.rank1_max_p && nb <= kTrackMaxRows && !c_zero && tail[0] == double(p) &&
+               tail[1] < double(kTrackRefresh) && eig[kMahaEigMeta] == n_state;
+    __syncthreads();
+    if (track) {
       // C_new = alpha C_old + sum_i c_i / den d_i d_i^T: one rank-1 update per row
       done = true;
       for (int i = 0; i < nb && done; ++i)

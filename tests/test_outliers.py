@@ -178,6 +178,23 @@ def test_mahalanobis_gpu_recurrence_matches_numpy():
 
 
 @pytest.mark.gpu
+def test_mahalanobis_tracking_crosses_cold_refresh():
+    """1,100 one-row steps at p = 20 (the 256-thread kernel): the tracked
+    eigendecomposition is re-solved cold after 1,024 steps (the branch into
+    it is taken by every wave or none), and the scores stay on numpy's."""
+    rng = np.random.default_rng(12)
+    cpu = OutlierMahalanobis(n_components=3, device=-1)
+    gpu = OutlierMahalanobis(n_components=3, device=0)
+    for i in range(1100):
+        X = rng.normal(size=(1, 20))
+        cpu.predict(X.copy(), [])
+        gpu.predict(X.copy(), [])
+        np.testing.assert_allclose(gpu.score, cpu.score, rtol=1e-6, atol=1e-9)
+    ss = gpu._dev.solver_stats()
+    assert ss["jacobi_solves"] >= 2 and ss["rank1_steps"] > 1000, ss
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("p", [7, 40])
 def test_mahalanobis_device_multirow_tracking_parity(p):
     """Requests of 1-16 rows: each row one rank-1 update of the tracked

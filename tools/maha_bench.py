@@ -55,10 +55,13 @@ def main() -> int:
         for X in warm:
             host.predict(X, [])
         lat_np = seq_latency(lambda X: host.predict(X, []), reqs)
+        print(f"p={p}: numpy done", file=sys.stderr, flush=True)
         dev = C.MahalanobisDevice(p, a.k, 3.0, 50.0, -1.0, 1e-8, 0)
         for X in warm:
             dev.step(X)
+        print(f"p={p}: device warm-up done {dev.solver_stats()}", file=sys.stderr, flush=True)
         lat_dev = seq_latency(dev.step, reqs)
+        print(f"p={p}: device sequential done {dev.solver_stats()}", file=sys.stderr, flush=True)
         # concurrent callers: requests share launches (segments)
         b0 = dev.batches()
         t0 = time.perf_counter()
