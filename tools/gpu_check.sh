@@ -24,6 +24,15 @@ run() {  # name timeout cmd...
 }
 
 rocm-smi --showproductname > "$OUT/rocm_smi.log" 2>&1 || true
+# rocprofv3 traces stay on the box (a full kernel trace is far beyond what
+# gpurun copies back); only the *_stats.csv summaries land in $OUT/<step>/
+keep_stats() {
+  local name=$1
+  mkdir -p "$OUT/$name"
+  find "/tmp/prof_trace/$name" -name '*stats*.csv' -exec cp {} "$OUT/$name/" \; 2>/dev/null
+  rm -rf "/tmp/prof_trace/$name"
+}
+
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
@@ -38,31 +47,36 @@ for s in $STEPS; do
     prof)
       export TMPDIR=/tmp
       export SCA_BENCH_CLEAN_EXIT=1  # bench.py ends with os._exit otherwise: rocprofv3 would write nothing
-      run prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-        python3 bench.py --steps 3 --warmup 1 --step-requests 20000 ;;
+      run prof 400 rocprofv3 --kernel-trace --stats -d /tmp/prof_trace/prof -o run --output-format csv -- \
+        python3 bench.py --steps 3 --warmup 1 --step-requests 20000
+      keep_stats prof ;;
     prof_xgb)
       export TMPDIR=/tmp
       export SCA_BENCH_CLEAN_EXIT=1
-      run prof_xgb 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_xgb" -o run --output-format csv -- \
-        python3 bench.py --model xgb1000 --steps 3 --warmup 1 --step-requests 10000 ;;
+      run prof_xgb 400 rocprofv3 --kernel-trace --stats -d /tmp/prof_trace/prof_xgb -o run --output-format csv -- \
+        python3 bench.py --model xgb1000 --steps 3 --warmup 1 --step-requests 10000
+      keep_stats prof_xgb ;;
     lstm) run lstm 300 python tools/kernel_microbench.py --only lstm --iters 20 ;;
     tree_small) run tree_small 300 python tools/kernel_microbench.py --only tree_small --iters 200 ;;
     prof_abtest)
       export TMPDIR=/tmp
       export SCA_BENCH_CLEAN_EXIT=1
-      run prof_abtest 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_abtest" -o run --output-format csv -- \
-        python3 bench.py --graph abtest --steps 3 --warmup 1 --step-requests 20000 ;;
+      run prof_abtest 400 rocprofv3 --kernel-trace --stats -d /tmp/prof_trace/prof_abtest -o run --output-format csv -- \
+        python3 bench.py --graph abtest --steps 3 --warmup 1 --step-requests 20000
+      keep_stats prof_abtest ;;
     prof_lstm)
       export TMPDIR=/tmp
-      run prof_lstm 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_lstm" -o run --output-format csv -- \
-        python3 tools/kernel_microbench.py --only lstm --iters 10 ;;
+      run prof_lstm 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_trace/prof_lstm -o run --output-format csv -- \
+        python3 tools/kernel_microbench.py --only lstm --iters 10
+      keep_stats prof_lstm ;;
     maha) run maha 300 python tools/maha_bench.py --p 9 20 32 64 --requests 2000 --threads 16 --out "$OUT/maha.json" ;;
     maha_jac) SCA_MAHA_RANK1_MAX_P=0 run maha_jac 300 python tools/maha_bench.py --p 9 20 32 --requests 2000 --threads 16 --out "$OUT/maha_jacobi.json" ;;
     maha_hh) SCA_MAHA_RANK1_MAX_P=0 SCA_MAHA_JACOBI_MAX_P=0 run maha_hh 300 python tools/maha_bench.py --p 9 32 64 --requests 2000 --threads 16 --out "$OUT/maha_householder.json" ;;
     prof_maha)
       export TMPDIR=/tmp
-      run prof_maha 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_maha" -o run --output-format csv -- \
-        python3 tools/maha_bench.py --p 9 64 --requests 1000 --threads 16 ;;
+      run prof_maha 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_trace/prof_maha -o run --output-format csv -- \
+        python3 tools/maha_bench.py --p 9 64 --requests 1000 --threads 16
+      keep_stats prof_maha ;;
     *) echo "unknown step $s" ;;
   esac
 done
