@@ -634,15 +634,16 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
 // recurrence all change by the same k x k rotation), so any orthonormal basis
 // of it gives the reference's scores.
 //
-// Lane r owns row r of B and row r of V^T (the eigenvectors are kept
-// transposed during the sweeps).  A round rotates m/2 disjoint pairs
+// Thread (r, c) owns row r of B and of V^T (the eigenvectors are kept
+// transposed during the sweeps), columns of chunk c = its wave: the whole
+// workgroup (1 or 4 waves) sweeps, 3 barriers per round.  A round rotates m/2 disjoint pairs
 // (round-robin tournament, m = p rounded up to even; pairs with the dummy
 // index p are skipped); every lane needs only ITS pair's (c, s) and partner:
 //   U = R^T B      row mix:          U[r][:]  = a_r B[r][:] + b_r B[pi_r][:]
 //   B' = U R       by symmetry:      B'[r][q] = a_r U[q][r] + b_r U[q][pi_r]
 //                  (column reads of U, conflict-free across the wave)
 //   V'^T = R^T V^T row mix in place (a column's loads precede its stores)
-// Every LDS loop runs in blocks of 8 independent loads.  A pair rotates only
+// A pair rotates only
 // while |b_ij| > tol * sqrt(|b_ii b_jj|) (tol = 1e-14; the rotated element is
 // set to exactly 0): the sweep with no rotation ends the solve.  On exit the eigenpairs are sorted by
 // descending eigenvalue into V (columns; sel = 0..k-1) and cached with their
@@ -651,167 +652,135 @@ constexpr int kJacobiRefresh = 256;   // Jacobi-only mode: cold solve period
 constexpr int kTrackRefresh = 1024;   // eigen-tracking mode: cold solve period
 constexpr int kTrackMaxRows = 16;     // requests with more rows re-solve by Jacobi
 
-__device__ __forceinline__ void jacobi_wave(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W, int* sel, int p,
-                            int k, double* __restrict__ cache, double* __restrict__ tail, double* __restrict__ lamv,
-                            double* __restrict__ lam_cache, int refresh, double* __restrict__ stats) {
-  const int lane = threadIdx.x & 63;
+template <int NT>
+__device__ __forceinline__ void jacobi_solve(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W,
+                                             int* sel, int p, int k, double* __restrict__ cache,
+                                             double* __restrict__ tail, double* __restrict__ lamv,
+                                             double* __restrict__ lam_cache, bool warm, double* __restrict__ stats) {
+  // thread (r, c): row r of B / V^T, column chunk c (= its wave) of width cw
+  constexpr int kWaves = NT / 64;
+  const int tid = threadIdx.x, r = tid & 63, c = tid >> 6;
   const int m = p + (p & 1);
-  const bool row = lane < p;
-  const bool warm = tail[0] == double(p) && tail[1] < double(refresh);
+  const int cw = (p + kWaves - 1) / kWaves;
+  const int q_lo = min(p, c * cw), q_hi = min(p, q_lo + cw);
+  const bool row = r < p;
   if (warm) {
-    for (int e = lane; e < p * p; e += 64) V[(e / p) * kLd + e % p] = cache[e];
-    wave_lds_sync();
-    // T = C V0 -> W (lane r: row r); then B = V0^T T -> A (lane r: row r)
-    if (row) {
-      for (int q0 = 0; q0 < p; q0 += 8) {
-        double acc[8] = {};
-        for (int j = 0; j < p; ++j) {
-          const double a = A[lane * kLdA + j];
-#pragma unroll
-          for (int b = 0; b < 8; ++b) acc[b] += a * V[j * kLd + q0 + b];  // (q0 + b <= 63: in the row)
-        }
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          if (q0 + b < p) W[lane * kLd + q0 + b] = acc[b];
-      }
-    }
-    wave_lds_sync();
-    if (row) {
-      for (int q0 = 0; q0 < p; q0 += 8) {
-        double acc[8] = {};
-        for (int j = 0; j < p; ++j) {
-          const double v = V[j * kLd + lane];
-#pragma unroll
-          for (int b = 0; b < 8; ++b) acc[b] += v * W[j * kLd + q0 + b];
-        }
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          if (q0 + b < p) A[lane * kLdA + q0 + b] = acc[b];
-      }
-    }
-    wave_lds_sync();
-    // V^T = V0^T
+    for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = cache[e];
+    __syncthreads();
+    // T = C V0 -> W, then B = V0^T T -> A (each thread its row's chunk)
     if (row)
-      for (int q = 0; q < p; ++q) V[lane * kLd + q] = cache[q * p + lane];
+      for (int q = q_lo; q < q_hi; ++q) {
+        double t = 0.0;
+        for (int j = 0; j < p; ++j) t += A[r * kLdA + j] * V[j * kLd + q];
+        W[r * kLd + q] = t;
+      }
+    __syncthreads();
+    if (row)
+      for (int q = q_lo; q < q_hi; ++q) {
+        double b = 0.0;
+        for (int j = 0; j < p; ++j) b += V[j * kLd + r] * W[j * kLd + q];
+        A[r * kLdA + q] = b;
+      }
+    __syncthreads();
+    if (row)
+      for (int q = q_lo; q < q_hi; ++q) V[r * kLd + q] = cache[q * p + r];  // V^T = V0^T
   } else if (row) {
-    for (int q = 0; q < p; ++q) V[lane * kLd + q] = lane == q ? 1.0 : 0.0;
+    for (int q = q_lo; q < q_hi; ++q) V[r * kLd + q] = r == q ? 1.0 : 0.0;
   }
-  wave_lds_sync();
+  __syncthreads();
   // symmetric working copy: B[r][q] for q < r taken from the upper triangle
   if (row)
-    for (int q = 0; q < lane; ++q) A[lane * kLdA + q] = A[q * kLdA + lane];
-  wave_lds_sync();
+    for (int q = q_lo; q < min(q_hi, r); ++q) A[r * kLdA + q] = A[q * kLdA + r];
+  __syncthreads();
   constexpr double tol = 1e-14;
+  int sweeps = 40;
   for (int sweep = 0; sweep < 40; ++sweep) {
-    bool rotated = false;
+    int rotated = 0;
     for (int rnd = 0; rnd < m - 1; ++rnd) {
-      // tournament position of player `lane`, and its partner
-      int pr = lane;
-      if (lane < m) {
-        const int pos = lane == 0 ? 0 : ((lane - 1 - rnd) % (m - 1) + (m - 1)) % (m - 1) + 1;
+      // tournament position of player r, and its partner
+      int pr = r;
+      if (r < m) {
+        const int pos = r == 0 ? 0 : ((r - 1 - rnd) % (m - 1) + (m - 1)) % (m - 1) + 1;
         const int opp = m - 1 - pos;
         pr = opp == 0 ? 0 : 1 + (opp - 1 + rnd) % (m - 1);
       }
       double al = 1.0, be = 0.0;
-      int pl = lane;
+      int pl = r;
       if (row && pr < p) {
-        const int i = min(lane, pr), j = max(lane, pr);
+        const int i = min(r, pr), j = max(r, pr);
         const double aii = A[i * kLdA + i], ajj = A[j * kLdA + j], aij = A[i * kLdA + j];
         if (aij != 0.0 && fabs(aij) > tol * sqrt(fabs(aii * ajj))) {
           const double th = (aii - ajj) / (2.0 * aij);
           const double t = -copysign(1.0, th) / (fabs(th) + sqrt(1.0 + th * th));
-          const double c = 1.0 / sqrt(1.0 + t * t), sn = t * c;
-          al = c;
-          be = lane == i ? -sn : sn;
+          const double cs = 1.0 / sqrt(1.0 + t * t), sn = t * cs;
+          al = cs;
+          be = r == i ? -sn : sn;
           pl = pr;
-          rotated = true;
+          rotated = 1;
         }
       }
+      __syncthreads();  // every thread has read this round's B entries
+      if (row)  // U = R^T B -> W (rows)
+        for (int q = q_lo; q < q_hi; ++q) W[r * kLd + q] = al * A[r * kLdA + q] + be * A[pl * kLdA + q];
+      __syncthreads();
       if (row) {
-        // U = R^T B -> W (rows)
-        for (int q0 = 0; q0 < p; q0 += 8) {
+        // B' = U R -> A, through the symmetry: B'[r][q] = a_r U[q][r] + b_r U[q][pi_r];
+        // the annihilated pair exactly 0
+        for (int q = q_lo; q < q_hi; ++q)
+          A[r * kLdA + q] = (q == pl && pl != r) ? 0.0 : al * W[q * kLd + r] + be * W[q * kLd + pl];
+        // V^T <- R^T V^T in place: partner rows share this thread's chunk, so
+        // its wave; each column's loads are issued before its stores
+        for (int q0 = q_lo; q0 < q_hi; q0 += 8) {
           double x[8], y[8];
 #pragma unroll
           for (int b = 0; b < 8; ++b) {
-            x[b] = A[lane * kLdA + q0 + b];  // (A rows carry 8 padding columns)
-            y[b] = A[pl * kLdA + q0 + b];
-          }
-#pragma unroll
-          for (int b = 0; b < 8; ++b)
-            if (q0 + b < p) W[lane * kLd + q0 + b] = al * x[b] + be * y[b];
-        }
-      }
-      wave_lds_sync();
-      if (row) {
-        // B' = U R -> A, through the symmetry: B'[r][q] = a_r U[q][r] + b_r U[q][pi_r]
-        for (int q0 = 0; q0 < p; q0 += 8) {
-          double x[8], y[8];
-#pragma unroll
-          for (int b = 0; b < 8; ++b) {
-            const int q = min(q0 + b, p - 1);
-            x[b] = W[q * kLd + lane];
-            y[b] = W[q * kLd + pl];
-          }
-#pragma unroll
-          for (int b = 0; b < 8; ++b)
-            if (q0 + b < p) A[lane * kLdA + q0 + b] = al * x[b] + be * y[b];
-        }
-        if (pl != lane) A[lane * kLdA + pl] = 0.0;  // the annihilated pair: exactly, not its rounding residue
-        // V^T <- R^T V^T in place: this block's loads (own and partner rows)
-        // are all issued before its stores
-        for (int q0 = 0; q0 < p; q0 += 8) {
-          double x[8], y[8];
-#pragma unroll
-          for (int b = 0; b < 8; ++b) {
-            x[b] = V[lane * kLd + q0 + b];
-            y[b] = V[pl * kLd + q0 + b];
+            const int q = min(q0 + b, q_hi - 1);
+            x[b] = V[r * kLd + q];
+            y[b] = V[pl * kLd + q];
           }
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
           for (int b = 0; b < 8; ++b)
-            if (q0 + b < p) V[lane * kLd + q0 + b] = al * x[b] + be * y[b];
+            if (q0 + b < q_hi) V[r * kLd + q0 + b] = al * x[b] + be * y[b];
         }
       }
-      wave_lds_sync();
+      __syncthreads();
     }
-    if (!__any(rotated)) {
-      if (lane == 0) {  // solver statistics (kMahaEigMeta + 3 / + 4)
-        stats[0] += double(sweep + 1);
-        stats[1] += 1.0;
-      }
+    if (!__syncthreads_or(rotated)) {
+      sweeps = sweep + 1;
       break;
     }
-    if (sweep == 39 && lane == 0) {
-      stats[0] += 40.0;
-      stats[1] += 1.0;
-    }
   }
-  // eigenvalues (the diagonal) in descending order: lane r's rank; the
+  if (tid == 0) {  // solver statistics (kMahaEigMeta + 3 / + 4)
+    stats[0] += double(sweeps);
+    stats[1] += 1.0;
+  }
+  // eigenvalues (the diagonal) in descending order: row r's rank; the
   // eigenvectors (rows of V^T) land sorted in the COLUMNS of V through W
-  const double lam = row ? A[lane * kLdA + lane] : 0.0;
-  if (row) lamv[lane] = lam;
-  wave_lds_sync();
-  int pos = 0;
+  if (row && c == 0) lamv[r] = A[r * kLdA + r];
+  __syncthreads();
   if (row) {
+    const double lam = lamv[r];
+    int pos = 0;
     for (int j = 0; j < p; ++j) {
       const double lj = lamv[j];
-      pos += (lj > lam || (lj == lam && j < lane)) ? 1 : 0;
+      pos += (lj > lam || (lj == lam && j < r)) ? 1 : 0;
     }
-    lam_cache[pos] = lam;
-    for (int r = 0; r < p; ++r) W[r * kLd + pos] = V[lane * kLd + r];
+    if (c == 0) lam_cache[pos] = lam;
+    for (int q = q_lo; q < q_hi; ++q) W[q * kLd + pos] = V[r * kLd + q];
   }
-  if (lane < k) sel[lane] = lane;
-  wave_lds_sync();
-  for (int e = lane; e < p * p; e += 64) {
+  if (tid < k) sel[tid] = tid;
+  __syncthreads();
+  for (int e = tid; e < p * p; e += NT) {
     const double v = W[(e / p) * kLd + e % p];
     V[(e / p) * kLd + e % p] = v;
     cache[e] = v;  // the basis for the next step's warm start / eigen-tracking
   }
-  if (lane == 0) {
+  if (tid == 0) {
     tail[0] = double(p);
     tail[1] = warm ? tail[1] + 1.0 : 0.0;
   }
-  wave_lds_sync();
+  __syncthreads();
 }
 
 // Eigen-tracking update for one row of a request (CoreMahalanobis.py:92-103;
@@ -1282,9 +1251,13 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
         __syncthreads();
       }
     }
-    if (!done && tid < 64)
-      jacobi_wave(A, V, W, sel, p, k, eig, tail, es.dg, eig + kMahaEigLam,
-                  p <= prm.rank1_max_p ? kTrackRefresh : kJacobiRefresh, eig + kMahaEigMeta + 3);
+    if (!done) {
+      // warm or cold: decided by one thread from the cache words (the solve has barriers)
+      if (tid == 0)
+        track = tail[0] == double(p) && tail[1] < double(p <= prm.rank1_max_p ? kTrackRefresh : kJacobiRefresh);
+      __syncthreads();
+      jacobi_solve<NT>(A, V, W, sel, p, k, eig, tail, es.dg, eig + kMahaEigLam, track != 0, eig + kMahaEigMeta + 3);
+    }
   } else if (NT >= 256 && p >= prm.mw_min_p) {
     topk_wave(A, V, W, es, sel, p, k, ph, 4);
   } else if (tid < 64) {

@@ -1,4 +1,4 @@
-// Times the Mahalanobis detector's one-wave Jacobi solver (jacobi_wave) in
+// Times the Mahalanobis detector's Jacobi solver (jacobi_solve<NT>) in
 // isolation: a cold solve of a random covariance, then warm solves after
 // rank-1 updates.  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17
 //   -I csrc/kernels tools/micro/jacobi_probe.hip -o /tmp/jacobi_probe
@@ -10,18 +10,21 @@
 #include <vector>
 
 namespace sca::kern {
-__global__ __launch_bounds__(64) void jac_probe(const double* C, double* eig, int p, int k, int reps,
+template <int NT>
+__global__ __launch_bounds__(NT) void jac_probe(const double* C, double* eig, int p, int k, int reps,
                                                 long long* cycles) {
   __shared__ double A[kMahaMaxP * kLdA], V[kMahaMaxP * kLd], W[kMahaMaxP * kLd];
   __shared__ double lamv[kMahaMaxP];
   __shared__ int sel[kMahaMaxK];
   long long total = 0;
   for (int r = 0; r < reps; ++r) {
-    for (int e = threadIdx.x; e < p * p; e += 64) A[(e / p) * kLdA + e % p] = C[e];
+    for (int e = threadIdx.x; e < p * p; e += NT) A[(e / p) * kLdA + e % p] = C[e];
     __syncthreads();
     const long long t0 = __builtin_amdgcn_s_memrealtime();
-    jacobi_wave(A, V, W, sel, p, k, eig, eig + kMahaEigTail, lamv, eig + kMahaEigLam, 1 << 30,
-                eig + kMahaEigMeta + 3);
+    const bool warm = eig[kMahaEigTail] == double(p);
+    __syncthreads();
+    jacobi_solve<NT>(A, V, W, sel, p, k, eig, eig + kMahaEigTail, lamv, eig + kMahaEigLam, warm,
+                     eig + kMahaEigMeta + 3);
     total += __builtin_amdgcn_s_memrealtime() - t0;
     __syncthreads();
   }
@@ -50,7 +53,10 @@ int main(int argc, char** argv) {
   hipMemset(deig, 0, sca::kern::kMahaEigDoubles * 8);
   for (int pass = 0; pass < 2; ++pass) {  // pass 0: cold (tail empty); pass 1: warm from pass 0's basis
     const int reps = pass == 0 ? 1 : 10;
-    hipLaunchKernelGGL(sca::kern::jac_probe, dim3(1), dim3(64), 0, nullptr, dC, deig, p, 3, reps, dcy);
+    if (p <= 16)
+      hipLaunchKernelGGL(sca::kern::jac_probe<64>, dim3(1), dim3(64), 0, nullptr, dC, deig, p, 3, reps, dcy);
+    else
+      hipLaunchKernelGGL(sca::kern::jac_probe<256>, dim3(1), dim3(256), 0, nullptr, dC, deig, p, 3, reps, dcy);
     hipDeviceSynchronize();
     long long cy;
     std::vector<double> meta(8);
