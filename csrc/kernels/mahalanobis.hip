@@ -808,7 +808,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
                             const double* __restrict__ Cn, double* __restrict__ A, double* __restrict__ V,
                             double* __restrict__ W, EigScratch& es, int* sel, double* __restrict__ cache,
                             double* __restrict__ tail, double* __restrict__ lam_cache, double* red, int* flag,
-                            bool first, bool last) {
+                            bool first, bool last, uint64_t* ph) {
   // first: the basis / eigenvalues come from the cache (else from the
   // previous update of this request: V and lam_new in LDS); last: check the
   // residual against C_new and write the cache
@@ -821,6 +821,17 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   double* inv_norm = es.part[0];
   double* lam_new = es.part[1];
   const double* lam_src = first ? lam_cache : lam_new;
+  // sub-phase timers (thread 0; the Householder path's slots, unused here):
+  // 7 = z = V^T d + deflation checks, 8 = secular roots + zt, 2 = Q + norms,
+  // 9 = V Q + residual + cache
+  uint64_t t_prev = __builtin_amdgcn_s_memrealtime();
+  auto mark = [&](int i) {
+    if (tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      ph[i] += t - t_prev;
+      t_prev = t;
+    }
+  };
   if (first)
     for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = cache[e];
   if (tid == 0) *flag = 1;
@@ -840,6 +851,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     const double tol = 8.0 * __DBL_EPSILON__ * fmax(wave_max(fabs(dl)), rho2);
     wave_lds_sync();
     bool bad = own && (!(rho2 > 0.0) || rho2 * fabs(zh) <= tol || (lane > 0 && dd[lane - 1] - dl <= tol));
+    mark(7);
     if (!__any(bad)) {
       int K = 0;
       double tau = 0.0;
@@ -926,6 +938,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
       }
     }
     if (__any(bad) && lane == 0) *flag = 0;
+    mark(8);
   }
   __syncthreads();
   if (!*flag) return false;
@@ -944,6 +957,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     inv_norm[tid] = rsq_nr(sq);
   }
   __syncthreads();
+  mark(2);
   // V_new = V Q diag(inv_norm) -> A (rows / columns past p of the 4x4
   // blocks read in-bounds LDS garbage and are not stored)
   const int nb4 = (p + 3) >> 2;
@@ -995,6 +1009,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   if (tid < k) sel[tid] = tid;
   if (tid == 0) tail[1] += 1.0;  // steps since the last cold solve (tail[0] = p already)
   __syncthreads();
+  mark(9);
   return true;
 }
 
@@ -1244,7 +1259,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
       for (int i = 0; i < nb && done; ++i)
         done = rank1_eigen<NT>(D + size_t(i) * p, i == 0 ? (n - 1.0) / den : 1.0, ((n + i) / (n + i + 1.0)) / den, p,
                                k, Tm, A, V, W, es, sel, eig, tail, eig + kMahaEigLam, red, &r1flag, i == 0,
-                               i == nb - 1);
+                               i == nb - 1, ph);
       if (tid == 0) eig[kMahaEigMeta + (done ? 1 : 2)] += 1.0;
       if (!done) {  // A held V_new: the new covariance back for the re-solve
         for (int e = tid; e < m * m; e += NT) A[(e / m) * kLdA + e % m] = Tm[(e / m) * kLd + e % m];

@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 200 python -u tools/maha_bench.py --p 9 32 64 --requests 1000 --threads 16 --out gpurun_out/maha_phase.json > gpurun_out/maha_phase.log 2>&1
+rc=$?; tail -4 gpurun_out/maha_phase.log; exit $rc
