@@ -839,8 +839,10 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   if (tid < 64) {
     const bool own = lane < p;
     double z = 0.0;
-    if (own)
+    if (own) {
+#pragma unroll 8
       for (int r = 0; r < p; ++r) z += V[r * kLd + lane] * dvec[r];
+    }
     const double nz2 = wave_sum(z * z);
     const double rho2 = rho * nz2;
     const double zh = nz2 > 0.0 ? z * rsq_nr(nz2) : 0.0;
@@ -861,7 +863,8 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
         if (lane > 0) {
           const double mid = 0.5 * (dl + dd[lane - 1]);
           double f = 0.0;
-          for (int j = 0; j < p; ++j) f += zz[j] / (dd[j] - mid);
+#pragma unroll 8
+          for (int j = 0; j < p; ++j) f += zz[j] * rcp_nr(dd[j] - mid);
           if (1.0 + rho2 * f > 0.0) {  // f increases: the root lies below mid, nearer pole D_i
             K = lane;
             hi = mid - dl;
@@ -873,13 +876,15 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
         }
         const double dK = dd[K];
         double r0 = 0.0;
+#pragma unroll 8
         for (int j = 0; j < p; ++j)
-          if (j != K) r0 += zz[j] / (dd[j] - dK);
+          if (j != K) r0 += zz[j] * rcp_nr(dd[j] - dK);
         const double t0 = rho2 * zz[K] / (1.0 + rho2 * r0);
         tau = (t0 > lo && t0 < hi) ? t0 : 0.5 * (lo + hi);
         const double Dp = lane > 0 ? dd[lane - 1] - dK : 0.0;
         for (int it = 0; it < 48 && !conv; ++it) {
           double psi = 0.0, dpsi = 0.0, phi = 0.0, dphi = 0.0;
+#pragma unroll 8
           for (int j = 0; j < p; ++j) {
             const double r = rcp_nr((dd[j] - dK) - tau);
             const double t = zz[j] * r;
@@ -931,8 +936,9 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
       if (!__any(bad) && own) {
         // zt_j^2 = prod_k (lam_k - D_j) / prod_{k != j} (D_k - D_j) / rho'
         double prod = ((dd[Ks[lane]] - dl) + taus[lane]) / rho2;
+#pragma unroll 8
         for (int q = 0; q < p; ++q)
-          if (q != lane) prod *= ((dd[Ks[q]] - dl) + taus[q]) / (dd[q] - dl);
+          if (q != lane) prod *= ((dd[Ks[q]] - dl) + taus[q]) * rcp_nr(dd[q] - dl);
         bad = !(prod > 0.0) || !isfinite(prod);
         zt[lane] = copysign(sqrt(fmax(prod, 0.0)), zh);
       }
@@ -950,6 +956,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   __syncthreads();
   if (tid < p) {
     double sq = 0.0;
+#pragma unroll 8
     for (int j = 0; j < p; ++j) {
       const double q = W[j * kLd + tid];
       sq += q * q;
@@ -964,6 +971,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   for (int e = tid; e < nb4 * nb4; e += NT) {
     const int r0 = (e / nb4) * 4, c0 = (e - (e / nb4) * nb4) * 4;
     double acc[4][4] = {};
+#pragma unroll 2
     for (int q = 0; q < p; ++q) {
       double v[4], w[4];
 #pragma unroll
@@ -992,6 +1000,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   for (int e = tid; e < p * k; e += NT) {
     const int r = e / k, c = e - r * k;
     double sacc = 0.0;
+#pragma unroll 8
     for (int j = 0; j < p; ++j) sacc += Cn[r * kLd + j] * A[j * kLdA + c];
     const double d = sacc - lam_new[c] * A[r * kLdA + c];
     res += d * d;
