@@ -909,18 +909,21 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
             break;
           }
           // psi ~ P / (Q - t) (poles at and below the interval), phi ~ R + S / (Dp - t)
-          const double qm = tau + psi / dpsi, pp = psi * psi / dpsi;
+          // (the model only proposes the next iterate -- the bracket and the
+          // test on f above decide convergence -- so Newton reciprocals do)
+          const double idp = rcp_nr(dpsi);
+          const double qm = tau + psi * idp, pp = psi * psi * idp;
           double nt = 0.5 * (lo + hi);
           if (lane == 0) {
             nt = qm + pp;
           } else {
             const double dt = Dp - tau;
-            const double S = dphi * dt * dt, R = phi - S / dt;
+            const double S = dphi * dt * dt, R = phi - S * rcp_nr(dt);
             const double a = 1.0 + R, b = -(a * (qm + Dp) + pp + S), c = a * qm * Dp + pp * Dp + S * qm;
             const double disc = b * b - 4.0 * a * c;
-            if (a != 0.0 && disc >= 0.0) {
-              const double r1 = (-b - copysign(sqrt(disc), b)) / (2.0 * a);
-              const double r2 = r1 != 0.0 ? c / (a * r1) : r1;
+            if (a != 0.0 && disc > 0.0) {
+              const double r1 = (-b - copysign(disc * rsq_nr(disc), b)) * rcp_nr(2.0 * a);
+              const double r2 = r1 != 0.0 ? c * rcp_nr(a * r1) : r1;
               if (r1 > lo && r1 < hi) nt = r1;
               else if (r2 > lo && r2 < hi) nt = r2;
             }
