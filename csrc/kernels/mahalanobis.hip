@@ -836,6 +836,8 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = cache[e];
   if (tid == 0) *flag = 1;
   __syncthreads();
+  double* rsc = es.part[2];  // [0] = rho' (z's squared norm folded in)
+  double zh = 0.0, dl = 0.0;  // (wave 0, lane j: zh_j, D_j)
   if (tid < 64) {
     const bool own = lane < p;
     double z = 0.0;
@@ -845,99 +847,142 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     }
     const double nz2 = wave_sum(z * z);
     const double rho2 = rho * nz2;
-    const double zh = nz2 > 0.0 ? z * rsq_nr(nz2) : 0.0;
-    const double dl = own ? alpha * lam_src[lane] : 0.0;
+    zh = nz2 > 0.0 ? z * rsq_nr(nz2) : 0.0;
+    dl = own ? alpha * lam_src[lane] : 0.0;
     wave_lds_sync();  // (lam_src may be lam_new, rewritten below)
     dd[lane] = dl;
     zz[lane] = zh * zh;
+    if (lane == 0) rsc[0] = rho2;
     const double tol = 8.0 * __DBL_EPSILON__ * fmax(wave_max(fabs(dl)), rho2);
     wave_lds_sync();
-    bool bad = own && (!(rho2 > 0.0) || rho2 * fabs(zh) <= tol || (lane > 0 && dd[lane - 1] - dl <= tol));
-    mark(7);
-    if (!__any(bad)) {
-      int K = 0;
-      double tau = 0.0;
-      bool conv = !own;
-      if (own) {
-        double lo = 0.0, hi = rho2;
-        if (lane > 0) {
-          const double mid = 0.5 * (dl + dd[lane - 1]);
-          double f = 0.0;
-#pragma unroll 8
-          for (int j = 0; j < p; ++j) f += zz[j] * rcp_nr(dd[j] - mid);
-          if (1.0 + rho2 * f > 0.0) {  // f increases: the root lies below mid, nearer pole D_i
-            K = lane;
-            hi = mid - dl;
-          } else {
-            K = lane - 1;
-            lo = mid - dd[lane - 1];
-            hi = 0.0;
-          }
+    const bool bad = own && (!(rho2 > 0.0) || rho2 * fabs(zh) <= tol || (lane > 0 && dd[lane - 1] - dl <= tol));
+    if (__any(bad) && lane == 0) *flag = 0;
+  }
+  __syncthreads();
+  mark(7);
+  if (!*flag) return false;
+  // ---- secular roots: 4 threads per root, each summing every 4th term.
+  // 64-thread kernel (p <= 16): lanes 4i..4i+3 (shuffle sums); 256-thread
+  // kernel: thread i of each wave (partials through LDS, W is free here).
+  // All 4 hold identical sums (fixed combine order), hence identical iterates.
+  constexpr int kSub = 4;
+  const int root = NT == 64 ? lane >> 2 : lane;
+  const int sub = NT == 64 ? lane & 3 : tid >> 6;
+  const bool own = root < p;
+  const double rho2 = rsc[0];
+  auto combine = [&](double (&v)[4], int nq) {
+    if constexpr (NT == 64) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < nq) {
+          v[q] += __shfl_xor(v[q], 1, 64);
+          v[q] += __shfl_xor(v[q], 2, 64);
         }
-        const double dK = dd[K];
-        double r0 = 0.0;
-#pragma unroll 8
-        for (int j = 0; j < p; ++j)
-          if (j != K) r0 += zz[j] * rcp_nr(dd[j] - dK);
-        const double t0 = rho2 * zz[K] / (1.0 + rho2 * r0);
-        tau = (t0 > lo && t0 < hi) ? t0 : 0.5 * (lo + hi);
-        const double Dp = lane > 0 ? dd[lane - 1] - dK : 0.0;
-        for (int it = 0; it < 48 && !conv; ++it) {
-          double psi = 0.0, dpsi = 0.0, phi = 0.0, dphi = 0.0;
-#pragma unroll 8
-          for (int j = 0; j < p; ++j) {
-            const double r = rcp_nr((dd[j] - dK) - tau);
-            const double t = zz[j] * r;
-            if (j >= lane) {
-              psi += t;
-              dpsi += t * r;
-            } else {
-              phi += t;
-              dphi += t * r;
-            }
-          }
-          psi *= rho2;
-          dpsi *= rho2;
-          phi *= rho2;
-          dphi *= rho2;
-          const double f = 1.0 + psi + phi;
-          if (f < 0.0) lo = tau;
-          else hi = tau;
-          if (fabs(f) <= 32.0 * __DBL_EPSILON__ * (1.0 + fabs(psi) + fabs(phi)) ||
-              hi - lo <= 4.0 * __DBL_EPSILON__ * fmax(fabs(lo), fabs(hi))) {
-            conv = true;
-            break;
-          }
-          // psi ~ P / (Q - t) (poles at and below the interval), phi ~ R + S / (Dp - t)
-          // (the model only proposes the next iterate -- the bracket and the
-          // test on f above decide convergence -- so Newton reciprocals do)
-          const double idp = rcp_nr(dpsi);
-          const double qm = tau + psi * idp, pp = psi * psi * idp;
-          double nt = 0.5 * (lo + hi);
-          if (lane == 0) {
-            nt = qm + pp;
-          } else {
-            const double dt = Dp - tau;
-            const double S = dphi * dt * dt, R = phi - S * rcp_nr(dt);
-            const double a = 1.0 + R, b = -(a * (qm + Dp) + pp + S), c = a * qm * Dp + pp * Dp + S * qm;
-            const double disc = b * b - 4.0 * a * c;
-            if (a != 0.0 && disc > 0.0) {
-              const double r1 = (-b - copysign(disc * rsq_nr(disc), b)) * rcp_nr(2.0 * a);
-              const double r2 = r1 != 0.0 ? c * rcp_nr(a * r1) : r1;
-              if (r1 > lo && r1 < hi) nt = r1;
-              else if (r2 > lo && r2 < hi) nt = r2;
-            }
-          }
-          tau = (nt > lo && nt < hi) ? nt : 0.5 * (lo + hi);
-        }
-        Ks[lane] = K;
-        taus[lane] = tau;
-        lam_new[lane] = dK + tau;
+    } else {
+      for (int q = 0; q < nq; ++q) W[(sub * 4 + q) * 64 + lane] = v[q];
+      __syncthreads();
+      for (int q = 0; q < nq; ++q)
+        v[q] = (W[(0 * 4 + q) * 64 + lane] + W[(1 * 4 + q) * 64 + lane]) +
+               (W[(2 * 4 + q) * 64 + lane] + W[(3 * 4 + q) * 64 + lane]);
+      __syncthreads();
+    }
+  };
+  int K = 0;
+  double tau = 0.0, lo = 0.0, hi = rho2, dK = 0.0, Dp = 0.0;
+  bool conv = !own;
+  {
+    // which pole is nearer: the sign of f at the interval's midpoint
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    const double dr = own ? dd[root] : 0.0;
+    const double mid = root > 0 && own ? 0.5 * (dr + dd[root - 1]) : 0.0;
+    if (own && root > 0)
+#pragma unroll 4
+      for (int j = sub; j < p; j += kSub) v[0] += zz[j] * rcp_nr(dd[j] - mid);
+    combine(v, 1);
+    if (own && root > 0) {
+      if (1.0 + rho2 * v[0] > 0.0) {  // f increases: the root lies below mid, nearer pole D_i
+        K = root;
+        hi = mid - dr;
+      } else {
+        K = root - 1;
+        lo = mid - dd[root - 1];
+        hi = 0.0;
       }
-      bad = !conv;
-      wave_lds_sync();
-      if (!__any(bad) && own) {
-        // zt_j^2 = prod_k (lam_k - D_j) / prod_{k != j} (D_k - D_j) / rho'
+    }
+    dK = own ? dd[K] : 0.0;
+    Dp = own && root > 0 ? dd[root - 1] - dK : 0.0;
+    // start from the one-pole estimate
+    v[0] = 0.0;
+    if (own)
+#pragma unroll 4
+      for (int j = sub; j < p; j += kSub)
+        if (j != K) v[0] += zz[j] * rcp_nr(dd[j] - dK);
+    combine(v, 1);
+    if (own) {
+      const double t0 = rho2 * zz[K] / (1.0 + rho2 * v[0]);
+      tau = (t0 > lo && t0 < hi) ? t0 : 0.5 * (lo + hi);
+    }
+  }
+  for (int it = 0; it < 48; ++it) {
+    double v[4] = {0.0, 0.0, 0.0, 0.0};  // psi, psi', phi, phi'
+    if (own && !conv)
+#pragma unroll 4
+      for (int j = sub; j < p; j += kSub) {
+        const double r = rcp_nr((dd[j] - dK) - tau);
+        const double t = zz[j] * r;
+        if (j >= root) {
+          v[0] += t;
+          v[1] += t * r;
+        } else {
+          v[2] += t;
+          v[3] += t * r;
+        }
+      }
+    combine(v, 4);
+    if (own && !conv) {
+      const double psi = rho2 * v[0], dpsi = rho2 * v[1], phi = rho2 * v[2], dphi = rho2 * v[3];
+      const double f = 1.0 + psi + phi;
+      if (f < 0.0) lo = tau;
+      else hi = tau;
+      if (fabs(f) <= 32.0 * __DBL_EPSILON__ * (1.0 + fabs(psi) + fabs(phi)) ||
+          hi - lo <= 4.0 * __DBL_EPSILON__ * fmax(fabs(lo), fabs(hi))) {
+        conv = true;
+      } else {
+        // psi ~ P / (Q - t) (poles at and below the interval), phi ~ R + S / (Dp - t)
+        // (the model only proposes the next iterate -- the bracket and the
+        // test on f above decide convergence -- so Newton reciprocals do)
+        const double idp = rcp_nr(dpsi);
+        const double qm = tau + psi * idp, pp = psi * psi * idp;
+        double nt = 0.5 * (lo + hi);
+        if (root == 0) {
+          nt = qm + pp;
+        } else {
+          const double dt = Dp - tau;
+          const double S = dphi * dt * dt, R = phi - S * rcp_nr(dt);
+          const double a = 1.0 + R, b = -(a * (qm + Dp) + pp + S), c = a * qm * Dp + pp * Dp + S * qm;
+          const double disc = b * b - 4.0 * a * c;
+          if (a != 0.0 && disc > 0.0) {
+            const double r1 = (-b - copysign(disc * rsq_nr(disc), b)) * rcp_nr(2.0 * a);
+            const double r2 = r1 != 0.0 ? c * rcp_nr(a * r1) : r1;
+            if (r1 > lo && r1 < hi) nt = r1;
+            else if (r2 > lo && r2 < hi) nt = r2;
+          }
+        }
+        tau = (nt > lo && nt < hi) ? nt : 0.5 * (lo + hi);
+      }
+    }
+    if (!__syncthreads_or(!conv)) break;
+  }
+  if (own && sub == 0) {
+    Ks[root] = K;
+    taus[root] = tau;
+    lam_new[root] = dK + tau;
+  }
+  if (!__syncthreads_or(!conv)) {
+    // zt_j^2 = prod_k (lam_k - D_j) / prod_{k != j} (D_k - D_j) / rho'  (wave 0, lane j)
+    if (tid < 64) {
+      bool bad = false;
+      if (lane < p) {
         double prod = ((dd[Ks[lane]] - dl) + taus[lane]) / rho2;
 #pragma unroll 8
         for (int q = 0; q < p; ++q)
@@ -945,11 +990,13 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
         bad = !(prod > 0.0) || !isfinite(prod);
         zt[lane] = copysign(sqrt(fmax(prod, 0.0)), zh);
       }
+      if (__any(bad) && lane == 0) *flag = 0;
     }
-    if (__any(bad) && lane == 0) *flag = 0;
-    mark(8);
+  } else if (tid == 0) {
+    *flag = 0;  // a root did not converge
   }
   __syncthreads();
+  mark(8);
   if (!*flag) return false;
   // Q (columns unnormalised) -> W: Q[j][i] = zt_j / (D_j - lam_i)
   for (int e = tid; e < p * p; e += NT) {
