@@ -810,20 +810,26 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
                             double* __restrict__ tail, double* __restrict__ lam_cache, double* red, int* flag,
                             bool first, bool last, uint64_t* ph) {
   // first: the basis / eigenvalues come from the cache (else from the
-  // previous update of this request: V and lam_new in LDS); last: check the
-  // residual against C_new and write the cache
+  // previous update of this request: V and lam_sorted in LDS); last: check
+  // the residual against C_new and write the cache
   const int tid = threadIdx.x, lane = tid & 63;
-  double* dd = es.dg;    // D = alpha lam
-  double* zz = es.eo;    // zh^2
-  double* taus = es.sd;  // root offsets from their pole
-  double* zt = es.se2;   // Gu-Eisenstat z
-  int* Ks = reinterpret_cast<int*>(es.rn);  // root poles
-  double* inv_norm = es.part[0];
-  double* lam_new = es.part[1];
-  const double* lam_src = first ? lam_cache : lam_new;
+  double* dd = es.dg;                                      // [orig] D = alpha lam
+  double* zhp = es.eo;                                     // [orig] z / |z| after the cluster reflections
+  double* uvec = reinterpret_cast<double*>(es.rv);         // [orig] cluster reflector
+  double* ztA = reinterpret_cast<double*>(es.rv) + 72;     // [active] Gu-Eisenstat z
+  double* ddA = es.sd;                                     // [active] D of the secular problem
+  double* zzA = es.se2;                                    // [active] zh^2
+  double* taus = es.part[0];                               // [active] root offsets from their pole
+  double* lam_sorted = es.part[1];                         // [sorted] eigenvalues (also inv_norm [active] before)
+  double* inv_norm = es.part[1];
+  double* vals = es.part[2];                               // [entry] eigenvalue of entry e (active roots, then the rest)
+  int* Ks = reinterpret_cast<int*>(es.rn);                 // [active] root poles; later [entry] sorted position
+  int* perm = reinterpret_cast<int*>(es.rn) + 64;          // [entry] original index (active first)
+  int* npc = reinterpret_cast<int*>(es.rn) + 128;          // [0] active count
+  double* rsc = es.lam;                                    // [0] rho'
+  const double* lam_src = first ? lam_cache : lam_sorted;
   // sub-phase timers (thread 0; the Householder path's slots, unused here):
-  // 7 = z = V^T d + deflation checks, 8 = secular roots + zt, 2 = Q + norms,
-  // 9 = V Q + residual + cache
+  // 7 = z, deflation, 8 = secular roots + zt, 2 = Q + norms, 9 = V Q + sort + residual + cache
   uint64_t t_prev = __builtin_amdgcn_s_memrealtime();
   auto mark = [&](int i) {
     if (tid == 0) {
@@ -836,8 +842,11 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = cache[e];
   if (tid == 0) *flag = 1;
   __syncthreads();
-  double* rsc = es.part[2];  // [0] = rho' (z's squared norm folded in)
-  double zh = 0.0, dl = 0.0;  // (wave 0, lane j: zh_j, D_j)
+  // ---- z = V^T d; deflation (wave 0, lane j = index j): clusters of
+  // eigenvalues closer than tol get one reflection within their columns of V
+  // that puts all of the cluster's z on its first index (any basis of a
+  // double eigenvalue's space is an eigenbasis); then every index with a
+  // negligible z keeps its eigenpair, the rest form the secular problem
   if (tid < 64) {
     const bool own = lane < p;
     double z = 0.0;
@@ -847,29 +856,72 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     }
     const double nz2 = wave_sum(z * z);
     const double rho2 = rho * nz2;
-    zh = nz2 > 0.0 ? z * rsq_nr(nz2) : 0.0;
-    dl = own ? alpha * lam_src[lane] : 0.0;
-    wave_lds_sync();  // (lam_src may be lam_new, rewritten below)
+    double zh = nz2 > 0.0 ? z * rsq_nr(nz2) : 0.0;
+    const double dl = own ? alpha * lam_src[lane] : 0.0;
+    wave_lds_sync();  // (lam_src may be lam_sorted: every lane has read it)
     dd[lane] = dl;
-    zz[lane] = zh * zh;
-    if (lane == 0) rsc[0] = rho2;
     const double tol = 8.0 * __DBL_EPSILON__ * fmax(wave_max(fabs(dl)), rho2);
+    if (lane == 0) rsc[0] = rho2;
     wave_lds_sync();
-    const bool bad = own && (!(rho2 > 0.0) || rho2 * fabs(zh) <= tol || (lane > 0 && dd[lane - 1] - dl <= tol));
-    if (__any(bad) && lane == 0) *flag = 0;
+    // cluster heads: a gap above tol to the previous eigenvalue
+    const unsigned long long heads = __ballot(own && (lane == 0 || dd[lane - 1] - dl > tol));
+    zhp[lane] = zh;
+    wave_lds_sync();
+    for (int s0 = 0; s0 < p;) {
+      const unsigned long long rest = (s0 + 1 < 64) ? heads >> (s0 + 1) : 0ull;
+      const int e0 = rest ? min(p, s0 + 1 + int(__builtin_ctzll(rest))) : p;
+      if (e0 - s0 > 1) {
+        double nrm2 = 0.0;
+        for (int c = s0; c < e0; ++c) nrm2 += zhp[c] * zhp[c];
+        if (nrm2 > 0.0) {
+          const double nrm = nrm2 * rsq_nr(nrm2), z0 = zhp[s0];
+          const double sg = z0 >= 0.0 ? 1.0 : -1.0;
+          const double beta = 1.0 / (nrm * (nrm + fabs(z0)));
+          if (lane >= s0 && lane < e0) uvec[lane] = lane == s0 ? z0 + sg * nrm : zhp[lane];
+          wave_lds_sync();
+          if (own) {  // V[r][cluster] <- V[r][cluster] (I - beta u u^T)
+            double t = 0.0;
+            for (int c = s0; c < e0; ++c) t += V[lane * kLd + c] * uvec[c];
+            t *= beta;
+            for (int c = s0; c < e0; ++c) V[lane * kLd + c] -= t * uvec[c];
+          }
+          if (lane >= s0 && lane < e0) zhp[lane] = lane == s0 ? -sg * nrm : 0.0;
+          wave_lds_sync();
+        }
+      }
+      s0 = e0;
+    }
+    zh = zhp[lane];
+    // active set: compaction by ballot (active indices first, in order)
+    const bool act = own && rho2 > 0.0 && rho2 * fabs(zh) > tol;
+    const unsigned long long am = __ballot(act), im = __ballot(own && !act);
+    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int pc = __popcll(am);
+    if (act) {
+      const int a = __popcll(am & below);
+      perm[a] = lane;
+      ddA[a] = dl;
+      zzA[a] = zh * zh;
+    } else if (own) {
+      const int e = pc + __popcll(im & below);
+      perm[e] = lane;
+      vals[e] = dl;  // a kept eigenvalue
+    }
+    if (lane == 0) *npc = pc;
   }
   __syncthreads();
   mark(7);
-  if (!*flag) return false;
-  // ---- secular roots: 4 threads per root, each summing every 4th term.
-  // 64-thread kernel (p <= 16): lanes 4i..4i+3 (shuffle sums); 256-thread
-  // kernel: thread i of each wave (partials through LDS, W is free here).
-  // All 4 hold identical sums (fixed combine order), hence identical iterates.
+  const int pc = *npc;
+  const double rho2 = rsc[0];
+  // ---- secular roots of the active set: 4 threads per root, each summing
+  // every 4th term.  64-thread kernel (p <= 16): lanes 4i..4i+3 (shuffle
+  // sums); 256-thread kernel: thread i of each wave (partials through LDS, W
+  // is free here).  All 4 hold identical sums (fixed combine order), hence
+  // identical iterates.
   constexpr int kSub = 4;
   const int root = NT == 64 ? lane >> 2 : lane;
   const int sub = NT == 64 ? lane & 3 : tid >> 6;
-  const bool own = root < p;
-  const double rho2 = rsc[0];
+  const bool own = root < pc;
   auto combine = [&](double (&v)[4], int nq) {
     if constexpr (NT == 64) {
 #pragma unroll
@@ -893,11 +945,11 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   {
     // which pole is nearer: the sign of f at the interval's midpoint
     double v[4] = {0.0, 0.0, 0.0, 0.0};
-    const double dr = own ? dd[root] : 0.0;
-    const double mid = root > 0 && own ? 0.5 * (dr + dd[root - 1]) : 0.0;
+    const double dr = own ? ddA[root] : 0.0;
+    const double mid = root > 0 && own ? 0.5 * (dr + ddA[root - 1]) : 0.0;
     if (own && root > 0)
 #pragma unroll 4
-      for (int j = sub; j < p; j += kSub) v[0] += zz[j] * rcp_nr(dd[j] - mid);
+      for (int j = sub; j < pc; j += kSub) v[0] += zzA[j] * rcp_nr(ddA[j] - mid);
     combine(v, 1);
     if (own && root > 0) {
       if (1.0 + rho2 * v[0] > 0.0) {  // f increases: the root lies below mid, nearer pole D_i
@@ -905,21 +957,21 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
         hi = mid - dr;
       } else {
         K = root - 1;
-        lo = mid - dd[root - 1];
+        lo = mid - ddA[root - 1];
         hi = 0.0;
       }
     }
-    dK = own ? dd[K] : 0.0;
-    Dp = own && root > 0 ? dd[root - 1] - dK : 0.0;
+    dK = own ? ddA[K] : 0.0;
+    Dp = own && root > 0 ? ddA[root - 1] - dK : 0.0;
     // start from the one-pole estimate
     v[0] = 0.0;
     if (own)
 #pragma unroll 4
-      for (int j = sub; j < p; j += kSub)
-        if (j != K) v[0] += zz[j] * rcp_nr(dd[j] - dK);
+      for (int j = sub; j < pc; j += kSub)
+        if (j != K) v[0] += zzA[j] * rcp_nr(ddA[j] - dK);
     combine(v, 1);
     if (own) {
-      const double t0 = rho2 * zz[K] / (1.0 + rho2 * v[0]);
+      const double t0 = rho2 * zzA[K] / (1.0 + rho2 * v[0]);
       tau = (t0 > lo && t0 < hi) ? t0 : 0.5 * (lo + hi);
     }
   }
@@ -927,9 +979,9 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     double v[4] = {0.0, 0.0, 0.0, 0.0};  // psi, psi', phi, phi'
     if (own && !conv)
 #pragma unroll 4
-      for (int j = sub; j < p; j += kSub) {
-        const double r = rcp_nr((dd[j] - dK) - tau);
-        const double t = zz[j] * r;
+      for (int j = sub; j < pc; j += kSub) {
+        const double r = rcp_nr((ddA[j] - dK) - tau);
+        const double t = zzA[j] * r;
         if (j >= root) {
           v[0] += t;
           v[1] += t * r;
@@ -976,19 +1028,20 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   if (own && sub == 0) {
     Ks[root] = K;
     taus[root] = tau;
-    lam_new[root] = dK + tau;
+    vals[root] = dK + tau;
   }
   if (!__syncthreads_or(!conv)) {
-    // zt_j^2 = prod_k (lam_k - D_j) / prod_{k != j} (D_k - D_j) / rho'  (wave 0, lane j)
+    // zt_a^2 = prod_k (lam_k - D_a) / prod_{k != a} (D_k - D_a) / rho'  (wave 0, lane a)
     if (tid < 64) {
       bool bad = false;
-      if (lane < p) {
-        double prod = ((dd[Ks[lane]] - dl) + taus[lane]) / rho2;
+      if (lane < pc) {
+        const double da = ddA[lane];
+        double prod = ((ddA[Ks[lane]] - da) + taus[lane]) / rho2;
 #pragma unroll 8
-        for (int q = 0; q < p; ++q)
-          if (q != lane) prod *= ((dd[Ks[q]] - dl) + taus[q]) * rcp_nr(dd[q] - dl);
+        for (int q = 0; q < pc; ++q)
+          if (q != lane) prod *= ((ddA[Ks[q]] - da) + taus[q]) * rcp_nr(ddA[q] - da);
         bad = !(prod > 0.0) || !isfinite(prod);
-        zt[lane] = copysign(sqrt(fmax(prod, 0.0)), zh);
+        ztA[lane] = copysign(sqrt(fmax(prod, 0.0)), zhp[perm[lane]]);
       }
       if (__any(bad) && lane == 0) *flag = 0;
     }
@@ -998,34 +1051,36 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   __syncthreads();
   mark(8);
   if (!*flag) return false;
-  // Q (columns unnormalised) -> W: Q[j][i] = zt_j / (D_j - lam_i)
-  for (int e = tid; e < p * p; e += NT) {
-    const int j = e / p, i = e - j * p;
-    W[j * kLd + i] = zt[j] / ((dd[j] - dd[Ks[i]]) - taus[i]);
+  // ---- Q (active block, columns unnormalised) -> W: Q[a][b] = zt_a / (D_a - lam_b)
+  for (int e = tid; e < pc * pc; e += NT) {
+    const int a = e / pc, b = e - a * pc;
+    W[a * kLd + b] = ztA[a] / ((ddA[a] - ddA[Ks[b]]) - taus[b]);
   }
   __syncthreads();
-  if (tid < p) {
+  if (tid < pc) {
     double sq = 0.0;
 #pragma unroll 8
-    for (int j = 0; j < p; ++j) {
-      const double q = W[j * kLd + tid];
+    for (int a = 0; a < pc; ++a) {
+      const double q = W[a * kLd + tid];
       sq += q * q;
     }
     inv_norm[tid] = rsq_nr(sq);
   }
   __syncthreads();
   mark(2);
-  // V_new = V Q diag(inv_norm) -> A (rows / columns past p of the 4x4
-  // blocks read in-bounds LDS garbage and are not stored)
-  const int nb4 = (p + 3) >> 2;
-  for (int e = tid; e < nb4 * nb4; e += NT) {
-    const int r0 = (e / nb4) * 4, c0 = (e - (e / nb4) * nb4) * 4;
+  // ---- entries -> A's columns: e < pc the new vectors V[:, act] Q[:, e]
+  // (4x4 register blocks; rows / columns past the ends read in-bounds LDS
+  // garbage and are not stored), e >= pc the kept columns of V
+  const int nr4 = (p + 3) >> 2, nc4 = (pc + 3) >> 2;
+  for (int e = tid; e < nr4 * nc4; e += NT) {
+    const int r0 = (e / nc4) * 4, c0 = (e - (e / nc4) * nc4) * 4;
     double acc[4][4] = {};
 #pragma unroll 2
-    for (int q = 0; q < p; ++q) {
+    for (int q = 0; q < pc; ++q) {
+      const int src = perm[q];
       double v[4], w[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) v[a] = V[(r0 + a) * kLd + q];
+      for (int a = 0; a < 4; ++a) v[a] = V[(r0 + a) * kLd + src];
 #pragma unroll
       for (int b = 0; b < 4; ++b) w[b] = W[q * kLd + c0 + b];
 #pragma unroll
@@ -1037,34 +1092,48 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b)
-        if (r0 + a < p && c0 + b < p) A[(r0 + a) * kLdA + c0 + b] = acc[a][b] * inv_norm[c0 + b];
+        if (r0 + a < p && c0 + b < pc) A[(r0 + a) * kLdA + c0 + b] = acc[a][b] * inv_norm[c0 + b];
+  }
+  for (int e = tid; e < p * (p - pc); e += NT) {
+    const int r = e / (p - pc), c = pc + (e - r * (p - pc));
+    A[r * kLdA + c] = V[r * kLd + perm[c]];
   }
   __syncthreads();
-  if (!last) {  // the next row's update starts from this basis
-    for (int e = tid; e < p * p; e += NT) V[(e / p) * kLd + e % p] = A[(e / p) * kLdA + e % p];
-    __syncthreads();
-    return true;
+  // ---- descending order: entry e's rank (ties by entry), eigenvalues and
+  // vectors land sorted (Ks is free again: it holds the ranks)
+  int* rank_of = Ks;
+  if (tid < p) {
+    const double ve = vals[tid];
+    int pos = 0;
+    for (int j = 0; j < p; ++j) {
+      const double vj = vals[j];
+      pos += (vj > ve || (vj == ve && j < tid)) ? 1 : 0;
+    }
+    rank_of[tid] = pos;
   }
-  // residual of the top-k pairs against the new covariance
+  __syncthreads();
+  if (tid < p) lam_sorted[rank_of[tid]] = vals[tid];  // (inv_norm is done with)
+  for (int e = tid; e < p * p; e += NT) {
+    const int r = e / p, c = e - r * p;
+    V[r * kLd + rank_of[c]] = A[r * kLdA + c];
+  }
+  __syncthreads();
+  if (!last) return true;  // the next row's update starts from this basis
+  // ---- residual of the top-k pairs against the new covariance
   double res = 0.0;
   for (int e = tid; e < p * k; e += NT) {
     const int r = e / k, c = e - r * k;
     double sacc = 0.0;
 #pragma unroll 8
-    for (int j = 0; j < p; ++j) sacc += Cn[r * kLd + j] * A[j * kLdA + c];
-    const double d = sacc - lam_new[c] * A[r * kLdA + c];
+    for (int j = 0; j < p; ++j) sacc += Cn[r * kLd + j] * V[j * kLd + c];
+    const double d = sacc - lam_sorted[c] * V[r * kLd + c];
     res += d * d;
   }
   res = block_sum<NT>(res, red);
-  const double lim = 1e-11 * fabs(lam_new[0]);
+  const double lim = 1e-11 * fabs(lam_sorted[0]);
   if (!(res <= lim * lim)) return false;  // (uniform: every thread holds the block sum)
-  for (int e = tid; e < p * p; e += NT) {
-    const int r = e / p, c = e - r * p;
-    const double v = A[r * kLdA + c];
-    V[r * kLd + c] = v;
-    cache[e] = v;
-  }
-  if (tid < p) lam_cache[tid] = lam_new[tid];
+  for (int e = tid; e < p * p; e += NT) cache[e] = V[(e / p) * kLd + e % p];
+  if (tid < p) lam_cache[tid] = lam_sorted[tid];
   if (tid < k) sel[tid] = tid;
   if (tid == 0) tail[1] += 1.0;  // steps since the last cold solve (tail[0] = p already)
   __syncthreads();
