@@ -1099,17 +1099,26 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     A[r * kLdA + c] = V[r * kLd + perm[c]];
   }
   __syncthreads();
-  // ---- descending order: entry e's rank (ties by entry), eigenvalues and
-  // vectors land sorted (Ks is free again: it holds the ranks)
+  // ---- descending order: the active roots (entries < pc) and the kept
+  // eigenvalues (entries >= pc) are each already descending, so an entry's
+  // rank is its place in its own list plus a binary search in the other
+  // (ties: active first); eigenvalues and vectors land sorted (Ks is free
+  // again: it holds the ranks)
   int* rank_of = Ks;
   if (tid < p) {
     const double ve = vals[tid];
-    int pos = 0;
-    for (int j = 0; j < p; ++j) {
-      const double vj = vals[j];
-      pos += (vj > ve || (vj == ve && j < tid)) ? 1 : 0;
+    const bool is_act = tid < pc;
+    // count of the other list's entries ranked above: active values >= ve
+    // (for a kept entry) or kept values > ve (for an active one)
+    int lo_i = is_act ? pc : 0, hi_i = is_act ? p : pc;  // search range [lo_i, hi_i)
+    const int base = lo_i;
+    while (lo_i < hi_i) {
+      const int mid = (lo_i + hi_i) >> 1;
+      const double vm = vals[mid];
+      if (is_act ? vm > ve : vm >= ve) lo_i = mid + 1;
+      else hi_i = mid;
     }
-    rank_of[tid] = pos;
+    rank_of[tid] = (is_act ? tid : tid - pc) + (lo_i - base);
   }
   __syncthreads();
   if (tid < p) lam_sorted[rank_of[tid]] = vals[tid];  // (inv_norm is done with)
