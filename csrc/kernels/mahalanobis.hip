@@ -867,10 +867,17 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     const unsigned long long heads = __ballot(own && (lane == 0 || dd[lane - 1] - dl > tol));
     zhp[lane] = zh;
     wave_lds_sync();
-    for (int s0 = 0; s0 < p;) {
-      const unsigned long long rest = (s0 + 1 < 64) ? heads >> (s0 + 1) : 0ull;
-      const int e0 = rest ? min(p, s0 + 1 + int(__builtin_ctzll(rest))) : p;
-      if (e0 - s0 > 1) {
+    // visit only the clusters with more than one member (usually none): each
+    // holds a non-head index; the cluster runs from the last head at or below
+    // it to the next head
+    unsigned long long nonheads = __ballot(own) & ~heads;
+    while (nonheads) {
+      const int j0 = int(__builtin_ctzll(nonheads));
+      const int s0 = 63 - int(__builtin_clzll(heads & ((2ull << j0) - 1ull)));
+      const unsigned long long rest = heads >> j0;  // (bit j0 of heads is clear)
+      const int e0 = rest ? min(p, j0 + int(__builtin_ctzll(rest))) : p;
+      nonheads &= e0 >= 64 ? 0ull : (~0ull << e0);
+      {
         double nrm2 = 0.0;
         for (int c = s0; c < e0; ++c) nrm2 += zhp[c] * zhp[c];
         if (nrm2 > 0.0) {
@@ -889,7 +896,6 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
           wave_lds_sync();
         }
       }
-      s0 = e0;
     }
     zh = zhp[lane];
     // active set: compaction by ballot (active indices first, in order)
