@@ -869,7 +869,11 @@ struct SyncWait {
   Outcome out;
   void set(Outcome o) {
     out = std::move(o);
-    state.store(1, std::memory_order_release);
+    // seq_cst on both sides of the state / sleeping handshake: a release
+    // store here could still sit in the store buffer while the load of
+    // `sleeping` below reads false and the waiter, about to sleep, reads
+    // state == 0 -- both would miss each other
+    state.store(1, std::memory_order_seq_cst);
     if (sleeping.load(std::memory_order_seq_cst)) {
       std::lock_guard<std::mutex> g(mu);
       cv.notify_all();
@@ -882,7 +886,7 @@ struct SyncWait {
       if ((n & 63) == 0 && std::chrono::steady_clock::now() >= until) {
         std::unique_lock<std::mutex> lk(mu);
         sleeping.store(true, std::memory_order_seq_cst);
-        cv.wait(lk, [&] { return state.load(std::memory_order_acquire) != 0; });
+        cv.wait(lk, [&] { return state.load(std::memory_order_seq_cst) != 0; });
         break;
       }
     }
