@@ -651,6 +651,7 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
 constexpr int kJacobiRefresh = 256;   // Jacobi-only mode: cold solve period
 constexpr int kTrackRefresh = 1024;   // eigen-tracking mode: cold solve period
 constexpr int kTrackMaxRows = 16;     // requests with more rows re-solve by Jacobi
+constexpr bool kMahaMfmaGemm = true;  // eigen-tracking V Q on v_mfma_f64_16x16x4
 
 template <int NT>
 __device__ __forceinline__ void jacobi_solve(double* __restrict__ A, double* __restrict__ V, double* __restrict__ W,
@@ -1074,10 +1075,38 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   }
   __syncthreads();
   mark(2);
-  // ---- entries -> A's columns: e < pc the new vectors V[:, act] Q[:, e]
-  // (4x4 register blocks; rows / columns past the ends read in-bounds LDS
-  // garbage and are not stored), e >= pc the kept columns of V
-  const int nr4 = (p + 3) >> 2, nc4 = (pc + 3) >> 2;
+  // ---- entries -> A's columns: e < pc the new vectors V[:, act] Q[:, e],
+  // e >= pc the kept columns of V.  The product on the f64 matrix cores
+  // (v_mfma_f64_16x16x4: lane l holds A[l&15][k = l>>4] and B[k = l>>4][l&15],
+  // result rows (l>>4) + 4i of column l&15): 16x16 tiles over the waves, k
+  // past pc fed as zeros; rows / columns past the ends read in-bounds LDS
+  // garbage that reaches only results that are not stored.  (The 4x4
+  // register-block VALU loop below is the kMahaMfmaGemm = false variant.)
+  if (kMahaMfmaGemm) {
+    const int tr = (p + 15) >> 4, tc = (pc + 15) >> 4;
+    const int wave = tid >> 6, li = lane & 15, lk = lane >> 4;
+    for (int t = wave; t < tr * tc; t += NT / 64) {
+      const int r0 = (t / tc) * 16, c0 = (t - (t / tc) * tc) * 16;
+      typedef double d4 __attribute__((ext_vector_type(4)));
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      for (int k0 = 0; k0 < pc; k0 += 4) {
+        const int kk = k0 + lk;
+        const double a = kk < pc ? V[(r0 + li) * kLd + perm[kk]] : 0.0;
+        const double b = kk < pc ? W[kk * kLd + c0 + li] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+      const int col = c0 + li;
+      if (col < pc) {
+        const double sc = inv_norm[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = r0 + lk + 4 * i;
+          if (row < p) A[row * kLdA + col] = acc[i] * sc;
+        }
+      }
+    }
+  }
+  const int nr4 = (p + 3) >> 2, nc4 = kMahaMfmaGemm ? 0 : (pc + 3) >> 2;
   for (int e = tid; e < nr4 * nc4; e += NT) {
     const int r0 = (e / nc4) * 4, c0 = (e - (e / nc4) * nc4) * 4;
     double acc[4][4] = {};
