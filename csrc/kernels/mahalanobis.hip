@@ -1088,13 +1088,24 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
     for (int t = wave; t < tr * tc; t += NT / 64) {
       const int r0 = (t / tc) * 16, c0 = (t - (t / tc) * tc) * 16;
       typedef double d4 __attribute__((ext_vector_type(4)));
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-      for (int k0 = 0; k0 < pc; k0 += 4) {
-        const int kk = k0 + lk;
-        const double a = kk < pc ? V[(r0 + li) * kLd + perm[kk]] : 0.0;
-        const double b = kk < pc ? W[kk * kLd + c0 + li] : 0.0;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      d4 acc = {0.0, 0.0, 0.0, 0.0}, acc2 = {0.0, 0.0, 0.0, 0.0};
+      // 16 k per round: the operand loads first (independent), then four
+      // MFMAs on two accumulators
+      for (int k0 = 0; k0 < pc; k0 += 16) {
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = k0 + 4 * u + lk;
+          const int src = perm[min(kk, pc - 1)];
+          a[u] = kk < pc ? V[(r0 + li) * kLd + src] : 0.0;
+          b[u] = kk < pc ? W[kk * kLd + c0 + li] : 0.0;
+        }
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], b[0], acc, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], b[1], acc2, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[2], b[2], acc, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[3], b[3], acc2, 0, 0, 0);
       }
+      acc += acc2;
       const int col = c0 + li;
       if (col < pc) {
         const double sc = inv_norm[col];
