@@ -1170,24 +1170,45 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   if (tid < p) lam_sorted[rank_of[tid]] = vals[tid];  // (inv_norm is done with)
   for (int e = tid; e < p * p; e += NT) {
     const int r = e / p, c = e - r * p;
-    V[r * kLd + rank_of[c]] = A[r * kLdA + c];
+    const double v = A[r * kLdA + c];
+    V[r * kLd + rank_of[c]] = v;
+    if (last) cache[r * p + rank_of[c]] = v;  // (invalidated below if the check fails)
   }
   __syncthreads();
   if (!last) return true;  // the next row's update starts from this basis
-  // ---- residual of the top-k pairs against the new covariance
+  // ---- residual of the top-k pairs against the new covariance, R = C_new
+  // V[:, 0:16] on the f64 matrix cores (one 16-row tile per wave; columns
+  // past k and rows past p are computed but not summed)
   double res = 0.0;
-  for (int e = tid; e < p * k; e += NT) {
-    const int r = e / k, c = e - r * k;
-    double sacc = 0.0;
-#pragma unroll 8
-    for (int j = 0; j < p; ++j) sacc += Cn[r * kLd + j] * V[j * kLd + c];
-    const double d = sacc - lam_sorted[c] * V[r * kLd + c];
-    res += d * d;
+  {
+    const int wave = tid >> 6, li = lane & 15, lk = lane >> 4;
+    for (int r0 = wave * 16; r0 < p; r0 += (NT / 64) * 16) {
+      typedef double d4 __attribute__((ext_vector_type(4)));
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      for (int k0 = 0; k0 < p; k0 += 4) {
+        const int kk = k0 + lk;
+        const double a = kk < p ? Cn[(r0 + li) * kLd + kk] : 0.0;
+        const double b = kk < p ? V[kk * kLd + li] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+      if (li < k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = r0 + lk + 4 * i;
+          if (row < p) {
+            const double d = acc[i] - lam_sorted[li] * V[row * kLd + li];
+            res += d * d;
+          }
+        }
+    }
   }
   res = block_sum<NT>(res, red);
   const double lim = 1e-11 * fabs(lam_sorted[0]);
-  if (!(res <= lim * lim)) return false;  // (uniform: every thread holds the block sum)
-  for (int e = tid; e < p * p; e += NT) cache[e] = V[(e / p) * kLd + e % p];
+  if (!(res <= lim * lim)) {  // (uniform: every thread holds the block sum)
+    if (tid == 0) tail[0] = -1.0;  // the cache already holds this basis: the re-solve starts cold
+    __syncthreads();
+    return false;
+  }
   if (tid < p) lam_cache[tid] = lam_sorted[tid];
   if (tid < k) sel[tid] = tid;
   if (tid == 0) tail[1] += 1.0;  // steps since the last cold solve (tail[0] = p already)
