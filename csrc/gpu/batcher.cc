@@ -737,8 +737,12 @@ void BatchedUnit::finish_all() {
 // its oldest batch -- unless the hang watchdog or an injected hang needs the
 // pump to keep polling.
 bool BatchedUnit::block_on_oldest() {
-  if (cpu_ || ps_.inflight.empty() || opts_.hang_timeout_ms > 0 || hang_ms_.load(std::memory_order_relaxed) > 0)
-    return false;
+  if (ps_.inflight.empty()) return false;
+  if (cpu_) {  // an asynchronous CPU call (a peer rank): a bounded wait on its replies
+    auto& c = ps_.inflight.front()->call;
+    return c && c->wait_us(200);
+  }
+  if (opts_.hang_timeout_ms > 0 || hang_ms_.load(std::memory_order_relaxed) > 0) return false;
   (void)hipEventSynchronize(ps_.inflight.front()->ev.get());
   return true;
 }

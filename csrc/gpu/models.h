@@ -25,6 +25,9 @@ struct CpuCall {
   virtual ~CpuCall() = default;
   virtual bool done() = 0;            // non-blocking; true once `out` holds the result (or it failed)
   virtual std::string error() const = 0;
+  // Block up to `us` for progress (the batcher's low-CPU mode, instead of a
+  // sleep-and-poll whose timer slack costs ~50 us); false = not supported.
+  virtual bool wait_us(int) { return false; }
 };
 using CpuCallPtr = std::shared_ptr<CpuCall>;
 

@@ -1,5 +1,7 @@
 #include "fabric.h"
 
+#include <poll.h>
+
 #include <fcntl.h>
 #include <immintrin.h>
 #include <sys/mman.h>
@@ -360,6 +362,19 @@ PeerHeader Fabric::take() {
   return h;
 }
 
+void Fabric::wait_readable(const std::vector<int>& peers, int us) const {
+  pollfd pf[16];
+  int n = 0;
+  for (int p : peers) {
+    if (n == 16 || p <= 0 || p >= world_) continue;
+    const int f = fds_[size_t(p)];
+    if (f >= 0) pf[n++] = pollfd{f, POLLIN, 0};
+  }
+  if (n == 0) return;
+  const timespec ts{0, long(std::max(1, us)) * 1000L};
+  (void)::ppoll(pf, nfds_t(n), &ts, nullptr);
+}
+
 int Fabric::backlog() const {
   if (rank_ == 0 || rings_.empty() || !rings_[0]) return 0;
   const HeaderRing* R = rings_[0];
@@ -604,6 +619,11 @@ struct PeerCall : gpu::CpuCall {
     return true;
   }
   std::string error() const override { return err; }
+  bool wait_us(int us) override {
+    if (finished || !pending()) return true;
+    f->wait_readable(peers, us);
+    return true;
+  }
 };
 }  // namespace
 

@@ -192,6 +192,8 @@ class Fabric {
   // block = true: waits for the oldest outstanding reply.  True if any
   // waiter was finished.
   bool poll_replies(int peer, bool block);
+  // Wait up to `us` until a reply of any of `peers` is readable (CPU fabrics).
+  void wait_readable(const std::vector<int>& peers, int us) const;
   // Worker: headers published behind the next one to take (the batches
   // rank 0 has outstanding here beyond the current one).
   int backlog() const;
