@@ -47,7 +47,9 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
         return
-    dep = sca.Deployment(spec, components=comps, device=-1, fabric=fabric)
+    low_cpu = os.environ.get("SCA_TEST_LOW_CPU") == "1"  # the batcher's low-CPU mode (bench setting)
+    dep = sca.Deployment(spec, components=comps, device=-1, fabric=fabric,
+                         batcher={"spin_wait": False} if low_cpu else None)
     rng = np.random.default_rng(0)
     worst = 0.0
     n = 0

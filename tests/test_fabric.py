@@ -94,6 +94,14 @@ def test_remote_model_node_cpu_fabric(world):
     assert last["host_syncs"] == 0  # CPU loop never waits on a device
 
 
+def test_remote_model_low_cpu_batcher_cpu_fabric():
+    """The batcher's low-CPU mode waits on the peer's link socket (ppoll)
+    instead of sleeping between polls: same answers, same row counts."""
+    outs = _run_ranks(2, "single", SCA_TEST_LOW_CPU="1")
+    assert outs[0]["worst"] < 1e-12 and outs[0]["rows"] > 0
+    assert outs[1]["error"] == "" and outs[1]["rows"] == outs[0]["rows"]
+
+
 def test_combiner_gathers_from_every_rank_cpu_fabric():
     outs = _run_ranks(3, "combiner")
     assert outs[0]["worst"] < 1e-12
