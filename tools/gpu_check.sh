@@ -70,6 +70,11 @@ for s in $STEPS; do
         python3 tools/kernel_microbench.py --only lstm --iters 10
       keep_stats prof_lstm ;;
     maha) run maha 300 python tools/maha_bench.py --p 9 20 32 64 --requests 2000 --threads 16 --out "$OUT/maha.json" ;;
+    maha_phase) run maha_phase 300 python -u tools/maha_bench.py --p 9 32 64 --requests 1000 --threads 16 --out "$OUT/maha_phase.json" ;;
+    jprobe)  # build first on the CPU: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc/kernels tools/micro/jacobi_probe.hip -o tools/micro/jacobi_probe
+      run jprobe 120 bash -c 'for p in 9 20 32 64; do ./tools/micro/jacobi_probe $p || exit 1; done' ;;
+    xgb_tpt) run xgb_tpt 700 bash tools/gpu_xgb_tpt.sh ;;
+    threads) run threads 900 bash tools/gpu_threads_sweep.sh ;;
     maha_jac) SCA_MAHA_RANK1_MAX_P=0 run maha_jac 300 python tools/maha_bench.py --p 9 20 32 --requests 2000 --threads 16 --out "$OUT/maha_jacobi.json" ;;
     maha_hh) SCA_MAHA_RANK1_MAX_P=0 SCA_MAHA_JACOBI_MAX_P=0 run maha_hh 300 python tools/maha_bench.py --p 9 32 64 --requests 2000 --threads 16 --out "$OUT/maha_householder.json" ;;
     prof_maha)
