@@ -1,5 +1,12 @@
+"""Latency / throughput probe of one rank-placed MODEL node over the CPU
+fabric (2 ranks, REST load on rank 0), against the same node in-process
+(PLACED=0).  Knobs: PLACED, SPIN (batcher spin_wait), SLOTS, THREADS, USERS.
+
+    CUDA_VISIBLE_DEVICES= python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 tools/fabric_lat_probe.py
+"""
 import json, os, sys, time
-sys.path.insert(0, "/root/repo")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import torch.distributed as dist
 dist.init_process_group("gloo")
