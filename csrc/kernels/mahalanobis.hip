@@ -1432,6 +1432,8 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   // after the projections, which still need the old one)
   const double den = n + fmax(1.0, double(nb) - 1.0);
   const int m = p + (p & 1);
+  // (unrolled: several of the state's HBM loads in flight per thread)
+#pragma unroll 4
   for (int e = tid; e < m * m; e += NT) {
     const int a = e / m, b = e - a * m;
     double cov = 0.0;
@@ -1493,6 +1495,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
   // ---- projections; proj_cov = V^T C_old V over the selected columns:
   // C_old (still in HBM) -> W, U = C_old V_sel -> A (free after the
   // selection), P = V_sel^T U
+#pragma unroll 4
   for (int e = tid; e < p * p; e += NT) W[(e / p) * kLd + e % p] = c_zero ? 0.0 : s_C[e];
   __syncthreads();
   for (int e = tid; e < p * k; e += NT) {
