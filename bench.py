@@ -29,8 +29,10 @@ After the headline (never inside it):
   over one replica per GPU, with concurrent feedback traffic) and
   ``replicas`` (one endpoint over a replica per GPU);
 * then every rank starts a fabric child: the same graphs with their nodes
-  placed on ranks (``abtest_rccl``, ``pipeline_rccl``, ``mab_rccl``), batches
-  travelling between the rank processes as RCCL send/recv over xGMI.
+  placed on ranks (``abtest_ranks``, ``pipeline_ranks``, ``mab_ranks``), one
+  engine process per GPU; placed subtrees run as mesh programs whose stages
+  hand rows to each other directly (HIP IPC + shared-memory doorbells; the
+  transport is reported per graph, SCA_FABRIC_TRANSPORT selects another).
 
 Robustness: the whole run has one budget (``BUDGET_S``); every child and load
 generator call gets a timeout from what is left; ranks hand results to rank 0
@@ -765,9 +767,9 @@ def run_fabric_phase(args, d: Dist, rep: Reporter, budget: bk.Budget, kinds) -> 
     if not go or "skip" in go:
         if d.rank == 0:
             for k in kinds:
-                rep.variants[f"{k}_rccl"] = {"error": (go or {}).get("skip", "not run")}
-                if f"{k}_rccl" in rep.pending:
-                    rep.pending.remove(f"{k}_rccl")
+                rep.variants[f"{k}_ranks"] = {"error": (go or {}).get("skip", "not run")}
+                if f"{k}_ranks" in rep.pending:
+                    rep.pending.remove(f"{k}_ranks")
         return
     deadline = float(go["deadline"])
     cmd = [sys.executable, os.path.abspath(__file__), "--model", args.model, "--slots", str(args.slots),
@@ -794,13 +796,13 @@ def run_fabric_phase(args, d: Dist, rep: Reporter, budget: bk.Budget, kinds) -> 
         return
     peers = ex.wait("fabric", list(range(1, d.world)), timeout=max(0.0, budget.left(REPORT_RESERVE_S)))
     for k in kinds:
-        key = f"{k}_rccl"
+        key = f"{k}_ranks"
         r0 = out["graphs"].get(k)
         if r0 is None:
             r0 = {"error": "timeout" if status == "timeout" else f"fabric child {status}: no result",
                   "stderr_tail": res["stderr"][-400:]}
         r0 = dict(r0)
-        r0["data_plane"] = out.get("data_plane", "rccl" if d.has_gpu else "sockets")
+        r0["data_plane"] = out.get("data_plane") or ("ipc" if d.has_gpu else "shm")
         r0["fabric_world"] = d.world
         r0["worker_ranks"] = {str(r): ((p.get("result") or {}).get("graphs") or {}).get(k, {"status": p["status"]})
                               for r, p in sorted(peers.items())}
@@ -813,11 +815,12 @@ def run_fabric_phase(args, d: Dist, rep: Reporter, budget: bk.Budget, kinds) -> 
 
 
 def fabric_child(args) -> None:
-    """Rank-placed graphs over the RCCL p2p fabric.
-    Rank 0 hosts the front end, router/combiner and the micro-batchers; the
-    nodes placed on rank r run in rank r's PeerServer on its GPU; batches and
-    replies are RCCL send/recv on GPUs (sockets on CPU).  Every rank walks the
-    same graph list in the same order."""
+    """Rank-placed graphs.  Rank 0 hosts the front end,
+    routers and the program units; the nodes placed on rank r run on rank r's
+    GPU (mesh programs over HIP IPC + shared memory by default, shared memory
+    alone on CPU; SCA_FABRIC_TRANSPORT=rccl|rccl1 for the RCCL star).  Every
+    rank walks the same graph list in the same order, with a fresh fabric per
+    graph."""
     import datetime
 
     import torch
@@ -832,30 +835,33 @@ def fabric_child(args) -> None:
     from seldon_core_amd.parallel.fabric import init_fabric, serve_peer
     from seldon_core_amd.serving.deployment import Deployment
 
-    fabric = init_fabric(device=dev)
     wl = bk.Workload(args.model)
     graphs = {}
+    transport = None
     for kind in [k for k in args.fabric_child.split(",") if k]:
         if (kind == "pipeline" and world < 4) or world < 2:
             continue
         g, comps, oracle, label = bk.build_rank_graph(wl, kind, world)
         spec = bk.sdep(g)
+        fabric = init_fabric(device=dev)  # one per graph: a mesh is set up once
+        transport = fabric.transport
         if rank != 0:
             t0 = time.perf_counter()
             try:
-                fault(f"{kind}_rccl", rank)
+                fault(f"{kind}_ranks", rank)
                 srv = serve_peer(spec, fabric, comps)
                 srv.join()
                 graphs[kind] = {"batches": srv.batches, "rows": srv.rows, "host_syncs": srv.host_syncs,
                                 "max_inflight": getattr(srv, "max_inflight", None), "error": srv.error(),
-                                "device": dev, "wall_s": round(time.perf_counter() - t0, 2)}
+                                "device": dev, "transport": transport, "wall_s": round(time.perf_counter() - t0, 2)}
             except Exception as e:
                 graphs[kind] = {"error": f"{type(e).__name__}: {e}"[:400]}
+            fabric.close()
             print(json.dumps({"kind": kind, "result": graphs[kind]}), flush=True)
             continue
         dep = h = None
         try:
-            fault(f"{kind}_rccl", 0)
+            fault(f"{kind}_ranks", 0)
             dep = Deployment(spec, components=comps, device=dev, fabric=fabric, fuse=False,
                              batcher={"max_batch": 4096, "slots": args.slots, "spin_wait": False})
             h = dep.serve(http_port=0, grpc_port=0, threads=args.server_threads, host="127.0.0.1")
@@ -898,6 +904,10 @@ def fabric_child(args) -> None:
                  "rank0_device_batches": {k: v["batches"] for k, v in st["per_device"].items()}}
             if kind == "mab":
                 r["feedback"] = {"rewarded_branch": world - 1, "rps": fb_out.get("rps"), "error": fb_out.get("error")}
+            if dep.mesh is not None:
+                r["mesh_programs"] = [{"root": p.root, "stages": p.describe(), "messages_per_batch": m}
+                                      for p, m in zip(dep.mesh.programs, dep.mesh.messages)]
+            r["transport"] = transport
             graphs[kind] = r
         except Exception as e:
             graphs[kind] = {"error": f"{type(e).__name__}: {e}"[:600]}
@@ -909,12 +919,11 @@ def fabric_child(args) -> None:
                     dep.close()  # stops the peers' loops for this graph
                 else:
                     fabric.stop_peers()  # keep the workers in step with the graph list
+                fabric.close()
             except Exception:
                 pass
         print(json.dumps({"kind": kind, "result": graphs[kind]}), flush=True)
-    fabric.close()
-    print(json.dumps({"rank": rank, "world": world, "device": dev,
-                      "data_plane": "rccl" if dev >= 0 else "sockets"}), flush=True)
+    print(json.dumps({"rank": rank, "world": world, "device": dev, "data_plane": transport}), flush=True)
     sys.stdout.flush()
     os._exit(0)  # no teardown collective: a peer that failed must not hold this child
 
@@ -950,7 +959,7 @@ def main() -> None:
     if extras and d.world >= 2 and args.model in ("iris", "xgb1000"):  # same lists on every rank
         inproc = [k for k in args.variants.split(",") if k and (k != "pipeline" or d.world >= 4)]
         rccl = [k for k in args.rank_variants.split(",") if k and (k != "pipeline" or d.world >= 4)]
-    rep.pending = inproc + [f"{k}_rccl" for k in rccl]
+    rep.pending = inproc + [f"{k}_ranks" for k in rccl]
     dep = handle = None
     try:
         dep, handle, pb, expect_pb, head_lg = headline(args, d, rep, budget, per_rank_cpus, pinned)

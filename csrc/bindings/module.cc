@@ -21,6 +21,7 @@
 #include "../gpu/router.h"
 #include "../kernels/kernels.h"
 #include "../parallel/fabric.h"
+#include "../parallel/mesh.h"
 #include "../server/grpc_server.h"
 #include "../server/http_server.h"
 #include "../server/remote_unit.h"
@@ -584,7 +585,8 @@ PYBIND11_MODULE(_C, m) {
       });
 
   // ------------------------------------------------------- RCCL fabric
-  m.def("rccl_unique_ids", [](int world) { return py::bytes(par::rccl_unique_ids(world)); }, py::arg("world"));
+  m.def("rccl_unique_ids", [](int world, int per_link) { return py::bytes(par::rccl_unique_ids(world, per_link)); },
+        py::arg("world"), py::arg("per_link") = 2);
   py::class_<par::LoopbackHub, std::shared_ptr<par::LoopbackHub>>(m, "LoopbackHub")
       .def(py::init<int>(), py::arg("device"))
       .def_property_readonly("device", &par::LoopbackHub::device)
@@ -593,13 +595,14 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("matched_immediately", &par::LoopbackHub::matched_immediately);
   py::class_<par::Fabric, std::shared_ptr<par::Fabric>>(m, "Fabric")
       .def(py::init([](int rank, int world, const py::bytes& uid, int device, std::vector<int> ctrl_fds,
-                       std::shared_ptr<par::LoopbackHub> hub) {
+                       std::shared_ptr<par::LoopbackHub> hub, int comms_per_link) {
              std::string id(uid);
              py::gil_scoped_release nogil;  // collective: blocks until every rank joins
-             return std::make_shared<par::Fabric>(rank, world, id, device, std::move(ctrl_fds), std::move(hub));
+             return std::make_shared<par::Fabric>(rank, world, id, device, std::move(ctrl_fds), std::move(hub),
+                                                  comms_per_link);
            }),
            py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"), py::arg("ctrl_fds"),
-           py::arg("hub") = nullptr)
+           py::arg("hub") = nullptr, py::arg("comms_per_link") = 2)
       .def_property_readonly("gpu", &par::Fabric::gpu)
       .def_property_readonly("transport", &par::Fabric::transport)
       .def_property_readonly("rank", &par::Fabric::rank)
@@ -637,6 +640,95 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("max_inflight", &par::PeerServer::max_inflight)
       .def_property_readonly("slots", &par::PeerServer::slots)
       .def("error", &par::PeerServer::error);
+
+  // ------------------------------------------------- mesh (ipc / shm)
+  py::class_<par::Mesh, std::shared_ptr<par::Mesh>>(m, "Mesh")
+      .def(py::init<int, int, int, std::vector<int>, int>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("ctrl_fds"), py::arg("slots") = 4)
+      .def_property_readonly("rank", &par::Mesh::rank)
+      .def_property_readonly("world", &par::Mesh::world)
+      .def_property_readonly("device", &par::Mesh::device)
+      .def_property_readonly("gpu", &par::Mesh::gpu)
+      .def_property_readonly("slots", &par::Mesh::slots)
+      .def_property_readonly("transport", &par::Mesh::transport)
+      .def("add_program",
+           [](par::Mesh& me, const py::dict& d) {
+             par::MeshProgram p;
+             p.max_rows = d["max_rows"].cast<int>();
+             p.in_cols = d["in_cols"].cast<int>();
+             for (auto item : d["stages"].cast<py::list>()) {
+               auto s = item.cast<py::dict>();
+               par::MeshStage st;
+               st.rank = s["rank"].cast<int>();
+               st.kind = s["kind"].cast<int>();
+               st.inputs = s["inputs"].cast<std::vector<int>>();
+               st.in_cols = s["in_cols"].cast<int>();
+               st.out_cols = s["out_cols"].cast<int>();
+               st.node = s.contains("node") ? s["node"].cast<std::string>() : std::string();
+               p.stages.push_back(std::move(st));
+             }
+             return me.add_program(std::move(p));
+           })
+      .def("set_model", &par::Mesh::set_model)
+      .def("set_host_fn",
+           [](par::Mesh& me, int prog, int stage, py::object fn) {
+             // A Python component on this rank: called with the GIL from the
+             // program's thread, on a copy of the rows.
+             auto f = std::make_shared<py::object>(std::move(fn));
+             me.set_host_fn(prog, stage, [f](const double* x, int rows, int cols, double* y, int oc) {
+               py::gil_scoped_acquire gil;
+               py::array_t<double> X({rows, cols});
+               std::memcpy(X.mutable_data(), x, size_t(rows) * size_t(cols) * sizeof(double));
+               py::object r = (*f)(X);
+               auto Y = py::array_t<double, py::array::c_style | py::array::forcecast>::ensure(r);
+               if (!Y) throw std::runtime_error("component returned a non-numeric payload");
+               const size_t want = size_t(rows) * size_t(oc);
+               if (size_t(Y.size()) != want)
+                 throw std::runtime_error("component returned " + std::to_string(Y.size()) + " values, expected " +
+                                          std::to_string(rows) + " x " + std::to_string(oc));
+               std::memcpy(y, Y.data(), want * sizeof(double));
+             });
+           })
+      .def("prepare", [](par::Mesh& me) { return py::bytes(me.prepare()); })
+      .def("connect",
+           [](par::Mesh& me, const std::vector<py::bytes>& blobs) {
+             std::vector<std::string> b;
+             for (auto& x : blobs) b.emplace_back(std::string(x));
+             py::gil_scoped_release nogil;
+             me.connect(b);
+           })
+      .def("unlink", &par::Mesh::unlink)
+      .def("start", [](par::Mesh& me) {
+        py::gil_scoped_release nogil;
+        me.start();
+      })
+      .def("join", [](par::Mesh& me) {
+        py::gil_scoped_release nogil;
+        me.join();
+      })
+      .def("stop_peers", [](par::Mesh& me) {
+        py::gil_scoped_release nogil;
+        me.stop_peers();
+      })
+      .def("close", [](par::Mesh& me) {
+        py::gil_scoped_release nogil;
+        me.close();
+      })
+      .def_property_readonly("open", &par::Mesh::open)
+      .def("error", &par::Mesh::error)
+      .def("messages_per_batch", &par::Mesh::messages_per_batch)
+      .def("stats", [](const par::Mesh& me) {
+        const auto s = me.stats();
+        py::dict d;
+        d["batches"] = s.batches;
+        d["rows"] = s.rows;
+        d["max_inflight"] = s.max_inflight;
+        d["host_waits"] = s.host_waits;
+        d["stage_errors"] = s.stage_errors;
+        return d;
+      })
+      .def("program_model", &par::Mesh::program_model, py::arg("prog"),
+           py::arg("class_names") = std::vector<std::string>(), py::arg("flat_output") = false);
 
   // ------------------------------------------------------------- engine
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")

@@ -89,7 +89,9 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
       cpu_ = true;
       for (int i = 0; i < opts_.slots; ++i) slots_.push_back(std::make_unique<Slot>());
       for (auto& s : slots_) ps_.free_list.push_back(s.get());
-      driver_ = DeviceDriver::acquire(-1, false);  // launch() may compute inline: a pump of its own
+      // launch() may compute inline: a pump of its own -- unless the model only
+      // issues work to other ranks (mesh programs), whose units share one pump
+      driver_ = model_->async_cpu() ? DeviceDriver::acquire(kAsyncCpuDriver, true) : DeviceDriver::acquire(-1, false);
       driver_->add(this);
     }
     return;

@@ -28,6 +28,9 @@
 
 namespace sca::gpu {
 
+// Driver key of the shared pump for asynchronous CPU-batching units.
+constexpr int kAsyncCpuDriver = -2;
+
 class DeviceDriver {
  public:
   // The shared driver of `device` (created on first use, gone with its last

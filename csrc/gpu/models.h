@@ -82,6 +82,9 @@ class RowModel {
   // the loopback transport's rendezvous): its unit gets a pump thread of its
   // own instead of sharing the GPU's, so it never stalls the other units.
   virtual bool exclusive_driver() const { return false; }
+  // True if start_cpu() never blocks for long (it only issues work to other
+  // processes): CPU-batching units of such models share one pump thread.
+  virtual bool async_cpu() const { return false; }
   // Asynchronous run_cpu: returns a call to poll, or nullptr if the model has
   // none (X must stay valid and `out` untouched until done()).
   virtual CpuCallPtr start_cpu(const double* X, int rows, int cols, double* out) {

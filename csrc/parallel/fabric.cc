@@ -81,9 +81,10 @@ void backoff_until(Ready ready, Slow slow) {
 constexpr int kChanX = 0, kChanY = 1;
 }  // namespace
 
-std::string rccl_unique_ids(int world) {
+std::string rccl_unique_ids(int world, int per_link) {
   if (world < 2) return std::string();
-  std::vector<ncclUniqueId> ids(size_t(2 * (world - 1)));
+  if (per_link != 1 && per_link != 2) throw std::runtime_error("rccl_unique_ids: 1 or 2 communicators per link");
+  std::vector<ncclUniqueId> ids(size_t(per_link * (world - 1)));
   for (auto& id : ids) SCA_NCCL_CHECK(ncclGetUniqueId(&id));
   return std::string(reinterpret_cast<const char*>(ids.data()), ids.size() * sizeof(ncclUniqueId));
 }
@@ -166,43 +167,42 @@ void LoopbackHub::close_rank(int rank) {
 
 // ------------------------------------------------------------------ fabric
 Fabric::Fabric(int rank, int world, const std::string& unique_ids, int device, std::vector<int> ctrl_fds,
-               LoopbackHubPtr hub)
-    : rank_(rank), world_(world), device_(device), hub_(std::move(hub)), fds_(std::move(ctrl_fds)) {
+               LoopbackHubPtr hub, int comms_per_link)
+    : rank_(rank), world_(world), device_(device), hub_(std::move(hub)), fds_(std::move(ctrl_fds)),
+      per_link_(comms_per_link) {
   if (rank < 0 || rank >= world) throw std::runtime_error("Fabric: rank out of range");
+  if (device < 0) throw std::runtime_error("Fabric: the RCCL / loopback fabric needs a GPU (CPU gangs use the shm mesh)");
+  if (per_link_ != 1 && per_link_ != 2) throw std::runtime_error("Fabric: 1 or 2 communicators per link");
   if (int(fds_.size()) != world) throw std::runtime_error("Fabric: need one control socket slot per rank");
   if (hub_ && hub_->device() != device) throw std::runtime_error("Fabric: loopback hub lives on another GPU");
   links_.resize(size_t(world));
   for (int r = 0; r < world; ++r)
     if ((rank == 0) != (r == 0)) links_[size_t(r)] = std::make_unique<Link>();
   map_rings();
-  if (device_ < 0) {
-    rq_.resize(size_t(world_));
-    if (rank_ == 0)
-      for (int r = 1; r < world_; ++r) rq_[size_t(r)] = std::make_unique<RecvQ>();
-    return;
-  }
   gpu::DeviceGuard g(device);
   for (auto& l : links_)
     if (l) {
       l->sx.create(device);
-      l->sy.create(device);
+      if (per_link_ == 2) l->sy.create(device);
     }
   if (hub_) return;
-  if (unique_ids.size() != size_t(2 * (world - 1)) * sizeof(ncclUniqueId))
+  if (unique_ids.size() != size_t(per_link_ * (world - 1)) * sizeof(ncclUniqueId))
     throw std::runtime_error("Fabric: bad RCCL unique id blob size");
   auto id_of = [&](int link, int chan) {
     ncclUniqueId id;
-    std::memcpy(&id, unique_ids.data() + size_t(2 * (link - 1) + chan) * sizeof(ncclUniqueId), sizeof id);
+    std::memcpy(&id, unique_ids.data() + size_t(per_link_ * (link - 1) + chan) * sizeof(ncclUniqueId), sizeof id);
     return id;
   };
-  // One 2-rank communicator pair per rank-0 <-> worker link: rank 0 is rank 0
-  // of each, the worker rank 1.  Rank 0 joins its links in worker order; a
-  // worker waits in its init until rank 0 reaches its link.
+  // One 2-rank communicator (pair) per rank-0 <-> worker link: rank 0 is rank
+  // 0 of each, the worker rank 1.  Rank 0 joins its links in worker order; a
+  // worker waits in its init until rank 0 reaches its link.  With one
+  // communicator per link, X and Y share it and one stream, so every
+  // operation of a communicator is issued from a single stream.
   for (int r = 1; r < world; ++r) {
     if (rank != 0 && rank != r) continue;
     Link& l = *links_[size_t(rank == 0 ? r : 0)];
     SCA_NCCL_CHECK(ncclCommInitRank(&l.cx, 2, id_of(r, kChanX), rank == 0 ? 0 : 1));
-    SCA_NCCL_CHECK(ncclCommInitRank(&l.cy, 2, id_of(r, kChanY), rank == 0 ? 0 : 1));
+    if (per_link_ == 2) SCA_NCCL_CHECK(ncclCommInitRank(&l.cy, 2, id_of(r, kChanY), rank == 0 ? 0 : 1));
   }
 }
 
@@ -287,7 +287,7 @@ void Fabric::close() {
     while (std::chrono::steady_clock::now() < until) {
       idle = true;
       for (auto& l : links_)
-        if (l && (hipStreamQuery(l->sx.get()) != hipSuccess || hipStreamQuery(l->sy.get()) != hipSuccess))
+        if (l && (hipStreamQuery(l->sx.get()) != hipSuccess || (l->sy.get() && hipStreamQuery(l->sy.get()) != hipSuccess)))
           idle = false;
       if (idle) break;
       std::this_thread::sleep_for(std::chrono::milliseconds(1));
@@ -301,15 +301,11 @@ void Fabric::close() {
     }
   }
   for (int& fd : fds_)
-    if (fd >= 0) ::shutdown(fd, SHUT_RDWR);  // a reader blocked in recv() returns
-  for (size_t r = 0; r < fds_.size(); ++r) {
-    std::unique_lock<std::mutex> rd;
-    if (r < rq_.size() && rq_[r]) rd = std::unique_lock<std::mutex>(rq_[r]->rd);
-    if (fds_[r] >= 0) {
-      ::close(fds_[r]);
-      fds_[r] = -1;
+    if (fd >= 0) {
+      ::shutdown(fd, SHUT_RDWR);
+      ::close(fd);
+      fd = -1;
     }
-  }
   // The rings stay mapped until the destructor: a worker thread may still be
   // polling one (its take() sees open_ == false and leaves).
 }
@@ -362,44 +358,15 @@ PeerHeader Fabric::take() {
   return h;
 }
 
-void Fabric::wait_readable(const std::vector<int>& peers, int us) const {
-  pollfd pf[16];
-  int n = 0;
-  for (int p : peers) {
-    if (n == 16 || p <= 0 || p >= world_) continue;
-    const int f = fds_[size_t(p)];
-    if (f >= 0) pf[n++] = pollfd{f, POLLIN, 0};
-  }
-  if (n == 0) return;
-  const timespec ts{0, long(std::max(1, us)) * 1000L};
-  (void)::ppoll(pf, nfds_t(n), &ts, nullptr);
-}
-
-int Fabric::backlog() const {
-  if (rank_ == 0 || rings_.empty() || !rings_[0]) return 0;
-  const HeaderRing* R = rings_[0];
-  const uint64_t seq = next_[0];
-  int n = 0;
-  while (n < 64 && R->slots[(seq + uint64_t(n)) % HeaderRing::kSlots].seq.load(std::memory_order_acquire) ==
-                       seq + uint64_t(n) + 1)
-    ++n;
-  return n;
-}
-
 void Fabric::xfer(bool send, int chan, void* p, size_t bytes, int peer) {
-  if (!gpu()) {
-    if (send) write_all(fd(peer), p, bytes);
-    else read_all(fd(peer), p, bytes);
-    return;
-  }
   Link& l = link(peer);
-  hipStream_t s = chan == kChanX ? l.sx.get() : l.sy.get();
+  hipStream_t s = chan == kChanX || per_link_ == 1 ? l.sx.get() : l.sy.get();
   if (hub_) {
     if (send) hub_->send(rank_, peer, chan, p, bytes, s);
     else hub_->recv(peer, rank_, chan, p, bytes, s);
     return;
   }
-  ncclComm_t c = chan == kChanX ? l.cx : l.cy;
+  ncclComm_t c = chan == kChanX || per_link_ == 1 ? l.cx : l.cy;
   const int to = rank_ == 0 ? 1 : 0;  // the other end, as a rank of the link's 2-rank communicator
   if (send) SCA_NCCL_CHECK(ncclSend(p, bytes, ncclChar, to, c, s));
   else SCA_NCCL_CHECK(ncclRecv(p, bytes, ncclChar, to, c, s));
@@ -409,79 +376,6 @@ void Fabric::send_x(const void* p, size_t bytes, int peer) { xfer(true, kChanX, 
 void Fabric::recv_x(void* p, size_t bytes, int peer) { xfer(false, kChanX, p, bytes, peer); }
 void Fabric::send_y(const void* p, size_t bytes, int peer) { xfer(true, kChanY, const_cast<void*>(p), bytes, peer); }
 void Fabric::recv_y(void* p, size_t bytes, int peer) { xfer(false, kChanY, p, bytes, peer); }
-
-void Fabric::expect_reply(int peer, void* dst, size_t bytes, std::shared_ptr<Waiter> w) {
-  RecvQ& q = recvq(peer);
-  std::lock_guard<std::mutex> g(q.mu);
-  q.q.push_back({dst, bytes, std::move(w)});
-}
-
-Fabric::RecvQ& Fabric::recvq(int peer) {
-  if (gpu() || rank_ != 0 || peer <= 0 || peer >= world_ || !rq_[size_t(peer)])
-    throw std::runtime_error("Fabric: no reply queue for rank " + std::to_string(peer));
-  return *rq_[size_t(peer)];
-}
-
-// Rank 0, CPU fabrics.  Replies of one worker arrive on its socket in issue
-// order; whichever caller polls reads them into the buffers queued by
-// expect_reply and finishes their waiters (no receiver thread: the batcher's
-// pump polls between launches, so a reply costs no extra thread wake-up).
-// One reader per link at a time (q.rd); the queue lock only guards push/pop,
-// and a deque's elements stay put under push_back.
-bool Fabric::poll_replies(int peer, bool block) {
-  RecvQ& q = recvq(peer);
-  std::unique_lock<std::mutex> rd(q.rd, std::defer_lock);
-  if (block) rd.lock();
-  else if (!rd.try_lock()) return false;
-  auto finish = [](Pending& p, const std::string& err) {
-    std::lock_guard<std::mutex> g(p.w->mu);
-    if (!err.empty() && p.w->error.empty()) p.w->error = err;
-    if (--p.w->pending == 0) p.w->cv.notify_all();
-  };
-  auto fail_all = [&](const std::string& err) {
-    std::lock_guard<std::mutex> g(q.mu);
-    for (auto& r : q.q) finish(r, err);
-    q.q.clear();
-    q.off = 0;
-  };
-  bool progress = false;
-  while (true) {
-    Pending* p;
-    {
-      std::lock_guard<std::mutex> g(q.mu);
-      if (q.q.empty()) return progress;
-      p = &q.q.front();
-    }
-    const int fd = fds_[size_t(peer)];
-    if (fd < 0) {
-      fail_all("fabric closed");
-      return true;
-    }
-    char* dst = static_cast<char*>(p->dst);
-    while (q.off < p->bytes) {
-      const ssize_t r = ::recv(fd, dst + q.off, p->bytes - q.off, block ? 0 : MSG_DONTWAIT);
-      if (r > 0) {
-        q.off += size_t(r);
-        continue;
-      }
-      if (r < 0 && errno == EINTR) continue;
-      if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return progress;
-      fail_all(r == 0 ? std::string("fabric peer closed the connection")
-                      : std::string("fabric socket read failed: ") + std::strerror(errno));
-      return true;
-    }
-    Pending done;
-    {
-      std::lock_guard<std::mutex> g(q.mu);
-      done = std::move(q.q.front());
-      q.q.pop_front();
-      q.off = 0;
-    }
-    finish(done, "");
-    progress = true;
-    if (block) return true;  // the caller re-checks its own waiter
-  }
-}
 
 void stop_peers(Fabric& f) {
   if (!f.open()) return;
@@ -558,112 +452,8 @@ void PeerRowModel::launch(const double* X, int rows, int cols, double* out, void
   batches_++;
 }
 
-// CPU fabric: header + payload go out under each link's mutex; the replies
-// land in call-owned buffers when a caller polls the link (poll_replies).
-std::shared_ptr<Fabric::Waiter> PeerRowModel::issue_cpu(const double* X, int rows, int cols) const {
-  if (f_->gpu()) throw std::runtime_error("rccl_peer: GPU fabric models run on their GPU");
-  if (!f_->open()) throw std::runtime_error("fabric closed");
-  const size_t bx = size_t(rows) * cols * sizeof(double), ny = size_t(rows) * out_cols_;
-  auto w = std::make_shared<Fabric::Waiter>();
-  w->pending = int(peers_.size());
-  w->bufs.assign(peers_.size(), std::vector<double>(ny));
-  for (size_t i = 0; i < peers_.size(); ++i) {
-    const int p = peers_[i];
-    std::lock_guard<std::mutex> g(f_->link_mutex(p));
-    // payload first: the worker, spinning on its ring, then finds the bytes
-    // already in its socket buffer instead of sleeping in read()
-    f_->expect_reply(p, w->bufs[i].data(), ny * sizeof(double), w);
-    f_->send_x(X, bx, p);
-    header(p, rows, cols);
-  }
-  batches_++;
-  return w;
-}
-
-namespace {
-// The reply (mean of the gathered replies for a fan-out) goes into `out` once.
-struct PeerCall : gpu::CpuCall {
-  FabricPtr f;             // held: an abandoned call may outlive its model
-  std::vector<int> peers;
-  std::shared_ptr<Fabric::Waiter> w;
-  double* out;
-  bool finished = false;
-  std::string err;
-  bool pending() {
-    std::lock_guard<std::mutex> g(w->mu);
-    return w->pending > 0;
-  }
-  bool done() override {
-    if (finished) return true;
-    if (pending())
-      for (int p : peers) f->poll_replies(p, false);
-    {
-      std::lock_guard<std::mutex> g(w->mu);
-      if (w->pending > 0) return false;
-      err = w->error;
-    }
-    if (err.empty()) {
-      const auto& b = w->bufs;
-      const size_t n = b[0].size();
-      if (b.size() == 1) {
-        std::copy(b[0].begin(), b[0].end(), out);
-      } else {
-        for (size_t i = 0; i < n; ++i) {
-          double acc = 0.0;
-          for (const auto& sl : b) acc += sl[i];
-          out[i] = acc / double(b.size());
-        }
-      }
-    }
-    finished = true;
-    return true;
-  }
-  std::string error() const override { return err; }
-  bool wait_us(int us) override {
-    if (finished || !pending()) return true;
-    f->wait_readable(peers, us);
-    return true;
-  }
-};
-}  // namespace
-
-gpu::CpuCallPtr PeerRowModel::start_cpu(const double* X, int rows, int cols, double* out) {
-  auto c = std::make_shared<PeerCall>();
-  c->f = f_;
-  c->peers = peers_;
-  c->w = issue_cpu(X, rows, cols);
-  c->out = out;
-  return c;
-}
-
-void PeerRowModel::run_cpu(const double* X, int rows, int cols, double* out) const {
-  PeerCall c;
-  c.f = f_;
-  c.peers = peers_;
-  c.w = issue_cpu(X, rows, cols);
-  c.out = out;
-  // Read replies (ours and older callers') until ours are in: a blocking
-  // read of a peer returns after one reply, so no peer is waited on for
-  // longer than its oldest outstanding batch.
-  // Spin briefly first: a worker's reply usually lands within tens of
-  // microseconds, and waking from a blocking read costs about as much again.
-  const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(100);
-  unsigned polls = 0;
-  while (c.pending()) {
-    bool got = false;
-    for (int p : peers_)
-      if (c.pending()) got |= f_->poll_replies(p, false);
-    if (!got && c.pending() && ((++polls & 7) != 0 || std::chrono::steady_clock::now() < spin_until)) {
-      _mm_pause();
-      continue;
-    }
-    if (!got && c.pending()) {
-      for (int p : peers_)
-        if (c.pending() && f_->poll_replies(p, true)) break;
-    }
-  }
-  c.done();
-  if (!c.err.empty()) throw std::runtime_error(c.err);
+void PeerRowModel::run_cpu(const double*, int, int, double*) const {
+  throw std::runtime_error("rccl_peer: GPU fabric models run on their GPU (CPU gangs use the shm mesh)");
 }
 
 // ---------------------------------------------------------------- worker side
@@ -677,7 +467,7 @@ PeerServer::~PeerServer() { join(); }
 
 int PeerServer::add_model(gpu::RowModelPtr m) {
   if (th_.joinable()) throw std::runtime_error("PeerServer: add models before start()");
-  if (f_->gpu()) m->to_device(f_->device());
+  m->to_device(f_->device());
   models_.push_back(std::move(m));
   return int(models_.size()) - 1;
 }
@@ -686,8 +476,7 @@ void PeerServer::start() {
   if (th_.joinable()) return;
   th_ = std::thread([this] {
     try {
-      if (f_->gpu()) loop();
-      else loop_cpu();
+      loop();
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(err_mu_);
       err_ = e.what();
@@ -780,36 +569,6 @@ void PeerServer::loop() {
   SCA_HIP_CHECK(hipStreamSynchronize(sx));
   SCA_HIP_CHECK(hipStreamSynchronize(sc.get()));
   SCA_HIP_CHECK(hipStreamSynchronize(sy));
-}
-
-// CPU worker (device -1 fabrics): one thread takes a header, reads its
-// payload, computes and replies, back to back.  Rank 0 keeps up to K calls
-// outstanding; their headers wait in the ring and their payloads in the
-// socket buffer, so a hand-off to a second thread would only add a wake-up
-// per batch (profiles/r04d_fabric_cpu).
-void PeerServer::loop_cpu() {
-  std::vector<double> x, y;
-  while (true) {
-    const PeerHeader h = f_->take();
-    if (h.op == kPeerStop) break;
-    if (h.model < 0 || h.model >= int(models_.size()) || h.rows <= 0 || h.cols <= 0)
-      throw std::runtime_error("PeerServer: bad header (model " + std::to_string(h.model) + ")");
-    note_inflight(uint64_t(1 + f_->backlog()));
-    x.resize(size_t(h.rows) * h.cols);
-    f_->recv_x(x.data(), x.size() * sizeof(double), 0);
-    try {
-      auto& m = models_[size_t(h.model)];
-      y.resize(size_t(h.rows) * m->out_cols(h.cols));
-      if (delay_us_) std::this_thread::sleep_for(std::chrono::microseconds(delay_us_));
-      m->run_cpu(x.data(), h.rows, h.cols, y.data());
-    } catch (...) {
-      f_->close();  // rank 0's outstanding calls fail instead of waiting for replies
-      throw;
-    }
-    f_->send_y(y.data(), y.size() * sizeof(double), 0);
-    batches_++;
-    rows_ += uint64_t(h.rows);
-  }
 }
 
 }  // namespace sca::par

@@ -47,12 +47,11 @@
 //      the matching send is posted, then copies out on the receiver's stream
 //      after the send's event.  No GPU-side wait on work not yet enqueued, so
 //      the transport cannot wedge a hardware queue;
-//    - sockets, CPU fabrics (device -1: multi-process tests and CPU serving
-//      run the same header ring; replies are read from the link's socket by
-//      whichever caller polls it (the batcher's pump, via CpuCall::done), the
-//      worker serves batches back to back from one thread (the ring and the
-//      socket buffer hold the backlog), and the front end's batcher keeps K
-//      calls outstanding through RowModel::start_cpu).
+//    CPU gangs and the default GPU transport ("shm" / "ipc") are the mesh
+//    (mesh.h): direct stage-to-stage edges over shared memory and HIP IPC.
+//    This star fabric stays as the RCCL transport ("rccl": an X and a Y
+//    communicator per link; "rccl1": one communicator and one stream per link,
+//    the conservative fallback) and its in-process loopback rehearsal.
 //
 // A fan-out to K ranks (COMBINER over replicas on K GPUs) sends the batch on
 // every link (the broadcast), receives every reply into its own slab (the
@@ -78,10 +77,10 @@
 
 namespace sca::par {
 
-// 2 * (world - 1) 128-byte RCCL ids (X and Y communicators of every
-// rank-0 <-> worker link, link r at [2(r-1), 2(r-1)+1]); rank 0 creates them,
-// everyone receives them out of band.
-std::string rccl_unique_ids(int world);
+// per_link * (world - 1) 128-byte RCCL ids (the X and Y communicators of
+// every rank-0 <-> worker link, link r at [2(r-1), 2(r-1)+1]; or one per link
+// when per_link == 1); rank 0 creates them, everyone receives them out of band.
+std::string rccl_unique_ids(int world, int per_link = 2);
 
 struct PeerHeader {
   int32_t op = 0, model = 0, rows = 0, cols = 0;
@@ -146,22 +145,22 @@ class Fabric {
  public:
   // ctrl_fds[r] = connected socket to rank r (-1 for self / no link): rank 0
   // holds one per worker, a worker one to rank 0.  The fabric owns them.
-  // device >= 0: GPU data plane -- RCCL (unique_ids from rccl_unique_ids on
-  // rank 0) or, with `hub`, the in-process loopback transport;
-  // device < 0: the sockets carry the data too (unique_ids ignored).
+  // GPU data plane: RCCL (unique_ids from rccl_unique_ids on rank 0, with
+  // comms_per_link 2 = separate X and Y communicators and streams, 1 = one of
+  // each per link) or, with `hub`, the in-process loopback transport.
   Fabric(int rank, int world, const std::string& unique_ids, int device, std::vector<int> ctrl_fds,
-         LoopbackHubPtr hub = nullptr);
+         LoopbackHubPtr hub = nullptr, int comms_per_link = 2);
   ~Fabric();
   int rank() const { return rank_; }
   int world() const { return world_; }
   int device() const { return device_; }
-  bool gpu() const { return device_ >= 0; }
+  bool gpu() const { return true; }
   bool loopback() const { return hub_ != nullptr; }
-  std::string transport() const { return !gpu() ? "sockets" : (hub_ ? "loopback" : "rccl"); }
+  std::string transport() const { return hub_ ? "loopback" : (per_link_ == 1 ? "rccl1" : "rccl"); }
   // Per-link resources (peer = the other end: a worker rank on rank 0, 0 on
   // a worker).
   hipStream_t stream_x(int peer) const { return link(peer).sx.get(); }
-  hipStream_t stream_y(int peer) const { return link(peer).sy.get(); }
+  hipStream_t stream_y(int peer) const { return per_link_ == 1 ? link(peer).sx.get() : link(peer).sy.get(); }
   std::mutex& link_mutex(int peer) { return link(peer).mu; }
   bool open() const { return open_.load(); }
   void close();
@@ -170,33 +169,11 @@ class Fabric {
   // throws once the peer's socket is gone)
   void publish(int peer, const PeerHeader& h);
   PeerHeader take();
-  // data plane: GPU fabrics enqueue on the link's X / Y stream; CPU fabrics
-  // write / read the link's socket
+  // data plane: enqueued on the link's X / Y stream
   void send_x(const void* p, size_t bytes, int peer);
   void recv_x(void* p, size_t bytes, int peer);
   void send_y(const void* p, size_t bytes, int peer);
   void recv_y(void* p, size_t bytes, int peer);
-
-  // CPU fabrics, rank 0: queue a reply read (bytes into `dst`); replies
-  // arrive in issue order and are read by poll_replies.
-  struct Waiter {
-    std::mutex mu;
-    std::condition_variable cv;
-    int pending = 0;
-    std::string error;
-    std::vector<std::vector<double>> bufs;  // reply buffers owned by the call (outlive an abandoned caller)
-  };
-  void expect_reply(int peer, void* dst, size_t bytes, std::shared_ptr<Waiter> w);
-  // Read the replies of `peer` that have arrived and finish their waiters.
-  // block = false: never waits (another thread reading that link -> returns);
-  // block = true: waits for the oldest outstanding reply.  True if any
-  // waiter was finished.
-  bool poll_replies(int peer, bool block);
-  // Wait up to `us` until a reply of any of `peers` is readable (CPU fabrics).
-  void wait_readable(const std::vector<int>& peers, int us) const;
-  // Worker: headers published behind the next one to take (the batches
-  // rank 0 has outstanding here beyond the current one).
-  int backlog() const;
 
  private:
   struct Link {
@@ -217,20 +194,7 @@ class Fabric {
   std::vector<uint64_t> next_;      // rank 0: next seq per worker; worker: next_[0] to take
   std::mutex close_mu_;
   std::atomic<bool> open_{true};
-  // CPU reply queues (rank 0, one per worker, created with the fabric)
-  struct Pending {
-    void* dst = nullptr;
-    size_t bytes = 0;
-    std::shared_ptr<Waiter> w;
-  };
-  struct RecvQ {
-    std::mutex mu;  // the queue
-    std::mutex rd;  // the reader of the link's socket (and `off`)
-    std::deque<Pending> q;
-    size_t off = 0;  // bytes of the front reply already read
-  };
-  RecvQ& recvq(int peer);
-  std::vector<std::unique_ptr<RecvQ>> rq_;
+  int per_link_ = 2;
 };
 using FabricPtr = std::shared_ptr<Fabric>;
 
@@ -247,16 +211,16 @@ class PeerRowModel : public gpu::RowModel {
   int in_cols() const override { return in_cols_; }
   int out_cols(int) const override { return out_cols_; }
   bool device_io_only() const override { return true; }
-  bool exclusive_driver() const override { return true; }  // one issuing thread per peer unit
+  // The loopback transport's receive blocks on the host until the matching
+  // send: those units need a pump of their own.  RCCL enqueues never block.
+  bool exclusive_driver() const override { return f_->loopback(); }
   void to_device(int device) override;
   size_t workspace_bytes(int max_rows, int cols) const override;
   void launch(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
-  gpu::CpuCallPtr start_cpu(const double* X, int rows, int cols, double* out) override;
   uint64_t batches() const { return batches_.load(); }
 
  private:
-  std::shared_ptr<Fabric::Waiter> issue_cpu(const double* X, int rows, int cols) const;
   void header(int peer, int rows, int cols) const;
   FabricPtr f_;
   std::vector<int> peers_;
@@ -285,7 +249,6 @@ class PeerServer {
 
  private:
   void loop();
-  void loop_cpu();
   void note_inflight(uint64_t n);
   FabricPtr f_;
   std::vector<gpu::RowModelPtr> models_;

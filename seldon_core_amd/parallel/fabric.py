@@ -1,19 +1,30 @@
 """Cross-process graph placement (one engine process per MI355X).
 
 Spec extension: a graph node may carry ``rank: r`` -- the torch.distributed
-rank (= GPU) whose process hosts that node's row model.  Rank 0 runs the front
-end (REST/gRPC), the graph executor, routers and the micro-batchers; every
-batch bound for a node on rank r is shipped GPU-to-GPU with RCCL point-to-point
-transfers over xGMI (csrc/parallel/fabric.h) and answered the same way.  Worker
-ranks run only a native ``PeerServer`` loop.
+rank (= GPU) whose process hosts that node.  Rank 0 runs the front end
+(REST/gRPC), the graph executor, routers and the micro-batchers; worker ranks
+serve the nodes placed on them.
+
+Transports (``SCA_FABRIC_TRANSPORT`` or ``init_fabric(transport=...)``):
+
+* ``ipc`` (GPU default) / ``shm`` (CPU gangs): the mesh (csrc/parallel/mesh.h,
+  ``parallel/mesh.py``).  Placed subtrees become programs with direct
+  stage-to-stage edges: HIP IPC device slabs between workers (peer copies over
+  xGMI across GPUs, plain copies when ranks share one GPU), shared-memory slabs
+  and doorbells to and from rank 0.  Any MODEL / TRANSFORMER /
+  OUTPUT_TRANSFORMER node -- a native row model or a Python component -- can
+  sit on a worker.
+* ``rccl`` / ``rccl1``: the star fabric (csrc/parallel/fabric.h): one
+  ``PeerRowModel`` per placed row-model node, RCCL point-to-point per batch
+  (two communicators and streams per link, or one of each with ``rccl1``).
 
 Typical launch (one process per GPU)::
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 my_server.py
 
-    fabric = init_fabric()                      # RCCL communicator over all ranks
+    fabric = init_fabric()                      # control links + the data plane
     if fabric.rank == 0:
-        dep = Deployment(spec, fabric=fabric)   # nodes with rank != 0 become PeerRowModels
+        dep = Deployment(spec, fabric=fabric)   # placed subtrees become remote units
         dep.serve(...)
     else:
         serve_peer(spec, fabric).join()         # until rank 0 calls dep.close()
@@ -62,25 +73,59 @@ def _control_links(rank: int, world: int, host: str = "127.0.0.1") -> List[int]:
     return fds
 
 
-def init_fabric(device: Optional[int] = None):
+TRANSPORTS = ("ipc", "shm", "rccl", "rccl1")
+
+
+def fabric_transport(device: int, transport: Optional[str] = None) -> str:
+    t = (transport or os.environ.get("SCA_FABRIC_TRANSPORT") or "").strip().lower()
+    if not t:
+        t = "ipc" if device >= 0 else "shm"
+    if t not in TRANSPORTS:
+        raise ValueError(f"unknown fabric transport {t!r} (one of {', '.join(TRANSPORTS)})")
+    if device < 0 and t != "shm":
+        raise ValueError(f"a CPU gang (device -1) uses the shm transport, not {t!r}")
+    if device >= 0 and t == "shm":
+        t = "ipc"  # GPU ranks: the same mesh, with device slabs
+    return t
+
+
+def gang_device(rank: int, world: int, requested: Optional[int] = None) -> int:
+    """One placement for the whole gang: every rank on its own GPU when there
+    are enough, all on ``requested`` when given (several ranks may share one
+    GPU over the ipc transport), otherwise every rank on the CPU -- never a
+    mix of GPU and CPU ranks."""
+    if requested is not None:
+        return int(requested)
+    n = gpu_count()
+    if n >= world:
+        return int(os.environ.get("LOCAL_RANK", rank))
+    return -1
+
+
+def is_mesh(fabric) -> bool:
+    return fabric is not None and isinstance(fabric, native().Mesh)
+
+
+def init_fabric(device: Optional[int] = None, transport: Optional[str] = None, slots: Optional[int] = None):
     """Create the fabric for the current torch.distributed job: control
-    sockets between rank 0 and every worker, plus (GPU ranks) an RCCL
-    communicator whose unique id is broadcast over the default process group.
-    ``device < 0`` (or no GPU) gives a CPU fabric: the same peer protocol with
-    the payloads on the sockets."""
+    sockets between rank 0 and every worker (liveness, ring names), then the
+    data plane of the chosen transport (see the module doc).  ``device``
+    defaults to ``gang_device``."""
     import torch.distributed as dist
 
     C = native()
     rank, world = dist.get_rank(), dist.get_world_size()
     if device is None:
-        device = int(os.environ.get("LOCAL_RANK", rank)) if gpu_count() > 0 else -1
+        device = gang_device(rank, world)
+    t = fabric_transport(int(device), transport)
     fds = _control_links(rank, world)
-    uid = b""
-    if device >= 0:
-        box = [C.rccl_unique_ids(world) if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        uid = box[0]
-    return C.Fabric(rank, world, uid, int(device), fds)
+    if t in ("ipc", "shm"):
+        k = int(slots or os.environ.get("SCA_FABRIC_SLOTS", "4") or 4)
+        return C.Mesh(rank, world, int(device), fds, k)
+    per_link = 1 if t == "rccl1" else 2
+    box = [C.rccl_unique_ids(world, per_link) if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return C.Fabric(rank, world, box[0], int(device), fds, None, per_link)
 
 
 def loopback_fabrics(world: int, device: int = 0) -> List[Any]:
@@ -146,14 +191,58 @@ def peer_model_for(C, fabric, node: Dict, local_rm, model_id: int):
                             list(local_rm.class_names()), bool(local_rm.flat_output))
 
 
+class MeshServer:
+    """A worker's side of the mesh: its program threads (serve_peer)."""
+
+    def __init__(self, mesh, setup):
+        self.mesh = mesh
+        self.setup = setup
+
+    def join(self) -> None:
+        self.mesh.join()
+
+    def error(self) -> str:
+        return self.mesh.error()
+
+    def stats(self) -> Dict[str, int]:
+        return dict(self.mesh.stats())
+
+    @property
+    def batches(self) -> int:
+        return int(self.mesh.stats()["batches"])
+
+    @property
+    def rows(self) -> int:
+        return int(self.mesh.stats()["rows"])
+
+    @property
+    def max_inflight(self) -> int:
+        return int(self.mesh.stats()["max_inflight"])
+
+    @property
+    def host_syncs(self) -> int:
+        return 0  # the mesh never waits on a device from the host
+
+    @property
+    def slots(self) -> int:
+        return int(self.mesh.slots)
+
+
 def serve_peer(spec: Any, fabric, components: Optional[Dict[str, Any]] = None, predictor: Optional[str] = None):
-    """Worker rank: build the row models of the nodes placed on this rank and
-    serve them until rank 0 stops the fabric.  Returns the started PeerServer."""
+    """Worker rank: build the nodes placed on this rank and serve them until
+    rank 0 stops the fabric.  Returns the started server (``join()``,
+    ``error()``, ``batches``, ``rows``, ``max_inflight``)."""
     from ..serving.deployment import Deployment
 
     sdep = load_spec(spec)
     pred = select_predictor(sdep, predictor)
     res = Deployment.resolver(sdep, components, pred)
+    if is_mesh(fabric):
+        from . import mesh as meshmod
+
+        st = meshmod.setup(fabric, pred["graph"], lambda node: meshmod.stage_info(res, node),
+                           bound=set(components or {}))
+        return MeshServer(fabric, st)
     C = native()
     server = C.PeerServer(fabric)
     for name in rank_assignments(pred["graph"]).get(fabric.rank, []):

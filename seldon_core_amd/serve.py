@@ -31,8 +31,11 @@ hosting that node, see ``seldon_core_amd.parallel.fabric``) runs as ONE graph
 over ``--gpus N`` processes instead of N copies: the supervisor starts the N
 rank processes as a gang (RANK / WORLD_SIZE / MASTER_* like torchrun, every
 GPU visible), rank 0 serves the REST/gRPC front end and the graph, and ranks
-1..N-1 run ``serve_peer`` -- batches cross to them over RCCL (xGMI) or, on
-CPU, sockets.  A rank that dies takes the gang down and the supervisor
+1..N-1 run ``serve_peer`` -- placed subtrees run there as mesh programs (HIP
+IPC + shared memory, or shared memory alone on CPU gangs; RCCL with
+``SCA_FABRIC_TRANSPORT=rccl``).  ``--device D`` puts every rank on GPU D; by
+default each rank gets its own GPU when there are enough, else the gang runs
+on the CPU.  A rank that dies takes the gang down and the supervisor
 restarts all of it (the communicators cannot be re-joined); SIGHUP restarts
 the gang from the current spec.
 
@@ -126,16 +129,14 @@ def run_fabric_worker(args: argparse.Namespace) -> int:
 
     import torch.distributed as dist
 
-    from .parallel.fabric import init_fabric, serve_peer
+    from .parallel.fabric import gang_device, init_fabric, serve_peer
     from .serving.spec import load_spec
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=120))
-    device = args.device
-    if device is None:
-        from ._native import gpu_count
-
-        device = rank if gpu_count() > rank else -1
+    # one placement for the whole gang (never GPU and CPU ranks mixed):
+    # --device D puts every rank on GPU D (ranks share it over the ipc mesh)
+    device = gang_device(rank, world, args.device)
     fabric = init_fabric(device=device)
     if rank == 0:
         return run_worker(args, fabric=fabric)
@@ -163,7 +164,8 @@ def run_fabric_worker(args: argparse.Namespace) -> int:
     fabric.close()
     if err:
         logger.error("rank %d peer loop ended: %s", rank, err)
-    logger.info("rank %d done: %d batches, %d rows", rank, srv.batches, srv.rows)
+    logger.info("rank %d done: %d batches, %d rows, max in flight %d", rank, srv.batches, srv.rows,
+                srv.max_inflight)
     os._exit(0 if not err or stop_requested.is_set() else 1)
 
 

@@ -104,8 +104,29 @@ class Deployment:
         self._row_models: Dict[str, Any] = {}
         self._row_nodes: Dict[str, Dict] = {}
         self.fuse = fuse if fuse is not None else fusion_enabled(self.annotations())
-        for node, _ in iter_nodes(self.predictor["graph"]):
-            self._bind(node)
+        self.mesh = None
+        self._mesh_plan = []
+        remote = set()
+        from ..parallel.fabric import is_mesh
+
+        self._mesh_entered = False
+        try:
+            if is_mesh(fabric):
+                from ..parallel import mesh as meshmod
+
+                self._mesh_plan = meshmod.plan(self.predictor["graph"], bound=set(self.components))
+                remote = {n for p in self._mesh_plan for n in p.absorbed}
+            for node, _ in iter_nodes(self.predictor["graph"]):
+                if node["name"] not in remote:  # placed subtrees are built on their ranks
+                    self._bind(node)
+            if is_mesh(fabric):
+                self._bind_mesh_programs()
+        except Exception as e:
+            if is_mesh(fabric) and not self._mesh_entered:
+                from ..parallel import mesh as meshmod
+
+                meshmod.abort(fabric, f"{type(e).__name__}: {e}")  # the workers wait for rank 0's setup
+            raise
         self._bind_row_models()
         self.engine.finalize()
         self._servers = []
@@ -192,11 +213,6 @@ class Deployment:
         devs = self.replica_devices(node)
         opts = self._batcher_opts(node)
         retries = int(opts.pop("max_retries", 1))
-        if self.fabric is not None and node.get("rank") is not None and devs == [-1]:
-            # CPU fabric: the peer call is asynchronous (RowModel.start_cpu),
-            # so the batcher's device thread keeps `slots` batches outstanding
-            # at the worker instead of one per blocked front-end thread.
-            opts.setdefault("cpu_batching", True)
         if len(devs) == 1:
             return self.C.BatchedUnit(row_model, devs[0], **opts)
         reps = []
@@ -211,13 +227,41 @@ class Deployment:
         self.batched[node["name"]] = unit
         self.units[node["name"]] = unit
 
+    def _bind_mesh_programs(self) -> None:
+        """Rank 0 of a mesh gang: plan + connect every placed subtree (collective
+        with the workers' serve_peer) and serve each as one fused unit whose
+        batches run on the worker ranks (parallel/mesh.py)."""
+        from ..parallel import mesh as meshmod
+
+        mr = int(self.batcher_defaults.get("max_batch", 1024))
+        self._mesh_entered = True
+        st = meshmod.setup(self.fabric, self.predictor["graph"], self._no_local_stage, max_rows=mr,
+                           bound=set(self.components))
+        self.mesh = st
+        nodes = {n["name"]: n for n, _ in iter_nodes(self.predictor["graph"])}
+        for p, pid, fin in zip(st.programs, st.ids, st.finals):
+            pm = self.fabric.program_model(pid, list(fin.get("names") or []), bool(fin.get("flat")))
+            opts = self._batcher_opts(nodes[p.root])
+            opts.pop("max_retries", None)
+            opts.update(cpu_batching=True, slots=int(self.fabric.slots), max_batch=st.max_rows)
+            unit = self.C.BatchedUnit(pm, -1, **opts)
+            self.engine.bind_fused(p.root, unit, p.absorbed)
+            self.batched[p.root] = unit
+            self.units[p.root] = unit
+            logger.info("mesh program %s (%s, %d messages per batch): %s", p.root, self.fabric.transport,
+                        st.messages[st.ids.index(pid)], p.describe())
+
+    @staticmethod
+    def _no_local_stage(node: Dict):
+        raise SpecError([f"node '{node['name']}' is placed on rank 0 inside a remote program"])
+
     def _bind_row_models(self) -> None:
         from ..parallel import device_graph
-        from ..parallel.fabric import peer_model_for, rank_assignments
+        from ..parallel.fabric import is_mesh, peer_model_for, rank_assignments
 
-        # Nodes placed on other ranks (``rank: r``) are served there; here they
-        # become RCCL peer models on this rank's GPU.
-        placed = rank_assignments(self.predictor["graph"])
+        # Nodes placed on other ranks (``rank: r``) are served there; with the
+        # star (RCCL) fabric they become peer models on this rank's GPU.
+        placed = {} if is_mesh(self.fabric) else rank_assignments(self.predictor["graph"])
         for r, names in placed.items():
             if self.fabric is None:
                 if r != 0:
@@ -556,7 +600,7 @@ class Deployment:
             self._span_exporter.close()
             self._span_exporter = None
         if getattr(self, "fabric", None) is not None and self.fabric.rank == 0:
-            self.fabric.stop_peers()  # worker ranks leave their PeerServer loops
+            self.fabric.stop_peers()  # worker ranks leave their serve loops
             self.fabric = None
 
     def __enter__(self):

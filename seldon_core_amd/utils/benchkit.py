@@ -14,7 +14,7 @@ front end, plus the pieces ``bench.py`` needs to run it robustly on a node of
 * :class:`Children` -- every child process in its own process group, killed
   as a group on timeout or when the watchdog fires;
 * the workloads, graph builders (one process driving N GPUs, or nodes placed
-  on ranks behind the RCCL fabric), the load generator wrapper with a sampled
+  on worker ranks behind the fabric), the load generator wrapper with a sampled
   reply-body check, the CPU-oracle self check and placement reports.
 """
 from __future__ import annotations
@@ -339,7 +339,7 @@ def build_graph(wl: Workload, kind: str, devs: List[int], reward_branch: Optiona
 def build_rank_graph(wl: Workload, kind: str, world: int):
     """(graph, components, oracle, label) of a graph whose nodes are placed on
     torch.distributed ranks (``rank: r`` -- one engine process per GPU, the
-    nodes of other ranks reached over the RCCL p2p fabric):
+    nodes of other ranks reached over the fabric: mesh programs by default):
 
     * ``abtest``   -- router + replica a on rank 0, replica b on rank 1;
     * ``pipeline`` -- scaler on rank 3 -> combiner on rank 0 over a (rank 1), b (rank 2);
@@ -355,14 +355,14 @@ def build_rank_graph(wl: Workload, kind: str, world: int):
         g = {"name": "ab", "type": "ROUTER", "implementation": "RANDOM_ABTEST",
              "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
              "children": [{"name": "a", "type": "MODEL", "rank": 0}, {"name": "b", "type": "MODEL", "rank": 1}]}
-        return g, {"a": rm, "b": rm.clone()}, wl.oracle, "RANDOM_ABTEST: a on rank 0, b on rank 1 (RCCL)"
+        return g, {"a": rm, "b": rm.clone()}, wl.oracle, "RANDOM_ABTEST: a on rank 0, b on rank 1 (mesh)"
     if kind == "pipeline":
         tr, scale = _scaler(C, len(wl.row))
         g = {"name": "scaler", "type": "TRANSFORMER", "rank": 3, "children": [
             {"name": "combiner", "type": "COMBINER", "implementation": "AVERAGE_COMBINER",
              "children": [{"name": "a", "type": "MODEL", "rank": 1}, {"name": "b", "type": "MODEL", "rank": 2}]}]}
         return (g, {"scaler": tr, "a": rm, "b": rm.clone()}, lambda X: wl.oracle(np.asarray(X) * scale),
-                "scaler (rank 3) -> AVERAGE_COMBINER (rank 0) over a (rank 1), b (rank 2) (RCCL)")
+                "scaler (rank 3) -> AVERAGE_COMBINER (rank 0) over a (rank 1), b (rank 2) (mesh)")
     if kind == "mab":
         from ..components.routers import EpsilonGreedy
 
@@ -370,7 +370,7 @@ def build_rank_graph(wl: Workload, kind: str, world: int):
         comps = {f"m{r}": (rm if r == 0 else rm.clone()) for r in range(world)}
         comps["mab"] = EpsilonGreedy(n_branches=world, epsilon=0.1, seed=1)
         g = {"name": "mab", "type": "ROUTER", "children": kids}
-        return g, comps, wl.oracle, f"EPSILON_GREEDY router (rank 0) over replicas on ranks 0..{world - 1} (RCCL)"
+        return g, comps, wl.oracle, f"EPSILON_GREEDY router (rank 0) over replicas on ranks 0..{world - 1} (mesh)"
     raise ValueError(kind)
 
 

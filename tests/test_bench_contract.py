@@ -51,7 +51,7 @@ def test_bench_two_ranks_torchrun_cpu():
     assert line["self_check"]["ok"] and line["self_check"]["sampled_replies_checked"] > 0
     assert set(line["step_ms"]) == {"min", "median", "max"}
     v = line["variants"]
-    assert set(v) == {"abtest", "mab", "replicas", "reuseport", "abtest_rccl", "mab_rccl"}  # pipeline needs 4
+    assert set(v) == {"abtest", "mab", "replicas", "reuseport", "abtest_ranks", "mab_ranks"}  # pipeline needs 4
     rp = v["reuseport"]  # serve --gpus 2: two workers on one SO_REUSEPORT port
     assert rp["workers"] == 2 and set(rp["per_worker_requests"]) == {"0", "1"}, rp
     assert sum(rp["per_worker_requests"].values()) > 0 and rp["balance_min_over_max"] > 0, rp
@@ -61,9 +61,10 @@ def test_bench_two_ranks_torchrun_cpu():
     assert set(v["abtest"]["placement"]) == {"ab", "a", "b"}
     assert v["replicas"]["placement"]["classifier"] == [-1, -1]
     assert v["mab"]["feedback"]["rps"] > 0 and v["mab"]["feedback"]["rewarded_branch"] == 1
-    rc = v["mab_rccl"]
-    assert rc["data_plane"] == "sockets" and rc["fabric_world"] == 2
-    assert rc["unit_kinds"]["m1"] == "gpu:rccl_peer"
+    rc = v["mab_ranks"]
+    assert rc["data_plane"] == "shm" and rc["fabric_world"] == 2
+    assert rc["unit_kinds"]["m1"] == "gpu:mesh_program"
+    assert rc["mesh_programs"] == [{"root": "m1", "stages": "s0=node:m1@rank1(in)", "messages_per_batch": 2}]
     assert rc["worker_ranks"]["1"]["batches"] > 0 and rc["worker_ranks"]["1"]["error"] == ""
     # the bandit learned the rewarded remote branch: most batches crossed the fabric
     b = rc["rank0_batches_per_unit"]
@@ -77,7 +78,7 @@ def test_bench_direct_launch_hang_in_variants_is_bounded():
     Both are killed at their deadlines; rc 0 within the budget, the headline
     and the other variants stand, the hung ones read "timeout"."""
     budget = 150
-    env = _cpu_env(SCA_BENCH_FAULT="hang:mab:0,hang:mab_rccl:1", SCA_BENCH_BUDGET_S=str(budget),
+    env = _cpu_env(SCA_BENCH_FAULT="hang:mab:0,hang:mab_ranks:1", SCA_BENCH_BUDGET_S=str(budget),
                    SCA_BENCH_VARIANT_CAP_S="20")
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--step-requests", "1000",
            "--users", "16", "--variants", "abtest,mab", "--rank-variants", "abtest,mab"]
@@ -95,8 +96,8 @@ def test_bench_direct_launch_hang_in_variants_is_bounded():
     v = line["variants"]
     assert v["mab"]["error"] == "timeout", v["mab"]
     assert v["abtest"].get("self_check", {}).get("ok"), v["abtest"]
-    assert v["abtest_rccl"].get("self_check", {}).get("ok"), v["abtest_rccl"]
-    assert "error" in v["mab_rccl"], v["mab_rccl"]
+    assert v["abtest_ranks"].get("self_check", {}).get("ok"), v["abtest_ranks"]
+    assert "error" in v["mab_ranks"], v["mab_ranks"]
 
 
 def test_bench_watchdog_prints_line_when_main_thread_hangs():

@@ -1,7 +1,8 @@
-"""Cross-rank placement (fabric).  The peer protocol runs here end to end on
-CPU fabrics (gloo rendezvous, control + data over sockets, device -1) through
-the real native PeerRowModel / PeerServer state machines; the RCCL data plane
-is exercised by tools/fabric_probe.py under torchrun on GPU boxes."""
+"""Cross-rank placement.  The mesh (csrc/parallel/mesh.h) runs here end to end
+on CPU gangs (gloo rendezvous, shared-memory slabs and doorbells, device -1):
+separate processes, the real native program threads on the workers and the
+program units on rank 0.  tests/test_mesh_gpu.py runs the same modes with every
+rank on GPU 0 over HIP IPC."""
 import json
 import os
 import socket
@@ -88,15 +89,15 @@ def _run_ranks(world, mode, **extra_env):
 def test_remote_model_node_cpu_fabric(world):
     outs = _run_ranks(world, "single")
     front = outs[0]
-    assert front["worst"] < 1e-12 and front["rows"] > 0
+    assert front["errors"] == [] and front["worst"] < 1e-12 and front["rows"] > 0, front
+    assert front["transport"] == "shm" and front["messages"] == [2], front
     last = outs[-1]
     assert last["error"] == "" and last["rows"] == front["rows"] and last["batches"] >= 1
-    assert last["host_syncs"] == 0  # CPU loop never waits on a device
 
 
 def test_remote_model_low_cpu_batcher_cpu_fabric():
-    """The batcher's low-CPU mode waits on the peer's link socket (ppoll)
-    instead of sleeping between polls: same answers, same row counts."""
+    """The batcher's low-CPU mode (blocking waits on the program's reply
+    flags instead of spinning): same answers, same row counts."""
     outs = _run_ranks(2, "single", SCA_TEST_LOW_CPU="1")
     assert outs[0]["worst"] < 1e-12 and outs[0]["rows"] > 0
     assert outs[1]["error"] == "" and outs[1]["rows"] == outs[0]["rows"]
@@ -104,22 +105,72 @@ def test_remote_model_low_cpu_batcher_cpu_fabric():
 
 def test_combiner_gathers_from_every_rank_cpu_fabric():
     outs = _run_ranks(3, "combiner")
-    assert outs[0]["worst"] < 1e-12
+    assert outs[0]["errors"] == [] and outs[0]["worst"] < 1e-12
+    assert outs[0]["messages"] == [2, 2], outs[0]  # m1 and m2: one program each, m0 local
     for w in outs[1:]:
         assert w["error"] == "" and w["rows"] == outs[0]["rows"]
 
 
+def test_remote_combiner_is_one_program_with_the_mean_on_rank0():
+    outs = _run_ranks(3, "remote_combiner")
+    front = outs[0]
+    assert front["errors"] == [] and front["worst"] < 1e-12, front
+    assert front["messages"] == [4] and "mean:comb@rank0" in front["programs"][0], front
+    for w in outs[1:]:
+        assert w["error"] == "" and w["rows"] == front["rows"]
+
+
+def test_pipeline_stages_hand_off_directly():
+    """scaler@1 -> scaler@2 -> iris@3: each stage sends its rows straight to
+    the next rank; 4 messages per batch (0->1, 1->2, 2->3, 3->0), not the 6 of
+    a round trip through rank 0 per stage."""
+    outs = _run_ranks(4, "pipeline")
+    front = outs[0]
+    assert front["errors"] == [] and front["worst"] < 1e-12 and front["rows"] > 0, front
+    assert front["messages"] == [4], front
+    assert front["kinds"]["s1"].startswith("gpu:mesh_program"), front["kinds"]
+    for w in outs[1:]:
+        assert w["error"] == "" and w["rows"] == front["rows"], w
+
+
+def test_bench_pipeline_dag_fans_out_from_the_scaler_rank():
+    outs = _run_ranks(4, "dag")
+    front = outs[0]
+    assert front["errors"] == [] and front["worst"] < 1e-12, front
+    assert front["messages"] == [5], front  # 0->3, 3->1, 3->2, 1->0, 2->0
+    for w in outs[1:]:
+        assert w["error"] == "" and w["rows"] == front["rows"], w
+
+
+def test_python_transformer_on_a_worker_rank():
+    """Any node on any rank: a Python TRANSFORMER on rank 1 feeds the iris
+    row model on rank 2."""
+    outs = _run_ranks(3, "python")
+    front = outs[0]
+    assert front["errors"] == [] and front["worst"] < 1e-12 and front["rows"] > 0, front
+    assert "node:double@rank1" in front["programs"][0] and front["messages"] == [3], front
+    for w in outs[1:]:
+        assert w["error"] == "" and w["rows"] == front["rows"], w
+
+
+def test_failing_python_stage_fails_only_its_requests():
+    outs = _run_ranks(3, "python_error")
+    front = outs[0]
+    assert front["errors"] == [] and front["failed"] == 8 and front["worst"] < 1e-12, front
+    assert outs[1]["stage_errors"] >= 1 and outs[1]["error"] == "", outs[1]
+
+
 def test_native_fabric_api_present():
     C = sca.native()
-    for name in ("rccl_unique_ids", "Fabric", "LoopbackHub", "PeerServer", "peer_row_model"):
+    for name in ("rccl_unique_ids", "Fabric", "LoopbackHub", "PeerServer", "peer_row_model", "Mesh"):
         assert hasattr(C, name)
 
 
-def test_concurrent_senders_keep_k_batches_in_flight_cpu_fabric():
-    """4 concurrent senders x 3 ranks, K = 4 slots per worker: every answer
-    (single peers and the broadcast/gather fan-out) matches sklearn to 1e-12,
-    and the workers really held more than one batch in flight (headers come
-    through the shared-memory ring, payloads are read ahead of compute)."""
+def test_concurrent_clients_keep_several_batches_in_flight_cpu_fabric():
+    """4 client threads through an A/B router over two remote programs, the
+    workers slowed down (SCA_FABRIC_WORKER_DELAY_US): every answer matches
+    sklearn to 1e-12 and the workers held more than one batch at a time
+    (rank 0 issues up to K = 4 batches per program ahead)."""
     outs = _run_ranks(3, "concurrent", SCA_FABRIC_SLOTS="4", SCA_FABRIC_WORKER_DELAY_US="3000")
     front = outs[0]
     assert front["errors"] == [] and front["worst"] < 1e-12 and front["rows"] > 0, front
@@ -128,14 +179,36 @@ def test_concurrent_senders_keep_k_batches_in_flight_cpu_fabric():
         assert 2 <= w["max_inflight"] <= 4, w
 
 
-def test_large_replies_arrive_in_pieces_cpu_fabric():
+def test_large_and_wide_batches_cpu_fabric():
+    """3000-row requests through 64-row slots (the request is split into
+    chunks, more chunks than slots) and 784-column outputs."""
     outs = _run_ranks(2, "large")
-    assert outs[0]["errors"] == [] and outs[0]["worst"] < 1e-12, outs[0]
-    assert outs[1]["error"] == "" and outs[1]["rows"] >= 3 * 60000, outs[1]
+    assert outs[0]["errors"] == [] and outs[0]["worst"] < 1e-9, outs[0]
+    assert outs[1]["error"] == "" and outs[1]["rows"] == outs[0]["rows"], outs[1]
 
 
-def test_header_ring_liveness_worker_exits_when_front_end_dies():
-    """A worker polling its header ring notices rank 0's death (control
-    socket EOF) and leaves with an error instead of spinning forever."""
+def test_worker_exits_when_front_end_dies():
+    """A worker polling its rings notices rank 0's death (control socket
+    EOF) and leaves with an error instead of spinning forever."""
     outs = _run_ranks(2, "orphan")
     assert "gone" in outs[1]["error"] or "closed" in outs[1]["error"], outs[1]
+
+
+def test_placed_router_is_rejected():
+    from seldon_core_amd.parallel.mesh import plan
+
+    g = {"name": "r", "type": "ROUTER", "rank": 1, "children": [{"name": "m", "type": "MODEL", "rank": 2}]}
+    with pytest.raises(SpecError, match="cannot be placed"):
+        plan(g)
+
+
+def test_plan_places_inner_means_on_their_consumer():
+    from seldon_core_amd.parallel.mesh import plan
+
+    g = {"name": "post", "type": "OUTPUT_TRANSFORMER", "rank": 3, "children": [
+        {"name": "comb", "type": "COMBINER", "implementation": "AVERAGE_COMBINER",
+         "children": [{"name": "a", "type": "MODEL", "rank": 1}, {"name": "b", "type": "MODEL", "rank": 2}]}]}
+    (p,) = plan(g)
+    assert [(s.node, s.kind, s.rank, s.inputs) for s in p.stages] == [
+        ("a", "node", 1, [-1]), ("b", "node", 2, [-1]), ("comb", "mean", 3, [0, 1]), ("post", "node", 3, [2])]
+    assert p.absorbed == ["post", "comb", "a", "b"]

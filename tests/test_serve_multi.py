@@ -20,6 +20,7 @@ import time
 import urllib.request
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -36,15 +37,16 @@ def _post(port, path, body, timeout=10):
     return json.loads(urllib.request.urlopen(req, timeout=timeout).read())
 
 
-def _start(tmp_path, spec, n, extra=(), env_extra=None):
+def _start(tmp_path, spec, n, extra=(), env_extra=None, device=-1):
     sp = tmp_path / "spec.json"
     sp.write_text(json.dumps(spec))
     hp, gp = _free_port(), _free_port()
     log = open(tmp_path / "serve.log", "w")
-    env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, str(tmp_path)]), CUDA_VISIBLE_DEVICES="",
-               **(env_extra or {}))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, str(tmp_path)]), **(env_extra or {}))
+    if device < 0:
+        env["CUDA_VISIBLE_DEVICES"] = ""
     p = subprocess.Popen([sys.executable, "-m", "seldon_core_amd.serve", "--spec", str(sp), "--gpus", str(n),
-                          "--device", "-1", "--http-port", str(hp), "--grpc-port", str(gp), "--admin-port", "0",
+                          "--device", str(device), "--http-port", str(hp), "--grpc-port", str(gp), "--admin-port", "0",
                           "--threads", "2", "--log-level", "INFO", *extra],
                          env=env, cwd=ROOT, start_new_session=True, stdout=log, stderr=subprocess.STDOUT)
     return p, hp, tmp_path / "serve.log"
@@ -117,7 +119,7 @@ def test_rank_placed_spec_serves_through_the_cli(tmp_path):
     try:
         assert _wait_log(log, "serving p:", 1), log.read_text()[-3000:]
         text = log.read_text()
-        assert "rccl_peer" in text, text[-2000:]  # rank 0 reaches a and b through the fabric
+        assert "mesh_program" in text, text[-2000:]  # rank 0 reaches a and b through the mesh
         from seldon_core_amd.models import iris_logistic_regression
 
         lr = iris_logistic_regression()
@@ -142,3 +144,90 @@ def test_rank_placement_needs_enough_gpus(tmp_path):
     p, _, log = _start(tmp_path, spec, 2)
     assert p.wait(timeout=60) == 2
     assert "places nodes on 4 ranks" in log.read_text()
+
+
+MYMODELS = (
+    "import numpy as np\n"
+    "from seldon_core_amd.models import iris_logistic_regression\n"
+    "from seldon_core_amd.servers import SKLearnServer\n\n"
+    "SCALE = 1.0 + 0.05 * np.arange(4)\n\n\n"
+    "class Iris(SKLearnServer):\n"
+    "    def __init__(self):\n"
+    "        super().__init__(model=iris_logistic_regression())\n\n\n"
+    "class Scaler:\n"
+    "    def row_model(self):\n"
+    "        import seldon_core_amd as sca\n"
+    "        return sca.native().linear_model(np.diag(SCALE), np.zeros(4), 0)\n")
+
+
+def _gang_spec(kind):
+    if kind == "abtest":
+        g = {"name": "ab", "type": "ROUTER", "implementation": "RANDOM_ABTEST",
+             "parameters": [{"name": "ratioA", "value": "0.5", "type": "FLOAT"}],
+             "children": [{"name": "a", "type": "MODEL", "rank": 1}, {"name": "b", "type": "MODEL", "rank": 2}]}
+        return g, 3, ("a=mymodels.Iris", "b=mymodels.Iris"), 1.0
+    if kind == "mab":
+        g = {"name": "mab", "type": "ROUTER", "implementation": "EPSILON_GREEDY",
+             "parameters": [{"name": "n_branches", "value": "2", "type": "INT"},
+                            {"name": "epsilon", "value": "0.5", "type": "FLOAT"}],
+             "children": [{"name": "m1", "type": "MODEL", "rank": 1}, {"name": "m2", "type": "MODEL", "rank": 2}]}
+        return g, 3, ("m1=mymodels.Iris", "m2=mymodels.Iris"), 1.0
+    g = {"name": "scaler", "type": "TRANSFORMER", "rank": 3, "children": [
+        {"name": "comb", "type": "COMBINER", "implementation": "AVERAGE_COMBINER",
+         "children": [{"name": "a", "type": "MODEL", "rank": 1}, {"name": "b", "type": "MODEL", "rank": 2}]}]}
+    return g, 4, ("scaler=mymodels.Scaler", "a=mymodels.Iris", "b=mymodels.Iris"), 1.0 + 0.05 * np.arange(4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["abtest", "mab", "pipeline"])
+def test_rank_placed_gang_on_one_gpu_over_ipc(tmp_path, kind):
+    """serve --gpus N --device 0: N rank processes, each with its own HIP
+    context on GPU 0, serve one rank-placed graph over the ipc mesh; answers
+    match sklearn to 1e-12 and the workers keep several batches in flight."""
+    from seldon_core_amd._native import gpu_count
+
+    if gpu_count() < 1:
+        pytest.skip("needs a GPU")
+    import threading
+
+    from seldon_core_amd.models import iris_logistic_regression
+
+    (tmp_path / "mymodels.py").write_text(MYMODELS)
+    graph, n, comps, scale = _gang_spec(kind)
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}], "graph": graph}
+    extra = []
+    for c in comps:
+        extra += ["--component", c]
+    p, hp, log = _start(tmp_path, spec, n, extra=extra, device=0,
+                        env_extra={"SCA_FABRIC_WORKER_DELAY_US": "1500", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    lr = iris_logistic_regression()
+    errs, worst = [], [0.0]
+    try:
+        assert _wait_log(log, "serving p:", 1, timeout=150), log.read_text()[-3000:]
+        text = log.read_text()
+        assert "mesh program" in text and "(ipc," in text, text[-3000:]
+
+        def client(t):
+            rng = np.random.default_rng(t)
+            for i in range(25):
+                X = rng.normal(loc=4.0, scale=1.5, size=(1 + (i + t) % 4, 4))
+                try:
+                    out = _post(hp, "/api/v0.1/predictions", {"data": {"ndarray": X.tolist()}}, timeout=30)
+                    err = float(np.abs(np.asarray(out["data"]["ndarray"]) - lr.predict_proba(X * scale)).max())
+                    worst[0] = max(worst[0], err)
+                except Exception as e:  # noqa: BLE001
+                    errs.append(repr(e))
+
+        th = [threading.Thread(target=client, args=(t,)) for t in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert errs == [] and worst[0] < 1e-12, (errs[:3], worst[0])
+        assert _stop(p) == 0
+    finally:
+        _stop(p)
+    text = log.read_text()
+    done = [ln for ln in text.splitlines() if " done: " in ln and "max in flight" in ln]
+    assert len(done) == n - 1, text[-3000:]
+    assert max(int(ln.rsplit("max in flight ", 1)[1].split()[0]) for ln in done) >= 2, done
