@@ -649,7 +649,7 @@ __device__ void topk_wave(double* __restrict__ A, double* __restrict__ V, double
 // descending eigenvalue into V (columns; sel = 0..k-1) and cached with their
 // eigenvalues for the eigen-tracking path (rank1_eigen).
 constexpr int kJacobiRefresh = 256;   // Jacobi-only mode: cold solve period
-constexpr int kTrackRefresh = 1024;   // eigen-tracking mode: cold solve period
+constexpr int kTrackRefresh = 1024;   // eigen-tracking mode: Newton-Schulz re-orthogonalisation period
 constexpr int kTrackMaxRows = 16;     // requests with more rows re-solve by Jacobi
 constexpr bool kMahaMfmaGemm = true;  // eigen-tracking V Q on v_mfma_f64_16x16x4
 
@@ -804,6 +804,37 @@ __device__ __forceinline__ void jacobi_solve(double* __restrict__ A, double* __r
 // on any of the top-k pairs (which also catches a stale cache).  A numpy
 // prototype over 1,000 steps stayed within 6e-15 of eigh's eigenvalues and
 // 1e-13 of its top-k subspace at p = 9, 32, 64.
+// Z[M x N] = op(X) Y on the f64 matrix cores (v_mfma_f64_16x16x4: lane l
+// holds X[l&15][k = l>>4] and Y[k = l>>4][l&15], result rows (l>>4) + 4i of
+// column l&15), 16x16 tiles over the workgroup's waves; op(X) = X^T when
+// TRANS.  Operands live in LDS with row strides ldx / ldy; k past K is fed
+// as zeros, rows / columns past M / N read in-bounds LDS whose results are
+// not stored.
+template <int NT, bool TRANS>
+__device__ void mfma_gemm_lds(const double* __restrict__ X, int ldx, const double* __restrict__ Y, int ldy,
+                              double* __restrict__ Z, int ldz, int M, int N, int K) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
+  const int tr = (M + 15) >> 4, tc = (N + 15) >> 4;
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  for (int t = wave; t < tr * tc; t += NT / 64) {
+    const int r0 = (t / tc) * 16, c0 = (t - (t / tc) * tc) * 16;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < K; k0 += 4) {
+      const int kk = k0 + lk;
+      const double a = kk < K ? (TRANS ? X[kk * ldx + r0 + li] : X[(r0 + li) * ldx + kk]) : 0.0;
+      const double b = kk < K ? Y[kk * ldy + c0 + li] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    const int col = c0 + li;
+    if (col < N)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = r0 + lk + 4 * i;
+        if (row < M) Z[row * ldz + col] = acc[i];
+      }
+  }
+}
+
 template <int NT>
 __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, double rho, int p, int k,
                             const double* __restrict__ Cn, double* __restrict__ A, double* __restrict__ V,
@@ -1176,6 +1207,32 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   }
   __syncthreads();
   if (!last) return true;  // the next row's update starts from this basis
+  // ---- every kTrackRefresh-th tracked step: one Newton-Schulz step
+  // V <- V (3I - V^T V) / 2, which takes V's orthogonality error e to O(e^2)
+  // (products of Gu-Eisenstat Q's drift by ~eps per step).  It replaces the
+  // periodic cold Jacobi re-solve (2 ms at p = 64, 25x a tracked step:
+  // profiles/r04c_maha) at the cost of two p^3 MFMA products; the residual
+  // check below then validates the refreshed basis, and a failure still
+  // falls back to Jacobi.
+  const bool refresh = tail[1] + 1.0 >= double(kTrackRefresh);  // (uniform: every thread reads the same word)
+  if (refresh) {
+    mfma_gemm_lds<NT, true>(V, kLd, V, kLd, W, kLd, p, p, p);  // G = V^T V
+    __syncthreads();
+    for (int e = tid; e < p * p; e += NT) {
+      const int r = e / p, c = e - r * p;
+      W[r * kLd + c] = (r == c ? 1.5 : 0.0) - 0.5 * W[r * kLd + c];
+    }
+    __syncthreads();
+    mfma_gemm_lds<NT, false>(V, kLd, W, kLd, A, kLdA, p, p, p);  // V (3I - G) / 2
+    __syncthreads();
+    for (int e = tid; e < p * p; e += NT) {
+      const int r = e / p, c = e - r * p;
+      const double v = A[r * kLdA + c];
+      V[r * kLd + c] = v;
+      cache[r * p + c] = v;
+    }
+    __syncthreads();
+  }
   // ---- residual of the top-k pairs against the new covariance, R = C_new
   // V[:, 0:16] on the f64 matrix cores (one 16-row tile per wave; columns
   // past k and rows past p are computed but not summed)
@@ -1211,7 +1268,7 @@ __device__ bool rank1_eigen(const double* __restrict__ dvec, double alpha, doubl
   }
   if (tid < p) lam_cache[tid] = lam_sorted[tid];
   if (tid < k) sel[tid] = tid;
-  if (tid == 0) tail[1] += 1.0;  // steps since the last cold solve (tail[0] = p already)
+  if (tid == 0) tail[1] = refresh ? 0.0 : tail[1] + 1.0;  // steps since the last refresh (tail[0] = p already)
   __syncthreads();
   mark(9);
   return true;
@@ -1457,7 +1514,7 @@ __device__ void maha_one(const double* __restrict__ X, int nb, const MahaParams&
     // words (global memory) and broadcast, so every wave takes it or none.
     if (tid == 0)
       track = p <= prm.rank1_max_p && nb <= kTrackMaxRows && !c_zero && tail[0] == double(p) &&
-               tail[1] < double(kTrackRefresh) && eig[kMahaEigMeta] == n_state;
+               eig[kMahaEigMeta] == n_state;  // (the periodic refresh happens inside the tracked step)
     __syncthreads();
     if (track) {
       // C_new = alpha C_old + sum_i c_i / den d_i d_i^T: one rank-1 update per row

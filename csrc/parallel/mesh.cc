@@ -3,8 +3,12 @@
 #include <fcntl.h>
 #include <immintrin.h>
 #include <sys/mman.h>
+#include <linux/futex.h>
 #include <sys/socket.h>
+#include <sys/syscall.h>
 #include <unistd.h>
+
+#include <climits>
 
 #include <algorithm>
 #include <cerrno>
@@ -51,13 +55,29 @@ struct Layout {
   std::vector<char> on_dev;   // per source: in the device slab allocation (GPU gangs, worker -> worker)
   std::vector<size_t> off;    // per source: slot 0's offset (region or device allocation)
   std::vector<size_t> slab;   // per source: bytes per slot
-  size_t ring_off = 0, flags_off = 0, err_off = 0, bytes = 0, dev_bytes = 0;
+  size_t ring_off = 0, bell_off = 0, flags_off = 0, err_off = 0, bytes = 0, dev_bytes = 0;
   int index_of(int s) const {
     for (size_t i = 0; i < src.size(); ++i)
       if (src[i] == s) return int(i);
     return -1;
   }
 };
+
+// A region's futex doorbell: every host store into the region (a ready or
+// freed flag, a ring header) bumps `seq` and wakes the sleepers, so host
+// waiters on host-written flags sleep in the kernel instead of spinning.
+// Flags written by a GPU (stream write-value) cannot ring it: their waiters
+// poll.
+struct Bell {
+  std::atomic<uint32_t> seq;
+  std::atomic<uint32_t> sleepers;
+};
+
+void bell_ring(Bell* b) {
+  b->seq.fetch_add(1, std::memory_order_seq_cst);  // (full barrier: the flag store is visible first)
+  if (b->sleepers.load(std::memory_order_seq_cst) != 0)
+    syscall(SYS_futex, reinterpret_cast<uint32_t*>(&b->seq), FUTEX_WAKE, INT_MAX, nullptr, nullptr, 0);
+}
 
 struct Region {
   char* host = nullptr;  // the mapping
@@ -110,6 +130,7 @@ struct Prog {
   uint64_t taken = 0;                     // headers taken from the ring
 
   HeaderRing* ring(int r) const { return reinterpret_cast<HeaderRing*>(reg[size_t(r)].host + lay[size_t(r)].ring_off); }
+  Bell* bell(int r) const { return reinterpret_cast<Bell*>(reg[size_t(r)].host + lay[size_t(r)].bell_off); }
   char* flag(int r, int k, int e) const {
     const Layout& L = lay[size_t(r)];
     return reg[size_t(r)].host + L.flags_off + (size_t(k) * (L.src.size() + 2) + size_t(e)) * kLine;
@@ -159,6 +180,7 @@ struct Mesh::Impl {
   bool prepared = false, connected = false, started = false;
   int timeout_ms = 60000;
   int delay_us = 0;
+  int spin_us = 20;
   mutable std::mutex err_mu;
   std::string err;
   std::atomic<uint64_t> batches{0}, rows{0}, max_inflight{0}, host_waits{0}, stage_errors{0};
@@ -175,34 +197,51 @@ struct Mesh::Impl {
 
 // ------------------------------------------------------------------ waiting
 namespace {
-// Spin through the usual few-microsecond hand-off, then yield, then sleep
-// (an idle program must not burn a core); `check` runs in the sleeping phase
-// and throws when the wait is hopeless (peer gone, mesh closed, timeout).
+// Wait for ready(): spin for `spin_us` (the usual back-to-back hand-off),
+// then -- when the flag's writer is a host thread that rings `bell` -- sleep
+// on the region's futex in 1 ms slices, else (a GPU writes the flag) yield
+// for 200 us and then sleep 20 us at a time.  `check(elapsed)` runs between
+// slices and throws when the wait is hopeless (peer gone, mesh closed,
+// timeout).  Returns whether it had to wait at all.
 template <class Ready, class Check>
-bool wait_until(Ready ready, Check check) {
-  int spins = 0;
-  clk::time_point t0{};
-  bool waited = false;
+bool wait_ready(Ready ready, Check check, Bell* bell, int spin_us) {
+  if (ready()) return false;
+  const auto t0 = clk::now();
+  const auto spin = std::chrono::microseconds(spin_us);
+  do {
+    for (int i = 0; i < 32; ++i) _mm_pause();
+    if (ready()) return true;
+  } while (clk::now() - t0 < spin);
+  if (bell) {
+    while (true) {
+      const uint32_t s = bell->seq.load(std::memory_order_seq_cst);
+      bell->sleepers.fetch_add(1, std::memory_order_seq_cst);
+      if (ready()) {
+        bell->sleepers.fetch_sub(1, std::memory_order_seq_cst);
+        return true;
+      }
+      const timespec ts{0, 1000000};
+      syscall(SYS_futex, reinterpret_cast<uint32_t*>(&bell->seq), FUTEX_WAIT, s, &ts, nullptr, 0);
+      bell->sleepers.fetch_sub(1, std::memory_order_seq_cst);
+      if (ready()) return true;
+      check(clk::now() - t0);
+    }
+  }
   while (!ready()) {
-    waited = true;
-    if (spins < 4096) {
-      ++spins;
-      _mm_pause();
-      continue;
-    }
-    if (spins == 4096) {
-      ++spins;
-      t0 = clk::now();
-    }
     const auto dt = clk::now() - t0;
-    if (dt < std::chrono::microseconds(200)) {
+    if (dt < spin + std::chrono::microseconds(200)) {
       std::this_thread::yield();
     } else {
       check(dt);
       std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
-  return waited;
+  return true;
+}
+
+template <class Ready, class Check>
+bool wait_until(Ready ready, Check check) {
+  return wait_ready(ready, check, nullptr, 20);
 }
 }  // namespace
 
@@ -214,6 +253,7 @@ Mesh::Mesh(int rank, int world, int device, std::vector<int> ctrl_fds, int slots
   if (int(fds_.size()) != world) throw std::runtime_error("Mesh: need one control socket slot per rank");
   im_->timeout_ms = std::max(100, env_int("SCA_MESH_TIMEOUT_MS", 60000));
   im_->delay_us = std::max(0, env_int("SCA_FABRIC_WORKER_DELAY_US", 0));
+  im_->spin_us = std::max(0, env_int("SCA_MESH_SPIN_US", 20));
 }
 
 Mesh::~Mesh() {
@@ -294,6 +334,8 @@ int Mesh::add_program(MeshProgram d) {
       L.ring_off = 0;
       cur = align_up(sizeof(HeaderRing), kLine);
     }
+    L.bell_off = cur;
+    cur += kLine;
     L.flags_off = cur;
     cur += size_t(K_) * (L.src.size() + 2) * kLine;
     L.err_off = cur;
@@ -539,46 +581,60 @@ struct WorkerCtx {
   Prog* P;
   int me, K;
   const std::vector<int>* fds;
-  // Bounded host wait for a flag of another process.
-  void wait_flag(const char* f, uint64_t v, const char* what) {
-    const bool waited = wait_until([&] { return load_acq(f) >= v; },
+  // Bounded host wait for a flag of another process; `bell`: the region's
+  // doorbell when a host thread writes the flag (else polled).
+  void wait_flag(const char* f, uint64_t v, const char* what, Bell* bell) {
+    const bool waited = wait_ready([&] { return load_acq(f) >= v; },
                                    [&](clk::duration dt) {
                                      if (!m->open()) throw std::runtime_error("mesh closed");
                                      if (fd_gone((*fds)[0])) throw std::runtime_error("mesh: rank 0 is gone");
                                      if (dt > std::chrono::milliseconds(im->timeout_ms))
                                        throw std::runtime_error(std::string("mesh: no ") + what + " within " +
                                                                 std::to_string(im->timeout_ms) + " ms");
-                                   });
+                                   },
+                                   bell, im->spin_us);
     if (waited) im->host_waits.fetch_add(1, std::memory_order_relaxed);
+  }
+  // A remote stage's output for this rank (written by the producer's host
+  // on CPU gangs, by its GPU on GPU gangs).
+  void wait_input(int k, int j, uint64_t seq) {
+    wait_flag(P->ready(me, k, j), seq, "stage input", m->gpu() ? nullptr : P->bell(me));
   }
   uint64_t credit(int c, int k) const {
     const auto a = P->alias[size_t(c)];
     return a.first >= 0 ? load_acq(P->ready(a.first, k, a.second)) : load_acq(P->freed(c, k));
   }
-  const char* credit_flag(int c, int k) const {
-    const auto a = P->alias[size_t(c)];
-    return a.first >= 0 ? P->ready(a.first, k, a.second) : P->freed(c, k);
-  }
   void wait_credit(int c, int k, uint64_t seq) {
     if (seq <= uint64_t(K)) return;
-    wait_flag(credit_flag(c, k), seq - uint64_t(K), "slot credit");
+    const auto a = P->alias[size_t(c)];
+    const int region = a.first >= 0 ? a.first : c;
+    const char* f = a.first >= 0 ? P->ready(a.first, k, a.second) : P->freed(c, k);
+    // rank 0 frees its own slots from the host; workers of a GPU gang from their streams
+    Bell* b = (!m->gpu() || (a.first < 0 && c == 0)) ? P->bell(region) : nullptr;
+    wait_flag(f, seq - uint64_t(K), "slot credit", b);
   }
   uint64_t completed() const {
     uint64_t mx = 0;
     for (int k = 0; k < K; ++k) mx = std::max(mx, credit(me, k));
     return mx;
   }
+  // Host store of a flag in rank r's region, then its doorbell.
+  void host_flag(int r, char* f, uint64_t v) {
+    store_rel(f, v);
+    bell_ring(P->bell(r));
+  }
   // Take the next header of this program (rank 0's doorbell in our ring).
   bool take(PeerHeader& h) {
     HeaderRing* R = P->ring(me);
     const uint64_t pos = P->taken;
     auto& s = R->slots[pos % HeaderRing::kSlots];
-    wait_until([&] { return s.seq.load(std::memory_order_acquire) == pos + 1; },
+    wait_ready([&] { return s.seq.load(std::memory_order_acquire) == pos + 1; },
                [&](clk::duration) {
                  if (!m->open()) throw std::runtime_error("mesh closed");
                  if (s.seq.load(std::memory_order_acquire) != pos + 1 && fd_gone((*fds)[0]))
                    throw std::runtime_error("mesh: rank 0 is gone");
-               });
+               },
+               P->bell(me), im->spin_us);
     h = s.h;
     R->consumed.store(pos + 1, std::memory_order_release);
     P->taken = pos + 1;
@@ -626,7 +682,7 @@ void run_cpu_loop(WorkerCtx& W) {
       auto in_ptr = [&](int j) -> const double* {
         if (j == -1) return reinterpret_cast<const double*>(P.slab_host(W.me, -1, k));
         if (st[size_t(j)].rank == W.me) return E.hout[size_t(j)].data() + size_t(k) * P.d.max_rows * st[size_t(j)].out_cols;
-        W.wait_flag(P.ready(W.me, k, j), seq, "stage input");
+        W.wait_input(k, j, seq);
         return reinterpret_cast<const double*>(P.slab_host(W.me, j, k));
       };
       std::vector<const double*> ins;
@@ -669,10 +725,10 @@ void run_cpu_loop(WorkerCtx& W) {
           W.wait_credit(c, k, seq);
           std::memcpy(P.slab_host(c, i, k), out, n * sizeof(double));
         }
-        store_rel(P.ready(c, k, i), seq);
+        W.host_flag(c, P.ready(c, k, i), seq);
       }
     }
-    if (P.alias[size_t(W.me)].first < 0) store_rel(P.freed(W.me, k), seq);
+    if (P.alias[size_t(W.me)].first < 0) W.host_flag(W.me, P.freed(W.me, k), seq);
     W.im->batches.fetch_add(1, std::memory_order_relaxed);
     W.im->rows.fetch_add(uint64_t(rows > 0 ? rows : 0), std::memory_order_relaxed);
   }
@@ -716,7 +772,7 @@ void run_gpu_loop(WorkerCtx& W) {
       char* own_out = E.out[size_t(i)].as<char>() + size_t(k) * E.out_slab[size_t(i)];
       // remote inputs must be in place before anything that reads them is enqueued
       for (int j : sg.inputs)
-        if (j >= 0 && st[size_t(j)].rank != W.me) W.wait_flag(P.ready(W.me, k, j), seq, "stage input");
+        if (j >= 0 && st[size_t(j)].rank != W.me) W.wait_input(k, j, seq);
       const bool zc_in = sg.kind == kMeshModel && !P.model[size_t(i)]->device_io_only() &&
                          P.model[size_t(i)]->zero_copy_input_for(rws, sg.in_cols) && xbytes <= kZeroCopyMax;
       auto dev_in = [&](int j) -> const double* {
@@ -886,6 +942,7 @@ void Mesh::stop_peers() {
       s.h = PeerHeader{};
       s.h.op = kPeerStop;
       s.seq.store(wpos + 1, std::memory_order_release);
+      bell_ring(P.bell(c));
     }
     P.next += 1;  // the stop occupies one ring position everywhere; no batch may follow
   }
@@ -921,6 +978,9 @@ class ProgramModel : public gpu::RowModel {
 
  public:
   std::atomic<uint32_t> polls{0};  // liveness checks every 1024th poll
+  // Rank 0's doorbell when CPU workers write its flags (GPU gangs: none, the
+  // flags are written by streams).
+  Bell* reply_bell() const { return m_->gpu() ? nullptr : P_->bell(0); }
 };
 
 namespace {
@@ -953,9 +1013,24 @@ struct MeshCall : gpu::CpuCall {
     return true;
   }
   std::string error() const override { return err; }
+  // The batcher's low-CPU mode: block up to `us` for this call's replies
+  // (CPU gangs: on rank 0's futex doorbell, woken by the worker's store;
+  // GPU gangs: yielding polls, since streams write the flags).
   bool wait_us(int us) override {
-    const auto until = clk::now() + std::chrono::microseconds(std::max(1, us));
-    while (!done() && clk::now() < until) std::this_thread::sleep_for(std::chrono::microseconds(10));
+    if (done()) return true;
+    const auto lim = std::chrono::microseconds(std::max(1, us));
+    if (Bell* b = pm->reply_bell()) {
+      const uint32_t s = b->seq.load(std::memory_order_seq_cst);
+      b->sleepers.fetch_add(1, std::memory_order_seq_cst);
+      if (!done()) {
+        const timespec ts{0, long(lim.count()) * 1000L};
+        syscall(SYS_futex, reinterpret_cast<uint32_t*>(&b->seq), FUTEX_WAIT, s, &ts, nullptr, 0);
+      }
+      b->sleepers.fetch_sub(1, std::memory_order_seq_cst);
+      return true;
+    }
+    const auto t0 = clk::now();
+    while (!done() && clk::now() - t0 < lim) std::this_thread::yield();
     return true;
   }
 };
@@ -1004,6 +1079,7 @@ bool ProgramModel::reap() {
       for (size_t i = 0; i < n; ++i) out[i] *= inv;
     }
     store_rel(P.freed(0, k), seq);
+    bell_ring(P.bell(0));  // a producer may wait for this slot
     auto call = std::move(pd.call);
     pd = Prog::Pend{};
     P.reaped = seq;
@@ -1073,6 +1149,7 @@ gpu::CpuCallPtr ProgramModel::start_cpu(const double* X, int rows, int cols, dou
         s.h.rows = nr;
         s.h.cols = cols;
         s.seq.store(pos + 1, std::memory_order_release);  // the doorbell
+        bell_ring(P.bell(c));
       }
       P.next = seq;
     }
