@@ -426,10 +426,13 @@ def test_mahalanobis_device_concurrent_callers_share_launches():
     allX = np.concatenate(data)
     np.testing.assert_allclose(st[:p], allX.mean(0), rtol=1e-9, atol=1e-12)
     # the running covariance depends on the arrival order (the reference's
-    # recursion uses the running mean at each step): only close, not equal
+    # recursion uses the running mean at each step): only close, not equal.
+    # 16 threads may run far out of step, and a full reordering of these
+    # rows moves the recursion's C by up to ~0.09 (numpy, 3 random
+    # permutations: 0.065 / 0.092 / 0.084), so the bound is set above that.
     ref = OutlierMahalanobis(n_components=k, start_clip=10 ** 12, device=-1)
     for X in data:
         ref.predict(X.copy(), [])
     Cg = st[p:p + p * p].reshape(p, p)
     np.testing.assert_allclose(Cg, Cg.T, rtol=0, atol=1e-15)
-    np.testing.assert_allclose(Cg, ref.C, rtol=0, atol=2e-2)
+    np.testing.assert_allclose(Cg, ref.C, rtol=0, atol=0.15)
