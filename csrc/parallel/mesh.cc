@@ -180,7 +180,7 @@ struct Mesh::Impl {
   bool prepared = false, connected = false, started = false;
   int timeout_ms = 60000;
   int delay_us = 0;
-  int spin_us = 20;
+  int spin_us = 100;
   mutable std::mutex err_mu;
   std::string err;
   std::atomic<uint64_t> batches{0}, rows{0}, max_inflight{0}, host_waits{0}, stage_errors{0};
@@ -253,7 +253,7 @@ Mesh::Mesh(int rank, int world, int device, std::vector<int> ctrl_fds, int slots
   if (int(fds_.size()) != world) throw std::runtime_error("Mesh: need one control socket slot per rank");
   im_->timeout_ms = std::max(100, env_int("SCA_MESH_TIMEOUT_MS", 60000));
   im_->delay_us = std::max(0, env_int("SCA_FABRIC_WORKER_DELAY_US", 0));
-  im_->spin_us = std::max(0, env_int("SCA_MESH_SPIN_US", 20));
+  im_->spin_us = std::max(0, env_int("SCA_MESH_SPIN_US", 100));
 }
 
 Mesh::~Mesh() {
