@@ -271,7 +271,25 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
         polling.store(false, std::memory_order_relaxed);
         continue;
       }
-      int n = epoll_wait(epfd, evs, 256, 200);
+      int n = 0;
+      if (srv->spin_us_ > 0) {  // poll briefly before sleeping: the next request usually arrives within microseconds
+        polling.store(false, std::memory_order_relaxed);
+        const auto until = Clock::now() + std::chrono::microseconds(srv->spin_us_);
+        do {
+          n = epoll_wait(epfd, evs, 256, 0);
+        } while (n == 0 && !has_work.load(std::memory_order_acquire) && Clock::now() < until);
+        if (n == 0 && has_work.load(std::memory_order_acquire)) continue;
+        if (n == 0) {
+          polling.store(true, std::memory_order_seq_cst);
+          if (has_work.load(std::memory_order_seq_cst)) {
+            polling.store(false, std::memory_order_relaxed);
+            continue;
+          }
+          n = epoll_wait(epfd, evs, 256, 200);
+        }
+      } else {
+        n = epoll_wait(epfd, evs, 256, 200);
+      }
       polling.store(false, std::memory_order_relaxed);
       for (int i = 0; i < n; ++i) {
         int fd = evs[i].data.fd;
@@ -855,7 +873,9 @@ static int make_listener(const std::string& host, int port, int* bound_port) {
 }
 
 HttpServer::HttpServer(std::shared_ptr<Engine> engine, HttpOptions opts)
-    : engine_(std::move(engine)), opts_(std::move(opts)) {}
+    : engine_(std::move(engine)), opts_(std::move(opts)) {
+  if (const char* e = std::getenv("SCA_HTTP_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
+}
 
 HttpServer::~HttpServer() { stop(); }
 

@@ -59,6 +59,7 @@ class HttpServer {
   std::atomic<bool> paused_{false};
   std::atomic<bool> running_{false};
   std::atomic<uint64_t> served_{0};
+  int spin_us_ = 0;  // SCA_HTTP_SPIN_US: poll epoll this long before blocking
   friend struct Worker;
 };
 

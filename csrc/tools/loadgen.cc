@@ -59,7 +59,23 @@ struct Args {
   // region fails the run instead of counting as a prediction.
   std::string expect;
   long check_every = 16;
+  // Poll epoll without blocking for up to this many microseconds before a
+  // blocking wait (0 = always block): a client thread that never sleeps costs
+  // the server no wake-up in its send path.
+  int spin_us = 0;
 };
+
+// epoll_wait that polls (timeout 0) for up to spin_us before blocking.
+static int wait_events(int epfd, epoll_event* evs, int max, int spin_us) {
+  if (spin_us > 0) {
+    const auto until = Clock::now() + std::chrono::microseconds(spin_us);
+    do {
+      const int n = epoll_wait(epfd, evs, max, 0);
+      if (n != 0) return n;
+    } while (Clock::now() < until);
+  }
+  return epoll_wait(epfd, evs, max, 1000);
+}
 
 static std::string read_file(const std::string& p) {
   std::ifstream f(p, std::ios::binary);
@@ -194,7 +210,7 @@ struct Worker {
     epoll_event evs[512];
     char buf[65536];
     while (active > 0) {
-      int n = epoll_wait(epfd, evs, 512, 1000);
+      int n = wait_events(epfd, evs, 512, a->spin_us);
       for (int i = 0; i < n; ++i) {
         RestConn& c = rconns[evs[i].data.u32];
         if (!c.busy) {
@@ -366,7 +382,7 @@ struct Worker {
       return t;
     };
     while (total_inflight() > 0) {
-      int n = epoll_wait(epfd, evs, 512, 1000);
+      int n = wait_events(epfd, evs, 512, a->spin_us);
       for (int i = 0; i < n; ++i) {
         GConn& c = *gconns[evs[i].data.u32];
         if (evs[i].events & EPOLLIN) {
@@ -419,6 +435,7 @@ int main(int argc, char** argv) {
     else if (k == "--expect") a.expect = v();
     else if (k == "--expect-file") a.expect = read_file(v());
     else if (k == "--check-every") a.check_every = std::max(1L, std::stol(v()));
+    else if (k == "--spin-us") a.spin_us = std::max(0, std::stoi(v()));
     else { fprintf(stderr, "unknown arg %s\n", k.c_str()); return 2; }
   }
   if (!body_file.empty()) a.body = read_file(body_file);

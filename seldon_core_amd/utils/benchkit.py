@@ -447,6 +447,9 @@ def run_loadgen(port: int, steps: int, warmup: int, api: str, body, users: int, 
     or on sampled replies whose body differs from `expect`."""
     cmd = [LOADGEN, "--host", "127.0.0.1", "--port", str(port), "--users", str(users), "--threads", str(threads),
            "--steps", str(steps), "--warmup", str(warmup), "--step-requests", str(step_requests)]
+    spin = int(os.environ.get("SCA_LOADGEN_SPIN_US", "0") or 0)
+    if spin > 0:
+        cmd += ["--spin-us", str(spin)]
     tmp = []
     if api == "rest":
         cmd += ["--mode", "rest", "--path", path, "--body", body]
