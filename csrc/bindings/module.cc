@@ -223,7 +223,7 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("W"), py::arg("b"), py::arg("act"));
   // stages: list of dicts {kind: "model"|"mean", model?, device, inputs: [int], node}
-  m.def("graph_model", [](py::list stages, int in_cols, bool split_streams) {
+  m.def("graph_model", [](py::list stages, int in_cols, int split_streams) {
     std::vector<gpu::GraphStage> st;
     for (auto h : stages) {
       py::dict d = h.cast<py::dict>();
@@ -237,9 +237,9 @@ PYBIND11_MODULE(_C, m) {
       st.push_back(std::move(s));
     }
     auto g = std::make_shared<gpu::GraphModel>(std::move(st), in_cols);
-    if (split_streams) g->set_split(true);
+    if (split_streams) g->set_split(split_streams);
     return std::static_pointer_cast<gpu::RowModel>(g);
-  }, py::arg("stages"), py::arg("in_cols") = 0, py::arg("split_streams") = false);
+  }, py::arg("stages"), py::arg("in_cols") = 0, py::arg("split_streams") = 0);
   m.def("graph_devices", [](std::shared_ptr<gpu::RowModel> m) {
     auto g = std::dynamic_pointer_cast<gpu::GraphModel>(m);
     if (!g) throw std::runtime_error("not a graph model");
@@ -251,6 +251,7 @@ PYBIND11_MODULE(_C, m) {
     py::dict d;
     d["devices"] = g->devices();
     d["split"] = g->split();
+    d["split_mode"] = g->split_mode();
     d["peer_direct"] = g->peer_direct();
     d["stages"] = int(g->stages().size());
     return d;
@@ -371,6 +372,11 @@ PYBIND11_MODULE(_C, m) {
         return py::array_t<double>(py::ssize_t(s.size()), s.data());
       })
       .def("set_state", [](gpu::MahalanobisDevice& d, std::vector<double> s) { d.set_state(s); })
+      .def("lock_state", [](gpu::MahalanobisDevice& d) {
+        py::gil_scoped_release nogil;  // a native step may hold it briefly
+        d.lock_state();
+      })
+      .def("unlock_state", &gpu::MahalanobisDevice::unlock_state)
       .def("solver_stats", [](const gpu::MahalanobisDevice& d) {
         const auto t = d.solver_stats();
         py::dict r;

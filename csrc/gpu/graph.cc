@@ -133,7 +133,7 @@ void GraphModel::to_device(int device) {
       if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
       else if (e != hipSuccess) { (void)hipGetLastError(); peer_direct_ = false; }
     }
-  if (split_) peer_direct_ = false;
+  if (split_ == 1) peer_direct_ = false;
 }
 
 int GraphModel::lane_of(int stage) const {

@@ -85,12 +85,15 @@ class GraphModel : public RowModel {
   std::vector<int> devices() const;
   bool peer_direct() const { return peer_direct_; }
   // Split mode (tests / rehearsal on one GPU): every stage gets its own
-  // stream and event chain even when stages share a GPU, and cross-stage
+  // stream and event chain even when stages share a GPU.  Mode 1: cross-stage
   // inputs go through the staged-copy branch (peer_direct_ = false) -- the
-  // exact code a graph spread over several GPUs without peer access runs.
-  // Set before to_device(); clone_on() keeps it.  Env: SCA_GRAPH_SPLIT=1.
-  void set_split(bool on) { split_ = on; }
-  bool split() const { return split_; }
+  // code a graph spread over GPUs WITHOUT peer access runs.  Mode 2: the
+  // lanes read each other's HBM directly and the last lane writes the
+  // caller's buffer (peer_direct_ as probed) -- the code an xGMI-connected
+  // multi-GPU graph runs.  Set before to_device(); clone_on() keeps it.
+  void set_split(int mode) { split_ = mode; }
+  bool split() const { return split_ != 0; }
+  int split_mode() const { return split_; }
 
  private:
   struct Aux;  // per-caller-stream resources (one per batcher slot)
@@ -107,7 +110,7 @@ class GraphModel : public RowModel {
   int in_cols_ = 0;
   int root_device_ = -1;
   bool peer_direct_ = true;
-  bool split_ = false;
+  int split_ = 0;
   std::mutex mu_;
   std::unordered_map<hipStream_t, std::unique_ptr<Aux>> aux_;
 };

@@ -259,7 +259,7 @@ void MahalanobisModel::init_state(int device) {
 }
 
 void MahalanobisModel::to_device(int device) {
-  std::lock_guard<std::mutex> g(st_->mu);
+  std::lock_guard<std::recursive_mutex> g(st_->mu);
   if (st_->device == device) return;
   if (st_->device >= 0) throw std::runtime_error("Mahalanobis state already lives on GPU " + std::to_string(st_->device));
   DeviceGuard dg(device);
@@ -282,7 +282,7 @@ void MahalanobisModel::launch(const double* X, int rows, int cols, double* out, 
 void MahalanobisModel::launch_segments(const double* X, int rows, int cols, double* out, void* ws,
                                        const int32_t* seg, int nseg, hipStream_t s) {
   if (cols != st_->prm.p) throw std::runtime_error("Mahalanobis: expected " + std::to_string(st_->prm.p) + " features");
-  std::lock_guard<std::mutex> g(st_->mu);
+  std::lock_guard<std::recursive_mutex> g(st_->mu);
   // after the previous step on whatever stream it ran
   if (st_->chained) SCA_HIP_CHECK(hipStreamWaitEvent(s, st_->chain.get(), 0));
   double* eig = st_->d_eig.as<double>();
@@ -297,13 +297,13 @@ void MahalanobisModel::launch_segments(const double* X, int rows, int cols, doub
 
 void MahalanobisModel::run_cpu(const double* X, int rows, int cols, double* out) const {
   if (cols != st_->prm.p) throw std::runtime_error("Mahalanobis: expected " + std::to_string(st_->prm.p) + " features");
-  std::lock_guard<std::mutex> g(st_->mu);
+  std::lock_guard<std::recursive_mutex> g(st_->mu);
   if (st_->device >= 0) throw std::runtime_error("Mahalanobis: state lives on the GPU (no CPU step)");
   maha_step_host(X, rows, view_, st_->h_state.data(), out);
 }
 
 std::vector<double> MahalanobisModel::state() const {
-  std::lock_guard<std::mutex> g(st_->mu);
+  std::lock_guard<std::recursive_mutex> g(st_->mu);
   if (st_->device < 0) return st_->h_state;
   DeviceGuard dg(st_->device);
   if (st_->chained) SCA_HIP_CHECK(hipEventSynchronize(st_->chain.get()));
@@ -313,7 +313,7 @@ std::vector<double> MahalanobisModel::state() const {
 }
 
 std::vector<double> MahalanobisModel::solver_stats() const {
-  std::lock_guard<std::mutex> g(st_->mu);
+  std::lock_guard<std::recursive_mutex> g(st_->mu);
   if (st_->device < 0) return {};
   DeviceGuard dg(st_->device);
   if (st_->chained) SCA_HIP_CHECK(hipEventSynchronize(st_->chain.get()));
@@ -326,7 +326,7 @@ std::vector<double> MahalanobisModel::solver_stats() const {
 }
 
 void MahalanobisModel::set_state(const std::vector<double>& s) {
-  std::lock_guard<std::mutex> g(st_->mu);
+  std::lock_guard<std::recursive_mutex> g(st_->mu);
   if (s.size() != kern::maha_state_doubles(st_->prm.p)) throw std::runtime_error("Mahalanobis: bad state size");
   if (st_->device < 0) {
     st_->h_state = s;

@@ -35,7 +35,10 @@ struct MahaState {
   std::vector<double> h_state;     // device -1
   Event chain;                     // completes after the last launched step
   bool chained = false;
-  std::mutex mu;                   // launch ordering across views / batchers
+  // launch ordering across views / batchers; recursive so the Python
+  // component can hold it across a pull -> host step -> push section
+  // (MahalanobisDevice::lock_state) while state() / set_state() re-take it
+  std::recursive_mutex mu;
 };
 
 class MahalanobisModel : public RowModel {
@@ -66,6 +69,7 @@ class MahalanobisModel : public RowModel {
   int p() const { return st_->prm.p; }
   int k() const { return st_->prm.k; }
   int device() const { return st_->device; }
+  std::recursive_mutex& state_mutex() const { return st_->mu; }
 
  private:
   void init_state(int device);
@@ -88,6 +92,10 @@ class MahalanobisDevice {
   std::shared_ptr<MahalanobisModel> predict_view(double threshold) const;
   BatcherStats stats() const { return unit_->stats(); }
   std::vector<double> solver_stats() const { return model_->solver_stats(); }
+  // Exclusive section over the shared state (same thread locks and unlocks):
+  // native steps of the graph node wait until it ends.
+  void lock_state() { model_->state_mutex().lock(); }
+  void unlock_state() { model_->state_mutex().unlock(); }
   int p() const { return model_->p(); }
   int k() const { return model_->k(); }
   int device() const { return model_->device(); }

@@ -1,10 +1,12 @@
 #include "router.h"
 
 #include <fcntl.h>
+#include <signal.h>
 #include <immintrin.h>
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <sstream>
@@ -17,8 +19,8 @@ namespace sca::gpu {
 // One bandit's state shared by the engine processes of a host.  Updates take
 // a spinlock in the mapping (feedback is rare next to routing, and the
 // critical section is a few hundred nanoseconds); readers compare `version`
-// with the last one they pulled.  A lock held for over a second belongs to a
-// process that died inside the critical section and is taken over.
+// with the last one they pulled.  A lock whose owner process died inside the
+// critical section is taken over (ShmLock).
 struct BanditModel::Shared {
   std::atomic<uint32_t> init;  // 0 fresh, 1 being seeded, 2 ready
   std::atomic<uint32_t> lock;
@@ -30,21 +32,29 @@ struct BanditModel::Shared {
 };
 
 namespace {
+// The lock word holds the owner's PID.  A waiter takes the lock over only
+// when that process no longer exists (kill(pid, 0) -> ESRCH): an owner that
+// is merely descheduled (CPU quota throttling, SIGSTOP) keeps it.
 struct ShmLock {
   std::atomic<uint32_t>& l;
   explicit ShmLock(std::atomic<uint32_t>& lk) : l(lk) {
-    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t me = uint32_t(getpid());
+    auto t_check = std::chrono::steady_clock::now();
     for (unsigned n = 0;; ++n) {
       uint32_t z = 0;
-      if (l.compare_exchange_weak(z, 1, std::memory_order_acquire)) return;
+      if (l.compare_exchange_weak(z, me, std::memory_order_acquire)) return;
       if (n < 4096) {
         _mm_pause();
-      } else {
-        std::this_thread::yield();
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-          l.store(1, std::memory_order_acquire);  // owner died mid-update: take it over
-          return;
-        }
+        continue;
+      }
+      std::this_thread::yield();
+      const auto now = std::chrono::steady_clock::now();
+      if (now - t_check > std::chrono::milliseconds(100)) {
+        t_check = now;
+        uint32_t owner = l.load(std::memory_order_relaxed);
+        if (owner != 0 && owner != me && ::kill(pid_t(owner), 0) != 0 && errno == ESRCH &&
+            l.compare_exchange_strong(owner, me, std::memory_order_acquire))
+          return;  // the owner died inside the critical section
       }
     }
   }
@@ -267,7 +277,10 @@ std::string BanditModel::snapshot() const {
   std::lock_guard<std::mutex> g(mu_);
   std::ostringstream o;
   o.precision(17);
-  o << "{\"kind\":" << int(kind_) << ",\"best\":" << best_ << ",\"offset\":" << offset_.load() << ",\"success\":[";
+  // version: the shared state's version this snapshot reflects (restore)
+  const uint64_t ver = shm_ ? shm_->version.load(std::memory_order_acquire) : seen_version_.load();
+  o << "{\"kind\":" << int(kind_) << ",\"best\":" << best_ << ",\"offset\":" << offset_.load()
+    << ",\"version\":" << ver << ",\"success\":[";
   for (int i = 0; i < nb_; ++i) o << (i ? "," : "") << success_[size_t(i)];
   o << "],\"tries\":[";
   for (int i = 0; i < nb_; ++i) o << (i ? "," : "") << tries_[size_t(i)];
@@ -297,17 +310,41 @@ void BanditModel::restore(const std::string& s) {
   arr("beta", b_);
   if (const Json* b = j.find("best")) best_ = int(b->as_number());
   if (const Json* o = j.find("offset")) offset_.store(uint64_t(o->as_number()));
-  if (shm_) {  // every worker restores the same snapshot: the shared state takes it once more
+  if (shm_) {
+    // Workers share one state: a snapshot replaces it only if it is newer
+    // than the shared state (its version is the shared version it was taken
+    // at).  The first worker restoring after a fresh start installs it; the
+    // others -- and a worker restarted while the rest kept serving -- find the
+    // live state at least as new and pull it instead, so feedback applied
+    // since the checkpoint is kept.
+    const Json* v = j.find("version");
+    const uint64_t snap_v = v ? uint64_t(v->as_number()) : 0;
     ShmLock l(shm_->lock);
-    for (int i = 0; i < nb_; ++i) {
-      shm_->success[i] = success_[size_t(i)];
-      shm_->tries[i] = tries_[size_t(i)];
-      shm_->values[i] = values_[size_t(i)];
-      shm_->alpha[i] = a_[size_t(i)];
-      shm_->beta[i] = b_[size_t(i)];
+    const uint64_t live_v = shm_->version.load(std::memory_order_acquire);
+    // version 1: seeded by the first worker, no feedback, nothing restored yet
+    if (live_v <= 1 || snap_v > live_v) {
+      for (int i = 0; i < nb_; ++i) {
+        shm_->success[i] = success_[size_t(i)];
+        shm_->tries[i] = tries_[size_t(i)];
+        shm_->values[i] = values_[size_t(i)];
+        shm_->alpha[i] = a_[size_t(i)];
+        shm_->beta[i] = b_[size_t(i)];
+      }
+      shm_->best.store(best_, std::memory_order_release);
+      const uint64_t nv = std::max(snap_v, live_v) + 1;
+      shm_->version.store(nv, std::memory_order_release);
+      seen_version_.store(nv, std::memory_order_relaxed);
+    } else {
+      for (int i = 0; i < nb_; ++i) {
+        success_[size_t(i)] = shm_->success[i];
+        tries_[size_t(i)] = shm_->tries[i];
+        values_[size_t(i)] = shm_->values[i];
+        a_[size_t(i)] = shm_->alpha[i];
+        b_[size_t(i)] = shm_->beta[i];
+      }
+      best_ = shm_->best.load(std::memory_order_relaxed);
+      seen_version_.store(live_v, std::memory_order_relaxed);
     }
-    shm_->best.store(best_, std::memory_order_release);
-    seen_version_.store(shm_->version.fetch_add(1, std::memory_order_acq_rel) + 1, std::memory_order_relaxed);
   }
   publish();
 }

@@ -347,11 +347,18 @@ class OutlierMahalanobis(_FeedbackMetrics):
             self.prediction = (self.score > self.threshold).astype(int)
             return self.prediction
         shared = self._dev is not None and X.ndim == 2 and self._dev.p == X.shape[1]
-        if shared:  # a native node (row_model) holds the state: one detector, two entry points
+        if not shared:
+            return self._get_preds_host(X)
+        # A native node (row_model) holds the state: one detector, two entry
+        # points.  Pull -> host step -> push runs under the state's lock, so a
+        # native step cannot land in between and be overwritten by the push.
+        self._dev.lock_state()
+        try:
             self._pull_state()
-        out = self._get_preds_host(X)
-        if shared:
+            out = self._get_preds_host(X)
             self._push_state(self._dev.p)
+        finally:
+            self._dev.unlock_state()
         return out
 
     def _get_preds_host(self, X):

@@ -123,11 +123,12 @@ def plan(graph: Dict, row_models: Dict[str, Any], bound: Dict[str, Any],
     return found
 
 
-def build(C, fg: FusedGraph, in_cols: int = 0, split: bool = False):
+def build(C, fg: FusedGraph, in_cols: int = 0, split: int = 0):
     """Native GraphModel for a plan entry (raises if the stage widths disagree).
-    ``split``: one stream per stage and staged copies between stages even on
-    one GPU -- the multi-GPU code path, rehearsed on a single device."""
-    return C.graph_model(fg.stages, in_cols, split)
+    ``split``: one stream per stage even on one GPU -- the multi-GPU code
+    paths rehearsed on a single device: 1 = staged copies between stages (no
+    peer access), 2 = direct cross-lane reads (xGMI peer access)."""
+    return C.graph_model(fg.stages, in_cols, int(split))
 
 
 def describe(fg: FusedGraph) -> str:
@@ -138,11 +139,14 @@ def describe(fg: FusedGraph) -> str:
     return " ".join(parts)
 
 
-def split_enabled(annotations: Optional[Dict[str, str]]) -> bool:
-    """``seldon.io/device-graph-split: true`` (or SCA_GRAPH_SPLIT=1): build
-    fused graphs in split mode (see ``build``)."""
-    v = (annotations or {}).get("seldon.io/device-graph-split")
-    return v is not None and str(v).lower() in ("1", "true", "yes", "on")
+def split_enabled(annotations: Optional[Dict[str, str]]) -> int:
+    """``seldon.io/device-graph-split``: ``true`` builds fused graphs in split
+    mode 1 (staged copies), ``peer`` in split mode 2 (direct cross-lane reads);
+    see ``build``."""
+    v = str((annotations or {}).get("seldon.io/device-graph-split", "")).lower()
+    if v == "peer":
+        return 2
+    return 1 if v in ("1", "true", "yes", "on") else 0
 
 
 def fusion_enabled(annotations: Optional[Dict[str, str]], default: bool = True) -> bool:

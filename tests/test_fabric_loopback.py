@@ -220,19 +220,25 @@ GRAPHS = {
 }
 
 
+@pytest.mark.parametrize("mode", ["true", "peer"])
 @pytest.mark.parametrize("name", sorted(GRAPHS))
-def test_split_device_graph_matches_cpu_under_concurrency(name):
+def test_split_device_graph_matches_cpu_under_concurrency(name, mode):
+    """Split lanes on one GPU, 8 callers, 4 slots, buffer growth: "true" runs
+    the staged-copy branch (GPUs without peer access), "peer" the direct
+    cross-lane reads and the last lane's direct write into the caller's
+    buffer (xGMI-connected GPUs, graph.cc launch_segments)."""
     C = sca.native()
     rng = np.random.default_rng(11)
     comps = {"tin": _lin(C, rng, 4, 4), "m1": _lin(C, rng, 3, 4, 1), "m2": _lin(C, rng, 3, 4, 1),
              "m3": _lin(C, rng, 3, 4, 1), "tout": _lin(C, rng, 2, 3)}
-    spec = _spec(GRAPHS[name], {"seldon.io/device-graph-split": "true"})
+    spec = _spec(GRAPHS[name], {"seldon.io/device-graph-split": mode})
     gpu = sca.Deployment(spec, components=comps, device=0, fuse=True, batcher={"slots": 4, "max_batch": 2048})
     cpu = sca.Deployment(spec, components=comps, device=-1, fuse=True)
     root = GRAPHS[name]["name"]
     try:
         info = C.graph_info(gpu.batched[root].model)
-        assert info["split"] and not info["peer_direct"] and info["stages"] >= 3, info
+        assert info["split"] and info["stages"] >= 3, info
+        assert info["peer_direct"] == (mode == "peer") and info["split_mode"] == (2 if mode == "peer" else 1), info
         errors, worst = [], [0.0]
         lock = threading.Lock()
 

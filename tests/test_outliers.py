@@ -436,3 +436,34 @@ def test_mahalanobis_device_concurrent_callers_share_launches():
     Cg = st[p:p + p * p].reshape(p, p)
     np.testing.assert_allclose(Cg, Cg.T, rtol=0, atol=1e-15)
     np.testing.assert_allclose(Cg, ref.C, rtol=0, atol=0.15)
+
+
+def test_mahalanobis_python_and_native_entry_points_do_not_lose_steps():
+    """the Python path pulls the shared state, steps on the host
+    and pushes it back; native steps of the graph node (row_model) landing in
+    between used to be overwritten.  Under the state lock every row of both
+    entry points is counted (CPU placement: both paths step the host state)."""
+    import threading
+
+    rng = np.random.default_rng(21)
+    det = OutlierMahalanobis(n_components=3, n_features=6, device=-1)
+    rm = det.row_model()
+    assert rm is not None
+    X_py = [rng.normal(size=(2, 6)) for _ in range(150)]
+    X_nat = [rng.normal(size=(3, 6)) for _ in range(150)]
+
+    def python_side():
+        for X in X_py:
+            det.predict(X, [])
+
+    def native_side():
+        for X in X_nat:
+            rm.run_cpu(X)
+
+    th = [threading.Thread(target=python_side), threading.Thread(target=native_side)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    det._pull_state()
+    assert det.n == 2 * 150 + 3 * 150, det.n

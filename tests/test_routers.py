@@ -115,3 +115,34 @@ def test_eg_host_route_matches_bandit_kernel():
     picks_host = np.array([host.route_host() for _ in range(3000)])
     assert (picks_dev == picks_host).all()
     assert abs(np.mean(picks_host == 2) - 0.65) < 0.03
+
+
+def test_shared_state_restore_keeps_newer_live_feedback():
+    """restoring a checkpoint used to overwrite the shared bandit
+    state of every worker.  Now a snapshot replaces the shared state only
+    when it is newer (or the state is fresh): the first worker's restore
+    installs it; a worker restarted later with the same old checkpoint pulls
+    the live state and keeps the feedback applied since."""
+    import os
+
+    name = f"/sca_test_bandit_{os.getpid()}"
+    try:
+        src = EpsilonGreedy(n_branches=3, epsilon=0.1, best_branch=0, seed=1)
+        src.send_feedback(np.ones((5, 1)), [], 1, 1.0, None)
+        ckpt = src.model.snapshot()
+        a = EpsilonGreedy(n_branches=3, epsilon=0.1, best_branch=0, seed=2)
+        a.share_state(name, 0)
+        a.model.restore(ckpt)  # fresh shared state: the checkpoint goes in
+        assert a.state()["success"] == [0, 5, 0]
+        a.send_feedback(np.ones((4, 1)), [], 2, 1.0, None)  # live feedback after the checkpoint
+        b = EpsilonGreedy(n_branches=3, epsilon=0.1, best_branch=0, seed=3)
+        b.share_state(name, 1)
+        b.model.restore(ckpt)  # a restarted worker with the old checkpoint
+        assert b.state()["success"] == [0, 5, 4], b.state()
+        assert a.state()["success"] == [0, 5, 4], a.state()
+        assert b.best_branch == a.best_branch
+    finally:
+        try:
+            os.unlink("/dev/shm" + name)
+        except OSError:
+            pass
