@@ -102,9 +102,13 @@ void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes
 // writes the transformed output -- one launch, no slab.  rows_per_block from
 // tree_whole_rows_per_block (power of two <= 16, <= 4 trees per thread).
 int tree_whole_rows_per_block(int n_trees, int rows);
+// lookahead (depth 8): 10 x levels per round + trees per iteration of the
+// lookahead descent (21 .. 42), 0 = the level-by-level descent, -1 =
+// SCA_TREE_LOOKAHEAD (default 0).
 void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, int n_trees, int rows_per_block, const float* base_margin, float scale,
-                        int transform, double* out, int out_cols, hipStream_t stream, hipEvent_t stop = nullptr);
+                        int transform, double* out, int out_cols, hipStream_t stream, hipEvent_t stop = nullptr,
+                        int lookahead = -1);
 
 // ------------------------------------------------------------ combiners
 // out = mean over N inputs (each [n] fp64). inputs: device array of pointers.

@@ -23,6 +23,8 @@
 
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace sca::kern {
 namespace {
 
@@ -390,6 +392,76 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
   if constexpr (FUSED) fused_tail(partial, rows, n_chunks, red);
 }
 
+// Lookahead descent of ONE perfect tree: each round loads the whole 4-level
+// subtree below the current node (1 + 2 + 4 + 8 nodes; each level's nodes are
+// contiguous in the breadth-first layout) with independent loads, then
+// resolves its 4 levels from registers (select chains on the path bits).  The
+// last round also loads its subtree's 2^levels leaves.  Depth 8 is TWO
+// dependent memory round trips instead of nine.  Why it matters: every
+// launch starts with the ensemble outside this XCD's L2 (PMC at 9 rows: L2
+// hit rate 6-8%, ~1 MB fetched per dispatch, profiles/r05i_tree_small), so
+// each dependent level costs an Infinity-Cache / HBM round trip, and the
+// latency of the chain -- not the number of workgroups -- set the ~11 us of
+// the whole-ensemble kernel at any batch size.
+template <int NL, bool LAST, bool STAGED>
+__device__ __forceinline__ void lookahead_round(const TreeNode* __restrict__ tn, const float* __restrict__ lf,
+                                                int n_internal, int& idx, float& leaf, const float* xs, int lrb,
+                                                const double* __restrict__ xg, int cmp_le) {
+  TreeNode sub[(1 << NL) - 1];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int first = ((idx + 1) << k) - 1;
+#pragma unroll
+    for (int m = 0; m < (1 << k); ++m) sub[(1 << k) - 1 + m] = tn[first + m];
+  }
+  float lv[1 << NL];
+  if constexpr (LAST) {
+    const int lfirst = ((idx + 1) << NL) - 1 - n_internal;
+#pragma unroll
+    for (int m = 0; m < (1 << NL); ++m) lv[m] = lf[lfirst + m];
+  }
+  int path = 0;  // decisions so far, MSB first (0 = left, 1 = right)
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    TreeNode nd = sub[(1 << k) - 1];
+#pragma unroll
+    for (int m = 1; m < (1 << k); ++m)
+      if (path == m) nd = sub[(1 << k) - 1 + m];
+    const float x = STAGED ? tile_x(xs, nd.feat, lrb) : float(xg[nd.feat & 0x7fffffff]);
+    path = 2 * path + (go_left(x, nd.thr, nd.feat, cmp_le) ? 0 : 1);
+  }
+  idx = ((idx + 1) << NL) - 1 + path;
+  if constexpr (LAST) {
+    float v = lv[0];
+#pragma unroll
+    for (int m = 1; m < (1 << NL); ++m)
+      if (path == m) v = lv[m];
+    leaf = v;
+  }
+}
+
+template <int REM, int L, bool STAGED>
+__device__ __forceinline__ void lookahead_rounds(const TreeNode* __restrict__ tn, const float* __restrict__ lf,
+                                                 int n_internal, int& idx, float& leaf, const float* xs, int lrb,
+                                                 const double* __restrict__ xg, int cmp_le) {
+  constexpr int NL = REM < L ? REM : L;
+  lookahead_round<NL, REM == NL, STAGED>(tn, lf, n_internal, idx, leaf, xs, lrb, xg, cmp_le);
+  if constexpr (REM > NL) lookahead_rounds<REM - NL, L, STAGED>(tn, lf, n_internal, idx, leaf, xs, lrb, xg, cmp_le);
+}
+
+// L levels per round (2..4): depth D costs ceil(D / L) dependent round trips
+// and (2^L - 1) / L node loads per level instead of one.
+template <int D, int L, bool STAGED>
+__device__ __forceinline__ float descend_lookahead(const TreeNode* __restrict__ tn, const float* __restrict__ lf,
+                                                   int n_internal, const float* xs, int lrb,
+                                                   const double* __restrict__ xg, int cmp_le) {
+  static_assert(D >= 1 && D <= 12 && L >= 1 && L <= 4, "lookahead descent: depth 1..12, 1..4 levels per round");
+  int idx = 0;
+  float leaf = 0.f;
+  lookahead_rounds<D, L, STAGED>(tn, lf, n_internal, idx, leaf, xs, lrb, xg, cmp_le);
+  return leaf;
+}
+
 // Small batches, single-output models: ONE workgroup of 1024 threads owns a
 // tile of RB rows and the WHOLE ensemble (thread i -> row i % RB, trees
 // i / RB, i / RB + 1024 / RB, ...; RB is sized so a thread walks <= 4 trees,
@@ -400,7 +472,7 @@ __global__ __launch_bounds__(kBlock) void sparse_partial(const double* __restric
 // straight from the batcher's pinned buffer (no H2D copy).
 constexpr int kWholeBlock = 1024;
 
-template <int D>
+template <int D, int LA, int TU>
 __global__ __launch_bounds__(kWholeBlock) void perfect_whole(const double* __restrict__ X, int rows, int F,
                                                              const TreeNode* __restrict__ nodes,
                                                              const float* __restrict__ leaves, int depth, int cmp_le,
@@ -425,7 +497,26 @@ __global__ __launch_bounds__(kWholeBlock) void perfect_whole(const double* __res
   const double* xg = X + size_t(min(row0 + r_local, rows - 1)) * F;
   constexpr int U = 4;
   double acc = 0.0;
-  if (stage_lds) {
+  if constexpr (LA > 0 && D > 0) {
+    // TU trees per iteration, all walked unconditionally (a clamped index
+    // contributes 0): one basic block, so their loads are in flight together
+    auto walk = [&](auto staged) {
+      constexpr bool S = decltype(staged)::value;
+      for (int t = slot; t < n_trees; t += TU * tpr) {
+        float v[TU];
+#pragma unroll
+        for (int u = 0; u < TU; ++u) {
+          const int tu = t + u * tpr < n_trees ? t + u * tpr : t;
+          v[u] = descend_lookahead<D, LA, S>(nodes + size_t(tu) * n_internal, leaves + size_t(tu) * (n_internal + 1),
+                                             n_internal, xs, lrb, xg, cmp_le);
+        }
+#pragma unroll
+        for (int u = 0; u < TU; ++u) acc += t + u * tpr < n_trees ? double(v[u]) : 0.0;
+      }
+    };
+    if (stage_lds) walk(std::true_type{});
+    else if (row_ok) walk(std::false_type{});
+  } else if (stage_lds) {
     for (int t = slot; t < n_trees; t += tpr * U)
       acc += descend_perfect<D, U, true>(nodes, leaves, n_internal, depth, t, n_trees, tpr, 0, xs, lrb, xg, cmp_le);
   } else if (row_ok) {
@@ -577,12 +668,15 @@ void tree_sparse_fused(const double* X, int rows, int F, const SparseNode* nodes
   launch_sparse<true>(X, rows, F, nodes, tree_root, cmp_le, chunk_begin, n_chunks, RB, partial, red, s, stop);
 }
 
+int tree_whole_lookahead_default();
+
 int tree_whole_rows_per_block(int n_trees, int rows) {
-  // trees one thread walks (SCA_TREE_WHOLE_TPT, default 4: one interleaved
-  // U = 4 round); fewer = more workgroups per batch
+  // trees one thread walks (SCA_TREE_WHOLE_TPT): 1 with the lookahead descent
+  // (one tree per lane, more workgroups per batch), 4 for the level-by-level
+  // descent (one interleaved U = 4 round)
   static const int tpt = [] {
     const char* e = std::getenv("SCA_TREE_WHOLE_TPT");
-    const int v = e ? std::atoi(e) : 4;
+    const int v = e ? std::atoi(e) : (tree_whole_lookahead_default() > 0 ? 1 : 4);
     return v < 1 ? 1 : v;
   }();
   int rb = 1;
@@ -590,23 +684,60 @@ int tree_whole_rows_per_block(int n_trees, int rows) {
   return rb;
 }
 
+int tree_whole_lookahead_default() {
+  static const int v = [] {
+    const char* e = std::getenv("SCA_TREE_LOOKAHEAD");
+    return e ? std::atoi(e) : 21;
+  }();
+  return v;
+}
+
 void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, int n_trees, int RB, const float* base_margin, float scale, int transform,
-                        double* out, int out_cols, hipStream_t s, hipEvent_t stop) {
+                        double* out, int out_cols, hipStream_t s, hipEvent_t stop, int lookahead) {
   if (rows <= 0 || n_trees <= 0) return;
+  // lookahead = 10 * levels per round + trees per iteration; 21 (default,
+  // depths 4..10): two levels per dependent round trip, one tree at a time
+  // (9 rows x 1000 trees x depth 8: 6.2 us vs 11.2 us level by level,
+  // profiles/r05i_tree_small); 22 .. 42 at depth 8 for A/B; 0 = the
+  // level-by-level descent
+  const int la = lookahead < 0 ? tree_whole_lookahead_default() : lookahead;
   const bool stage = RB * F <= kMaxLdsFloats;
   const uint32_t lds = uint32_t((2 * 256 + (stage ? ((RB * F + 3) & ~3) : 0)) * sizeof(float));
   const dim3 grid((rows + RB - 1) / RB);
-#define SCA_WHOLE_LAUNCH(DD)                                                                                       \
+#define SCA_WHOLE_LAUNCH1(DD, LA, TU)                                                                              \
   do {                                                                                                            \
     if (stop)                                                                                                     \
-      hipExtLaunchKernelGGL((perfect_whole<DD>), grid, dim3(kWholeBlock), lds, s, nullptr, stop, 0, X, rows, F,     \
-                            nodes, leaves, depth, cmp_le, n_trees, RB, int(stage), base_margin, scale, transform,  \
-                            out, out_cols);                                                                       \
+      hipExtLaunchKernelGGL((perfect_whole<DD, LA, TU>), grid, dim3(kWholeBlock), lds, s, nullptr, stop, 0, X,     \
+                            rows, F, nodes, leaves, depth, cmp_le, n_trees, RB, int(stage), base_margin, scale,    \
+                            transform, out, out_cols);                                                            \
     else                                                                                                          \
-      hipLaunchKernelGGL((perfect_whole<DD>), grid, dim3(kWholeBlock), lds, s, X, rows, F, nodes, leaves, depth,   \
-                         cmp_le, n_trees, RB, int(stage), base_margin, scale, transform, out, out_cols);          \
+      hipLaunchKernelGGL((perfect_whole<DD, LA, TU>), grid, dim3(kWholeBlock), lds, s, X, rows, F, nodes, leaves,  \
+                         depth, cmp_le, n_trees, RB, int(stage), base_margin, scale, transform, out, out_cols);   \
   } while (0)
+#define SCA_WHOLE_LAUNCH(DD) SCA_WHOLE_LAUNCH1(DD, 0, 1)
+  if (la == 21 && depth >= 4 && depth <= 10) {
+    switch (depth) {
+      case 4: SCA_WHOLE_LAUNCH1(4, 2, 1); return;
+      case 5: SCA_WHOLE_LAUNCH1(5, 2, 1); return;
+      case 6: SCA_WHOLE_LAUNCH1(6, 2, 1); return;
+      case 7: SCA_WHOLE_LAUNCH1(7, 2, 1); return;
+      case 8: SCA_WHOLE_LAUNCH1(8, 2, 1); return;
+      case 9: SCA_WHOLE_LAUNCH1(9, 2, 1); return;
+      default: SCA_WHOLE_LAUNCH1(10, 2, 1); return;
+    }
+  }
+  if (depth == 8 && la > 0) {
+    switch (la) {
+      case 21: SCA_WHOLE_LAUNCH1(8, 2, 1); return;
+      case 22: SCA_WHOLE_LAUNCH1(8, 2, 2); return;
+      case 31: SCA_WHOLE_LAUNCH1(8, 3, 1); return;
+      case 32: SCA_WHOLE_LAUNCH1(8, 3, 2); return;
+      case 41: SCA_WHOLE_LAUNCH1(8, 4, 1); return;
+      case 42: SCA_WHOLE_LAUNCH1(8, 4, 2); return;
+      default: break;
+    }
+  }
   switch (depth) {
     case 4: SCA_WHOLE_LAUNCH(4); break;
     case 5: SCA_WHOLE_LAUNCH(5); break;
@@ -615,9 +746,10 @@ void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes,
     case 8: SCA_WHOLE_LAUNCH(8); break;
     case 9: SCA_WHOLE_LAUNCH(9); break;
     case 10: SCA_WHOLE_LAUNCH(10); break;
-    default: SCA_WHOLE_LAUNCH(0);
+    default: SCA_WHOLE_LAUNCH1(0, 0, 1);
   }
 #undef SCA_WHOLE_LAUNCH
+#undef SCA_WHOLE_LAUNCH1
 }
 
 void tree_reduce(const double* partial, int rows, int n_chunks, const int* chunk_group, int groups,

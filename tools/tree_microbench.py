@@ -10,9 +10,13 @@ cost), and checks every variant against the two-pass global result.
 """
 import argparse
 import json
+import os
+import sys
 
 import numpy as np
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
@@ -24,6 +28,9 @@ def main():
     ap.add_argument("--rows", default="1,4,17,32,64,128,512,2048")
     ap.add_argument("--sweep", action="store_true", help="two-pass global at chunk = tpr x {1,2,4,8,16}")
     ap.add_argument("--sweep-rb", action="store_true", help="two-pass global, rows/block 1..64 at one tree/lane")
+    ap.add_argument("--small", action="store_true",
+                    help="small-batch plans: the whole-ensemble kernel at 1/2/4 trees per thread vs the fused "
+                         "partial kernel (last-workgroup reduce) at 16-256 trees per workgroup")
     a = ap.parse_args()
     from seldon_core_amd import native
 
@@ -65,9 +72,50 @@ def main():
             while r <= rb:
                 variants.append((f"rb{r}", 256 // r, 0, False, r))
                 r <<= 1
+        if a.small:
+            variants = []
+            for tpt in (1, 2, 4):
+                r = 1
+                while r < 16 and r < rows and T * (r * 2) <= tpt * 1024:
+                    r <<= 1
+                variants.append((f"whole_tpt{tpt}", 0, 0, "whole", r, 0))
+                if D == 8:
+                    for la in (21, 22, 31, 32, 41, 42):
+                        variants.append((f"whole_la{la}_tpt{tpt}", 0, 0, "whole", r, la))
+            for r in sorted({1, 2, 4, min(rb, 16)}):
+                for c in (16, 32, 64, 128, 256):
+                    if c >= 256 // r:  # a chunk fills the block's tree lanes
+                        variants.append((f"fused_rb{r}_c{c}", c, 0, True, r))
+                cap = K.tree_lds_max_trees(D, r, F)  # trees copied whole into LDS: D LDS reads per walk
+                for c in (4, 8, 16):
+                    if c <= cap:
+                        variants.append((f"fused_lds_rb{r}_c{c}", c, c, True, r))
         for v in variants:
             name, chunk, lds, fused = v[:4]
             rb_v = v[4] if len(v) > 4 else rb
+            if fused == "whole":
+                out = torch.empty(rows, dtype=torch.float64, device=dev)
+                la = v[5]
+
+                def launch():
+                    K.tree_perfect_whole(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0, T, rb_v,
+                                         0, 1.0, 0, out.data_ptr(), 1, s, la)
+
+                for _ in range(20):
+                    launch()
+                torch.cuda.synchronize()
+                if out_ref is None:
+                    out_ref = out.clone()
+                err = float((out - out_ref).abs().max())
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    launch()
+                e1.record()
+                torch.cuda.synchronize()
+                row[name] = {"us": round(e0.elapsed_time(e1) * 1000 / a.iters, 2), "rb": rb_v,
+                             "workgroups": -(-rows // rb_v), "max_err": err}
+                continue
             if lds and not lds_cap:
                 continue
             begin = torch.arange(0, T + chunk, chunk, dtype=torch.int32).clamp_(max=T)
