@@ -90,8 +90,9 @@ struct Region {
 
 // Rank 0: one issued batch (a chunk of a call) waiting for its output.
 struct CallState {
-  double* out = nullptr;
+  double* out = nullptr;  // the batcher's buffer: written only while the call is live
   int out_cols = 0;
+  bool abandoned = false;  // (guarded by the program's reap_mu) the caller gave up: never write `out` again
   std::atomic<int> remaining{0};
   std::mutex mu;
   std::string error;
@@ -967,6 +968,12 @@ class ProgramModel : public gpu::RowModel {
 
   // Copy out every finished batch in seq order (any thread).  True if any.
   bool reap();
+  // The caller gave up on a call (error, watchdog, shutdown): its batches
+  // still complete and free their slots, but nothing is written to `out`.
+  void abandon(const CallStatePtr& cs) {
+    std::lock_guard<std::mutex> g(P_->reap_mu);
+    cs->abandoned = true;
+  }
   void check_alive(const char* what, clk::time_point since);
 
  private:
@@ -990,6 +997,9 @@ struct MeshCall : gpu::CpuCall {
   clk::time_point t0;
   bool finished = false;
   std::string err;
+  ~MeshCall() override {
+    if (pm && cs && cs->remaining.load(std::memory_order_acquire) > 0) pm->abandon(cs);
+  }
   bool done() override {
     if (finished) return true;
     if (cs->remaining.load(std::memory_order_acquire) > 0) {
@@ -999,6 +1009,7 @@ struct MeshCall : gpu::CpuCall {
           try {
             pm->check_alive("reply", t0);
           } catch (const std::exception& e) {
+            pm->abandon(cs);  // late replies must not land in the batcher's reused buffer
             err = e.what();
             finished = true;
             return true;
@@ -1064,7 +1075,9 @@ bool ProgramModel::reap() {
     const int oc = cs.out_cols;
     const size_t n = size_t(pd.rows) * size_t(oc);
     double* out = cs.out + size_t(pd.row0) * size_t(oc);
-    if (load_acq(P.errf(0, k)) == seq) {
+    if (cs.abandoned) {
+      // the caller is gone: free the slot, write nothing
+    } else if (load_acq(P.errf(0, k)) == seq) {
       std::lock_guard<std::mutex> lk(cs.mu);
       if (cs.error.empty()) cs.error = std::string(P.err_text(0, k));
     } else if (L.src.size() == 1) {
@@ -1103,7 +1116,7 @@ gpu::CpuCallPtr ProgramModel::start_cpu(const double* X, int rows, int cols, dou
   const int chunks = std::max(1, (rows + mr - 1) / mr);
   cs->remaining.store(rows > 0 ? chunks : 0);
   const auto t0 = clk::now();
-  {
+  try {
     std::lock_guard<std::mutex> g(P.issue_mu);
     for (int ch = 0; ch < chunks && rows > 0; ++ch) {
       const int row0 = ch * mr, nr = std::min(mr, rows - row0);
@@ -1153,6 +1166,13 @@ gpu::CpuCallPtr ProgramModel::start_cpu(const double* X, int rows, int cols, dou
       }
       P.next = seq;
     }
+  } catch (...) {
+    // a peer is gone or stuck past the timeout: the program's ranks can no
+    // longer be kept in step, so the mesh closes (the supervisor restarts the
+    // gang); chunks already issued never touch `out`
+    abandon(cs);
+    m_->close();
+    throw;
   }
   auto c = std::make_shared<MeshCall>();
   c->pm = self_.lock();
