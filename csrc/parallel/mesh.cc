@@ -305,7 +305,7 @@ int Mesh::add_program(MeshProgram d) {
       throw std::runtime_error(where + ": only the final mean may run on rank 0");
     if (s.kind == kMeshMean)
       for (int j : s.inputs)
-        if (d.stages[size_t(j < 0 ? 0 : j)].out_cols != s.out_cols && j >= 0)
+        if ((j >= 0 ? d.stages[size_t(j)].out_cols : d.in_cols) != s.out_cols)
           throw std::runtime_error(where + ": mean over inputs of different widths");
   }
   P->d = std::move(d);
