@@ -56,6 +56,10 @@ std::shared_ptr<DeviceDriver> DeviceDriver::acquire(int device, bool shared) {
 }
 
 DeviceDriver::DeviceDriver(int device) : device_(device) {
+  if (device == kAsyncCpuDriver) {
+    const char* e = std::getenv("SCA_ASYNC_INLINE_HANDOFF");
+    inline_handoff_ = !e || std::atoi(e) != 0;
+  }
   if (const char* e = std::getenv("SCA_IDLE_SPIN_US")) idle_spin_us_ = std::max(0, std::atoi(e));
   ho_spin_us_ = idle_spin_us_;
   if (const char* e = std::getenv("SCA_HANDOFF_SPIN_US")) ho_spin_us_ = std::max(0, std::atoi(e));
@@ -77,6 +81,7 @@ DeviceDriver::~DeviceDriver() {
   }
   ho_cv_.notify_all();
   if (ho_th_.joinable()) ho_th_.join();
+  for (auto* p : inline_spare_) delete p;
 }
 
 int DeviceDriver::units() const {
@@ -240,6 +245,13 @@ void DeviceDriver::pump_loop() {
 }
 
 void DeviceDriver::push_handoff(BatchedUnit::Handoff&& h) {
+  if (inline_handoff_ && !h.fence) {  // (pump thread)
+    h.unit->post_responses(h, inline_spare_);
+    h.unit = nullptr;
+    std::lock_guard<std::mutex> g(ho_mu_);
+    ho_free_.push_back(std::move(h));
+    return;
+  }
   bool wake;
   {
     std::lock_guard<std::mutex> g(ho_mu_);

@@ -83,6 +83,12 @@ class DeviceDriver {
   bool ho_stop_ = false;                       // guarded by ho_mu_
   uint64_t ho_fences_pushed_ = 0, ho_fences_done_ = 0;  // guarded by ho_mu_
   std::atomic<bool> ho_pending_{false};
+  // The shared pump of asynchronous CPU units (mesh programs) posts their
+  // responses itself: their batches complete in the pump's done() poll with
+  // no device work to overlap, and a second thread would add a wake-up per
+  // batch (fences still go through the hand-off thread).
+  bool inline_handoff_ = false;
+  std::vector<BatchedUnit::Parcel*> inline_spare_;  // pump thread only
   std::thread pump_th_, ho_th_;
 };
 
