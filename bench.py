@@ -218,6 +218,11 @@ class Dist:
 
         self.torch = torch
         self.has_gpu = torch.cuda.is_available()
+        # SCA_BENCH_FOLD_GPUS=1: every rank on GPU 0 (a rehearsal of the
+        # multi-rank flow on a 1-GPU box -- not a scaling measurement; RCCL
+        # refuses two ranks on one device, so the collectives use gloo)
+        self.fold = os.environ.get("SCA_BENCH_FOLD_GPUS") == "1" and self.has_gpu
+        self.gpu_index = 0 if self.fold else self.local_rank
         self.dist = None
         self.backend = None
         if self.world > 1:
@@ -226,17 +231,17 @@ class Dist:
             import torch.distributed as dist
 
             if self.has_gpu:
-                torch.cuda.set_device(self.local_rank)
-            self.backend = backend or ("nccl" if self.has_gpu else "gloo")
+                torch.cuda.set_device(self.gpu_index)
+            self.backend = backend or ("nccl" if self.has_gpu and not self.fold else "gloo")
             dist.init_process_group(backend=self.backend,
                                     timeout=datetime.timedelta(seconds=max(30.0, budget.left())))
             self.dist = dist
-        self.device = self.local_rank if self.has_gpu else -1
+        self.device = self.gpu_index if self.has_gpu else -1
 
     def barrier(self):
         if self.dist is not None:
             if self.backend == "nccl":
-                self.dist.barrier(device_ids=[self.local_rank])
+                self.dist.barrier(device_ids=[self.gpu_index])
             else:
                 self.dist.barrier()
 
@@ -594,7 +599,7 @@ def variant_child(args) -> None:
         ngpu = sca.gpu_count()
         devs = list(range(args.span)) if ngpu > 0 else [-1] * args.span
         if ngpu and args.span > ngpu:
-            if not os.environ.get("SCA_BENCH_FOLD"):
+            if not (os.environ.get("SCA_BENCH_FOLD") or os.environ.get("SCA_BENCH_FOLD_GPUS")):
                 raise RuntimeError(f"{kind} needs {args.span} GPUs, {ngpu} visible")
             devs = [i % ngpu for i in devs]  # rehearsal on a smaller box: nodes fold onto the GPUs present
         cpus = bk.cpu_budget()
@@ -829,6 +834,8 @@ def fabric_child(args) -> None:
     budget = bk.Budget(args.deadline)
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev = int(os.environ.get("LOCAL_RANK", rank)) if torch.cuda.is_available() else -1
+    if dev >= 0 and os.environ.get("SCA_BENCH_FOLD_GPUS") == "1":
+        dev = 0  # rehearsal: every rank process on GPU 0 (the ipc mesh runs between them)
     if dev >= 0:
         torch.cuda.set_device(dev)
     dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(10.0, budget.left())))

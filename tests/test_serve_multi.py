@@ -9,7 +9,8 @@
   operator-built multi-component deployment
   (operator/controllers/seldondeployment_controller.go:253-392).
 
-Both run on CPU devices (device -1: fabric payloads over sockets)."""
+The CPU tests use device -1 (the mesh over shared memory); the gang test
+marked gpu runs every rank on GPU 0 (the mesh over HIP IPC)."""
 import json
 import os
 import signal
@@ -136,6 +137,43 @@ def test_rank_placed_spec_serves_through_the_cli(tmp_path):
         _stop(p)
     text = log.read_text()
     assert text.count("done:") == 2, text[-3000:]  # both peer ranks left their loops on rank 0's stop
+
+
+def test_python_transformer_and_model_on_worker_ranks_through_the_cli(tmp_path):
+    """Any node on any rank: a Python TRANSFORMER on rank
+    1 feeds the iris MODEL on rank 2; rank 0 only runs the front end."""
+    (tmp_path / "mymodels.py").write_text(
+        "import numpy as np\n"
+        "from seldon_core_amd.models import iris_logistic_regression\n"
+        "from seldon_core_amd.servers import SKLearnServer\n\n\n"
+        "class Iris(SKLearnServer):\n"
+        "    def __init__(self):\n"
+        "        super().__init__(model=iris_logistic_regression())\n\n\n"
+        "class Shift:\n"
+        "    def transform_input(self, X, names):\n"
+        "        return np.asarray(X, dtype=np.float64) * 0.5 + 1.0\n")
+    spec = {"name": "p", "componentSpecs": [{"spec": {"containers": []}}],
+            "graph": {"name": "t", "type": "TRANSFORMER", "rank": 1, "in_cols": 4,
+                      "children": [{"name": "m", "type": "MODEL", "rank": 2}]}}
+    p, hp, log = _start(tmp_path, spec, 3, extra=("--component", "t=mymodels.Shift", "--component", "m=mymodels.Iris"))
+    try:
+        assert _wait_log(log, "serving p:", 1), log.read_text()[-3000:]
+        text = log.read_text()
+        assert "mesh program" in text and "node:t@rank1" in text, text[-2000:]
+        from seldon_core_amd.models import iris_logistic_regression
+
+        lr = iris_logistic_regression()
+        rng = np.random.default_rng(1)
+        for i in range(30):
+            X = rng.normal(loc=4.0, scale=1.5, size=(1 + i % 5, 4))
+            out = _post(hp, "/api/v0.1/predictions", {"data": {"ndarray": X.tolist()}})
+            np.testing.assert_allclose(np.asarray(out["data"]["ndarray"]), lr.predict_proba(X * 0.5 + 1.0),
+                                       rtol=0, atol=1e-12)
+        assert _stop(p) == 0
+    finally:
+        _stop(p)
+    text = log.read_text()
+    assert text.count("done:") == 2, text[-3000:]
 
 
 def test_rank_placement_needs_enough_gpus(tmp_path):
