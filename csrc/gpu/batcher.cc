@@ -22,6 +22,33 @@ int device_count() {
 
 bool available() { return device_count() > 0; }
 
+bool large_bar(int device) {
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeIsLargeBar, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return v != 0;
+}
+
+namespace {
+// SCA_BATCH_INPUT=bar|host: where a zero-copy batch's rows are staged.
+// "bar" writes them into fine-grained HBM through the BAR (large-BAR devices
+// only), "host" leaves them in pinned host memory read over PCIe.
+bool bar_input_wanted(int device) {
+  const char* e = std::getenv("SCA_BATCH_INPUT");
+  const std::string v = e ? e : "host";
+  if (v != "bar") return false;
+  return large_bar(device);
+}
+
+// Write-combined stores into BAR-mapped memory (the caller drains them with
+// sfence before the launch: the kernel must see every byte).
+inline void bar_store(double* dst, const double* src, size_t n) {
+  std::memcpy(dst, src, n * sizeof(double));
+}
+}  // namespace
+
 namespace {
 
 int64_t now_ns() {
@@ -73,6 +100,7 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
   inject_fault(fault_from_env(opts_.device));
   device_io_ = model_->device_io_only();
   zc_input_ = model_->zero_copy_input();
+  bar_input_ = opts_.device >= 0 && opts_.device < device_count() && bar_input_wanted(opts_.device);
   segmented_ = model_->segmented();
   {
     auto info = std::make_shared<RespInfo>();
@@ -172,6 +200,8 @@ void BatchedUnit::ensure_capacity(Slot& s, int rows, int cols) {
     s.h_out.alloc(b);
     s.d_out.alloc(b, opts_.device);
   }
+  if (bar_input_ && need_in <= opts_.zero_copy_max_bytes && s.v_in.bytes() < need_in)
+    s.v_in.alloc(std::min(grow(s.v_in.bytes(), need_in), std::max(need_in, opts_.zero_copy_max_bytes)), opts_.device);
   const size_t ws = model_->workspace_bytes(rows, cols);
   if (s.ws.bytes() < ws) s.ws.alloc(grow(s.ws.bytes(), ws), opts_.device);
   s.cap_rows = std::max(s.cap_rows, size_t(rows));
@@ -384,13 +414,19 @@ bool BatchedUnit::launch(Slot* s) {
     // caller (who then frees the buffer) while the device may still read.
     const bool direct = s->items.size() == 1 && bin >= kDirectH2DBytes && !s->items[0].caller_mem;
     s->direct = direct;
+    const bool zc = !direct && opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes;
+    // zero-copy batches on a large-BAR device: rows straight into HBM
+    const bool bar = zc && bar_input_ && s->v_in.bytes() >= bin;
     if (!direct) {
+      double* dst = bar ? s->v_in.as<double>() : hin;
       size_t off = 0;
       for (const auto& it : s->items) {
         const size_t n = size_t(it.rows) * it.cols;
-        memcpy(hin + off, it.xp, n * sizeof(double));
+        if (bar) bar_store(dst + off, it.xp, n);
+        else memcpy(dst + off, it.xp, n * sizeof(double));
         off += n;
       }
+      if (bar) _mm_sfence();
     }
     hipStream_t st = s->stream.get();
     const int32_t* seg = nullptr;
@@ -408,12 +444,13 @@ bool BatchedUnit::launch(Slot* s) {
       if (seg) model_->launch_segments(x, rows, cols, y, s->ws.get(), seg, nseg, st);
       else model_->launch(x, rows, cols, y, s->ws.get(), st);
     };
-    if (!direct && opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes) {
+    if (zc) {
       // Output always zero-copy (written once); input zero-copy only if the
       // kernel reads each element once -- models that re-read X from many
-      // workgroups (tree chunks) get one DMA into HBM first.
-      const double* xin = s->h_in.dev<double>();
-      if (!zc_input_ && !model_->zero_copy_input_for(rows, cols)) {
+      // workgroups (tree chunks) get one DMA into HBM first.  Rows already
+      // written into HBM through the BAR need neither.
+      const double* xin = bar ? s->v_in.as<double>() : s->h_in.dev<double>();
+      if (!bar && !zc_input_ && !model_->zero_copy_input_for(rows, cols)) {
         err = hipMemcpyAsync(s->d_in.get(), hin, bin, hipMemcpyHostToDevice, st);
         xin = s->d_in.as<double>();
       }

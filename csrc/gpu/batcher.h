@@ -148,6 +148,7 @@ class BatchedUnit : public Unit {
   };
   struct Slot {
     PinnedBuffer h_in, h_out, h_seg;
+    BarBuffer v_in;  // SCA_BATCH_INPUT=bar: zero-copy batch rows in HBM, written by the CPU
     std::vector<double> cpu_out;  // device -1 (cpu_batching)
     std::vector<double> cpu_in;   // device -1, asynchronous models: the batch's rows back to back
     CpuCallPtr call;              // device -1: the batch's outstanding start_cpu() call
@@ -249,6 +250,7 @@ class BatchedUnit : public Unit {
   std::atomic<bool> running_{false};
   std::atomic<int64_t> inflight_rows_{0};
   bool device_io_ = false;  // model needs device-memory I/O (no zero-copy)
+  bool bar_input_ = false;  // SCA_BATCH_INPUT=bar on a large-BAR device
   bool zc_input_ = true;    // model reads X once per element (zero-copy input is cheaper than a DMA)
   bool segmented_ = false;
   bool cpu_ = false;        // device -1 with cpu_batching

@@ -122,6 +122,45 @@ class PinnedBuffer {
   size_t bytes_ = 0;
 };
 
+// Fine-grained device memory that the CPU writes through the PCIe BAR (the
+// MI355X exposes all of HBM to the host: large BAR).  A small batch's rows go
+// straight into HBM with write-combined stores, so the kernel's first loads
+// hit local memory instead of crossing PCIe (tools/micro/vram_probe.hip).
+// The CPU never reads it back (uncached reads over PCIe are slow).
+class BarBuffer {
+ public:
+  BarBuffer() = default;
+  ~BarBuffer() { reset(); }
+  BarBuffer(const BarBuffer&) = delete;
+  BarBuffer& operator=(const BarBuffer&) = delete;
+  void alloc(size_t bytes, int device) {
+    reset();
+    device_ = device;
+    bytes_ = bytes;
+    if (!bytes) return;
+    DeviceGuard g(device);
+    SCA_HIP_CHECK(hipExtMallocWithFlags(&ptr_, bytes, hipDeviceMallocFinegrained));
+  }
+  void reset() {
+    if (ptr_) {
+      DeviceGuard g(device_);
+      (void)hipFree(ptr_);
+    }
+    ptr_ = nullptr;
+    bytes_ = 0;
+  }
+  template <class T> T* as() const { return static_cast<T*>(ptr_); }
+  size_t bytes() const { return bytes_; }
+
+ private:
+  void* ptr_ = nullptr;
+  size_t bytes_ = 0;
+  int device_ = 0;
+};
+
+// True when the device's whole memory is CPU-visible (BarBuffer usable).
+bool large_bar(int device);
+
 class Stream {
  public:
   Stream() = default;
