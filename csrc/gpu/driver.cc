@@ -59,6 +59,8 @@ DeviceDriver::DeviceDriver(int device) : device_(device) {
   if (device == kAsyncCpuDriver) {
     const char* e = std::getenv("SCA_ASYNC_INLINE_HANDOFF");
     inline_handoff_ = !e || std::atoi(e) != 0;
+  } else if (const char* e = std::getenv("SCA_INLINE_HANDOFF")) {
+    inline_handoff_ = std::atoi(e) != 0;  // GPU / CPU pumps: post responses from the pump itself
   }
   if (const char* e = std::getenv("SCA_IDLE_SPIN_US")) idle_spin_us_ = std::max(0, std::atoi(e));
   ho_spin_us_ = idle_spin_us_;

@@ -46,13 +46,16 @@ class DeviceBuffer {
   DeviceBuffer& operator=(const DeviceBuffer&) = delete;
   DeviceBuffer(DeviceBuffer&& o) noexcept { swap(o); }
   DeviceBuffer& operator=(DeviceBuffer&& o) noexcept { reset(); swap(o); return *this; }
-  void alloc(size_t bytes, int device) {
+  // fine: fine-grained (coherent) device memory -- for buffers another GPU
+  // writes into over xGMI while this GPU's kernels read them
+  void alloc(size_t bytes, int device, bool fine = false) {
     reset();
     device_ = device;
     bytes_ = bytes;
     if (!bytes) return;
     DeviceGuard g(device);
-    SCA_HIP_CHECK(hipMalloc(&ptr_, bytes));
+    if (fine) SCA_HIP_CHECK(hipExtMallocWithFlags(&ptr_, bytes, hipDeviceMallocFinegrained));
+    else SCA_HIP_CHECK(hipMalloc(&ptr_, bytes));
     // Zero it (workspaces may hold counters that must start at 0) and WAIT:
     // hipMemset is queued on the null stream, which our non-blocking streams
     // do not order against, so a buffer grown mid-stream could be zeroed

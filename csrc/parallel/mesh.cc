@@ -446,7 +446,15 @@ std::string Mesh::prepare() {
       R.bytes = L.bytes;
       R.name = name;
       if (gpu() && rank_ != 0 && L.dev_bytes > 0) {
-        P.own_dev.alloc(L.dev_bytes, device_);
+        // Producers on other GPUs write these slabs over xGMI and this GPU's
+        // kernels then read them: fine-grained (coherent) memory keeps a line
+        // of an earlier use of the slot from being served out of this GPU's
+        // L2.  SCA_MESH_SLAB=coarse selects plain hipMalloc memory.
+        static const bool coarse = [] {
+          const char* e = std::getenv("SCA_MESH_SLAB");
+          return e && std::string(e) == "coarse";
+        }();
+        P.own_dev.alloc(L.dev_bytes, device_, !coarse);
         gpu::DeviceGuard g(device_);
         SCA_HIP_CHECK(hipIpcGetMemHandle(&h, P.own_dev.get()));
         R.dev = static_cast<char*>(P.own_dev.get());
