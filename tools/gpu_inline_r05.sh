@@ -6,6 +6,8 @@ set -o pipefail
 O=gpurun_out/r05l
 mkdir -p $O
 R=$GRAFT_REPO_ROOT
+timeout -k 10 60 ./tools/micro/xcd_l2_probe 50 > $O/xcd_l2_probe.txt 2>&1 || { cat $O/xcd_l2_probe.txt; exit 1; }
+cat $O/xcd_l2_probe.txt
 for m in xgb1000 iris; do
   for mode in host bar; do
     (cd /tmp && SCA_BATCH_INPUT=$mode SCA_BENCH_CLEAN_EXIT=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$R/$O/prof_${m}_$mode" -o run --output-format csv -- python "$R/bench.py" --model $m --steps 10 --warmup 3 --extras none > "$R/$O/prof_${m}_$mode.log" 2>&1) || exit 1
