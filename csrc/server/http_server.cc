@@ -6,6 +6,8 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+
+#include <deque>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -187,7 +189,7 @@ struct Completion {
   bool has_outcome = false;
   Outcome outcome;
   int kind = 0;  // 0 external predict, 1 internal call
-  std::string uri;
+  const std::string* uri = nullptr;  // interned by the worker (Worker::intern)
   Clock::time_point t0;
 };
 
@@ -225,7 +227,7 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
   std::unordered_map<std::string, Series*> timers;
   Series* last_timer = nullptr;
   int last_status = 0;
-  std::string last_uri;
+  const std::string* last_uri = nullptr;
 
   ~Worker() {
     for (auto& kv : conns)
@@ -235,15 +237,32 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
     if (epfd >= 0) ::close(epfd);
   }
 
-  Series* server_timer(const std::string& uri, int status) {
-    // hot path: the last (uri, status) seen by this worker, without building a key
-    if (last_timer && status == last_status && uri == last_uri) return last_timer;
+  // Request paths seen by this worker, interned so a request's completion
+  // carries a pointer instead of two heap copies of the path.  Bounded: past
+  // kMaxUris distinct paths the rest share one "other" entry (metrics label).
+  static constexpr size_t kMaxUris = 64;
+  std::deque<std::string> uris;
+  const std::string* intern(std::string_view path) {
+    for (const auto& u : uris)
+      if (u == path) return &u;
+    if (uris.size() >= kMaxUris) {
+      static const std::string other = "other";
+      return &other;
+    }
+    uris.emplace_back(path);
+    return &uris.back();
+  }
+
+  Series* server_timer(const std::string* up, int status) {
+    // hot path: the last (uri, status) seen by this worker (interned: a pointer compare)
+    if (last_timer && status == last_status && up == last_uri) return last_timer;
+    const std::string& uri = *up;
     std::string key = uri + "#" + std::to_string(status);
     auto it = timers.find(key);
     if (it != timers.end()) {
       last_timer = it->second;
       last_status = status;
-      last_uri = uri;
+      last_uri = up;
       return it->second;
     }
     Labels l = {{"deployment_name", srv->engine_->options().deployment_name},
@@ -258,6 +277,9 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
                 {"uri", uri}};
     Series* s = srv->engine_->metrics().timer("seldon_api_engine_server_requests", std::move(l), true);
     timers.emplace(key, s);
+    last_timer = s;
+    last_status = status;
+    last_uri = up;
     return s;
   }
 
@@ -683,10 +705,10 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
       } else {
         body = "{}";
       }
-      if (d.kind == 0) server_timer(d.uri, status)->observe_seconds(std::chrono::duration<double>(Clock::now() - d.t0).count());
+      if (d.kind == 0 && d.uri) server_timer(d.uri, status)->observe_seconds(std::chrono::duration<double>(Clock::now() - d.t0).count());
       write_response(c, status, "application/json", body, d.keep_alive);
     } else {
-      if (d.kind == 0 && !d.uri.empty())
+      if (d.kind == 0 && d.uri)
         server_timer(d.uri, d.status)->observe_seconds(std::chrono::duration<double>(Clock::now() - d.t0).count());
       write_response(c, d.status, d.ctype, d.body, d.keep_alive);
     }
@@ -721,7 +743,7 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
 
   void predict_external(Conn* c, const Request& rq) {
     const auto t0 = Clock::now();
-    std::string uri(rq.path);
+    const std::string* uri = intern(rq.path);
     auto msg = std::make_shared<SeldonMessage>();
     Json j;
     std::string err;
@@ -767,7 +789,7 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
 
   void feedback_external(Conn* c, const Request& rq) {
     const auto t0 = Clock::now();
-    std::string uri(rq.path);
+    const std::string* uri = intern(rq.path);
     auto fb = std::make_shared<Feedback>();
     try {
       Json j = parse_json(rq.body);

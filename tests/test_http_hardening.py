@@ -106,3 +106,24 @@ def test_negative_shape_protobuf_rejected():
     msg = b"\x1a" + bytes([len(dd)]) + dd
     with pytest.raises(Exception):
         C.pb_to_json(msg)
+
+
+def test_distinct_gateway_paths_do_not_grow_metric_series_without_bound(server):
+    """Gateway-prefixed predict paths are client-chosen: the per-uri request
+    timer keeps at most 64 distinct uri labels per front-end worker (the rest
+    are counted under uri="other")."""
+    dep, h = server
+    body = json.dumps({"data": {"ndarray": [[5.1, 3.5, 1.4, 0.2]]}}).encode()
+    for i in range(300):
+        req = urllib.request.Request(f"http://127.0.0.1:{h.http_port}/seldon/ns{i}/p/api/v0.1/predictions", data=body,
+                                     headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=10) as r:
+            assert r.status == 200
+    with urllib.request.urlopen(f"http://127.0.0.1:{h.http_port}/prometheus", timeout=10) as r:
+        text = r.read().decode()
+    uris = {line.split('uri="')[1].split('"')[0] for line in text.splitlines()
+            if line.startswith("seldon_api_engine_server_requests") and 'uri="' in line}
+    assert any(u.startswith("/seldon/ns") for u in uris)
+    assert len([u for u in uris if u.startswith("/seldon/ns")]) <= 2 * 64  # two front-end threads
+    assert "other" in uris
+    _ok(h.http_port)
