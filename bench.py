@@ -452,6 +452,16 @@ def headline(args, d: Dist, rep: Reporter, budget: bk.Budget, per_rank_cpus: flo
     else:
         span = SPAN.get(args.graph, max(2, d.world))
         devs = [(d.device + i) % ngpu for i in range(span)] if ngpu else [-1] * span
+    lg_cores = int(os.environ.get("SCA_BENCH_LG_CORES", "0") or 0)
+    if lg_cores > 0 and pinned and len(pinned) % 2 == 0 and 2 * lg_cores < len(pinned):
+        # placement A/B: the load generator on the last `lg_cores` cores (both
+        # SMT threads), the server's threads -- created below -- on the rest
+        # of the rank's CCD.  pinned = [cores..., their siblings...]
+        half = len(pinned) // 2
+        cores, sibs = pinned[:half], pinned[half:]
+        lg = cores[half - lg_cores:] + sibs[half - lg_cores:]
+        os.environ["SCA_LOADGEN_CPUS"] = ",".join(map(str, lg))
+        os.sched_setaffinity(0, [c for c in pinned if c not in lg])
     dep, oracle, label = bk.make_deployment(wl, args.graph, devs, d.device, args.slots, not args.no_spin)
     if args.graph != "single":
         if not wl.impl:

@@ -18,6 +18,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <nghttp2/nghttp2.h>
+#include <sched.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -436,6 +437,19 @@ int main(int argc, char** argv) {
     else if (k == "--expect-file") a.expect = read_file(v());
     else if (k == "--check-every") a.check_every = std::max(1L, std::stol(v()));
     else if (k == "--spin-us") a.spin_us = std::max(0, std::stoi(v()));
+    else if (k == "--cpus") {  // comma-separated CPU ids: pin this process (bench placement A/B)
+      cpu_set_t set;
+      CPU_ZERO(&set);
+      const std::string list = v();
+      size_t pos = 0;
+      while (pos < list.size()) {
+        const size_t e = list.find(',', pos);
+        CPU_SET(std::stoi(list.substr(pos, e == std::string::npos ? std::string::npos : e - pos)), &set);
+        if (e == std::string::npos) break;
+        pos = e + 1;
+      }
+      if (sched_setaffinity(0, sizeof set, &set) != 0) { perror("sched_setaffinity"); return 2; }
+    }
     else { fprintf(stderr, "unknown arg %s\n", k.c_str()); return 2; }
   }
   if (!body_file.empty()) a.body = read_file(body_file);

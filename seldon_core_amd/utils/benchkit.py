@@ -450,6 +450,8 @@ def run_loadgen(port: int, steps: int, warmup: int, api: str, body, users: int, 
     spin = int(os.environ.get("SCA_LOADGEN_SPIN_US", "0") or 0)
     if spin > 0:
         cmd += ["--spin-us", str(spin)]
+    if os.environ.get("SCA_LOADGEN_CPUS"):  # set by bench.py's SCA_BENCH_LG_CORES placement A/B
+        cmd += ["--cpus", os.environ["SCA_LOADGEN_CPUS"]]
     tmp = []
     if api == "rest":
         cmd += ["--mode", "rest", "--path", path, "--body", body]
