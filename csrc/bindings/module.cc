@@ -8,6 +8,7 @@
 
 #include "../core/cpuprof.h"
 #include "../core/engine.h"
+#include "../core/pool_executor.h"
 #include "../core/json.h"
 #include "../core/message.h"
 #include "../core/msglog.h"
@@ -852,9 +853,10 @@ PYBIND11_MODULE(_C, m) {
              std::vector<std::pair<std::string, std::string>> hv;
              for (const auto& kv : headers)
                if (e.is_route_header(kv.first)) hv.emplace_back(kv.first, kv.second);
+             // continuations on the shared pool, never on a GPU pump (pool_executor.h)
              Outcome o = wait_outcome([&](Done k) {
-               if (hv.empty()) e.predict(msg, std::move(k));
-               else e.predict_with_headers(msg, std::move(k), nullptr, hv);
+               if (hv.empty()) e.predict(msg, std::move(k), PoolExecutor::shared());
+               else e.predict_with_headers(msg, std::move(k), PoolExecutor::shared(), hv);
              });
              return render(o);
            },
@@ -866,7 +868,7 @@ PYBIND11_MODULE(_C, m) {
                auto err = make_error(ApiError::INVALID_JSON, "invalid protobuf");
                return py::make_tuple(err->http_status, py::bytes(error_to_json(*err)));
              }
-             Outcome o = wait_outcome([&](Done k) { e.predict(msg, std::move(k)); });
+             Outcome o = wait_outcome([&](Done k) { e.predict(msg, std::move(k), PoolExecutor::shared()); });
              if (o.err) return py::make_tuple(o.err->http_status, py::bytes(error_to_json(*o.err)));
              std::string out;
              message_to_pb(*o.msg, out);

@@ -127,3 +127,50 @@ def test_gpu_abtest_two_devices_or_one():
         assert seen == {0, 1}
     finally:
         dep.close()
+
+
+def test_python_api_graph_never_continues_on_the_gpu_pump():
+    """Deployment.predict (no front-end thread): the Python OUTPUT_TRANSFORMER
+    after the GPU model calls a device Mahalanobis detector synchronously; that
+    detector's batcher shares GPU 0's pump with the model.  The continuation
+    must run on the shared pool (csrc/core/pool_executor.h), not on the pump
+    that would then wait for itself."""
+    import seldon_core_amd as sca
+    from seldon_core_amd.models import iris_logistic_regression
+    from seldon_core_amd.servers import SKLearnServer
+
+    C = sca.native()
+    det = C.MahalanobisDevice(3, 2, 3.0, 50.0, -1.0, 1e-8, 0)
+
+    class Post:
+        def transform_output(self, X, names):
+            X = np.asarray(X, dtype=np.float64)
+            det.step(X)  # synchronous device call (run_ptr) on GPU 0's pump
+            return X
+
+    clf = iris_logistic_regression()
+    spec = {"name": "p", "graph": {"name": "post", "type": "OUTPUT_TRANSFORMER", "children": [
+        {"name": "classifier", "type": "MODEL", "implementation": "SKLEARN_SERVER", "modelUri": "memory://iris"}]}}
+    dep = sca.Deployment(spec, components={"classifier": SKLearnServer(model=clf), "post": Post()}, device=0)
+    try:
+        assert dep.engine.unit_kind("classifier") == "gpu:linear"
+        out, err = {}, []
+
+        def call():
+            try:
+                for i in range(20):
+                    X = np.random.default_rng(i).normal(loc=4.0, scale=1.0, size=(1 + i % 3, 4))
+                    r = dep.predict({"data": {"ndarray": X.tolist()}})
+                    np.testing.assert_allclose(np.asarray(r["data"]["ndarray"]), clf.predict_proba(X),
+                                               rtol=0, atol=1e-12)
+                out["ok"] = True
+            except Exception as e:  # noqa: BLE001
+                err.append(repr(e))
+
+        th = threading.Thread(target=call, daemon=True)
+        th.start()
+        th.join(60)
+        assert not th.is_alive(), "Deployment.predict deadlocked on the GPU pump"
+        assert err == [] and out.get("ok"), err
+    finally:
+        dep.close()
