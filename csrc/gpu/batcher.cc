@@ -415,8 +415,10 @@ bool BatchedUnit::launch(Slot* s) {
     const bool direct = s->items.size() == 1 && bin >= kDirectH2DBytes && !s->items[0].caller_mem;
     s->direct = direct;
     const bool zc = !direct && opts_.zero_copy && !device_io_ && bin + bout <= opts_.zero_copy_max_bytes;
-    // zero-copy batches on a large-BAR device: rows straight into HBM
-    const bool bar = zc && bar_input_ && s->v_in.bytes() >= bin;
+    // zero-copy batches on a large-BAR device: rows straight into HBM -- for
+    // kernels that read each row once (fine-grained HBM is not L2-cached, so
+    // models that re-read X from many workgroups keep their DMA into d_in)
+    const bool bar = zc && bar_input_ && s->v_in.bytes() >= bin && (zc_input_ || model_->zero_copy_input_for(rows, cols));
     if (!direct) {
       double* dst = bar ? s->v_in.as<double>() : hin;
       size_t off = 0;
