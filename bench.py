@@ -177,16 +177,17 @@ def spawn_ranks(n: int, argv) -> int:
 # ------------------------------------------------------------------ sizing
 def size_threads(args, per_rank: float) -> float:
     """Split the CPU share of one rank between the front end (~60%), the
-    closed-loop load generator (~25%) and the GPU device / hand-off threads
-    (measured on a 16-CPU MI355X share: 10 front-end / 5 generator threads
-    was the best split unpinned, profiles/r01f_sweep_executor; pinned to one
-    CCD, 10 / 4 serves 1.44M vs 1.38M REST pred/s with p99 0.29-0.35 vs
-    0.46-1.08 ms, and gRPC 2.10M vs 1.99M, profiles/r02v_threads)."""
+    closed-loop load generator (~30%) and the GPU pump thread.  On a 16-CPU
+    MI355X share pinned to one CCD, with responses posted from the pump
+    (round 5): 10 front-end / 5 generator threads serve 1.705-1.715M REST
+    pred/s (p99 0.23-0.29 ms) against 1.57-1.59M at 10 / 4, 1.62-1.63M at
+    11 / 5 and 1.66M at 10 / 6 (profiles/r05x_threads; round 2 had found 10 / 4
+    best before the hand-off thread went, profiles/r02v_threads)."""
     per_rank = max(2.0, per_rank)
     if args.server_threads is None:
         args.server_threads = max(1, min(16, int(round(per_rank * 0.6))))
     if args.client_threads is None:
-        args.client_threads = max(1, min(10, int(round(per_rank * 0.25))))
+        args.client_threads = max(1, min(10, int(round(per_rank * 0.3125))))
     return per_rank
 
 
