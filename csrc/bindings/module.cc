@@ -853,7 +853,7 @@ PYBIND11_MODULE(_C, m) {
              std::vector<std::pair<std::string, std::string>> hv;
              for (const auto& kv : headers)
                if (e.is_route_header(kv.first)) hv.emplace_back(kv.first, kv.second);
-             // continuations on the shared pool, never on a GPU pump (pool_executor.h)
+             // continuations on the shared pool, off the GPU pumps (pool_executor.h)
              Outcome o = wait_outcome([&](Done k) {
                if (hv.empty()) e.predict(msg, std::move(k), PoolExecutor::shared());
                else e.predict_with_headers(msg, std::move(k), PoolExecutor::shared(), hv);

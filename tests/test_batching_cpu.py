@@ -139,3 +139,59 @@ def test_loadgen_storm_through_shards_handoff_and_parcels():
     finally:
         h.stop()
         dep.close()
+
+
+def test_python_api_nested_predictions():
+    """A Python node that synchronously calls ANOTHER deployment's predict,
+    from 8 concurrent Python-API callers; both models are CPU-batched units
+    whose completions are posted to the shared continuation pool
+    (csrc/core/pool_executor.h).  Every answer matches sklearn."""
+    import threading
+
+    import numpy as np
+
+    import seldon_core_amd as sca
+    from seldon_core_amd.models import iris_logistic_regression
+    from seldon_core_amd.servers import SKLearnServer
+
+    clf = iris_logistic_regression()
+    inner = sca.Deployment({"name": "inner", "graph": {"name": "m", "type": "MODEL"}},
+                           components={"m": SKLearnServer(model=clf)}, device=-1,
+                           batcher={"cpu_batching": True, "slots": 2})
+
+    def pad(P):  # 3 class probabilities -> 4 iris-scale features
+        P = np.asarray(P, dtype=np.float64)
+        return np.hstack([P * 5.0, np.ones((P.shape[0], 1))])
+
+    class Post:
+        def transform_output(self, X, names):
+            r = inner.predict({"data": {"ndarray": pad(X).tolist()}})
+            return np.asarray(r["data"]["ndarray"])
+
+    outer = sca.Deployment({"name": "outer", "graph": {"name": "post", "type": "OUTPUT_TRANSFORMER", "children": [
+        {"name": "m", "type": "MODEL"}]}}, components={"m": SKLearnServer(model=clf), "post": Post()}, device=-1,
+        batcher={"cpu_batching": True, "slots": 4, "max_batch": 2})  # one request per batch: parallel continuations
+    try:
+        errs, done = [], []
+
+        def call(t):
+            try:
+                for i in range(10):
+                    X = np.random.default_rng(t * 100 + i).normal(loc=4.0, size=(2, 4))
+                    out = outer.predict({"data": {"ndarray": X.tolist()}})
+                    want = clf.predict_proba(pad(clf.predict_proba(X)))
+                    np.testing.assert_allclose(np.asarray(out["data"]["ndarray"]), want, rtol=0, atol=1e-12)
+                done.append(t)
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=call, args=(t,), daemon=True) for t in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert not any(t.is_alive() for t in th), "nested Python-API predictions deadlocked"
+        assert errs == [] and len(done) == 8, errs[:3]
+    finally:
+        outer.close()
+        inner.close()

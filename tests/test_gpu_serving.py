@@ -129,12 +129,13 @@ def test_gpu_abtest_two_devices_or_one():
         dep.close()
 
 
-def test_python_api_graph_never_continues_on_the_gpu_pump():
+def test_python_api_graph_with_a_device_call_inside_a_python_node():
     """Deployment.predict (no front-end thread): the Python OUTPUT_TRANSFORMER
     after the GPU model calls a device Mahalanobis detector synchronously; that
-    detector's batcher shares GPU 0's pump with the model.  The continuation
-    must run on the shared pool (csrc/core/pool_executor.h), not on the pump
-    that would then wait for itself."""
+    detector's batcher shares GPU 0's pump with the model.  The request's
+    continuations run on the shared pool (csrc/core/pool_executor.h) and the
+    Python node on its own unit thread, so the pump stays free to run the
+    nested device call."""
     import seldon_core_amd as sca
     from seldon_core_amd.models import iris_logistic_regression
     from seldon_core_amd.servers import SKLearnServer
@@ -170,7 +171,7 @@ def test_python_api_graph_never_continues_on_the_gpu_pump():
         th = threading.Thread(target=call, daemon=True)
         th.start()
         th.join(60)
-        assert not th.is_alive(), "Deployment.predict deadlocked on the GPU pump"
+        assert not th.is_alive(), "Deployment.predict did not finish"
         assert err == [] and out.get("ok"), err
     finally:
         dep.close()
