@@ -16,6 +16,11 @@
 //                                  path (cpu_batching): per-thread submission shards,
 //                                  device thread, hand-off thread, recycled response
 //                                  parcels posted to 8 executors by 8 producer threads
+//   core_stress mesh <requests>    a CPU gang's mesh (csrc/parallel/mesh.cc) with rank 0
+//                                  and rank 1 in this one process: 8 producer threads
+//                                  through a cpu_batching unit over the program model
+//                                  (async pump, chunked issue, reap, doorbells), the
+//                                  worker's program thread, and calls abandoned mid-flight
 //
 // Exit status 0 = every check passed; sanitizer reports make it non-zero.
 #include <unistd.h>
@@ -35,8 +40,12 @@
 #include <functional>
 #include <mutex>
 
+#include <sys/socket.h>
+
 #include "core/engine.h"
 #include "gpu/batcher.h"
+#include "kernels/kernels.h"
+#include "parallel/mesh.h"
 #include "core/json.h"
 #include "core/message.h"
 #include "core/spec.h"
@@ -354,7 +363,127 @@ void batcher_mode(int n) {
   std::cout << "batches " << st.batches << " requests " << st.requests << std::endl;
 }
 
+void mesh_mode(int n) {
+  // control sockets: rank 0 holds one end per worker, the worker the other
+  int sp[2];
+  check(socketpair(AF_UNIX, SOCK_STREAM, 0, sp) == 0, "socketpair");
+  constexpr int kSlots = 4;
+  auto m0 = std::make_shared<par::Mesh>(0, 2, -1, std::vector<int>{-1, sp[0]}, kSlots);
+  auto m1 = std::make_shared<par::Mesh>(1, 2, -1, std::vector<int>{sp[1], -1}, kSlots);
+  par::MeshProgram prog;
+  prog.max_rows = 16;  // small: multi-row batches are issued in chunks
+  prog.in_cols = 4;
+  par::MeshStage st;
+  st.rank = 1;
+  st.kind = par::kMeshModel;
+  st.inputs = {-1};
+  st.in_cols = 4;
+  st.out_cols = 3;
+  st.node = "fake";
+  prog.stages.push_back(st);
+  m0->add_program(prog);
+  m1->add_program(prog);
+  m1->set_model(0, 0, std::make_shared<FakeRowModel>());
+  const std::vector<std::string> blobs{m0->prepare(), m1->prepare()};
+  m0->connect(blobs);
+  m1->connect(blobs);
+  m0->unlink();
+  m1->unlink();
+  m1->start();
+  m0->start();
+  gpu::BatcherOptions o;
+  o.device = -1;
+  o.cpu_batching = true;
+  o.slots = kSlots;
+  o.max_batch = 64;
+  auto unit = std::make_shared<gpu::BatchedUnit>(m0->program_model(0, {}, false), o);
+  constexpr int kThreads = 8;
+  std::vector<ExecPtr> execs;
+  for (int i = 0; i < kThreads; ++i) execs.push_back(std::make_shared<ThreadExecutor>());
+  std::atomic<int> done{0}, wrong{0};
+  std::vector<std::thread> producers;
+  const std::string puid = "stress";
+  for (int t = 0; t < kThreads; ++t) {
+    producers.emplace_back([&, t] {
+      std::mt19937 rng(4321 + t);
+      for (int i = 0; i < n; ++i) {
+        const int rows = 1 + int(rng() % 5);
+        auto m = std::make_shared<SeldonMessage>();
+        m->payload = Payload::Data;
+        std::vector<double> vals;
+        for (int r = 0; r < rows; ++r) {
+          const double id = double(t) * 1e6 + i * 10 + r;
+          vals.insert(vals.end(), {1.0 * r, 0.5, 0.25, id});
+        }
+        m->data.set_dense(DataKind::Tensor, {int64_t(rows), 4}, std::move(vals));
+        const ExecPtr* ex = (i % 3 == 0) ? nullptr : &execs[size_t((t + i) % kThreads)];
+        CallCtx c{nullptr, &puid, ex};
+        unit->transform_input(c, m, [&, t, i, rows](Outcome out) {
+          bool ok = !out.err && out.msg && out.msg->data.values.size() == size_t(rows) * 3;
+          if (ok)
+            for (int r = 0; r < rows; ++r) {
+              const double id = double(t) * 1e6 + i * 10 + r;
+              const double* y = out.msg->data.values.data() + r * 3;
+              ok = ok && y[0] == 1.0 * r + 0.75 + id && y[1] == 2.0 * r && y[2] == id;
+            }
+          if (!ok) wrong.fetch_add(1);
+          done.fetch_add(1);
+        });
+      }
+    });
+  }
+  // direct callers of the program model on the side, half of them giving up
+  // mid-flight (their batches complete and free their slots, `out` untouched)
+  auto pm = m0->program_model(0, {}, false);
+  std::atomic<int> direct_ok{0};
+  std::thread side([&] {
+    std::vector<double> x(4 * 7), y(3 * 7);
+    for (int i = 0; i < n / 4; ++i) {
+      for (int r = 0; r < 7; ++r) {
+        x[size_t(r) * 4 + 0] = r;
+        x[size_t(r) * 4 + 1] = 0.5;
+        x[size_t(r) * 4 + 2] = 0.25;
+        x[size_t(r) * 4 + 3] = 7e6 + i;
+      }
+      auto call = pm->start_cpu(x.data(), 7, 4, y.data());
+      if (i % 2) {
+        call.reset();  // abandoned
+        continue;
+      }
+      while (!call->done()) call->wait_us(100);
+      bool ok = call->error().empty();
+      for (int r = 0; r < 7 && ok; ++r) ok = y[size_t(r) * 3 + 2] == 7e6 + i && y[size_t(r) * 3 + 1] == 2.0 * r;
+      if (ok) direct_ok.fetch_add(1);
+    }
+  });
+  for (auto& p : producers) p.join();
+  side.join();
+  for (int spin = 0; done.load() < kThreads * n && spin < 60000; ++spin)
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  const auto stu = unit->stats();
+  unit->stop();
+  execs.clear();
+  m0->stop_peers();
+  m1->join();
+  const auto ms = m1->stats();
+  check(done.load() == kThreads * n, "every mesh request answered exactly once");
+  check(wrong.load() == 0, "every mesh request got its own rows back");
+  check(direct_ok.load() == (n / 4 + 1) / 2, "every direct (not abandoned) call got its rows");
+  check(m0->error().empty() && m1->error().empty(), "no mesh error");
+  check(stu.batches < stu.requests, "mesh requests shared batches");
+  std::cout << "mesh batches " << ms.batches << " rows " << ms.rows << " max_inflight " << ms.max_inflight << std::endl;
+  ::close(sp[0]);
+  ::close(sp[1]);
+}
+
 }  // namespace
+
+// The mesh's GPU-gang path references two device helpers; a CPU gang never
+// calls them, and the sanitizer build has no device code.
+namespace sca::kern {
+void combine_mean_f64(const double* const*, int, int64_t, double*, hipStream_t) { std::abort(); }
+void device_delay_us(int, hipStream_t) { std::abort(); }
+}  // namespace sca::kern
 
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "engine";
@@ -369,8 +498,10 @@ int main(int argc, char** argv) {
     serve_mode();
   } else if (mode == "batcher") {
     batcher_mode(n);
+  } else if (mode == "mesh") {
+    mesh_mode(n);
   } else {
-    std::cerr << "usage: core_stress fuzz|engine|serve|batcher [n]\n";
+    std::cerr << "usage: core_stress fuzz|engine|serve|batcher|mesh [n]\n";
     return 2;
   }
   if (fails) {

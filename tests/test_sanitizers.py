@@ -30,7 +30,7 @@ def _clean(stderr: str) -> bool:
             and "WARNING: ThreadSanitizer" not in stderr and "ERROR: LeakSanitizer" not in stderr)
 
 
-@pytest.mark.parametrize("mode,n", [("fuzz", "2000"), ("engine", "3000"), ("batcher", "2000")])
+@pytest.mark.parametrize("mode,n", [("fuzz", "2000"), ("engine", "3000"), ("batcher", "2000"), ("mesh", "600")])
 def test_core_stress(stress_exe, mode, n):
     exe, kind = stress_exe
     r = subprocess.run([exe, mode, n], capture_output=True, text=True, timeout=600, env=SAN_ENV)

@@ -35,6 +35,7 @@ SOURCES = [
     "server/http_server.cc", "server/grpc_server.cc", "server/remote_unit.cc",
     "gpu/batcher.cc",  # host machinery only: the stress driver runs it on its CPU path
     "gpu/driver.cc",
+    "parallel/mesh.cc",  # CPU gangs (shared memory); the GPU path is not exercised here
     "tests/core_stress.cc",
 ]
 FLAGS = {
