@@ -1,7 +1,7 @@
 # Round-5 close-out on one MI355X: the full GPU suite, smoke(), the default
 # headline bench, and the folded 2-rank rehearsal of the driver's multi-GPU run.
 set -o pipefail
-O=gpurun_out/r05t
+O=gpurun_out/${R05_OUT:-r05t}
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
