@@ -175,3 +175,41 @@ def test_python_api_graph_with_a_device_call_inside_a_python_node():
         assert err == [] and out.get("ok"), err
     finally:
         dep.close()
+
+
+@pytest.mark.parametrize("model", ["iris", "xgb1000"])
+def test_bar_staged_rows_match_the_cpu_oracle(monkeypatch, model):
+    """SCA_BATCH_INPUT=bar: the CPU writes each zero-copy batch into
+    fine-grained HBM through the PCIe BAR (csrc/gpu/batcher.cc) and the
+    kernel reads it there.  Answers must match the CPU oracle under
+    concurrency (slots and their BAR buffers reused)."""
+    import seldon_core_amd as sca
+    from seldon_core_amd.utils import benchkit as bk
+
+    monkeypatch.setenv("SCA_BATCH_INPUT", "bar")
+    wl = bk.Workload(model)
+    dep = sca.Deployment({"name": "p", "graph": {"name": "m", "type": "MODEL"}}, components={"m": wl.comp},
+                         device=0)
+    try:
+        errs, worst = [], [0.0]
+        cols = len(wl.row)
+
+        def client(t):
+            rng = np.random.default_rng(100 + t)
+            for i in range(40):
+                X = np.asarray(wl.row) + rng.normal(scale=0.5, size=(1 + (i + t) % 5, cols))
+                try:
+                    out = np.asarray(dep.predict({"data": {"ndarray": X.tolist()}})["data"]["ndarray"], dtype=float)
+                    worst[0] = max(worst[0], float(np.abs(out.reshape(len(X), -1) - wl.oracle(X)).max()))
+                except Exception as e:  # noqa: BLE001
+                    errs.append(repr(e))
+
+        th = [threading.Thread(target=client, args=(t,)) for t in range(6)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert errs == [], errs[:3]
+        assert worst[0] < 1e-9, worst[0]
+    finally:
+        dep.close()
