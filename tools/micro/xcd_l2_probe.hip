@@ -1,6 +1,11 @@
 // Does an XCD's L2 keep a kernel's data for the NEXT launch?
 //
-//   xcd_l2_probe [launches]
+//   xcd_l2_probe [launches] [slice_kb]
+//
+// slice_kb (default 256): each launch chases through EVERY line of its slice,
+// so the data one XCD touches per launch is the slice, and 8 x slice_kb is the
+// rotating working set (> 4 MB from slice_kb = 1024: the rot modes then miss
+// the XCD's L2 by construction, the same modes still fit it).
 //
 // The tree kernels re-read the same ~3 MB ensemble on every batch; whether a
 // launch finds it in its XCD's 4 MB L2 or must go to the Infinity Cache / HBM
@@ -36,21 +41,20 @@
     }                                                              \
   } while (0)
 
-constexpr int kSliceBytes = 256 << 10;
 constexpr int kLineWords = 32;  // 128-B lines of uint32
-constexpr int kSliceWords = kSliceBytes / 4;
-constexpr int kHops = 256;
 constexpr int kBlocks = 64;     // 8 per XCD
+int g_slice_words = (256 << 10) / 4;
 
-__global__ __launch_bounds__(64) void chase(const uint32_t* __restrict__ buf, int rot, unsigned long long* out) {
+__global__ __launch_bounds__(64) void chase(const uint32_t* __restrict__ buf, int rot, int slice_words, int hops,
+                                            unsigned long long* out) {
   uint32_t xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   xcc &= 7u;
-  const uint32_t* base = buf + size_t((xcc + uint32_t(rot)) & 7u) * kSliceWords;
+  const uint32_t* base = buf + size_t((xcc + uint32_t(rot)) & 7u) * size_t(slice_words);
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();
     uint32_t i = 0;
-    for (int h = 0; h < kHops; ++h) i = base[i];
+    for (int h = 0; h < hops; ++h) i = base[i];
     const unsigned long long t1 = wall_clock64();
     out[blockIdx.x * 2] = (t1 - t0) + (i == 0xffffffffu ? 1ull : 0ull);
     out[blockIdx.x * 2 + 1] = xcc;
@@ -64,6 +68,11 @@ __global__ void scribble(uint4* p, size_t n) {
 
 int main(int argc, char** argv) {
   const int launches = argc > 1 ? std::atoi(argv[1]) : 50;
+  const int slice_kb = argc > 2 ? std::atoi(argv[2]) : 256;
+  if (slice_kb < 4 || slice_kb > 8192) { std::printf("slice_kb 4..8192\n"); return 2; }
+  g_slice_words = slice_kb * 1024 / 4;
+  const int kSliceWords = g_slice_words;
+  const int kHops = kSliceWords / kLineWords;  // every line of the slice once per launch
   CK(hipSetDevice(0));
   // eight slices, each one random cycle over its lines
   std::vector<uint32_t> h(size_t(8) * kSliceWords, 0);
@@ -98,7 +107,7 @@ int main(int argc, char** argv) {
     int xcc_seen = 0;
     for (int l = 0; l < launches; ++l) {
       if (evict) scribble<<<1024, 256, 0, st>>>(big, big_n);
-      chase<<<kBlocks, 64, 0, st>>>(buf, rotate ? l : 0, out);
+      chase<<<kBlocks, 64, 0, st>>>(buf, rotate ? l : 0, kSliceWords, kHops, out);
       if (sync || evict || l == launches - 1) CK(hipStreamSynchronize(st));
       if (sync || evict) {
         if (l > 0) v.push_back(ns_per_hop());
@@ -109,8 +118,8 @@ int main(int argc, char** argv) {
     }
     if (v.empty()) v.push_back(ns_per_hop());  // back to back: the last launch
     std::sort(v.begin(), v.end());
-    std::printf("{\"mode\": \"%s\", \"ns_per_hop_p50\": %.1f, \"ns_per_hop_min\": %.1f, \"ns_per_hop_max\": %.1f, "
-                "\"xccs_seen\": %d}\n", name, v[v.size() / 2], v.front(), v.back(), xcc_seen);
+    std::printf("{\"slice_kb\": %d, \"mode\": \"%s\", \"ns_per_hop_p50\": %.1f, \"ns_per_hop_min\": %.1f, \"ns_per_hop_max\": %.1f, "
+                "\"xccs_seen\": %d}\n", slice_kb, name, v[v.size() / 2], v.front(), v.back(), xcc_seen);
     std::fflush(stdout);
   };
   run("same/sync", false, true, false);
