@@ -997,6 +997,13 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("X"), py::arg("rows"), py::arg("F"), py::arg("nodes"), py::arg("leaves"), py::arg("depth"),
      py::arg("cmp_le"), py::arg("n_trees"), py::arg("rb"), py::arg("base"), py::arg("scale"), py::arg("transform"),
      py::arg("out"), py::arg("out_cols"), py::arg("s"), py::arg("lookahead") = -1);
+  k.def("tree_perfect_split", [](uintptr_t X, int rows, int F, uintptr_t nodes, uintptr_t leaves, int depth,
+                                 int cmp_le, int n_trees, int parts, uintptr_t base, float scale, int transform,
+                                 uintptr_t out, int out_cols, uintptr_t acc, uintptr_t counter, uintptr_t s) {
+    kern::tree_perfect_split(P<const double>(X), rows, F, P<const kern::TreeNode>(nodes), P<const float>(leaves),
+                             depth, cmp_le, n_trees, parts, P<const float>(base), scale, transform, P<double>(out),
+                             out_cols, P<double>(acc), P<int>(counter), as_stream(s));
+  });
   k.def("tree_reduce", [](uintptr_t partial, int rows, int n_chunks, uintptr_t chunk_group, int groups,
                           uintptr_t base, float scale, int transform, uintptr_t out, int out_cols, uintptr_t s) {
     kern::tree_reduce(P<const double>(partial), rows, n_chunks, P<const int>(chunk_group), groups, P<const float>(base),

@@ -33,13 +33,16 @@ bool large_bar(int device) {
 
 namespace {
 // SCA_BATCH_INPUT=bar|host: where a zero-copy batch's rows are staged.
-// "bar" writes them into fine-grained HBM through the BAR (large-BAR devices
-// only), "host" leaves them in pinned host memory read over PCIe.
-bool bar_input_wanted(int device) {
+// "bar" writes them into fine-grained HBM through the PCIe BAR (large-BAR
+// devices only), so the kernel's row read stays on the device (2.3 vs 4.1 us,
+// profiles/r05n_launch_floor); "host" leaves them in pinned host memory, read
+// over PCIe.  Unset: each model's preference (tree ensembles: bar -- xgb1000
+// 7.04 -> 5.96 us per small batch; the rest host: the pump's write-combined
+// stores cost the iris headline ~2%, profiles/r05sl_tree_split).
+bool bar_input_wanted(int device, bool model_prefers) {
   const char* e = std::getenv("SCA_BATCH_INPUT");
-  const std::string v = e ? e : "host";
-  if (v != "bar") return false;
-  return large_bar(device);
+  const bool want = e ? std::string(e) == "bar" : model_prefers;
+  return want && large_bar(device);
 }
 
 // Write-combined stores into BAR-mapped memory (the caller drains them with
@@ -100,7 +103,8 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
   inject_fault(fault_from_env(opts_.device));
   device_io_ = model_->device_io_only();
   zc_input_ = model_->zero_copy_input();
-  bar_input_ = opts_.device >= 0 && opts_.device < device_count() && bar_input_wanted(opts_.device);
+  bar_input_ = opts_.device >= 0 && opts_.device < device_count() &&
+               bar_input_wanted(opts_.device, model_->prefers_bar_input());
   segmented_ = model_->segmented();
   {
     auto info = std::make_shared<RespInfo>();

@@ -144,8 +144,12 @@ void TreeEnsembleModel::to_device(int device) {
   }
 }
 
-// Workspace: [fused-reduce counter, padded to 256 B][chunk partial slab].
-static constexpr size_t kTreeWsHeader = 256;
+// Workspace: [fused-reduce counter | split-kernel counter at byte 128 |
+// split-kernel row accumulators from byte 256, up to kSplitMaxRows]
+// [chunk partial slab].  The header starts zeroed (DeviceBuffer::alloc) and
+// every kernel that uses a counter or accumulator re-zeroes it.
+static constexpr size_t kTreeWsHeader = 4096;
+static constexpr int kSplitMaxRows = int((kTreeWsHeader - 256) / sizeof(double));
 
 size_t TreeEnsembleModel::workspace_bytes(int max_rows, int) const {
   // Largest slab any batch size up to max_rows plans for (chunks shrink as
@@ -225,6 +229,15 @@ bool TreeEnsembleModel::uses_fused(int rows) const {
 bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
                                     hipEvent_t done) {
   (void)cols;
+  if (uses_whole(rows) && kern::tree_split_parts() > 0 && rows <= std::min(kSplitMaxRows, kern::tree_split_max_rows()) &&
+      spec_.depth >= 4 && spec_.depth <= 10) {
+    char* hdr = static_cast<char*>(ws);
+    kern::tree_perfect_split(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
+                             spec_.depth, spec_.cmp_le, spec_.n_trees, kern::tree_split_parts(), d_base_.as<float>(),
+                             spec_.scale, spec_.transform, out, spec_.out_cols, reinterpret_cast<double*>(hdr + 256),
+                             reinterpret_cast<int*>(hdr + 128), s, done);
+    return done != nullptr;
+  }
   if (uses_whole(rows)) {
     kern::tree_perfect_whole(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
                              spec_.depth, spec_.cmp_le, spec_.n_trees,

@@ -54,6 +54,10 @@ class RowModel {
   // False if many workgroups re-read X (stage it in HBM instead of reading
   // pinned host memory over PCIe from every workgroup).
   virtual bool zero_copy_input() const { return true; }
+  // Stage zero-copy batches in HBM through the BAR by default
+  // (SCA_BATCH_INPUT unset; batcher.cc): for kernels whose time the row read
+  // dominates and whose workgroups read the rows more than once.
+  virtual bool prefers_bar_input() const { return false; }
   // Per-batch refinement: a model whose re-read factor depends on the batch
   // geometry may still read small batches straight from pinned host memory
   // (saves the H2D blit launch).
@@ -154,6 +158,9 @@ struct TreeEnsembleSpec {
 
 class TreeEnsembleModel : public RowModel {
  public:
+  // xgb1000 serving kernel 8.04 -> 7.17 us (whole) / 7.04 -> 5.96 us (split)
+  // with BAR rows (profiles/r05sl_tree_split)
+  bool prefers_bar_input() const override { return true; }
   explicit TreeEnsembleModel(TreeEnsembleSpec spec);
   std::string name() const override { return spec_.depth > 0 ? "tree_perfect" : "tree_sparse"; }
   int in_cols() const override { return spec_.n_features; }

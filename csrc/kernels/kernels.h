@@ -105,6 +105,18 @@ int tree_whole_rows_per_block(int n_trees, int rows);
 // lookahead (depth 8): 10 x levels per round + trees per iteration of the
 // lookahead descent (21 .. 42), 0 = the level-by-level descent, -1 =
 // SCA_TREE_LOOKAHEAD (default 0).
+// The whole-ensemble small-batch kernel with each row tile's trees split
+// over `parts` workgroups (one fp64 atomic per row and part into acc, the
+// last workgroup transforms and writes the rows and re-zeroes acc[0..rows)
+// and *counter).  acc and counter must be zero before the first launch.
+// SCA_TREE_SPLIT / SCA_TREE_SPLIT_ROWS set the serving default (8 parts for
+// batches of up to 16 rows); depths 4..10.
+int tree_split_parts();
+int tree_split_max_rows();
+void tree_perfect_split(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                        int cmp_le, int n_trees, int parts, const float* base_margin, float scale, int transform,
+                        double* out, int out_cols, double* acc, int* counter, hipStream_t s,
+                        hipEvent_t stop = nullptr);
 void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, int n_trees, int rows_per_block, const float* base_margin, float scale,
                         int transform, double* out, int out_cols, hipStream_t stream, hipEvent_t stop = nullptr,

@@ -539,6 +539,82 @@ __global__ __launch_bounds__(kWholeBlock) void perfect_whole(const double* __res
   }
 }
 
+// Small batches, single-output models, the ensemble SPLIT over S workgroups
+// per row tile (blockIdx.y = part): with the whole ensemble on one CU per
+// row, the descent is bound by that CU's load issue (profiles/r05xl_l2_levels:
+// the ensemble stays L2-resident between batches, a dependent hop costs
+// ~70 ns), so S CUs walk S shares of the trees.  Each workgroup folds its
+// rows in-workgroup and adds them into acc[row] with one agent-scope fp64
+// atomic per row (exact under the same span condition as reduce_write, so
+// the order of the S adds does not matter); the workgroup that brings the
+// counter to the grid size applies the objective transform, writes the rows
+// and re-zeroes acc and the counter for the next batch on this slot.
+template <int D>
+__global__ __launch_bounds__(kBlock) void perfect_split(const double* __restrict__ X, int rows, int F,
+                                                        const TreeNode* __restrict__ nodes,
+                                                        const float* __restrict__ leaves, int cmp_le, int n_trees,
+                                                        int RB, int stage_lds, const float* __restrict__ base_margin,
+                                                        float scale, int transform, double* __restrict__ out,
+                                                        int out_cols, double* __restrict__ acc,
+                                                        int* __restrict__ counter) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  double* red = reinterpret_cast<double*>(lds);  // [4 waves][RB]
+  float* tile = lds + 2 * kBlock;                // [F][RB] when staged
+  __shared__ int s_last;
+  constexpr int n_internal = (1 << D) - 1;
+  const int lrb = __builtin_ctz(unsigned(RB));
+  const int row0 = int(blockIdx.x) * RB;
+  const int r_local = int(threadIdx.x) & (RB - 1);
+  const int slot = int(threadIdx.x) >> lrb;
+  const int tpr = kBlock >> lrb;
+  const int parts = int(gridDim.y), part = int(blockIdx.y);
+  const int t_begin = int((long long)n_trees * part / parts), t_end = int((long long)n_trees * (part + 1) / parts);
+  if (stage_lds) {
+    stage_tile<kBlock>(tile, X, row0, rows, RB, lrb, F);
+    __syncthreads();
+  }
+  const float* xs = tile + r_local;
+  const bool row_ok = row0 + r_local < rows;
+  const double* xg = X + size_t(min(row0 + r_local, rows - 1)) * F;
+  double a = 0.0;
+  if (stage_lds) {
+    for (int t = t_begin + slot; t < t_end; t += tpr)
+      a += double(descend_lookahead<D, 2, true>(nodes + size_t(t) * n_internal, leaves + size_t(t) * (n_internal + 1),
+                                                n_internal, xs, lrb, xg, cmp_le));
+  } else if (row_ok) {
+    for (int t = t_begin + slot; t < t_end; t += tpr)
+      a += double(descend_lookahead<D, 2, false>(nodes + size_t(t) * n_internal, leaves + size_t(t) * (n_internal + 1),
+                                                 n_internal, xs, lrb, xg, cmp_le));
+  }
+  if (!row_ok) a = 0.0;
+  for (int off = 32; off >= RB; off >>= 1) a += __shfl_xor(a, off, 64);
+  const int lane = int(threadIdx.x) & 63, wave = int(threadIdx.x) >> 6;
+  if (lane < RB) red[wave * RB + lane] = a;
+  __syncthreads();
+  if (int(threadIdx.x) < RB) {
+    const int r = row0 + int(threadIdx.x);
+    if (r < rows) {
+      double m = 0.0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) m += red[w * RB + threadIdx.x];
+      __hip_atomic_fetch_add(acc + r, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's adds performed at the coherence point
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             int(gridDim.x * gridDim.y) - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int r = int(threadIdx.x); r < rows; r += kBlock) {
+    double m[1] = {__hip_atomic_load(acc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+    __hip_atomic_store(acc + r, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    apply_transform<1>(m, 1, transform, scale, base_margin, out + size_t(r) * out_cols);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int kMaxGroups = 64;
 
 // Block = RB rows x (blockDim / RB) chunk-lanes: the lanes of a row sum a
@@ -750,6 +826,61 @@ void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes,
   }
 #undef SCA_WHOLE_LAUNCH
 #undef SCA_WHOLE_LAUNCH1
+}
+
+// SCA_TREE_SPLIT: workgroups per row tile (default 8; 0 = one workgroup, the
+// perfect_whole kernel).  SCA_TREE_SPLIT_ROWS: largest batch split (default
+// 16).  xgb1000 at 9 rows (profiles/r05sl_tree_split): 6.21 -> 5.27 us in the
+// microbench, 7.17 -> 5.96 us serving with BAR-staged rows, 8.04 -> 7.04 us
+// with host rows; from ~32 rows on the single workgroup per row tile wins.
+int tree_split_parts() {
+  static const int v = [] {
+    const char* e = std::getenv("SCA_TREE_SPLIT");
+    const int p = e ? std::atoi(e) : 8;
+    return p < 0 ? 0 : (p > 64 ? 64 : p);
+  }();
+  return v;
+}
+
+int tree_split_max_rows() {
+  static const int v = [] {
+    const char* e = std::getenv("SCA_TREE_SPLIT_ROWS");
+    return e ? std::max(0, std::atoi(e)) : 16;
+  }();
+  return v;
+}
+
+void tree_perfect_split(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                        int cmp_le, int n_trees, int parts, const float* base_margin, float scale, int transform,
+                        double* out, int out_cols, double* acc, int* counter, hipStream_t s, hipEvent_t stop) {
+  if (rows <= 0 || n_trees <= 0 || parts <= 0 || depth < 4 || depth > 10) return;
+  // rows per workgroup: one tree per lane of the part while the rows fit
+  const int per_part = (n_trees + parts - 1) / parts;
+  int RB = 1;
+  while (RB < 16 && RB < rows && per_part * (RB * 2) <= kBlock) RB <<= 1;
+  const bool stage = RB * F <= kMaxLdsFloats;
+  const uint32_t lds = uint32_t((2 * kBlock + (stage ? ((RB * F + 3) & ~3) : 0)) * sizeof(float));
+  const dim3 grid((rows + RB - 1) / RB, parts);
+#define SCA_SPLIT_LAUNCH(DD)                                                                                      \
+  do {                                                                                                            \
+    if (stop)                                                                                                     \
+      hipExtLaunchKernelGGL((perfect_split<DD>), grid, dim3(kBlock), lds, s, nullptr, stop, 0, X, rows, F, nodes,  \
+                            leaves, cmp_le, n_trees, RB, int(stage), base_margin, scale, transform, out, out_cols,  \
+                            acc, counter);                                                                        \
+    else                                                                                                          \
+      hipLaunchKernelGGL((perfect_split<DD>), grid, dim3(kBlock), lds, s, X, rows, F, nodes, leaves, cmp_le,       \
+                         n_trees, RB, int(stage), base_margin, scale, transform, out, out_cols, acc, counter);    \
+  } while (0)
+  switch (depth) {
+    case 4: SCA_SPLIT_LAUNCH(4); break;
+    case 5: SCA_SPLIT_LAUNCH(5); break;
+    case 6: SCA_SPLIT_LAUNCH(6); break;
+    case 7: SCA_SPLIT_LAUNCH(7); break;
+    case 8: SCA_SPLIT_LAUNCH(8); break;
+    case 9: SCA_SPLIT_LAUNCH(9); break;
+    default: SCA_SPLIT_LAUNCH(10); break;
+  }
+#undef SCA_SPLIT_LAUNCH
 }
 
 void tree_reduce(const double* partial, int rows, int n_chunks, const int* chunk_group, int groups,
