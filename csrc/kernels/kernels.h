@@ -110,7 +110,7 @@ int tree_whole_rows_per_block(int n_trees, int rows);
 // last workgroup transforms and writes the rows and re-zeroes acc[0..rows)
 // and *counter).  acc and counter must be zero before the first launch.
 // SCA_TREE_SPLIT / SCA_TREE_SPLIT_ROWS set the serving default (8 parts for
-// batches of up to 16 rows); depths 4..10.
+// batches of up to 32 rows); depths 4..10.
 int tree_split_parts();
 int tree_split_max_rows();
 void tree_perfect_split(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,

@@ -830,9 +830,10 @@ void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes,
 
 // SCA_TREE_SPLIT: workgroups per row tile (default 8; 0 = one workgroup, the
 // perfect_whole kernel).  SCA_TREE_SPLIT_ROWS: largest batch split (default
-// 16).  xgb1000 at 9 rows (profiles/r05sl_tree_split): 6.21 -> 5.27 us in the
+// 32).  xgb1000 at 9 rows (profiles/r05sl_tree_split): 6.21 -> 5.27 us in the
 // microbench, 7.17 -> 5.96 us serving with BAR-staged rows, 8.04 -> 7.04 us
-// with host rows; from ~32 rows on the single workgroup per row tile wins.
+// with host rows; serving batches of 17-32 rows 7.3 -> 5.8 us; in the
+// microbench the single workgroup per row tile wins again at 128 rows.
 int tree_split_parts() {
   static const int v = [] {
     const char* e = std::getenv("SCA_TREE_SPLIT");
@@ -845,7 +846,7 @@ int tree_split_parts() {
 int tree_split_max_rows() {
   static const int v = [] {
     const char* e = std::getenv("SCA_TREE_SPLIT_ROWS");
-    return e ? std::max(0, std::atoi(e)) : 16;
+    return e ? std::max(0, std::atoi(e)) : 32;
   }();
   return v;
 }
