@@ -738,7 +738,13 @@ def reuseport_child(args, budget: bk.Budget) -> dict:
         lg = bk.run_loadgen(port, 2, 0, "rest", body, users, cthreads, bk.window_requests(rate, EXTRA_WINDOW_S),
                             budget.timeout(reserve=10), expect=expect)
         os.killpg(proc.pid, signal.SIGTERM)  # drain: every worker files its request count
-        proc.wait(timeout=max(5.0, budget.left(5)))
+        drain_timeout = None
+        try:
+            proc.wait(timeout=max(5.0, min(30.0, budget.left(5))))
+        except subprocess.TimeoutExpired:  # the window is measured: report it, note the slow exit
+            drain_timeout = "serve supervisor still running 30 s after SIGTERM (killed)"
+            os.killpg(proc.pid, signal.SIGKILL)
+            proc.wait()
         per = []
         for fn in sorted(os.listdir(stats)):
             with open(os.path.join(stats, fn)) as f:
@@ -751,7 +757,8 @@ def reuseport_child(args, budget: bk.Budget) -> dict:
                 "self_check": {"ok": lg.get("bad_body", 0) == 0},
                 "per_worker_requests": {str(w["rank"]): w["requests"] for w in per},
                 "balance_min_over_max": round(min(counts) / max(1, max(counts)), 3) if counts else None,
-                "server_threads_per_worker": threads, "client_threads": cthreads}
+                "server_threads_per_worker": threads, "client_threads": cthreads,
+                **({"drain_timeout": drain_timeout} if drain_timeout else {})}
     except Exception as e:
         return {"error": f"{type(e).__name__}: {e}"[:600]}
     finally:
