@@ -678,6 +678,14 @@ def variant_child(args) -> None:
     print(json.dumps(out), flush=True)
 
 
+def _tail(path: str, n: int) -> list:
+    try:
+        with open(path, errors="replace") as f:
+            return [ln.rstrip()[:300] for ln in f.readlines()[-n:]]
+    except OSError:
+        return []
+
+
 def reuseport_child(args, budget: bk.Budget) -> dict:
     """The production multi-worker path: ``serve --gpus
     N`` -- the Supervisor's N worker processes, one per GPU, all bound to ONE
@@ -737,14 +745,20 @@ def reuseport_child(args, budget: bk.Budget) -> dict:
                              expect=expect)
         lg = bk.run_loadgen(port, 2, 0, "rest", body, users, cthreads, bk.window_requests(rate, EXTRA_WINDOW_S),
                             budget.timeout(reserve=10), expect=expect)
-        os.killpg(proc.pid, signal.SIGTERM)  # drain: every worker files its request count
+        # drain: SIGTERM to the supervisor ONLY -- it forwards one SIGTERM to
+        # each worker (every worker files its request count) and SIGKILLs
+        # stragglers itself; a killpg would hand every worker a second signal
+        proc.send_signal(signal.SIGTERM)
         drain_timeout = None
+        t_stop = time.time()
         try:
-            proc.wait(timeout=max(5.0, min(30.0, budget.left(5))))
+            proc.wait(timeout=max(5.0, min(40.0, budget.left(5))))
         except subprocess.TimeoutExpired:  # the window is measured: report it, note the slow exit
-            drain_timeout = "serve supervisor still running 30 s after SIGTERM (killed)"
+            drain_timeout = {"error": "serve supervisor still running after SIGTERM (killed)",
+                             "serve_log_tail": _tail(os.path.join(work, "serve.log"), 40)}
             os.killpg(proc.pid, signal.SIGKILL)
             proc.wait()
+        stop_s = round(time.time() - t_stop, 3)
         per = []
         for fn in sorted(os.listdir(stats)):
             with open(os.path.join(stats, fn)) as f:
@@ -757,8 +771,10 @@ def reuseport_child(args, budget: bk.Budget) -> dict:
                 "self_check": {"ok": lg.get("bad_body", 0) == 0},
                 "per_worker_requests": {str(w["rank"]): w["requests"] for w in per},
                 "balance_min_over_max": round(min(counts) / max(1, max(counts)), 3) if counts else None,
-                "server_threads_per_worker": threads, "client_threads": cthreads,
-                **({"drain_timeout": drain_timeout} if drain_timeout else {})}
+                "server_threads_per_worker": threads, "client_threads": cthreads, "shutdown_s": stop_s,
+                **({"drain_timeout": drain_timeout} if drain_timeout else {}),
+                **({"missing_worker_stats": sorted(set(map(str, range(n))) - {str(w["rank"]) for w in per}),
+                    "serve_log_tail": _tail(os.path.join(work, "serve.log"), 40)} if len(per) < n else {})}
     except Exception as e:
         return {"error": f"{type(e).__name__}: {e}"[:600]}
     finally:

@@ -21,10 +21,8 @@ import importlib
 import json
 import logging
 import os
-import signal
 import sys
 import threading
-import time
 from typing import Any, Dict, List
 
 logger = logging.getLogger(__name__)
@@ -176,15 +174,11 @@ def main(argv=None) -> None:
     if callable(getattr(user_object, "custom_service", None)):
         threading.Thread(target=user_object.custom_service, daemon=True).start()
 
-    stop = threading.Event()
+    from .utils.shutdown import StopSignal
 
-    def _term(*_):
-        stop.set()
-
-    signal.signal(signal.SIGTERM, _term)
-    signal.signal(signal.SIGINT, _term)
-    while not stop.is_set():
-        time.sleep(0.5)
+    # the handlers only flip a flag: a lock taken inside a handler (Event.set)
+    # deadlocks when a second SIGTERM/SIGINT lands in it
+    StopSignal().install().wait()
     for s in servers:
         s.stop()
     if persister is not None:

@@ -61,6 +61,8 @@ import threading
 import time
 from typing import Dict, List, Optional
 
+from .utils.shutdown import StopSignal
+
 logger = logging.getLogger("seldon_core_amd.serve")
 
 
@@ -90,6 +92,9 @@ def parse_args(argv: Optional[List[str]] = None) -> argparse.Namespace:
                     help="pin each worker to whole CCDs of its GPU's socket covering this many CPUs (0 = off)")
     ap.add_argument("--supervise", action="store_true",
                     help="run even a single worker under the supervisor (SIGHUP rolling updates, restarts)")
+    ap.add_argument("--kill-after", type=float, default=30.0,
+                    help="supervisor: SIGKILL workers still running this many seconds after the forwarded "
+                         "SIGTERM (their own drain is seldon.io/engine-drain-seconds, default 20)")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -144,11 +149,10 @@ def run_fabric_worker(args: argparse.Namespace) -> int:
     for c in args.component:
         node, _, cls = c.partition("=")
         comps[node] = cls
-    stop_requested = threading.Event()
     # SIGTERM: rank 0 drains first and then stops this loop; leave on our own
-    # only if it never does.
-    signal.signal(signal.SIGTERM, lambda *_: stop_requested.set())
-    signal.signal(signal.SIGINT, lambda *_: stop_requested.set())
+    # only if it never does.  The handler only flips a flag (utils/shutdown.py).
+    stop_requested = StopSignal().install()
+    _stack_dumps()
     srv = serve_peer(load_spec(args.spec), fabric, comps, predictor=args.predictor)
     logger.info("rank %d/%d serving its placed nodes on device %s (%s)", rank, world, device, fabric.transport)
     joiner = threading.Thread(target=srv.join, daemon=True)
@@ -170,7 +174,22 @@ def run_fabric_worker(args: argparse.Namespace) -> int:
 
 
 # ------------------------------------------------------------------ worker
+def _stack_dumps() -> None:
+    """SIGUSR1 dumps every thread's Python stack to stderr (hang triage in
+    production: ``kill -USR1 <worker pid>``)."""
+    import faulthandler
+
+    try:
+        faulthandler.register(signal.SIGUSR1, all_threads=True, chain=False)
+    except (AttributeError, ValueError, RuntimeError):
+        pass
+
+
 def run_worker(args: argparse.Namespace, fabric=None) -> int:
+    # installed first: a SIGTERM during start-up becomes a drain as soon as
+    # the servers are up instead of the default action killing the process
+    stop = StopSignal().install()
+    _stack_dumps()
     if args.pin_cpus > 0 and (args.device is None or args.device >= 0):
         # before the front end and the GPU units start their threads (they inherit it)
         from .utils.topology import pin
@@ -220,19 +239,12 @@ def run_worker(args: argparse.Namespace, fabric=None) -> int:
         explainer = from_spec(dep.predictor, deployment_predictor(dep), model_name, cfg.host, args.explainer_port)
         explainer.start()
         logger.info("explainer %s on :%d", dep.predictor["explainer"]["type"], explainer.port)
-    stop = threading.Event()
-
-    def on_signal(signum, frame):  # noqa: ARG001
-        stop.set()
-
     def on_hup(signum, frame):  # noqa: ARG001
         # SIGHUP's default action would kill the only serving process: a
         # rolling update needs a supervisor to start the replacement first.
         if not os.environ.get("SCA_WORKER_RANK"):
             logger.warning("SIGHUP ignored: rolling updates need the supervisor (--supervise or --gpus > 1)")
 
-    signal.signal(signal.SIGTERM, on_signal)
-    signal.signal(signal.SIGINT, on_signal)
     signal.signal(signal.SIGHUP, on_hup)
     stop.wait()
     if explainer is not None:
@@ -261,7 +273,7 @@ class Supervisor:
     """Keeps one worker process per GPU alive."""
 
     def __init__(self, n: int, worker_argv: List[str], max_restarts: int = 5, ready_timeout: float = 120.0,
-                 drain_timeout: float = 60.0, gang: bool = False):
+                 drain_timeout: float = 60.0, gang: bool = False, kill_after: float = 30.0):
         self.n = n
         self.gang = gang  # rank-placed graph: the N processes are ranks of ONE graph
         self.master_port = 0
@@ -277,6 +289,11 @@ class Supervisor:
         self.generation = 0
         self.rollouts: List[Dict] = []
         self._surge: Optional[subprocess.Popen] = None  # the rollout's new worker before it is swapped in
+        self.stop_signal = StopSignal()
+        self.kill_after = kill_after       # SIGKILL workers this long after the forwarded SIGTERM
+        self._forwarded_at: Optional[float] = None
+        self._killed = False
+        self.killed_pids: List[int] = []
 
     def _start(self, rank: int, ready_file: Optional[str] = None) -> subprocess.Popen:
         env = dict(os.environ)
@@ -403,11 +420,46 @@ class Supervisor:
                 p.kill()
                 p.wait()
 
-    def terminate(self) -> None:
+    def request_stop(self, signum=None, frame=None) -> None:  # noqa: ARG002
+        """Signal handler: flips flags only (no lock, no Popen call -- see
+        utils/shutdown.py); the main loop forwards and escalates."""
+        self.stop_signal.handler(signum or 0)
         self.stopping = True
-        for p in list(self.procs.values()) + ([self._surge] if self._surge is not None else []):
+
+    def _children(self) -> List[subprocess.Popen]:
+        return list(self.procs.values()) + ([self._surge] if self._surge is not None else [])
+
+    def terminate(self) -> None:
+        """Main-loop side, idempotent: forward ONE SIGTERM to every worker
+        (they drain: readiness off, in-flight requests finish), then
+        :meth:`_escalate` SIGKILLs whatever is still alive ``kill_after``
+        seconds later -- the reference's forced stop after its 20 s drain
+        (``App.java:89-92``)."""
+        self.stopping = True
+        if self._forwarded_at is not None:
+            return
+        self._forwarded_at = time.monotonic()
+        for p in self._children():
             if p.poll() is None:
-                p.send_signal(signal.SIGTERM)
+                try:
+                    p.send_signal(signal.SIGTERM)
+                except OSError:
+                    pass
+
+    def _escalate(self) -> None:
+        if self._forwarded_at is None or self._killed:
+            return
+        if time.monotonic() - self._forwarded_at < self.kill_after:
+            return
+        self._killed = True
+        for p in self._children():
+            if p.poll() is None:
+                logger.error("worker pid %d still running %.0f s after SIGTERM: SIGKILL", p.pid, self.kill_after)
+                self.killed_pids.append(p.pid)
+                try:
+                    p.kill()
+                except OSError:
+                    pass
 
     def run(self) -> int:
         try:
@@ -421,12 +473,18 @@ class Supervisor:
         else:
             for r in range(self.n):
                 self.spawn(r)
-        signal.signal(signal.SIGTERM, lambda *_: self.terminate())
-        signal.signal(signal.SIGINT, lambda *_: self.terminate())
+        signal.signal(signal.SIGTERM, self.request_stop)
+        signal.signal(signal.SIGINT, self.request_stop)
         signal.signal(signal.SIGHUP, lambda *_: setattr(self, "roll_requested", True))
+        return self._loop()
+
+    def _loop(self) -> int:
         rc = 0
         while True:
-            time.sleep(0.2)
+            self.stop_signal.wait(0.2)
+            if self.stopping:
+                self.terminate()
+                self._escalate()
             if self.roll_requested and not self.stopping:
                 self.roll_requested = False
                 self.rolling_update()
@@ -486,7 +544,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         if a.startswith("--gpus="):
             continue
         worker_argv.append(a)
-    return Supervisor(n, worker_argv, args.max_restarts, gang=placed > 0).run()
+    return Supervisor(n, worker_argv, args.max_restarts, gang=placed > 0, kill_after=args.kill_after).run()
 
 
 if __name__ == "__main__":
