@@ -63,7 +63,7 @@ struct PyUnitOptions {
 struct PoolFrame {
   static constexpr uint32_t kMagic = 0x57414353;  // "SCAW"
   uint32_t magic = kMagic;
-  uint32_t op = 0;     // request: PyUnit::Op; response: 0 dense, 1 json, 3 error
+  uint32_t op = 0;     // request: PyUnit::Op; response: 0 dense, 1 json, 3 error, 4 component error reply
   uint32_t ndim = 0;
   uint32_t flags = 0;  // request: 1 = dense payload
   int64_t shape[8] = {};
@@ -445,9 +445,7 @@ class PyUnit : public Unit {
       std::lock_guard<std::mutex> sg(stats_mu_);
       stats_.calls++;
     } catch (py::error_already_set& e) {
-      auto err = make_error(ApiError::MICROSERVICE_ERROR, e.what());
-      e.restore();
-      PyErr_Clear();
+      auto err = user_error(e);
       for (auto& r : res) r = Outcome::fail(err);
       fb_res.assign(1, err);
     } catch (const std::exception& e) {
@@ -455,6 +453,42 @@ class PyUnit : public Unit {
       for (auto& r : res) r = Outcome::fail(err);
       fb_res.assign(1, err);
     }
+  }
+
+  // A Python exception -> engine error.  The adapter's error_reply() applies
+  // the reference wrapper's rules (wrapper.py:22-31, flask_utils.py:67-81):
+  // the component's model_error_handler, else SeldonMicroserviceException's
+  // own status / reason / to_dict(); anything else stays a plain 203.
+  // Called with the GIL held.
+  ErrPtr user_error(py::error_already_set& e) {
+    std::string what = e.what();
+    try {
+      if (py::hasattr(adapter_, "error_reply")) {
+        py::object r = adapter_.attr("error_reply")(e.value());
+        if (!r.is_none()) {
+          auto t = r.cast<py::tuple>();
+          return make_user_error(t[0].cast<int>(), t[1].cast<std::string>(), t[2].cast<std::string>());
+        }
+      }
+    } catch (py::error_already_set& inner) {
+      what += std::string(" (error handler failed: ") + inner.what() + ")";
+    } catch (const std::exception& inner) {
+      what += std::string(" (error handler failed: ") + inner.what() + ")";
+    }
+    return make_error(ApiError::MICROSERVICE_ERROR, what);
+  }
+
+  // Pool reply op 4: {"status": int, "body": "<json>", "info": "..."}.
+  static ErrPtr pool_user_error(const std::string& text) {
+    try {
+      Json j = parse_json(text);
+      const Json* st = j.find("status");
+      const Json* body = j.find("body");
+      const Json* info = j.find("info");
+      if (st && body) return make_user_error(int(st->as_number()), body->as_string(), info ? info->as_string() : "");
+    } catch (const std::exception&) {
+    }
+    return make_error(ApiError::MICROSERVICE_ERROR, text);
   }
 
   void call_dense_inproc(std::vector<Job>& jobs, std::vector<Outcome>& res) {
@@ -620,8 +654,8 @@ class PyUnit : public Unit {
       stats_.rows += uint64_t(total);
       if (jobs.size() > 1) stats_.batched_calls++;
     }
-    if (r.op == 3) {
-      auto err = make_error(ApiError::MICROSERVICE_ERROR, rtext);
+    if (r.op == 3 || r.op == 4) {
+      auto err = r.op == 4 ? pool_user_error(rtext) : make_error(ApiError::MICROSERVICE_ERROR, rtext);
       for (auto& o : res) o = Outcome::fail(err);
       fb_res.assign(1, err);
       return;

@@ -34,7 +34,15 @@ ErrPtr make_error(ApiError kind, std::string info) {
   return e;
 }
 
+ErrPtr make_user_error(int http_status, std::string body, std::string info) {
+  auto e = std::make_shared<EngineError>(*make_error(ApiError::MICROSERVICE_ERROR, std::move(info)));
+  e->http_status = (http_status >= 100 && http_status <= 599) ? http_status : 500;
+  e->body = std::move(body);
+  return e;
+}
+
 std::string error_to_json(const EngineError& e) {
+  if (!e.body.empty()) return e.body;
   Status s;
   s.code = e.code;
   s.info = e.info;

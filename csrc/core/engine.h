@@ -56,10 +56,17 @@ struct EngineError {
   // error, hang, unhealthy replica), not of the request: a replica set may
   // re-run the request on another GPU.
   bool device_fault = false;
+  // A component's own error reply (python/seldon_core/wrapper.py:22-31,
+  // flask_utils.py:67-81): the JSON body its model_error_handler or
+  // SeldonMicroserviceException.to_dict() produced, sent verbatim with
+  // `http_status` (REST) or carried as the gRPC status message.
+  std::string body;
 };
 using ErrPtr = std::shared_ptr<const EngineError>;
 
 ErrPtr make_error(ApiError kind, std::string info);
+// 203 MICROSERVICE_ERROR that answers with the component's status and body.
+ErrPtr make_user_error(int http_status, std::string body, std::string info);
 std::string error_to_json(const EngineError& e);
 
 struct Outcome {

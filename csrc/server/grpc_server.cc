@@ -77,6 +77,20 @@ nghttp2_nv make_nv(const char* n, const char* v, size_t vlen) {
 }
 
 int grpc_status_of(const EngineError& e) {
+  if (!e.body.empty()) {  // a component's own error: its HTTP status in gRPC terms
+    switch (e.http_status) {
+      case 400: return kInvalidArgument;
+      case 401: return 16;  // UNAUTHENTICATED
+      case 403: return 7;   // PERMISSION_DENIED
+      case 404: return 5;   // NOT_FOUND
+      case 409: return 10;  // ABORTED
+      case 429: return kResourceExhausted;
+      case 501: return kUnimplemented;
+      case 503: return kUnavailable;
+      case 504: return kDeadline;
+      default: return kUnknown;
+    }
+  }
   switch (e.code) {
     case 201: return kInvalidArgument;
     case 209: return kUnavailable;

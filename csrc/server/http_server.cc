@@ -690,7 +690,10 @@ struct HttpServer::Worker : Executor, std::enable_shared_from_this<HttpServer::W
       std::string body;
       int status = 200;
       if (d.outcome.err) {
-        if (d.kind == 1) {  // wrapper-style error (flask_utils.py:67-82)
+        if (!d.outcome.err->body.empty()) {  // the component's own status + body (wrapper.py:22-31)
+          status = d.outcome.err->http_status;
+          body = d.outcome.err->body;
+        } else if (d.kind == 1) {  // wrapper-style error (flask_utils.py:67-82)
           status = 400;
           body = "{\"status\":{\"status\":1,\"info\":";
           append_quoted(body, d.outcome.err->info);

@@ -27,6 +27,13 @@ struct NetError : std::runtime_error {
   NetError(const std::string& m, bool c) : std::runtime_error(m), connect_failure(c) {}
 };
 
+struct RemoteUserError : std::runtime_error {
+  int status;
+  std::string body;
+  RemoteUserError(int s, std::string b)
+      : std::runtime_error("Bad return code " + std::to_string(s) + ": " + b), status(s), body(std::move(b)) {}
+};
+
 int connect_timeout(const std::string& host, int port, int connect_ms, int io_ms) {
   addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_INET;
@@ -276,6 +283,16 @@ std::string RemoteUnit::call_rest(const std::string& path, const std::string& js
         tl_rest.erase(key);
       }
       if (status < 200 || status >= 300) {
+        // A component's own error reply (a JSON object, e.g. its
+        // model_error_handler's body) travels back to the client with its
+        // status; anything else is the reference's "Bad return code"
+        // (InternalPredictionService.java:426-427).
+        bool obj = false;
+        try {
+          obj = parse_json(body).is_object();
+        } catch (const std::exception&) {
+        }
+        if (obj) throw RemoteUserError(status, body);
         throw std::runtime_error("Bad return code " + std::to_string(status) + ": " + body);
       }
       return body;
@@ -373,6 +390,8 @@ void RemoteUnit::call_message(const char* rest_path, const char* grpc_method, Ms
         message_from_json(parse_json(call_rest(rp, js)), *m);
       }
       k(Outcome::ok(std::move(m)));
+    } catch (const RemoteUserError& e) {
+      k(Outcome::fail(make_user_error(e.status, e.body, e.what())));
     } catch (const std::exception& e) {
       k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, e.what())));
     }
@@ -404,6 +423,8 @@ void RemoteUnit::aggregate(const CallCtx&, std::vector<MsgPtr> in, Done k) {
         message_from_json(parse_json(call_rest("aggregate", js)), *m);
       }
       k(Outcome::ok(std::move(m)));
+    } catch (const RemoteUserError& e) {
+      k(Outcome::fail(make_user_error(e.status, e.body, e.what())));
     } catch (const std::exception& e) {
       k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, e.what())));
     }
@@ -423,6 +444,8 @@ void RemoteUnit::send_feedback(const CallCtx&, std::shared_ptr<const Feedback> f
         call_rest("send-feedback", js);
       }
       k(nullptr);
+    } catch (const RemoteUserError& e) {
+      k(make_user_error(e.status, e.body, e.what()));
     } catch (const std::exception& e) {
       k(make_error(ApiError::MICROSERVICE_ERROR, e.what()));
     }

@@ -38,7 +38,7 @@ import numpy as np
 
 from . import dispatch
 from .codec import construct_response_json, dumps
-from .errors import SeldonMicroserviceException, SeldonNotImplementedError
+from .errors import SeldonMicroserviceException, SeldonNotImplementedError, component_error_reply
 from .user_model import (SeldonComponent, client_class_names, client_custom_metrics, client_custom_tags,
                          client_predict, client_route, client_transform_input, client_transform_output)
 
@@ -154,6 +154,16 @@ class PythonUnit:
 
     def send_feedback(self, text: str, node: str) -> str:
         return dumps(self._run(dispatch.send_feedback, self.user_model, json.loads(text), node or self.name))
+
+    def error_reply(self, exc: BaseException):
+        """(http status, JSON body, info) for an exception the component's
+        error contract covers (its model_error_handler, or a
+        SeldonMicroserviceException), else None -- see errors.component_error_reply."""
+        try:
+            return component_error_reply(self.user_model, exc, self.__dict__.setdefault("_err_cache", {}))
+        except Exception:  # noqa: BLE001  a broken handler must not take the request path down
+            logger.exception("model_error_handler failed for %r", exc)
+            return None
 
     def ready(self) -> bool:
         if self._procs and all(p.poll() is not None for p in self._procs):

@@ -66,7 +66,12 @@ def serve(fd: int) -> None:
                 send_frame(sock, 1, b"", (out or "").encode())
         except Exception as e:  # noqa: BLE001
             try:
-                send_frame(sock, 3, b"", f"{type(e).__name__}: {e}".encode())
+                reply = unit.error_reply(e)  # the component's own status + body (op 4)
+                if reply is not None:
+                    send_frame(sock, 4, b"", json.dumps({"status": reply[0], "body": reply[1],
+                                                         "info": reply[2]}).encode())
+                else:
+                    send_frame(sock, 3, b"", f"{type(e).__name__}: {e}".encode())
             except OSError:
                 return
 
