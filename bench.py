@@ -946,8 +946,10 @@ def fabric_child(args) -> None:
             if kind == "mab":
                 r["feedback"] = {"rewarded_branch": world - 1, "rps": fb_out.get("rps"), "error": fb_out.get("error")}
             if dep.mesh is not None:
-                r["mesh_programs"] = [{"root": p.root, "stages": p.describe(), "messages_per_batch": m}
-                                      for p, m in zip(dep.mesh.programs, dep.mesh.messages)]
+                r["mesh_programs"] = [{"root": p.root, "stages": p.describe(), "messages_per_batch": m,
+                                       "edges": (dep.mesh.edges[i] if i < len(dep.mesh.edges) else [])}
+                                      for i, (p, m) in enumerate(zip(dep.mesh.programs, dep.mesh.messages))]
+                r["peer"] = dep.mesh.peer  # GPUs, hipDeviceCanAccessPeer, IPC canary per edge
             r["transport"] = transport
             graphs[kind] = r
         except Exception as e:

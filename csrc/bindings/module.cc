@@ -255,6 +255,7 @@ PYBIND11_MODULE(_C, m) {
     d["split_mode"] = g->split_mode();
     d["peer_direct"] = g->peer_direct();
     d["stages"] = int(g->stages().size());
+    d["fused"] = g->fused();  // one linear_graph kernel per batch
     return d;
   });
   auto to_layers = [](py::list ls) {
@@ -368,6 +369,17 @@ PYBIND11_MODULE(_C, m) {
         }
         return py::array_t<double>(py::ssize_t(s.size()), s.data());
       })
+      .def("step_seq", [](gpu::MahalanobisDevice& d, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
+        if (X.ndim() != 2 || X.shape(1) != d.p()) throw std::runtime_error("X must be [rows, p]");
+        std::vector<double> s;
+        int64_t seq = -1;
+        {
+          py::gil_scoped_release nogil;
+          s = d.step(X.data(), int(X.shape(0)), &seq);
+        }
+        return py::make_tuple(py::array_t<double>(py::ssize_t(s.size()), s.data()), seq);
+      }, "step() that also returns where the state applied this request's first row (launch order over every "
+         "view of the state): concurrent callers can be replayed in the device's order")
       .def("state", [](const gpu::MahalanobisDevice& d) {
         auto s = d.state();
         return py::array_t<double>(py::ssize_t(s.size()), s.data());
@@ -676,6 +688,18 @@ PYBIND11_MODULE(_C, m) {
              }
              return me.add_program(std::move(p));
            })
+      .def("probe_prepare", [](par::Mesh& me) { return py::bytes(me.probe_prepare()); })
+      .def("probe_connect",
+           [](par::Mesh& me, const std::vector<py::bytes>& blobs) {
+             std::vector<std::string> b;
+             for (auto& x : blobs) b.push_back(std::string(x));
+             py::gil_scoped_release nogil;
+             return me.probe_connect(b);
+           })
+      .def("probe_error", &par::Mesh::probe_error)
+      .def("probe_finish", &par::Mesh::probe_finish)
+      .def("set_peer_ok", &par::Mesh::set_peer_ok)
+      .def("edge_transports", &par::Mesh::edge_transports)
       .def("set_model", &par::Mesh::set_model)
       .def("set_host_fn",
            [](par::Mesh& me, int prog, int stage, py::object fn) {
@@ -967,6 +991,8 @@ PYBIND11_MODULE(_C, m) {
     kern::linear_f64(P<const double>(X), rows, K, P<const double>(W), P<const double>(b), C, act, P<double>(out),
                      as_stream(s));
   });
+  k.def("linear_uses_mfma", &kern::linear_uses_mfma, py::arg("rows"), py::arg("K"), py::arg("C"),
+        "Does linear_f64 run this shape on the f64 matrix cores (SCA_LINEAR_MFMA=0 off, =2 forced)?");
   k.def("tree_perfect_partial", [](uintptr_t X, int rows, int F, uintptr_t nodes, uintptr_t leaves, int depth,
                                    int cmp_le, uintptr_t chunk_begin, int n_chunks, int rb, uintptr_t partial,
                                    uintptr_t s, int lds_trees) {

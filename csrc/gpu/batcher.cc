@@ -106,6 +106,14 @@ BatchedUnit::BatchedUnit(RowModelPtr model, BatcherOptions opts) : model_(std::m
   bar_input_ = opts_.device >= 0 && opts_.device < device_count() &&
                bar_input_wanted(opts_.device, model_->prefers_bar_input());
   segmented_ = model_->segmented();
+  if (bar_input_) {
+    const char* f = std::getenv("SCA_HDP_FLUSH");
+    if (!f || std::atoi(f) != 0) {
+      hipDeviceProp_t prop{};
+      if (hipGetDeviceProperties(&prop, opts_.device) == hipSuccess && prop.hdpMemFlushCntl)
+        hdp_flush_ = prop.hdpMemFlushCntl;
+    }
+  }
   {
     auto info = std::make_shared<RespInfo>();
     info->model = model_;
@@ -395,6 +403,7 @@ bool BatchedUnit::launch(Slot* s) {
       size_t row = 0;
       for (const auto& it : s->items) {
         model_->run_cpu(it.xp, it.rows, cols, s->cpu_out.data() + row * s->out_cols);
+        if (it.seq_out) *it.seq_out = model_->last_sequence_base();
         row += size_t(it.rows);
       }
       return true;
@@ -432,7 +441,13 @@ bool BatchedUnit::launch(Slot* s) {
         else memcpy(dst + off, it.xp, n * sizeof(double));
         off += n;
       }
-      if (bar) _mm_sfence();
+      if (bar) {
+        _mm_sfence();  // the write-combined stores are out of the CPU ...
+        if (hdp_flush_) {  // ... and out of the HDP write buffer before the launch (as the HIP runtime does)
+          *hdp_flush_ = 1u;
+          (void)*hdp_flush_;
+        }
+      }
     }
     hipStream_t st = s->stream.get();
     const int32_t* seg = nullptr;
@@ -447,8 +462,17 @@ bool BatchedUnit::launch(Slot* s) {
     }
     bool signalled = false;  // the model's last kernel completes s->ev itself
     auto run = [&](const double* x, double* y) {
-      if (seg) model_->launch_segments(x, rows, cols, y, s->ws.get(), seg, nseg, st);
-      else model_->launch(x, rows, cols, y, s->ws.get(), st);
+      if (seg) {
+        model_->launch_segments(x, rows, cols, y, s->ws.get(), seg, nseg, st);
+        const int64_t base = model_->last_sequence_base();
+        int64_t off = 0;
+        for (auto& it : s->items) {
+          if (it.seq_out) *it.seq_out = base < 0 ? -1 : base + off;
+          off += it.rows;
+        }
+      } else {
+        model_->launch(x, rows, cols, y, s->ws.get(), st);
+      }
     };
     if (zc) {
       // Output always zero-copy (written once); input zero-copy only if the
@@ -944,7 +968,7 @@ struct SyncWait {
 };
 }  // namespace
 
-std::vector<double> BatchedUnit::run_ptr(const double* X, int rows, int cols) {
+std::vector<double> BatchedUnit::run_ptr(const double* X, int rows, int cols, int64_t* seq) {
   if (rows <= 0 || cols <= 0) throw std::runtime_error("run_ptr: empty input");
   const int want = model_->in_cols();
   if (want > 0 && cols != want)
@@ -961,6 +985,10 @@ std::vector<double> BatchedUnit::run_ptr(const double* X, int rows, int cols) {
   it.caller_mem = true;
   it.rows = rows;
   it.cols = cols;
+  if (seq) {  // written by the pump thread before the continuation; read after wait()
+    *seq = -1;
+    it.seq_out = seq;
+  }
   it.k = [w](Outcome o) { w->set(std::move(o)); };
   submit_item(std::move(it));
   Outcome o = w->wait();

@@ -123,7 +123,7 @@ class BatchedUnit : public Unit {
   std::vector<double> run_dense(const std::vector<double>& X, int rows, int cols);
   // Same, reading the rows straight from caller memory (kept alive by the
   // caller until the call returns): no copy before the GPU staging / DMA.
-  std::vector<double> run_ptr(const double* X, int rows, int cols);
+  std::vector<double> run_ptr(const double* X, int rows, int cols, int64_t* seq = nullptr);
 
   void stop();
 
@@ -145,6 +145,7 @@ class BatchedUnit : public Unit {
     Done k;
     ExecPtr exec;
     bool caller_mem = false;  // xp is the run_ptr caller's buffer (freed once the caller is answered)
+    int64_t* seq_out = nullptr;  // run_ptr callers: where the model applied this request's first row
   };
   struct Slot {
     PinnedBuffer h_in, h_out, h_seg;
@@ -251,6 +252,10 @@ class BatchedUnit : public Unit {
   std::atomic<int64_t> inflight_rows_{0};
   bool device_io_ = false;  // model needs device-memory I/O (no zero-copy)
   bool bar_input_ = false;  // SCA_BATCH_INPUT=bar on a large-BAR device
+  // HDP_MEM_COHERENCY_FLUSH_CNTL of the device (BAR staging): CPU stores into
+  // HBM pass the GPU's host data path, whose write buffer is flushed before
+  // the kernel that reads them is launched (SCA_HDP_FLUSH=0 skips it)
+  volatile uint32_t* hdp_flush_ = nullptr;
   bool zc_input_ = true;    // model reads X once per element (zero-copy input is cheaper than a DMA)
   bool segmented_ = false;
   bool cpu_ = false;        // device -1 with cpu_batching

@@ -134,6 +134,73 @@ void GraphModel::to_device(int device) {
       else if (e != hipSuccess) { (void)hipGetLastError(); peer_direct_ = false; }
     }
   if (split_ == 1) peer_direct_ = false;
+  build_fused();
+}
+
+void GraphModel::build_fused() {
+  fused_ = false;
+  if (const char* e = std::getenv("SCA_GRAPH_FUSE"))
+    if (std::atoi(e) == 0) return;
+  if (split_ || st_.empty() || int(st_.size()) > kern::kLinearGraphMaxStages || in_cols_ <= 0 ||
+      in_cols_ > kern::kLinearGraphMaxWidth)
+    return;
+  for (const auto& s : st_)
+    if (s.device != root_device_) return;
+  std::vector<int> oc;
+  try {
+    stage_cols(in_cols_, oc);
+  } catch (const std::exception&) {
+    return;
+  }
+  std::vector<kern::LinearGraphStage> fs(st_.size());
+  std::vector<double> params;
+  int slots = 0;
+  for (size_t i = 0; i < st_.size(); ++i) {
+    const auto& s = st_[i];
+    kern::LinearGraphStage& f = fs[i];
+    if (s.inputs.empty() || int(s.inputs.size()) > kern::kLinearGraphMaxInputs) return;
+    f.n_in = int(s.inputs.size());
+    for (size_t q = 0; q < s.inputs.size(); ++q) f.in[q] = s.inputs[q];
+    f.out_cols = oc[i];
+    if (oc[i] > kern::kLinearGraphMaxWidth) return;
+    if (s.kind == GraphStage::kMean) {
+      f.kind = 1;
+      f.C = oc[i];
+    } else {
+      const auto* lm = dynamic_cast<const LinearModel*>(s.model.get());
+      if (!lm || lm->features() > kern::kLinearGraphMaxWidth || lm->classes() > kern::kLinearGraphMaxWidth) return;
+      f.kind = 0;
+      f.K = lm->features();
+      f.C = lm->classes();
+      f.act = lm->activation();
+      f.w_off = int(params.size());
+      params.insert(params.end(), lm->weights().begin(), lm->weights().end());
+      if (!lm->bias().empty()) {
+        f.b_off = int(params.size());
+        params.insert(params.end(), lm->bias().begin(), lm->bias().end());
+      }
+    }
+    f.out_off = slots;
+    slots += oc[i];
+  }
+  if (slots > kern::kLinearGraphMaxSlots || int(params.size()) > kern::kLinearGraphMaxParams) return;
+  d_fstages_.alloc(fs.size() * sizeof(kern::LinearGraphStage), root_device_);
+  d_fstages_.upload(fs.data(), fs.size() * sizeof(kern::LinearGraphStage));
+  d_fparams_.alloc(std::max<size_t>(1, params.size()) * sizeof(double), root_device_);
+  if (!params.empty()) d_fparams_.upload(params.data(), params.size() * sizeof(double));
+  fused_stages_ = int(fs.size());
+  fused_params_ = int(params.size());
+  fused_slots_ = slots;
+  fused_ = true;
+}
+
+bool GraphModel::launch_signal(const double* X, int rows, int cols, double* out, void*, hipStream_t s,
+                               hipEvent_t done) {
+  if (!fused_ || cols != in_cols_) return false;
+  DeviceGuard g(root_device_);
+  kern::linear_graph_f64(X, rows, cols, d_fstages_.as<kern::LinearGraphStage>(), fused_stages_,
+                         d_fparams_.as<double>(), fused_params_, fused_slots_, out, s, done);
+  return true;
 }
 
 int GraphModel::lane_of(int stage) const {
@@ -210,6 +277,12 @@ GraphModel::Aux& GraphModel::aux_for(hipStream_t s, int rows, int cols) {
 void GraphModel::launch_segments(const double* X, int rows, int cols, double* out, void*, const int32_t* seg,
                                  int nseg, hipStream_t s) {
   if (root_device_ < 0) throw std::runtime_error("GraphModel: to_device() not called");
+  if (fused_ && cols == in_cols_) {
+    DeviceGuard g(root_device_);
+    kern::linear_graph_f64(X, rows, cols, d_fstages_.as<kern::LinearGraphStage>(), fused_stages_,
+                           d_fparams_.as<double>(), fused_params_, fused_slots_, out, s);
+    return;
+  }
   Aux& a = aux_for(s, rows, cols);
   const bool multi = a.ev_start.get() != nullptr;
   const size_t last = st_.size() - 1;

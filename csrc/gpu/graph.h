@@ -76,6 +76,11 @@ class GraphModel : public RowModel {
   void launch_segments(const double* X, int rows, int cols, double* out, void* ws, const int32_t* seg, int nseg,
                        hipStream_t s) override;
   void run_cpu(const double* X, int rows, int cols, double* out) const override;
+  // Fused graphs (every stage a small linear model or a mean, one GPU): the
+  // whole graph is one kernel, which completes `done` itself.
+  bool launch_signal(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
+                     hipEvent_t done) override;
+  bool fused() const { return fused_; }
 
   std::shared_ptr<RowModel> clone() const override { return clone_on(-2); }
   // Copy with every stage placed on `device` (-2: keep stage placement): one
@@ -111,6 +116,11 @@ class GraphModel : public RowModel {
   int root_device_ = -1;
   bool peer_direct_ = true;
   int split_ = 0;
+  // one-kernel form (kern::linear_graph_f64), built at to_device()
+  void build_fused();
+  bool fused_ = false;
+  int fused_stages_ = 0, fused_params_ = 0, fused_slots_ = 0;
+  DeviceBuffer d_fstages_, d_fparams_;
   std::mutex mu_;
   std::unordered_map<hipStream_t, std::unique_ptr<Aux>> aux_;
 };

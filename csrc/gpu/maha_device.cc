@@ -283,6 +283,8 @@ void MahalanobisModel::launch_segments(const double* X, int rows, int cols, doub
                                        const int32_t* seg, int nseg, hipStream_t s) {
   if (cols != st_->prm.p) throw std::runtime_error("Mahalanobis: expected " + std::to_string(st_->prm.p) + " features");
   std::lock_guard<std::recursive_mutex> g(st_->mu);
+  seq_base_ = st_->seq;
+  st_->seq += rows;
   // after the previous step on whatever stream it ran
   if (st_->chained) SCA_HIP_CHECK(hipStreamWaitEvent(s, st_->chain.get(), 0));
   double* eig = st_->d_eig.as<double>();
@@ -299,6 +301,8 @@ void MahalanobisModel::run_cpu(const double* X, int rows, int cols, double* out)
   if (cols != st_->prm.p) throw std::runtime_error("Mahalanobis: expected " + std::to_string(st_->prm.p) + " features");
   std::lock_guard<std::recursive_mutex> g(st_->mu);
   if (st_->device >= 0) throw std::runtime_error("Mahalanobis: state lives on the GPU (no CPU step)");
+  seq_base_ = st_->seq;
+  st_->seq += rows;
   maha_step_host(X, rows, view_, st_->h_state.data(), out);
 }
 
@@ -356,9 +360,9 @@ MahalanobisDevice::~MahalanobisDevice() {
   if (unit_) unit_->stop();
 }
 
-std::vector<double> MahalanobisDevice::step(const double* X, int nb) {
+std::vector<double> MahalanobisDevice::step(const double* X, int nb, int64_t* seq) {
   if (nb <= 0) return {};
-  return unit_->run_ptr(X, nb, model_->p());
+  return unit_->run_ptr(X, nb, model_->p(), seq);
 }
 
 std::shared_ptr<MahalanobisModel> MahalanobisDevice::predict_view(double threshold) const {

@@ -39,6 +39,9 @@ struct MahaState {
   // component can hold it across a pull -> host step -> push section
   // (MahalanobisDevice::lock_state) while state() / set_state() re-take it
   std::recursive_mutex mu;
+  // rows launched so far, every view (under mu): the application order the
+  // chained launches give the device state
+  int64_t seq = 0;
 };
 
 class MahalanobisModel : public RowModel {
@@ -52,6 +55,7 @@ class MahalanobisModel : public RowModel {
   int out_cols(int) const override { return 1; }
   void to_device(int device) override;
   bool segmented() const override { return true; }
+  int64_t last_sequence_base() const override { return seq_base_; }
   bool zero_copy_input() const override { return false; }
   bool zero_copy_input_for(int rows, int cols) const override { return size_t(rows) * cols <= 4096; }
   size_t workspace_bytes(int max_rows, int cols) const override;
@@ -75,6 +79,7 @@ class MahalanobisModel : public RowModel {
   void init_state(int device);
   std::shared_ptr<MahaState> st_;
   kern::MahaParams view_;  // prm with this view's out_mode / threshold
+  mutable int64_t seq_base_ = -1;  // this view's last launch (one batcher, one pump thread)
 };
 
 // Synchronous scores for the Python component: one batcher over a scores view.
@@ -85,7 +90,7 @@ class MahalanobisDevice {
  public:
   MahalanobisDevice(int p, int k, double n_stdev, double start_clip, double max_n, double eps, int device);
   ~MahalanobisDevice();
-  std::vector<double> step(const double* X, int nb);
+  std::vector<double> step(const double* X, int nb, int64_t* seq = nullptr);
   std::vector<double> state() const { return model_->state(); }
   void set_state(const std::vector<double>& s) { model_->set_state(s); }
   // Predictions view over the same state (for a native graph node).

@@ -65,6 +65,11 @@ class RowModel {
   // Segment-aware models compute per request (not per row): the batcher passes
   // the request boundaries (nseg + 1 row offsets, device-visible).
   virtual bool segmented() const { return false; }
+  // Stateful segmented models: the position in the state's application order
+  // of the first row of the last launch_segments() / run_cpu() call made on
+  // this view (-1: not tracked).  Read by the batcher right after the call,
+  // on the same thread, to tell each request where its rows were applied.
+  virtual int64_t last_sequence_base() const { return -1; }
   virtual void launch_segments(const double* X, int rows, int cols, double* out, void* ws, const int32_t* seg, int nseg,
                                hipStream_t s) {
     (void)seg;
@@ -127,6 +132,12 @@ class LinearModel : public RowModel {
   std::shared_ptr<RowModel> clone() const override {
     return with_meta(std::make_shared<LinearModel>(W_, b_, C_, K_, act_));
   }
+  // parameters, for graph fusion (csrc/kernels/linear_graph.hip)
+  const std::vector<double>& weights() const { return W_; }
+  const std::vector<double>& bias() const { return b_; }
+  int classes() const { return C_; }
+  int features() const { return K_; }
+  int activation() const { return act_; }
 
  private:
   std::vector<double> W_, b_;

@@ -26,6 +26,31 @@ enum LinearAct : int {
 // fp64 I/O, fp64 accumulate (parity with sklearn to ~1e-15).
 // `stop` (optional): completed by the kernel's own dispatch, replacing a
 // hipEventRecord after it.
+// Fused device graph of small linear stages (linear_graph.hip): one thread
+// per row runs every stage in LDS.  kind 0 = linear (K, C <= 16), 1 = mean
+// over n_in inputs; in[] = producer stages (-1 = the request row); out_off =
+// the stage's first activation slot; out_cols = its output width (2 for a
+// binary logistic stage).
+constexpr int kLinearGraphMaxStages = 16;
+constexpr int kLinearGraphMaxWidth = 16;
+constexpr int kLinearGraphMaxInputs = 8;
+constexpr int kLinearGraphMaxSlots = 96;    // activation doubles per row
+constexpr int kLinearGraphMaxParams = 4096; // W + b doubles of every stage
+struct LinearGraphStage {
+  int kind = 0;
+  int n_in = 1;
+  int in[kLinearGraphMaxInputs] = {};
+  int K = 0, C = 0, act = 0;
+  int w_off = 0, b_off = -1;
+  int out_off = 0, out_cols = 0;
+};
+size_t linear_graph_lds_bytes(int n_params, int act_slots);
+void linear_graph_f64(const double* X, int rows, int cols, const LinearGraphStage* stages, int n_stages,
+                      const double* params, int n_params, int act_slots, double* out, hipStream_t stream,
+                      hipEvent_t stop = nullptr);
+
+// True when linear_f64 runs this shape on the f64 matrix cores (SCA_LINEAR_MFMA=0 off, =2 forced).
+bool linear_uses_mfma(int rows, int K, int C);
 void linear_f64(const double* X, int rows, int K, const double* W, const double* b, int C, int act,
                 double* out, hipStream_t stream, hipEvent_t stop = nullptr);
 

@@ -2,14 +2,18 @@
 // servers/sklearnserver/sklearnserver/SKLearnServer.py:32-42 which calls
 // sklearn's predict_proba on the CPU for every request).
 //
-// Two CDNA4 mappings, chosen by shape on the host:
+// Three CDNA4 mappings, chosen by shape on the host:
 //  * thread-per-row: tiny K*C (iris: K=4, C=3).  W, b and the per-thread
 //    logits live in LDS; a 64-wide wave covers 64 requests of a micro-batch.
-//  * wave-per-row: larger K.  Lanes stride K (coalesced row reads), each
-//    class logit is a 64-lane shuffle reduction; logits staged in LDS.
+//  * wave-per-row: larger K, small batches.  Lanes stride K (coalesced row
+//    reads), each class logit is a 64-lane shuffle reduction.
+//  * MFMA: large batches / wide models (rows*K*C >= 2^20, C <= 1024): the
+//    logits GEMM on v_mfma_f64_16x16x4 with the activation fused.
 // fp64 throughout so results match sklearn bit-for-bit up to summation order.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -104,6 +108,216 @@ __global__ __launch_bounds__(kBlock) void linear_wave_rows(const double* __restr
   }
 }
 
+// ---------------------------------------------------------------- MFMA path
+// Large batches and wide models (rows * K * C >= 2^20, C <= 1024): the
+// logits tile is a GEMM on the fp64 matrix cores, v_mfma_f64_16x16x4 --
+// A = 16 rows of X x 4 k, B = 4 k x 16 classes of W^T, result lane l holds
+// rows (l>>4) + 4i of column l&15 -- with bias + softmax / sigmoid fused into
+// the epilogue, so logits never reach HBM.
+//
+// One workgroup (4 waves) owns 16 rows and EVERY class, so the row
+// normaliser needs no second pass: the waves split the classes (CW waves x
+// NCT 16-column tiles each) and the rest of the factor 4 splits K (KS = 4 /
+// CW slices, partial logits summed through LDS).  Operands come straight
+// from global memory as 32-byte vectors: lane group g = l>>4 reads k = 4g..4g+3
+// of its row / class for a 16-k chunk and feeds them to the chunk's 4 MFMAs
+// as k-step s = 0..3 -- the k order inside a chunk is permuted identically in
+// A and B, so the dot products are exact sums of the same terms.  K past the
+// end (and classes past C) are fed as zeros.
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+
+constexpr int kMfmaRows = 16;
+constexpr int kMfmaThreads = 256;
+
+template <int ACT, int NCT, int CW>
+__global__ __launch_bounds__(kMfmaThreads) void linear_mfma_rows(const double* __restrict__ X, int rows, int K,
+                                                                 const double* __restrict__ W,
+                                                                 const double* __restrict__ b, int C,
+                                                                 double* __restrict__ out) {
+  constexpr int KS = 4 / CW;                 // K slices per workgroup
+  __shared__ double red[KS > 1 ? (KS - 1) * NCT * 4 * 64 : 1];  // partial logits of slices 1..KS-1
+  __shared__ double rowst[CW][kMfmaRows];    // per-wave row max / sum
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cw = wave % CW, ks = wave / CW;
+  const int li = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * kMfmaRows;
+  const int row = r0 + li;                   // the A row this lane reads
+  const int col0 = cw * NCT * 16;            // first class of this wave
+  // K slice of this wave, in 16-k chunks
+  const int chunks = (K + 15) >> 4;
+  const int per = (chunks + KS - 1) / KS;
+  const int c_begin = ks * per, c_end = min(chunks, c_begin + per);
+  f64x4 acc[NCT];
+#pragma unroll
+  for (int t = 0; t < NCT; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const double* xr = X + size_t(row < rows ? row : 0) * K;
+  const bool vec = (K & 3) == 0;             // rows 32-byte aligned: vector loads
+  for (int c = c_begin; c < c_end; ++c) {
+    const int k = (c << 4) + (g << 2);
+    double a[4];
+    if (row < rows && vec && k + 3 < K) {
+      const double2 lo = *reinterpret_cast<const double2*>(xr + k);
+      const double2 hi = *reinterpret_cast<const double2*>(xr + k + 2);
+      a[0] = lo.x; a[1] = lo.y; a[2] = hi.x; a[3] = hi.y;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[s] = (row < rows && k + s < K) ? xr[k + s] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) {
+      const int j = col0 + t * 16 + li;      // the B column (class) this lane reads
+      const double* wr = W + size_t(j < C ? j : 0) * K;
+      double w[4];
+      if (j < C && vec && k + 3 < K) {
+        const double2 lo = *reinterpret_cast<const double2*>(wr + k);
+        const double2 hi = *reinterpret_cast<const double2*>(wr + k + 2);
+        w[0] = lo.x; w[1] = lo.y; w[2] = hi.x; w[3] = hi.y;
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) w[s] = (j < C && k + s < K) ? wr[k + s] : 0.0;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], w[s], acc[t], 0, 0, 0);
+    }
+  }
+  if constexpr (KS > 1) {  // slices 1.. hand their partial logits to slice 0
+    if (ks > 0) {  // (KS > 1 only with CW == 1: one wave per slice)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[((size_t(ks - 1) * NCT + t) * 4 + i) * 64 + lane] = acc[t][i];
+    }
+    __syncthreads();
+    if (ks > 0) return;
+#pragma unroll
+    for (int q = 0; q < KS - 1; ++q)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[t][i] += red[((size_t(q) * NCT + t) * 4 + i) * 64 + lane];
+  }
+  // ---- epilogue: lane holds rows g + 4i (i = 0..3) of columns col0 + 16t + li
+  double bias[NCT];
+#pragma unroll
+  for (int t = 0; t < NCT; ++t) {
+    const int j = col0 + t * 16 + li;
+    bias[t] = (b && j < C) ? b[j] : 0.0;
+  }
+#pragma unroll
+  for (int t = 0; t < NCT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[t][i] += bias[t];
+  const int out_cols = ACT == kActBinaryLogistic ? 2 : C;
+  if constexpr (ACT == kActSoftmax || ACT == kActOvr) {
+    // row normaliser over every class: lanes (16 per row group), then waves
+    double m[4], ssum[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double v = ACT == kActSoftmax ? -__builtin_inf() : 0.0;
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const int j = col0 + t * 16 + li;
+        if (ACT == kActSoftmax) v = j < C ? fmax(v, acc[t][i]) : v;
+      }
+      m[i] = v;
+    }
+    if constexpr (ACT == kActSoftmax) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) m[i] = fmax(m[i], __shfl_xor(m[i], off, 64));
+      if constexpr (CW > 1) {
+        if (li == 0)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rowst[cw][g + 4 * i] = m[i];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double v = rowst[0][g + 4 * i];
+#pragma unroll
+          for (int q = 1; q < CW; ++q) v = fmax(v, rowst[q][g + 4 * i]);
+          m[i] = v;
+        }
+        __syncthreads();
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double v = 0.0;
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const int j = col0 + t * 16 + li;
+        const double e = ACT == kActSoftmax ? exp(acc[t][i] - m[i]) : sigmoid(acc[t][i]);
+        acc[t][i] = e;
+        v += j < C ? e : 0.0;
+      }
+      ssum[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) ssum[i] += __shfl_xor(ssum[i], off, 64);
+    if constexpr (CW > 1) {
+      if (li == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rowst[cw][g + 4 * i] = ssum[i];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) v += rowst[q][g + 4 * i];
+        ssum[i] = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + g + 4 * i;
+      if (r >= rows) continue;
+      const double inv = 1.0 / ssum[i];
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const int j = col0 + t * 16 + li;
+        if (j < C) out[size_t(r) * out_cols + j] = acc[t][i] * inv;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + g + 4 * i;
+      if (r >= rows) continue;
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const int j = col0 + t * 16 + li;
+        if (j >= C) continue;
+        const double z = acc[t][i];
+        if constexpr (ACT == kActIdentity) {
+          out[size_t(r) * out_cols + j] = z;
+        } else if constexpr (ACT == kActBinaryLogistic) {
+          const double p = sigmoid(z);
+          out[size_t(r) * 2] = 1.0 - p;
+          out[size_t(r) * 2 + 1] = p;
+        } else {
+          out[size_t(r) * out_cols + j] = sigmoid(z);
+        }
+      }
+    }
+  }
+}
+
+// Shape rule of the MFMA path (also exported for the host's choice / tests).
+bool mfma_eligible(int rows, int K, int C) {
+  if (const char* e = std::getenv("SCA_LINEAR_MFMA")) {
+    if (std::atoi(e) == 0) return false;
+    if (std::atoi(e) == 2) return C <= 1024;  // forced on (tests, A/B)
+  }
+  return C <= 1024 && double(rows) * K * C >= double(1 << 20);
+}
+
+template <int ACT, int NCT, int CW>
+void launch_mfma_t(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
+                   hipStream_t s, hipEvent_t stop);
+
 // `stop` (optional) is completed by the kernel's own dispatch packet
 // (hipExtLaunchKernelGGL): one HIP call per batch instead of launch +
 // hipEventRecord (2.1 + 2.6 us of host time, tools/micro/launch_cost.hip).
@@ -114,11 +328,35 @@ void launch_maybe_ext(void (*k)(Args...), dim3 grid, dim3 block, size_t lds, hip
   else hipLaunchKernelGGL(k, grid, block, lds, s, args...);
 }
 
+template <int ACT, int NCT, int CW>
+void launch_mfma_t(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
+                   hipStream_t s, hipEvent_t stop) {
+  launch_maybe_ext(linear_mfma_rows<ACT, NCT, CW>, dim3((rows + kMfmaRows - 1) / kMfmaRows), dim3(kMfmaThreads), 0,
+                   s, stop, X, rows, K, W, b, C, out);
+}
+
+// Column tiling by C: up to 4 tiles in one wave (K split over the 4 waves),
+// else the 4 waves split the classes (NCT tiles each, <= 1024 classes).
+template <int ACT>
+void launch_mfma(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
+                 hipStream_t s, hipEvent_t stop) {
+  const int tiles = (C + 15) / 16;
+  if (tiles <= 1) launch_mfma_t<ACT, 1, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 2) launch_mfma_t<ACT, 2, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 4) launch_mfma_t<ACT, 4, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 8) launch_mfma_t<ACT, 2, 4>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 16) launch_mfma_t<ACT, 4, 4>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 32) launch_mfma_t<ACT, 8, 4>(X, rows, K, W, b, C, out, s, stop);
+  else launch_mfma_t<ACT, 16, 4>(X, rows, K, W, b, C, out, s, stop);
+}
+
 template <int ACT>
 void launch_linear(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
                    hipStream_t s, hipEvent_t stop) {
   if (rows <= 0) return;
-  if (C <= kMaxThreadC && C * K + C <= kMaxLdsDoubles) {
+  if (mfma_eligible(rows, K, C) && (ACT != kActBinaryLogistic || C == 1)) {
+    launch_mfma<ACT>(X, rows, K, W, b, C, out, s, stop);
+  } else if (C <= kMaxThreadC && C * K + C <= kMaxLdsDoubles) {
     const size_t lds = size_t(C * K + C + kBlock * C) * sizeof(double);
     launch_maybe_ext(linear_thread_rows<ACT>, dim3((rows + kBlock - 1) / kBlock), dim3(kBlock), lds, s, stop, X, rows,
                      K, W, b, C, out);
@@ -131,6 +369,8 @@ void launch_linear(const double* X, int rows, int K, const double* W, const doub
 }
 
 }  // namespace
+
+bool linear_uses_mfma(int rows, int K, int C) { return mfma_eligible(rows, K, C); }
 
 void linear_f64(const double* X, int rows, int K, const double* W, const double* b, int C, int act, double* out,
                 hipStream_t s, hipEvent_t stop) {

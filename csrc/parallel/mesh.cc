@@ -178,6 +178,11 @@ struct Exec {
 
 struct Mesh::Impl {
   std::vector<std::unique_ptr<Prog>> progs;
+  // peer readiness (probe_*): [producer][consumer] 1 = device slabs over IPC
+  std::vector<std::vector<int>> peer_ok;
+  gpu::DeviceBuffer probe_buf;                 // this worker's probe buffer
+  std::vector<void*> probe_opened;             // other workers' buffers, IPC-opened
+  std::string probe_err;
   bool prepared = false, connected = false, started = false;
   int timeout_ms = 60000;
   int delay_us = 0;
@@ -346,7 +351,13 @@ int Mesh::add_program(MeshProgram d) {
     for (int s : L.src) {
       const int w = P->width_of(s);
       const size_t slab = align_up(size_t(P->d.max_rows) * size_t(w) * sizeof(double), 256);
-      const bool dev = gpu() && c != 0 && s != -1;
+      // worker -> worker edges land in the consumer's HBM unless the peer
+      // probe failed for the producing rank (then: host-staged, "ipc-host")
+      bool dev = gpu() && c != 0 && s != -1;
+      if (dev && !im_->peer_ok.empty()) {
+        const int prod = P->d.stages[size_t(s)].rank;
+        dev = im_->peer_ok[size_t(prod)][size_t(c)] != 0;
+      }
       L.width.push_back(w);
       L.on_dev.push_back(dev ? 1 : 0);
       L.slab.push_back(slab);
@@ -403,6 +414,127 @@ int Mesh::messages_per_batch(int prog) const {
     if (P.part[size_t(c)] && P.lay[size_t(c)].index_of(-1) >= 0) ++m;
   for (auto& cs : P.consumers) m += int(cs.size());
   return m;
+}
+
+// ------------------------------------------------------------------ probe
+namespace {
+constexpr int kProbeLane = 32;  // doubles per rank lane of a probe buffer
+double probe_value(int owner, int writer, int i) { return 1e6 * (owner + 1) + 1e3 * (writer + 1) + i + 0.25; }
+}  // namespace
+
+std::string Mesh::probe_prepare() {
+  std::string blob(1 + sizeof(hipIpcMemHandle_t), '\0');
+  if (!gpu() || rank_ == 0) return blob;
+  gpu::DeviceGuard g(device_);
+  const size_t bytes = size_t(world_) * kProbeLane * sizeof(double);
+  im_->probe_buf.alloc(bytes, device_, true);  // fine-grained, like the program slabs
+  std::vector<double> pat(size_t(world_) * kProbeLane, 0.0);
+  for (int i = 0; i < kProbeLane; ++i) pat[size_t(rank_) * kProbeLane + size_t(i)] = probe_value(rank_, rank_, i);
+  SCA_HIP_CHECK(hipMemcpy(im_->probe_buf.get(), pat.data(), bytes, hipMemcpyHostToDevice));
+  hipIpcMemHandle_t h{};
+  SCA_HIP_CHECK(hipIpcGetMemHandle(&h, im_->probe_buf.get()));
+  blob[0] = 1;
+  std::memcpy(&blob[1], &h, sizeof h);
+  return blob;
+}
+
+std::vector<int> Mesh::probe_connect(const std::vector<std::string>& blobs) {
+  if (int(blobs.size()) != world_) throw std::runtime_error("Mesh::probe_connect: one blob per rank");
+  std::vector<int> res(size_t(world_), -1);
+  im_->probe_opened.assign(size_t(world_), nullptr);
+  if (!gpu() || rank_ == 0) return res;
+  const char* fe = std::getenv("SCA_MESH_FAULT");
+  const std::string fault = fe ? fe : "";
+  gpu::DeviceGuard g(device_);
+  gpu::DeviceBuffer mine(kProbeLane * sizeof(double), device_);
+  std::vector<double> pat(kProbeLane), back(kProbeLane);
+  auto note = [&](int r, const std::string& why) {
+    res[size_t(r)] = 0;
+    if (im_->probe_err.empty()) im_->probe_err = "rank " + std::to_string(rank_) + " -> " + std::to_string(r) + ": " + why;
+  };
+  for (int r = 1; r < world_; ++r) {
+    if (r == rank_) {
+      res[size_t(r)] = 1;
+      continue;
+    }
+    const std::string& b = blobs[size_t(r)];
+    if (b.size() < 1 + sizeof(hipIpcMemHandle_t) || b[0] == 0) {
+      note(r, "no probe buffer exported");
+      continue;
+    }
+    if (fault == "peer") {
+      note(r, "injected hipIpcOpenMemHandle failure (SCA_MESH_FAULT=peer)");
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, b.data() + 1, sizeof h);
+    void* dv = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&dv, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess || !dv) {
+      (void)hipGetLastError();
+      note(r, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+      continue;
+    }
+    im_->probe_opened[size_t(r)] = dv;
+    // the programs' write path: a device-to-device copy into the peer's HBM
+    for (int i = 0; i < kProbeLane; ++i) pat[size_t(i)] = probe_value(r, rank_, i);
+    double* lane = static_cast<double*>(dv) + size_t(rank_) * kProbeLane;
+    double* owner = static_cast<double*>(dv) + size_t(r) * kProbeLane;
+    bool ok = hipMemcpy(mine.get(), pat.data(), kProbeLane * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(lane, mine.get(), kProbeLane * sizeof(double), hipMemcpyDeviceToDevice) == hipSuccess &&
+              hipDeviceSynchronize() == hipSuccess &&
+              hipMemcpy(back.data(), lane, kProbeLane * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+    if (!ok) {
+      (void)hipGetLastError();
+      note(r, "canary copy failed");
+      continue;
+    }
+    for (int i = 0; i < kProbeLane && ok; ++i) ok = back[size_t(i)] == pat[size_t(i)];
+    if (ok && hipMemcpy(back.data(), owner, kProbeLane * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess) {
+      for (int i = 0; i < kProbeLane && ok; ++i) ok = back[size_t(i)] == probe_value(r, r, i);
+    } else {
+      ok = false;
+    }
+    if (fault == "canary") ok = false;
+    if (!ok) note(r, fault == "canary" ? "injected canary mismatch (SCA_MESH_FAULT=canary)" : "canary mismatch");
+    else res[size_t(r)] = 1;
+  }
+  return res;
+}
+
+std::string Mesh::probe_error() const { return im_->probe_err; }
+
+void Mesh::probe_finish() {
+  std::unique_ptr<gpu::DeviceGuard> g;
+  if (gpu() && rank_ != 0) g = std::make_unique<gpu::DeviceGuard>(device_);
+  for (void*& p : im_->probe_opened)
+    if (p) {
+      (void)hipIpcCloseMemHandle(p);
+      p = nullptr;
+    }
+  im_->probe_buf.reset();
+}
+
+void Mesh::set_peer_ok(const std::vector<std::vector<int>>& ok) {
+  if (!im_->progs.empty()) throw std::runtime_error("Mesh::set_peer_ok: before add_program");
+  if (int(ok.size()) != world_) throw std::runtime_error("Mesh::set_peer_ok: world x world matrix");
+  for (auto& row : ok)
+    if (int(row.size()) != world_) throw std::runtime_error("Mesh::set_peer_ok: world x world matrix");
+  im_->peer_ok = ok;
+}
+
+std::vector<std::tuple<int, int, std::string>> Mesh::edge_transports(int prog) const {
+  const Prog& P = *im_->progs.at(size_t(prog));
+  std::vector<std::tuple<int, int, std::string>> out;
+  for (size_t i = 0; i < P.consumers.size(); ++i)
+    for (int c : P.consumers[i]) {
+      std::string t;
+      if (!gpu()) t = "shm";
+      else if (c == 0) t = "host";
+      else t = P.slab_on_dev(c, int(i)) ? "ipc" : "ipc-host";
+      out.emplace_back(int(i), c, t);
+    }
+  return out;
 }
 
 // Blob: per program [u8 part][u32 len][name][u8 has_dev][hipIpcMemHandle_t]

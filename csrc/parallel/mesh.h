@@ -53,6 +53,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../gpu/hip_util.h"
@@ -117,6 +118,26 @@ class Mesh : public std::enable_shared_from_this<Mesh> {
   MeshStats stats() const;
   // Messages one batch of `prog` moves between ranks (edges of its DAG).
   int messages_per_batch(int prog) const;
+
+  // Peer readiness, before add_program (collective, same order everywhere):
+  // probe_prepare() -> exchange blobs -> probe_connect() -> exchange the
+  // rows -> set_peer_ok(matrix) -> barrier -> probe_finish().  Every GPU
+  // worker exports a small fine-grained buffer; every worker opens every
+  // other worker's buffer over HIP IPC, writes a canary into it with the
+  // same device-to-device copy the programs use, reads it back with the
+  // owner's pattern, and reports per rank: 1 ok, 0 failed, -1 not probed
+  // (rank 0, CPU gangs).  SCA_MESH_FAULT=peer|canary injects a failure.
+  // A worker -> worker edge whose probe failed gets a host-staged slab
+  // ("ipc-host") instead of the consumer's HBM.
+  std::string probe_prepare();
+  std::vector<int> probe_connect(const std::vector<std::string>& blobs);
+  std::string probe_error() const;
+  void probe_finish();
+  void set_peer_ok(const std::vector<std::vector<int>>& ok);  // [producer rank][consumer rank]
+  // Per edge of `prog`: (producer stage, consumer rank, transport) with
+  // transport "ipc" (consumer HBM over xGMI), "ipc-host" (host-staged after a
+  // failed probe), "host" (rank 0 / program input slabs), "shm" (CPU gangs).
+  std::vector<std::tuple<int, int, std::string>> edge_transports(int prog) const;
 
   // Rank 0: the front-end row model of a program (cpu_batching unit).
   gpu::RowModelPtr program_model(int prog, std::vector<std::string> class_names, bool flat);

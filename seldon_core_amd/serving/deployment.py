@@ -238,6 +238,9 @@ class Deployment:
         st = meshmod.setup(self.fabric, self.predictor["graph"], self._no_local_stage, max_rows=mr,
                            bound=set(self.components))
         self.mesh = st
+        if st.peer.get("failed_edges"):
+            logger.warning("mesh peer probe: edges %s fall back to host-staged slabs (%s)", st.peer["failed_edges"],
+                           "; ".join(st.peer.get("errors") or []))
         nodes = {n["name"]: n for n, _ in iter_nodes(self.predictor["graph"])}
         for p, pid, fin in zip(st.programs, st.ids, st.finals):
             pm = self.fabric.program_model(pid, list(fin.get("names") or []), bool(fin.get("flat")))
@@ -248,8 +251,11 @@ class Deployment:
             self.engine.bind_fused(p.root, unit, p.absorbed)
             self.batched[p.root] = unit
             self.units[p.root] = unit
-            logger.info("mesh program %s (%s, %d messages per batch): %s", p.root, self.fabric.transport,
-                        st.messages[st.ids.index(pid)], p.describe())
+            i = st.ids.index(pid)
+            logger.info("mesh program %s (%s, %d messages per batch): %s; edges %s", p.root, self.fabric.transport,
+                        st.messages[i], p.describe(),
+                        ", ".join(f"{e['from']}->{e['to_rank']}:{e['transport']}" for e in
+                                  (st.edges[i] if i < len(st.edges) else [])))
 
     @staticmethod
     def _no_local_stage(node: Dict):

@@ -58,6 +58,15 @@ def build(mode, world):
             {"name": "comb", "type": "COMBINER", "implementation": "AVERAGE_COMBINER",
              "children": [{"name": "a", "type": "MODEL", "rank": 1}, {"name": "b", "type": "MODEL", "rank": 2}]}]}
         return g, {"scaler": s, "a": lr, "b": lr}, lambda X: proba(np.asarray(X) * scale), opts
+    if mode == "nested_combiner":  # AVERAGE(AVERAGE(a@1, b@2), c@3), no ranks on the combiners
+        W2 = np.random.default_rng(7).normal(size=(3, 4)) * 0.1
+        s = C.linear_model(W2, np.zeros(3), 0)
+        g = {"name": "outer", "type": "COMBINER", "implementation": "AVERAGE_COMBINER", "children": [
+            {"name": "inner", "type": "COMBINER", "implementation": "AVERAGE_COMBINER",
+             "children": [{"name": "a", "type": "MODEL", "rank": 1}, {"name": "b", "type": "MODEL", "rank": 2}]},
+            {"name": "c", "type": "MODEL", "rank": 3}]}
+        return (g, {"a": lr, "b": s, "c": lr},
+                lambda X: 0.5 * (0.5 * (proba(X) + np.asarray(X) @ W2.T) + proba(X)), opts)
     if mode == "python":  # a Python TRANSFORMER on rank 1 feeding the iris MODEL on rank 2
         g = {"name": "double", "type": "TRANSFORMER", "rank": 1, "in_cols": 4,
              "children": [{"name": "m", "type": "MODEL", "rank": 2}]}
@@ -157,10 +166,13 @@ def main():
     kinds = {name: dep.engine.unit_kind(name) for name in dep.engine.node_names()}
     msgs = list(dep.mesh.messages) if dep.mesh is not None else []
     programs = [p.describe() for p in dep.mesh.programs] if dep.mesh is not None else []
+    edges = list(dep.mesh.edges) if dep.mesh is not None else []
+    peer = dict(dep.mesh.peer) if dep.mesh is not None else {}
     dep.close()  # stops the workers' loops
     fabric.close()
     print(json.dumps({"rank": 0, "worst": worst[0], "rows": rows[0], "errors": errors, "failed": failed[0],
-                      "kinds": kinds, "messages": msgs, "programs": programs, "transport": fabric.transport}),
+                      "kinds": kinds, "messages": msgs, "programs": programs, "transport": fabric.transport,
+                      "edges": edges, "peer": peer}),
           flush=True)
     dist.barrier()
     dist.destroy_process_group()

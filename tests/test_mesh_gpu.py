@@ -105,3 +105,24 @@ def test_ipc_large_chunked_wide():
     outs = _run_gpu_ranks(2, "large")
     assert outs[0]["errors"] == [] and outs[0]["worst"] < 1e-9, outs[0]
     assert outs[1]["error"] == "" and outs[1]["rows"] == outs[0]["rows"], outs[1]
+
+
+def test_ipc_pipeline_edges_are_device_slabs_after_a_clean_probe():
+    front = _check(_run_gpu_ranks(4, "pipeline"), [4])
+    (edges,) = front["edges"]
+    kinds = {(e["from"], e["to_rank"]): e["transport"] for e in edges}
+    assert kinds == {("s1@1", 2): "ipc", ("s2@2", 3): "ipc", ("m@3", 0): "host"}, kinds
+    assert front["peer"]["failed_edges"] == [] and front["peer"]["devices"] == [0, 0, 0, 0], front["peer"]
+
+
+@pytest.mark.parametrize("fault", ["peer", "canary"])
+def test_ipc_probe_failure_falls_back_to_host_staged_edges(fault):
+    """an injected hipIpcOpenMemHandle failure (or canary
+    mismatch) on every worker -> worker edge: the gang still serves, those
+    edges become host-staged slabs ("ipc-host"), answers stay at 1e-12."""
+    front = _check(_run_gpu_ranks(4, "pipeline", SCA_MESH_FAULT=fault), [4])
+    (edges,) = front["edges"]
+    kinds = {(e["from"], e["to_rank"]): e["transport"] for e in edges}
+    assert kinds == {("s1@1", 2): "ipc-host", ("s2@2", 3): "ipc-host", ("m@3", 0): "host"}, kinds
+    assert {"1->2", "2->3", "3->1"} <= set(front["peer"]["failed_edges"]), front["peer"]
+    assert any(fault in e for e in front["peer"]["errors"]), front["peer"]

@@ -406,10 +406,14 @@ def test_mahalanobis_device_concurrent_callers_share_launches():
     data = [rng.normal(size=(1, p)) * np.linspace(1, 2, p) for _ in range(1600)]
     errs = []
 
+    seqs = {}
+
     def worker(t):
         try:
-            for X in data[t::16]:
-                assert dev.step(X).shape == (1,)
+            for i in range(t, len(data), 16):
+                sc, seq = dev.step_seq(data[i])
+                assert sc.shape == (1,)
+                seqs[i] = seq
         except Exception as e:  # pragma: no cover - reported below
             errs.append(e)
 
@@ -426,16 +430,18 @@ def test_mahalanobis_device_concurrent_callers_share_launches():
     allX = np.concatenate(data)
     np.testing.assert_allclose(st[:p], allX.mean(0), rtol=1e-9, atol=1e-12)
     # the running covariance depends on the arrival order (the reference's
-    # recursion uses the running mean at each step): only close, not equal.
-    # 16 threads may run far out of step, and a full reordering of these
-    # rows moves the recursion's C by up to ~0.09 (numpy, 3 random
-    # permutations: 0.065 / 0.092 / 0.084), so the bound is set above that.
+    # recursion uses the running mean at each step), so the oracle replays
+    # numpy in the order the device applied the requests (step_seq): every
+    # request exactly once, at distinct positions 0..1599, and C equal to
+    # the reference recursion in that order
+    order = sorted(seqs, key=seqs.get)
+    assert sorted(seqs.values()) == list(range(1600))
     ref = OutlierMahalanobis(n_components=k, start_clip=10 ** 12, device=-1)
-    for X in data:
-        ref.predict(X.copy(), [])
+    for i in order:
+        ref.predict(data[i].copy(), [])
     Cg = st[p:p + p * p].reshape(p, p)
     np.testing.assert_allclose(Cg, Cg.T, rtol=0, atol=1e-15)
-    np.testing.assert_allclose(Cg, ref.C, rtol=0, atol=0.15)
+    np.testing.assert_allclose(Cg, ref.C, rtol=0, atol=1e-9)
 
 
 def test_mahalanobis_python_and_native_entry_points_do_not_lose_steps():

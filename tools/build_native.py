@@ -35,7 +35,7 @@ LIB_SOURCES = [
     "core/engine.cc", "core/units.cc", "core/msglog.cc", "core/roctx.cc", "core/cpuprof.cc",
     "server/http_server.cc", "server/grpc_server.cc", "server/remote_unit.cc",
     "gpu/models.cc", "gpu/batcher.cc", "gpu/driver.cc", "gpu/router.cc", "gpu/graph.cc", "gpu/replica.cc", "gpu/mlp_model.cc", "gpu/lstm_model.cc", "gpu/maha_device.cc", "parallel/fabric.cc", "parallel/mesh.cc",
-    "kernels/linear.hip", "kernels/tree.hip", "kernels/combine.hip", "kernels/bandit.hip", "kernels/image.hip", "kernels/mlp.hip", "kernels/mahalanobis.hip", "kernels/lstm.hip", "kernels/lstm_valu.hip", "kernels/gemm.hip",
+    "kernels/linear.hip", "kernels/linear_graph.hip", "kernels/tree.hip", "kernels/combine.hip", "kernels/bandit.hip", "kernels/image.hip", "kernels/mlp.hip", "kernels/mahalanobis.hip", "kernels/lstm.hip", "kernels/lstm_valu.hip", "kernels/gemm.hip",
     "bindings/module.cc",
 ]
 LOADGEN_SOURCES = ["tools/loadgen.cc", "core/json.cc"]
