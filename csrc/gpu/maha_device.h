@@ -56,6 +56,10 @@ class MahalanobisModel : public RowModel {
   void to_device(int device) override;
   bool segmented() const override { return true; }
   int64_t last_sequence_base() const override { return seq_base_; }
+  // launch_segments() takes the state mutex, which the Python component holds
+  // across its pull -> host step -> push section: a pump thread of
+  // its own, so that wait never stalls the other units on this GPU
+  bool exclusive_driver() const override { return true; }
   bool zero_copy_input() const override { return false; }
   bool zero_copy_input_for(int rows, int cols) const override { return size_t(rows) * cols <= 4096; }
   size_t workspace_bytes(int max_rows, int cols) const override;

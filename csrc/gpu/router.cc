@@ -1,6 +1,7 @@
 #include "router.h"
 
 #include <fcntl.h>
+#include <pthread.h>
 #include <signal.h>
 #include <immintrin.h>
 #include <sys/mman.h>
@@ -17,13 +18,14 @@
 namespace sca::gpu {
 
 // One bandit's state shared by the engine processes of a host.  Updates take
-// a spinlock in the mapping (feedback is rare next to routing, and the
-// critical section is a few hundred nanoseconds); readers compare `version`
-// with the last one they pulled.  A lock whose owner process died inside the
-// critical section is taken over (ShmLock).
+// a robust process-shared mutex in the mapping (feedback is rare next to
+// routing, and the critical section is a few hundred nanoseconds); readers
+// compare `version` with the last one they pulled.  A lock whose owner
+// process died inside the critical section passes to the next waiter
+// (ShmLock, EOWNERDEAD).
 struct BanditModel::Shared {
   std::atomic<uint32_t> init;  // 0 fresh, 1 being seeded, 2 ready
-  std::atomic<uint32_t> lock;
+  pthread_mutex_t mu;          // process-shared, robust (initialised by the seeding worker)
   std::atomic<uint64_t> version;
   std::atomic<int32_t> best;
   int32_t kind, nb;
@@ -32,34 +34,30 @@ struct BanditModel::Shared {
 };
 
 namespace {
-// The lock word holds the owner's PID.  A waiter takes the lock over only
-// when that process no longer exists (kill(pid, 0) -> ESRCH): an owner that
-// is merely descheduled (CPU quota throttling, SIGSTOP) keeps it.
+// A robust process-shared mutex in the mapping: the kernel hands a lock
+// whose owner died inside the critical section to the next waiter with
+// EOWNERDEAD (no PID liveness guess, which fails across PID namespaces and
+// on PID reuse).  The dead owner's partial update is at most one feedback's
+// counters; the state is marked consistent and used as is.
 struct ShmLock {
-  std::atomic<uint32_t>& l;
-  explicit ShmLock(std::atomic<uint32_t>& lk) : l(lk) {
-    const uint32_t me = uint32_t(getpid());
-    auto t_check = std::chrono::steady_clock::now();
-    for (unsigned n = 0;; ++n) {
-      uint32_t z = 0;
-      if (l.compare_exchange_weak(z, me, std::memory_order_acquire)) return;
-      if (n < 4096) {
-        _mm_pause();
-        continue;
-      }
-      std::this_thread::yield();
-      const auto now = std::chrono::steady_clock::now();
-      if (now - t_check > std::chrono::milliseconds(100)) {
-        t_check = now;
-        uint32_t owner = l.load(std::memory_order_relaxed);
-        if (owner != 0 && owner != me && ::kill(pid_t(owner), 0) != 0 && errno == ESRCH &&
-            l.compare_exchange_strong(owner, me, std::memory_order_acquire))
-          return;  // the owner died inside the critical section
-      }
-    }
+  pthread_mutex_t* m;
+  explicit ShmLock(pthread_mutex_t& mu) : m(&mu) {
+    const int r = pthread_mutex_lock(m);
+    if (r == EOWNERDEAD) pthread_mutex_consistent(m);
+    else if (r != 0) throw std::runtime_error(std::string("bandit: shared lock failed: ") + std::strerror(r));
   }
-  ~ShmLock() { l.store(0, std::memory_order_release); }
+  ~ShmLock() { pthread_mutex_unlock(m); }
 };
+
+void init_shared_mutex(pthread_mutex_t* m) {
+  pthread_mutexattr_t a;
+  pthread_mutexattr_init(&a);
+  pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+  pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST);
+  const int r = pthread_mutex_init(m, &a);
+  pthread_mutexattr_destroy(&a);
+  if (r != 0) throw std::runtime_error(std::string("bandit: shared mutex init failed: ") + std::strerror(r));
+}
 }  // namespace
 
 BanditModel::~BanditModel() {
@@ -81,6 +79,7 @@ void BanditModel::attach_shared(const std::string& name, int worker) {
   uint32_t fresh = 0;
   std::lock_guard<std::mutex> g(mu_);
   if (sh->init.compare_exchange_strong(fresh, 1)) {  // first worker seeds the shared state with its own
+    init_shared_mutex(&sh->mu);
     sh->kind = int32_t(kind_);
     sh->nb = nb_;
     for (int i = 0; i < nb_; ++i) {
@@ -114,7 +113,7 @@ void BanditModel::attach_shared(const std::string& name, int worker) {
 }
 
 void BanditModel::pull_shared() {
-  ShmLock l(shm_->lock);
+  ShmLock l(shm_->mu);
   for (int i = 0; i < nb_; ++i) {
     success_[size_t(i)] = shm_->success[i];
     tries_[size_t(i)] = shm_->tries[i];
@@ -220,7 +219,7 @@ void BanditModel::feedback(int routing, int n_success, int n_failures) {
   if (routing < 0 || routing >= nb_) throw std::runtime_error("bandit feedback: invalid routing " + std::to_string(routing));
   std::lock_guard<std::mutex> g(mu_);
   if (shm_) {  // the update happens on the shared counters, under their lock
-    ShmLock l(shm_->lock);
+    ShmLock l(shm_->mu);
     for (int i = 0; i < nb_; ++i) {
       success_[size_t(i)] = shm_->success[i];
       tries_[size_t(i)] = shm_->tries[i];
@@ -319,7 +318,7 @@ void BanditModel::restore(const std::string& s) {
     // since the checkpoint is kept.
     const Json* v = j.find("version");
     const uint64_t snap_v = v ? uint64_t(v->as_number()) : 0;
-    ShmLock l(shm_->lock);
+    ShmLock l(shm_->mu);
     const uint64_t live_v = shm_->version.load(std::memory_order_acquire);
     // version 1: seeded by the first worker, no feedback, nothing restored yet
     if (live_v <= 1 || snap_v > live_v) {

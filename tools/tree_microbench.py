@@ -91,7 +91,7 @@ def main():
                     if c <= cap:
                         variants.append((f"fused_lds_rb{r}_c{c}", c, c, True, r))
         if a.small:  # whole ensemble split over `parts` workgroups per row tile (atomic fold)
-            for parts in (2, 4, 8, 16):
+            for parts in (4, 8, 16, 32):
                 variants.append((f"split{parts}", parts, 0, "split"))
         for v in variants:
             name, chunk, lds, fused = v[:4]
