@@ -1030,6 +1030,13 @@ PYBIND11_MODULE(_C, m) {
                              depth, cmp_le, n_trees, parts, P<const float>(base), scale, transform, P<double>(out),
                              out_cols, P<double>(acc), P<int>(counter), as_stream(s));
   });
+  k.def("tree_perfect_tile", [](uintptr_t X, int rows, int F, uintptr_t nodes, uintptr_t leaves, int depth,
+                                int cmp_le, int n_trees, uintptr_t base, float scale, int transform, uintptr_t out,
+                                int out_cols, uintptr_t acc, uintptr_t counter, uintptr_t s) {
+    return kern::tree_perfect_tile(P<const double>(X), rows, F, P<const kern::TreeNode>(nodes), P<const float>(leaves),
+                                   depth, cmp_le, n_trees, P<const float>(base), scale, transform, P<double>(out),
+                                   out_cols, P<double>(acc), P<int>(counter), as_stream(s));
+  });
   k.def("tree_reduce", [](uintptr_t partial, int rows, int n_chunks, uintptr_t chunk_group, int groups,
                           uintptr_t base, float scale, int transform, uintptr_t out, int out_cols, uintptr_t s) {
     kern::tree_reduce(P<const double>(partial), rows, n_chunks, P<const int>(chunk_group), groups, P<const float>(base),

@@ -431,7 +431,8 @@ bool BatchedUnit::launch(Slot* s) {
     // zero-copy batches on a large-BAR device: rows straight into HBM -- for
     // kernels that read each row once (fine-grained HBM is not L2-cached, so
     // models that re-read X from many workgroups keep their DMA into d_in)
-    const bool bar = zc && bar_input_ && s->v_in.bytes() >= bin && (zc_input_ || model_->zero_copy_input_for(rows, cols));
+    const bool bar = zc && bar_input_ && s->v_in.bytes() >= bin &&
+                     (zc_input_ || model_->zero_copy_input_for(rows, cols) || model_->bar_input_for(rows, cols));
     if (!direct) {
       double* dst = bar ? s->v_in.as<double>() : hin;
       size_t off = 0;

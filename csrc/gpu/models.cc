@@ -197,7 +197,16 @@ bool TreeEnsembleModel::uses_whole(int rows) const {
   return spec_.depth > 0 && spec_.groups == 1 && rows <= whole_max_rows_;
 }
 
+bool TreeEnsembleModel::uses_tile(int rows) const {
+  return uses_whole(rows) && spec_.depth >= 4 && spec_.depth <= 10 && rows <= kSplitMaxRows &&
+         rows <= kern::tree_tile_max_rows() &&
+         !(kern::tree_split_parts() > 0 && rows <= std::min(kSplitMaxRows, kern::tree_split_max_rows()));
+}
+
 bool TreeEnsembleModel::zero_copy_input_for(int rows, int cols) const {
+  // tree tiles: every tree chunk's workgroups re-read the rows -- HBM only
+  // (BAR-written, bar_input_for, or DMA'd), never pinned host memory
+  if (uses_tile(rows)) return false;
   // whole-ensemble kernel: each workgroup reads its rows once
   if (uses_whole(rows)) return size_t(rows) * size_t(cols) * sizeof(double) <= (256u << 10);
   int rb, pi;
@@ -237,6 +246,14 @@ bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double*
                              spec_.scale, spec_.transform, out, spec_.out_cols, reinterpret_cast<double*>(hdr + 256),
                              reinterpret_cast<int*>(hdr + 128), s, done);
     return done != nullptr;
+  }
+  if (uses_tile(rows)) {
+    char* hdr = static_cast<char*>(ws);
+    if (kern::tree_perfect_tile(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
+                                spec_.depth, spec_.cmp_le, spec_.n_trees, d_base_.as<float>(), spec_.scale,
+                                spec_.transform, out, spec_.out_cols, reinterpret_cast<double*>(hdr + 256),
+                                reinterpret_cast<int*>(hdr + 128), s, done))
+      return done != nullptr;
   }
   if (uses_whole(rows)) {
     kern::tree_perfect_whole(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),

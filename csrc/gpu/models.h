@@ -62,6 +62,10 @@ class RowModel {
   // geometry may still read small batches straight from pinned host memory
   // (saves the H2D blit launch).
   virtual bool zero_copy_input_for(int rows, int cols) const { (void)rows; (void)cols; return zero_copy_input(); }
+  // Rows many workgroups re-read (not zero-copy from pinned host), but which
+  // may be written straight into HBM through the BAR (SCA_BATCH_INPUT=bar)
+  // instead of DMA'd there.
+  virtual bool bar_input_for(int rows, int cols) const { (void)rows; (void)cols; return false; }
   // Segment-aware models compute per request (not per row): the batcher passes
   // the request boundaries (nseg + 1 row offsets, device-visible).
   virtual bool segmented() const { return false; }
@@ -186,6 +190,9 @@ class TreeEnsembleModel : public RowModel {
   bool zero_copy_input() const override { return false; }  // every tree-chunk block stages the X tile
   // Host reads = rows x cols x 8 B x chunks: zero-copy while that stays small.
   bool zero_copy_input_for(int rows, int cols) const override;
+  bool bar_input_for(int rows, int cols) const override { (void)cols; return uses_tile(rows); }
+  // mid-size batches of single-output perfect ensembles: kern::tree_perfect_tile
+  bool uses_tile(int rows) const;
   std::shared_ptr<RowModel> clone() const override {
     auto m = std::make_shared<TreeEnsembleModel>(spec_);
     m->fused_reduce_ = fused_reduce_;

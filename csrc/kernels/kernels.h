@@ -138,6 +138,13 @@ int tree_whole_rows_per_block(int n_trees, int rows);
 // batches of up to 32 rows); depths 4..10.
 int tree_split_parts();
 int tree_split_max_rows();
+// Tree-major tiles for mid-size batches (single output, depth 4..10): one
+// launch, trees staged in LDS per row tile, atomic row fold (acc / counter as
+// tree_perfect_split).  Returns false when the shape does not apply.
+bool tree_perfect_tile(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                       int cmp_le, int n_trees, const float* base_margin, float scale, int transform, double* out,
+                       int out_cols, double* acc, int* counter, hipStream_t stream, hipEvent_t stop = nullptr);
+int tree_tile_max_rows();  // SCA_TREE_TILE_ROWS (default 256; 0 = off)
 void tree_perfect_split(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, int n_trees, int parts, const float* base_margin, float scale, int transform,
                         double* out, int out_cols, double* acc, int* counter, hipStream_t s,

@@ -126,182 +126,197 @@ __global__ __launch_bounds__(kBlock) void linear_wave_rows(const double* __restr
 // end (and classes past C) are fed as zeros.
 using f64x4 = __attribute__((ext_vector_type(4))) double;
 
-constexpr int kMfmaRows = 16;
-constexpr int kMfmaThreads = 256;
-
-template <int ACT, int NCT, int CW>
-__global__ __launch_bounds__(kMfmaThreads) void linear_mfma_rows(const double* __restrict__ X, int rows, int K,
+// NCT 16-column tiles x RT 16-row tiles per wave; CW waves split the classes
+// and KS waves split K (KS > 1 only with CW == 1); a workgroup owns 16 RT rows
+// and every class.
+template <int ACT, int NCT, int CW, int KS, int RT>
+__global__ __launch_bounds__(64 * CW * KS) void linear_mfma_rows(const double* __restrict__ X, int rows, int K,
                                                                  const double* __restrict__ W,
                                                                  const double* __restrict__ b, int C,
                                                                  double* __restrict__ out) {
-  constexpr int KS = 4 / CW;                 // K slices per workgroup
-  __shared__ double red[KS > 1 ? (KS - 1) * NCT * 4 * 64 : 1];  // partial logits of slices 1..KS-1
-  __shared__ double rowst[CW][kMfmaRows];    // per-wave row max / sum
+  static_assert(KS == 1 || CW == 1, "split K or split classes");
+  constexpr int R = 16 * RT;                 // rows per workgroup
+  __shared__ double red[KS > 1 ? (KS - 1) * NCT * RT * 4 * 64 : 1];  // partial logits of slices 1..KS-1
+  __shared__ double rowst[CW][R];            // per-wave row max / sum
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int cw = wave % CW, ks = wave / CW;
   const int li = lane & 15, g = lane >> 4;
-  const int r0 = blockIdx.x * kMfmaRows;
-  const int row = r0 + li;                   // the A row this lane reads
+  const int r0 = blockIdx.x * R;
   const int col0 = cw * NCT * 16;            // first class of this wave
-  // K slice of this wave, in 16-k chunks
-  const int chunks = (K + 15) >> 4;
+  const int chunks = (K + 15) >> 4;          // K in 16-k chunks, split over the KS slices
   const int per = (chunks + KS - 1) / KS;
   const int c_begin = ks * per, c_end = min(chunks, c_begin + per);
-  f64x4 acc[NCT];
+  f64x4 acc[RT][NCT];
 #pragma unroll
-  for (int t = 0; t < NCT; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-  const double* xr = X + size_t(row < rows ? row : 0) * K;
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) acc[rt][t] = f64x4{0.0, 0.0, 0.0, 0.0};
   const bool vec = (K & 3) == 0;             // rows 32-byte aligned: vector loads
-  for (int c = c_begin; c < c_end; ++c) {
-    const int k = (c << 4) + (g << 2);
-    double a[4];
-    if (row < rows && vec && k + 3 < K) {
-      const double2 lo = *reinterpret_cast<const double2*>(xr + k);
-      const double2 hi = *reinterpret_cast<const double2*>(xr + k + 2);
-      a[0] = lo.x; a[1] = lo.y; a[2] = hi.x; a[3] = hi.y;
+  auto load4 = [&](const double* p, bool ok, int k, double* v) {
+    if (ok && vec && k + 3 < K) {
+      const double2 lo = *reinterpret_cast<const double2*>(p + k);
+      const double2 hi = *reinterpret_cast<const double2*>(p + k + 2);
+      v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
     } else {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) a[s] = (row < rows && k + s < K) ? xr[k + s] : 0.0;
+      for (int s2 = 0; s2 < 4; ++s2) v[s2] = (ok && k + s2 < K) ? p[k + s2] : 0.0;
+    }
+  };
+  for (int c = c_begin; c < c_end; ++c) {
+    const int k = (c << 4) + (g << 2);
+    double a[RT][4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int row = r0 + rt * 16 + li;     // the A row this lane reads
+      load4(X + size_t(row < rows ? row : 0) * K, row < rows, k, a[rt]);
     }
 #pragma unroll
     for (int t = 0; t < NCT; ++t) {
       const int j = col0 + t * 16 + li;      // the B column (class) this lane reads
-      const double* wr = W + size_t(j < C ? j : 0) * K;
       double w[4];
-      if (j < C && vec && k + 3 < K) {
-        const double2 lo = *reinterpret_cast<const double2*>(wr + k);
-        const double2 hi = *reinterpret_cast<const double2*>(wr + k + 2);
-        w[0] = lo.x; w[1] = lo.y; w[2] = hi.x; w[3] = hi.y;
-      } else {
+      load4(W + size_t(j < C ? j : 0) * K, j < C, k, w);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) w[s] = (j < C && k + s < K) ? wr[k + s] : 0.0;
-      }
+      for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], w[s], acc[t], 0, 0, 0);
+        for (int rt = 0; rt < RT; ++rt)
+          acc[rt][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt][s2], w[s2], acc[rt][t], 0, 0, 0);
     }
   }
   if constexpr (KS > 1) {  // slices 1.. hand their partial logits to slice 0
-    if (ks > 0) {  // (KS > 1 only with CW == 1: one wave per slice)
+    if (ks > 0) {
 #pragma unroll
-      for (int t = 0; t < NCT; ++t)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) red[((size_t(ks - 1) * NCT + t) * 4 + i) * 64 + lane] = acc[t][i];
+        for (int t = 0; t < NCT; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            red[((((size_t(ks - 1) * RT + rt) * NCT + t) * 4) + i) * 64 + lane] = acc[rt][t][i];
     }
     __syncthreads();
     if (ks > 0) return;
 #pragma unroll
     for (int q = 0; q < KS - 1; ++q)
 #pragma unroll
-      for (int t = 0; t < NCT; ++t)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[t][i] += red[((size_t(q) * NCT + t) * 4 + i) * 64 + lane];
+        for (int t = 0; t < NCT; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[rt][t][i] += red[((((size_t(q) * RT + rt) * NCT + t) * 4) + i) * 64 + lane];
   }
-  // ---- epilogue: lane holds rows g + 4i (i = 0..3) of columns col0 + 16t + li
-  double bias[NCT];
+  // ---- epilogue: lane holds rows 16 rt + g + 4i of columns col0 + 16t + li
 #pragma unroll
   for (int t = 0; t < NCT; ++t) {
     const int j = col0 + t * 16 + li;
-    bias[t] = (b && j < C) ? b[j] : 0.0;
+    const double bj = (b && j < C) ? b[j] : 0.0;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[rt][t][i] += bj;
   }
-#pragma unroll
-  for (int t = 0; t < NCT; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[t][i] += bias[t];
   const int out_cols = ACT == kActBinaryLogistic ? 2 : C;
   if constexpr (ACT == kActSoftmax || ACT == kActOvr) {
     // row normaliser over every class: lanes (16 per row group), then waves
-    double m[4], ssum[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      double v = ACT == kActSoftmax ? -__builtin_inf() : 0.0;
-#pragma unroll
-      for (int t = 0; t < NCT; ++t) {
-        const int j = col0 + t * 16 + li;
-        if (ACT == kActSoftmax) v = j < C ? fmax(v, acc[t][i]) : v;
-      }
-      m[i] = v;
-    }
+    double m[RT][4], ssum[RT][4];
     if constexpr (ACT == kActSoftmax) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) m[i] = fmax(m[i], __shfl_xor(m[i], off, 64));
+        for (int i = 0; i < 4; ++i) {
+          double v = -__builtin_inf();
+#pragma unroll
+          for (int t = 0; t < NCT; ++t) v = (col0 + t * 16 + li) < C ? fmax(v, acc[rt][t][i]) : v;
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) v = fmax(v, __shfl_xor(v, off, 64));
+          m[rt][i] = v;
+        }
       if constexpr (CW > 1) {
         if (li == 0)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) rowst[cw][g + 4 * i] = m[i];
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rowst[cw][rt * 16 + g + 4 * i] = m[rt][i];
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          double v = rowst[0][g + 4 * i];
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-          for (int q = 1; q < CW; ++q) v = fmax(v, rowst[q][g + 4 * i]);
-          m[i] = v;
-        }
+          for (int i = 0; i < 4; ++i) {
+            double v = rowst[0][rt * 16 + g + 4 * i];
+#pragma unroll
+            for (int q = 1; q < CW; ++q) v = fmax(v, rowst[q][rt * 16 + g + 4 * i]);
+            m[rt][i] = v;
+          }
         __syncthreads();
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      double v = 0.0;
-#pragma unroll
-      for (int t = 0; t < NCT; ++t) {
-        const int j = col0 + t * 16 + li;
-        const double e = ACT == kActSoftmax ? exp(acc[t][i] - m[i]) : sigmoid(acc[t][i]);
-        acc[t][i] = e;
-        v += j < C ? e : 0.0;
-      }
-      ssum[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) ssum[i] += __shfl_xor(ssum[i], off, 64);
-    if constexpr (CW > 1) {
-      if (li == 0)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rowst[cw][g + 4 * i] = ssum[i];
-      __syncthreads();
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         double v = 0.0;
 #pragma unroll
-        for (int q = 0; q < CW; ++q) v += rowst[q][g + 4 * i];
-        ssum[i] = v;
+        for (int t = 0; t < NCT; ++t) {
+          const int j = col0 + t * 16 + li;
+          const double e = ACT == kActSoftmax ? exp(acc[rt][t][i] - m[rt][i]) : sigmoid(acc[rt][t][i]);
+          acc[rt][t][i] = e;
+          v += j < C ? e : 0.0;
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off, 64);
+        ssum[rt][i] = v;
       }
+    if constexpr (CW > 1) {
+      if (li == 0)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rowst[cw][rt * 16 + g + 4 * i] = ssum[rt][i];
+      __syncthreads();
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double v = 0.0;
+#pragma unroll
+          for (int q = 0; q < CW; ++q) v += rowst[q][rt * 16 + g + 4 * i];
+          ssum[rt][i] = v;
+        }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = r0 + g + 4 * i;
-      if (r >= rows) continue;
-      const double inv = 1.0 / ssum[i];
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int t = 0; t < NCT; ++t) {
-        const int j = col0 + t * 16 + li;
-        if (j < C) out[size_t(r) * out_cols + j] = acc[t][i] * inv;
-      }
-    }
-  } else {
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + rt * 16 + g + 4 * i;
+        if (r >= rows) continue;
+        const double inv = 1.0 / ssum[rt][i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = r0 + g + 4 * i;
-      if (r >= rows) continue;
-#pragma unroll
-      for (int t = 0; t < NCT; ++t) {
-        const int j = col0 + t * 16 + li;
-        if (j >= C) continue;
-        const double z = acc[t][i];
-        if constexpr (ACT == kActIdentity) {
-          out[size_t(r) * out_cols + j] = z;
-        } else if constexpr (ACT == kActBinaryLogistic) {
-          const double p = sigmoid(z);
-          out[size_t(r) * 2] = 1.0 - p;
-          out[size_t(r) * 2 + 1] = p;
-        } else {
-          out[size_t(r) * out_cols + j] = sigmoid(z);
+        for (int t = 0; t < NCT; ++t) {
+          const int j = col0 + t * 16 + li;
+          if (j < C) out[size_t(r) * out_cols + j] = acc[rt][t][i] * inv;
         }
       }
-    }
+  } else {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + rt * 16 + g + 4 * i;
+        if (r >= rows) continue;
+#pragma unroll
+        for (int t = 0; t < NCT; ++t) {
+          const int j = col0 + t * 16 + li;
+          if (j >= C) continue;
+          const double z = acc[rt][t][i];
+          if constexpr (ACT == kActIdentity) {
+            out[size_t(r) * out_cols + j] = z;
+          } else if constexpr (ACT == kActBinaryLogistic) {
+            const double p = sigmoid(z);
+            out[size_t(r) * 2] = 1.0 - p;
+            out[size_t(r) * 2 + 1] = p;
+          } else {
+            out[size_t(r) * out_cols + j] = sigmoid(z);
+          }
+        }
+      }
   }
 }
 
@@ -314,7 +329,7 @@ bool mfma_eligible(int rows, int K, int C) {
   return C <= 1024 && double(rows) * K * C >= double(1 << 20);
 }
 
-template <int ACT, int NCT, int CW>
+template <int ACT, int NCT, int CW, int KS, int RT>
 void launch_mfma_t(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
                    hipStream_t s, hipEvent_t stop);
 
@@ -328,26 +343,29 @@ void launch_maybe_ext(void (*k)(Args...), dim3 grid, dim3 block, size_t lds, hip
   else hipLaunchKernelGGL(k, grid, block, lds, s, args...);
 }
 
-template <int ACT, int NCT, int CW>
+template <int ACT, int NCT, int CW, int KS, int RT>
 void launch_mfma_t(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
                    hipStream_t s, hipEvent_t stop) {
-  launch_maybe_ext(linear_mfma_rows<ACT, NCT, CW>, dim3((rows + kMfmaRows - 1) / kMfmaRows), dim3(kMfmaThreads), 0,
-                   s, stop, X, rows, K, W, b, C, out);
+  constexpr int R = 16 * RT;
+  launch_maybe_ext(linear_mfma_rows<ACT, NCT, CW, KS, RT>, dim3((rows + R - 1) / R), dim3(64 * CW * KS), 0, s, stop,
+                   X, rows, K, W, b, C, out);
 }
 
-// Column tiling by C: up to 4 tiles in one wave (K split over the 4 waves),
-// else the 4 waves split the classes (NCT tiles each, <= 1024 classes).
+// Tiling by C (16-column tiles T): up to 4 tiles in one wave with K split over
+// 4 waves; up to 16 tiles over 4 class-waves; beyond, 8 class-waves with two
+// 16-row tiles each (every W fragment feeds two MFMAs: half the L2 traffic
+// per MFMA), <= 1024 classes.
 template <int ACT>
 void launch_mfma(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
                  hipStream_t s, hipEvent_t stop) {
   const int tiles = (C + 15) / 16;
-  if (tiles <= 1) launch_mfma_t<ACT, 1, 1>(X, rows, K, W, b, C, out, s, stop);
-  else if (tiles <= 2) launch_mfma_t<ACT, 2, 1>(X, rows, K, W, b, C, out, s, stop);
-  else if (tiles <= 4) launch_mfma_t<ACT, 4, 1>(X, rows, K, W, b, C, out, s, stop);
-  else if (tiles <= 8) launch_mfma_t<ACT, 2, 4>(X, rows, K, W, b, C, out, s, stop);
-  else if (tiles <= 16) launch_mfma_t<ACT, 4, 4>(X, rows, K, W, b, C, out, s, stop);
-  else if (tiles <= 32) launch_mfma_t<ACT, 8, 4>(X, rows, K, W, b, C, out, s, stop);
-  else launch_mfma_t<ACT, 16, 4>(X, rows, K, W, b, C, out, s, stop);
+  if (tiles <= 1) launch_mfma_t<ACT, 1, 1, 4, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 2) launch_mfma_t<ACT, 2, 1, 4, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 4) launch_mfma_t<ACT, 4, 1, 4, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 8) launch_mfma_t<ACT, 2, 4, 1, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 16) launch_mfma_t<ACT, 4, 4, 1, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 32) launch_mfma_t<ACT, 4, 8, 1, 2>(X, rows, K, W, b, C, out, s, stop);
+  else launch_mfma_t<ACT, 8, 8, 1, 2>(X, rows, K, W, b, C, out, s, stop);
 }
 
 template <int ACT>

@@ -615,6 +615,103 @@ __global__ __launch_bounds__(kBlock) void perfect_split(const double* __restrict
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Mid-size batches (33..256 rows), single-output models: tree-major tiles.
+// A workgroup is RB rows x TPW trees (thread i -> tree i >> lrb, row i & (RB-1));
+// the chunk's TPW trees -- contiguous in the perfect layout -- are staged into
+// LDS once and every row of the tile descends them there: D dependent LDS
+// reads (~100 cycles each) instead of ceil(D/2) L2 round trips, and each
+// node line leaves L2 once per row tile instead of once per row, which is what
+// bounded the one-row-per-workgroup whole-ensemble kernel at these sizes
+// (xgb1000: 6.7 us at 64 rows, 9.5-10.7 us at 256, profiles/r06d_micro).
+// Rows fold as in perfect_split: in-workgroup sum over the TPW trees, one
+// agent-scope fp64 atomic per row and tree chunk, the last workgroup applies
+// the transform and re-zeroes the accumulators.  Consecutive lanes are
+// consecutive rows of ONE tree, so a wave starts its descent on one node
+// (an LDS broadcast) and the X tile reads hit 32 distinct banks (tile_x).
+constexpr int kTileMaxBlock = 1024;
+
+template <int D>
+__global__ __launch_bounds__(kTileMaxBlock) void perfect_tile(const double* __restrict__ X, int rows, int F,
+                                                              const TreeNode* __restrict__ nodes,
+                                                              const float* __restrict__ leaves, int cmp_le,
+                                                              int n_trees, int RB, int TPW, int stage_x,
+                                                              const float* __restrict__ base_margin, float scale,
+                                                              int transform, double* __restrict__ out, int out_cols,
+                                                              double* __restrict__ acc, int* __restrict__ counter) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NI = (1 << D) - 1;
+  const int nthr = int(blockDim.x);
+  uint2* sN = reinterpret_cast<uint2*>(lds);                                      // [TPW][NI] TreeNode bits
+  float* sL = reinterpret_cast<float*>(sN + size_t(TPW) * NI);                    // [TPW][NI + 1]
+  float* tile = sL + size_t(TPW) * (NI + 1);                                      // [F][RB] when staged
+  __shared__ int s_last;
+  const int lrb = __builtin_ctz(unsigned(RB));
+  const int row0 = int(blockIdx.x) * RB;
+  const int t0 = int(blockIdx.y) * TPW;
+  const int nt = min(TPW, n_trees - t0);
+  {  // the chunk's nodes and leaves: two contiguous runs
+    const uint2* gn = reinterpret_cast<const uint2*>(nodes) + size_t(t0) * NI;
+    for (int i = int(threadIdx.x); i < nt * NI; i += nthr) sN[i] = gn[i];
+    const float* gl = leaves + size_t(t0) * (NI + 1);
+    for (int i = int(threadIdx.x); i < nt * (NI + 1); i += nthr) sL[i] = gl[i];
+  }
+  if (stage_x) {  // RB x F rows -> fp32 feature-major tile (tile_x), zero past the batch
+    const int n = RB * F, nrow = min(RB, rows - row0);
+    for (int i = int(threadIdx.x); i < n; i += nthr) {
+      const int r = i & (RB - 1), f = i >> lrb;
+      tile[i] = r < nrow ? float(X[size_t(row0 + r) * F + f]) : 0.f;
+    }
+  }
+  __syncthreads();
+  const int r_local = int(threadIdx.x) & (RB - 1);
+  const int tl = int(threadIdx.x) >> lrb;
+  const bool row_ok = row0 + r_local < rows;
+  double a = 0.0;
+  if (tl < nt && row_ok) {
+    const uint2* tn = sN + size_t(tl) * NI;
+    const float* xs = tile + r_local;
+    const double* xg = X + size_t(row0 + r_local) * F;
+    int idx = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const uint2 nb = tn[idx];
+      const float thr = __uint_as_float(nb.x);
+      const int32_t feat = int32_t(nb.y);
+      const float x = stage_x ? tile_x(xs, feat, lrb) : float(xg[feat & 0x7fffffff]);
+      idx = 2 * idx + (go_left(x, thr, feat, cmp_le) ? 1 : 2);
+    }
+    a = double(sL[size_t(tl) * (NI + 1) + (idx - NI)]);
+  }
+  for (int off = 32; off >= RB; off >>= 1) a += __shfl_xor(a, off, 64);
+  const int lane = int(threadIdx.x) & 63, wave = int(threadIdx.x) >> 6;
+  __syncthreads();  // every descent is done with the staged trees: their LDS becomes the fold area
+  double* red = reinterpret_cast<double*>(lds);  // [waves][RB]
+  // (RB <= 64: after the fold lanes 0..RB-1 of every wave hold its rows' sums)
+  if (lane < RB) red[wave * RB + lane] = a;
+  __syncthreads();
+  if (int(threadIdx.x) < RB) {
+    const int r = row0 + int(threadIdx.x);
+    if (r < rows) {
+      double m = 0.0;
+      for (int w = 0; w < nthr / 64; ++w) m += red[w * RB + int(threadIdx.x)];
+      __hip_atomic_fetch_add(acc + r, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's adds performed at the coherence point
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             int(gridDim.x * gridDim.y) - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int r = int(threadIdx.x); r < rows; r += nthr) {
+    double m[1] = {__hip_atomic_load(acc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+    __hip_atomic_store(acc + r, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    apply_transform<1>(m, 1, transform, scale, base_margin, out + size_t(r) * out_cols);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int kMaxGroups = 64;
 
 // Block = RB rows x (blockDim / RB) chunk-lanes: the lanes of a row sum a
@@ -882,6 +979,65 @@ void tree_perfect_split(const double* X, int rows, int F, const TreeNode* nodes,
     default: SCA_SPLIT_LAUNCH(10); break;
   }
 #undef SCA_SPLIT_LAUNCH
+}
+
+// Tile geometry for a batch: RB rows (16 / 32 / 64 as the batch grows) x
+// TPW trees per workgroup, TPW the largest power of two (<= 16) whose trees
+// fit 96 KB of LDS.  Returns false when the kernel does not apply.
+bool tree_tile_plan(int rows, int F, int depth, int* RB, int* TPW, int* lds_bytes, int* stage_x) {
+  if (depth < 4 || depth > 10 || rows <= 0) return false;
+  constexpr int kLdsCap = 64 * 1024;  // dynamic LDS without a per-kernel attribute
+  const int tb = tree_bytes(depth);
+  int tpw = 16;
+  while (tpw > 1 && tpw * tb > 56 * 1024) tpw >>= 1;
+  int rb = rows > 96 ? 64 : (rows > 48 ? 32 : 16);
+  if (rb * tpw > kTileMaxBlock) rb = kTileMaxBlock / tpw;
+  const int red = (kTileMaxBlock / 64) * rb * int(sizeof(double));  // the fold reuses the tree area
+  const int trees = std::max(tpw * tb, red);
+  const int xt = ((rb * F + 3) & ~3) * int(sizeof(float));
+  const int sx = trees + xt <= kLdsCap ? 1 : 0;
+  *RB = rb;
+  *TPW = tpw;
+  *stage_x = sx;
+  *lds_bytes = trees + (sx ? xt : 0);
+  return *lds_bytes <= kLdsCap;
+}
+
+int tree_tile_max_rows() {
+  static const int v = [] {
+    const char* e = std::getenv("SCA_TREE_TILE_ROWS");  // 0 = off
+    return e ? std::max(0, std::atoi(e)) : 256;
+  }();
+  return v;
+}
+
+bool tree_perfect_tile(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
+                       int cmp_le, int n_trees, const float* base_margin, float scale, int transform, double* out,
+                       int out_cols, double* acc, int* counter, hipStream_t s, hipEvent_t stop) {
+  int RB, TPW, lds, sx;
+  if (n_trees <= 0 || !tree_tile_plan(rows, F, depth, &RB, &TPW, &lds, &sx)) return false;
+  const dim3 grid((rows + RB - 1) / RB, (n_trees + TPW - 1) / TPW), block(RB * TPW);
+#define SCA_TILE_LAUNCH(DD)                                                                                       \
+  do {                                                                                                            \
+    if (stop)                                                                                                     \
+      hipExtLaunchKernelGGL((perfect_tile<DD>), grid, block, uint32_t(lds), s, nullptr, stop, 0, X, rows, F, nodes, \
+                            leaves, cmp_le, n_trees, RB, TPW, sx, base_margin, scale, transform, out, out_cols, acc,  \
+                            counter);                                                                             \
+    else                                                                                                          \
+      hipLaunchKernelGGL((perfect_tile<DD>), grid, block, uint32_t(lds), s, X, rows, F, nodes, leaves, cmp_le,      \
+                         n_trees, RB, TPW, sx, base_margin, scale, transform, out, out_cols, acc, counter);       \
+  } while (0)
+  switch (depth) {
+    case 4: SCA_TILE_LAUNCH(4); break;
+    case 5: SCA_TILE_LAUNCH(5); break;
+    case 6: SCA_TILE_LAUNCH(6); break;
+    case 7: SCA_TILE_LAUNCH(7); break;
+    case 8: SCA_TILE_LAUNCH(8); break;
+    case 9: SCA_TILE_LAUNCH(9); break;
+    default: SCA_TILE_LAUNCH(10); break;
+  }
+#undef SCA_TILE_LAUNCH
+  return true;
 }
 
 void tree_reduce(const double* partial, int rows, int n_chunks, const int* chunk_group, int groups,

@@ -349,3 +349,25 @@ def test_ts_route_prefers_better_arm(C_):
     # P(Beta(50,2) > Beta(5,5)) and > Beta(2,50) is ~1
     assert frac[1].item() > 0.99
     assert out.min().item() >= 0 and out.max().item() <= 2
+
+
+@pytest.mark.parametrize("trees,depth,F,rows", [(1000, 8, 32, 33), (1000, 8, 32, 100), (1000, 8, 32, 256),
+                                               (300, 10, 16, 64), (97, 5, 700, 50), (64, 4, 8, 200)])
+def test_tree_tile_kernel_vs_cpu(C_, trees, depth, F, rows):
+    """Tree-major tiles for 33..256-row batches: trees
+    staged in LDS per row tile, atomic row fold; the serving unit routes these
+    batch sizes to it.  Against the CPU ensemble, NaN default directions
+    included, and twice in a row (the fold re-zeroes its accumulators)."""
+    from seldon_core_amd.models import synthetic_xgboost, to_row_model
+
+    ens = synthetic_xgboost(trees, depth, F, seed=rows + depth)
+    unit = C_.BatchedUnit(to_row_model(ens), 0, max_batch=4096)
+    try:
+        for rep in range(2):
+            X = np.random.default_rng(rows + rep).standard_normal((rows, F))
+            X[::5, 0] = np.nan
+            got = np.asarray(unit.run(X))
+            ref = ens.predict(X)
+            np.testing.assert_allclose(got.reshape(ref.shape), ref, rtol=2e-5, atol=2e-5)
+    finally:
+        unit.stop()

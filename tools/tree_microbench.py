@@ -93,8 +93,31 @@ def main():
         if a.small:  # whole ensemble split over `parts` workgroups per row tile (atomic fold)
             for parts in (4, 8, 16, 32):
                 variants.append((f"split{parts}", parts, 0, "split"))
+            variants.append(("tile", 0, 0, "tile"))
         for v in variants:
             name, chunk, lds, fused = v[:4]
+            if fused == "tile":
+                out = torch.empty(rows, dtype=torch.float64, device=dev)
+                acc = torch.zeros(rows, dtype=torch.float64, device=dev)
+                cnt = torch.zeros(16, dtype=torch.int32, device=dev)
+
+                def launch():
+                    K.tree_perfect_tile(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0, T, 0, 1.0,
+                                        0, out.data_ptr(), 1, acc.data_ptr(), cnt.data_ptr(), s)
+
+                for _ in range(20):
+                    launch()
+                torch.cuda.synchronize()
+                err = float((out - out_ref).abs().max()) if out_ref is not None else None
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    launch()
+                e1.record()
+                torch.cuda.synchronize()
+                row[name] = {"us": round(e0.elapsed_time(e1) * 1000 / a.iters, 2), "max_err": err,
+                             "acc_rezeroed": float(acc.abs().max()) == 0.0 and int(cnt[0]) == 0}
+                continue
             if fused == "split":
                 out = torch.empty(rows, dtype=torch.float64, device=dev)
                 acc = torch.zeros(rows, dtype=torch.float64, device=dev)
