@@ -144,12 +144,14 @@ void TreeEnsembleModel::to_device(int device) {
   }
 }
 
-// Workspace: [fused-reduce counter | split-kernel counter at byte 128 |
-// split-kernel row accumulators from byte 256, up to kSplitMaxRows]
+// Workspace: [fused-reduce counter | tile-kernel counter at byte 128 |
+// split / tile row accumulators from byte 256, up to kSplitMaxRows |
+// split-kernel per-row-tile arrival counters from byte 4096 (1024)]
 // [chunk partial slab].  The header starts zeroed (DeviceBuffer::alloc) and
 // every kernel that uses a counter or accumulator re-zeroes it.
-static constexpr size_t kTreeWsHeader = 4096;
-static constexpr int kSplitMaxRows = int((kTreeWsHeader - 256) / sizeof(double));
+static constexpr size_t kTreeWsHeader = 8192;
+static constexpr size_t kSplitCounters = 4096;
+static constexpr int kSplitMaxRows = int((kSplitCounters - 256) / sizeof(double));
 
 size_t TreeEnsembleModel::workspace_bytes(int max_rows, int) const {
   // Largest slab any batch size up to max_rows plans for (chunks shrink as
@@ -244,7 +246,7 @@ bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double*
     kern::tree_perfect_split(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
                              spec_.depth, spec_.cmp_le, spec_.n_trees, kern::tree_split_parts(), d_base_.as<float>(),
                              spec_.scale, spec_.transform, out, spec_.out_cols, reinterpret_cast<double*>(hdr + 256),
-                             reinterpret_cast<int*>(hdr + 128), s, done);
+                             reinterpret_cast<int*>(hdr + kSplitCounters), s, done);
     return done != nullptr;
   }
   if (uses_tile(rows)) {

@@ -144,7 +144,7 @@ int tree_split_max_rows();
 bool tree_perfect_tile(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                        int cmp_le, int n_trees, const float* base_margin, float scale, int transform, double* out,
                        int out_cols, double* acc, int* counter, hipStream_t stream, hipEvent_t stop = nullptr);
-int tree_tile_max_rows();  // SCA_TREE_TILE_ROWS (default 256; 0 = off)
+int tree_tile_max_rows();  // SCA_TREE_TILE_ROWS (default 0 = off)
 void tree_perfect_split(const double* X, int rows, int F, const TreeNode* nodes, const float* leaves, int depth,
                         int cmp_le, int n_trees, int parts, const float* base_margin, float scale, int transform,
                         double* out, int out_cols, double* acc, int* counter, hipStream_t s,

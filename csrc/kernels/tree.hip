@@ -602,17 +602,20 @@ __global__ __launch_bounds__(kBlock) void perfect_split(const double* __restrict
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's adds performed at the coherence point
   __syncthreads();
+  // one arrival counter per row tile: the `parts` workgroups of a tile
+  // serialise on it, not every workgroup of the grid on one word (that single
+  // counter grew the kernel 5.5 -> 8.0 us from 16 to 64 rows, r06e)
   if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             int(gridDim.x * gridDim.y) - 1;
+    s_last = __hip_atomic_fetch_add(counter + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == parts - 1;
   __syncthreads();
   if (!s_last) return;
-  for (int r = int(threadIdx.x); r < rows; r += kBlock) {
+  if (int(threadIdx.x) < RB && row0 + int(threadIdx.x) < rows) {
+    const int r = row0 + int(threadIdx.x);
     double m[1] = {__hip_atomic_load(acc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
     __hip_atomic_store(acc + r, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     apply_transform<1>(m, 1, transform, scale, base_margin, out + size_t(r) * out_cols);
   }
-  if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(counter + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Mid-size batches (33..256 rows), single-output models: tree-major tiles.
@@ -1003,10 +1006,15 @@ bool tree_tile_plan(int rows, int F, int depth, int* RB, int* TPW, int* lds_byte
   return *lds_bytes <= kLdsCap;
 }
 
+// Off by default (SCA_TREE_TILE_ROWS=N opts in for batches of 33..N rows):
+// at the xgb1000 shape the tile kernel only beats the whole-ensemble kernel
+// from ~192 rows (8.3 vs 8.8 us), loses below 128 (9.6 vs 6.3 us at 33 rows,
+// the LDS staging of 16 trees per workgroup is not amortised), and serving
+// batches are mostly small: 9.36 us mean vs 7.61 (profiles/r06e_tree_tile).
 int tree_tile_max_rows() {
   static const int v = [] {
-    const char* e = std::getenv("SCA_TREE_TILE_ROWS");  // 0 = off
-    return e ? std::max(0, std::atoi(e)) : 256;
+    const char* e = std::getenv("SCA_TREE_TILE_ROWS");
+    return e ? std::max(0, std::atoi(e)) : 0;
   }();
   return v;
 }

@@ -5,7 +5,7 @@ O=gpurun_out/${R06_OUT:-r06d}
 mkdir -p $O
 timeout -k 10 120 ./tools/micro/graph_cost > $O/graph_cost.jsonl 2>&1 || { cat $O/graph_cost.jsonl; exit 1; }
 cat $O/graph_cost.jsonl
-timeout -k 10 400 python3 tools/tree_microbench.py --small --rows 8,16,24,32,48,64,96,128,192,256 --iters 200 > $O/tree_small.jsonl 2>&1 || { tail -20 $O/tree_small.jsonl; exit 1; }
+timeout -k 10 400 python3 tools/tree_microbench.py --small --rows 16,32,48,64,96,128,192 --iters 200 > $O/tree_small.jsonl 2>&1 || { tail -20 $O/tree_small.jsonl; exit 1; }
 python3 - <<'PY'
 import json
 for ln in open("gpurun_out/r06d/tree_small.jsonl"):

@@ -116,12 +116,12 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 row[name] = {"us": round(e0.elapsed_time(e1) * 1000 / a.iters, 2), "max_err": err,
-                             "acc_rezeroed": float(acc.abs().max()) == 0.0 and int(cnt[0]) == 0}
+                             "acc_rezeroed": float(acc.abs().max()) == 0.0 and int(cnt.abs().max()) == 0}
                 continue
             if fused == "split":
                 out = torch.empty(rows, dtype=torch.float64, device=dev)
                 acc = torch.zeros(rows, dtype=torch.float64, device=dev)
-                cnt = torch.zeros(16, dtype=torch.int32, device=dev)
+                cnt = torch.zeros(1024, dtype=torch.int32, device=dev)
 
                 def launch():
                     K.tree_perfect_split(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0, T, chunk,
@@ -140,7 +140,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 row[name] = {"us": round(e0.elapsed_time(e1) * 1000 / a.iters, 2), "parts": chunk, "max_err": err,
-                             "acc_rezeroed": float(acc.abs().max()) == 0.0 and int(cnt[0]) == 0}
+                             "acc_rezeroed": float(acc.abs().max()) == 0.0 and int(cnt.abs().max()) == 0}
                 continue
             rb_v = v[4] if len(v) > 4 else rb
             if fused == "whole":
