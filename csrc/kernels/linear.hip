@@ -162,25 +162,37 @@ __global__ __launch_bounds__(64 * CW * KS) void linear_mfma_rows(const double* _
       for (int s2 = 0; s2 < 4; ++s2) v[s2] = (ok && k + s2 < K) ? p[k + s2] : 0.0;
     }
   };
-  for (int c = c_begin; c < c_end; ++c) {
-    const int k = (c << 4) + (g << 2);
-    double a[RT][4];
+  // Chunks go in groups of G: the group's loads are issued together, then its
+  // MFMAs -- narrow tiles (the memory-bound shapes) keep 4 chunks' loads in
+  // flight per wave instead of one 2 KB round trip at a time.
+  constexpr int G = NCT * RT <= 2 ? 4 : 1;
+  for (int c0 = c_begin; c0 < c_end; c0 += G) {
+    double a[G][RT][4], w[G][NCT][4];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int row = r0 + rt * 16 + li;     // the A row this lane reads
-      load4(X + size_t(row < rows ? row : 0) * K, row < rows, k, a[rt]);
+    for (int u = 0; u < G; ++u) {
+      const int c = c0 + u;
+      const bool live = c < c_end;
+      const int k = (c << 4) + (g << 2);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int row = r0 + rt * 16 + li;   // the A row this lane reads
+        load4(X + size_t(row < rows ? row : 0) * K, live && row < rows, k, a[u][rt]);
+      }
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const int j = col0 + t * 16 + li;    // the B column (class) this lane reads
+        load4(W + size_t(j < C ? j : 0) * K, live && j < C, k, w[u][t]);
+      }
     }
 #pragma unroll
-    for (int t = 0; t < NCT; ++t) {
-      const int j = col0 + t * 16 + li;      // the B column (class) this lane reads
-      double w[4];
-      load4(W + size_t(j < C ? j : 0) * K, j < C, k, w);
+    for (int u = 0; u < G; ++u)
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2)
+      for (int t = 0; t < NCT; ++t)
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-          acc[rt][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rt][s2], w[s2], acc[rt][t], 0, 0, 0);
-    }
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+            acc[rt][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt][s2], w[u][t][s2], acc[rt][t], 0, 0, 0);
   }
   if constexpr (KS > 1) {  // slices 1.. hand their partial logits to slice 0
     if (ks > 0) {

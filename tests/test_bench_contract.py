@@ -64,7 +64,9 @@ def test_bench_two_ranks_torchrun_cpu():
     rc = v["mab_ranks"]
     assert rc["data_plane"] == "shm" and rc["fabric_world"] == 2
     assert rc["unit_kinds"]["m1"] == "gpu:mesh_program"
-    assert rc["mesh_programs"] == [{"root": "m1", "stages": "s0=node:m1@rank1(in)", "messages_per_batch": 2}]
+    assert rc["mesh_programs"] == [{"root": "m1", "stages": "s0=node:m1@rank1(in)", "messages_per_batch": 2,
+                                    "edges": [{"from": "m1@1", "to_rank": 0, "transport": "shm"}]}]
+    assert rc["peer"]["failed_edges"] == [] and rc["peer"]["devices"] == [-1, -1], rc["peer"]
     assert rc["worker_ranks"]["1"]["batches"] > 0 and rc["worker_ranks"]["1"]["error"] == ""
     # the bandit learned the rewarded remote branch: most batches crossed the fabric
     b = rc["rank0_batches_per_unit"]

@@ -26,3 +26,8 @@ for H in 1 0; do
   SCA_HDP_FLUSH=$H timeout -k 10 300 python3 bench.py --model xgb1000 --extras none > $O/xgb_hdp$H.log 2>&1 || { tail -30 $O/xgb_hdp$H.log; exit 1; }
   grep '^{' $O/xgb_hdp$H.log | tail -1 | cut -c1-300
 done
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu \
+  tests/test_kernels_gpu.py -k "linear" > $O/pytest_linear.log 2>&1 || { tail -60 $O/pytest_linear.log; exit 1; }
+tail -1 $O/pytest_linear.log
+timeout -k 10 240 python3 tools/r06/linear_bench.py > $O/linear_bench.log 2>&1 || { tail -30 $O/linear_bench.log; exit 1; }
+grep '"mfma"' $O/linear_bench.log
