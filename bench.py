@@ -660,6 +660,7 @@ def variant_child(args) -> None:
                "p50_ms": lg["p50_ms"], "p99_ms": lg["p99_ms"], "window_s": round(lg["seconds"], 3),
                "step_ms": bk.step_spread(lg["step_ms"]), "sampled_replies_checked": lg.get("checked", 0),
                "self_check": check, "placement": pl, "peer_access": bk.peer_access(used),
+               "device_graphs": bk.device_graphs(dep),
                "batches_per_device": {k: v["batches"] for k, v in st["per_device"].items()},
                "rows_per_device": {k: v["rows"] for k, v in st["per_device"].items()},
                "server_threads": server_threads, "client_threads": client_threads, "cpu_budget": cpus}

@@ -256,6 +256,10 @@ PYBIND11_MODULE(_C, m) {
     d["peer_direct"] = g->peer_direct();
     d["stages"] = int(g->stages().size());
     d["fused"] = g->fused();  // one linear_graph kernel per batch
+    py::dict pc;
+    for (const auto& c : g->peer_canary_results())
+      pc[py::str(std::to_string(c.producer) + "->" + std::to_string(c.consumer))] = c.ok;
+    d["peer_canary"] = pc;  // producer -> consumer: a consumer kernel read the producer's HBM correctly
     return d;
   });
   auto to_layers = [](py::list ls) {

@@ -134,7 +134,55 @@ void GraphModel::to_device(int device) {
       else if (e != hipSuccess) { (void)hipGetLastError(); peer_direct_ = false; }
     }
   if (split_ == 1) peer_direct_ = false;
+  // Verify every cross-GPU edge before serving: a kernel
+  // on the consumer GPU reads a pattern out of the producer's HBM through the
+  // peer pointer -- exactly what a stage kernel does -- and the result is
+  // compared on the host.  Any failure drops the graph to staged copies.
+  // Split mode 2 (lanes on one GPU reading each other's buffers) checks the
+  // device against itself.  SCA_GRAPH_PEER_FAULT=1 injects a failure.
+  peer_canary_.clear();
+  if (peer_direct_) {
+    std::vector<std::pair<int, int>> pairs;
+    for (int a : devs)
+      for (int b : devs)
+        if (a != b) pairs.push_back({a, b});
+    if (split_ == 2 && devs.size() == 1) pairs.push_back({device, device});
+    for (auto& pr : pairs) {
+      const bool ok = peer_canary(pr.first, pr.second);
+      peer_canary_.push_back({pr.first, pr.second, ok});
+      if (!ok) peer_direct_ = false;
+    }
+  }
   build_fused();
+}
+
+bool GraphModel::peer_canary(int consumer, int producer) {
+  if (const char* e = std::getenv("SCA_GRAPH_PEER_FAULT"))
+    if (std::atoi(e) != 0) return false;
+  constexpr int n = 256;
+  std::vector<double> pat(n), back(n, 0.0);
+  for (int i = 0; i < n; ++i) pat[size_t(i)] = 1e3 * (producer + 1) + 7.0 * (consumer + 1) + i + 0.125;
+  try {
+    DeviceBuffer src(n * sizeof(double), producer);
+    src.upload(pat.data(), n * sizeof(double));
+    DeviceBuffer dst(n * sizeof(double), consumer), tab(sizeof(double*), consumer);
+    const double* p = src.as<double>();
+    tab.upload(&p, sizeof p);
+    DeviceGuard g(consumer);
+    kern::combine_mean_f64(tab.as<const double* const>(), 1, n, dst.as<double>(), nullptr);  // mean of one = copy
+    if (hipDeviceSynchronize() != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (hipMemcpy(back.data(), dst.get(), n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+  } catch (const std::exception&) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return back == pat;
 }
 
 void GraphModel::build_fused() {

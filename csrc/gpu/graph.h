@@ -81,6 +81,12 @@ class GraphModel : public RowModel {
   bool launch_signal(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
                      hipEvent_t done) override;
   bool fused() const { return fused_; }
+  struct PeerCheck {
+    int consumer, producer;
+    bool ok;
+  };
+  // start-up canaries of the cross-GPU edges (to_device)
+  const std::vector<PeerCheck>& peer_canary_results() const { return peer_canary_; }
 
   std::shared_ptr<RowModel> clone() const override { return clone_on(-2); }
   // Copy with every stage placed on `device` (-2: keep stage placement): one
@@ -116,6 +122,8 @@ class GraphModel : public RowModel {
   int root_device_ = -1;
   bool peer_direct_ = true;
   int split_ = 0;
+  bool peer_canary(int consumer, int producer);
+  std::vector<PeerCheck> peer_canary_;
   // one-kernel form (kern::linear_graph_f64), built at to_device()
   void build_fused();
   bool fused_ = false;

@@ -576,6 +576,20 @@ def placement(dep) -> Dict[str, Any]:
     return out
 
 
+def device_graphs(dep) -> Dict[str, Any]:
+    """Per fused device graph: devices, peer-direct or staged edges, the
+    start-up peer canaries and whether it runs as one fused kernel."""
+    out: Dict[str, Any] = {}
+    C = dep.C
+    for name, unit in getattr(dep, "batched", {}).items():
+        try:
+            info = dict(C.graph_info(unit.model))
+        except Exception:  # noqa: BLE001  not a graph model
+            continue
+        out[name] = {k: info[k] for k in ("devices", "peer_direct", "peer_canary", "fused", "stages") if k in info}
+    return out
+
+
 def peer_access(devs) -> Dict[str, bool]:
     """hipDeviceCanAccessPeer between every ordered pair of distinct GPUs used."""
     from .._native import gpu_count, native

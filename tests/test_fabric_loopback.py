@@ -220,9 +220,9 @@ GRAPHS = {
 }
 
 
-@pytest.mark.parametrize("mode", ["true", "peer"])
+@pytest.mark.parametrize("mode", ["true", "peer", "peer-fault"])
 @pytest.mark.parametrize("name", sorted(GRAPHS))
-def test_split_device_graph_matches_cpu_under_concurrency(name, mode):
+def test_split_device_graph_matches_cpu_under_concurrency(name, mode, monkeypatch):
     """Split lanes on one GPU, 8 callers, 4 slots, buffer growth: "true" runs
     the staged-copy branch (GPUs without peer access), "peer" the direct
     cross-lane reads and the last lane's direct write into the caller's
@@ -231,14 +231,19 @@ def test_split_device_graph_matches_cpu_under_concurrency(name, mode):
     rng = np.random.default_rng(11)
     comps = {"tin": _lin(C, rng, 4, 4), "m1": _lin(C, rng, 3, 4, 1), "m2": _lin(C, rng, 3, 4, 1),
              "m3": _lin(C, rng, 3, 4, 1), "tout": _lin(C, rng, 2, 3)}
-    spec = _spec(GRAPHS[name], {"seldon.io/device-graph-split": mode})
+    if mode == "peer-fault":  # the start-up canary fails: the graph must fall back to staged copies
+        monkeypatch.setenv("SCA_GRAPH_PEER_FAULT", "1")
+    spec = _spec(GRAPHS[name], {"seldon.io/device-graph-split": mode.split("-")[0]})
     gpu = sca.Deployment(spec, components=comps, device=0, fuse=True, batcher={"slots": 4, "max_batch": 2048})
     cpu = sca.Deployment(spec, components=comps, device=-1, fuse=True)
     root = GRAPHS[name]["name"]
     try:
         info = C.graph_info(gpu.batched[root].model)
         assert info["split"] and info["stages"] >= 3, info
-        assert info["peer_direct"] == (mode == "peer") and info["split_mode"] == (2 if mode == "peer" else 1), info
+        assert info["peer_direct"] == (mode == "peer"), info
+        assert info["split_mode"] == (1 if mode == "true" else 2), info
+        # the canary runs for peer-direct graphs: the device against itself here
+        assert info["peer_canary"] == ({} if mode == "true" else {"0->0": mode == "peer"}), info
         errors, worst = [], [0.0]
         lock = threading.Lock()
 
