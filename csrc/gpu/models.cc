@@ -244,7 +244,7 @@ bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double*
       spec_.depth >= 4 && spec_.depth <= 10) {
     char* hdr = static_cast<char*>(ws);
     kern::tree_perfect_split(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
-                             spec_.depth, spec_.cmp_le, spec_.n_trees, kern::tree_split_parts(), d_base_.as<float>(),
+                             spec_.depth, spec_.cmp_le, spec_.n_trees, kern::tree_split_parts_for(rows), d_base_.as<float>(),
                              spec_.scale, spec_.transform, out, spec_.out_cols, reinterpret_cast<double*>(hdr + 256),
                              reinterpret_cast<int*>(hdr + kSplitCounters), s, done);
     return done != nullptr;

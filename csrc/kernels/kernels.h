@@ -137,6 +137,7 @@ int tree_whole_rows_per_block(int n_trees, int rows);
 // SCA_TREE_SPLIT / SCA_TREE_SPLIT_ROWS set the serving default (8 parts for
 // batches of up to 32 rows); depths 4..10.
 int tree_split_parts();
+int tree_split_parts_for(int rows);  // workgroups per row tile for a batch (0 = no split)
 int tree_split_max_rows();
 // Tree-major tiles for mid-size batches (single output, depth 4..10): one
 // launch, trees staged in LDS per row tile, atomic row fold (acc / counter as

@@ -934,6 +934,10 @@ void tree_perfect_whole(const double* X, int rows, int F, const TreeNode* nodes,
 // microbench, 7.17 -> 5.96 us serving with BAR-staged rows, 8.04 -> 7.04 us
 // with host rows; serving batches of 17-32 rows 7.3 -> 5.8 us; in the
 // microbench the single workgroup per row tile wins again at 128 rows.
+// Round 6 (profiles/r06f_ab, one arrival counter per row tile): 16 parts
+// win up to 16 rows (5.27 vs 5.58 us), 8 parts tie the whole kernel at 48-64
+// rows and beat it at 96 (7.17 vs 7.37 us): defaults 16 / 8 parts, split up
+// to 96 rows.
 int tree_split_parts() {
   static const int v = [] {
     const char* e = std::getenv("SCA_TREE_SPLIT");
@@ -943,10 +947,17 @@ int tree_split_parts() {
   return v;
 }
 
+int tree_split_parts_for(int rows) {
+  const int p = tree_split_parts();
+  if (p <= 0) return 0;
+  if (std::getenv("SCA_TREE_SPLIT")) return p;  // an explicit setting holds at every batch size
+  return rows <= 16 ? 16 : p;
+}
+
 int tree_split_max_rows() {
   static const int v = [] {
     const char* e = std::getenv("SCA_TREE_SPLIT_ROWS");
-    return e ? std::max(0, std::atoi(e)) : 32;
+    return e ? std::max(0, std::atoi(e)) : 96;
   }();
   return v;
 }
