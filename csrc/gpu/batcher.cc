@@ -197,7 +197,7 @@ void BatchedUnit::drain_shards(std::deque<Item>& into) {
 constexpr size_t kDirectH2DBytes = size_t(1) << 20;
 
 void BatchedUnit::ensure_capacity(Slot& s, int rows, int cols) {
-  const int oc = model_->out_cols(cols);
+  const int oc = std::max(model_->out_cols(cols), model_->raw_out_cols(rows, cols));
   const size_t need_in = size_t(rows) * cols * sizeof(double);
   const size_t need_out = size_t(rows) * oc * sizeof(double);
   // Geometric growth: pinned/device allocations are slow, batches vary.
@@ -419,8 +419,15 @@ bool BatchedUnit::launch(Slot* s) {
   std::string launch_error;
   try {
     ensure_capacity(*s, rows, cols);
+    s->raw_cols = model_->raw_out_cols(rows, cols);
+    struct RawScope {  // this model (not a graph's stage models) may write raw output
+      const RowModel* prev;
+      explicit RawScope(const RowModel* m) : prev(g_raw_output_model) { g_raw_output_model = m; }
+      ~RawScope() { g_raw_output_model = prev; }
+    } raw_scope(model_.get());
+    const int dev_cols = s->raw_cols > 0 ? s->raw_cols : s->out_cols;  // what the kernel writes per row
     double* hin = s->h_in.host<double>();
-    const size_t bin = size_t(rows) * cols * sizeof(double), bout = size_t(rows) * s->out_cols * sizeof(double);
+    const size_t bin = size_t(rows) * cols * sizeof(double), bout = size_t(rows) * dev_cols * sizeof(double);
     // A lone large request is DMA'd straight from its message's memory: no
     // host copy into the pinned slot first (8192 x 784 fp64: 51 MB).  Not a
     // run_ptr caller's buffer: the watchdog must be able to answer that
@@ -634,6 +641,11 @@ void BatchedUnit::complete(Slot* s, hipError_t st) {
     // answered here, before the slot is reused.
     const int oc = s->out_cols;
     const double* out = cpu_ ? s->cpu_out.data() : s->h_out.host<double>();
+    if (!cpu_ && s->raw_cols > 0) {  // fold the kernel's raw values (RowModel::finish_host)
+      s->fin.resize(size_t(s->rows) * size_t(oc));
+      model_->finish_host(out, s->rows, s->raw_cols, s->fin.data());
+      out = s->fin.data();
+    }
     Handoff h = driver_->take_free_handoff();  // reuse a drained hand-off's buffers
     h.unit = this;
     h.out_cols = oc;

@@ -151,6 +151,8 @@ class BatchedUnit : public Unit {
     PinnedBuffer h_in, h_out, h_seg;
     BarBuffer v_in;  // SCA_BATCH_INPUT=bar: zero-copy batch rows in HBM, written by the CPU
     std::vector<double> cpu_out;  // device -1 (cpu_batching)
+    std::vector<double> fin;      // host-finished outputs (RowModel::finish_host)
+    int raw_cols = 0;             // > 0: the kernel wrote raw_cols values per row into h_out
     std::vector<double> cpu_in;   // device -1, asynchronous models: the batch's rows back to back
     CpuCallPtr call;              // device -1: the batch's outstanding start_cpu() call
     DeviceBuffer d_in, d_out, ws;

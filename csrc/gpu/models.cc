@@ -68,6 +68,8 @@ void LinearModel::run_cpu(const double* X, int rows, int, double* out) const {
   }
 }
 
+thread_local const RowModel* g_raw_output_model = nullptr;
+
 // ------------------------------------------------------------ tree ensemble
 static const int kPlanSizes[] = {4, 8, 16, 32, 64, 128, 256, 512};
 
@@ -199,10 +201,51 @@ bool TreeEnsembleModel::uses_whole(int rows) const {
   return spec_.depth > 0 && spec_.groups == 1 && rows <= whole_max_rows_;
 }
 
+bool TreeEnsembleModel::uses_split(int rows) const {
+  return uses_whole(rows) && kern::tree_split_parts() > 0 &&
+         rows <= std::min(kSplitMaxRows, kern::tree_split_max_rows()) && spec_.depth >= 4 && spec_.depth <= 10;
+}
+
+static bool tree_host_fold() {
+  static const bool v = [] {
+    const char* e = std::getenv("SCA_TREE_HOST_FOLD");
+    return !e || std::atoi(e) != 0;
+  }();
+  return v;
+}
+
+int TreeEnsembleModel::raw_out_cols(int rows, int) const {
+  return tree_host_fold() && uses_split(rows) ? kern::tree_split_parts_for(rows) : 0;
+}
+
+// The split kernel's per-part row sums -> the objective transform, exactly as
+// the kernels' apply_transform (and run_cpu) state it; parts are added in
+// part order, so the result does not depend on which workgroup finished first.
+void TreeEnsembleModel::finish_host(const double* raw, int rows, int parts, double* out) const {
+  const double base = spec_.base_margin.empty() ? 0.0 : double(spec_.base_margin[0]);
+  for (int r = 0; r < rows; ++r) {
+    double m = 0.0;
+    const double* p = raw + size_t(r) * size_t(parts);
+    for (int i = 0; i < parts; ++i) m += p[i];
+    m = m * double(spec_.scale) + base;
+    double* o = out + size_t(r) * spec_.out_cols;
+    switch (spec_.transform) {
+      case kern::kTreeSigmoid: o[0] = 1.0 / (1.0 + std::exp(-m)); break;
+      case kern::kTreeBinaryProba: {
+        const double pr = 1.0 / (1.0 + std::exp(-m));
+        o[0] = 1.0 - pr;
+        o[1] = pr;
+        break;
+      }
+      case kern::kTreeIsolation: o[0] = -std::exp2(-(m - base)) - base; break;
+      default: o[0] = m;  // identity / mean (single group)
+    }
+  }
+}
+
 bool TreeEnsembleModel::uses_tile(int rows) const {
   return uses_whole(rows) && spec_.depth >= 4 && spec_.depth <= 10 && rows <= kSplitMaxRows &&
-         rows <= kern::tree_tile_max_rows() &&
-         !(kern::tree_split_parts() > 0 && rows <= std::min(kSplitMaxRows, kern::tree_split_max_rows()));
+         rows <= kern::tree_tile_max_rows() && !uses_split(rows);
 }
 
 bool TreeEnsembleModel::zero_copy_input_for(int rows, int cols) const {
@@ -240,13 +283,15 @@ bool TreeEnsembleModel::uses_fused(int rows) const {
 bool TreeEnsembleModel::launch_impl(const double* X, int rows, int cols, double* out, void* ws, hipStream_t s,
                                     hipEvent_t done) {
   (void)cols;
-  if (uses_whole(rows) && kern::tree_split_parts() > 0 && rows <= std::min(kSplitMaxRows, kern::tree_split_max_rows()) &&
-      spec_.depth >= 4 && spec_.depth <= 10) {
+  if (uses_split(rows)) {
     char* hdr = static_cast<char*>(ws);
+    // out holds [rows][parts] part sums (finish_host) when the batcher launches this model itself
+    const bool host = raw_output_allowed() && raw_out_cols(rows, cols) > 0;
     kern::tree_perfect_split(X, rows, spec_.n_features, d_nodes_.as<kern::TreeNode>(), d_leaves_.as<float>(),
-                             spec_.depth, spec_.cmp_le, spec_.n_trees, kern::tree_split_parts_for(rows), d_base_.as<float>(),
-                             spec_.scale, spec_.transform, out, spec_.out_cols, reinterpret_cast<double*>(hdr + 256),
-                             reinterpret_cast<int*>(hdr + kSplitCounters), s, done);
+                             spec_.depth, spec_.cmp_le, spec_.n_trees, kern::tree_split_parts_for(rows),
+                             d_base_.as<float>(), spec_.scale, spec_.transform, out, spec_.out_cols,
+                             host ? nullptr : reinterpret_cast<double*>(hdr + 256),
+                             host ? nullptr : reinterpret_cast<int*>(hdr + kSplitCounters), s, done);
     return done != nullptr;
   }
   if (uses_tile(rows)) {

@@ -31,6 +31,11 @@ struct CpuCall {
 };
 using CpuCallPtr = std::shared_ptr<CpuCall>;
 
+class RowModel;
+// The row model a BatchedUnit is launching directly, set by the batcher around
+// its launch call: only that model may write host-finished raw output.
+extern thread_local const RowModel* g_raw_output_model;
+
 class RowModel {
  public:
   virtual ~RowModel() = default;
@@ -68,6 +73,20 @@ class RowModel {
   virtual bool bar_input_for(int rows, int cols) const { (void)rows; (void)cols; return false; }
   // Segment-aware models compute per request (not per row): the batcher passes
   // the request boundaries (nseg + 1 row offsets, device-visible).
+  // Host-finished outputs (only when the batcher launches this model itself,
+  // raw_output_allowed(); a model launched as a stage of a device graph or a
+  // mesh program always writes final output): for a batch of `rows` the kernel writes
+  // raw_out_cols(rows, cols) values per row (e.g. one partial sum per tree
+  // part) and finish_host() folds them into the out_cols() values of the
+  // response on the pump thread once the batch completed -- for folds whose
+  // cross-workgroup form (atomics + an arrival counter + a last workgroup)
+  // costs more device time than the host spends adding a few doubles per
+  // row.  0 = the kernel writes the final output.
+  virtual int raw_out_cols(int rows, int cols) const { (void)rows; (void)cols; return 0; }
+  bool raw_output_allowed() const { return g_raw_output_model == this; }
+  virtual void finish_host(const double* raw, int rows, int raw_cols, double* out) const {
+    (void)raw; (void)rows; (void)raw_cols; (void)out;
+  }
   virtual bool segmented() const { return false; }
   // Stateful segmented models: the position in the state's application order
   // of the first row of the last launch_segments() / run_cpu() call made on
@@ -191,6 +210,12 @@ class TreeEnsembleModel : public RowModel {
   // Host reads = rows x cols x 8 B x chunks: zero-copy while that stays small.
   bool zero_copy_input_for(int rows, int cols) const override;
   bool bar_input_for(int rows, int cols) const override { (void)cols; return uses_tile(rows); }
+  // split batches fold their per-part sums on the host (SCA_TREE_HOST_FOLD=0:
+  // in-kernel atomic fold instead): 3.8-4.5 vs 5.0-7.2 us per batch at 4-96
+  // rows (profiles/r06i_host_fold)
+  int raw_out_cols(int rows, int cols) const override;
+  void finish_host(const double* raw, int rows, int raw_cols, double* out) const override;
+  bool uses_split(int rows) const;
   // mid-size batches of single-output perfect ensembles: kern::tree_perfect_tile
   bool uses_tile(int rows) const;
   std::shared_ptr<RowModel> clone() const override {

@@ -597,9 +597,14 @@ __global__ __launch_bounds__(kBlock) void perfect_split(const double* __restrict
       double m = 0.0;
 #pragma unroll
       for (int w = 0; w < kBlock / 64; ++w) m += red[w * RB + threadIdx.x];
+      if (!acc) {  // host fold: part sums out[r][part]; the host adds them in part order and transforms
+        out[size_t(r) * parts + part] = m;
+        return;
+      }
       __hip_atomic_fetch_add(acc + r, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if (!acc) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's adds performed at the coherence point
   __syncthreads();
   // one arrival counter per row tile: the `parts` workgroups of a tile

@@ -206,3 +206,32 @@ def test_linear_graph_fusion_rules_cpu():
     C = sca.native()
     g = C.graph_model(_linear_graph_stages(C, np.random.default_rng(1)), 4)
     assert C.graph_info(g)["fused"] is False  # never placed on a GPU here
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [5, 40, 300])
+def test_tree_stage_in_device_graph_writes_final_output(rows):
+    """A tree ensemble launched by its own batcher folds its split-kernel part
+    sums on the host (RowModel::finish_host); as a device-graph stage it must
+    write its final output (the next stage reads it on the GPU)."""
+    from seldon_core_amd.models import synthetic_xgboost, to_row_model
+
+    C = sca.native()
+    ens = synthetic_xgboost(200, 6, 4, seed=3)
+    scaler = _lin(C, np.eye(4) * 1.5, np.zeros(4))
+    tail = _lin(C, np.array([[2.0]]), np.array([-1.0]))  # reads the tree's output on the GPU
+    g = C.graph_model([{"kind": "model", "model": scaler, "inputs": [-1]},
+                       {"kind": "model", "model": to_row_model(ens), "inputs": [0]},
+                       {"kind": "model", "model": tail, "inputs": [1]}], 4)
+    unit = C.BatchedUnit(g, 0, max_batch=4096)
+    direct = C.BatchedUnit(to_row_model(ens), 0, max_batch=4096)
+    try:
+        X = np.random.default_rng(rows).normal(size=(rows, 4))
+        ref = np.asarray(ens.predict(X * 1.5)).reshape(rows, -1)
+        got = np.asarray(unit.run(X)).reshape(rows, -1)
+        np.testing.assert_allclose(got, 2.0 * ref - 1.0, rtol=2e-5, atol=4e-5)
+        got_direct = np.asarray(direct.run(X * 1.5)).reshape(rows, -1)
+        np.testing.assert_allclose(got_direct, ref, rtol=2e-5, atol=2e-5)
+    finally:
+        unit.stop()
+        direct.stop()

@@ -94,8 +94,30 @@ def main():
             for parts in (4, 8, 16, 32):
                 variants.append((f"split{parts}", parts, 0, "split"))
             variants.append(("tile", 0, 0, "tile"))
+            for parts in (8, 16):
+                variants.append((f"split{parts}_hostfold", parts, 0, "split_host"))
         for v in variants:
             name, chunk, lds, fused = v[:4]
+            if fused == "split_host":  # part sums to out[r][part]; the host adds them (timed kernel only)
+                out = torch.empty(rows * chunk, dtype=torch.float64, device=dev)
+
+                def launch():
+                    K.tree_perfect_split(X.data_ptr(), rows, F, nodes.data_ptr(), leaves.data_ptr(), D, 0, T, chunk,
+                                         0, 1.0, 0, out.data_ptr(), 1, 0, 0, s)
+
+                for _ in range(20):
+                    launch()
+                torch.cuda.synchronize()
+                folded = out.view(rows, chunk).sum(1)
+                err = float((folded - out_ref).abs().max()) if out_ref is not None else None
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    launch()
+                e1.record()
+                torch.cuda.synchronize()
+                row[name] = {"us": round(e0.elapsed_time(e1) * 1000 / a.iters, 2), "max_err": err}
+                continue
             if fused == "tile":
                 out = torch.empty(rows, dtype=torch.float64, device=dev)
                 acc = torch.zeros(rows, dtype=torch.float64, device=dev)
