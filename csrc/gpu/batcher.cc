@@ -196,6 +196,8 @@ void BatchedUnit::drain_shards(std::deque<Item>& into) {
 
 constexpr size_t kDirectH2DBytes = size_t(1) << 20;
 
+thread_local const RowModel* g_raw_output_model = nullptr;
+
 void BatchedUnit::ensure_capacity(Slot& s, int rows, int cols) {
   const int oc = std::max(model_->out_cols(cols), model_->raw_out_cols(rows, cols));
   const size_t need_in = size_t(rows) * cols * sizeof(double);

@@ -68,8 +68,6 @@ void LinearModel::run_cpu(const double* X, int rows, int, double* out) const {
   }
 }
 
-thread_local const RowModel* g_raw_output_model = nullptr;
-
 // ------------------------------------------------------------ tree ensemble
 static const int kPlanSizes[] = {4, 8, 16, 32, 64, 128, 256, 512};
 
