@@ -122,15 +122,15 @@ void guarded(Series* timer, Done k, F&& body) {
   st->k = std::move(k);
   st->timer = timer;
   st->t0 = Clock::now();
-  Done kk = [st](Outcome o) {
-    if (st->fired.exchange(true)) return;
-    if (st->timer) st->timer->observe_seconds(std::chrono::duration<double>(Clock::now() - st->t0).count());
-    st->k(std::move(o));
+  auto fire = [](const std::shared_ptr<Once>& o1, Outcome o) {
+    if (o1->fired.exchange(true)) return;
+    if (o1->timer) o1->timer->observe_seconds(std::chrono::duration<double>(Clock::now() - o1->t0).count());
+    o1->k(std::move(o));
   };
   try {
-    body(kk);
+    body(Done([st, fire](Outcome o) { fire(st, std::move(o)); }));  // handed over, not copied
   } catch (const std::exception& e) {
-    kk(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, e.what())));
+    fire(st, Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, e.what())));
   }
 }
 
@@ -567,7 +567,7 @@ void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
   if (!n->fused.empty()) {
     CallCtx cc{n, &ctx->puid, &ctx->exec};
     guarded(n->client_timer[int(Method::TRANSFORM_INPUT)],
-            traced(ctx, n, "device-graph", [this, n, input, ctx, k](Outcome o) mutable {
+            traced(ctx, n, "device-graph", [this, n, input, ctx, k = std::move(k)](Outcome o) mutable {
               if (o.err) { k(std::move(o)); return; }
               if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
               add_metrics(n, *o.msg, ctx.get());
@@ -582,7 +582,8 @@ void Engine::eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k) {
   }
   CallCtx cc{n, &ctx->puid, &ctx->exec};
   guarded(n->client_timer[int(Method::TRANSFORM_INPUT)],
-          traced(ctx, n, n->is_model ? "predict" : "transform-input", [this, n, input, ctx, k](Outcome o) mutable {
+          traced(ctx, n, n->is_model ? "predict" : "transform-input",
+                 [this, n, input, ctx, k = std::move(k)](Outcome o) mutable {
             if (o.err) { k(std::move(o)); return; }
             if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
             after_input(n, std::move(input), std::move(o.msg), std::move(ctx), std::move(k));
@@ -597,51 +598,24 @@ void Engine::after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCt
   add_metrics(n, *ti, ctx.get());
   const SeldonMessage* in_raw = input.get();
   MsgPtr keep_in = std::move(input);
+  // a node without transform-input passes its input through: then `ti` IS the
+  // input and the extra reference would force merge_meta to copy the message
+  // (merge_meta reads every tag before it rewrites the meta)
+  if (keep_in.get() == ti.get()) keep_in.reset();
   ti = merge_meta(std::move(ti), {in_raw}, ctx->puid);
   keep_in.reset();
   if (n->children.empty()) {
     k(Outcome::ok(std::move(ti)));
     return;
   }
-  auto dispatch = [this, n, ctx, k](MsgPtr ti2, int routing) {
-    {
-      std::lock_guard<std::mutex> g(ctx->mu);
-      bool found = false;
-      for (auto& kv : ctx->routing)
-        if (kv.first == n->name) { kv.second = routing; found = true; break; }
-      if (!found) ctx->routing.emplace_back(n->name, routing);
-    }
-    std::vector<Node*> selected;
-    if (routing == -1) selected = n->children;
-    else selected.push_back(n->children[size_t(routing)]);
-    struct Fan {
-      std::vector<MsgPtr> outs;
-      std::atomic<int> remaining;
-      std::atomic<bool> failed{false};
-    };
-    auto fan = std::make_shared<Fan>();
-    fan->outs.resize(selected.size());
-    fan->remaining.store(int(selected.size()));
-    for (size_t i = 0; i < selected.size(); ++i) {
-      eval(selected[i], ti2, ctx, [this, n, ctx, k, fan, i](Outcome o) {
-        if (o.err) {
-          if (!fan->failed.exchange(true)) k(std::move(o));
-          return;
-        }
-        fan->outs[i] = std::move(o.msg);
-        if (fan->remaining.fetch_sub(1, std::memory_order_acq_rel) == 1 && !fan->failed.load())
-          fan_in(n, std::move(fan->outs), ctx, k);
-      });
-    }
-  };
   if (!n->has(Method::ROUTE)) {
-    dispatch(std::move(ti), -1);
+    dispatch_children(n, std::move(ctx), std::move(k), std::move(ti), -1);
     return;
   }
   CallCtx cc{n, &ctx->puid, &ctx->exec};
   MsgPtr ti_keep = ti;
   guarded(n->client_timer[int(Method::ROUTE)],
-          traced(ctx, n, "route", [this, n, ctx, k, ti_keep, dispatch](Outcome o) {
+          traced(ctx, n, "route", [this, n, ctx, ti_keep, k = std::move(k)](Outcome o) mutable {
             if (o.err) { k(std::move(o)); return; }
             int routing = -1;
             if (o.msg) {
@@ -656,41 +630,83 @@ void Engine::after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCt
               }
               add_metrics(n, *o.msg, ctx.get());
             }
-            dispatch(ti_keep, routing);
+            dispatch_children(n, ctx, std::move(k), std::move(ti_keep), routing);
           }),
           [&](Done kk) { n->unit->route(cc, ti, std::move(kk)); });
 }
 
-void Engine::fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> ctx, Done k) {
-  auto after_agg = [this, n, ctx, k, outs](Outcome o) {
-    if (o.err) { k(std::move(o)); return; }
-    if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty aggregate from " + n->name))); return; }
-    add_metrics(n, *o.msg, ctx.get());
-    std::vector<const SeldonMessage*> prev;
-    prev.reserve(outs.size());
-    for (const auto& m : outs) prev.push_back(m.get());
-    MsgPtr agg = merge_meta(std::move(o.msg), prev, ctx->puid);
-    if (!n->has(Method::TRANSFORM_OUTPUT)) {  // identity transform: meta already merged
-      k(Outcome::ok(std::move(agg)));
-      return;
-    }
-    CallCtx cc{n, &ctx->puid, &ctx->exec};
-    guarded(n->client_timer[int(Method::TRANSFORM_OUTPUT)],
-            traced(ctx, n, "transform-output", [this, n, ctx, k, agg](Outcome o2) {
-              if (o2.err) { k(std::move(o2)); return; }
-              if (!o2.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
-              add_metrics(n, *o2.msg, ctx.get());
-              k(Outcome::ok(merge_meta(std::move(o2.msg), {agg.get()}, ctx->puid)));
-            }),
-            [&](Done kk) { n->unit->transform_output(cc, agg, std::move(kk)); });
+void Engine::dispatch_children(Node* n, std::shared_ptr<ReqCtx> ctx, Done k, MsgPtr ti2, int routing) {
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    bool found = false;
+    for (auto& kv : ctx->routing)
+      if (kv.first == n->name) { kv.second = routing; found = true; break; }
+    if (!found) ctx->routing.emplace_back(n->name, routing);
+  }
+  std::vector<Node*> selected;
+  if (routing == -1) selected = n->children;
+  else selected.push_back(n->children[size_t(routing)]);
+  struct Fan {
+    std::vector<MsgPtr> outs;
+    std::atomic<int> remaining;
+    std::atomic<bool> failed{false};
   };
+  auto fan = std::make_shared<Fan>();
+  fan->outs.resize(selected.size());
+  fan->remaining.store(int(selected.size()));
+  for (size_t i = 0; i < selected.size(); ++i) {
+    eval(selected[i], ti2, ctx, [this, n, ctx, k, fan, i](Outcome o) {
+      if (o.err) {
+        if (!fan->failed.exchange(true)) k(std::move(o));
+        return;
+      }
+      fan->outs[i] = std::move(o.msg);
+      if (fan->remaining.fetch_sub(1, std::memory_order_acq_rel) == 1 && !fan->failed.load())
+        fan_in(n, std::move(fan->outs), ctx, k);
+    });
+  }
+}
+
+void Engine::fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> ctx, Done k) {
+  std::vector<const SeldonMessage*> prev;
+  prev.reserve(outs.size());
+  for (const auto& m : outs) prev.push_back(m.get());
   if (!n->has(Method::AGGREGATE)) {
-    after_agg(Outcome::ok(outs[0]));
+    // identity aggregate: hand the first child's reply over without another
+    // reference so merge_meta rewrites it in place (prev[0] stays valid: the
+    // message lives on in `first`)
+    MsgPtr first = std::move(outs[0]);
+    after_aggregate(n, std::move(first), prev, std::move(ctx), std::move(k));
     return;
   }
   CallCtx cc{n, &ctx->puid, &ctx->exec};
-  guarded(n->client_timer[int(Method::AGGREGATE)], traced(ctx, n, "aggregate", after_agg),
-          [&](Done kk) { n->unit->aggregate(cc, outs, std::move(kk)); });
+  auto held = std::make_shared<std::vector<MsgPtr>>(std::move(outs));
+  guarded(n->client_timer[int(Method::AGGREGATE)],
+          traced(ctx, n, "aggregate", [this, n, ctx, k, held, prev = std::move(prev)](Outcome o) mutable {
+            if (o.err) { k(std::move(o)); return; }
+            if (!o.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty aggregate from " + n->name))); return; }
+            after_aggregate(n, std::move(o.msg), prev, std::move(ctx), std::move(k));
+          }),
+          [&](Done kk) { n->unit->aggregate(cc, *held, std::move(kk)); });
+}
+
+void Engine::after_aggregate(Node* n, MsgPtr agg_raw, const std::vector<const SeldonMessage*>& prev,
+                             std::shared_ptr<ReqCtx> ctx, Done k) {
+  add_metrics(n, *agg_raw, ctx.get());
+  MsgPtr agg = merge_meta(std::move(agg_raw), prev, ctx->puid);
+  if (!n->has(Method::TRANSFORM_OUTPUT)) {  // identity transform: meta already merged
+    k(Outcome::ok(std::move(agg)));
+    return;
+  }
+  CallCtx cc{n, &ctx->puid, &ctx->exec};
+  guarded(n->client_timer[int(Method::TRANSFORM_OUTPUT)],
+          traced(ctx, n, "transform-output", [this, n, ctx, k = std::move(k), agg](Outcome o2) mutable {
+            if (o2.err) { k(std::move(o2)); return; }
+            if (!o2.msg) { k(Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, "empty response from " + n->name))); return; }
+            add_metrics(n, *o2.msg, ctx.get());
+            k(Outcome::ok(merge_meta(std::move(o2.msg), {agg.get()}, ctx->puid)));
+          }),
+          [&](Done kk) { n->unit->transform_output(cc, agg, std::move(kk)); });
 }
 
 // ----------------------------------------------------------------- feedback

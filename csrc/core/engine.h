@@ -249,6 +249,9 @@ class Engine {
   void eval(Node* n, MsgPtr input, std::shared_ptr<ReqCtx> ctx, Done k);
   void after_input(Node* n, MsgPtr input, MsgPtr ti, std::shared_ptr<ReqCtx> ctx, Done k);
   void fan_in(Node* n, std::vector<MsgPtr> outs, std::shared_ptr<ReqCtx> ctx, Done k);
+  void dispatch_children(Node* n, std::shared_ptr<ReqCtx> ctx, Done k, MsgPtr ti, int routing);
+  void after_aggregate(Node* n, MsgPtr agg_raw, const std::vector<const SeldonMessage*>& prev,
+                       std::shared_ptr<ReqCtx> ctx, Done k);
   void feedback_node(Node* n, std::shared_ptr<const Feedback> fb, FbDone k);
   void add_metrics(Node* n, const SeldonMessage& m, ReqCtx* ctx);
   Node* compile(const UnitSpec& u);
