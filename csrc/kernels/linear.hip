@@ -129,7 +129,7 @@ using f64x4 = __attribute__((ext_vector_type(4))) double;
 // NCT 16-column tiles x RT 16-row tiles per wave; CW waves split the classes
 // and KS waves split K (KS > 1 only with CW == 1); a workgroup owns 16 RT rows
 // and every class.
-template <int ACT, int NCT, int CW, int KS, int RT>
+template <int ACT, int NCT, int CW, int KS, int RT, int G>
 __global__ __launch_bounds__(64 * CW * KS) void linear_mfma_rows(const double* __restrict__ X, int rows, int K,
                                                                  const double* __restrict__ W,
                                                                  const double* __restrict__ b, int C,
@@ -146,11 +146,20 @@ __global__ __launch_bounds__(64 * CW * KS) void linear_mfma_rows(const double* _
   const int chunks = (K + 15) >> 4;          // K in 16-k chunks, split over the KS slices
   const int per = (chunks + KS - 1) / KS;
   const int c_begin = ks * per, c_end = min(chunks, c_begin + per);
-  f64x4 acc[RT][NCT];
+  // P accumulator sets: a 1-2 tile wave alternates two sets by k-step so
+  // consecutive MFMAs are independent (a dependent MFMA waits out the whole
+  // latency of the one before)
+  constexpr int P = NCT * RT <= 2 ? 2 : 1;
+  f64x4 acc[RT][NCT], acc2[P > 1 ? RT : 1][P > 1 ? NCT : 1];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < NCT; ++t) acc[rt][t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  if constexpr (P > 1)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc2[rt][t] = f64x4{0.0, 0.0, 0.0, 0.0};
   const bool vec = (K & 3) == 0;             // rows 32-byte aligned: vector loads
   auto load4 = [&](const double* p, bool ok, int k, double* v) {
     if (ok && vec && k + 3 < K) {
@@ -163,9 +172,8 @@ __global__ __launch_bounds__(64 * CW * KS) void linear_mfma_rows(const double* _
     }
   };
   // Chunks go in groups of G: the group's loads are issued together, then its
-  // MFMAs -- narrow tiles (the memory-bound shapes) keep 4 chunks' loads in
-  // flight per wave instead of one 2 KB round trip at a time.
-  constexpr int G = NCT * RT <= 2 ? 4 : 1;
+  // MFMAs -- narrow tiles (the memory-bound shapes) keep several chunks' loads
+  // in flight per wave instead of one 2 KB round trip at a time.
   for (int c0 = c_begin; c0 < c_end; c0 += G) {
     double a[G][RT][4], w[G][NCT][4];
 #pragma unroll
@@ -184,6 +192,9 @@ __global__ __launch_bounds__(64 * CW * KS) void linear_mfma_rows(const double* _
         load4(W + size_t(j < C ? j : 0) * K, live && j < C, k, w[u][t]);
       }
     }
+    // (class tile, k-step, row tile): a W fragment feeds its RT MFMAs back to
+    // back (k-step outermost measured the same at 8192 x 256 -> 1000: 139.7
+    // vs 136-140 us, profiles/r06m_linear_split)
 #pragma unroll
     for (int u = 0; u < G; ++u)
 #pragma unroll
@@ -191,9 +202,21 @@ __global__ __launch_bounds__(64 * CW * KS) void linear_mfma_rows(const double* _
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
+          for (int rt = 0; rt < RT; ++rt) {
+            if constexpr (P > 1) {
+              if (s2 & 1) {
+                acc2[rt][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt][s2], w[u][t][s2], acc2[rt][t], 0, 0, 0);
+                continue;
+              }
+            }
             acc[rt][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt][s2], w[u][t][s2], acc[rt][t], 0, 0, 0);
+          }
   }
+  if constexpr (P > 1)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc[rt][t] += acc2[rt][t];
   if constexpr (KS > 1) {  // slices 1.. hand their partial logits to slice 0
     if (ks > 0) {
 #pragma unroll
@@ -341,7 +364,7 @@ bool mfma_eligible(int rows, int K, int C) {
   return C <= 1024 && double(rows) * K * C >= double(1 << 20);
 }
 
-template <int ACT, int NCT, int CW, int KS, int RT>
+template <int ACT, int NCT, int CW, int KS, int RT, int G = (NCT * RT <= 2 ? 4 : 1)>
 void launch_mfma_t(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
                    hipStream_t s, hipEvent_t stop);
 
@@ -355,12 +378,37 @@ void launch_maybe_ext(void (*k)(Args...), dim3 grid, dim3 block, size_t lds, hip
   else hipLaunchKernelGGL(k, grid, block, lds, s, args...);
 }
 
-template <int ACT, int NCT, int CW, int KS, int RT>
+template <int ACT, int NCT, int CW, int KS, int RT, int G>
 void launch_mfma_t(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
                    hipStream_t s, hipEvent_t stop) {
   constexpr int R = 16 * RT;
-  launch_maybe_ext(linear_mfma_rows<ACT, NCT, CW, KS, RT>, dim3((rows + R - 1) / R), dim3(64 * CW * KS), 0, s, stop,
+  launch_maybe_ext(linear_mfma_rows<ACT, NCT, CW, KS, RT, G>, dim3((rows + R - 1) / R), dim3(64 * CW * KS), 0, s, stop,
                    X, rows, K, W, b, C, out);
+}
+
+// Narrow models (<= 2 class tiles) are memory bound on X: what matters is
+// how many bytes each CU keeps in flight.  Variant v = (K slices KS, chunk
+// group G): 0 (4, 4), 1 (4, 8), 2 (8, 4), 3 (16, 4), 4 (16, 2), 5 (8, 8).
+// Measured (profiles/r06m_linear_split): deep rows (K >= 512) in batches of
+// fewer than 16384 rows want more K slices -- 4096 x 784 -> 10 8.8 us on
+// (16, 2) vs 11.3 on (4, 4), 4096 x 3072 22.7 on (8, 4) vs 29.7 -- while
+// shallow rows and very large batches already fill the chip with (4, 4)
+// (16384 x 64: 6.4 vs 7.4-15 us; 32768 x 784: 45 vs 48-62).
+// SCA_LINEAR_MFMA_SPLIT=v+1 forces one (A/B).
+template <int ACT, int NCT>
+void launch_mfma_narrow(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
+                        hipStream_t s, hipEvent_t stop) {
+  int v = -1;
+  if (const char* e = std::getenv("SCA_LINEAR_MFMA_SPLIT")) v = std::atoi(e) - 1;
+  if (v < 0 || v > 5) v = (rows < 16384 && K >= 512) ? (K <= 1024 ? 4 : 2) : 0;
+  switch (v) {
+    case 1: launch_mfma_t<ACT, NCT, 1, 4, 1, 8>(X, rows, K, W, b, C, out, s, stop); break;
+    case 2: launch_mfma_t<ACT, NCT, 1, 8, 1, 4>(X, rows, K, W, b, C, out, s, stop); break;
+    case 3: launch_mfma_t<ACT, NCT, 1, 16, 1, 4>(X, rows, K, W, b, C, out, s, stop); break;
+    case 4: launch_mfma_t<ACT, NCT, 1, 16, 1, 2>(X, rows, K, W, b, C, out, s, stop); break;
+    case 5: launch_mfma_t<ACT, NCT, 1, 8, 1, 8>(X, rows, K, W, b, C, out, s, stop); break;
+    default: launch_mfma_t<ACT, NCT, 1, 4, 1, 4>(X, rows, K, W, b, C, out, s, stop); break;
+  }
 }
 
 // Tiling by C (16-column tiles T): up to 4 tiles in one wave with K split over
@@ -371,8 +419,8 @@ template <int ACT>
 void launch_mfma(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
                  hipStream_t s, hipEvent_t stop) {
   const int tiles = (C + 15) / 16;
-  if (tiles <= 1) launch_mfma_t<ACT, 1, 1, 4, 1>(X, rows, K, W, b, C, out, s, stop);
-  else if (tiles <= 2) launch_mfma_t<ACT, 2, 1, 4, 1>(X, rows, K, W, b, C, out, s, stop);
+  if (tiles <= 1) launch_mfma_narrow<ACT, 1>(X, rows, K, W, b, C, out, s, stop);
+  else if (tiles <= 2) launch_mfma_narrow<ACT, 2>(X, rows, K, W, b, C, out, s, stop);
   else if (tiles <= 4) launch_mfma_t<ACT, 4, 1, 4, 1>(X, rows, K, W, b, C, out, s, stop);
   else if (tiles <= 8) launch_mfma_t<ACT, 2, 4, 1, 1>(X, rows, K, W, b, C, out, s, stop);
   else if (tiles <= 16) launch_mfma_t<ACT, 4, 4, 1, 1>(X, rows, K, W, b, C, out, s, stop);

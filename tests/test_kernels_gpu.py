@@ -82,6 +82,25 @@ def test_linear_mfma_f64(C_, monkeypatch, rows, K, C, act, mode):
     torch.testing.assert_close(out, _linear_ref(X, W, b, act), rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("variant", range(1, 7))
+@pytest.mark.parametrize("rows,K,C,act", [(4096, 784, 10, 1), (97, 789, 20, 3), (33, 1030, 1, 2), (700, 3072, 7, 0)])
+def test_linear_mfma_narrow_split_variants(C_, monkeypatch, variant, rows, K, C, act):
+    """Every K-slice / chunk-group variant of the narrow MFMA tiles (1-2 class
+    tiles; SCA_LINEAR_MFMA_SPLIT forces one) equals torch fp64 at 1e-12,
+    including K not a multiple of 4 (scalar loads) and fewer rows than one
+    16-row tile per slice."""
+    monkeypatch.setenv("SCA_LINEAR_MFMA", "2")
+    monkeypatch.setenv("SCA_LINEAR_MFMA_SPLIT", str(variant))
+    g = torch.Generator().manual_seed(variant * 1000 + rows + K + C)
+    X = torch.randn(rows, K, dtype=torch.float64, generator=g).to(dev)
+    W = (torch.randn(C, K, dtype=torch.float64, generator=g) / K ** 0.5).to(dev)
+    b = torch.randn(C, dtype=torch.float64, generator=g).to(dev)
+    out = torch.full((rows, 2 if act == 2 else C), float("nan"), dtype=torch.float64, device=dev)
+    C_.kernels.linear_f64(X.data_ptr(), rows, K, W.data_ptr(), b.data_ptr(), C, act, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, _linear_ref(X, W, b, act), rtol=1e-12, atol=1e-12)
+
+
 def test_iris_headline_shape_stays_on_the_thread_kernel(C_):
     for rows in (1, 14, 256, 4096):
         assert not C_.kernels.linear_uses_mfma(rows, 4, 3)
