@@ -284,11 +284,12 @@ class PyUnit : public Unit {
     for (auto& j : q) lk_fail(j, why);
   }
 
-  // Two dense jobs can share one stacked call: same method, 2-D rows of one
-  // width, same feature names.
+  // Two dense jobs can share one stacked call: same method, same trailing
+  // dimensions (2-D rows of one width, or e.g. [n, 3, 224, 224] images), same
+  // feature names; they stack along the first axis.
   static bool stackable(const Job& a, const Job& b) {
-    return a.dense && b.dense && a.op == b.op && a.shape.size() == 2 && b.shape.size() == 2 && a.cols == b.cols &&
-           a.in->data.names == b.in->data.names;
+    return a.dense && b.dense && a.op == b.op && a.shape.size() >= 2 && a.shape.size() == b.shape.size() &&
+           std::equal(a.shape.begin() + 1, a.shape.end(), b.shape.begin() + 1) && a.in->data.names == b.in->data.names;
   }
 
   bool take(std::vector<Job>& out) {
@@ -297,7 +298,7 @@ class PyUnit : public Unit {
     if (!running_ && queue_.empty()) return false;
     out.push_back(std::move(queue_.front()));
     queue_.pop_front();
-    if (opts_.batch_rows > 0 && out[0].dense && out[0].op != kRoute && out[0].shape.size() == 2) {
+    if (opts_.batch_rows > 0 && out[0].dense && out[0].op != kRoute && out[0].shape.size() >= 2) {
       int64_t rows = out[0].rows;
       for (auto it = queue_.begin(); it != queue_.end() && rows < opts_.batch_rows;) {
         if (stackable(out[0], *it) && rows + it->rows <= opts_.batch_rows) {
@@ -505,7 +506,9 @@ class PyUnit : public Unit {
       X = py::array_t<double>(shp, ptr, base);
       j0.x = ptr;
     } else {
-      py::array_t<double> a({py::ssize_t(total), py::ssize_t(j0.cols)});
+      std::vector<py::ssize_t> shp(j0.shape.begin(), j0.shape.end());
+      shp[0] = py::ssize_t(total);
+      py::array_t<double> a(shp);
       double* dst = a.mutable_data();
       for (auto& j : jobs) {
         std::memcpy(dst, j.x, size_t(j.rows * j.cols) * sizeof(double));

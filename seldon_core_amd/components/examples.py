@@ -237,3 +237,49 @@ class EchoModel:
 
     def predict(self, X, features_names):
         return X
+
+
+@register("IMAGENET_MODEL")
+class ImageNetModel:
+    """The ensemble's two MODEL nodes (resources/model/Prediction.py:70-104:
+    an OpenVINO DenseNet-169 / ResNet-50 ``exec_net.infer`` on ``[1, 3, 224,
+    224]``, float64 probabilities back), here a :mod:`seldon_core_amd.models.cnn`
+    network on PyTorch-ROCm: BN folded into the convolutions, bf16 NHWC on the
+    matrix cores, one captured HIP graph per batch bucket.
+
+    ``seldon_batching``: concurrent requests reach ``predict`` as one stacked
+    ``[B, 3, H, W]`` batch (up to ``max_batch`` images), one graph launch.
+    ``device=-1`` (or no GPU) runs the folded fp32 network on the CPU.
+    """
+
+    def __init__(self, arch: str = "resnet50", weights: str = "", device: Optional[int] = None, dtype: str = "bf16",
+                 max_batch: int = 32, graphs: bool = True, seed: int = 0, image: int = 224):
+        from ..models import cnn
+
+        self.arch = arch
+        self.image = int(image)
+        self.seldon_batching = int(max_batch)
+        net = cnn.build(arch, weights=weights, seed=int(seed))
+        dev = _gpu_device(device)
+        self.gpu = dev is not None
+        if self.gpu:
+            self.net = cnn.CompiledCnn(net, device=dev, dtype=dtype, max_batch=int(max_batch), graphs=bool(graphs),
+                                       image=self.image)
+            if self.net.graph_error:
+                logger.warning("%s: HIP graph capture failed (%s); serving eagerly", arch, self.net.graph_error)
+        else:
+            self.cpu_net = cnn.fold_for_inference(net).float()
+        self.calls = 0
+        self.images = 0
+
+    def predict(self, X, feature_names):
+        X = np.asarray(X)
+        X = X.reshape(-1, 3, self.image, self.image)
+        self.calls += 1
+        self.images += X.shape[0]
+        if self.gpu:
+            return self.net(X)
+        import torch
+
+        with torch.no_grad():
+            return torch.softmax(self.cpu_net(torch.from_numpy(X.astype(np.float32))), 1).double().numpy()

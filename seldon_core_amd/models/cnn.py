@@ -1,0 +1,398 @@
+"""ImageNet CNNs for the reference's OpenVINO ensemble, served on PyTorch-ROCm.
+
+The reference's ImageNet ensemble
+(``examples/models/openvino_imagenet_ensemble/seldon_ov_predict_ensemble.json``)
+runs two OpenVINO IR classifiers on the CPU, DenseNet-169 and ResNet-50
+(``resources/model/Prediction.py:70-104``: ``exec_net.infer`` on a
+``[1, 3, 224, 224]`` float32 tensor, probabilities ``[1, 1000]`` back as
+float64).  It publishes 26.2-27.3 ms per image for one model
+(``openvino_imagenet_ensemble.ipynb:1161-1170``).
+
+Here the same two architectures are plain ``torch.nn`` modules, written from
+the papers (He et al. 2015, bottleneck v1.5 with the stride on the 3x3;
+Huang et al. 2016, DenseNet-BC, growth 32), with torchvision's parameter
+names so a torchvision ``state_dict`` loads unchanged.  There is no network
+here and torchvision is not installed, so the default weights are a seeded
+random initialisation scaled to keep activations O(1); ``weights=`` loads a
+real checkpoint (safetensors, or a ``state_dict`` via
+``torch.load(weights_only=True)``).
+
+MI355X execution (:class:`CompiledCnn`): inference-only rewrites first --
+every BatchNorm that directly follows a convolution is folded into that
+convolution's weights and bias (ResNet-50 loses all 53 BN kernels; DenseNet
+keeps its pre-activation BNs, which sit before a ReLU) -- then bf16 weights
+in channels-last layout (MIOpen's NHWC implicit-GEMM convolutions on the
+matrix cores), and one HIP graph per batch bucket (1, 2, 4, ... max) so a
+request is a single graph launch instead of ~170 (ResNet-50) to ~600
+(DenseNet-169) kernel launches.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+try:
+    import torch
+    from torch import nn
+    import torch.nn.functional as F
+except ImportError:  # pragma: no cover - torch is part of the image
+    torch = None
+    nn = None
+
+
+# The ensemble's transformer hands the models raw BGR pixels, 0..255, CHW
+# (ImageNetTransformer, as the reference's cv2-based one does); the OpenVINO
+# IRs carry their own mean / scale.  These networks do the same: ImageNet
+# mean / std in BGR order, as non-persistent buffers (not in the state_dict).
+BGR_MEAN = (103.53, 116.28, 123.675)
+BGR_STD = (57.375, 57.12, 58.395)
+
+
+def _input_norm(module: "nn.Module") -> None:
+    module.register_buffer("in_mean", torch.tensor(BGR_MEAN).reshape(1, 3, 1, 1), persistent=False)
+    module.register_buffer("in_scale", 1.0 / torch.tensor(BGR_STD).reshape(1, 3, 1, 1), persistent=False)
+
+
+# ------------------------------------------------------------------ ResNet-50
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.downsample = downsample
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        idn = self.downsample(x) if self.downsample is not None else x
+        return F.relu(out + idn)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers: Sequence[int] = (3, 4, 6, 3), num_classes: int = 1000):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.layer1 = self._stage(64, layers[0], 1)
+        self.layer2 = self._stage(128, layers[1], 2)
+        self.layer3 = self._stage(256, layers[2], 2)
+        self.layer4 = self._stage(512, layers[3], 2)
+        self.fc = nn.Linear(512 * 4, num_classes)
+        _input_norm(self)
+
+    def _stage(self, planes: int, blocks: int, stride: int) -> nn.Sequential:
+        down = None
+        if stride != 1 or self.inplanes != planes * 4:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+                                 nn.BatchNorm2d(planes * 4))
+        mods = [Bottleneck(self.inplanes, planes, stride, down)]
+        self.inplanes = planes * 4
+        mods += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*mods)
+
+    def forward(self, x):
+        x = (x - self.in_mean) * self.in_scale
+        x = F.max_pool2d(F.relu(self.bn1(self.conv1(x))), 3, 2, 1)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+# -------------------------------------------------------------- DenseNet-169
+class DenseLayer(nn.Module):
+    def __init__(self, cin: int, growth: int, bn_size: int):
+        super().__init__()
+        self.norm1 = nn.BatchNorm2d(cin)
+        self.conv1 = nn.Conv2d(cin, bn_size * growth, 1, bias=False)
+        self.norm2 = nn.BatchNorm2d(bn_size * growth)
+        self.conv2 = nn.Conv2d(bn_size * growth, growth, 3, padding=1, bias=False)
+
+    def forward(self, x):
+        y = self.conv1(F.relu(self.norm1(x)))
+        return self.conv2(F.relu(self.norm2(y)))
+
+
+class DenseBlock(nn.ModuleDict):
+    def __init__(self, n: int, cin: int, growth: int, bn_size: int):
+        super().__init__()
+        for i in range(n):
+            self[f"denselayer{i + 1}"] = DenseLayer(cin + i * growth, growth, bn_size)
+
+    def forward(self, x):
+        feats = [x]
+        for layer in self.values():
+            feats.append(layer(torch.cat(feats, 1)))
+        return torch.cat(feats, 1)
+
+
+class Transition(nn.Sequential):
+    def __init__(self, cin: int, cout: int):
+        super().__init__()
+        self.norm = nn.BatchNorm2d(cin)
+        self.conv = nn.Conv2d(cin, cout, 1, bias=False)
+
+    def forward(self, x):
+        return F.avg_pool2d(self.conv(F.relu(self.norm(x))), 2, 2)
+
+
+class DenseNet(nn.Module):
+    def __init__(self, blocks: Sequence[int] = (6, 12, 32, 32), growth: int = 32, init: int = 64, bn_size: int = 4,
+                 num_classes: int = 1000):
+        super().__init__()
+        f = nn.Sequential()
+        f.add_module("conv0", nn.Conv2d(3, init, 7, stride=2, padding=3, bias=False))
+        f.add_module("norm0", nn.BatchNorm2d(init))
+        f.add_module("relu0", nn.ReLU(inplace=True))
+        f.add_module("pool0", nn.MaxPool2d(3, 2, 1))
+        c = init
+        for i, n in enumerate(blocks):
+            f.add_module(f"denseblock{i + 1}", DenseBlock(n, c, growth, bn_size))
+            c += n * growth
+            if i != len(blocks) - 1:
+                f.add_module(f"transition{i + 1}", Transition(c, c // 2))
+                c //= 2
+        f.add_module("norm5", nn.BatchNorm2d(c))
+        self.features = f
+        self.classifier = nn.Linear(c, num_classes)
+        _input_norm(self)
+
+    def forward(self, x):
+        x = F.relu(self.features((x - self.in_mean) * self.in_scale))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.classifier(x)
+
+
+ARCHS = {
+    "resnet50": lambda: ResNet((3, 4, 6, 3)),
+    "resnet101": lambda: ResNet((3, 4, 23, 3)),
+    "densenet121": lambda: DenseNet((6, 12, 24, 16)),
+    "densenet169": lambda: DenseNet((6, 12, 32, 32)),
+}
+
+
+def random_init(model: nn.Module, seed: int = 0) -> nn.Module:
+    """Seeded stand-in for trained weights: He-normal convolutions and
+    BatchNorm statistics / affines drawn so every block's output stays O(1)
+    through the whole network (residual branches enter scaled down), and a
+    classifier giving O(1) logits -- so the softmax is not one-hot and numerics
+    tests compare something meaningful."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, m in model.named_modules():
+            if isinstance(m, nn.Conv2d):
+                fan_in = m.in_channels * m.kernel_size[0] * m.kernel_size[1] // m.groups
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) * math.sqrt(2.0 / fan_in))
+            elif isinstance(m, nn.BatchNorm2d):
+                n = m.num_features
+                m.running_mean.copy_(torch.randn(n, generator=g) * 0.1)
+                m.running_var.copy_(1.0 + torch.rand(n, generator=g))
+                gamma = 0.2 if name.endswith("bn3") or (name.endswith(".1") and "downsample" in name) else 1.0
+                m.weight.copy_(gamma * (1.0 + 0.1 * torch.randn(n, generator=g)))
+                m.bias.copy_(0.05 * torch.randn(n, generator=g))
+            elif isinstance(m, nn.Linear):
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) / math.sqrt(m.in_features) * 8.0)
+                m.bias.copy_(0.1 * torch.randn(m.bias.shape, generator=g))
+    return model
+
+
+def load_weights(model: nn.Module, path: str) -> nn.Module:
+    """A torchvision-named state_dict: ``.safetensors`` via safetensors, else
+    ``torch.load(weights_only=True)`` (never unpickles arbitrary objects)."""
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+
+        sd = load_file(path)
+    else:
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
+            sd = sd["state_dict"]
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    real_missing = [k for k in missing if not k.endswith("num_batches_tracked")]
+    if real_missing or unexpected:
+        raise ValueError(f"{path}: missing {real_missing[:5]}, unexpected {list(unexpected)[:5]}")
+    return model
+
+
+def build(arch: str = "resnet50", weights: str = "", seed: int = 0) -> nn.Module:
+    if arch not in ARCHS:
+        raise ValueError(f"unknown CNN arch {arch!r}; one of {sorted(ARCHS)}")
+    m = ARCHS[arch]()
+    if weights:
+        load_weights(m, weights)
+    else:
+        random_init(m, seed)
+    return m.eval()
+
+
+# ------------------------------------------------------- inference rewrites
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
+    """conv followed by eval-mode BN -> one conv with bias (exact algebra, fp32)."""
+    s = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+    out = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride, conv.padding,
+                    conv.dilation, conv.groups, bias=True)
+    with torch.no_grad():
+        out.weight.copy_(conv.weight * s.reshape(-1, 1, 1, 1))
+        b0 = conv.bias if conv.bias is not None else torch.zeros_like(bn.running_mean)
+        out.bias.copy_((b0 - bn.running_mean) * s + bn.bias)
+    return out
+
+
+class _FoldedBottleneck(nn.Module):
+    def __init__(self, b: Bottleneck):
+        super().__init__()
+        self.c1, self.c2, self.c3 = _fold(b.conv1, b.bn1), _fold(b.conv2, b.bn2), _fold(b.conv3, b.bn3)
+        self.down = _fold(b.downsample[0], b.downsample[1]) if b.downsample is not None else None
+
+    def forward(self, x):
+        out = self.c3(F.relu(self.c2(F.relu(self.c1(x)))))
+        return F.relu(out + (self.down(x) if self.down is not None else x))
+
+
+class _FoldedResNet(nn.Module):
+    def __init__(self, r: ResNet):
+        super().__init__()
+        self.stem = _fold(r.conv1, r.bn1)
+        self.blocks = nn.Sequential(*[_FoldedBottleneck(b) for st in (r.layer1, r.layer2, r.layer3, r.layer4)
+                                      for b in st])
+        self.fc = r.fc
+        _input_norm(self)
+
+    def forward(self, x):
+        x = F.max_pool2d(F.relu(self.stem((x - self.in_mean) * self.in_scale)), 3, 2, 1)
+        x = torch.flatten(F.adaptive_avg_pool2d(self.blocks(x), 1), 1)
+        return self.fc(x)
+
+
+class _FoldedDenseLayer(nn.Module):
+    def __init__(self, l: DenseLayer):
+        super().__init__()
+        self.norm1 = l.norm1
+        self.c1 = _fold(l.conv1, l.norm2)   # the 1x1's output BN folds into it
+        self.conv2 = l.conv2
+
+    def forward(self, x):
+        return self.conv2(F.relu(self.c1(F.relu(self.norm1(x)))))
+
+
+def fold_for_inference(model: nn.Module) -> nn.Module:
+    """Inference graph with conv -> BN pairs folded (fp32 algebra, done once)."""
+    model = model.eval()
+    if isinstance(model, ResNet):
+        return _FoldedResNet(model).eval()
+    if isinstance(model, DenseNet):
+        for blk in model.features:
+            if isinstance(blk, DenseBlock):
+                for k in list(blk.keys()):
+                    blk[k] = _FoldedDenseLayer(blk[k])
+        return model
+    return model
+
+
+# ------------------------------------------------------------ GPU execution
+class CompiledCnn:
+    """A classifier ready to serve on one GPU: folded, cast, channels-last,
+    with one captured HIP graph per batch bucket.
+
+    ``__call__(x)`` takes ``[B, 3, H, W]`` (numpy or tensor, any float dtype)
+    and returns softmax probabilities ``[B, classes]`` as float64 numpy, as the
+    reference's ``Prediction.predict`` does.  Batches larger than the biggest
+    bucket run in bucket-sized pieces; a batch is padded up to its bucket.
+    """
+
+    def __init__(self, model: nn.Module, device: int = 0, dtype: str = "bf16", max_batch: int = 32,
+                 graphs: bool = True, image: int = 224, channels_last: bool = True):
+        self.device = torch.device(f"cuda:{device}")
+        self.dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
+        self.channels_last = channels_last
+        self.image = image
+        m = fold_for_inference(model).to(self.device, dtype=self.dtype)
+        if channels_last:
+            m = m.to(memory_format=torch.channels_last)
+        self.model = m
+        self.buckets: List[int] = []
+        b = 1
+        while b < max_batch:
+            self.buckets.append(b)
+            b *= 2
+        self.buckets.append(max_batch)
+        self.graphs: Dict[int, tuple] = {}
+        self.stream = torch.cuda.Stream(self.device)
+        self.graph_error: Optional[str] = None
+        if graphs:
+            try:
+                for bs in self.buckets:
+                    self._capture(bs)
+            except Exception as e:  # a capture the runtime refuses: serve eagerly
+                self.graphs.clear()
+                self.graph_error = f"{type(e).__name__}: {e}"
+
+    def _forward(self, x):
+        with torch.no_grad():
+            return torch.softmax(self.model(x).float(), dim=1)
+
+    def _static_input(self, bs: int):
+        x = torch.zeros(bs, 3, self.image, self.image, device=self.device, dtype=self.dtype)
+        return x.contiguous(memory_format=torch.channels_last) if self.channels_last else x
+
+    def _capture(self, bs: int) -> None:
+        x = self._static_input(bs)
+        with torch.cuda.stream(self.stream):
+            for _ in range(2):  # library algorithm choice / workspace before capture
+                self._forward(x)
+        self.stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self.stream):
+            y = self._forward(x)
+        self.graphs[bs] = (g, x, y)
+
+    def _bucket(self, n: int) -> int:
+        for b in self.buckets:
+            if n <= b:
+                return b
+        return self.buckets[-1]
+
+    def run(self, x: "torch.Tensor") -> "torch.Tensor":
+        """Device tensor in, device float32 probabilities out (stream-ordered
+        on this object's stream)."""
+        n = x.shape[0]
+        outs = []
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            for i in range(0, n, self.buckets[-1]):
+                part = x[i:i + self.buckets[-1]]
+                k = part.shape[0]
+                bs = self._bucket(k)
+                if bs in self.graphs:
+                    g, xs, ys = self.graphs[bs]
+                    xs[:k].copy_(part)
+                    if k < bs:
+                        xs[k:].zero_()
+                    g.replay()
+                    outs.append(ys[:k].clone())
+                else:
+                    xi = part.to(self.dtype)
+                    if self.channels_last:
+                        xi = xi.contiguous(memory_format=torch.channels_last)
+                    outs.append(self._forward(xi))
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
+
+    def __call__(self, X) -> np.ndarray:
+        if isinstance(X, np.ndarray):
+            t = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32))
+        else:
+            t = X.float()
+        t = t.reshape(-1, 3, self.image, self.image).to(self.device, non_blocking=False)
+        y = self.run(t)
+        self.stream.synchronize()
+        return y.double().cpu().numpy()
