@@ -89,6 +89,7 @@ class PyUnit : public Unit {
         if (op) dense_mask_ |= 1u << op;
       }
     }
+    has_call_json_ = py::hasattr(adapter_, "call_json");
     dead_.reset(new std::atomic<bool>[std::max<size_t>(1, opts_.worker_fds.size())]());
     running_ = true;
     if (opts_.worker_fds.empty()) {
@@ -386,6 +387,31 @@ class PyUnit : public Unit {
     return m;
   }
 
+  // (float64 array, names, kind, meta json | None) from PythonUnit.call_json;
+  // called with the GIL held.
+  static Outcome dense_reply(const Job& j, const py::tuple& t) {
+    py::array_t<double, py::array::c_style | py::array::forcecast> Y(t[0]);
+    std::vector<int64_t> shape(Y.shape(), Y.shape() + Y.ndim());
+    const std::string kind = t[2].cast<std::string>();
+    const DataKind k = kind == "tftensor" ? DataKind::TfTensor : kind == "ndarray" ? DataKind::NdArray : DataKind::Tensor;
+    auto m = std::make_shared<SeldonMessage>();
+    m->payload = Payload::Data;
+    m->data.set_dense(k, shape, std::vector<double>(Y.data(), Y.data() + Y.size()));
+    m->data.names = t[1].cast<std::vector<std::string>>();
+    m->has_meta = true;
+    if (!t[3].is_none()) {
+      try {
+        SeldonMessage tmp;
+        message_from_json(parse_json("{\"meta\":" + t[3].cast<std::string>() + "}"), tmp);
+        m->meta = std::move(tmp.meta);
+      } catch (const std::exception& e) {
+        return Outcome::fail(make_error(ApiError::MICROSERVICE_ERROR, std::string("bad meta from python unit: ") + e.what()));
+      }
+    }
+    if (j.in) m->meta.puid = j.in->meta.puid;
+    return Outcome::ok(std::move(m));
+  }
+
   static Outcome json_response(const std::string& text) {
     if (text.empty() || text == "null") return Outcome::ok(nullptr);
     auto m = std::make_shared<SeldonMessage>();
@@ -435,10 +461,13 @@ class PyUnit : public Unit {
       if (j0.dense) {
         call_dense_inproc(jobs, res);
       } else {
-        py::object r = adapter_.attr(op_name(j0.op))(texts[0], j0.node);
-        std::string out = r.is_none() ? std::string() : r.cast<std::string>();
+        py::object r = has_call_json_ ? adapter_.attr("call_json")(op_name(j0.op), texts[0], j0.node)
+                                      : adapter_.attr(op_name(j0.op))(texts[0], j0.node);
         if (j0.op == kFeedback) fb_res.push_back(nullptr);
-        else {
+        else if (py::isinstance<py::tuple>(r)) {
+          res[0] = dense_reply(j0, r.cast<py::tuple>());  // a raw hook's numeric array: no JSON
+        } else {
+          std::string out = r.is_none() ? std::string() : r.cast<std::string>();
           py::gil_scoped_release nogil;
           res[0] = json_response(out);
         }
@@ -710,6 +739,7 @@ class PyUnit : public Unit {
   uint32_t builtin_;
   PyUnitOptions opts_;
   uint32_t dense_mask_ = 0;
+  bool has_call_json_ = false;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Job> queue_;

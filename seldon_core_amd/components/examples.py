@@ -130,8 +130,9 @@ class ImageNetTransformer:
 
             from .. import ops
 
-            t = torch.from_numpy(img).cuda(self.device or 0)
-            out = ops.crop_resize_chw(t, self.size).cpu().numpy()
+            with _side_stream(self, self.device or 0):
+                t = torch.from_numpy(img).cuda(self.device or 0)
+                out = ops.crop_resize_chw(t, self.size).cpu().numpy()
         else:
             from ..ops import crop_resize_chw_ref
 
@@ -141,7 +142,22 @@ class ImageNetTransformer:
     def transform_input_raw(self, request: dict) -> dict:
         jpeg = base64.b64decode(request["binData"]) if isinstance(request.get("binData"), str) else request["binData"]
         X = self.preprocess(jpeg)
-        return {"data": {"names": ["x"], "tftensor": _tftensor_json(X)}}
+        # the array itself: inside an engine graph it becomes a dense tftensor
+        # message with no JSON / base64 round trip (PythonUnit.call_json); a
+        # JSON reply (dispatch path) encodes it as the reference's TensorProto
+        return {"data": {"names": ["x"], "tftensor": X}}
+
+
+def _side_stream(obj, dev: int):
+    """The component's own (non-blocking) stream: its GPU work must not sit
+    on the null stream, which orders it behind every other component's
+    (e.g. the ensemble's CNN graphs) -- see models/cnn.py CompiledCnn.__call__."""
+    import torch
+
+    st = obj.__dict__.get("_stream")
+    if st is None:
+        st = obj.__dict__["_stream"] = torch.cuda.Stream(torch.device(f"cuda:{dev}"))
+    return torch.cuda.stream(st)
 
 
 def _gpu_device(device: Optional[int]) -> Optional[int]:
@@ -172,10 +188,11 @@ class ImageNetCombiner:
 
             from .. import ops
 
-            ts = [torch.as_tensor(np.reshape(np.asarray(x, dtype=np.float64), (1, -1)), device=f"cuda:{dev}")
-                  for x in Xs[:2]]
-            self.gpu_calls += 1
-            return ops.combine_mean(ts).cpu().numpy()
+            with _side_stream(self, dev):
+                ts = [torch.as_tensor(np.reshape(np.asarray(x, dtype=np.float64), (1, -1)), device=f"cuda:{dev}")
+                      for x in Xs[:2]]
+                self.gpu_calls += 1
+                return ops.combine_mean(ts).cpu().numpy()
         return (np.reshape(Xs[0], (1, -1)) + np.reshape(Xs[1], (1, -1))) / 2.0
 
 
@@ -207,7 +224,8 @@ class ImageNetOutputTransformer:
             from .. import ops
 
             self.gpu_calls += 1
-            idx = int(ops.argmax_rows(torch.as_tensor(result, device=f"cuda:{dev}")).cpu()[0])
+            with _side_stream(self, dev):
+                idx = int(ops.argmax_rows(torch.as_tensor(result, device=f"cuda:{dev}")).cpu()[0])
         else:
             idx = int(np.argmax(result[0]))
         return {"strData": self.cnames[idx]}

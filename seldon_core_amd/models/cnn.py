@@ -362,11 +362,16 @@ class CompiledCnn:
         return self.buckets[-1]
 
     def run(self, x: "torch.Tensor") -> "torch.Tensor":
-        """Device tensor in, device float32 probabilities out (stream-ordered
-        on this object's stream)."""
+        """Device tensor in, device float32 probabilities out, ordered after
+        the caller's current stream and before it."""
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        y = self._run(x)
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        return y
+
+    def _run(self, x: "torch.Tensor") -> "torch.Tensor":
         n = x.shape[0]
         outs = []
-        self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             for i in range(0, n, self.buckets[-1]):
                 part = x[i:i + self.buckets[-1]]
@@ -384,15 +389,17 @@ class CompiledCnn:
                     if self.channels_last:
                         xi = xi.contiguous(memory_format=torch.channels_last)
                     outs.append(self._forward(xi))
-        torch.cuda.current_stream(self.device).wait_stream(self.stream)
-        return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
+            return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
 
     def __call__(self, X) -> np.ndarray:
-        if isinstance(X, np.ndarray):
-            t = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32))
-        else:
-            t = X.float()
-        t = t.reshape(-1, 3, self.image, self.image).to(self.device, non_blocking=False)
-        y = self.run(t)
-        self.stream.synchronize()
-        return y.double().cpu().numpy()
+        """Host batch in, host float64 probabilities out.  Every step -- the
+        copy in (the host array as it is; the cast runs on the GPU), the graph,
+        the copy out -- is on this object's own stream, never the null stream:
+        the null stream would order each model's copies behind every other
+        component's GPU work, and the ensemble's two models (and the image
+        transformer) would run one after another instead of side by side."""
+        t = torch.from_numpy(np.ascontiguousarray(X)) if isinstance(X, np.ndarray) else X
+        with torch.cuda.stream(self.stream):
+            td = t.reshape(-1, 3, self.image, self.image).to(self.device, non_blocking=False)
+            y = self._run(td).double().cpu()
+        return y.numpy()

@@ -107,7 +107,26 @@ class NumpyJSONEncoder(json.JSONEncoder):
 
 
 def dumps(obj: Any) -> str:
-    return json.dumps(obj, cls=NumpyJSONEncoder)
+    return json.dumps(_wire_arrays(obj), cls=NumpyJSONEncoder)
+
+
+def _wire_arrays(obj: Any) -> Any:
+    """A reply whose ``data.tensor`` / ``data.tftensor`` is a numpy array (a raw
+    hook may return one: inside an engine graph it travels densely, see
+    PythonUnit.call_json) in its wire form: ``{"shape", "values"}`` / a
+    TensorProto JSON."""
+    if not isinstance(obj, dict) or not isinstance(obj.get("data"), dict):
+        return obj
+    data = obj["data"]
+    t, tf = data.get("tensor"), data.get("tftensor")
+    if not isinstance(t, np.ndarray) and not isinstance(tf, np.ndarray):
+        return obj
+    data = dict(data)
+    if isinstance(t, np.ndarray):
+        data["tensor"] = {"shape": list(t.shape), "values": t.ravel().tolist()}
+    if isinstance(tf, np.ndarray):
+        data["tftensor"] = array_to_tftensor(tf)
+    return dict(obj, data=data)
 
 
 def array_to_rest_datadef(data_type: str, array: np.ndarray, names: Optional[List[str]] = None) -> Dict:

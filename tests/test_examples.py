@@ -4,6 +4,7 @@ combiners/mnist_combiner, output_transformers, openvino_imagenet_ensemble)."""
 import base64
 import concurrent.futures as cf
 import io
+import json
 import os
 
 import numpy as np
@@ -13,6 +14,7 @@ import seldon_core_amd as sca
 from seldon_core_amd.components.examples import (ImageNetCombiner, ImageNetOutputTransformer, ImageNetTransformer,
                                                   MeanClassifier, MeanTransformer, MnistCombiner, OutputTransformer)
 from seldon_core_amd.ops import crop_resize_chw_ref
+from seldon_core_amd.serving.codec import dumps
 
 REF_NPY = "/root/reference/examples/models/mean_classifier/model.npy"
 
@@ -80,7 +82,9 @@ def test_imagenet_transformer_cpu(hw):
     data, img = _jpeg(*hw)
     t = ImageNetTransformer(device=-1, size=64)
     out = t.transform_input_raw({"binData": base64.b64encode(data).decode()})
-    tf = out["data"]["tftensor"]
+    assert isinstance(out["data"]["tftensor"], np.ndarray)  # dense inside a graph (PythonUnit.call_json)
+    tf = json.loads(dumps(out))["data"]["tftensor"]  # the reference's TensorProto JSON on the wire
+    assert tf["dtype"] == "DT_FLOAT"
     arr = np.frombuffer(base64.b64decode(tf["tensorContent"]), dtype="<f4").reshape(1, 3, 64, 64)
     bgr = np.ascontiguousarray(img[:, :, ::-1])
     np.testing.assert_array_equal(arr[0], crop_resize_chw_ref(bgr, 64))

@@ -382,3 +382,66 @@ def test_process_pool_rejects_malformed_worker_replies(monkeypatch):
         assert out["data"]["ndarray"] == [[42.0]]
     finally:
         dep.close()
+
+
+class _ArrayTransformer:
+    """A raw hook whose reply carries a numpy array (an image transformer's
+    [1, 3, H, W] tensor): dense inside a graph, TensorProto / tensor JSON on
+    the wire."""
+
+    def __init__(self, kind="tftensor"):
+        self.kind = kind
+
+    def transform_input_raw(self, request):
+        x = np.asarray(request["jsonData"]["x"], dtype=np.float32)
+        return {"data": {"names": ["a", "b"], self.kind: x.reshape(1, 2, 1, len(x) // 2) * 2},
+                "meta": {"tags": {"seen": len(x)}}}
+
+
+class _Sum4d:
+    def __init__(self):
+        self.shapes = []
+
+    def predict(self, X, names):
+        self.shapes.append(X.shape)
+        time.sleep(0.002)
+        return X.reshape(len(X), -1).sum(axis=1, keepdims=True)
+
+
+@pytest.mark.parametrize("kind", ["tftensor", "tensor"])
+def test_raw_hook_array_reply_is_dense_in_a_graph_and_wire_encoded_alone(kind):
+    graph = {"name": "t", "type": "TRANSFORMER", "children": [{"name": "m", "type": "MODEL"}]}
+    model = _Sum4d()
+    model.seldon_batching = 16
+    spec = {"name": "p", "graph": graph, "componentSpecs": [{"spec": {"containers": []}}]}
+    dep = sca.Deployment(spec, device=-1, components={"t": _ArrayTransformer(kind), "m": model})
+    try:
+        reqs = [{"jsonData": {"x": [float(i), 1.0, 2.0, 3.0]}} for i in range(24)]
+        with cf.ThreadPoolExecutor(8) as ex:
+            outs = list(ex.map(dep.predict, reqs))
+        for i, o in enumerate(outs):
+            got = o["data"].get("tensor", {}).get("values") or o["data"].get("tftensor")
+            assert o["meta"]["tags"]["seen"] == 4
+            if kind == "tensor":
+                assert got == [2.0 * (i + 6)]
+        assert all(len(s) == 4 and s[1:] == (2, 1, 2) for s in model.shapes)  # 4-D rows stacked on axis 0
+        assert dep.python_units["m"].native.stats()["rows"] == 24
+    finally:
+        dep.close()
+    alone = sca.Deployment({"name": "p", "graph": {"name": "t", "type": "TRANSFORMER"},
+                            "componentSpecs": [{"spec": {"containers": []}}]}, device=-1,
+                           components={"t": _ArrayTransformer(kind)})
+    try:
+        o = alone.predict({"jsonData": {"x": [1.0, 2.0, 3.0, 4.0]}})
+        if kind == "tensor":
+            assert o["data"]["tensor"] == {"shape": [1, 2, 1, 2], "values": [2.0, 4.0, 6.0, 8.0]}
+        else:
+            assert [int(d["size"]) for d in o["data"]["tftensor"]["tensorShape"]["dim"]] == [1, 2, 1, 2]
+    finally:
+        alone.close()
+    # the JSON path (a microservice or a pool worker) encodes the same reply
+    from seldon_core_amd.serving.adapter import PythonUnit
+
+    txt = PythonUnit(_ArrayTransformer(kind), "TRANSFORMER").transform_input(json.dumps(reqs[0]), "t")
+    d = json.loads(txt)["data"]
+    assert ("values" in d["tensor"]) if kind == "tensor" else ("tensorContent" in d["tftensor"])

@@ -26,6 +26,34 @@ def jpeg(seed):
     return base64.b64encode(b.getvalue()).decode()
 
 
+def stage_breakdown(comps, reqs):
+    """Each node's own work for one request, called directly (ms, mean of 20)."""
+    from seldon_core_amd.components.examples import (ImageNetCombiner, ImageNetOutputTransformer,
+                                                      ImageNetTransformer)
+
+    tr, comb, ot = ImageNetTransformer(device=0), ImageNetCombiner(device=0), ImageNetOutputTransformer(device=0)
+
+    def t(fn, n=20):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            out = fn()
+        return out, round((time.perf_counter() - t0) / n * 1e3, 3)
+
+    ti, ms_tr = t(lambda: tr.transform_input_raw(reqs[0]))
+    from seldon_core_amd.serving.codec import dumps
+    _, ms_tr_json = t(lambda: dumps(ti))  # what the reply would cost as JSON (not paid inside a graph)
+    X = np.asarray(ti["data"]["tftensor"], dtype=np.float64)
+    p1, ms_m1 = t(lambda: comps["prediction1"].predict(X, []))
+    p2, ms_m2 = t(lambda: comps["prediction2"].predict(X, []))
+    avg, ms_comb = t(lambda: comb.aggregate([p1, p2], []))
+    _, ms_ot = t(lambda: ot.transform_output_raw({"data": {"ndarray": avg.tolist()}}))
+    print(json.dumps({"stage_ms": {"transformer": ms_tr, "transformer_json_dump": ms_tr_json, "densenet169_b1": ms_m1,
+                                   "resnet50_b1": ms_m2, "combiner": ms_comb, "output_transformer": ms_ot}}),
+          flush=True)
+    comps["prediction1"].calls = comps["prediction2"].calls = 0
+
+
 def main():
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests"))
     from test_cnn import _ensemble
@@ -40,6 +68,7 @@ def main():
     try:
         for _ in range(4):
             dep.predict(reqs[0])
+        stage_breakdown(comps, reqs)
         for conc, n in ((1, 64), (4, 128), (16, 256), (32, 512)):
             lat = []
 
@@ -57,10 +86,13 @@ def main():
             assert all(o.get("strData", "").isdigit() for o in outs), outs[:2]
             lat.sort()
             print(json.dumps({"graph": "imagenet-ensemble (densenet169 + resnet50, bf16, HIP graphs)",
+                              "switch_interval_ms": round(sys.getswitchinterval() * 1e3, 3),
                               "concurrency": conc, "requests": n, "images_per_s": round(n / wall, 1),
                               "p50_ms": round(lat[len(lat) // 2] * 1e3, 2),
                               "p99_ms": round(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3, 2),
-                              "model_calls": comps["prediction2"].calls - c0, "setup_s": round(setup, 1)}),
+                              "model_calls": comps["prediction2"].calls - c0, "setup_s": round(setup, 1),
+                              "units": {k: getattr(u, "native").stats() for k, u in dep.python_units.items()
+                                        if getattr(u, "native", None) is not None}}),
                   flush=True)
     finally:
         dep.close()
