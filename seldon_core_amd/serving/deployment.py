@@ -26,7 +26,6 @@ import json
 import logging
 import pickle
 import os
-import sys
 from typing import Any, Dict, Optional, Union
 
 from .._native import gpu_count, native
@@ -49,26 +48,6 @@ def import_class(path: str):
     if not mod:
         mod, cls = cls, cls  # reference convention: module and class share a name
     return getattr(importlib.import_module(mod), cls)
-
-
-# In-process Python units share one GIL.  A unit whose call is mostly GPU
-# work (an ImageNet CNN: copy in, graph replay, wait, copy out) gives the GIL
-# up around every library call and must win it back each time; while another
-# unit runs Python code (JPEG decode, numpy), each win waits out the
-# interpreter's switch interval, 5 ms by default.  Measured on the ImageNet
-# ensemble (profiles/r06n_imagenet): the stage times then simply add up.  With
-# two or more in-process units the interval drops to 0.2 ms (never raised;
-# SCA_PY_SWITCH_INTERVAL=<seconds> overrides, 0 leaves it alone).
-PY_SWITCH_INTERVAL_S = 2e-4
-
-
-def _shorten_switch_interval(python_units: int) -> None:
-    env = os.environ.get("SCA_PY_SWITCH_INTERVAL")
-    target = float(env) if env else (PY_SWITCH_INTERVAL_S if python_units >= 2 else 0.0)
-    if target > 0 and sys.getswitchinterval() > target:
-        logger.info("%d in-process python units: interpreter switch interval %.1f -> %.2f ms", python_units,
-                    sys.getswitchinterval() * 1e3, target * 1e3)
-        sys.setswitchinterval(target)
 
 
 class Deployment:
@@ -337,8 +316,6 @@ class Deployment:
         adapter.native = self.engine.bind_python(node["name"], adapter, 0, batch_rows, fds)
         self.units[node["name"]] = adapter
         self.__dict__.setdefault("python_units", {})[node["name"]] = adapter
-        if not fds:
-            _shorten_switch_interval(sum(1 for u in self.python_units.values() if not getattr(u, "_procs", None)))
 
     def _python_options(self, node: Dict, obj: Any):
         """(batch_rows, workers) of a Python node.  Precedence: node extension

@@ -86,7 +86,6 @@ def main():
             assert all(o.get("strData", "").isdigit() for o in outs), outs[:2]
             lat.sort()
             print(json.dumps({"graph": "imagenet-ensemble (densenet169 + resnet50, bf16, HIP graphs)",
-                              "switch_interval_ms": round(sys.getswitchinterval() * 1e3, 3),
                               "concurrency": conc, "requests": n, "images_per_s": round(n / wall, 1),
                               "p50_ms": round(lat[len(lat) // 2] * 1e3, 2),
                               "p99_ms": round(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3, 2),
