@@ -156,3 +156,20 @@ def test_ensemble_graph_on_gpu():
         assert comps["prediction2"].images == 16
     finally:
         dep.close()
+
+
+def test_example_spec_serves_a_jpeg_on_cpu():
+    """examples/imagenet/seldon_imagenet_ensemble.json: the reference's
+    ensemble graph, node names and all, answering one binData request."""
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "imagenet",
+                        "seldon_imagenet_ensemble.json")
+    dep = sca.Deployment(path, device=-1)
+    try:
+        out = dep.predict({"binData": base64.b64encode(_png(240, 320, 5)).decode()})
+        assert out["strData"].isdigit() and 0 <= int(out["strData"]) < 1000
+        assert set(out["meta"]["requestPath"]) == {"imagenet-otransformer", "imagenet-itransformer",
+                                                   "imagenet-combiner", "prediction1", "prediction2"}
+    finally:
+        dep.close()
