@@ -62,7 +62,11 @@ def main():
     comps = {"prediction1": ImageNetModel("densenet169", device=0, max_batch=32),
              "prediction2": ImageNetModel("resnet50", device=0, max_batch=32)}
     setup = time.perf_counter() - t0
-    spec = {"name": "p", "graph": _ensemble(0, 224), "componentSpecs": [{"spec": {"containers": []}}]}
+    graph = _ensemble(0, 224)
+    workers = int(os.environ.get("IMAGENET_TR_WORKERS", "0"))
+    if workers:  # the transformer (JPEG decode + crop) in a pool of worker processes
+        graph["children"][0]["workers"] = workers
+    spec = {"name": "p", "graph": graph, "componentSpecs": [{"spec": {"containers": []}}]}
     dep = sca.Deployment(spec, device=0, components=comps)
     reqs = [{"binData": jpeg(i)} for i in range(64)]
     try:
@@ -86,6 +90,7 @@ def main():
             assert all(o.get("strData", "").isdigit() for o in outs), outs[:2]
             lat.sort()
             print(json.dumps({"graph": "imagenet-ensemble (densenet169 + resnet50, bf16, HIP graphs)",
+                              "transformer_workers": workers,
                               "concurrency": conc, "requests": n, "images_per_s": round(n / wall, 1),
                               "p50_ms": round(lat[len(lat) // 2] * 1e3, 2),
                               "p99_ms": round(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3, 2),
