@@ -271,7 +271,7 @@ class ImageNetModel:
     """
 
     def __init__(self, arch: str = "resnet50", weights: str = "", device: Optional[int] = None, dtype: str = "bf16",
-                 max_batch: int = 32, graphs: bool = True, seed: int = 0, image: int = 224):
+                 max_batch: int = 32, graphs: bool = True, seed: int = 0, image: int = 224, tune: bool = True):
         from ..models import cnn
 
         self.arch = arch
@@ -282,7 +282,7 @@ class ImageNetModel:
         self.gpu = dev is not None
         if self.gpu:
             self.net = cnn.CompiledCnn(net, device=dev, dtype=dtype, max_batch=int(max_batch), graphs=bool(graphs),
-                                       image=self.image)
+                                       image=self.image, tune=bool(tune))
             if self.net.graph_error:
                 logger.warning("%s: HIP graph capture failed (%s); serving eagerly", arch, self.net.graph_error)
         else:

@@ -48,15 +48,23 @@ for arch in ARCHS:
     with torch.no_grad():
         ref_logits = net(x_cpu)
     ref = torch.softmax(ref_logits, 1).double().numpy()
-    for dtype, cl, graphs in (("fp32", False, False), ("bf16", True, False), ("bf16", True, True)):
+    # (dtype, channels_last, graphs, tune)
+    configs = [("fp32", False, False, False), ("bf16", True, False, False), ("bf16", True, True, False),
+               ("bf16", None, True, True)]
+    if os.environ.get("CNN_CONFIGS") == "layouts":  # dtype / layout A/B, graphs on, untuned
+        configs = [("bf16", True, True, False), ("fp16", True, True, False), ("bf16", False, True, False),
+                   ("fp16", False, True, False)]
+    if os.environ.get("CNN_CONFIGS") == "tuned":  # both layouts with MIOpen's solver search
+        configs = [("bf16", True, True, True), ("bf16", False, True, True)]
+    for dtype, cl, graphs, tune in configs:
         t0 = time.perf_counter()
         m = cnn.CompiledCnn(cnn.build(arch, seed=1), device=0, dtype=dtype, max_batch=32, graphs=graphs,
-                            channels_last=cl)
+                            channels_last=cl, tune=tune)
         setup_s = time.perf_counter() - t0
         got = m(x_cpu.numpy())
         err = float(np.abs(got - ref).max())
         top1 = float((got.argmax(1) == ref.argmax(1)).mean())
-        res = {"arch": arch, "dtype": dtype, "channels_last": cl, "graphs": bool(m.graphs), "setup_s": round(setup_s, 1),
+        res = {"arch": arch, "tune": tune, "dtype": dtype, "channels_last": m.channels_last, "graphs": bool(m.graphs), "setup_s": round(setup_s, 1),
                "graph_error": m.graph_error, "max_abs_prob_err": err, "top1_agree": top1}
         for bs in (1, 8, 32):
             xd = torch.rand(bs, 3, 224, 224, device="cuda")
