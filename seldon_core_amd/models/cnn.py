@@ -21,10 +21,10 @@ MI355X execution (:class:`CompiledCnn`): inference-only rewrites first --
 every BatchNorm that directly follows a convolution is folded into that
 convolution's weights and bias (ResNet-50 loses all 53 BN kernels; DenseNet
 keeps its pre-activation BNs, which sit before a ReLU) -- then bf16 weights
-in channels-last layout (MIOpen's NHWC implicit-GEMM convolutions on the
-matrix cores), and one HIP graph per batch bucket (1, 2, 4, ... max) so a
-request is a single graph launch instead of ~170 (ResNet-50) to ~600
-(DenseNet-169) kernel launches.
+in channels-last layout, MIOpen's solver search run once per shape at set-up
+(its NHWC implicit-GEMM convolutions on the matrix cores), and one HIP graph
+per batch bucket (1, 2, 4, ... max) so a request is a single graph launch
+instead of ~170 (ResNet-50) to ~600 (DenseNet-169) kernel launches.
 """
 from __future__ import annotations
 
@@ -313,8 +313,8 @@ class CompiledCnn:
                  graphs: bool = True, image: int = 224, channels_last: Optional[bool] = None, tune: bool = True):
         self.device = torch.device(f"cuda:{device}")
         self.dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
-        if channels_last is None:  # measured per family (profiles/r06n_imagenet)
-            channels_last = not isinstance(model, DenseNet)
+        if channels_last is None:  # measured (profiles/r06n_imagenet): NHWC once tuned; untuned,
+            channels_last = tune or not isinstance(model, DenseNet)  # DenseNet is faster NCHW
         self.channels_last = channels_last
         self.tune = tune
         self.image = image
@@ -332,9 +332,12 @@ class CompiledCnn:
         self.stream = torch.cuda.Stream(self.device)
         self.graph_error: Optional[str] = None
         # `tune`: MIOpen times every applicable convolution solver once per
-        # shape during the warm-up (cudnn.benchmark; the choice is cached for
-        # the process), so the captured graphs hold the fastest kernels --
-        # ResNet-50 bf16 at 32 images 4.25 -> 2.2 ms.  Scoped to set-up.
+        # shape during the warm-up (cudnn.benchmark), so the captured graphs
+        # hold the fastest kernels -- ResNet-50 bf16 at 32 images 4.25 -> 2.2
+        # ms, DenseNet-169 9.3 -> 6.5 ms.  It costs set-up time on a machine
+        # whose MIOpen find database has not seen the shapes yet (44 s /
+        # 128 s for the six buckets); MIOpen keeps the results in its user
+        # database for later starts.  Scoped to set-up.
         prev = torch.backends.cudnn.benchmark
         torch.backends.cudnn.benchmark = bool(tune)
         try:

@@ -128,7 +128,9 @@ def test_compiled_cnn_bf16_graphs_match_fp32(arch):
     of images, for batches that hit a bucket exactly, pad into one, and span
     several."""
     net = cnn.build(arch, seed=1)
-    m = cnn.CompiledCnn(cnn.build(arch, seed=1), device=0, dtype="bf16", max_batch=8, graphs=True)
+    # tune=False keeps the test short (MIOpen's solver search is 44-128 s on a fresh box)
+    m = cnn.CompiledCnn(cnn.build(arch, seed=1), device=0, dtype="bf16", max_batch=8, graphs=True,
+                        tune=arch == "resnet50")
     assert m.graphs and m.graph_error is None, m.graph_error
     for n in (1, 3, 8, 11):
         x = torch.rand(n, 3, 224, 224, generator=torch.Generator().manual_seed(n)) * 255
@@ -143,8 +145,8 @@ def test_compiled_cnn_bf16_graphs_match_fp32(arch):
 @pytest.mark.gpu
 def test_ensemble_graph_on_gpu():
     size = 224
-    comps = {"prediction1": ImageNetModel("densenet169", device=0, max_batch=8),
-             "prediction2": ImageNetModel("resnet50", device=0, max_batch=8)}
+    comps = {"prediction1": ImageNetModel("densenet169", device=0, max_batch=8, tune=False),
+             "prediction2": ImageNetModel("resnet50", device=0, max_batch=8, tune=False)}
     assert comps["prediction1"].gpu and comps["prediction1"].net.graphs
     spec = {"name": "p", "graph": _ensemble(0, size), "componentSpecs": [{"spec": {"containers": []}}]}
     dep = sca.Deployment(spec, device=0, components=comps)

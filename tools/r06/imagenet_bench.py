@@ -54,7 +54,21 @@ def stage_breakdown(comps, reqs):
     comps["prediction1"].calls = comps["prediction2"].calls = 0
 
 
+def _heartbeat():
+    import threading
+
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(20)
+            print(f"# alive {time.time() - t0:.0f} s", flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
+    _heartbeat()
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests"))
     from test_cnn import _ensemble
 
