@@ -215,6 +215,17 @@ def load_pytorch(path: str, device: Optional[str] = None) -> LoadedFlavour:
         # mlflow.pytorch pickles the whole nn.Module: a user artifact, loaded as pyfunc would
         mod = torch.load(path, map_location=dev, weights_only=False)
     mod.eval()
+    if str(dev).startswith("cuda") and os.environ.get("SCA_TORCH_GRAPHS", "1") != "0":
+        # one captured HIP graph per batch bucket instead of a launch per op
+        from ..models.graphed import GraphedModule
+
+        gm = GraphedModule(mod, device=torch.device(dev).index or 0)
+
+        def graphed(X):
+            return gm(np.asarray(X, dtype=np.float32))
+
+        graphed.graphed = gm  # replay / eager counters for tests and stats
+        return LoadedFlavour("pytorch", graphed, None)
 
     def fn(X):
         with torch.no_grad():

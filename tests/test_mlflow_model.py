@@ -170,3 +170,44 @@ def test_parse_signature_forms():
     assert out.dtype == np.int64
     with pytest.raises(MLmodelError, match="unsupported"):
         parse_signature({"inputs": [{"name": "a", "type": "binary"}]})
+
+
+@pytest.mark.gpu
+def test_pytorch_flavour_on_gpu_replays_hip_graphs(tmp_path):
+    """On a GPU the pytorch flavour serves through GraphedModule: one captured
+    HIP graph per batch bucket; outputs equal eager torch at fp32 rounding for
+    batches that hit, pad into and span buckets."""
+    import torch
+
+    torch.manual_seed(1)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64), torch.nn.GELU(),
+                              torch.nn.Linear(64, 5), torch.nn.Softmax(dim=1))
+    (tmp_path / "data").mkdir()
+    torch.jit.save(torch.jit.script(net), str(tmp_path / "data" / "model.pth"))
+    _write_mlmodel(tmp_path, {"pytorch": {"model_data": "data", "pytorch_version": "2.0"}})
+    s = MLFlowServer(str(tmp_path), device="cuda:0")
+    s.load()
+    gm = s._fn.graphed
+    for n in (1, 3, 64, 300):
+        X = np.random.default_rng(n).normal(size=(n, 8))
+        with torch.no_grad():
+            want = net(torch.as_tensor(X, dtype=torch.float32)).numpy()
+        np.testing.assert_allclose(s.predict(X), want, rtol=1e-5, atol=1e-6)
+    assert gm.graph_error is None and gm.replays >= 5 and gm.eager_calls == 0  # 300 rows: 2 pieces
+
+
+@pytest.mark.gpu
+def test_graphed_module_falls_back_when_capture_is_refused():
+    import torch
+
+    from seldon_core_amd.models.graphed import GraphedModule
+
+    class HostSync(torch.nn.Module):  # .item() synchronises the host: not capturable
+        def forward(self, x):
+            return x * float(x.abs().max().item())
+
+    gm = GraphedModule(HostSync(), device=0)
+    X = np.arange(12, dtype=np.float32).reshape(3, 4)
+    np.testing.assert_allclose(gm(X), X * 11.0)
+    assert gm.graph_error is not None and gm.eager_calls >= 1
+    np.testing.assert_allclose(gm(X), X * 11.0)  # keeps serving eagerly
