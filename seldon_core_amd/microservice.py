@@ -99,6 +99,149 @@ def build_microservice(user_object: Any, service_type: str = "MODEL", name: str 
     return Deployment(spec, components={name: user_object}, device=device)
 
 
+class _Response:
+    """What a Flask test client returns, as far as component tests use it."""
+
+    def __init__(self, status: int, data: bytes, headers: Dict[str, str]):
+        self.status_code = status
+        self.data = data
+        self.headers = headers
+
+    @property
+    def status(self) -> str:
+        return str(self.status_code)
+
+    def get_json(self):
+        return json.loads(self.data)
+
+    def get_data(self, as_text: bool = False):
+        return self.data.decode() if as_text else self.data
+
+
+class _TestClient:
+    """``app.test_client()``: real HTTP requests to the app's native server on
+    a loopback port, with Flask's call shapes -- ``get(path_with_query)``,
+    ``post(path, data={...}, content_type=...)`` where a value may be a
+    ``(path, filename)`` file tuple (multipart) -- so component tests written
+    for the reference's Flask wrapper keep running."""
+
+    def __init__(self, app: "MicroserviceApp"):
+        self.app = app
+
+    def _send(self, method: str, path: str, body: bytes = None, content_type: str = None) -> _Response:
+        import urllib.error
+        import urllib.parse
+        import urllib.request
+
+        base, _, query = path.partition("?")
+        if query:  # Flask's client percent-encodes the query; so do we
+            query = urllib.parse.urlencode(urllib.parse.parse_qsl(query, keep_blank_values=True))
+        url = f"http://127.0.0.1:{self.app.port}{base}" + (f"?{query}" if query else "")
+        req = urllib.request.Request(url, data=body, method=method)
+        if content_type:
+            req.add_header("Content-Type", content_type)
+        try:
+            with urllib.request.urlopen(req, timeout=60) as r:
+                return _Response(r.status, r.read(), dict(r.headers))
+        except urllib.error.HTTPError as e:
+            return _Response(e.code, e.read(), dict(e.headers))
+
+    def get(self, path: str, **_kw) -> _Response:
+        return self._send("GET", path)
+
+    def post(self, path: str, data=None, json_body=None, content_type: str = None, **kw) -> _Response:
+        import urllib.parse
+
+        if "json" in kw:
+            json_body = kw["json"]
+        if json_body is not None:
+            return self._send("POST", path, json.dumps(json_body).encode(), "application/json")
+        if isinstance(data, (bytes, str)):
+            return self._send("POST", path, data.encode() if isinstance(data, str) else data,
+                              content_type or "application/json")
+        data = data or {}
+        if content_type and content_type.startswith("multipart/form-data"):
+            body, ctype = _multipart(data)
+            return self._send("POST", path, body, ctype)
+        return self._send("POST", path, urllib.parse.urlencode(data).encode(), "application/x-www-form-urlencoded")
+
+
+def _multipart(fields: Dict[str, Any]):
+    import uuid
+
+    boundary = uuid.uuid4().hex
+    out = []
+    for k, v in fields.items():
+        if isinstance(v, tuple):  # (path or file object, filename)
+            src, fname = v[0], v[1] if len(v) > 1 else "file"
+            content = open(src, "rb").read() if isinstance(src, str) else src.read()
+            out.append(f'--{boundary}\r\nContent-Disposition: form-data; name="{k}"; filename="{fname}"\r\n'
+                       f"Content-Type: application/octet-stream\r\n\r\n".encode() + content + b"\r\n")
+        else:
+            out.append(f'--{boundary}\r\nContent-Disposition: form-data; name="{k}"\r\n\r\n{v}\r\n'.encode())
+    out.append(f"--{boundary}--\r\n".encode())
+    return b"".join(out), f"multipart/form-data; boundary={boundary}"
+
+
+class MicroserviceApp:
+    """``get_rest_microservice(user_object)``: the component behind the native
+    internal-API server (what ``python -m seldon_core_amd.microservice``
+    serves), with the reference's Flask-app surface for tests and embedding:
+    ``test_client()`` and ``run(host, port)``.  The server starts on first use
+    on an ephemeral loopback port; ``close()`` stops it."""
+
+    def __init__(self, user_object: Any, service_type: str = "MODEL"):
+        self.user_object = user_object
+        self.service_type = service_type
+        self._dep = None
+        self._http = None
+
+    def _start(self, host: str = "127.0.0.1", port: int = 0, threads: int = 4):
+        if self._http is None:
+            from .serving.openapi import wrapper_spec_json
+
+            self._dep = build_microservice(self.user_object, self.service_type, device=-1)
+            node = self._dep.predictor["graph"]["name"]
+            self._http = self._dep.C.HttpServer(self._dep.engine, host, [port], threads, node, True,
+                                                wrapper_spec_json())
+            self._http.start()
+        return self
+
+    @property
+    def port(self) -> int:
+        return self._start()._http.ports[0]
+
+    def test_client(self) -> _TestClient:
+        self._start()
+        return _TestClient(self)
+
+    def run(self, host: str = "0.0.0.0", port: int = DEFAULT_PORT, **_kw) -> None:
+        from .utils.shutdown import StopSignal
+
+        self._start(host, port)
+        StopSignal().install().wait()
+        self.close()
+
+    def close(self) -> None:
+        if self._http is not None:
+            self._http.stop()
+            self._http = None
+        if self._dep is not None:
+            self._dep.close()
+            self._dep = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  interpreter shutdown
+            pass
+
+
+def get_rest_microservice(user_object: Any, service_type: str = "MODEL") -> MicroserviceApp:
+    """The reference's ``seldon_core.wrapper.get_rest_microservice`` (wrapper.py:22-31)."""
+    return MicroserviceApp(user_object, service_type)
+
+
 def main(argv=None) -> None:
     logging.basicConfig(level=logging.INFO,
                         format="%(asctime)s - %(name)s:%(funcName)s:%(lineno)s - %(levelname)s:  %(message)s")

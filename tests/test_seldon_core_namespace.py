@@ -26,6 +26,7 @@ REFERENCE_NAMES = {
     "persistence": "restore persist PersistenceThread",
     "serving_test_gen": "create_seldon_api_testing_file",
     "microservice": "main",
+    "wrapper": "get_rest_microservice",
 }
 
 
@@ -127,3 +128,50 @@ def test_component_written_against_seldon_core_serves_and_keeps_its_error_contra
         assert "422" in str(ei.value) or "NEGATIVE" in str(ei.value) or "negative input" in str(ei.value)
     finally:
         dep.close()
+
+
+def test_wrapper_app_test_client_in_the_reference_call_shapes(tmp_path):
+    """seldon_core.wrapper.get_rest_microservice(user_object).test_client():
+    the reference's Flask-client call shapes against the native server."""
+    import json
+
+    from seldon_core.flask_utils import SeldonMicroserviceException
+    from seldon_core.wrapper import get_rest_microservice
+
+    class Echo:
+        def __init__(self):
+            self.rewards = []
+
+        def predict(self, X, names):
+            if isinstance(X, (bytes, bytearray)) or getattr(X, "dtype", None) is not None and X.dtype.kind == "S":
+                return np.array([[len(bytes(np.asarray(X).tobytes()))]], dtype=float)
+            X = np.asarray(X, dtype=float)
+            if X.size and X.min() < 0:
+                raise SeldonMicroserviceException("negative", status_code=402, reason="NEG")
+            return X * 2
+
+        def send_feedback(self, features, feature_names, reward, truth, routing=None):
+            self.rewards.append(reward)
+
+    comp = Echo()
+    app = get_rest_microservice(comp)
+    try:
+        c = app.test_client()
+        rv = c.get('/predict?json={"data":{"names":["a","b"],"ndarray":[[1,2]]}}')
+        assert rv.status_code == 200 and rv.get_json()["data"]["ndarray"] == [[2.0, 4.0]]
+        rv = c.post("/predict", data={"json": '{"data":{"ndarray":[[3,4]]}}'})
+        assert rv.get_json()["data"]["ndarray"] == [[6.0, 8.0]]
+        rv = c.post("/predict", data={"data": '{"names":["a","b"],"ndarray":[[1,2]]}'},
+                    content_type="multipart/form-data")
+        assert rv.status_code == 200 and rv.get_json()["data"]["ndarray"] == [[2.0, 4.0]]
+        f = tmp_path / "test.txt"
+        f.write_bytes(b"hello world")
+        rv = c.post("/predict", data={"meta": '{"puid":"1234"}', "binData": (str(f), "test.txt")},
+                    content_type="multipart/form-data")
+        assert rv.status_code == 200, rv.data
+        rv = c.get('/send-feedback?json={"request":{"data":{"ndarray":[]}},"reward":1.0}')
+        assert rv.status_code == 200 and comp.rewards == [1.0]
+        rv = c.get('/predict?json={"data":{"ndarray":[[-1,2]]}}')
+        assert rv.status_code == 402 and json.loads(rv.data)["status"]["reason"] == "NEG"
+    finally:
+        app.close()
