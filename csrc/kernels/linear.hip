@@ -386,6 +386,264 @@ void launch_mfma_t(const double* X, int rows, int K, const double* W, const doub
                    X, rows, K, W, b, C, out);
 }
 
+// ---------------------------------------------------------- wide softmax
+// Wide softmax models (C > 256 classes) at large batches.  linear_mfma_rows
+// keeps every class of a row in one workgroup's registers, which caps a
+// workgroup at 32 rows: each W fragment then feeds only 32 rows, and W is
+// re-read from L2 rows / 32 times (8192 x 256 -> 1000: 512 MB for a 2 MB W).
+// Here a workgroup owns a 64-row x 128-class tile (2 x 2 waves, each 32 rows
+// x 64 classes: 8 independent MFMA chains, next chunk's operands prefetched),
+// so W is re-read rows / 64 times and X C / 128 times, and the grid has
+// (rows / 64) x (C / 128) workgroups instead of rows / 32.  The softmax is
+// split: a tile writes exp(z - m_tile) and its rows' (m_tile, s_tile); then
+// either a second launch rescales every row by exp(m_tile - M) / S (variant
+// 2), or -- variant 1 -- the tiles store with write-through (agent-scope)
+// stores and the last of a row tile's class-group workgroups (one arrival
+// counter per row tile) folds and rescales the row tile in place with
+// coherent loads, the tree kernels' last-arriver protocol.
+constexpr int kWideRows = 64, kWideCols = 128;
+
+__device__ __forceinline__ void wide_store(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double wide_load(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool FOLD>
+__global__ __launch_bounds__(256) void linear_mfma_wide_softmax(const double* __restrict__ X, int rows, int K,
+                                                                const double* __restrict__ W,
+                                                                const double* __restrict__ b, int C,
+                                                                double* __restrict__ out, double* __restrict__ ms,
+                                                                int* __restrict__ counter) {
+  constexpr int RT = 2, NCT = 4;
+  __shared__ double s_red[2][kWideRows];               // per class-wave row max / sum
+  __shared__ double s_fac[kWideRows][8];               // fixup: per row, per class group factor
+  __shared__ int s_last;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int li = lane & 15, g = lane >> 4;
+  const int tile_r0 = blockIdx.x * kWideRows;
+  const int r0 = tile_r0 + wr * 32;
+  const int grp = blockIdx.y, groups = gridDim.y;
+  const int col0 = grp * kWideCols + wc * 64;
+  f64x4 acc[RT][NCT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) acc[rt][t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const bool vec = (K & 3) == 0;
+  auto load4 = [&](const double* p, bool ok, int k, double* v) {
+    if (ok && vec && k + 3 < K) {
+      const double2 lo = *reinterpret_cast<const double2*>(p + k);
+      const double2 hi = *reinterpret_cast<const double2*>(p + k + 2);
+      v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) v[s2] = (ok && k + s2 < K) ? p[k + s2] : 0.0;
+    }
+  };
+  const int chunks = (K + 15) >> 4;
+  constexpr int G = 2;  // chunks whose loads are in flight together
+  for (int c0 = 0; c0 < chunks; c0 += G) {
+    double a[G][RT][4], w[G][NCT][4];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const bool live = c0 + u < chunks;
+      const int k = ((c0 + u) << 4) + (g << 2);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int row = r0 + rt * 16 + li;
+        load4(X + size_t(row < rows ? row : 0) * K, live && row < rows, k, a[u][rt]);
+      }
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const int j = col0 + t * 16 + li;
+        load4(W + size_t(j < C ? j : 0) * K, live && j < C, k, w[u][t]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int t = 0; t < NCT; ++t)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+            acc[rt][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][rt][s2], w[u][t][s2], acc[rt][t], 0, 0, 0);
+  }
+  // ---- tile softmax: lane holds rows 16 rt + g + 4i (of the wave's 32) of
+  // classes col0 + 16 t + li
+#pragma unroll
+  for (int t = 0; t < NCT; ++t) {
+    const int j = col0 + t * 16 + li;
+    const double bj = (b && j < C) ? b[j] : 0.0;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[rt][t][i] += bj;
+  }
+  double m[RT][4], ssum[RT][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double v = -__builtin_inf();
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) v = (col0 + t * 16 + li) < C ? fmax(v, acc[rt][t][i]) : v;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) v = fmax(v, __shfl_xor(v, off, 64));
+      m[rt][i] = v;
+    }
+  if (li == 0)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_red[wc][wr * 32 + rt * 16 + g + 4 * i] = m[rt][i];
+  __syncthreads();
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lr = wr * 32 + rt * 16 + g + 4 * i;
+      m[rt][i] = fmax(s_red[0][lr], s_red[1][lr]);
+    }
+  __syncthreads();
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double v = 0.0;
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const bool in = (col0 + t * 16 + li) < C;
+        const double e = in ? exp(acc[rt][t][i] - m[rt][i]) : 0.0;
+        acc[rt][t][i] = e;
+        v += e;
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off, 64);
+      ssum[rt][i] = v;
+    }
+  if (li == 0)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_red[wc][wr * 32 + rt * 16 + g + 4 * i] = ssum[rt][i];
+  __syncthreads();
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lr = wr * 32 + rt * 16 + g + 4 * i;
+      const int r = tile_r0 + lr;
+      if (r >= rows) continue;
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) {
+        const int j = col0 + t * 16 + li;
+        if (j < C) {
+          if constexpr (FOLD) wide_store(out + size_t(r) * C + j, acc[rt][t][i]);
+          else out[size_t(r) * C + j] = acc[rt][t][i];
+        }
+      }
+      if (wc == 0 && li == 0) {  // the tile's (max, sum) of this row
+        if constexpr (FOLD) {
+          wide_store(ms + (size_t(r) * groups + grp) * 2, m[rt][i]);
+          wide_store(ms + (size_t(r) * groups + grp) * 2 + 1, s_red[0][lr] + s_red[1][lr]);
+        } else {
+          ms[(size_t(r) * groups + grp) * 2] = m[rt][i];
+          ms[(size_t(r) * groups + grp) * 2 + 1] = s_red[0][lr] + s_red[1][lr];
+        }
+      }
+    }
+  if constexpr (!FOLD) return;  // linear_wide_softmax_fix rescales after this launch
+  // ---- last of the row tile's class groups: fold and rescale
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores acknowledged at the coherence point
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(counter + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             groups - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x < kWideRows) {
+    const int r = tile_r0 + threadIdx.x;
+    if (r < rows) {
+      double M = -__builtin_inf();
+      for (int q = 0; q < groups; ++q) M = fmax(M, wide_load(ms + (size_t(r) * groups + q) * 2));
+      double S = 0.0;
+      for (int q = 0; q < groups; ++q)
+        S += wide_load(ms + (size_t(r) * groups + q) * 2 + 1) * exp(wide_load(ms + (size_t(r) * groups + q) * 2) - M);
+      for (int q = 0; q < groups; ++q) s_fac[threadIdx.x][q] = exp(wide_load(ms + (size_t(r) * groups + q) * 2) - M) / S;
+    }
+  }
+  __syncthreads();
+  const int nr = min(kWideRows, rows - tile_r0);
+  for (int lr = 0; lr < nr; ++lr) {
+    double* o = out + size_t(tile_r0 + lr) * C;
+    for (int j = threadIdx.x; j < C; j += 256) o[j] = wide_load(o + j) * s_fac[lr][j / kWideCols];
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(counter + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Second pass of the two-launch variant: one workgroup per row rescales the
+// row's tiles by exp(m_tile - M) / S (plain loads: the kernel boundary orders
+// them after the first launch's stores).
+__global__ __launch_bounds__(256) void linear_wide_softmax_fix(double* __restrict__ out, const double* __restrict__ ms,
+                                                               int rows, int C, int groups) {
+  const int r = blockIdx.x;
+  if (r >= rows) return;
+  const double* p = ms + size_t(r) * groups * 2;
+  double M = -__builtin_inf();
+  for (int q = 0; q < groups; ++q) M = fmax(M, p[2 * q]);
+  double S = 0.0;
+  for (int q = 0; q < groups; ++q) S += p[2 * q + 1] * exp(p[2 * q] - M);
+  double* o = out + size_t(r) * C;
+  for (int j = threadIdx.x; j < C; j += 256) o[j] *= exp(p[2 * (j / kWideCols)] - M) / S;
+}
+
+// Variant: 0 = off (linear_mfma_rows), 1 = one launch with the last-arriver
+// fold, 2 = two launches.  Measured (profiles/r06s_linear_wide, us per call):
+// the fold's write-through stores cost ~70 us of a 200 us launch, so the
+// two-launch form is the one used.  It wins where linear_mfma_rows underfills
+// the chip -- fewer than 8192 rows is fewer than 256 of its 32-row
+// workgroups: 4096 x 512 -> 1000 132 vs 239 us, 2048 x 1024 -> 1000 138 vs
+// 450 -- and for deep, wide rows (8192 x 784 -> 1000: 333 vs 358); from 8192
+// rows at K < 512 or C < 512 the old kernel stays ahead (8192 x 256 -> 1000:
+// 135 vs 157; 16384 x 384 -> 300: 160 vs 178).  SCA_LINEAR_WIDE=v forces one.
+int wide_softmax_variant(int rows, int K, int C) {
+  if (C <= 256 || C > 8 * kWideCols || rows < 256) return 0;
+  if (const char* e = std::getenv("SCA_LINEAR_WIDE")) return std::atoi(e);
+  return (rows < 8192 || (K >= 512 && C >= 512)) ? 2 : 0;
+}
+
+// Scratch (per-row per-group (max, sum) pairs + one counter per row tile) is
+// stream-ordered: allocated, zeroed, used and freed on the launch's stream, so
+// concurrent launches on other streams never share it.
+void launch_wide_softmax(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
+                         hipStream_t s, hipEvent_t stop, int variant) {
+  const int tiles = (rows + kWideRows - 1) / kWideRows, groups = (C + kWideCols - 1) / kWideCols;
+  const size_t ms_bytes = size_t(rows) * groups * 2 * sizeof(double);
+  const size_t bytes = ms_bytes + size_t(tiles) * sizeof(int);
+  void* buf = nullptr;
+  if (hipMallocAsync(&buf, bytes, s) != hipSuccess) {
+    (void)hipGetLastError();  // no pool memory: the one-workgroup-per-row-tile kernel instead
+    launch_mfma_t<kActSoftmax, 8, 8, 1, 2>(X, rows, K, W, b, C, out, s, stop);
+    return;
+  }
+  int* counter = reinterpret_cast<int*>(static_cast<char*>(buf) + ms_bytes);
+  if (variant == 2) {  // two launches: plain stores, separate rescale pass
+    hipLaunchKernelGGL(linear_mfma_wide_softmax<false>, dim3(tiles, groups), dim3(256), 0, s, X, rows, K, W, b, C,
+                       out, static_cast<double*>(buf), counter);
+    launch_maybe_ext(linear_wide_softmax_fix, dim3(rows), dim3(256), 0, s, stop, out,
+                     static_cast<const double*>(buf), rows, C, groups);
+  } else {
+    (void)hipMemsetAsync(counter, 0, size_t(tiles) * sizeof(int), s);
+    launch_maybe_ext(linear_mfma_wide_softmax<true>, dim3(tiles, groups), dim3(256), 0, s, stop, X, rows, K, W, b,
+                     C, out, static_cast<double*>(buf), counter);
+  }
+  (void)hipFreeAsync(buf, s);
+}
+
 // Narrow models (<= 2 class tiles) are memory bound on X: what matters is
 // how many bytes each CU keeps in flight.  Variant v = (K slices KS, chunk
 // group G): 0 (4, 4), 1 (4, 8), 2 (8, 4), 3 (16, 4), 4 (16, 2), 5 (8, 8).
@@ -419,6 +677,13 @@ template <int ACT>
 void launch_mfma(const double* X, int rows, int K, const double* W, const double* b, int C, double* out,
                  hipStream_t s, hipEvent_t stop) {
   const int tiles = (C + 15) / 16;
+  if (ACT == kActSoftmax) {
+    const int v = wide_softmax_variant(rows, K, C);
+    if (v == 1 || v == 2) {
+      launch_wide_softmax(X, rows, K, W, b, C, out, s, stop, v);
+      return;
+    }
+  }
   if (tiles <= 1) launch_mfma_narrow<ACT, 1>(X, rows, K, W, b, C, out, s, stop);
   else if (tiles <= 2) launch_mfma_narrow<ACT, 2>(X, rows, K, W, b, C, out, s, stop);
   else if (tiles <= 4) launch_mfma_t<ACT, 4, 1, 4, 1>(X, rows, K, W, b, C, out, s, stop);

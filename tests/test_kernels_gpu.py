@@ -101,6 +101,53 @@ def test_linear_mfma_narrow_split_variants(C_, monkeypatch, variant, rows, K, C,
     torch.testing.assert_close(out, _linear_ref(X, W, b, act), rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("rows,K,C", [(8192, 256, 1000), (257, 33, 257), (1000, 100, 1024), (4099, 7, 700),
+                                      (300, 512, 385)])
+def test_linear_wide_softmax_split_tiles(C_, monkeypatch, rows, K, C):
+    """Wide softmax (C > 256) on 64-row x 128-class tiles, with the in-kernel
+    last-arriver fold (SCA_LINEAR_WIDE=1) and with the rescale launch (2):
+    both equal torch fp64 at 1e-12 and the one-workgroup-per-row-tile kernel
+    (0), with ragged rows / classes / K."""
+    monkeypatch.setenv("SCA_LINEAR_MFMA", "2")
+    g = torch.Generator().manual_seed(rows + K + C)
+    X = torch.randn(rows, K, dtype=torch.float64, generator=g).to(dev)
+    W = (torch.randn(C, K, dtype=torch.float64, generator=g) / K ** 0.5 * 3).to(dev)
+    b = torch.randn(C, dtype=torch.float64, generator=g).to(dev)
+    outs = []
+    for wide in ("1", "0", "2"):
+        monkeypatch.setenv("SCA_LINEAR_WIDE", wide)
+        out = torch.full((rows, C), float("nan"), dtype=torch.float64, device=dev)
+        for _ in range(2):  # the second launch reuses nothing stale (counters / scratch are per launch)
+            C_.kernels.linear_f64(X.data_ptr(), rows, K, W.data_ptr(), b.data_ptr(), C, 1, out.data_ptr(), _stream())
+        torch.cuda.synchronize()
+        outs.append(out)
+    ref = _linear_ref(X, W, b, 1)
+    torch.testing.assert_close(outs[0], ref, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-12, atol=1e-14)
+    torch.testing.assert_close(outs[2], ref, rtol=1e-12, atol=1e-12)
+
+
+def test_linear_wide_softmax_concurrent_streams(C_, monkeypatch):
+    """Launches on different streams at once each get their own scratch."""
+    monkeypatch.setenv("SCA_LINEAR_MFMA", "2")
+    monkeypatch.setenv("SCA_LINEAR_WIDE", "1")
+    rows, K, C = 2048, 128, 900
+    g = torch.Generator().manual_seed(7)
+    W = (torch.randn(C, K, dtype=torch.float64, generator=g) / K ** 0.5).to(dev)
+    b = torch.randn(C, dtype=torch.float64, generator=g).to(dev)
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    Xs = [torch.randn(rows, K, dtype=torch.float64, generator=g).to(dev) for _ in streams]
+    outs = [torch.empty(rows, C, dtype=torch.float64, device=dev) for _ in streams]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for st, X, out in zip(streams, Xs, outs):
+            C_.kernels.linear_f64(X.data_ptr(), rows, K, W.data_ptr(), b.data_ptr(), C, 1, out.data_ptr(),
+                                  st.cuda_stream)
+    torch.cuda.synchronize()
+    for X, out in zip(Xs, outs):
+        torch.testing.assert_close(out, _linear_ref(X, W, b, 1), rtol=1e-12, atol=1e-12)
+
+
 def test_iris_headline_shape_stays_on_the_thread_kernel(C_):
     for rows in (1, 14, 256, 4096):
         assert not C_.kernels.linear_uses_mfma(rows, 4, 3)
