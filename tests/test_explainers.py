@@ -137,11 +137,9 @@ def test_explainer_server_over_engine(tmp_path):
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from portutil import free_port
+
+    return free_port()
 
 
 def test_serve_starts_explainer_from_spec(tmp_path):

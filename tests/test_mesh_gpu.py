@@ -22,9 +22,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from portutil import free_port
+
+    return free_port()
 
 
 def _run_gpu_ranks(world, mode, timeout=150, **extra_env):

@@ -23,9 +23,9 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from portutil import free_port
+
+    return free_port()
 
 
 def _start(api, service="MODEL", params=None):

@@ -25,30 +25,10 @@ ROUNDS = int(os.environ.get("SCA_SHUTDOWN_ROUNDS", "20"))
 PAR = 4  # process trees in flight at once (8 CPUs here; each tree is 3 processes)
 
 
-_TAKEN = set()
-
-
 def _free_port():
-    """A free port below the kernel's ephemeral range, never handed out twice
-    here: an OS-picked ephemeral port can be taken by another tree's gang
-    rendezvous or gloo sockets between this check and the server's bind."""
-    import random
+    from portutil import free_port
 
-    lo, _ = (int(x) for x in open("/proc/sys/net/ipv4/ip_local_port_range").read().split())
-    for _ in range(1000):
-        port = random.randrange(20000, max(20001, min(lo, 32768)))
-        if port in _TAKEN:
-            continue
-        with socket.socket() as s:
-            try:
-                s.bind(("127.0.0.1", port))
-            except OSError:
-                continue
-        _TAKEN.add(port)
-        return port
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    return free_port()
 
 
 def test_stop_signal_reentrant_handler_never_blocks():
