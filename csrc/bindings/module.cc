@@ -1061,6 +1061,13 @@ PYBIND11_MODULE(_C, m) {
   k.def("segment_minmax_f64", [](uintptr_t in, uintptr_t seg, int nseg, int cols, uintptr_t out, uintptr_t s) {
     kern::segment_minmax_f64(P<const double>(in), P<const int32_t>(seg), nseg, cols, P<double>(out), as_stream(s));
   });
+  k.def("scale_shift_relu_bf16_ok", &kern::scale_shift_relu_bf16_ok);
+  k.def("scale_shift_relu_bf16", [](uintptr_t x, uintptr_t scale, uintptr_t shift, int N, int C, int HW, int cl,
+                                    uintptr_t out, uintptr_t s) {
+    if (!kern::scale_shift_relu_bf16_ok(C, HW, cl)) throw std::invalid_argument("scale_shift_relu_bf16: shape not 8-aligned");
+    kern::scale_shift_relu_bf16(P<const void>(x), P<const float>(scale), P<const float>(shift), N, C, HW, cl,
+                                P<void>(out), as_stream(s));
+  });
   k.def("crop_resize_chw_u8", [](uintptr_t img, int H, int W, int C, int crop, uintptr_t out, uintptr_t s) {
     kern::crop_resize_chw_u8(P<const uint8_t>(img), H, W, C, crop, P<float>(out), as_stream(s));
   });

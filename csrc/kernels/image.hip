@@ -53,7 +53,53 @@ __global__ __launch_bounds__(256) void crop_resize_chw(const uint8_t* __restrict
   }
 }
 
+// Eval-mode BatchNorm + ReLU in one pass over a bf16 activation (DenseNet's
+// pre-activation norm -> relu, which cannot fold into a neighbouring conv):
+// out = max(0, x * scale[c] + shift[c]) in fp32, rounded to bf16.  Channels
+// innermost (NHWC, `cl`): a thread takes 8 consecutive channels as one
+// 16-byte load (C % 8 == 0); NCHW: 8 consecutive pixels of one channel
+// (HW % 8 == 0).  Replaces two kernels and one round trip through HBM.
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) { return __uint_as_float(unsigned(h) << 16); }
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) {  // round to nearest even (no NaNs here)
+  const unsigned u = __float_as_uint(f);
+  return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+__global__ __launch_bounds__(256) void scale_shift_relu_bf16(const uint4* __restrict__ x, const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, int C, int HW, int cl,
+                                                             size_t n8, uint4* __restrict__ out) {
+  const size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const uint4 v = x[i];
+  const unsigned short* h = reinterpret_cast<const unsigned short*>(&v);
+  uint4 r;
+  unsigned short* o = reinterpret_cast<unsigned short*>(&r);
+  if (cl) {
+    const int c0 = int((i * 8) % size_t(C));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = f32_to_bf16(fmaxf(0.f, bf16_to_f32(h[k]) * scale[c0 + k] + shift[c0 + k]));
+  } else {
+    const int c = int(((i * 8) / size_t(HW)) % size_t(C));
+    const float a = scale[c], b = shift[c];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = f32_to_bf16(fmaxf(0.f, bf16_to_f32(h[k]) * a + b));
+  }
+  out[i] = r;
+}
+
 }  // namespace
+
+bool scale_shift_relu_bf16_ok(int C, int HW, int channels_last) {
+  return channels_last ? C % 8 == 0 : HW % 8 == 0;
+}
+
+void scale_shift_relu_bf16(const void* x, const float* scale, const float* shift, int N, int C, int HW,
+                           int channels_last, void* out, hipStream_t s) {
+  const size_t n8 = size_t(N) * C * HW / 8;
+  if (n8 == 0) return;
+  hipLaunchKernelGGL(scale_shift_relu_bf16, dim3(unsigned((n8 + 255) / 256)), dim3(256), 0, s,
+                     static_cast<const uint4*>(x), scale, shift, C, HW, channels_last, n8, static_cast<uint4*>(out));
+}
 
 void crop_resize_chw_u8(const uint8_t* img, int H, int W, int C, int crop, float* out, hipStream_t s) {
   const int rh = H < crop ? crop : H, rw = W < crop ? crop : W;

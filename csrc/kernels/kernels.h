@@ -166,6 +166,11 @@ void device_delay_us(int us, hipStream_t stream);
 void segment_minmax_f64(const double* in, const int32_t* seg, int nseg, int cols, double* out, hipStream_t stream);
 // Decoded HWC uint8 image -> centre crop (bilinear up-size of short axes) -> CHW fp32.
 void crop_resize_chw_u8(const uint8_t* img, int H, int W, int C, int crop, float* out, hipStream_t stream);
+// relu(x * scale[c] + shift[c]) over a bf16 [N, C, H, W] activation stored
+// NCHW or (channels_last) NHWC; needs C % 8 == 0 (NHWC) or H*W % 8 == 0 (NCHW).
+bool scale_shift_relu_bf16_ok(int C, int HW, int channels_last);
+void scale_shift_relu_bf16(const void* x, const float* scale, const float* shift, int N, int C, int HW,
+                           int channels_last, void* out, hipStream_t stream);
 // ------------------------------------------------------------ fused MLP
 // A whole dense network (and the VAE outlier detector's encoder -> MC
 // reparameterised decoder -> reconstruction-MSE loop) in one launch: a

@@ -273,15 +273,54 @@ class _FoldedResNet(nn.Module):
         return self.fc(x)
 
 
+class _BnRelu(nn.Module):
+    """relu(bn(x)) for an eval-mode BatchNorm that precedes a ReLU (DenseNet's
+    pre-activation: nothing to fold it into).  On a bf16 GPU activation it is
+    one hand-written pass (``ops.bn_relu_bf16``: per-channel scale / shift +
+    ReLU) instead of PyTorch's two kernels; the fp32 scale / shift are derived
+    from the BN's current parameters on first use on a device (before graph
+    capture) and cached."""
+
+    def __init__(self, bn: nn.BatchNorm2d):
+        super().__init__()
+        self.bn = bn
+        self._ss: Dict[str, tuple] = {}
+
+    def forward(self, x):
+        if x.is_cuda and x.dtype == torch.bfloat16:
+            from .. import ops
+
+            if ops.bn_relu_bf16_applies(x):
+                key = str(x.device)
+                ss = self._ss.get(key)
+                if ss is None:
+                    bn = self.bn
+                    scale = (bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)).contiguous()
+                    shift = (bn.bias.float() - bn.running_mean.float() * scale).contiguous()
+                    ss = self._ss[key] = (scale, shift)
+                return ops.bn_relu_bf16(x, *ss)
+        return F.relu(self.bn(x))
+
+
 class _FoldedDenseLayer(nn.Module):
     def __init__(self, l: DenseLayer):
         super().__init__()
-        self.norm1 = l.norm1
+        self.pre = _BnRelu(l.norm1)
         self.c1 = _fold(l.conv1, l.norm2)   # the 1x1's output BN folds into it
         self.conv2 = l.conv2
 
     def forward(self, x):
-        return self.conv2(F.relu(self.c1(F.relu(self.norm1(x)))))
+        return self.conv2(F.relu(self.c1(self.pre(x))))
+
+
+class _FoldedTransition(nn.Module):
+    def __init__(self, t: Transition):
+        super().__init__()
+        self.pre = _BnRelu(t.norm)
+        self.conv = t.conv
+
+    def forward(self, x):
+        return F.avg_pool2d(self.conv(self.pre(x)), 2, 2)
 
 
 def fold_for_inference(model: nn.Module) -> nn.Module:
@@ -290,10 +329,12 @@ def fold_for_inference(model: nn.Module) -> nn.Module:
     if isinstance(model, ResNet):
         return _FoldedResNet(model).eval()
     if isinstance(model, DenseNet):
-        for blk in model.features:
+        for name, blk in list(model.features.named_children()):
             if isinstance(blk, DenseBlock):
                 for k in list(blk.keys()):
                     blk[k] = _FoldedDenseLayer(blk[k])
+            elif isinstance(blk, Transition):
+                setattr(model.features, name, _FoldedTransition(blk))
         return model
     return model
 

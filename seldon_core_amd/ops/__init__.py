@@ -52,6 +52,39 @@ def linear(X, W, b, act: str = "softmax"):
     return out
 
 
+def bn_relu_bf16(x, scale, shift):
+    """relu(x * scale[c] + shift[c]) over a bf16 [N, C, H, W] activation, NCHW
+    or channels_last, in one pass (``scale_shift_relu_bf16``, image.hip).
+    ``scale`` / ``shift`` are fp32 [C] on the same GPU."""
+    import torch
+
+    if not x.is_cuda or x.dtype != torch.bfloat16 or x.dim() != 4:
+        raise ValueError("bn_relu_bf16 takes a 4-D bf16 GPU tensor")
+    N, C, H, W = x.shape
+    cl = x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+    if not cl:
+        x = x.contiguous()
+    if x.data_ptr() % 16 or not _k().scale_shift_relu_bf16_ok(C, H * W, int(cl)):
+        raise ValueError("bn_relu_bf16: activation not 16-byte aligned / 8-element divisible")
+    out = torch.empty_like(x)
+    _k().scale_shift_relu_bf16(x.data_ptr(), _check(scale, torch.float32, "scale").data_ptr(),
+                               _check(shift, torch.float32, "shift").data_ptr(), N, C, H * W, int(cl),
+                               out.data_ptr(), _stream(x))
+    return out
+
+
+def bn_relu_bf16_applies(x) -> bool:
+    """Whether :func:`bn_relu_bf16` takes ``x`` as it is (else use torch)."""
+    import torch
+
+    if not x.is_cuda or x.dtype != torch.bfloat16 or x.dim() != 4 or x.data_ptr() % 16:
+        return False
+    cl = x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+    if not cl and not x.is_contiguous():
+        return False
+    return bool(_k().scale_shift_relu_bf16_ok(x.shape[1], x.shape[2] * x.shape[3], int(cl)))
+
+
 def softmax_rows(x):
     import torch
 

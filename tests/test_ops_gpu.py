@@ -75,3 +75,26 @@ def test_crop_resize_chw(torch, hw):
     ref = ops.crop_resize_chw_ref(img, 224)
     # pure crops are exact; resized axes may differ by one rounding step (fp32 fma order)
     assert np.abs(out - ref).max() <= (0 if hw[0] >= 224 and hw[1] >= 224 else 1)
+
+
+@pytest.mark.parametrize("shape,cl", [((1, 256, 56, 56), True), ((3, 64, 28, 28), False), ((2, 1664, 7, 7), True),
+                                      ((1, 128, 8, 8), False), ((4, 32, 3, 5), True)])
+def test_bn_relu_bf16_matches_torch(shape, cl):
+    """scale_shift_relu_bf16 (image.hip) == relu(batch_norm) in fp32 rounded to
+    bf16: at most one bf16 ulp apart, NCHW and channels_last."""
+    import torch
+
+    from seldon_core_amd import ops
+
+    g = torch.Generator().manual_seed(sum(shape))
+    x = (torch.randn(shape, generator=g) * 3).to("cuda", torch.bfloat16)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    C = shape[1]
+    scale = (torch.rand(C, generator=g) + 0.5).cuda()
+    shift = torch.randn(C, generator=g).cuda()
+    assert ops.bn_relu_bf16_applies(x)
+    got = ops.bn_relu_bf16(x, scale, shift)
+    assert got.is_contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format)
+    want = torch.relu(x.float() * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)).to(torch.bfloat16)
+    torch.testing.assert_close(got.float(), want.float(), rtol=8e-3, atol=1e-6)

@@ -54,6 +54,8 @@ for arch in ARCHS:
     if os.environ.get("CNN_CONFIGS") == "layouts":  # dtype / layout A/B, graphs on, untuned
         configs = [("bf16", True, True, False), ("fp16", True, True, False), ("bf16", False, True, False),
                    ("fp16", False, True, False)]
+    if os.environ.get("CNN_CONFIGS") == "default":  # the serving default (tuned NHWC) + untuned NCHW
+        configs = [("bf16", None, True, True), ("bf16", False, True, False)]
     if os.environ.get("CNN_CONFIGS") == "tuned":  # both layouts with MIOpen's solver search
         configs = [("bf16", True, True, True), ("bf16", False, True, True)]
     for dtype, cl, graphs, tune in configs:
