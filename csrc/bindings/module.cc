@@ -1061,6 +1061,10 @@ PYBIND11_MODULE(_C, m) {
   k.def("segment_minmax_f64", [](uintptr_t in, uintptr_t seg, int nseg, int cols, uintptr_t out, uintptr_t s) {
     kern::segment_minmax_f64(P<const double>(in), P<const int32_t>(seg), nseg, cols, P<double>(out), as_stream(s));
   });
+  k.def("add_relu_bf16", [](uintptr_t a, uintptr_t b, size_t n, uintptr_t out, uintptr_t s) {
+    if (n % 8) throw std::invalid_argument("add_relu_bf16: element count not a multiple of 8");
+    kern::add_relu_bf16(P<const void>(a), P<const void>(b), n, P<void>(out), as_stream(s));
+  });
   k.def("scale_shift_relu_bf16_ok", &kern::scale_shift_relu_bf16_ok);
   k.def("scale_shift_relu_bf16", [](uintptr_t x, uintptr_t scale, uintptr_t shift, int N, int C, int HW, int cl,
                                     uintptr_t out, uintptr_t s) {

@@ -87,7 +87,30 @@ __global__ __launch_bounds__(256) void scale_shift_relu_bf16(const uint4* __rest
   out[i] = r;
 }
 
+// ResNet's residual join, relu(a + b), on bf16 in one pass (8 elements per
+// thread as 16-byte vectors): replaces PyTorch's add and its ReLU kernel.
+__global__ __launch_bounds__(256) void add_relu_bf16(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                     size_t n8, uint4* __restrict__ out) {
+  const size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const uint4 va = a[i], vb = b[i];
+  const unsigned short* ha = reinterpret_cast<const unsigned short*>(&va);
+  const unsigned short* hb = reinterpret_cast<const unsigned short*>(&vb);
+  uint4 r;
+  unsigned short* o = reinterpret_cast<unsigned short*>(&r);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = f32_to_bf16(fmaxf(0.f, bf16_to_f32(ha[k]) + bf16_to_f32(hb[k])));
+  out[i] = r;
+}
+
 }  // namespace
+
+void add_relu_bf16(const void* a, const void* b, size_t n, void* out, hipStream_t s) {
+  const size_t n8 = n / 8;
+  if (n8 == 0) return;
+  hipLaunchKernelGGL(add_relu_bf16, dim3(unsigned((n8 + 255) / 256)), dim3(256), 0, s, static_cast<const uint4*>(a),
+                     static_cast<const uint4*>(b), n8, static_cast<uint4*>(out));
+}
 
 bool scale_shift_relu_bf16_ok(int C, int HW, int channels_last) {
   return channels_last ? C % 8 == 0 : HW % 8 == 0;

@@ -169,6 +169,8 @@ void crop_resize_chw_u8(const uint8_t* img, int H, int W, int C, int crop, float
 // relu(x * scale[c] + shift[c]) over a bf16 [N, C, H, W] activation stored
 // NCHW or (channels_last) NHWC; needs C % 8 == 0 (NHWC) or H*W % 8 == 0 (NCHW).
 bool scale_shift_relu_bf16_ok(int C, int HW, int channels_last);
+// relu(a + b) over n bf16 elements (n % 8 == 0, 16-byte aligned buffers).
+void add_relu_bf16(const void* a, const void* b, size_t n, void* out, hipStream_t stream);
 void scale_shift_relu_bf16(const void* x, const float* scale, const float* shift, int N, int C, int HW,
                            int channels_last, void* out, hipStream_t stream);
 // ------------------------------------------------------------ fused MLP

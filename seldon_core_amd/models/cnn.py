@@ -255,7 +255,13 @@ class _FoldedBottleneck(nn.Module):
 
     def forward(self, x):
         out = self.c3(F.relu(self.c2(F.relu(self.c1(x)))))
-        return F.relu(out + (self.down(x) if self.down is not None else x))
+        idn = self.down(x) if self.down is not None else x
+        if out.is_cuda and out.dtype == torch.bfloat16:
+            from .. import ops
+
+            if ops.add_relu_bf16_applies(out, idn):  # the residual join in one pass
+                return ops.add_relu_bf16(out, idn)
+        return F.relu(out + idn)
 
 
 class _FoldedResNet(nn.Module):

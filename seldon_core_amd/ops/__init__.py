@@ -73,6 +73,29 @@ def bn_relu_bf16(x, scale, shift):
     return out
 
 
+def add_relu_bf16(a, b):
+    """relu(a + b) for two bf16 GPU tensors of one shape and memory layout
+    (ResNet's residual join) in one pass (``add_relu_bf16``, image.hip)."""
+    if not add_relu_bf16_applies(a, b):
+        raise ValueError("add_relu_bf16 takes two same-layout, 16-byte aligned bf16 GPU tensors, numel % 8 == 0")
+    import torch
+
+    out = torch.empty_like(a)
+    _k().add_relu_bf16(a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), _stream(a))
+    return out
+
+
+def add_relu_bf16_applies(a, b) -> bool:
+    import torch
+
+    if not (a.is_cuda and b.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+        return False
+    if a.shape != b.shape or a.stride() != b.stride() or a.numel() % 8 or a.data_ptr() % 16 or b.data_ptr() % 16:
+        return False
+    fmt = torch.channels_last if a.dim() == 4 and not a.is_contiguous() else torch.contiguous_format
+    return a.is_contiguous(memory_format=fmt) and b.is_contiguous(memory_format=fmt)
+
+
 def bn_relu_bf16_applies(x) -> bool:
     """Whether :func:`bn_relu_bf16` takes ``x`` as it is (else use torch)."""
     import torch

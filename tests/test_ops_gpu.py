@@ -98,3 +98,21 @@ def test_bn_relu_bf16_matches_torch(shape, cl):
     assert got.is_contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format)
     want = torch.relu(x.float() * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)).to(torch.bfloat16)
     torch.testing.assert_close(got.float(), want.float(), rtol=8e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape,cl", [((1, 256, 56, 56), True), ((2, 2048, 7, 7), True), ((3, 64, 10, 8), False)])
+def test_add_relu_bf16_matches_torch(shape, cl):
+    import torch
+
+    from seldon_core_amd import ops
+
+    g = torch.Generator().manual_seed(sum(shape) + 1)
+    a = torch.randn(shape, generator=g).to("cuda", torch.bfloat16)
+    b = torch.randn(shape, generator=g).to("cuda", torch.bfloat16)
+    if cl:
+        a, b = a.contiguous(memory_format=torch.channels_last), b.contiguous(memory_format=torch.channels_last)
+    assert ops.add_relu_bf16_applies(a, b)
+    got = ops.add_relu_bf16(a, b)
+    want = torch.relu(a.float() + b.float()).to(torch.bfloat16)
+    torch.testing.assert_close(got.float(), want.float(), rtol=8e-3, atol=1e-6)
+    assert not ops.add_relu_bf16_applies(a, b.contiguous()) or not cl  # mixed layouts go to torch
