@@ -338,7 +338,8 @@ def fold_for_inference(model: nn.Module) -> nn.Module:
         for name, blk in list(model.features.named_children()):
             if isinstance(blk, DenseBlock):
                 for k in list(blk.keys()):
-                    blk[k] = _FoldedDenseLayer(blk[k])
+                    if isinstance(blk[k], DenseLayer):  # idempotent: a folded layer stays as it is
+                        blk[k] = _FoldedDenseLayer(blk[k])
             elif isinstance(blk, Transition):
                 setattr(model.features, name, _FoldedTransition(blk))
         return model

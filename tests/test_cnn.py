@@ -175,3 +175,13 @@ def test_example_spec_serves_a_jpeg_on_cpu():
                                                    "imagenet-combiner", "prediction1", "prediction2"}
     finally:
         dep.close()
+
+
+def test_folding_twice_is_a_no_op():
+    net = cnn.build("densenet121", seed=2)
+    x = torch.rand(1, 3, 64, 64, generator=torch.Generator().manual_seed(1)) * 255
+    with torch.no_grad():
+        once = cnn.fold_for_inference(net)
+        a = once(x)
+        b = cnn.fold_for_inference(once)(x)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
