@@ -370,12 +370,13 @@ class PyUnit : public Unit {
 
   // ------------------------------------------------------------ response
   static MsgPtr dense_response(const Job& j, const double* y, const std::vector<int64_t>& shape,
-                               std::vector<std::string> names, const std::string& meta_text) {
+                               std::vector<std::string> names, const std::string& meta_text,
+                               const DataKind* kind = nullptr) {
     auto m = std::make_shared<SeldonMessage>();
     m->payload = Payload::Data;
     int64_t n = 1;
     for (auto s : shape) n *= s;
-    m->data.set_dense(j.in->data.kind, shape, std::vector<double>(y, y + n));
+    m->data.set_dense(kind ? *kind : j.in->data.kind, shape, std::vector<double>(y, y + n));
     m->data.names = std::move(names);
     m->has_meta = true;
     if (!meta_text.empty()) {
@@ -577,10 +578,11 @@ class PyUnit : public Unit {
   // One result array -> one response per job (rows in job order).
   static void split_dense(std::vector<Job>& jobs, std::vector<Outcome>& res, const double* y,
                           const std::vector<int64_t>& yshape, const std::vector<std::string>& names,
-                          const std::string& meta_all, const std::string& meta_first, int64_t total) {
+                          const std::string& meta_all, const std::string& meta_first, int64_t total,
+                          const DataKind* kind = nullptr) {
     if (jobs.size() == 1) {
       const std::string& mt = meta_first.empty() ? meta_all : meta_first;
-      res[0] = Outcome::ok(dense_response(jobs[0], y, yshape, names, mt));
+      res[0] = Outcome::ok(dense_response(jobs[0], y, yshape, names, mt, kind));
       return;
     }
     if (yshape.empty() || yshape[0] != total) {
@@ -728,7 +730,16 @@ class PyUnit : public Unit {
         return m && !m->is_null() ? m->dump() : std::string();
       };
       std::vector<int64_t> yshape(r.shape, r.shape + r.ndim);
-      split_dense(jobs, res, y.data(), yshape, names, meta_of("meta"), meta_of("meta_first"), total);
+      // a raw hook's numeric reply (worker-side PythonUnit.call_json) names
+      // its own data kind; a dense call keeps the request's
+      DataKind k = DataKind::None;
+      const Json* kj = info.find("kind");
+      if (kj && kj->is_string() && jobs.size() == 1) {
+        const std::string ks = kj->as_string();
+        k = ks == "tftensor" ? DataKind::TfTensor : ks == "ndarray" ? DataKind::NdArray : DataKind::Tensor;
+      }
+      split_dense(jobs, res, y.data(), yshape, names, meta_of("meta"), meta_of("meta_first"), total,
+                  k == DataKind::None ? nullptr : &k);
     } catch (const std::exception& e) {
       auto err = make_error(ApiError::MICROSERVICE_ERROR, std::string("bad reply from python worker: ") + e.what());
       for (auto& o : res) o = Outcome::fail(err);

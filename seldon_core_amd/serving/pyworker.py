@@ -62,8 +62,14 @@ def serve(fd: int) -> None:
                     send_frame(sock, 1, b"", res[1].encode())
             else:
                 node_json, _, msg = text.decode().partition("\n")
-                out = getattr(unit, method)(msg, json.loads(node_json))
-                send_frame(sock, 1, b"", (out or "").encode())
+                out = unit.call_json(method, msg, json.loads(node_json))
+                if isinstance(out, tuple):  # a raw hook's numeric array: binary frame, no JSON
+                    y, names, kind, meta = out
+                    info = json.dumps({"names": names, "meta": json.loads(meta) if meta else None,
+                                       "meta_first": None, "kind": kind})
+                    send_frame(sock, 0, y.tobytes(), info.encode(), shape=y.shape)
+                else:
+                    send_frame(sock, 1, b"", (out or "").encode())
         except Exception as e:  # noqa: BLE001
             try:
                 reply = unit.error_reply(e)  # the component's own status + body (op 4)

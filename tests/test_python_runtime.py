@@ -445,3 +445,27 @@ def test_raw_hook_array_reply_is_dense_in_a_graph_and_wire_encoded_alone(kind):
     txt = PythonUnit(_ArrayTransformer(kind), "TRANSFORMER").transform_input(json.dumps(reqs[0]), "t")
     d = json.loads(txt)["data"]
     assert ("values" in d["tensor"]) if kind == "tensor" else ("tensorContent" in d["tftensor"])
+
+
+def test_raw_hook_array_reply_from_worker_processes_is_a_binary_frame():
+    """In a process pool the same reply crosses the socket as a binary frame
+    (worker-side PythonUnit.call_json), keeps its data kind, and feeds a model."""
+    graph = {"name": "t", "type": "TRANSFORMER", "workers": 2, "children": [{"name": "m", "type": "MODEL"}]}
+    spec = {"name": "p", "graph": graph, "componentSpecs": [{"spec": {"containers": []}}]}
+    dep = sca.Deployment(spec, device=-1, components={"t": _ArrayTransformer("tftensor"), "m": _Sum4d()})
+    try:
+        assert dep.python_units["t"].native.stats()["workers"] == 2
+        outs = [dep.predict({"jsonData": {"x": [float(i), 1.0, 2.0, 3.0]}}) for i in range(6)]
+        for o in outs:
+            assert o["meta"]["tags"]["seen"] == 4
+        assert dep.python_units["t"].native.stats()["pool_calls"] >= 6
+    finally:
+        dep.close()
+    alone = sca.Deployment({"name": "p", "graph": {"name": "t", "type": "TRANSFORMER", "workers": 2},
+                            "componentSpecs": [{"spec": {"containers": []}}]}, device=-1,
+                           components={"t": _ArrayTransformer("tftensor")})
+    try:
+        o = alone.predict({"jsonData": {"x": [1.0, 2.0, 3.0, 4.0]}})
+        assert [int(d["size"]) for d in o["data"]["tftensor"]["tensorShape"]["dim"]] == [1, 2, 1, 2]
+    finally:
+        alone.close()
