@@ -361,8 +361,8 @@ class CompiledCnn:
                  graphs: bool = True, image: int = 224, channels_last: Optional[bool] = None, tune: bool = True):
         self.device = torch.device(f"cuda:{device}")
         self.dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
-        if channels_last is None:  # measured (profiles/r06n_imagenet): NHWC once tuned; untuned,
-            channels_last = tune or not isinstance(model, DenseNet)  # DenseNet is faster NCHW
+        if channels_last is None:  # measured (profiles/r06n_imagenet, cnn_layouts_fused.log): NHWC once
+            channels_last = tune or isinstance(model, DenseNet)  # tuned; untuned, ResNet is faster NCHW
         self.channels_last = channels_last
         self.tune = tune
         self.image = image
